@@ -1,0 +1,184 @@
+"""Benchmark: pileup positions/s at 10,000x depth on 1..8 MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over one batch: reset the accumulators (new sample), accumulate
+the batch's CSR pileup (HBM-resident, borrowed), finalize (per-position table + call table), and —
+for N > 1 — gather the call tables to rank 0 over RCCL.  Workload (BASELINE config 2/"metric
+point"): synthetic SARS-CoV-2 reference (L = 29,903), 10,000x depth, 150-bp reads, uncapped
+(max_depth 0).  Weak scaling: with N GPUs a step processes N samples; rank r owns the r-th
+coordinate range of every sample (one engine over the concatenated shards).
+
+Timing: W untimed warm-up steps, then K steps between barrier + device synchronize; max over
+ranks.  The dominant kernel's duration is measured with HIP events on the engine's stream.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM = 8.0e12          # B/s per MI355X (MI355X_MICROARCH.md: 8.0 TB/s spec)
+L_SARS = 29903
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--depth", type=float, default=10000.0)
+    ap.add_argument("--max-depth", type=int, default=0, help="0 = uncapped; 8000 = pysam parity cap")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-positions", type=int, default=600)
+    return ap.parse_args()
+
+
+def build_shard(rank, world, depth, max_depth):
+    """CSR of this rank's coordinate range of each of `world` samples, concatenated."""
+    from covid_spings_variant_caller_amd import synth
+    ref = synth.reference(L_SARS, seed=1)
+    shard = (L_SARS + world - 1) // world
+    lo, hi = rank * shard, min(L_SARS, (rank + 1) * shard)
+    offs, codes, quals, refs = [np.zeros(1, np.uint64)], [], [], []
+    base = 0
+    for s in range(world):
+        _, o, c, q = synth.pileup(L_SARS, depth, seed=2 + s, ref=ref, lo=lo, hi=hi, max_depth=max_depth)
+        offs.append(o[1:] + np.uint64(base))
+        base += len(c)
+        codes.append(c)
+        quals.append(q)
+        refs.append(ref[lo:hi])
+    off = np.concatenate(offs)
+    return ref, "".join(refs), off, np.concatenate(codes), np.concatenate(quals), hi - lo
+
+
+def cpu_baseline(args):
+    """Oracle restatements of the reference path on a bounded sample of the same workload."""
+    from covid_spings_variant_caller_amd import synth
+    from oracle import reference_port as rp
+    from oracle.c_oracle import COracle
+    ref = synth.reference(L_SARS, seed=1)
+    lo = 12000
+    n = args.cpu_positions
+    _, off, c, q = synth.pileup(L_SARS, args.depth, seed=2, ref=ref, lo=lo, hi=lo + n, max_depth=args.max_depth)
+    t0 = time.perf_counter()
+    o = rp.OracleCaller(ref, 30, 10, 5, 0.10)
+    o.accumulate(lo, off, c, q)
+    o.prepare_variants()
+    t_py = time.perf_counter() - t0
+    n_c = min(L_SARS - lo, 8 * n)
+    _, off2, c2, q2 = synth.pileup(L_SARS, args.depth, seed=2, ref=ref, lo=lo, hi=lo + n_c, max_depth=args.max_depth)
+    t0 = time.perf_counter()
+    co = COracle(ref, 30, 10, 5, 0.10)
+    co.accumulate(lo, off2, c2, q2)
+    co.finalize()
+    t_c = time.perf_counter() - t0
+    return {"value": n / t_py, "unit": "positions/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/reference_port.py (Python/numpy restatement of live_variant_caller.py:74-185) "
+                      f"on {n} positions x {args.depth:.0f}x ({int(off[-1])} entries), {t_py:.2f} s, 1 core; "
+                      f"pysam pileup/BAM decode not included (absent)",
+            "c_restatement": {"value": n_c / t_c, "unit": "positions/s", "cores": 1,
+                              "sample": f"oracle/spg_oracle.c on {n_c} positions ({int(off2[-1])} entries), {t_c:.2f} s"}}
+
+
+def main():
+    args = parse()
+    import torch
+    import spings  # noqa: F401
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+
+    t_gen = time.perf_counter()
+    ref, vref, off, codes, quals, shard_len = build_shard(rank, world, args.depth, args.max_depth)
+    E = len(codes)
+    C = len(off) - 1
+    t_gen = time.perf_counter() - t_gen
+    d_off, d_c, d_q = synth.to_device(off, codes, quals, device=local if world > 1 else 0)
+    eng = PileupEngine(C, 30, 10, 5, 0.10, device=local if world > 1 else 0, reference=vref)
+
+    cand_cap = 1 << 14
+    gather_buf = torch.zeros(cand_cap * 56 + 8, dtype=torch.uint8, device=d_c.device)
+
+    def step():
+        eng.reset()
+        eng.accumulate(0, d_off, d_c, d_q, borrow=True, n_entries=E)
+        eng.finalize()
+        if dist is not None:
+            eng.copy_candidates_device(gather_buf)
+            out = [torch.empty_like(gather_buf) for _ in range(world)] if rank == 0 else None
+            dist.gather(gather_buf, out, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+    torch.cuda.synchronize()
+    acc_ms, fin_ms = [], []
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        a, f = eng.last_kernel_ms()      # syncs the engine stream (events)
+        acc_ms.append(a)
+        fin_ms.append(f)
+    eng.sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=d_c.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    n_cand = eng.counts()[0]
+    positions_per_step = world * L_SARS
+    value = positions_per_step * args.steps / dt
+    t_acc = float(np.mean(acc_ms)) * 1e-3
+    t_fin = float(np.mean(fin_ms)) * 1e-3
+    algo_bytes = 2 * E + 8 * (C + 1)          # base_code + qual + u64 offsets read by k_accumulate
+    achieved = algo_bytes / t_acc
+    res = {
+        "metric": "pileup positions/s at 10,000x depth (SARS-CoV-2, synthetic)",
+        "value": value, "unit": "positions/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8/f64", "data": "synthetic",
+        "config": {"workload": f"SARS-CoV-2 L={L_SARS}, {args.depth:.0f}x, 150-bp reads, "
+                               + ("uncapped" if not args.max_depth else f"max_depth {args.max_depth}")
+                               + ", 1 sample per GPU per step (coordinate-sharded)",
+                   "positions_per_step": positions_per_step, "entries_per_gpu_step": E, "columns_per_gpu": C,
+                   "parallelism": f"coord-shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM, "traffic": None,
+                     "kernel": "k_accumulate", "kernel_ms": t_acc * 1e3, "algorithmic_bytes": algo_bytes},
+        "finalize_ms": t_fin * 1e3, "candidates_per_gpu_step": n_cand, "datagen_s": t_gen,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(args)
+        res["cpu_baseline"]["cores_available"] = len(os.sched_getaffinity(0))
+    if rank == 0:
+        print(json.dumps(res))
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

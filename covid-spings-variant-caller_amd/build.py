@@ -1,0 +1,76 @@
+"""Build the native libraries in-tree (gfx950).
+
+* ``_lib/libspings_gpu.so``    — HIP kernels + C-ABI (include/spings_gpu.h), hipcc --offload-arch=gfx950
+* ``_lib/libspings_pileup.so`` — host C++ BAM/SAM reader + htslib-faithful pileup (include/spings_pileup.h)
+
+The .so files are git-ignored but travel to the GPU box with the gpurun snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIBDIR = os.path.join(PKG, "_lib")
+INC = os.path.join(ROOT, "include")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+GPU_SOURCES = ["spg_kernels.hip", "spg_api.cpp"]
+GPU_HEADERS = ["spg_device.h"]
+PILEUP_SOURCES = ["spp_pileup.cpp"]
+
+
+def _stale(out, deps):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def build_gpu(force=False, verbose=False) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    out = os.path.join(LIBDIR, "libspings_gpu.so")
+    deps = [os.path.join(CSRC, f) for f in GPU_SOURCES + GPU_HEADERS] + [os.path.join(INC, "spings_gpu.h")]
+    if force or _stale(out, deps):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", f"-I{INC}", "-o", out + ".tmp"]
+        cmd += [os.path.join(CSRC, f) for f in GPU_SOURCES]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        _run(cmd)
+        os.replace(out + ".tmp", out)
+    return out
+
+
+def build_pileup(force=False, verbose=False) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    out = os.path.join(LIBDIR, "libspings_pileup.so")
+    srcs = [os.path.join(CSRC, f) for f in PILEUP_SOURCES]
+    if not all(os.path.exists(s) for s in srcs):
+        return ""
+    deps = srcs + [os.path.join(INC, "spings_pileup.h")]
+    if force or _stale(out, deps):
+        cxx = shutil.which("g++") or "g++"
+        cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{INC}", "-o", out + ".tmp"] + srcs + ["-lz"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        _run(cmd)
+        os.replace(out + ".tmp", out)
+    return out
+
+
+def build_all(force=False, verbose=False):
+    return build_gpu(force, verbose), build_pileup(force, verbose)
+
+
+if __name__ == "__main__":
+    print(build_all(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,479 @@
+// spg_api.cpp — C-ABI of the engine (include/spings_gpu.h): context, HBM buffers, stream-ordered
+// copies and kernel launches.  Compiled by hipcc together with spg_kernels.hip into
+// libspings_gpu.so.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "spg_device.h"
+
+namespace spg {
+hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_t *code, const uint8_t *qual,
+                             const uint8_t *ref, const Tables *T, Acc *acc, hipStream_t st);
+hipError_t launch_finalize(const FParams &F, const Acc *acc, const Tables *T, const Out &O, const Hist *H,
+                           hipStream_t st);
+hipError_t launch_set_hist(Hist *dst, const Hist &h, hipStream_t st);
+}  // namespace spg
+
+using namespace spg;
+
+static thread_local std::string g_err;
+
+static int fail(const std::string &m) {
+    g_err = m;
+    return -1;
+}
+
+#define HIPCHK(x)                                                                                       \
+    do {                                                                                                \
+        hipError_t e_ = (x);                                                                            \
+        if (e_ != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(e_));              \
+    } while (0)
+
+struct HistBatch {
+    int64_t pos_begin, n_cols;
+    uint64_t *off;
+    uint8_t *code, *qual;
+    bool owned;
+};
+
+struct spg_ctx {
+    int device = 0;
+    int64_t n_pos = 0;
+    spg_params p{};
+    hipStream_t stream = nullptr;
+    Acc *acc = nullptr;
+    Tables *tables = nullptr;
+    bool lut_set = false;
+    uint8_t *ref = nullptr;
+    int64_t ref_len = 0;
+    std::vector<HistBatch> hist;
+    Hist *d_hist = nullptr;
+    int64_t d_hist_cap = 0;
+    uint32_t batch_seq = 0;
+    // outputs
+    uint32_t *o_depth = nullptr, *o_counts = nullptr, *o_order = nullptr, *o_first = nullptr;
+    double *o_gl = nullptr;
+    uint8_t *o_flags = nullptr;
+    spg_candidate *cand = nullptr;
+    int64_t cand_cap = 0;
+    int64_t *band = nullptr;
+    int64_t band_cap = 0;
+    spg_detail *detail = nullptr;
+    int64_t detail_cap = 0;
+    Counters *ctr = nullptr;
+    bool finalized = false;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    bool ev_acc = false, ev_fin = false;
+};
+
+extern "C" {
+
+const char *spg_last_error(void) { return g_err.c_str(); }
+int spg_abi_version(void) { return SPG_ABI_VERSION; }
+size_t spg_sizeof_candidate(void) { return sizeof(spg_candidate); }
+size_t spg_sizeof_detail(void) { return sizeof(spg_detail); }
+size_t spg_sizeof_acc(void) { return sizeof(Acc); }
+
+int spg_device_count(int *n) {
+    if (!n) return fail("spg_device_count: null");
+    HIPCHK(hipGetDeviceCount(n));
+    return 0;
+}
+
+static int alloc_outputs(spg_ctx *c) {
+    const int64_t n = c->n_pos;
+    HIPCHK(hipMalloc(&c->o_depth, sizeof(uint32_t) * (n + 1)));
+    HIPCHK(hipMalloc(&c->o_counts, sizeof(uint32_t) * SPG_NCOUNT * (n + 1)));
+    HIPCHK(hipMalloc(&c->o_order, sizeof(uint32_t) * (n + 1)));
+    HIPCHK(hipMalloc(&c->o_first, sizeof(uint32_t) * (n + 1)));
+    HIPCHK(hipMalloc(&c->o_gl, sizeof(double) * SPG_NSLOT * (n + 1)));
+    HIPCHK(hipMalloc(&c->o_flags, n + 16));
+    c->band_cap = n + 1;
+    HIPCHK(hipMalloc(&c->band, sizeof(int64_t) * c->band_cap));
+    c->cand_cap = std::max<int64_t>(4096, n / 4 + 1024);
+    HIPCHK(hipMalloc(&c->cand, sizeof(spg_candidate) * c->cand_cap));
+    c->detail_cap = std::max<int64_t>(1024, std::min<int64_t>(n + 1, 65536));
+    HIPCHK(hipMalloc(&c->detail, sizeof(spg_detail) * c->detail_cap));
+    HIPCHK(hipMalloc(&c->ctr, sizeof(Counters)));
+    HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
+    return 0;
+}
+
+int spg_create(int device, int64_t n_pos, const spg_params *p, spg_ctx **out) {
+    if (!out || !p) return fail("spg_create: null argument");
+    if (n_pos <= 0) return fail("spg_create: n_pos must be > 0");
+    *out = nullptr;
+    spg_ctx *c = new spg_ctx();
+    c->device = device;
+    c->n_pos = n_pos;
+    c->p = *p;
+    int rc = 0;
+    auto bail = [&](int r) { spg_destroy(c); return r; };
+    if (hipSetDevice(device) != hipSuccess) return bail(fail("spg_create: hipSetDevice failed"));
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail("spg_create: stream"));
+    if (hipMalloc(&c->acc, sizeof(Acc) * n_pos) != hipSuccess) return bail(fail("spg_create: acc alloc"));
+    if (hipMalloc(&c->tables, sizeof(Tables)) != hipSuccess) return bail(fail("spg_create: tables alloc"));
+    if (hipMemsetAsync(c->acc, 0, sizeof(Acc) * n_pos, c->stream) != hipSuccess) return bail(fail("memset"));
+    if ((rc = alloc_outputs(c)) != 0) return bail(rc);
+    for (auto &e : c->ev)
+        if (hipEventCreate(&e) != hipSuccess) return bail(fail("spg_create: event"));
+    *out = c;
+    return 0;
+}
+
+static void free_history(spg_ctx *c) {
+    for (auto &h : c->hist)
+        if (h.owned) {
+            (void)hipFree(h.off);
+            (void)hipFree(h.code);
+            (void)hipFree(h.qual);
+        }
+    c->hist.clear();
+}
+
+int spg_destroy(spg_ctx *c) {
+    if (!c) return 0;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_history(c);
+    void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
+                    c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    for (auto &e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+int spg_reset(spg_ctx *c) {
+    if (!c) return fail("spg_reset: null ctx");
+    HIPCHK(hipSetDevice(c->device));
+    bool owned = false;
+    for (auto &h : c->hist) owned |= h.owned;
+    if (owned) HIPCHK(hipStreamSynchronize(c->stream));
+    free_history(c);
+    HIPCHK(hipMemsetAsync(c->acc, 0, sizeof(Acc) * c->n_pos, c->stream));
+    c->batch_seq = 0;
+    c->finalized = false;
+    return 0;
+}
+
+int spg_set_eps_lut(spg_ctx *c, const double lut[256]) {
+    if (!c || !lut) return fail("spg_set_eps_lut: null argument");
+    Tables *t = (Tables *)calloc(1, sizeof(Tables));
+    for (int q = 0; q < 256; q++) {
+        t->eps[q] = lut[q];
+        t->l1m[q] = q == 0 ? 0.0 : std::log1p(-lut[q]);
+        if (!(lut[q] > 0.0 && lut[q] <= 1.0)) {
+            free(t);
+            return fail("spg_set_eps_lut: eps out of (0,1]");
+        }
+    }
+    if (lut[0] != 1.0) { free(t); return fail("spg_set_eps_lut: eps[0] must be 1.0 (10^-0)"); }
+    for (int k = 0; k < 336; k++) {
+        char buf[32];
+        snprintf(buf, sizeof buf, "1e-%d", k);
+        t->p10k[k] = strtod(buf, nullptr);   // correctly rounded decimal -> binary
+    }
+    t->fast[0][0] = 0.0;
+    t->fast[0][1] = 0.0;
+    for (int q = 1; q < 128; q++) {
+        t->fast[q][0] = t->l1m[q];
+        t->fast[q][1] = t->eps[q];
+    }
+    hipError_t e = hipSetDevice(c->device);
+    if (e == hipSuccess) e = hipMemcpyAsync(c->tables, t, sizeof(Tables), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    free(t);
+    if (e != hipSuccess) return fail(std::string("spg_set_eps_lut: ") + hipGetErrorString(e));
+    c->lut_set = true;
+    return 0;
+}
+
+int spg_set_reference(spg_ctx *c, const char *seq, int64_t len) {
+    if (!c || !seq || len < 0) return fail("spg_set_reference: bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    if (c->ref) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipFree(c->ref));
+        c->ref = nullptr;
+    }
+    HIPCHK(hipMalloc(&c->ref, len + 16));
+    HIPCHK(hipMemcpyAsync(c->ref, seq, len, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->ref_len = len;
+    return 0;
+}
+
+static int push_history_table(spg_ctx *c) {
+    const int64_t n = (int64_t)c->hist.size();
+    if (n > c->d_hist_cap) {
+        int64_t cap = std::max<int64_t>(16, c->d_hist_cap * 2);
+        while (cap < n) cap *= 2;
+        Hist *nh = nullptr;
+        HIPCHK(hipMalloc(&nh, sizeof(Hist) * cap));
+        if (c->d_hist) {
+            HIPCHK(hipMemcpyAsync(nh, c->d_hist, sizeof(Hist) * (n - 1), hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            HIPCHK(hipFree(c->d_hist));
+        }
+        c->d_hist = nh;
+        c->d_hist_cap = cap;
+    }
+    const HistBatch &b = c->hist.back();
+    Hist h{b.pos_begin, b.n_cols, b.off, b.code, b.qual};
+    // stream-ordered by-value write: no host synchronisation per batch
+    HIPCHK(launch_set_hist(c->d_hist + (n - 1), h, c->stream));
+    return 0;
+}
+
+int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
+                      const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags) {
+    if (!c) return fail("spg_accumulate: null ctx");
+    if (!c->lut_set) return fail("spg_accumulate: spg_set_eps_lut not called");
+    if (!c->ref) return fail("spg_accumulate: spg_set_reference not called");
+    if (n_cols < 0 || pos_begin < 0 || pos_begin + n_cols > c->n_pos)
+        return fail("spg_accumulate: column range outside the context's positions");
+    if (pos_begin + n_cols > c->ref_len)
+        return fail("spg_accumulate: column range beyond the reference sequence (IndexError in the reference)");
+    if (n_cols == 0) return 0;
+    if (!offsets || (n_entries && (!base_code || !qual))) return fail("spg_accumulate: null buffer");
+    if (n_entries >= (1ull << 40)) return fail("spg_accumulate: batch too large");
+    HIPCHK(hipSetDevice(c->device));
+    const bool dev = flags & SPG_IN_DEVICE;
+    const bool borrow = dev && (flags & SPG_IN_BORROW);
+    HistBatch hb{pos_begin, n_cols, nullptr, nullptr, nullptr, !borrow};
+    if (!dev) {
+        // validate the host CSR (cheap, O(n_cols)); device inputs are trusted
+        if (offsets[0] != 0 || offsets[n_cols] != n_entries) return fail("spg_accumulate: offsets[0] must be 0 and offsets[n_cols] == n_entries");
+        for (int64_t i = 0; i < n_cols; i++)
+            if (offsets[i + 1] < offsets[i]) return fail("spg_accumulate: offsets not monotone");
+    }
+    const size_t pad = (n_entries + 16 + 15) & ~size_t(15);
+    if (borrow) {
+        hb.off = const_cast<uint64_t *>(offsets);
+        hb.code = const_cast<uint8_t *>(base_code);
+        hb.qual = const_cast<uint8_t *>(qual);
+    } else {
+        HIPCHK(hipMalloc(&hb.off, sizeof(uint64_t) * (n_cols + 1)));
+        HIPCHK(hipMalloc(&hb.code, pad));
+        HIPCHK(hipMalloc(&hb.qual, pad));
+        const hipMemcpyKind k = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+        HIPCHK(hipMemcpyAsync(hb.off, offsets, sizeof(uint64_t) * (n_cols + 1), k, c->stream));
+        if (n_entries) {
+            HIPCHK(hipMemcpyAsync(hb.code, base_code, n_entries, k, c->stream));
+            HIPCHK(hipMemcpyAsync(hb.qual, qual, n_entries, k, c->stream));
+        }
+        HIPCHK(hipMemsetAsync(hb.code + n_entries, 0xFF, pad - n_entries, c->stream));
+        HIPCHK(hipMemsetAsync(hb.qual + n_entries, 0, pad - n_entries, c->stream));
+    }
+    if (!dev) {
+        for (uint64_t i = 0; i < n_entries; i++)
+            if (base_code[i] > SPG_CODE_SKIP) {
+                if (!borrow) { (void)hipStreamSynchronize(c->stream); (void)hipFree(hb.off); (void)hipFree(hb.code); (void)hipFree(hb.qual); }
+                return fail("spg_accumulate: base_code > 17 at entry " + std::to_string(i));
+            }
+    }
+    c->hist.push_back(hb);
+    int rc = push_history_table(c);
+    if (rc) return rc;
+    c->batch_seq++;
+    const double avg = (double)n_entries / (double)n_cols;
+    uint32_t G = 1;
+    if (avg < 2048.0) {
+        const double want = 2048.0 / std::max(avg, 1.0);
+        while (G * 2 <= want && G < 64) G *= 2;
+    }
+    KParams P{};
+    P.pos_begin = pos_begin;
+    P.n_cols = n_cols;
+    P.min_bq = c->p.min_base_quality;
+    P.qlo = std::max(c->p.min_base_quality, 4);
+    const int mb = c->p.min_base_quality;
+    P.kpass = mb <= 0 ? 0x80808080u : (mb >= 128 ? 0u : (uint32_t)(0x80 - mb) * 0x01010101u);
+    P.kok = P.qlo >= 128 ? 0u : (uint32_t)(0x80 - P.qlo) * 0x01010101u;
+    P.batch_seq = c->batch_seq;
+    P.G = G;
+    P.t_deep = G == 1 ? 64u : 128u;
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    HIPCHK(launch_accumulate(P, hb.off, hb.code, hb.qual, c->ref, c->tables, c->acc, c->stream));
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    c->ev_acc = true;
+    c->finalized = false;
+    return 0;
+}
+
+int spg_accumulate(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets, const uint8_t *base_code,
+                   const uint8_t *qual, uint64_t n_entries) {
+    return spg_accumulate_ex(c, pos_begin, n_cols, offsets, base_code, qual, n_entries, 0);
+}
+
+static Out make_out(spg_ctx *c) {
+    Out O;
+    O.depth = c->o_depth; O.counts = c->o_counts; O.order = c->o_order; O.first = c->o_first;
+    O.gl = c->o_gl; O.flags = c->o_flags; O.cand = c->cand; O.band = c->band; O.detail = c->detail;
+    O.ctr = c->ctr;
+    return O;
+}
+
+static FParams make_fparams(spg_ctx *c) {
+    FParams F{};
+    F.n_pos = c->n_pos;
+    F.min_td = c->p.min_total_depth;
+    F.min_ad = c->p.min_allele_depth;
+    F.ratio = c->p.min_evidence_ratio;
+    F.cand_cap = c->cand_cap;
+    F.band_cap = c->band_cap;
+    F.detail_cap = c->detail_cap;
+    F.min_bq = c->p.min_base_quality;
+    F.n_hist = (int32_t)c->hist.size();
+    return F;
+}
+
+int spg_finalize(spg_ctx *c) {
+    if (!c) return fail("spg_finalize: null ctx");
+    if (!c->lut_set) return fail("spg_finalize: spg_set_eps_lut not called");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
+    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    HIPCHK(launch_finalize(make_fparams(c), c->acc, c->tables, make_out(c), c->d_hist, c->stream));
+    HIPCHK(hipEventRecord(c->ev[3], c->stream));
+    c->ev_fin = true;
+    c->finalized = true;
+    return 0;
+}
+
+int spg_sync(spg_ctx *c) {
+    if (!c) return fail("spg_sync: null ctx");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// Grow the candidate / detail buffers and re-run finalize when the last one overflowed.
+static int settle(spg_ctx *c, Counters &h) {
+    if (!c->finalized) return fail("spg: spg_finalize has not been called since the last accumulate/reset");
+    HIPCHK(hipSetDevice(c->device));
+    for (int iter = 0; iter < 4; iter++) {
+        HIPCHK(hipMemcpyAsync(&h, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (h.err) return fail("spg: replay found a depth mismatch between history and accumulators");
+        bool again = false;
+        if ((int64_t)h.n_cand > c->cand_cap) {
+            HIPCHK(hipFree(c->cand));
+            c->cand_cap = (int64_t)h.n_cand * 2;
+            HIPCHK(hipMalloc(&c->cand, sizeof(spg_candidate) * c->cand_cap));
+            again = true;
+        }
+        if ((int64_t)h.n_detail > c->detail_cap) {
+            HIPCHK(hipFree(c->detail));
+            c->detail_cap = (int64_t)h.n_detail * 2;
+            HIPCHK(hipMalloc(&c->detail, sizeof(spg_detail) * c->detail_cap));
+            again = true;
+        }
+        if (!again) return 0;
+        int rc = spg_finalize(c);
+        if (rc) return rc;
+    }
+    return fail("spg: result buffers did not settle");
+}
+
+int spg_count(spg_ctx *c, int64_t *n_candidates, int64_t *n_details) {
+    if (!c) return fail("spg_count: null ctx");
+    Counters h{};
+    int rc = settle(c, h);
+    if (rc) return rc;
+    if (n_candidates) *n_candidates = h.n_cand;
+    if (n_details) *n_details = h.n_detail;
+    return 0;
+}
+
+int spg_get_candidates(spg_ctx *c, spg_candidate *out, int64_t cap, int64_t *n_out) {
+    if (!c || !n_out) return fail("spg_get_candidates: null argument");
+    Counters h{};
+    int rc = settle(c, h);
+    if (rc) return rc;
+    *n_out = h.n_cand;
+    if ((int64_t)h.n_cand > cap) return fail("spg_get_candidates: output capacity too small");
+    if (h.n_cand) {
+        HIPCHK(hipMemcpyAsync(out, c->cand, sizeof(spg_candidate) * h.n_cand, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    return 0;
+}
+
+int spg_get_details(spg_ctx *c, spg_detail *out, int64_t cap, int64_t *n_out) {
+    if (!c || !n_out) return fail("spg_get_details: null argument");
+    Counters h{};
+    int rc = settle(c, h);
+    if (rc) return rc;
+    *n_out = h.n_detail;
+    if ((int64_t)h.n_detail > cap) return fail("spg_get_details: output capacity too small");
+    if (h.n_detail) {
+        HIPCHK(hipMemcpyAsync(out, c->detail, sizeof(spg_detail) * h.n_detail, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    return 0;
+}
+
+int spg_get_table(spg_ctx *c, int64_t pos0, int64_t n, uint32_t *depth, uint32_t *counts, double *gl,
+                  uint8_t *flags, uint32_t *order, uint32_t *first_batch) {
+    if (!c) return fail("spg_get_table: null ctx");
+    if (pos0 < 0 || n < 0 || pos0 + n > c->n_pos) return fail("spg_get_table: range outside the context");
+    Counters h{};
+    int rc = settle(c, h);
+    if (rc) return rc;
+    const hipMemcpyKind k = hipMemcpyDeviceToHost;
+    if (depth) HIPCHK(hipMemcpyAsync(depth, c->o_depth + pos0, 4 * n, k, c->stream));
+    if (counts) HIPCHK(hipMemcpyAsync(counts, c->o_counts + pos0 * SPG_NCOUNT, 4 * SPG_NCOUNT * n, k, c->stream));
+    if (gl) HIPCHK(hipMemcpyAsync(gl, c->o_gl + pos0 * SPG_NSLOT, 8 * SPG_NSLOT * n, k, c->stream));
+    if (flags) HIPCHK(hipMemcpyAsync(flags, c->o_flags + pos0, n, k, c->stream));
+    if (order) HIPCHK(hipMemcpyAsync(order, c->o_order + pos0, 4 * n, k, c->stream));
+    if (first_batch) HIPCHK(hipMemcpyAsync(first_batch, c->o_first + pos0, 4 * n, k, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int spg_device_results(spg_ctx *c, void **candidates, void **n_candidates) {
+    if (!c) return fail("spg_device_results: null ctx");
+    if (candidates) *candidates = c->cand;
+    if (n_candidates) *n_candidates = &c->ctr->n_cand;
+    return 0;
+}
+
+int spg_copy_candidates_device(spg_ctx *c, void *dst, int64_t cap) {
+    if (!c || !dst || cap < 0) return fail("spg_copy_candidates_device: bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemsetAsync(dst, 0, 8, c->stream));
+    HIPCHK(hipMemcpyAsync(dst, &c->ctr->n_cand, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+    const int64_t n = std::min<int64_t>(cap, c->cand_cap);
+    if (n) HIPCHK(hipMemcpyAsync((char *)dst + 8, c->cand, sizeof(spg_candidate) * n, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int spg_last_kernel_ms(spg_ctx *c, float *acc_ms, float *fin_ms) {
+    if (!c) return fail("spg_last_kernel_ms: null ctx");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (acc_ms) {
+        *acc_ms = 0.f;
+        if (c->ev_acc) HIPCHK(hipEventElapsedTime(acc_ms, c->ev[0], c->ev[1]));
+    }
+    if (fin_ms) {
+        *fin_ms = 0.f;
+        if (c->ev_fin) HIPCHK(hipEventElapsedTime(fin_ms, c->ev[2], c->ev[3]));
+    }
+    return 0;
+}
+
+}  // extern "C"

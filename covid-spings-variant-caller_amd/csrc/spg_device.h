@@ -1,0 +1,97 @@
+// spg_device.h — device-side data layout and helpers shared by the engine kernels (gfx950).
+//
+// Layout in HBM (one context = one contiguous reference range of n_pos positions):
+//   Acc      acc[n_pos]      160 B AoS record per position (accumulators of LiveVariantCaller.memory)
+//   Tables   *tables         eps / ln(1-eps) / 10^-k LUTs (from the reference's from_phred_scale)
+//   batch CSR (history)      offsets u64[n_cols+1], base_code u8[E], qual u8[E] (16-B padded)
+//   outputs (SoA)            depth u32, counts u32[8], gl f64[5], flags u8, order u32, first_batch u32
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "spings_gpu.h"
+
+namespace spg {
+
+constexpr int NSLOT = SPG_NSLOT;          // A C G T N
+constexpr uint32_t INF32 = 0xFFFFFFFFu;
+constexpr uint32_t MISC_EXOTIC = 0x100u;  // acc.misc bit: an allele outside A,C,G,T,N was seen
+
+// Accumulators replacing Site (structs.py:2-6) — the q lists are replaced by sufficient
+// statistics: counts, integer sum of q (log10 of the eps product up to fp64 rounding),
+// sum of ln(1-eps) (the hypothesis product), sum of eps (QUAL), a lower bound on q (H == 0 iff
+// a Q0 entry; q >= 4 makes every eps factor < 1/2, which the underflow proof needs) and the
+// dict insertion order of the alleles.  The exact ordered lists live on as the batch history
+// that the replay kernel walks for the rare positions where order matters (subnormal band).
+struct __align__(16) Acc {
+    uint32_t depth;        // totalDepth (:75, :87)
+    uint32_t first_batch;  // 0 = not in memory; else batch seq of first visit (dict order)
+    uint32_t order;        // bits 0-2 n alleles; bits 3+3i.. slot of i-th allele (snvs dict order)
+    uint32_t misc;         // bits 0-7 REF char stored at first visit (:81); MISC_EXOTIC
+    uint32_t n_del, n_skip, n_other, pad0;
+    uint32_t cnt[NSLOT];
+    uint32_t sq[NSLOT];    // sum q, saturating at 2^31
+    uint8_t qf[8];         // q lower bound per slot (exact below 4)
+    double sl[NSLOT];      // sum ln(1 - eps)
+    double se[NSLOT];      // sum eps
+};
+static_assert(sizeof(Acc) == 160, "Acc layout");
+
+struct Tables {
+    double eps[256];       // from_phred_scale(q), bit-identical to the reference (host-supplied)
+    double l1m[256];       // log1p(-eps[q]); l1m[0] = 0 (Q0 handled through qf == 0)
+    double p10k[336];      // 10^-k, correctly rounded, k = 0..335
+    double fast[128][2];   // {l1m, eps} for q = 1..127; row 0 = {0, 0} ("not selected")
+};
+
+struct KParams {
+    int64_t pos_begin, n_cols;
+    int32_t min_bq, qlo;   // qlo = max(min_bq, 4): fast-path floor
+    uint32_t kpass, kok;   // SWAR compare constants
+    uint32_t batch_seq;    // 1-based
+    uint32_t G;            // columns per wave group
+    uint32_t t_deep;       // columns with >= t_deep raw entries are processed wave-wide
+    uint32_t pad;
+};
+
+struct FParams {
+    int64_t n_pos;
+    int32_t min_td, min_ad;
+    double ratio;
+    int64_t cand_cap, band_cap, detail_cap;
+    int32_t min_bq, n_hist;
+};
+
+struct Hist {               // one accumulated batch, kept for the exact replay
+    int64_t pos_begin, n_cols;
+    const uint64_t *off;
+    const uint8_t *code;
+    const uint8_t *qual;
+};
+
+struct Counters {           // zeroed at the start of every finalize
+    uint32_t n_cand, n_band, n_detail, err;
+};
+
+struct Out {                // SoA result table
+    uint32_t *depth, *counts, *order, *first;
+    double *gl;
+    uint8_t *flags;
+    spg_candidate *cand;
+    int64_t *band;
+    spg_detail *detail;
+    Counters *ctr;
+};
+
+__device__ __forceinline__ int slot_of(uint32_t c) {
+    return c == 1u ? 0 : c == 2u ? 1 : c == 4u ? 2 : c == 8u ? 3 : c == 15u ? 4 : -1;
+}
+__host__ __device__ __forceinline__ uint32_t slot_code(int s) {
+    return s == 0 ? 1u : s == 1 ? 2u : s == 2 ? 4u : s == 3 ? 8u : 15u;
+}
+__host__ __device__ __forceinline__ uint8_t nibble_char(uint32_t c) {
+    const char *t = "=ACMGRSVTWYHKDBN";
+    return (uint8_t)t[c & 15u];
+}
+
+}  // namespace spg

@@ -1,0 +1,218 @@
+"""PileupEngine — Python front end of the MI355X engine context (include/spings_gpu.h).
+
+One engine = one spg_ctx = one HIP device's accumulators for ``n_pos`` reference positions.
+It replaces LiveVariantCaller's ``memory`` dict and the statistics loop
+(variant_caller/live_variant_caller.py:37-231, utils.py:9-24).  Calls are serialised with a
+lock: the C context is not re-entrant, while the reference drives its engine from daemon
+threads (client_server/vc_queue.py:99-111).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import threading
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from . import _native as N
+
+
+def eps_lut() -> np.ndarray:
+    """from_phred_scale (utils.py:9-10) with the same math.pow, so device eps are bit-identical."""
+    return np.array([math.pow(10, q / -10) for q in range(256)], dtype=np.float64)
+
+
+class PileupEngine:
+    def __init__(self, n_pos: int, min_base_quality: int = 30, min_total_depth: int = 10,
+                 min_allele_depth: int = 5, min_evidence_ratio: float = 0.10, device: int = 0,
+                 reference: Optional[str] = None):
+        self._L = N.gpu_lib()
+        self._lock = threading.RLock()
+        self.n_pos = int(n_pos)
+        self.device = int(device)
+        self.params = N.SpgParams(int(min_base_quality), int(min_total_depth), int(min_allele_depth), 0,
+                                  float(min_evidence_ratio))
+        h = C.c_void_p()
+        N.check(self._L.spg_create(self.device, self.n_pos, C.byref(self.params), C.byref(h)), "spg_create")
+        self._h = h
+        self._lut = eps_lut()
+        N.check(self._L.spg_set_eps_lut(self._h, N.ptr(self._lut)), "spg_set_eps_lut")
+        self._borrowed = []          # device tensors kept alive while borrowed as history
+        self.reference = None
+        if reference is not None:
+            self.set_reference(reference)
+
+    # -- lifecycle --------------------------------------------------------------------------
+    def close(self):
+        with self._lock:
+            if getattr(self, "_h", None):
+                self._L.spg_destroy(self._h)
+                self._h = None
+            self._borrowed = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self):
+        """reset_memory (live_variant_caller.py:37-38)."""
+        with self._lock:
+            N.check(self._L.spg_reset(self._h), "spg_reset")
+            self._borrowed = []
+
+    def set_reference(self, seq: str):
+        """fastaFile.fetch (:78): REF chars for first visits."""
+        with self._lock:
+            b = seq.encode("latin-1") if isinstance(seq, str) else bytes(seq)
+            N.check(self._L.spg_set_reference(self._h, b, len(b)), "spg_set_reference")
+            self.reference = seq
+
+    # -- hot path ---------------------------------------------------------------------------
+    def accumulate(self, pos_begin: int, offsets, codes, quals, borrow: bool = False, n_entries=None):
+        """process_pileup_column over one CSR batch (:74-103).  numpy arrays are host buffers;
+        torch tensors on this engine's device are consumed in place (``borrow`` keeps them as
+        replay history without a copy — they must stay alive until reset())."""
+        with self._lock:
+            if isinstance(offsets, np.ndarray) or isinstance(offsets, (list, tuple)):
+                o = np.ascontiguousarray(offsets, dtype=np.uint64)
+                c = np.ascontiguousarray(codes, dtype=np.uint8)
+                q = np.ascontiguousarray(quals, dtype=np.uint8)
+                n_cols = len(o) - 1
+                if len(c) != len(q):
+                    raise ValueError("codes and quals differ in length")
+                N.check(self._L.spg_accumulate(self._h, int(pos_begin), n_cols, N.ptr(o), N.ptr(c), N.ptr(q),
+                                               len(c)), "spg_accumulate")
+            else:
+                import torch
+                for t in (offsets, codes, quals):
+                    if not t.is_cuda or t.device.index != self.device or not t.is_contiguous():
+                        raise ValueError("device inputs must be contiguous tensors on the engine's device")
+                if offsets.dtype not in (torch.int64, torch.uint64) or codes.dtype != torch.uint8 or quals.dtype != torch.uint8:
+                    raise ValueError("device inputs: offsets int64, codes/quals uint8")
+                torch.cuda.current_stream(self.device).synchronize()
+                flags = N.SPG_IN_DEVICE | (N.SPG_IN_BORROW if borrow else 0)
+                n_cols = offsets.numel() - 1
+                if n_entries is None:
+                    n_entries = int(offsets[-1].item())
+                if borrow and (codes.numel() < n_entries + 16 or quals.numel() < n_entries + 16):
+                    raise ValueError("borrowed device buffers need >= 16 bytes of padding past the last entry")
+                N.check(self._L.spg_accumulate_ex(self._h, int(pos_begin), n_cols, N.ptr(offsets), N.ptr(codes),
+                                                  N.ptr(quals), int(n_entries), flags), "spg_accumulate_ex")
+                if borrow:
+                    self._borrowed.append((offsets, codes, quals))
+
+    def finalize(self):
+        """prepare_variants (:120-231): per-position table + candidates, on device."""
+        with self._lock:
+            N.check(self._L.spg_finalize(self._h), "spg_finalize")
+
+    def sync(self):
+        with self._lock:
+            N.check(self._L.spg_sync(self._h), "spg_sync")
+
+    def copy_candidates_device(self, dst, cap=None):
+        """Call table -> a torch uint8 device tensor (u64 count, then spg_candidate records)."""
+        cap = (dst.numel() - 8) // N.CANDIDATE_DTYPE.itemsize if cap is None else cap
+        with self._lock:
+            N.check(self._L.spg_copy_candidates_device(self._h, N.ptr(dst), int(cap)), "spg_copy_candidates_device")
+
+    def last_kernel_ms(self):
+        a, f = C.c_float(), C.c_float()
+        with self._lock:
+            N.check(self._L.spg_last_kernel_ms(self._h, C.byref(a), C.byref(f)), "spg_last_kernel_ms")
+        return a.value, f.value
+
+    # -- results ------------------------------------------------------------------------------
+    def table(self, pos0: int = 0, n: Optional[int] = None) -> Dict[str, np.ndarray]:
+        n = self.n_pos - pos0 if n is None else n
+        out = dict(depth=np.zeros(n, np.uint32), counts=np.zeros((n, N.SPG_NCOUNT), np.uint32),
+                   gl=np.zeros((n, N.SPG_NSLOT), np.float64), flags=np.zeros(n, np.uint8),
+                   order=np.zeros(n, np.uint32), first_batch=np.zeros(n, np.uint32))
+        with self._lock:
+            N.check(self._L.spg_get_table(self._h, pos0, n, *[N.ptr(out[k]) for k in
+                                                              ("depth", "counts", "gl", "flags", "order",
+                                                               "first_batch")]), "spg_get_table")
+        return out
+
+    def counts(self):
+        nc, nd = C.c_int64(), C.c_int64()
+        with self._lock:
+            N.check(self._L.spg_count(self._h, C.byref(nc), C.byref(nd)), "spg_count")
+        return nc.value, nd.value
+
+    def candidates(self) -> np.ndarray:
+        """Variants ordered like prepare_variants(): memory insertion order (first batch, then
+        position — htslib emits columns in coordinate order), then snvs dict order."""
+        with self._lock:
+            nc, _ = self.counts()
+            arr = np.zeros(nc, N.CANDIDATE_DTYPE)
+            got = C.c_int64()
+            N.check(self._L.spg_get_candidates(self._h, N.ptr(arr), nc, C.byref(got)), "spg_get_candidates")
+        arr = arr[:got.value]
+        return arr[np.lexsort((arr["rank"], arr["pos"], arr["first_batch"]))]
+
+    def details(self) -> np.ndarray:
+        with self._lock:
+            _, nd = self.counts()
+            arr = np.zeros(nd, N.DETAIL_DTYPE)
+            got = C.c_int64()
+            N.check(self._L.spg_get_details(self._h, N.ptr(arr), nd, C.byref(got)), "spg_get_details")
+        return arr[:got.value]
+
+    # -- reference-shaped views -----------------------------------------------------------------
+    def variants(self) -> List[dict]:
+        """The list prepare_variants() returns (live_variant_caller.py:170-185)."""
+        out = []
+        for r in self.candidates():
+            gl = 0 if r["gl_zero"] else float(r["gl"])
+            out.append({
+                "start": int(r["pos"]), "stop": int(r["pos"]) + 1,
+                "alleles": (chr(r["ref"]), chr(r["alt"])),
+                "qual": np.float64(r["qual"]),
+                "info": {"DP": int(r["dp"]), "AD": int(r["ad"]), "GL": gl, "PL": int(r["pl"]),
+                         "SCORE": int(r["score"])},
+            })
+        return out
+
+    def memory_summary(self):
+        """[pos, REF, totalDepth, [[allele, count] in snvs dict order]] in memory insertion order."""
+        t = self.table()
+        det = {int(d["pos"]): d for d in self.details()}
+        present = np.nonzero(t["flags"] & N.SPG_F_PRESENT)[0]
+        order = present[np.lexsort((present, t["first_batch"][present]))]
+        ref = self.reference
+        out = []
+        for p in order.tolist():
+            if p in det:
+                d = det[p]
+                alle = [[N.NIBBLE[d["code"][k]], int(d["count"][k])] for k in range(d["n_alleles"])]
+            else:
+                o = int(t["order"][p])
+                alle = [[N.SLOT_CHARS[(o >> (3 + 3 * i)) & 7], int(t["counts"][p][(o >> (3 + 3 * i)) & 7])]
+                        for i in range(o & 7)]
+            out.append([p, ref[p] if ref is not None else None, int(t["depth"][p]), alle])
+        return out
+
+    def gl_table(self):
+        """{pos: {allele: GL}} for evaluated positions, alleles in dict order."""
+        t = self.table()
+        det = {int(d["pos"]): d for d in self.details()}
+        out = {}
+        for p in np.nonzero(t["flags"] & N.SPG_F_EVALUATED)[0].tolist():
+            if p in det:
+                d = det[p]
+                out[p] = {N.NIBBLE[d["code"][k]]: float(d["gl"][k]) for k in range(d["n_alleles"])}
+            else:
+                o = int(t["order"][p])
+                out[p] = {N.SLOT_CHARS[(o >> (3 + 3 * i)) & 7]: float(t["gl"][p][(o >> (3 + 3 * i)) & 7])
+                          for i in range(o & 7)}
+        return out
+
+
+def device_count() -> int:
+    n = C.c_int()
+    N.check(N.gpu_lib().spg_device_count(C.byref(n)), "spg_device_count")
+    return n.value

@@ -1,0 +1,168 @@
+/*
+ * spings_gpu.h — C-ABI of the MI355X (gfx950) pileup + genotype-likelihood engine.
+ *
+ * Drop-in boundary for the hot path of COVID-SpiNGS/covid-spings-variant-caller
+ * (SURVEY.md §8 b).  The reference has no FFI for this path (it is pure Python over pysam);
+ * these entry points are what its `LiveVariantCaller` (variant_caller/live_variant_caller.py)
+ * binds through ctypes — see INTEGRATION.md for the binding stub.  Every function cites the
+ * reference interface it replaces.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no torch or HIP types in signatures.
+ *   - Every function returns int status: 0 = ok, < 0 = error; spg_last_error() returns the
+ *     thread-local message of the last failing call (replaces pysam's Python exceptions, which
+ *     the reference lets propagate uncaught).
+ *   - A context is NOT re-entrant: callers serialise calls on one context (the Python shim
+ *     holds a lock; the reference calls the engine from daemon threads, vc_queue.py:99-111).
+ *   - Work is enqueued on the context's own HIP stream; spg_sync() blocks.  Every spg_get_*
+ *     call synchronises the stream before copying.
+ *
+ * Column boundary (CSR): a batch is `n_cols` consecutive reference positions
+ * starting at `pos_begin`; `offsets[n_cols+1]` (u64) delimit each column's pileup entries in
+ * `base_code[]` / `qual[]` (u8 each).  base_code is the BAM 4-bit nibble (0..15,
+ * "=ACMGRSVTWYHKDBN"), 16 = CIGAR D (is_del), 17 = CIGAR N (is_refskip).  For D/N entries
+ * `qual` is the quality of the next aligned query base (0 if none) — the value pysam's
+ * base-quality filter tests.  Entries are in htslib pileup order (surviving reads in BAM order);
+ * the maxcnt cap and the read filters (flags, MAPQ) are applied before the boundary; the
+ * base-quality filter is applied by the engine.  A column with no entries is "not emitted"
+ * (htslib never yields an empty column).
+ */
+#ifndef SPINGS_GPU_H
+#define SPINGS_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPG_ABI_VERSION 1
+
+/* Allele slots of the per-position table (dict keys of Site.snvs, structs.py:2-6).
+ * Other IUPAC nibbles / '=' are exact too, but reported through spg_detail records. */
+#define SPG_NSLOT 5           /* A C G T N */
+#define SPG_NCOUNT 8          /* A C G T N DEL REFSKIP OTHER */
+#define SPG_CODE_DEL 16
+#define SPG_CODE_SKIP 17
+
+/* per-position flags (spg_get_table) */
+#define SPG_F_PRESENT 0x01    /* position is in LiveVariantCaller.memory */
+#define SPG_F_EVALUATED 0x02  /* totalDepth >= minTotalDepth: GLs computed (:131) */
+#define SPG_F_REPLAYED 0x04   /* resolved by the exact sequential replay (subnormal band / exotic) */
+#define SPG_F_EXOTIC 0x08     /* has alleles outside A,C,G,T,N (see spg_detail) */
+#define SPG_F_CANDIDATE 0x10  /* produced >= 1 variant */
+
+/* accumulate flags */
+#define SPG_IN_DEVICE 0x1     /* offsets/base_code/qual are device pointers on the ctx device */
+#define SPG_IN_BORROW 0x2     /* with SPG_IN_DEVICE: keep the caller's device buffers as replay
+                                 history without copying; they must stay valid until
+                                 spg_reset/spg_destroy */
+
+/* LiveVariantCaller ctor thresholds (live_variant_caller.py:22-29); minMappingQuality and
+ * maxVariants act before the boundary / are unused by the reference, so they are not here. */
+typedef struct {
+    int32_t min_base_quality;    /* pileup min_base_quality -> pysam pileup_base_qual_skip */
+    int32_t min_total_depth;     /* :131 */
+    int32_t min_allele_depth;    /* :153 */
+    int32_t reserved0;
+    double min_evidence_ratio;   /* :154 */
+    int64_t reserved1[4];
+} spg_params;
+
+/* One emitted variant (a row of prepare_variants(), live_variant_caller.py:170-185). */
+typedef struct {
+    int64_t pos;           /* 'start' (0-based); 'stop' = pos + 1 */
+    int32_t dp;            /* info DP  = totalDepth */
+    int32_t ad;            /* info AD  = len(snvs[allele]) */
+    int32_t pl;            /* info PL  = round(-10*gl), 0 when GL == 0 */
+    int32_t score;         /* info SCORE = to_phred_scale(1 - GL/sum(GL)) */
+    uint8_t ref;           /* alleles[0]: reference char as stored at first visit (case kept) */
+    uint8_t alt;           /* alleles[1]: allele char "=ACMGRSVTWYHKDBN"[code] */
+    uint8_t gl_zero;       /* 1 when GL == 0 (then info GL is the int 0) */
+    uint8_t rank;          /* index of the allele in snvs dict order */
+    uint32_t first_batch;  /* batch sequence number (1-based) of the position's first visit:
+                              prepare_variants iterates memory in insertion order */
+    double gl;             /* info GL = log10(GL) (0 when GL == 0) */
+    double gl_linear;      /* GL itself (utils.genotype_likelihood) */
+    double qual;           /* 'qual' = np.mean(eps list) */
+} spg_candidate;           /* 56 bytes */
+
+/* Full per-allele record of a replayed position (exotic alleles, subnormal band). */
+typedef struct {
+    int64_t pos;
+    uint32_t depth;
+    uint8_t n_alleles;     /* alleles in dict order */
+    uint8_t pad[3];
+    uint8_t code[16];      /* nibble codes in dict order */
+    uint32_t count[16];
+    double gl[16];         /* exact reference-order GL per allele (NaN if not evaluated) */
+} spg_detail;              /* 224 bytes */
+
+typedef struct spg_ctx spg_ctx;
+
+/* thread-local message of the last failing call ("" if none) */
+const char *spg_last_error(void);
+int spg_abi_version(void);
+
+/* LiveVariantCaller.__init__ (live_variant_caller.py:22-32): device accumulators for n_pos
+ * reference positions on HIP device `device`. */
+int spg_create(int device, int64_t n_pos, const spg_params *p, spg_ctx **out);
+int spg_destroy(spg_ctx *ctx);                             /* __del__ (:34-35) */
+int spg_reset(spg_ctx *ctx);                               /* reset_memory (:37-38) */
+
+/* from_phred_scale (utils.py:9-10): the 256 eps values, produced by the caller with the
+ * reference's own math.pow so device eps are bit-identical. */
+int spg_set_eps_lut(spg_ctx *ctx, const double lut[256]);
+
+/* fastaFile.fetch(reference_name) (:78): the contig the next batches belong to; the char at
+ * a position is stored on its first visit (memory[pos]['reference'], :81). */
+int spg_set_reference(spg_ctx *ctx, const char *seq, int64_t len);
+
+/* process_bam / process_pileup_column / process_svn (:54-103) for one CSR batch.
+ * Accumulates across calls like `memory` does.  Host pointers by default (copied on the ctx
+ * stream); see SPG_IN_* flags.  Returns after enqueue. */
+int spg_accumulate(spg_ctx *ctx, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
+                   const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries);
+int spg_accumulate_ex(spg_ctx *ctx, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
+                      const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags);
+
+/* prepare_variants (:120-231) + genotype_likelihood / to_phred_scale (utils.py:12-24):
+ * per-position table and the candidate list, on device.  Returns after enqueue. */
+int spg_finalize(spg_ctx *ctx);
+
+int spg_sync(spg_ctx *ctx);
+
+/* Copy table rows [pos0, pos0+n) to host; any pointer may be NULL.
+ *   depth[n] u32; counts[n*8] u32 (A C G T N DEL REFSKIP OTHER); gl[n*5] f64 (A C G T N,
+ *   NaN where not evaluated / allele absent); flags[n] u8 (SPG_F_*); order[n] u32 (snvs dict
+ *   order: bits 0-2 = k, bits 3+3i..5+3i = slot of the i-th allele); first_batch[n] u32. */
+int spg_get_table(spg_ctx *ctx, int64_t pos0, int64_t n, uint32_t *depth, uint32_t *counts, double *gl,
+                  uint8_t *flags, uint32_t *order, uint32_t *first_batch);
+/* Number of candidates / replayed details produced by the last spg_finalize. */
+int spg_count(spg_ctx *ctx, int64_t *n_candidates, int64_t *n_details);
+/* Candidates in device append order (the shim orders them by (first_batch, pos, rank)). */
+int spg_get_candidates(spg_ctx *ctx, spg_candidate *out, int64_t cap, int64_t *n_out);
+int spg_get_details(spg_ctx *ctx, spg_detail *out, int64_t cap, int64_t *n_out);
+
+/* Device pointers of the result buffers (for zero-copy consumers on the same device, e.g. a
+ * torch.distributed gather).  Valid until the next spg_finalize / spg_reset / spg_destroy. */
+int spg_device_results(spg_ctx *ctx, void **candidates, void **n_candidates);
+
+/* Device-to-device copy of the call table into caller memory on the ctx device: dst[0..8) gets the
+ * candidate count (u64), dst + 8 up to `cap` spg_candidate records; synchronises the ctx stream so
+ * another stream (e.g. an RCCL gather) may read dst afterwards. */
+int spg_copy_candidates_device(spg_ctx *ctx, void *dst, int64_t cap);
+
+/* Timing hooks (bench): HIP events around the last accumulate / finalize kernels, ms. */
+int spg_last_kernel_ms(spg_ctx *ctx, float *accumulate_ms, float *finalize_ms);
+
+/* Introspection for tests. */
+int spg_device_count(int *n);
+size_t spg_sizeof_candidate(void);
+size_t spg_sizeof_detail(void);
+size_t spg_sizeof_acc(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPINGS_GPU_H */
