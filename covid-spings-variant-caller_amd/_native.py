@@ -11,7 +11,7 @@ import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIBDIR = os.path.join(PKG, "_lib")
-GPU_LIB = os.path.join(LIBDIR, "libspings_gpu.so")
+GPU_LIB = os.environ.get("SPG_GPU_LIB") or os.path.join(LIBDIR, "libspings_gpu.so")   # override: A/B builds
 PILEUP_LIB = os.path.join(LIBDIR, "libspings_pileup.so")
 
 SPG_NSLOT = 5
@@ -55,6 +55,13 @@ def gpu_lib():
     global _gpu
     if _gpu is not None:
         return _gpu
+    # One HIP runtime per process: torch ships its own libamdhip64 (same SONAME).  Loading torch
+    # first makes our library bind to that already-loaded runtime instead of /opt/rocm's copy
+    # (two runtimes in one process leave the second without GPUs).
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
     if not os.path.exists(GPU_LIB):
         raise NativeError(f"{GPU_LIB} not found: build it with __graft_entry__.build() "
                           "(python covid-spings-variant-caller_amd/build.py); the engine has no CPU path")

@@ -17,7 +17,6 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
                              const uint8_t *ref, const Tables *T, Acc *acc, hipStream_t st);
 hipError_t launch_finalize(const FParams &F, const Acc *acc, const Tables *T, const Out &O, const Hist *H,
                            hipStream_t st);
-hipError_t launch_set_hist(Hist *dst, const Hist &h, hipStream_t st);
 }  // namespace spg
 
 using namespace spg;
@@ -56,6 +55,8 @@ struct spg_ctx {
     Hist *d_hist = nullptr;
     int64_t d_hist_cap = 0;
     uint32_t batch_seq = 0;
+    uint32_t epoch = 1;        // Acc records of other epochs read as empty (reset = epoch bump)
+    uint32_t cslot = 0;        // Counters slot of the last finalize
     // outputs
     uint32_t *o_depth = nullptr, *o_counts = nullptr, *o_order = nullptr, *o_first = nullptr;
     double *o_gl = nullptr;
@@ -100,8 +101,8 @@ static int alloc_outputs(spg_ctx *c) {
     HIPCHK(hipMalloc(&c->cand, sizeof(spg_candidate) * c->cand_cap));
     c->detail_cap = std::max<int64_t>(1024, std::min<int64_t>(n + 1, 65536));
     HIPCHK(hipMalloc(&c->detail, sizeof(spg_detail) * c->detail_cap));
-    HIPCHK(hipMalloc(&c->ctr, sizeof(Counters)));
-    HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
+    HIPCHK(hipMalloc(&c->ctr, 2 * sizeof(Counters)));
+    HIPCHK(hipMemsetAsync(c->ctr, 0, 2 * sizeof(Counters), c->stream));
     return 0;
 }
 
@@ -161,7 +162,10 @@ int spg_reset(spg_ctx *c) {
     for (auto &h : c->hist) owned |= h.owned;
     if (owned) HIPCHK(hipStreamSynchronize(c->stream));
     free_history(c);
-    HIPCHK(hipMemsetAsync(c->acc, 0, sizeof(Acc) * c->n_pos, c->stream));
+    if (++c->epoch == 0) {     // wrapped: clear the records once and restart at epoch 1
+        HIPCHK(hipMemsetAsync(c->acc, 0, sizeof(Acc) * c->n_pos, c->stream));
+        c->epoch = 1;
+    }
     c->batch_seq = 0;
     c->finalized = false;
     return 0;
@@ -186,7 +190,7 @@ int spg_set_eps_lut(spg_ctx *c, const double lut[256]) {
     }
     t->fast[0][0] = 0.0;
     t->fast[0][1] = 0.0;
-    for (int q = 1; q < 128; q++) {
+    for (int q = 1; q < 256; q++) {
         t->fast[q][0] = t->l1m[q];
         t->fast[q][1] = t->eps[q];
     }
@@ -214,25 +218,20 @@ int spg_set_reference(spg_ctx *c, const char *seq, int64_t len) {
     return 0;
 }
 
-static int push_history_table(spg_ctx *c) {
+static int grow_history_table(spg_ctx *c) {
     const int64_t n = (int64_t)c->hist.size();
-    if (n > c->d_hist_cap) {
-        int64_t cap = std::max<int64_t>(16, c->d_hist_cap * 2);
-        while (cap < n) cap *= 2;
-        Hist *nh = nullptr;
-        HIPCHK(hipMalloc(&nh, sizeof(Hist) * cap));
-        if (c->d_hist) {
-            HIPCHK(hipMemcpyAsync(nh, c->d_hist, sizeof(Hist) * (n - 1), hipMemcpyDeviceToDevice, c->stream));
-            HIPCHK(hipStreamSynchronize(c->stream));
-            HIPCHK(hipFree(c->d_hist));
-        }
-        c->d_hist = nh;
-        c->d_hist_cap = cap;
+    if (n <= c->d_hist_cap) return 0;
+    int64_t cap = std::max<int64_t>(64, c->d_hist_cap * 2);
+    while (cap < n) cap *= 2;
+    Hist *nh = nullptr;
+    HIPCHK(hipMalloc(&nh, sizeof(Hist) * cap));
+    if (c->d_hist) {
+        HIPCHK(hipMemcpyAsync(nh, c->d_hist, sizeof(Hist) * (n - 1), hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipFree(c->d_hist));
     }
-    const HistBatch &b = c->hist.back();
-    Hist h{b.pos_begin, b.n_cols, b.off, b.code, b.qual};
-    // stream-ordered by-value write: no host synchronisation per batch
-    HIPCHK(launch_set_hist(c->d_hist + (n - 1), h, c->stream));
+    c->d_hist = nh;
+    c->d_hist_cap = cap;
     return 0;
 }
 
@@ -284,15 +283,21 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
             }
     }
     c->hist.push_back(hb);
-    int rc = push_history_table(c);
+    int rc = grow_history_table(c);
     if (rc) return rc;
     c->batch_seq++;
+    // Work decomposition from the batch's mean depth (no per-column host pass, so device inputs
+    // need no host copy of the offsets).  Deep batches (mean >= 2048 entries per column) stream every
+    // column through k_acc_seg<4> (16 entries/lane/chunk); shallower batches run a lane-per-column
+    // pass for columns below t_deep = 128 and k_acc_seg<1> (4 entries/lane/chunk) for the rest.
+    // Each wave owns G consecutive columns; G targets ~one resident wave per slot.
     const double avg = (double)n_entries / (double)n_cols;
-    uint32_t G = 1;
-    if (avg < 2048.0) {
-        const double want = 2048.0 / std::max(avg, 1.0);
-        while (G * 2 <= want && G < 64) G *= 2;
-    }
+    static const int64_t target_waves = [] {
+        const char *e = getenv("SPG_TARGET_WAVES");
+        return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)4096;
+    }();
+    const bool deep_batch = avg >= 2048.0;
+    const uint32_t G = (uint32_t)std::min<int64_t>(64, std::max<int64_t>(1, (n_cols + target_waves - 1) / target_waves));
     KParams P{};
     P.pos_begin = pos_begin;
     P.n_cols = n_cols;
@@ -302,8 +307,11 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
     P.kpass = mb <= 0 ? 0x80808080u : (mb >= 128 ? 0u : (uint32_t)(0x80 - mb) * 0x01010101u);
     P.kok = P.qlo >= 128 ? 0u : (uint32_t)(0x80 - P.qlo) * 0x01010101u;
     P.batch_seq = c->batch_seq;
+    P.epoch = c->epoch;
+    P.hdesc = Hist{pos_begin, n_cols, hb.off, hb.code, hb.qual};
+    P.hslot = c->d_hist + (c->hist.size() - 1);
     P.G = G;
-    P.t_deep = G == 1 ? 64u : 128u;
+    P.t_deep = deep_batch ? 1u : 128u;
     HIPCHK(hipEventRecord(c->ev[0], c->stream));
     HIPCHK(launch_accumulate(P, hb.off, hb.code, hb.qual, c->ref, c->tables, c->acc, c->stream));
     HIPCHK(hipEventRecord(c->ev[1], c->stream));
@@ -336,6 +344,8 @@ static FParams make_fparams(spg_ctx *c) {
     F.detail_cap = c->detail_cap;
     F.min_bq = c->p.min_base_quality;
     F.n_hist = (int32_t)c->hist.size();
+    F.epoch = c->epoch;
+    F.cslot = c->cslot;
     return F;
 }
 
@@ -343,7 +353,7 @@ int spg_finalize(spg_ctx *c) {
     if (!c) return fail("spg_finalize: null ctx");
     if (!c->lut_set) return fail("spg_finalize: spg_set_eps_lut not called");
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
+    c->cslot ^= 1u;            // this call counts in slot cslot (zeroed by the previous call / creation)
     HIPCHK(hipEventRecord(c->ev[2], c->stream));
     HIPCHK(launch_finalize(make_fparams(c), c->acc, c->tables, make_out(c), c->d_hist, c->stream));
     HIPCHK(hipEventRecord(c->ev[3], c->stream));
@@ -364,7 +374,7 @@ static int settle(spg_ctx *c, Counters &h) {
     if (!c->finalized) return fail("spg: spg_finalize has not been called since the last accumulate/reset");
     HIPCHK(hipSetDevice(c->device));
     for (int iter = 0; iter < 4; iter++) {
-        HIPCHK(hipMemcpyAsync(&h, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(&h, c->ctr + c->cslot, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (h.err) return fail("spg: replay found a depth mismatch between history and accumulators");
         bool again = false;
@@ -446,7 +456,7 @@ int spg_get_table(spg_ctx *c, int64_t pos0, int64_t n, uint32_t *depth, uint32_t
 int spg_device_results(spg_ctx *c, void **candidates, void **n_candidates) {
     if (!c) return fail("spg_device_results: null ctx");
     if (candidates) *candidates = c->cand;
-    if (n_candidates) *n_candidates = &c->ctr->n_cand;
+    if (n_candidates) *n_candidates = &c->ctr[c->cslot].n_cand;
     return 0;
 }
 
@@ -454,7 +464,7 @@ int spg_copy_candidates_device(spg_ctx *c, void *dst, int64_t cap) {
     if (!c || !dst || cap < 0) return fail("spg_copy_candidates_device: bad argument");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemsetAsync(dst, 0, 8, c->stream));
-    HIPCHK(hipMemcpyAsync(dst, &c->ctr->n_cand, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(dst, &c->ctr[c->cslot].n_cand, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
     const int64_t n = std::min<int64_t>(cap, c->cand_cap);
     if (n) HIPCHK(hipMemcpyAsync((char *)dst + 8, c->cand, sizeof(spg_candidate) * n, hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));

@@ -1,10 +1,12 @@
-// spg_device.h — device-side data layout and helpers shared by the engine kernels (gfx950).
+// spg_device.h — device-side data layout shared by the engine kernels (gfx950) and the host API.
 //
 // Layout in HBM (one context = one contiguous reference range of n_pos positions):
 //   Acc      acc[n_pos]      160 B AoS record per position (accumulators of LiveVariantCaller.memory)
 //   Tables   *tables         eps / ln(1-eps) / 10^-k LUTs (from the reference's from_phred_scale)
-//   batch CSR (history)      offsets u64[n_cols+1], base_code u8[E], qual u8[E] (16-B padded)
-//   outputs (SoA)            depth u32, counts u32[8], gl f64[5], flags u8, order u32, first_batch u32
+//   Hist     hist[n_batches] descriptors of the accumulated CSR batches (the exact replay walks them)
+//   batch CSR                offsets u64[n_cols+1], base_code u8[E], qual u8[E] (16-B padded)
+//   outputs (SoA)            depth u32, counts u32[8], gl f64[5], flags u8, order u32, first_batch u32,
+//                            candidates, details, Counters[2]
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,18 +19,20 @@ constexpr int NSLOT = SPG_NSLOT;          // A C G T N
 constexpr uint32_t INF32 = 0xFFFFFFFFu;
 constexpr uint32_t MISC_EXOTIC = 0x100u;  // acc.misc bit: an allele outside A,C,G,T,N was seen
 
-// Accumulators replacing Site (structs.py:2-6) — the q lists are replaced by sufficient
-// statistics: counts, integer sum of q (log10 of the eps product up to fp64 rounding),
-// sum of ln(1-eps) (the hypothesis product), sum of eps (QUAL), a lower bound on q (H == 0 iff
-// a Q0 entry; q >= 4 makes every eps factor < 1/2, which the underflow proof needs) and the
-// dict insertion order of the alleles.  The exact ordered lists live on as the batch history
-// that the replay kernel walks for the rare positions where order matters (subnormal band).
+// Accumulators replacing Site (structs.py:2-6).  The q lists are replaced by sufficient
+// statistics: counts, the integer sum of q (log10 of the eps product up to fp64 rounding), the sum
+// of ln(1-eps) (the hypothesis product), the sum of eps (QUAL), a lower bound on q (H == 0 iff a
+// Q0 entry; q >= 4 makes every eps factor < 1/2, which the underflow proof needs) and the dict
+// insertion order of the alleles.  The exact ordered lists live on as the batch history that the
+// replay walks for the rare positions where the order of fp64 roundings matters.
+// A record belongs to the current sample only when `epoch` matches the context's epoch: reset is
+// an epoch bump, not a memset.
 struct __align__(16) Acc {
     uint32_t depth;        // totalDepth (:75, :87)
-    uint32_t first_batch;  // 0 = not in memory; else batch seq of first visit (dict order)
+    uint32_t first_batch;  // batch seq of first visit (dict insertion order); 0 = not in memory
     uint32_t order;        // bits 0-2 n alleles; bits 3+3i.. slot of i-th allele (snvs dict order)
     uint32_t misc;         // bits 0-7 REF char stored at first visit (:81); MISC_EXOTIC
-    uint32_t n_del, n_skip, n_other, pad0;
+    uint32_t n_del, n_skip, n_other, epoch;
     uint32_t cnt[NSLOT];
     uint32_t sq[NSLOT];    // sum q, saturating at 2^31
     uint8_t qf[8];         // q lower bound per slot (exact below 4)
@@ -41,25 +45,7 @@ struct Tables {
     double eps[256];       // from_phred_scale(q), bit-identical to the reference (host-supplied)
     double l1m[256];       // log1p(-eps[q]); l1m[0] = 0 (Q0 handled through qf == 0)
     double p10k[336];      // 10^-k, correctly rounded, k = 0..335
-    double fast[128][2];   // {l1m, eps} for q = 1..127; row 0 = {0, 0} ("not selected")
-};
-
-struct KParams {
-    int64_t pos_begin, n_cols;
-    int32_t min_bq, qlo;   // qlo = max(min_bq, 4): fast-path floor
-    uint32_t kpass, kok;   // SWAR compare constants
-    uint32_t batch_seq;    // 1-based
-    uint32_t G;            // columns per wave group
-    uint32_t t_deep;       // columns with >= t_deep raw entries are processed wave-wide
-    uint32_t pad;
-};
-
-struct FParams {
-    int64_t n_pos;
-    int32_t min_td, min_ad;
-    double ratio;
-    int64_t cand_cap, band_cap, detail_cap;
-    int32_t min_bq, n_hist;
+    double fast[256][2];   // {l1m, eps} for q = 1..255; row 0 = {0, 0} ("not selected" / Q0)
 };
 
 struct Hist {               // one accumulated batch, kept for the exact replay
@@ -69,8 +55,29 @@ struct Hist {               // one accumulated batch, kept for the exact replay
     const uint8_t *qual;
 };
 
-struct Counters {           // zeroed at the start of every finalize
+struct KParams {
+    int64_t pos_begin, n_cols;
+    int32_t min_bq, qlo;   // qlo = max(min_bq, 4): fast-path floor
+    uint32_t kpass, kok;   // SWAR compare constants
+    uint32_t batch_seq;    // 1-based within the epoch
+    uint32_t epoch;
+    uint32_t G;            // columns per wave group
+    uint32_t t_deep;       // columns with >= t_deep raw entries are processed wave-wide
+    Hist hdesc;            // this batch's history descriptor ...
+    Hist *hslot;           // ... written here by the first thread of the launch
+};
+
+struct Counters {           // per finalize; two slots, the kernel zeroes the other one
     uint32_t n_cand, n_band, n_detail, err;
+};
+
+struct FParams {
+    int64_t n_pos;
+    int32_t min_td, min_ad;
+    double ratio;
+    int64_t cand_cap, band_cap, detail_cap;
+    int32_t min_bq, n_hist;
+    uint32_t epoch, cslot;
 };
 
 struct Out {                // SoA result table
@@ -80,7 +87,7 @@ struct Out {                // SoA result table
     spg_candidate *cand;
     int64_t *band;
     spg_detail *detail;
-    Counters *ctr;
+    Counters *ctr;          // Counters[2]
 };
 
 __device__ __forceinline__ int slot_of(uint32_t c) {

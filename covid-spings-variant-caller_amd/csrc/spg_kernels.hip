@@ -1,24 +1,25 @@
 // spg_kernels.hip — CDNA4 (gfx950) kernels of the pileup + genotype-likelihood engine.
 //
-//   k_accumulate  process_pileup_column / process_svn (live_variant_caller.py:74-103) + pysam's
-//                 base-quality filter, for one CSR batch; merges into the per-position Acc records.
-//                 Deep columns: one wave64 per column, 16 entries per lane per step (dwordx4 loads
-//                 of base_code and qual), SWAR byte tests, v_dot4_u32_u8 quality sums, v_bcnt
-//                 counts and an LDS-resident {ln(1-eps), eps} table; the rare entries (minor
-//                 alleles, D/N, q < 4, q >= 128, IUPAC) take an exact per-entry path.
-//                 Shallow columns: one lane per column, sequential.
-//   k_finalize    prepare_variants (:120-185) + genotype_likelihood / to_phred_scale
-//                 (utils.py:12-24): per-position GL in fp64 with the reference's underflow
-//                 decisions, candidate filters, GL/PL/SCORE/QUAL; positions whose result depends
-//                 on the order of fp64 roundings in the subnormal range go to k_replay.
-//   k_replay      exact sequential recomputation (np.prod left folds in BAM order, dict-order
-//                 GL chains) over the batch history for the listed positions.
+//   k_acc_deep<W>  process_pileup_column / process_svn (live_variant_caller.py:74-103) + pysam's
+//                  base-quality filter for one CSR batch, one wave64 per column: coalesced dwordx4
+//                  (W=4) or dword (W=1) loads of base_code and qual two steps ahead, SWAR byte tests,
+//                  v_dot4_u32_u8 quality sums, v_bcnt counts and an LDS {ln(1-eps), eps} table for the
+//                  column's major allele; the rare entries (minor alleles, D/N, q < 4, q >= 128, IUPAC)
+//                  go exactly, one by one, into a per-wave LDS record (LDS atomics).
+//   k_acc_shallow  the same for short columns, one lane per column, sequential.
+//   k_finalize     prepare_variants (:120-185) + genotype_likelihood / to_phred_scale
+//                  (utils.py:12-24): per-position GL in fp64 with the reference's underflow decisions,
+//                  candidate filters, GL/PL/SCORE/QUAL.  A position whose result depends on the order
+//                  of fp64 roundings in the subnormal range (or that holds IUPAC alleles) is recomputed
+//                  exactly by walking the batch history (np.prod left folds in BAM order).
+#include <type_traits>
+
 #include "spg_device.h"
 
 namespace spg {
 
 // ------------------------------------------------------------------------------------------
-// per-lane column state (rare/exact path and shallow columns)
+// per-lane column state (shallow columns)
 // ------------------------------------------------------------------------------------------
 struct ColState {
     uint32_t depth, n_del, n_skip, n_other;
@@ -71,11 +72,83 @@ __device__ __forceinline__ double wsumd(double v) {
     return v;
 }
 
-// ------------------------------------------------------------------------------------------
-// merge one column's batch statistics into its Acc record (single lane)
-// ------------------------------------------------------------------------------------------
-__device__ void merge_acc(Acc *__restrict__ A, const ColState &c, uint32_t batch_seq, uint8_t refc) {
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// DPP wave reductions: quad_perm / row_half_mirror / row_mirror give every lane its 16-lane row
+// total with VALU-latency steps (no LDS round trips); the four row totals are combined through
+// readlane.  Fixed pattern -> deterministic fp64 summation order.
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v, int ctrl) {
+    switch (ctrl) {
+        case 0: return __builtin_amdgcn_update_dpp(0u, v, 0xB1, 0xF, 0xF, false);    // quad_perm [1,0,3,2]
+        case 1: return __builtin_amdgcn_update_dpp(0u, v, 0x4E, 0xF, 0xF, false);    // quad_perm [2,3,0,1]
+        case 2: return __builtin_amdgcn_update_dpp(0u, v, 0x141, 0xF, 0xF, false);   // row_half_mirror
+        default: return __builtin_amdgcn_update_dpp(0u, v, 0x140, 0xF, 0xF, false);  // row_mirror
+    }
+}
+__device__ __forceinline__ uint32_t dsum_u32(uint32_t v) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) v += dpp_u32(v, c);
+    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
+           __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+}
+__device__ __forceinline__ uint32_t dmin_u32(uint32_t v) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) v = min(v, dpp_u32(v, c));
+    return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+               min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+__device__ __forceinline__ double rl_f64(double v, int l) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double dsum_f64(double v) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const uint64_t b = __builtin_bit_cast(uint64_t, v);
+        const uint32_t lo = dpp_u32((uint32_t)b, c), hi = dpp_u32((uint32_t)(b >> 32), c);
+        v += __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+    }
+    return (rl_f64(v, 0) + rl_f64(v, 16)) + (rl_f64(v, 32) + rl_f64(v, 48));
+}
+
+// New alleles join the dict in order of first appearance in this batch (:100-101).
+__device__ __forceinline__ uint32_t merge_order(uint32_t order, uint32_t newmask, const uint32_t *first) {
+    uint32_t n = order & 7u;
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) {
+        if ((newmask >> k) & 1u) {
+            uint32_t rank = 0;
+#pragma unroll
+            for (int j = 0; j < NSLOT; j++)
+                if (j != k && ((newmask >> j) & 1u) && (first[j] < first[k] || (first[j] == first[k] && j < k)))
+                    rank++;
+            order |= (uint32_t)k << (3 + 3 * (n + rank));
+        }
+    }
+    return (order & ~7u) | (n + __popc(newmask));
+}
+
+__device__ __forceinline__ uint32_t order_mask(uint32_t order) {
+    uint32_t have = 0;
+    const uint32_t n = order & 7u;
+#pragma unroll
+    for (uint32_t i = 0; i < NSLOT; i++)
+        if (i < n) have |= 1u << ((order >> (3 + 3 * i)) & 7u);
+    return have;
+}
+
+// Merge one column's batch statistics into its Acc record (single lane; shallow path).
+__device__ void merge_acc(Acc *__restrict__ A, const ColState &c, uint32_t batch_seq, uint32_t epoch, uint8_t refc) {
     Acc a = *A;
+    if (a.epoch != epoch) {                         // record of an older sample: start afresh
+        a = Acc{};
+        a.epoch = epoch;
+    }
     if (a.first_batch == 0) {                       // first visit (:77-85)
         a.first_batch = batch_seq;
         a.misc = refc;
@@ -85,9 +158,7 @@ __device__ void merge_acc(Acc *__restrict__ A, const ColState &c, uint32_t batch
     a.n_skip += c.n_skip;
     a.n_other += c.n_other;
     if (c.n_other) a.misc |= MISC_EXOTIC;
-    uint32_t n = a.order & 7u;
-    uint32_t have = 0;
-    for (uint32_t i = 0; i < n; i++) have |= 1u << ((a.order >> (3 + 3 * i)) & 7u);
+    const uint32_t have = order_mask(a.order);
     uint32_t newmask = 0;
 #pragma unroll
     for (int k = 0; k < NSLOT; k++) {
@@ -102,20 +173,7 @@ __device__ void merge_acc(Acc *__restrict__ A, const ColState &c, uint32_t batch
             if (!((have >> k) & 1u)) newmask |= 1u << k;
         }
     }
-    // new alleles join the dict in order of first appearance in this batch (:100-101)
-#pragma unroll
-    for (int k = 0; k < NSLOT; k++) {
-        if ((newmask >> k) & 1u) {
-            uint32_t rank = 0;
-#pragma unroll
-            for (int j = 0; j < NSLOT; j++)
-                if (j != k && ((newmask >> j) & 1u) && (c.first[j] < c.first[k] || (c.first[j] == c.first[k] && j < k)))
-                    rank++;
-            a.order |= (uint32_t)k << (3 + 3 * (n + rank));
-        }
-    }
-    n += __popc(newmask);
-    a.order = (a.order & ~7u) | n;
+    a.order = merge_order(a.order, newmask, c.first);
     *A = a;
 }
 
@@ -136,21 +194,17 @@ __device__ __forceinline__ void swar4(uint32_t cw, uint32_t qw, uint32_t v80, ui
     rare80 = (pass80 | hi80) & ~fast80 & v80;
 }
 
-__device__ __forceinline__ uint32_t valid80(int64_t base, int64_t b, int64_t e) {
-    int64_t lead = b - base, end = e - base;
+__device__ __forceinline__ uint32_t valid80(int32_t x, int32_t b, int32_t e) {   // bytes x..x+3 in [b,e)
+    int32_t lead = b - x, end = e - x;
     lead = lead < 0 ? 0 : (lead > 4 ? 4 : lead);
     end = end < 0 ? 0 : (end > 4 ? 4 : end);
     return (uint32_t)((0x80808080ull << (8 * lead)) & (0x80808080ull >> (8 * (4 - end))));
 }
 
-__device__ __forceinline__ uint32_t pack_rare(uint32_t r80) {   // bits 7,15,23,31 -> 0..3
-    const uint32_t t = r80 >> 7;
-    return (t | (t >> 7) | (t >> 14) | (t >> 21)) & 0xFu;
-}
-
 template <int W>   // W dwords per lane per step: 4 (16 entries, dwordx4) or 1 (4 entries)
 struct Vec;
-template <> struct Vec<4> { using T = uint4; };
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <> struct Vec<4> { using T = u32x4; };
 template <> struct Vec<1> { using T = uint32_t; };
 
 template <int W>
@@ -159,194 +213,440 @@ __device__ __forceinline__ uint32_t dw(const typename Vec<W>::T &v, int d) {
     else return d == 0 ? v.x : d == 1 ? v.y : d == 2 ? v.z : v.w;
 }
 
-// Wave-wide processing of one deep column [b, e) of the batch arrays.  Every lane returns the
-// column's complete statistics in `out`.
+// Per-wave LDS record of the column the wave is processing.  Rare entries are few, so LDS atomics
+// from the lanes that hold one are cheap, and the wave needs no register state for them.
+struct __align__(8) WaveRare {
+    double sl[NSLOT], se[NSLOT];
+    uint32_t depth, n_del, n_skip, n_other;
+    uint32_t cnt[NSLOT], sq[NSLOT], qf[NSLOT], first[NSLOT];
+};
+static_assert(sizeof(WaveRare) == 176, "WaveRare");
+
+__device__ __forceinline__ void rare_init(WaveRare *R, int lane) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(R);
+    // words 0..19 doubles, 20..23 counters, 24..33 cnt/sq: 0; 34..38 qf: 255; 39..43 first: INF
+    if (lane < 44) w[lane] = lane < 34 ? 0u : (lane < 39 ? 255u : INF32);
+}
+
+__device__ __forceinline__ void rare_entry(WaveRare *R, uint32_t code, uint32_t q, uint32_t idx,
+                                           const double2 *__restrict__ lut) {
+    atomicAdd(&R->depth, 1u);
+    if (code == SPG_CODE_DEL) { atomicAdd(&R->n_del, 1u); return; }
+    if (code == SPG_CODE_SKIP) { atomicAdd(&R->n_skip, 1u); return; }
+    const int sl = slot_of(code);
+    if (sl < 0) { atomicAdd(&R->n_other, 1u); return; }
+    atomicAdd(&R->cnt[sl], 1u);
+    atomicAdd(&R->sq[sl], q);
+    atomicMin(&R->qf[sl], q);
+    atomicMin(&R->first[sl], idx);
+    const double2 t = lut[q];                          // {ln(1-eps), eps}; row 0 holds {0, 0}
+    atomicAdd(&R->sl[sl], t.x);
+    atomicAdd(&R->se[sl], q == 0 ? 1.0 : t.y);         // eps(Q0) = 1
+}
+
+// Wave-uniform buffer descriptor over bytes [0, n) of a column (T8/T20: the inputs go through
+// readfirstlane so hipcc can prove uniformity; out-of-range lanes read zeros, no per-lane branch).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t column_rsrc(const uint8_t *p, uint32_t n) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void *base = (void *)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)__builtin_amdgcn_readfirstlane(n), 0x00020000);
+}
+
 template <int W>
-__device__ void deep_column(const uint8_t *__restrict__ code, const uint8_t *__restrict__ qual, int64_t b, int64_t e,
-                            const KParams &P, const Tables *__restrict__ T, const double2 *__restrict__ lut,
-                            ColState &out) {
-    using V = typename Vec<W>::T;
-    constexpr int STEP = 64 * 4 * W;              // entries per wave step
-    const int lane = threadIdx.x & 63;
-    const int64_t a0 = b & ~(int64_t)(4 * W - 1);
-    const int nstep = (int)((e - a0 + STEP - 1) / STEP);
+__device__ __forceinline__ typename Vec<W>::T bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    if constexpr (W == 4) return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    else return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+}
 
-    // major allele: vote over the first entry of each lane's first chunk
-    uint32_t M;
-    {
-        const int64_t o = a0 + (int64_t)lane * 4 * W;
-        int vote = -1;
-        if (o >= b && o < e) vote = (int)code[o];
-        const uint64_t mA = __ballot(vote == 1), mC = __ballot(vote == 2), mG = __ballot(vote == 4),
-                       mT = __ballot(vote == 8);
-        const int cA = __popcll(mA), cC = __popcll(mC), cG = __popcll(mG), cT = __popcll(mT);
-        M = 1; int best = cA;
-        if (cC > best) { best = cC; M = 2; }
-        if (cG > best) { best = cG; M = 4; }
-        if (cT > best) { best = cT; M = 8; }
-    }
-    const uint32_t mrep = M * 0x01010101u;
-    const int Ms = slot_of(M);
+__device__ __forceinline__ void write_hist(const KParams &P) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *P.hslot = P.hdesc;
+}
 
-    uint32_t fcnt = 0, fsq = 0, ffirst = INF32;
-    double fsl0 = 0.0, fsl1 = 0.0, fse0 = 0.0, fse1 = 0.0;
-    bool found = false;
-    ColState rs;
-    cs_init(rs);
-
-    V cc, qq, cn, qn;
-    {
-        const int64_t o = a0 + (int64_t)lane * 4 * W;
-        if (o < e) { cc = *(const V *)(code + o); qq = *(const V *)(qual + o); }
-        else { cc = V{}; qq = V{}; }
-    }
-    for (int s = 0; s < nstep; s++) {
-        const int64_t base = a0 + (int64_t)s * STEP;
-        const int64_t o = base + (int64_t)lane * 4 * W;
-        if (s + 1 < nstep) {                       // prefetch the next step
-            const int64_t on = o + STEP;
-            if (on < e) { cn = *(const V *)(code + on); qn = *(const V *)(qual + on); }
-            else { cn = V{}; qn = V{}; }
-        }
-        const bool full = base >= b && base + STEP <= e;   // wave-uniform
-        uint32_t f80[W], r80[W];
-#pragma unroll
-        for (int d = 0; d < W; d++) {
-            const uint32_t v = full ? 0x80808080u : valid80(o + 4 * d, b, e);
-            swar4(dw<W>(cc, d), dw<W>(qq, d), v, mrep, P.kpass, P.kok, f80[d], r80[d]);
-        }
-        // fast path: major allele, 4 <= q < 128
-#pragma unroll
-        for (int d = 0; d < W; d++) {
-            const uint32_t qw = dw<W>(qq, d);
-            const uint32_t f01 = f80[d] >> 7;
-            fcnt += __popc(f80[d]);
-            fsq = __builtin_amdgcn_udot4(qw, f01, fsq, false);
-            const uint32_t idx = qw & (f01 * 0xFFu);
-            const double2 t0 = lut[idx & 0xFFu], t1 = lut[(idx >> 8) & 0xFFu];
-            const double2 t2 = lut[(idx >> 16) & 0xFFu], t3 = lut[idx >> 24];
-            fsl0 += t0.x; fse0 += t0.y; fsl1 += t1.x; fse1 += t1.y;
-            fsl0 += t2.x; fse0 += t2.y; fsl1 += t3.x; fse1 += t3.y;
-        }
-        if (!found) {                              // first fast entry of the column (dict order)
-            uint32_t mine = INF32;
-#pragma unroll
-            for (int d = W - 1; d >= 0; d--)
-                if (f80[d]) mine = (uint32_t)(o + 4 * d - b) + ((uint32_t)__builtin_ctz(f80[d]) >> 3);
-            const uint32_t w = wmin(mine);
-            if (w != INF32) { ffirst = w; found = true; }
-        }
-        // rare path: exact per entry
-        uint32_t m = 0;
-#pragma unroll
-        for (int d = 0; d < W; d++) m |= pack_rare(r80[d]) << (4 * d);
-        if (__ballot(m != 0)) {
-            while (m) {
-                const int j = __builtin_ctz(m);
-                m &= m - 1;
-                const int d = j >> 2, sh = (j & 3) * 8;
-                uint32_t cwd = dw<W>(cc, 0), qwd = dw<W>(qq, 0);
-#pragma unroll
-                for (int dd = 1; dd < W; dd++)
-                    if (d == dd) { cwd = dw<W>(cc, dd); qwd = dw<W>(qq, dd); }
-                const uint32_t c = (cwd >> sh) & 0xFFu, q = (qwd >> sh) & 0xFFu;
-                if ((int)q >= P.min_bq) entry_update(rs, c, q, (uint32_t)(o + j - b), T);
-            }
-        }
-        cc = cn; qq = qn;
-    }
-
-    // ---- wave reduction ----
-    out.depth = wsum(rs.depth) + wsum(fcnt);
-    out.n_del = wsum(rs.n_del);
-    out.n_skip = wsum(rs.n_skip);
-    out.n_other = wsum(rs.n_other);
-#pragma unroll
-    for (int k = 0; k < NSLOT; k++) {
-        if (__ballot(rs.cnt[k] != 0)) {
-            out.cnt[k] = wsum(rs.cnt[k]);
-            out.sq[k] = wsum(rs.sq[k]);
-            out.qf[k] = wmin(rs.qf[k]);
-            out.first[k] = wmin(rs.first[k]);
-            out.sl[k] = wsumd(rs.sl[k]);
-            out.se[k] = wsumd(rs.se[k]);
-        } else {
-            out.cnt[k] = 0; out.sq[k] = 0; out.qf[k] = 255u; out.first[k] = INF32; out.sl[k] = 0.0; out.se[k] = 0.0;
-        }
-    }
-    const uint32_t fc = wsum(fcnt);
-    if (fc) {
-        const uint32_t fs = wsum(fsq);
-        const double fl = wsumd(fsl0 + fsl1), fe = wsumd(fse0 + fse1);
+// Merge the column record R (LDS) into its Acc.  Cooperative: lane 0 writes the header and the dict
+// order, lanes 1..5 one allele slot each.  FRESH (first batch since reset): every record belongs to
+// an older epoch, so nothing is read back — the merge is pure stores.
+template <bool FRESH>
+__device__ __forceinline__ void merge_column(Acc *__restrict__ A, const WaveRare *R, uint32_t batch_seq,
+                                             uint32_t epoch, uint8_t refc, int lane) {
+    bool fresh = FRESH;
+    if constexpr (!FRESH) fresh = A->epoch != epoch;    // read by every lane before any lane writes
+    if (lane == 0) {
+        uint4 h0 = make_uint4(0, 0, 0, 0), h1 = make_uint4(0, 0, 0, 0);
+        if (!fresh) { h0 = reinterpret_cast<const uint4 *>(A)[0]; h1 = reinterpret_cast<const uint4 *>(A)[1]; }
+        if (h0.y == 0) { h0.y = batch_seq; h0.w = refc; }          // first visit (:77-85)
+        h0.x += R->depth;                                           // :87
+        h1.x += R->n_del; h1.y += R->n_skip; h1.z += R->n_other; h1.w = epoch;
+        if (R->n_other) h0.w |= MISC_EXOTIC;
+        const uint32_t have = order_mask(h0.z);
+        uint32_t newmask = 0, first[NSLOT];
 #pragma unroll
         for (int k = 0; k < NSLOT; k++) {
-            if (k == Ms) {
-                out.cnt[k] += fc; out.sq[k] += fs; out.sl[k] += fl; out.se[k] += fe;
-                out.qf[k] = min(out.qf[k], (uint32_t)P.qlo);
-                out.first[k] = min(out.first[k], ffirst);
+            first[k] = R->first[k];
+            if (R->cnt[k] && !((have >> k) & 1u)) newmask |= 1u << k;
+        }
+        h0.z = merge_order(h0.z, newmask, first);
+        reinterpret_cast<uint4 *>(A)[0] = h0;
+        reinterpret_cast<uint4 *>(A)[1] = h1;
+    } else if (lane <= NSLOT) {
+        const int k = lane - 1;
+        const uint32_t c = R->cnt[k];
+        uint32_t old = 0;
+        if (!fresh) old = A->cnt[k];
+        if (c) {
+            if (old) {
+                A->qf[k] = (uint8_t)min((uint32_t)A->qf[k], R->qf[k]);
+                const uint64_t sq = (uint64_t)A->sq[k] + R->sq[k];
+                A->sq[k] = sq > 0x80000000ull ? 0x80000000u : (uint32_t)sq;
+                A->sl[k] = A->sl[k] + R->sl[k];
+                A->se[k] = A->se[k] + R->se[k];
+            } else {
+                A->qf[k] = (uint8_t)R->qf[k];
+                A->sq[k] = R->sq[k] > 0x80000000u ? 0x80000000u : R->sq[k];
+                A->sl[k] = R->sl[k];
+                A->se[k] = R->se[k];
             }
+            A->cnt[k] = old + c;
+        } else if (fresh) {
+            A->cnt[k] = 0;
         }
     }
 }
 
-__global__ __launch_bounds__(256) void k_accumulate(KParams P, const uint64_t *__restrict__ off,
-                                                    const uint8_t *__restrict__ code,
-                                                    const uint8_t *__restrict__ qual,
-                                                    const uint8_t *__restrict__ ref,
-                                                    const Tables *__restrict__ T, Acc *__restrict__ acc) {
-    __shared__ double2 lut[128];
-    if (threadIdx.x < 128) lut[threadIdx.x] = make_double2(T->fast[threadIdx.x][0], T->fast[threadIdx.x][1]);
-    __syncthreads();
+struct Dual2 {              // per-lane partial sums of a wave's second fast allele
+    double sl[64], se[64];
+    uint32_t cnt[64], sq[64];
+};
 
+// Segment streaming: wave w owns G consecutive columns and walks them as ONE stream of 64 x 4W-entry
+// chunks (each column's chunks start at its 4W-aligned first entry), loaded two chunks ahead into
+// three register sets across column boundaries, so a column start costs no memory latency.
+// Loads go through one wave-uniform buffer descriptor per array over the segment (range-checked:
+// chunks past the end read zeros).  Per column: allele vote on its first chunk, SWAR/LUT fast path
+// for the major allele, exact rare path into the wave's LDS record, then a cooperative merge.
+template <int W, bool FRESH>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_acc_seg(KParams P, const uint64_t *__restrict__ off,
+                                                 const uint8_t *__restrict__ code, const uint8_t *__restrict__ qual,
+                                                 const uint8_t *__restrict__ ref, const Tables *__restrict__ T,
+                                                 Acc *__restrict__ acc) {
+    using V = typename Vec<W>::T;
+    constexpr uint32_t ALIGN = 4 * W;
+    constexpr uint32_t STEP = 64 * ALIGN;               // entries per chunk
+    constexpr uint32_t QCAP = 512;                     // per-wave rare-entry queue (LDS)
+    __shared__ double2 lut[256];
+    __shared__ WaveRare rare[4];
+    __shared__ uint2 rqueue[4][QCAP];
+    __shared__ Dual2 dual2[4];
+    write_hist(P);
+    lut[threadIdx.x] = make_double2(T->fast[threadIdx.x][0], T->fast[threadIdx.x][1]);
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int64_t g0 = wave * P.G;
     if (g0 >= P.n_cols) return;
-    const int64_t ng = min((int64_t)P.G, P.n_cols - g0);
+    const int ng = (int)min((int64_t)P.G, P.n_cols - g0);
+    WaveRare *R = rare + (threadIdx.x >> 6);
+    Dual2 *D2 = dual2 + (threadIdx.x >> 6);
+    uint2 *Q = rqueue[threadIdx.x >> 6];
+    uint32_t qn = 0;                                   // queued entries (wave-uniform)
+    // drain the queue into the LDS record: every lane takes one entry per round (LDS atomics)
+    auto drain = [&]() {                     // drain the queue into the LDS record (LDS atomics)
+        wave_sync();
+        for (uint32_t b0 = 0; b0 < qn; b0 += 64) {
+            if (b0 + lane < qn) {
+                const uint2 e = Q[b0 + lane];
+                rare_entry(R, e.x >> 8, e.x & 0xFFu, e.y, lut);
+            }
+        }
+        qn = 0;
+        wave_sync();
+    };
 
+    // lane j < ng describes column g0 + j
     uint64_t ob = 0, oe = 0;
-    if (lane < ng) { ob = off[g0 + lane]; oe = off[g0 + lane + 1]; }
-    const uint64_t len = oe - ob;
+    uint32_t refc = 0;
+    if (lane < ng) { ob = off[g0 + lane]; oe = off[g0 + lane + 1]; refc = ref[P.pos_begin + g0 + lane]; }
+    const uint64_t sb = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)ob) |
+                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ob >> 32)) << 32);
+    const uint64_t base = sb & ~(uint64_t)(ALIGN - 1);
+    const uint64_t send = (uint64_t)__builtin_amdgcn_readlane((uint32_t)oe, ng - 1) |
+                          ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(oe >> 32), ng - 1) << 32);
+    const uint32_t nbytes = (uint32_t)(((send - base) + ALIGN - 1) & ~(uint64_t)(ALIGN - 1));
+    const __amdgpu_buffer_rsrc_t rc = column_rsrc(code + base, nbytes), rq = column_rsrc(qual + base, nbytes);
+    const uint32_t b_rel = (uint32_t)(ob - base), e_rel = (uint32_t)(oe - base);
+    const uint32_t a_rel = b_rel & ~(ALIGN - 1);
+    const uint32_t len = (uint32_t)(oe - ob);
+    const uint32_t nch = (lane < ng && len > 0 && len >= P.t_deep) ? (e_rel - a_rel + STEP - 1) / STEP : 0u;
+    // exclusive prefix of the chunk counts: chunk i belongs to column popcount(pre <= i) - 1
+    uint32_t pre = nch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(pre, o);
+        if (lane >= o) pre += t;
+    }
+    const uint32_t total = __builtin_amdgcn_readlane(pre, 63);   // SGPR: loop bounds stay scalar
+    pre -= nch;
+    if (total == 0) return;
+    const uint32_t lo = (uint32_t)lane * ALIGN;
+    const uint32_t pre_m = lane < ng ? pre : 0xFFFFFFFFu;   // lanes without a column never count
+    auto col_of = [&](uint32_t i) -> int {       // wave-uniform: one v_cmp into an SGPR mask
+        return (int)__popcll(__ballot(pre_m <= i)) - 1;
+    };
+    auto chunk_off = [&](uint32_t i) -> uint32_t {   // branch-free: chunks past the end are loaded and ignored
+        const int j = col_of(min(i, total - 1));
+        return __builtin_amdgcn_readlane(a_rel, j) + (i - __builtin_amdgcn_readlane(pre, j)) * STEP + lo;
+    };
 
-    // shallow columns: one lane each, sequential
-    if (lane < ng && len > 0 && len < P.t_deep) {
-        ColState st;
-        cs_init(st);
-        for (uint64_t i = ob; i < oe; i++) {
-            const uint32_t c = code[i], q = qual[i];
-            if ((int)q >= P.min_bq) entry_update(st, c, q, (uint32_t)(i - ob), T);
+    V c0 = bload<W>(rc, chunk_off(0)), q0 = bload<W>(rq, chunk_off(0));
+    V c1 = bload<W>(rc, chunk_off(1)), q1 = bload<W>(rq, chunk_off(1));
+    V c2, q2;
+
+    // per-column state
+    int cj = 0;
+    uint32_t cs = 0, cpre = 0, cn = 0;
+    int32_t bl = 0, el = 0;                    // column bounds relative to its first chunk
+    uint32_t mrep = 0, M = 1;
+    uint32_t fcnt = 0, fsq = 0, ffirst = INF32;
+    double fsl = 0.0, fse = 0.0;
+    bool found = false;
+    // second fast allele (dual mode): a frequent minor allele (an SNV, an indel's D entries) would
+    // otherwise push thousands of entries through the rare path and stall its wave
+    bool dual = false;
+    uint32_t mrep2 = 0, M2 = 0;
+    uint32_t ffirst2 = INF32;
+    bool found2 = false;
+
+    auto process = [&](const V &cc, const V &qq, uint32_t i) {
+        cj = col_of(i);
+        cpre = __builtin_amdgcn_readlane(pre, cj);
+        cs = i - cpre;
+        if (cs == 0) {                         // ---- column begin ----
+            cn = __builtin_amdgcn_readlane(nch, cj);
+            const uint32_t a = __builtin_amdgcn_readlane(a_rel, cj);
+            bl = (int32_t)(__builtin_amdgcn_readlane(b_rel, cj) - a);
+            el = (int32_t)(__builtin_amdgcn_readlane(e_rel, cj) - a);
+            rare_init(R, lane);
+            const uint32_t v0 = dw<W>(cc, 0) & 0xFFu;
+            const int vote = ((int32_t)lo >= bl && (int32_t)lo < el) ? (int)v0 : -1;
+            int cnt7[7];
+            constexpr uint32_t VC[7] = {1u, 2u, 4u, 8u, 15u, SPG_CODE_DEL, SPG_CODE_SKIP};
+#pragma unroll
+            for (int k = 0; k < 7; k++) cnt7[k] = __popcll(__ballot(vote == (int)VC[k]));
+            int b1 = 0;                         // major: a base (its products need the LUT path)
+#pragma unroll
+            for (int k = 1; k < 4; k++) if (cnt7[k] > cnt7[b1]) b1 = k;
+            int b2 = -1, c2n = 1;               // second: any frequent code, >= 2 of 64 votes
+#pragma unroll
+            for (int k = 0; k < 7; k++) if (k != b1 && cnt7[k] > c2n) { c2n = cnt7[k]; b2 = k; }
+            M = VC[b1];
+            mrep = M * 0x01010101u;
+            dual = b2 >= 0;
+            M2 = dual ? VC[b2] : 0u;
+            mrep2 = dual ? M2 * 0x01010101u : 0xFFFFFFFFu;
+            fcnt = 0; fsq = 0; ffirst = INF32; fsl = 0.0; fse = 0.0; found = false;
+            ffirst2 = INF32; found2 = false;
+            if (dual) { D2->cnt[lane] = 0; D2->sq[lane] = 0; D2->sl[lane] = 0.0; D2->se[lane] = 0.0; }
+            wave_sync();
         }
-        const int64_t pos = P.pos_begin + g0 + lane;
-        merge_acc(acc + pos, st, P.batch_seq, ref[pos]);
-    }
-    // deep columns: the whole wave, one after another
-    uint64_t deep = __ballot(lane < ng && len >= P.t_deep);
-    while (deep) {
-        const int i = __builtin_ctzll(deep);
-        deep &= deep - 1;
-        const int64_t b = (int64_t)__shfl(ob, i), e = (int64_t)__shfl(oe, i);
-        ColState st;
-        if (e - b >= 2048) deep_column<4>(code, qual, b, e, P, T, lut, st);
-        else deep_column<1>(code, qual, b, e, P, T, lut, st);
-        if (lane == 0) {
-            const int64_t pos = P.pos_begin + g0 + i;
-            merge_acc(acc + pos, st, P.batch_seq, ref[pos]);
+        const int32_t o = (int32_t)(cs * STEP + lo);
+        const bool full = (int32_t)(cs * STEP) >= bl && (int32_t)(cs * STEP + STEP) <= el;   // wave-uniform
+        // SWAR classes of dword d: fast (major), second (dual mode) and rare.  Recomputed where
+        // needed instead of kept in registers across the chunk.
+        auto classify = [&](auto full_tag, auto dual_tag, int d, uint32_t &f80, uint32_t &g80, uint32_t &r80,
+                            bool again = false) {
+            constexpr bool FULL = decltype(full_tag)::value;
+            constexpr bool DUAL = decltype(dual_tag)::value;
+            uint32_t cw = dw<W>(cc, d), qw = dw<W>(qq, d);
+            if (again) asm volatile("" : "+v"(cw), "+v"(qw));   // a recomputation, not a value kept live
+            const uint32_t v = FULL ? 0x80808080u : valid80(o + 4 * d, bl, el);
+            swar4(cw, qw, v, mrep, P.kpass, P.kok, f80, r80);
+            g80 = 0;
+            if constexpr (DUAL) {
+                uint32_t r2;
+                swar4(cw, qw, v, mrep2, P.kpass, P.kok, g80, r2);
+                r80 &= ~g80;
+            }
+        };
+        auto body = [&](auto full_tag, auto dual_tag) {
+            constexpr bool DUAL = decltype(dual_tag)::value;
+            uint32_t rany = 0;
+            uint32_t fcnt2 = 0, fsq2 = 0;
+            double fsl2 = 0.0, fse2 = 0.0;
+#pragma unroll
+            for (int d = 0; d < W; d++) {
+                const uint32_t qw = dw<W>(qq, d);
+                uint32_t f80, g80, r80;
+                classify(full_tag, dual_tag, d, f80, g80, r80);
+                if constexpr (DUAL) {           // the second allele's entries leave the rare set
+                    fcnt2 += __popc(g80);
+                    fsq2 = __builtin_amdgcn_udot4(qw, g80 >> 7, fsq2, false);
+                    const uint32_t idx2 = qw & (g80 | (g80 - (g80 >> 7)));
+                    const double2 u0 = lut[idx2 & 0xFFu], u1 = lut[(idx2 >> 8) & 0xFFu];
+                    fsl2 += u0.x + u1.x;
+                    fse2 += u0.y + u1.y;
+                    asm volatile("" : "+v"(fsl2), "+v"(fse2) :: "memory");   // two lookups in flight: registers
+                    const double2 u2 = lut[(idx2 >> 16) & 0xFFu], u3 = lut[idx2 >> 24];
+                    fsl2 += u2.x + u3.x;
+                    fse2 += u2.y + u3.y;
+                    asm volatile("" : "+v"(fsl2), "+v"(fse2) :: "memory");
+                }
+                fcnt += __popc(f80);
+                fsq = __builtin_amdgcn_udot4(qw, f80 >> 7, fsq, false);
+                const uint32_t idx = qw & (f80 | (f80 - (f80 >> 7)));     // q where fast, 0 elsewhere
+                const double2 t0 = lut[idx & 0xFFu], t1 = lut[(idx >> 8) & 0xFFu];
+                const double2 t2 = lut[(idx >> 16) & 0xFFu], t3 = lut[idx >> 24];
+                fsl += (t0.x + t1.x) + (t2.x + t3.x);
+                fse += (t0.y + t1.y) + (t2.y + t3.y);
+                rany |= r80;
+                asm volatile("" : "+v"(fsl), "+v"(fse) :: "memory");   // keep each dword's lookups together
+            }
+            if constexpr (DUAL) {
+                // second allele: lane-private LDS accumulators (no registers held across chunks)
+                __hip_atomic_fetch_add(&D2->cnt[lane], fcnt2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&D2->sq[lane], fsq2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&D2->sl[lane], fsl2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&D2->se[lane], fse2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            if (!found || (DUAL && !found2)) {   // first fast entry of each fast allele (dict order)
+                uint32_t mine = INF32, mine2 = INF32;
+#pragma unroll
+                for (int d = W - 1; d >= 0; d--) {
+                    uint32_t f80, g80, r80;
+                    classify(full_tag, dual_tag, d, f80, g80, r80, true);
+                    if (f80) mine = (uint32_t)(o + 4 * d - bl) + ((uint32_t)__builtin_ctz(f80) >> 3);
+                    if (DUAL && g80) mine2 = (uint32_t)(o + 4 * d - bl) + ((uint32_t)__builtin_ctz(g80) >> 3);
+                }
+                if (!found) {
+                    const uint32_t w = wmin(mine);
+                    if (w != INF32) { ffirst = w; found = true; }
+                }
+                if (DUAL && !found2) {
+                    const uint32_t w = wmin(mine2);
+                    if (w != INF32) { ffirst2 = w; found2 = true; }
+                }
+            }
+            if (__ballot(rany != 0)) {         // rare entries: append to the wave's LDS queue
+                uint32_t m = 0;
+#pragma unroll
+                for (int d = 0; d < W; d++) {
+                    uint32_t f80, g80, r80;
+                    classify(full_tag, dual_tag, d, f80, g80, r80, true);
+                    const uint32_t t = r80 >> 7;
+                    m |= ((t | (t >> 7) | (t >> 14) | (t >> 21)) & 0xFu) << (4 * d);
+                }
+                while (__ballot(m != 0)) {
+                    const int j = m ? __builtin_ctz(m) : 0;
+                    const int d = j >> 2, sh = (j & 3) * 8;
+                    uint32_t cw = dw<W>(cc, 0), qw = dw<W>(qq, 0);
+#pragma unroll
+                    for (int dd = 1; dd < W; dd++)
+                        if (d == dd) { cw = dw<W>(cc, dd); qw = dw<W>(qq, dd); }
+                    const uint32_t c = (cw >> sh) & 0xFFu, q = (qw >> sh) & 0xFFu;
+                    const bool ok = m != 0 && (int)q >= P.min_bq;
+                    m &= m - 1;
+                    const uint64_t bal = __ballot(ok);
+                    const uint32_t n = (uint32_t)__popcll(bal);
+                    if (qn + n > QCAP) drain();
+                    if (ok) {
+                        const uint32_t slot = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                        Q[slot] = make_uint2((c << 8) | q, (uint32_t)(o + j - bl));
+                    }
+                    qn += n;
+                }
+            }
+        };
+        if (dual) {
+            if (full) body(std::true_type{}, std::true_type{});
+            else body(std::false_type{}, std::true_type{});
+        } else {
+            if (full) body(std::true_type{}, std::false_type{});
+            else body(std::false_type{}, std::false_type{});
         }
+        if (cs + 1 == cn) {                    // ---- column end ----
+            if (qn) drain();
+            const uint32_t fc = wsum(fcnt), fs = wsum(fsq);
+            const double fl = wsumd(fsl), fe = wsumd(fse);
+            uint32_t fc2 = 0, fs2 = 0;
+            double fl2 = 0.0, fe2 = 0.0;
+            if (dual) {
+                wave_sync();
+                fc2 = wsum(D2->cnt[lane]); fs2 = wsum(D2->sq[lane]);
+                fl2 = wsumd(D2->sl[lane]); fe2 = wsumd(D2->se[lane]);
+            }
+            wave_sync();
+            if (lane == 0) {
+                R->depth += fc + fc2;
+                if (fc) {
+                    const int Ms = slot_of(M);
+                    R->cnt[Ms] += fc; R->sq[Ms] += fs; R->sl[Ms] += fl; R->se[Ms] += fe;
+                    R->qf[Ms] = min(R->qf[Ms], (uint32_t)P.qlo);
+                    R->first[Ms] = min(R->first[Ms], ffirst);
+                }
+                if (fc2) {
+                    const int s2 = slot_of(M2);
+                    if (M2 == SPG_CODE_DEL) R->n_del += fc2;
+                    else if (M2 == SPG_CODE_SKIP) R->n_skip += fc2;
+                    else {
+                        R->cnt[s2] += fc2; R->sq[s2] += fs2; R->sl[s2] += fl2; R->se[s2] += fe2;
+                        R->qf[s2] = min(R->qf[s2], (uint32_t)P.qlo);
+                        R->first[s2] = min(R->first[s2], ffirst2);
+                    }
+                }
+            }
+            wave_sync();
+            merge_column<FRESH>(acc + P.pos_begin + g0 + cj, R, P.batch_seq, P.epoch,
+                                (uint8_t)__builtin_amdgcn_readlane(refc, cj), lane);
+            wave_sync();
+        }
+    };
+
+    for (uint32_t i = 0; i < total; i += 3) {
+        c2 = bload<W>(rc, chunk_off(i + 2)); q2 = bload<W>(rq, chunk_off(i + 2));
+        process(c0, q0, i);
+        if (i + 1 >= total) break;
+        c0 = bload<W>(rc, chunk_off(i + 3)); q0 = bload<W>(rq, chunk_off(i + 3));
+        process(c1, q1, i + 1);
+        if (i + 2 >= total) break;
+        c1 = bload<W>(rc, chunk_off(i + 4)); q1 = bload<W>(rq, chunk_off(i + 4));
+        process(c2, q2, i + 2);
     }
+}
+
+// Short columns (< t_deep raw entries): one lane per column, sequential, registers only.
+__global__ __launch_bounds__(256) void k_acc_shallow(KParams P, const uint64_t *__restrict__ off,
+                                                     const uint8_t *__restrict__ code,
+                                                     const uint8_t *__restrict__ qual,
+                                                     const uint8_t *__restrict__ ref, const Tables *__restrict__ T,
+                                                     Acc *__restrict__ acc) {
+    write_hist(P);
+    const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (col >= P.n_cols) return;
+    const uint64_t ob = off[col], oe = off[col + 1];
+    const uint64_t len = oe - ob;
+    if (len == 0 || len >= P.t_deep) return;
+    ColState st;
+    cs_init(st);
+    for (uint64_t i = ob; i < oe; i++) {
+        const uint32_t c = code[i], q = qual[i];
+        if ((int)q >= P.min_bq) entry_update(st, c, q, (uint32_t)(i - ob), T);
+    }
+    const int64_t pos = P.pos_begin + col;
+    merge_acc(acc + pos, st, P.batch_seq, P.epoch, ref[pos]);
 }
 
 // ------------------------------------------------------------------------------------------
 // finalize: GL with the reference's underflow decisions
 // ------------------------------------------------------------------------------------------
-constexpr double DMIN = 0x1p-1022;            // smallest normal
 constexpr double LOG2_10_OVER_10 = 0.33219280948873623;   // log2(10)/10
 constexpr double INV_LN2 = 1.4426950408889634;
-constexpr double MARGIN = 1e-5;               // log2 margin around the band edges (>> rounding)
+constexpr double MARGIN = 1e-5;               // log2 margin around the band edges (>> rounding error)
 
-// A value of the reference's fp64 computation, known either exactly as 0, or accurately (state 0:
-// value within ~1e-12 relative, normal, l2 = log2 of it), or only by an upper bound (state 2,
-// "band": l2 bounds log2 of the reference's value, which depends on the order of roundings in
-// the subnormal range).  lv_mul follows one reference multiplication fl(a*b).
+// A value of the reference's fp64 computation, known either exactly as 0 (state 1), or accurately
+// (state 0: normal, within ~1e-12 relative, l2 = its log2), or only by an upper bound (state 2,
+// "band": l2 bounds log2 of the reference's value, which depends on the order of roundings in the
+// subnormal range).  lv_mul follows one reference multiplication fl(a*b).
 struct LV { int s; double v, l2; };
 __device__ __forceinline__ LV lv_normal(double v, double l2) { return LV{0, v, l2}; }
 __device__ __forceinline__ LV lv_zero() { return LV{1, 0.0, -1e300}; }
@@ -370,80 +670,132 @@ __device__ __forceinline__ int to_phred(double p) {      // utils.py:12-13
     return r < 99.0 ? (int)r : 99;
 }
 
-// Emit the candidates of one position given final GL values in dict order (:145-185).
-__device__ void emit_candidates(const FParams &F, const Out &O, int64_t pos, const Acc &a, int n,
-                                const uint32_t *codes, const uint32_t *cnts, const double *G, const double *qual,
-                                uint8_t &flags) {
-    double S = 0.0;
-    for (int k = 0; k < n; k++) S = S + G[k];              // :145
-    if (S == 0) S = 1.0;                                   // :146
-    const uint8_t refc = (uint8_t)(a.misc & 0xFFu);
-    for (int k = 0; k < n; k++) {
-        const uint8_t allele = nibble_char(codes[k]);
-        const uint32_t ad = cnts[k];
-        if (refc != allele && (int64_t)ad >= F.min_ad && (double)ad / (double)a.depth >= F.ratio) {
-            spg_candidate c;
-            c.pos = pos; c.dp = (int32_t)a.depth; c.ad = (int32_t)ad;
-            c.ref = refc; c.alt = allele; c.rank = (uint8_t)k; c.first_batch = a.first_batch;
-            c.gl_linear = G[k];
-            if (G[k] != 0) { c.gl = log10(G[k]); c.pl = (int32_t)rint(-10.0 * c.gl); c.gl_zero = 0; }
-            else { c.gl = 0.0; c.pl = 0; c.gl_zero = 1; }
-            c.score = to_phred(1.0 - (G[k] / S));
-            c.qual = qual[k];
-            const uint32_t at = atomicAdd(&O.ctr->n_cand, 1u);
-            if (at < (uint32_t)F.cand_cap) O.cand[at] = c;
-            flags |= SPG_F_CANDIDATE;
+__device__ __forceinline__ void write_candidate(const FParams &F, const Out &O, int64_t pos, const Acc &a, int k,
+                                                uint32_t code, uint32_t ad, double g, double S, double qual) {
+    spg_candidate c;
+    c.pos = pos; c.dp = (int32_t)a.depth; c.ad = (int32_t)ad;
+    c.ref = (uint8_t)(a.misc & 0xFFu); c.alt = nibble_char(code); c.rank = (uint8_t)k;
+    c.first_batch = a.first_batch;
+    c.gl_linear = g;
+    if (g != 0) { c.gl = log10(g); c.pl = (int32_t)rint(-10.0 * c.gl); c.gl_zero = 0; }
+    else { c.gl = 0.0; c.pl = 0; c.gl_zero = 1; }
+    c.score = to_phred(1.0 - (g / S));
+    c.qual = qual;
+    const uint32_t at = atomicAdd(&O.ctr[F.cslot].n_cand, 1u);
+    if (at < (uint32_t)F.cand_cap) O.cand[at] = c;
+}
+
+__device__ __forceinline__ bool is_candidate(const FParams &F, const Acc &a, uint32_t code, uint32_t ad) {
+    return (uint8_t)(a.misc & 0xFFu) != nibble_char(code) && (int64_t)ad >= F.min_ad &&
+           (double)ad / (double)a.depth >= F.ratio;                            // :151-157
+}
+
+// Exact sequential recomputation of one position over the batch history (rare: subnormal band,
+// IUPAC alleles).  np.prod left folds in BAM order, dict-order chains, exactly as utils.py:16-24.
+__device__ __noinline__ void replay_position(const FParams &F, const Hist *__restrict__ H, const Acc &a,
+                                             const Tables *__restrict__ T, const Out &O, int64_t pos) {
+    uint32_t cnt[16], ord[16];
+    double P[16], Hh[16], se[16];
+    int n = 0;
+    uint32_t depth = 0;
+    for (int c = 0; c < 16; c++) { cnt[c] = 0; P[c] = 1.0; Hh[c] = 1.0; se[c] = 0.0; }
+    for (int b = 0; b < F.n_hist; b++) {
+        const Hist h = H[b];
+        const int64_t col = pos - h.pos_begin;
+        if (col < 0 || col >= h.n_cols) continue;
+        const uint64_t lo = h.off[col], hi = h.off[col + 1];
+        for (uint64_t i = lo; i < hi; i++) {
+            const uint32_t q = h.qual[i], c = h.code[i];
+            if ((int)q < F.min_bq) continue;
+            depth++;
+            if (c >= 16) continue;                         // D / N: depth only
+            const double e = T->eps[q];
+            if (cnt[c] == 0) { ord[n++] = c; P[c] = e; Hh[c] = 1.0 - e; }   // np.prod: x0, then *=
+            else { P[c] = P[c] * e; Hh[c] = Hh[c] * (1.0 - e); }
+            cnt[c]++;
+            se[c] += e;
         }
+    }
+    const bool evaluated = (int64_t)depth >= (int64_t)F.min_td;
+    double G[16];
+    double S = 0.0;
+    for (int h = 0; h < n; h++) {
+        double non = 1.0;
+        for (int j = 0; j < n; j++)
+            if (j != h) non = non * P[ord[j]];
+        G[h] = Hh[ord[h]] * non;
+        S = S + G[h];
+    }
+    if (S == 0) S = 1.0;
+    uint8_t flags = O.flags[pos];
+    if (evaluated) {
+        double *gl = O.gl + pos * NSLOT;
+        for (int h = 0; h < n; h++) {
+            const int s = slot_of(ord[h]);
+            if (s >= 0) gl[s] = G[h];
+            if (is_candidate(F, a, ord[h], cnt[ord[h]])) {
+                write_candidate(F, O, pos, a, h, ord[h], cnt[ord[h]], G[h], S, se[ord[h]] / (double)cnt[ord[h]]);
+                flags |= SPG_F_CANDIDATE;
+            }
+        }
+    }
+    O.flags[pos] = flags;
+    if (depth != a.depth) atomicOr(&O.ctr[F.cslot].err, 1u);   // history / accumulator mismatch
+    const uint32_t at = atomicAdd(&O.ctr[F.cslot].n_detail, 1u);
+    if (at < (uint32_t)F.detail_cap) {
+        spg_detail d;
+        d.pos = pos; d.depth = depth; d.n_alleles = (uint8_t)n;
+        d.pad[0] = d.pad[1] = d.pad[2] = 0;
+        for (int k = 0; k < 16; k++) {
+            d.code[k] = k < n ? (uint8_t)ord[k] : 0xFF;
+            d.count[k] = k < n ? cnt[ord[k]] : 0;
+            d.gl[k] = (k < n && evaluated) ? G[k] : __builtin_nan("");
+        }
+        O.detail[at] = d;
     }
 }
 
 __global__ __launch_bounds__(256) void k_finalize(FParams F, const Acc *__restrict__ acc,
-                                                  const Tables *__restrict__ T, Out O) {
+                                                  const Tables *__restrict__ T, const Hist *__restrict__ H, Out O) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) O.ctr[F.cslot ^ 1u] = Counters{0, 0, 0, 0};   // next call's slot
     const int64_t pos = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (pos >= F.n_pos) return;
     const Acc a = acc[pos];
+    const bool live = a.epoch == F.epoch && a.first_batch != 0;
     const double NaN = __builtin_nan("");
-    uint8_t flags = 0;
-    O.depth[pos] = a.depth;
-    O.order[pos] = a.order;
-    O.first[pos] = a.first_batch;
+    O.depth[pos] = live ? a.depth : 0u;
+    O.order[pos] = live ? a.order : 0u;
+    O.first[pos] = live ? a.first_batch : 0u;
     uint32_t *cnt8 = O.counts + pos * SPG_NCOUNT;
-#pragma unroll
-    for (int k = 0; k < NSLOT; k++) cnt8[k] = a.cnt[k];
-    cnt8[5] = a.n_del; cnt8[6] = a.n_skip; cnt8[7] = a.n_other;
     double *gl = O.gl + pos * NSLOT;
 #pragma unroll
-    for (int k = 0; k < NSLOT; k++) gl[k] = NaN;
-    if (a.first_batch == 0) { O.flags[pos] = 0; return; }
-    flags |= SPG_F_PRESENT;
+    for (int k = 0; k < NSLOT; k++) { cnt8[k] = live ? a.cnt[k] : 0u; gl[k] = NaN; }
+    cnt8[5] = live ? a.n_del : 0u; cnt8[6] = live ? a.n_skip : 0u; cnt8[7] = live ? a.n_other : 0u;
+    if (!live) { O.flags[pos] = 0; return; }
+    uint8_t flags = SPG_F_PRESENT;
     const bool evaluated = (int64_t)a.depth >= (int64_t)F.min_td;   // :131
     if (evaluated) flags |= SPG_F_EVALUATED;
-    if (a.misc & MISC_EXOTIC) {      // IUPAC / '=' alleles: exact replay tabulates every allele
-        const uint32_t at = atomicAdd(&O.ctr->n_band, 1u);
-        if (at < (uint32_t)F.band_cap) O.band[at] = pos;
+    if (a.misc & MISC_EXOTIC) {       // IUPAC / '=' alleles: the exact replay tabulates every allele
         O.flags[pos] = flags | SPG_F_EXOTIC | SPG_F_REPLAYED;
+        replay_position(F, H, a, T, O, pos);
         return;
     }
     if (!evaluated) { O.flags[pos] = flags; return; }
 
     const int n = (int)(a.order & 7u);
-    uint32_t sl_[NSLOT], codes[NSLOT], cnts[NSLOT];
-    for (int k = 0; k < n; k++) {
-        sl_[k] = (a.order >> (3 + 3 * k)) & 7u;
-        codes[k] = slot_code((int)sl_[k]);
-    }
-    bool band = false;
-    // per-allele P (= prod eps, utils.py:19) and H (= prod 1-eps, utils.py:17) in dict order
+    uint32_t slot[NSLOT], cnts[NSLOT];
     LV Pv[NSLOT], Hv[NSLOT];
     double Qv[NSLOT];
-    for (int k = 0; k < n && !band; k++) {
-        const int s = (int)sl_[k];
+    // per-allele P (= prod eps, utils.py:19) and H (= prod 1-eps, utils.py:17) in dict order
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) {
+        slot[k] = (a.order >> (3 + 3 * k)) & 7u;
         uint32_t c_ = 0, sq = 0, qf = 0; double sl = 0.0, se = 0.0;
 #pragma unroll
         for (int j = 0; j < NSLOT; j++)
-            if (s == j) { c_ = a.cnt[j]; sq = a.sq[j]; qf = a.qf[j]; sl = a.sl[j]; se = a.se[j]; }
+            if (slot[k] == (uint32_t)j) { c_ = a.cnt[j]; sq = a.sq[j]; qf = a.qf[j]; sl = a.sl[j]; se = a.se[j]; }
         cnts[k] = c_;
-        Qv[k] = se / (double)c_;
+        Qv[k] = k < n ? se / (double)c_ : 0.0;
         // P: log10 P = -sum(q)/10 up to (n+2) ulp; exact zero proven when every factor < 1/2
         if (sq <= 3076u) Pv[k] = lv_normal(T->p10k[sq / 10u] * T->eps[sq % 10u], -(double)sq * LOG2_10_OVER_10);
         else if (sq >= 3245u && qf >= 4u) Pv[k] = lv_zero();
@@ -456,98 +808,43 @@ __global__ __launch_bounds__(256) void k_finalize(FParams F, const Acc *__restri
         }
     }
     double G[NSLOT];
-    for (int h = 0; h < n && !band; h++) {
-        // N = ((1.0 * P_a1) * P_a2) ... over a != h in dict order (utils.py:18-22), then GL = H * N
+    bool band = false;
+#pragma unroll
+    for (int h = 0; h < NSLOT; h++) {
+        // N = ((1.0 * P_a1) * P_a2) ... over a != h in dict order (utils.py:18-22), GL = H * N
         LV c = lv_normal(1.0, 0.0);
-        for (int j = 0; j < n; j++)
-            if (j != h) c = lv_mul(c, Pv[j]);
-        const LV g = lv_mul(Hv[h], c);
-        if (g.s == 2) { band = true; break; }
-        G[h] = g.s == 1 ? 0.0 : g.v;
-    }
-    if (band) {
-        const uint32_t at = atomicAdd(&O.ctr->n_band, 1u);
-        if (at < (uint32_t)F.band_cap) O.band[at] = pos;
-        O.flags[pos] = flags | SPG_F_REPLAYED;
-        return;
-    }
-    for (int k = 0; k < n; k++) {
-        const int s = (int)sl_[k];
 #pragma unroll
         for (int j = 0; j < NSLOT; j++)
-            if (s == j) gl[j] = G[k];
+            if (j != h && j < n) c = lv_mul(c, Pv[j]);
+        const LV g = lv_mul(Hv[h], c);
+        if (h < n && g.s == 2) band = true;
+        G[h] = g.s == 0 ? g.v : 0.0;
     }
-    emit_candidates(F, O, pos, a, n, codes, cnts, G, Qv, flags);
+    if (band) {
+        O.flags[pos] = flags | SPG_F_REPLAYED;
+        atomicAdd(&O.ctr[F.cslot].n_band, 1u);
+        replay_position(F, H, a, T, O, pos);
+        return;
+    }
+    double S = 0.0;
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++)
+        if (k < n) S = S + G[k];                             // :145
+    if (S == 0) S = 1.0;                                     // :146
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) {
+        if (k < n) {
+#pragma unroll
+            for (int j = 0; j < NSLOT; j++)
+                if (slot[k] == (uint32_t)j) gl[j] = G[k];
+            const uint32_t code = slot_code((int)slot[k]);
+            if (is_candidate(F, a, code, cnts[k])) {
+                write_candidate(F, O, pos, a, k, code, cnts[k], G[k], S, Qv[k]);
+                flags |= SPG_F_CANDIDATE;
+            }
+        }
+    }
     O.flags[pos] = flags;
-}
-
-// ------------------------------------------------------------------------------------------
-// replay: exact sequential recomputation over the batch history
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void k_replay(FParams F, const Hist *__restrict__ H, const Acc *__restrict__ acc,
-                                               const Tables *__restrict__ T, Out O) {
-    const uint32_t nb = min(O.ctr->n_band, (uint32_t)F.band_cap);
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nb; t += gridDim.x * blockDim.x) {
-        const int64_t pos = O.band[t];
-        const Acc a = acc[pos];
-        uint32_t cnt[16], ord[16];
-        double P[16], Hh[16], se[16];
-        int n = 0;
-        uint32_t depth = 0;
-        for (int c = 0; c < 16; c++) { cnt[c] = 0; P[c] = 1.0; Hh[c] = 1.0; se[c] = 0.0; }
-        for (int b = 0; b < F.n_hist; b++) {
-            const Hist h = H[b];
-            const int64_t col = pos - h.pos_begin;
-            if (col < 0 || col >= h.n_cols) continue;
-            const uint64_t lo = h.off[col], hi = h.off[col + 1];
-            for (uint64_t i = lo; i < hi; i++) {
-                const uint32_t q = h.qual[i], c = h.code[i];
-                if ((int)q < F.min_bq) continue;
-                depth++;
-                if (c >= 16) continue;                         // D / N: depth only
-                const double e = T->eps[q];
-                if (cnt[c] == 0) { ord[n++] = c; P[c] = e; Hh[c] = 1.0 - e; }   // np.prod: x0, then *=
-                else { P[c] = P[c] * e; Hh[c] = Hh[c] * (1.0 - e); }
-                cnt[c]++;
-                se[c] += e;
-            }
-        }
-        double G[16], Q[16];
-        uint32_t codes[16], cnts[16];
-        const bool evaluated = (int64_t)depth >= (int64_t)F.min_td;
-        for (int h = 0; h < n; h++) {
-            double non = 1.0;
-            for (int j = 0; j < n; j++)
-                if (j != h) non = non * P[ord[j]];
-            G[h] = evaluated ? Hh[ord[h]] * non : __builtin_nan("");
-            codes[h] = ord[h];
-            cnts[h] = cnt[ord[h]];
-            Q[h] = se[ord[h]] / (double)cnt[ord[h]];
-        }
-        if (evaluated) {
-            double *gl = O.gl + pos * NSLOT;
-            for (int h = 0; h < n; h++) {
-                const int s = slot_of(codes[h]);
-                if (s >= 0) gl[s] = G[h];
-            }
-            uint8_t flags = O.flags[pos];
-            emit_candidates(F, O, pos, a, n, codes, cnts, G, Q, flags);
-            O.flags[pos] = flags;
-        }
-        if (depth != a.depth) atomicOr(&O.ctr->err, 1u);       // history / accumulator mismatch
-        const uint32_t at = atomicAdd(&O.ctr->n_detail, 1u);
-        if (at < (uint32_t)F.detail_cap) {
-            spg_detail d;
-            d.pos = pos; d.depth = depth; d.n_alleles = (uint8_t)n;
-            d.pad[0] = d.pad[1] = d.pad[2] = 0;
-            for (int k = 0; k < 16; k++) {
-                d.code[k] = k < n ? (uint8_t)codes[k] : 0xFF;
-                d.count[k] = k < n ? cnts[k] : 0;
-                d.gl[k] = k < n ? G[k] : __builtin_nan("");
-            }
-            O.detail[at] = d;
-        }
-    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -555,25 +852,26 @@ __global__ __launch_bounds__(64) void k_replay(FParams F, const Hist *__restrict
 // ------------------------------------------------------------------------------------------
 hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_t *code, const uint8_t *qual,
                              const uint8_t *ref, const Tables *T, Acc *acc, hipStream_t st) {
+    if (P.n_cols == 0) return hipSuccess;
+    if (P.t_deep > 1) {      // mixed / shallow batches: lane-per-column pass for the short columns
+        const int64_t blocks = (P.n_cols + 255) / 256;
+        hipLaunchKernelGGL(k_acc_shallow, dim3((unsigned)blocks), dim3(256), 0, st, P, off, code, qual, ref, T, acc);
+    }
     const int64_t waves = (P.n_cols + P.G - 1) / P.G;
     const int64_t blocks = (waves + 3) / 4;
-    if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_accumulate, dim3((unsigned)blocks), dim3(256), 0, st, P, off, code, qual, ref, T, acc);
-    return hipGetLastError();
-}
-
-__global__ void k_set_hist(Hist *dst, Hist h) { *dst = h; }
-
-hipError_t launch_set_hist(Hist *dst, const Hist &h, hipStream_t st) {
-    hipLaunchKernelGGL(k_set_hist, dim3(1), dim3(1), 0, st, dst, h);
+    const bool fresh = P.batch_seq == 1;
+    const bool w4 = P.t_deep <= 1;
+#define SPG_SEG(WW, FF) hipLaunchKernelGGL((k_acc_seg<WW, FF>), dim3((unsigned)blocks), dim3(256), 0, st, P, off, code, qual, ref, T, acc)
+    if (w4) { if (fresh) SPG_SEG(4, true); else SPG_SEG(4, false); }
+    else { if (fresh) SPG_SEG(1, true); else SPG_SEG(1, false); }
+#undef SPG_SEG
     return hipGetLastError();
 }
 
 hipError_t launch_finalize(const FParams &F, const Acc *acc, const Tables *T, const Out &O, const Hist *H,
                            hipStream_t st) {
     const int64_t blocks = (F.n_pos + 255) / 256;
-    if (blocks) hipLaunchKernelGGL(k_finalize, dim3((unsigned)blocks), dim3(256), 0, st, F, acc, T, O);
-    hipLaunchKernelGGL(k_replay, dim3(64), dim3(64), 0, st, F, H, acc, T, O);
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)blocks), dim3(256), 0, st, F, acc, T, H, O);
     return hipGetLastError();
 }
 
