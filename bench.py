@@ -30,12 +30,12 @@ L_SARS = 29903
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--depth", type=float, default=10000.0)
     ap.add_argument("--max-depth", type=int, default=0, help="0 = uncapped; 8000 = pysam parity cap")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-positions", type=int, default=600)
+    ap.add_argument("--cpu-positions", type=int, default=8000)
     return ap.parse_args()
 
 
@@ -64,7 +64,7 @@ def cpu_baseline(args):
     from oracle import reference_port as rp
     from oracle.c_oracle import COracle
     ref = synth.reference(L_SARS, seed=1)
-    lo = 12000
+    lo = 8000
     n = args.cpu_positions
     _, off, c, q = synth.pileup(L_SARS, args.depth, seed=2, ref=ref, lo=lo, hi=lo + n, max_depth=args.max_depth)
     t0 = time.perf_counter()
@@ -72,11 +72,11 @@ def cpu_baseline(args):
     o.accumulate(lo, off, c, q)
     o.prepare_variants()
     t_py = time.perf_counter() - t0
-    n_c = min(L_SARS - lo, 8 * n)
-    _, off2, c2, q2 = synth.pileup(L_SARS, args.depth, seed=2, ref=ref, lo=lo, hi=lo + n_c, max_depth=args.max_depth)
+    n_c = L_SARS                              # the C restatement takes the whole genome
+    _, off2, c2, q2 = synth.pileup(L_SARS, args.depth, seed=2, ref=ref, max_depth=args.max_depth)
     t0 = time.perf_counter()
     co = COracle(ref, 30, 10, 5, 0.10)
-    co.accumulate(lo, off2, c2, q2)
+    co.accumulate(0, off2, c2, q2)
     co.finalize()
     t_c = time.perf_counter() - t0
     return {"value": n / t_py, "unit": "positions/s", "cores": 1, "kind": "port",
@@ -85,6 +85,24 @@ def cpu_baseline(args):
                       f"pysam pileup/BAM decode not included (absent)",
             "c_restatement": {"value": n_c / t_c, "unit": "positions/s", "cores": 1,
                               "sample": f"oracle/spg_oracle.c on {n_c} positions ({int(off2[-1])} entries), {t_c:.2f} s"}}
+
+
+def pmc_traffic(E):
+    """HBM bytes per launch of the accumulate kernel from the newest committed PMC summary
+    (profiles/rNN_bench_pmc.json, written by tools/summarize_prof.py from rocprofv3 --pmc passes of
+    this bench: FETCH_SIZE x2 + WRITE_SIZE), when it was measured on this workload; else None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench_pmc.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+        rec = d.get("spg::k_acc_seg<4, true>")
+        if rec is None or rec.get("entries") not in (None, E):
+            return None
+        return rec.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
 
 
 def main():
@@ -128,17 +146,14 @@ def main():
     for _ in range(args.warmup):
         step()
     eng.sync()
+    eng.kernel_times()                   # drop the warm-up steps' timings
     torch.cuda.synchronize()
-    acc_ms, fin_ms = [], []
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        a, f = eng.last_kernel_ms()      # syncs the engine stream (events)
-        acc_ms.append(a)
-        fin_ms.append(f)
     eng.sync()
     torch.cuda.synchronize()
     if dist is not None:
@@ -148,12 +163,13 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=d_c.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    acc_ms, fin_ms = eng.kernel_times(max(64, args.steps))   # HIP events of the timed steps (last <= 64)
     n_cand = eng.counts()[0]
     positions_per_step = world * L_SARS
     value = positions_per_step * args.steps / dt
     t_acc = float(np.mean(acc_ms)) * 1e-3
     t_fin = float(np.mean(fin_ms)) * 1e-3
-    algo_bytes = 2 * E + 8 * (C + 1)          # base_code + qual + u64 offsets read by k_accumulate
+    algo_bytes = 2 * E + 8 * (C + 1)          # base_code + qual + u64 offsets read by the accumulate kernel
     achieved = algo_bytes / t_acc
     res = {
         "metric": "pileup positions/s at 10,000x depth (SARS-CoV-2, synthetic)",
@@ -166,8 +182,8 @@ def main():
                    "positions_per_step": positions_per_step, "entries_per_gpu_step": E, "columns_per_gpu": C,
                    "parallelism": f"coord-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM, "traffic": None,
-                     "kernel": "k_accumulate", "kernel_ms": t_acc * 1e3, "algorithmic_bytes": algo_bytes},
+                     "frac": achieved / PEAK_HBM, "traffic": pmc_traffic(E),
+                     "kernel": "k_acc_seg<4,true> (spg_accumulate)", "kernel_ms": t_acc * 1e3, "algorithmic_bytes": algo_bytes},
         "finalize_ms": t_fin * 1e3, "candidates_per_gpu_step": n_cand, "datagen_s": t_gen,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

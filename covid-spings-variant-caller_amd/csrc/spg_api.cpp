@@ -69,8 +69,13 @@ struct spg_ctx {
     int64_t detail_cap = 0;
     Counters *ctr = nullptr;
     bool finalized = false;
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-    bool ev_acc = false, ev_fin = false;
+    // timing ring: one entry per finalize; events around the accumulate launches (first begin ..
+    // last end) and around the finalize launch.  Read back without stalling the pipeline.
+    static constexpr int NRING = 64;
+    hipEvent_t ev[NRING][4] = {};
+    int64_t ring_w = 0, ring_r = 0;     // entries [ring_r, ring_w) are complete
+    bool acc_open = false, acc_any = false;
+    bool last_acc = false, last_fin = false;
 };
 
 extern "C" {
@@ -123,8 +128,9 @@ int spg_create(int device, int64_t n_pos, const spg_params *p, spg_ctx **out) {
     if (hipMalloc(&c->tables, sizeof(Tables)) != hipSuccess) return bail(fail("spg_create: tables alloc"));
     if (hipMemsetAsync(c->acc, 0, sizeof(Acc) * n_pos, c->stream) != hipSuccess) return bail(fail("memset"));
     if ((rc = alloc_outputs(c)) != 0) return bail(rc);
-    for (auto &e : c->ev)
-        if (hipEventCreate(&e) != hipSuccess) return bail(fail("spg_create: event"));
+    for (auto &row : c->ev)
+        for (auto &e : row)
+            if (hipEventCreate(&e) != hipSuccess) return bail(fail("spg_create: event"));
     *out = c;
     return 0;
 }
@@ -148,8 +154,9 @@ int spg_destroy(spg_ctx *c) {
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
-    for (auto &e : c->ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto &row : c->ev)
+        for (auto &e : row)
+            if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -294,7 +301,7 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
     const double avg = (double)n_entries / (double)n_cols;
     static const int64_t target_waves = [] {
         const char *e = getenv("SPG_TARGET_WAVES");
-        return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)4096;
+        return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)16384;
     }();
     const bool deep_batch = avg >= 2048.0;
     const uint32_t G = (uint32_t)std::min<int64_t>(64, std::max<int64_t>(1, (n_cols + target_waves - 1) / target_waves));
@@ -312,10 +319,12 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
     P.hslot = c->d_hist + (c->hist.size() - 1);
     P.G = G;
     P.t_deep = deep_batch ? 1u : 128u;
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    hipEvent_t *ev = c->ev[c->ring_w % spg_ctx::NRING];
+    if (!c->acc_open) HIPCHK(hipEventRecord(ev[0], c->stream));
     HIPCHK(launch_accumulate(P, hb.off, hb.code, hb.qual, c->ref, c->tables, c->acc, c->stream));
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    c->ev_acc = true;
+    HIPCHK(hipEventRecord(ev[1], c->stream));
+    c->acc_open = true;
+    c->acc_any = true;
     c->finalized = false;
     return 0;
 }
@@ -354,10 +363,19 @@ int spg_finalize(spg_ctx *c) {
     if (!c->lut_set) return fail("spg_finalize: spg_set_eps_lut not called");
     HIPCHK(hipSetDevice(c->device));
     c->cslot ^= 1u;            // this call counts in slot cslot (zeroed by the previous call / creation)
-    HIPCHK(hipEventRecord(c->ev[2], c->stream));
+    hipEvent_t *ev = c->ev[c->ring_w % spg_ctx::NRING];
+    if (!c->acc_open) {        // no accumulate since the last finalize: empty accumulate interval
+        HIPCHK(hipEventRecord(ev[0], c->stream));
+        HIPCHK(hipEventRecord(ev[1], c->stream));
+    }
+    HIPCHK(hipEventRecord(ev[2], c->stream));
     HIPCHK(launch_finalize(make_fparams(c), c->acc, c->tables, make_out(c), c->d_hist, c->stream));
-    HIPCHK(hipEventRecord(c->ev[3], c->stream));
-    c->ev_fin = true;
+    HIPCHK(hipEventRecord(ev[3], c->stream));
+    c->last_acc = c->acc_open;
+    c->last_fin = true;
+    c->acc_open = false;
+    c->ring_w++;
+    if (c->ring_w - c->ring_r > spg_ctx::NRING) c->ring_r = c->ring_w - spg_ctx::NRING;
     c->finalized = true;
     return 0;
 }
@@ -475,14 +493,32 @@ int spg_last_kernel_ms(spg_ctx *c, float *acc_ms, float *fin_ms) {
     if (!c) return fail("spg_last_kernel_ms: null ctx");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (acc_ms) {
-        *acc_ms = 0.f;
-        if (c->ev_acc) HIPCHK(hipEventElapsedTime(acc_ms, c->ev[0], c->ev[1]));
+    if (acc_ms) *acc_ms = 0.f;
+    if (fin_ms) *fin_ms = 0.f;
+    if (c->acc_open) {         // accumulates since the last finalize
+        if (acc_ms) HIPCHK(hipEventElapsedTime(acc_ms, c->ev[c->ring_w % spg_ctx::NRING][0],
+                                               c->ev[c->ring_w % spg_ctx::NRING][1]));
+        return 0;
     }
-    if (fin_ms) {
-        *fin_ms = 0.f;
-        if (c->ev_fin) HIPCHK(hipEventElapsedTime(fin_ms, c->ev[2], c->ev[3]));
+    if (c->ring_w == 0) return 0;
+    hipEvent_t *ev = c->ev[(c->ring_w - 1) % spg_ctx::NRING];
+    if (acc_ms && c->last_acc) HIPCHK(hipEventElapsedTime(acc_ms, ev[0], ev[1]));
+    if (fin_ms && c->last_fin) HIPCHK(hipEventElapsedTime(fin_ms, ev[2], ev[3]));
+    return 0;
+}
+
+int spg_kernel_times(spg_ctx *c, float *acc_ms, float *fin_ms, int64_t cap, int64_t *n_out) {
+    if (!c || !n_out) return fail("spg_kernel_times: null argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    int64_t n = 0;
+    for (int64_t i = c->ring_r; i < c->ring_w && n < cap; i++, n++) {
+        hipEvent_t *ev = c->ev[i % spg_ctx::NRING];
+        if (acc_ms) HIPCHK(hipEventElapsedTime(acc_ms + n, ev[0], ev[1]));
+        if (fin_ms) HIPCHK(hipEventElapsedTime(fin_ms + n, ev[2], ev[3]));
     }
+    c->ring_r += n;
+    *n_out = n;
     return 0;
 }
 

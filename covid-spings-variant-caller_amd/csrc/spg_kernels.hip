@@ -15,6 +15,7 @@
 #include <type_traits>
 
 #include "spg_device.h"
+#include <stdlib.h>
 
 namespace spg {
 
@@ -870,8 +871,9 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
 
 hipError_t launch_finalize(const FParams &F, const Acc *acc, const Tables *T, const Out &O, const Hist *H,
                            hipStream_t st) {
-    const int64_t blocks = (F.n_pos + 255) / 256;
-    hipLaunchKernelGGL(k_finalize, dim3((unsigned)blocks), dim3(256), 0, st, F, acc, T, H, O);
+    static const int bs = [] { const char *e = getenv("SPG_FIN_BLOCK"); return e ? atoi(e) : 64; }();
+    const int64_t blocks = (F.n_pos + bs - 1) / bs;
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)blocks), dim3(bs), 0, st, F, acc, T, H, O);
     return hipGetLastError();
 }
 

@@ -125,6 +125,15 @@ class PileupEngine:
             N.check(self._L.spg_last_kernel_ms(self._h, C.byref(a), C.byref(f)), "spg_last_kernel_ms")
         return a.value, f.value
 
+    def kernel_times(self, cap: int = 64):
+        """(accumulate_ms, finalize_ms) arrays of every step finalized since the previous call."""
+        a = np.zeros(cap, np.float32)
+        f = np.zeros(cap, np.float32)
+        n = C.c_int64()
+        with self._lock:
+            N.check(self._L.spg_kernel_times(self._h, N.ptr(a), N.ptr(f), int(cap), C.byref(n)), "spg_kernel_times")
+        return a[:n.value].astype(np.float64), f[:n.value].astype(np.float64)
+
     # -- results ------------------------------------------------------------------------------
     def table(self, pos0: int = 0, n: Optional[int] = None) -> Dict[str, np.ndarray]:
         n = self.n_pos - pos0 if n is None else n

@@ -153,8 +153,12 @@ int spg_device_results(spg_ctx *ctx, void **candidates, void **n_candidates);
  * another stream (e.g. an RCCL gather) may read dst afterwards. */
 int spg_copy_candidates_device(spg_ctx *ctx, void *dst, int64_t cap);
 
-/* Timing hooks (bench): HIP events around the last accumulate / finalize kernels, ms. */
+/* Timing hooks (bench): HIP events around the accumulate launches of one finalize step (first
+ * begin .. last end) and around the finalize launch, ms.  spg_last_kernel_ms: the latest step.
+ * spg_kernel_times: every step completed since the previous spg_kernel_times call (at most 64
+ * are kept), oldest first, without timing-induced stalls between steps.  Both synchronise. */
 int spg_last_kernel_ms(spg_ctx *ctx, float *accumulate_ms, float *finalize_ms);
+int spg_kernel_times(spg_ctx *ctx, float *accumulate_ms, float *finalize_ms, int64_t cap, int64_t *n_out);
 
 /* Introspection for tests. */
 int spg_device_count(int *n);
