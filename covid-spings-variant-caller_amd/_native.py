@@ -109,3 +109,46 @@ def ptr(a) -> C.c_void_p:
     if isinstance(a, np.ndarray):
         return a.ctypes.data_as(C.c_void_p)
     return C.c_void_p(int(a.data_ptr()))
+
+
+# ------------------------------------------------------------------------------------------------
+# libspings_pileup.so (include/spings_pileup.h): host BAM/SAM reader + pileup emulator
+# ------------------------------------------------------------------------------------------------
+SPP_STEPPER = {"all": 0, "nofilter": 1, "samtools": 2}
+
+
+class SppParams(C.Structure):
+    _fields_ = [("stepper", C.c_int32), ("min_mapping_quality", C.c_int32), ("max_depth", C.c_int32),
+                ("ignore_overlaps", C.c_int32), ("flag_filter", C.c_uint32), ("n_threads", C.c_int32),
+                ("reserved", C.c_int64 * 2)]
+
+
+def pileup_lib():
+    """Load libspings_pileup.so (host-only; raises if it has not been built)."""
+    global _pileup
+    if _pileup is not None:
+        return _pileup
+    if not os.path.exists(PILEUP_LIB):
+        raise NativeError(f"{PILEUP_LIB} not found: build it with __graft_entry__.build()")
+    L = C.CDLL(PILEUP_LIB)
+    vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int32
+    _sig(L.spp_last_error, C.c_char_p)
+    _sig(L.spp_default_params, None, C.POINTER(SppParams))
+    _sig(L.spp_open, C.c_int, C.c_char_p, C.POINTER(vp))
+    _sig(L.spp_close, C.c_int, vp)
+    _sig(L.spp_n_targets, C.c_int, vp, C.POINTER(i32))
+    _sig(L.spp_target, C.c_int, vp, i32, C.POINTER(C.c_char_p), C.POINTER(i64))
+    _sig(L.spp_target_id, C.c_int, vp, C.c_char_p, C.POINTER(i32))
+    _sig(L.spp_pileup, C.c_int, vp, i32, C.POINTER(SppParams), C.POINTER(vp))
+    _sig(L.spp_batch_info, C.c_int, vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(C.c_uint64),
+         C.POINTER(i64), C.POINTER(i64))
+    _sig(L.spp_batch_arrays, C.c_int, vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp))
+    _sig(L.spp_batch_free, C.c_int, vp)
+    _pileup = L
+    return L
+
+
+def pcheck(rc: int, what: str = ""):
+    if rc != 0:
+        msg = pileup_lib().spp_last_error().decode(errors="replace")
+        raise NativeError(f"{what}: {msg}" if what else msg)

@@ -1,0 +1,738 @@
+// spp_pileup.cpp — host BAM/SAM reader + htslib-faithful pileup emulator (include/spings_pileup.h).
+//
+// Replaces pysam.AlignmentFile.pileup() as driven by LiveVariantCaller.process_bam
+// (variant_caller/live_variant_caller.py:54-72).  Two stages:
+//   1. read: stream the file (BGZF blocks inflated in parallel, or SAM text), keep the reads of
+//      one contig (position, reference end, flags, mate fields, CIGAR, base nibbles, qualities);
+//   2. pileup: replay htslib's bam_plp_push / bam_plp_next bookkeeping exactly where it decides
+//      anything (the maxcnt drop rule depends on when buffered reads are freed), apply the mate
+//      overlap tweak, then write the CSR columns — every kept read contributes one entry to each
+//      column of [pos, end) in read order, which is htslib's per-column order.
+// Semantics restated from the published htslib sam.c / pysam libcalignmentfile.pyx (absent here:
+// parity unpinned; oracle/pileup_port.py is the independent restatement the tests compare with).
+#include "spings_pileup.h"
+
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <queue>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+int fail(const std::string &m) {
+    g_err = m;
+    return -1;
+}
+
+enum : uint32_t {   // SAM flags
+    F_PAIRED = 0x1, F_PROPER = 0x2, F_UNMAP = 0x4, F_MUNMAP = 0x8, F_SECONDARY = 0x100,
+    F_QCFAIL = 0x200, F_DUP = 0x400,
+};
+enum : uint32_t { C_M = 0, C_I = 1, C_D = 2, C_N = 3, C_S = 4, C_H = 5, C_P = 6, C_EQ = 7, C_X = 8 };
+
+inline bool consumes_ref(uint32_t op) { return op == C_M || op == C_D || op == C_N || op == C_EQ || op == C_X; }
+inline bool consumes_query(uint32_t op) { return op == C_M || op == C_I || op == C_S || op == C_EQ || op == C_X; }
+
+// htslib seq_nt16_table: text base -> 4-bit code
+struct Nt16 {
+    uint8_t t[256];
+    Nt16() {
+        std::fill(t, t + 256, 15);
+        const char *s = "=ACMGRSVTWYHKDBN";
+        for (int i = 0; i < 16; i++) {
+            t[(uint8_t)s[i]] = (uint8_t)i;
+            t[(uint8_t)tolower(s[i])] = (uint8_t)i;
+        }
+        t[(uint8_t)'U'] = t[(uint8_t)'u'] = 8;
+    }
+} const NT16;
+
+struct Reads {                 // one contig's reads, structure of arrays
+    std::vector<int64_t> pos, end, mpos, isize;
+    std::vector<int32_t> mtid;
+    std::vector<uint16_t> flag;
+    std::vector<uint8_t> mapq;
+    std::vector<uint64_t> cig_off, seq_off, name_off;
+    std::vector<uint32_t> n_cig, l_seq;
+    std::vector<uint32_t> cigar;
+    std::vector<uint8_t> seq, qual;   // one nibble code / quality per query base
+    std::vector<char> names;
+    size_t size() const { return pos.size(); }
+};
+
+struct Target {
+    std::string name;
+    int64_t len;
+};
+
+}  // namespace
+
+struct spp_file {
+    std::string path;
+    bool bam = false;
+    std::vector<Target> targets;
+    std::unordered_map<std::string, int32_t> tid_of;
+};
+
+struct spp_batch {
+    int64_t pos_begin = 0, n_cols = 0;
+    uint64_t n_entries = 0;
+    int64_t n_used = 0, n_dropped = 0;
+    std::vector<uint64_t> off;
+    uint8_t *code = nullptr, *qual = nullptr;
+    ~spp_batch() {
+        free(code);
+        free(qual);
+    }
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// BGZF: blocks are independent raw-deflate members; inflate a window of blocks in parallel.
+// ---------------------------------------------------------------------------------------------
+class BgzfReader {
+  public:
+    BgzfReader(const std::string &path, int threads) : threads_(std::max(1, threads)) {
+        f_ = fopen(path.c_str(), "rb");
+        if (!f_) throw std::runtime_error("cannot open " + path);
+    }
+    ~BgzfReader() {
+        if (f_) fclose(f_);
+    }
+    // Append the next window of decompressed bytes to `out`; false at EOF.
+    bool next(std::vector<uint8_t> &out) {
+        std::vector<uint8_t> comp(kWindow);
+        size_t n = carry_.size();
+        std::copy(carry_.begin(), carry_.end(), comp.begin());
+        n += fread(comp.data() + n, 1, kWindow - n, f_);
+        if (n == 0) return false;
+        struct Blk { size_t off, clen, ulen; };
+        std::vector<Blk> blks;
+        size_t p = 0;
+        while (p + 18 <= n) {
+            const uint8_t *h = comp.data() + p;
+            if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) throw std::runtime_error("not a BGZF block");
+            const size_t xlen = h[10] | (h[11] << 8);
+            size_t bsize = 0;
+            for (size_t x = 12; x + 4 <= 12 + xlen;) {
+                const size_t slen = h[x + 2] | (h[x + 3] << 8);
+                if (h[x] == 66 && h[x + 1] == 67 && slen == 2) bsize = (h[x + 4] | (h[x + 5] << 8)) + 1;
+                x += 4 + slen;
+            }
+            if (!bsize) throw std::runtime_error("BGZF block without BSIZE");
+            if (p + bsize > n) break;
+            const size_t ulen = (size_t)h[bsize - 4] | ((size_t)h[bsize - 3] << 8) | ((size_t)h[bsize - 2] << 16) |
+                                ((size_t)h[bsize - 1] << 24);
+            blks.push_back({p + 12 + xlen, bsize - xlen - 20, ulen});
+            p += bsize;
+        }
+        if (blks.empty()) {
+            if (feof(f_)) {
+                if (n) throw std::runtime_error("truncated BGZF file");
+                return false;
+            }
+            throw std::runtime_error("BGZF block larger than the read window");
+        }
+        carry_.assign(comp.begin() + p, comp.begin() + n);
+        std::vector<size_t> uoff(blks.size() + 1, 0);
+        for (size_t i = 0; i < blks.size(); i++) uoff[i + 1] = uoff[i] + blks[i].ulen;
+        const size_t base = out.size();
+        out.resize(base + uoff.back());
+        std::atomic<size_t> next_blk{0};
+        std::atomic<bool> bad{false};
+        auto work = [&]() {
+            z_stream zs;
+            memset(&zs, 0, sizeof(zs));
+            if (inflateInit2(&zs, -15) != Z_OK) { bad = true; return; }
+            for (size_t i; (i = next_blk++) < blks.size();) {
+                if (blks[i].ulen == 0) continue;
+                inflateReset(&zs);
+                zs.next_in = comp.data() + blks[i].off;
+                zs.avail_in = (uInt)blks[i].clen;
+                zs.next_out = out.data() + base + uoff[i];
+                zs.avail_out = (uInt)blks[i].ulen;
+                if (inflate(&zs, Z_FINISH) != Z_STREAM_END || zs.avail_out != 0) bad = true;
+            }
+            inflateEnd(&zs);
+        };
+        const int nt = (int)std::min<size_t>(threads_, blks.size());
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; t++) pool.emplace_back(work);
+        work();
+        for (auto &t : pool) t.join();
+        if (bad) throw std::runtime_error("BGZF inflate failed");
+        return true;
+    }
+
+  private:
+    static constexpr size_t kWindow = 16u << 20;
+    FILE *f_ = nullptr;
+    int threads_;
+    std::vector<uint8_t> carry_;
+};
+
+// Sequential byte source over the decompressed BAM stream.
+class BamStream {
+  public:
+    BamStream(const std::string &path, int threads) : z_(path, threads) {}
+    bool need(size_t n) {            // ensure n bytes available at cur_
+        while (buf_.size() - cur_ < n) {
+            if (cur_ > (64u << 20)) {
+                buf_.erase(buf_.begin(), buf_.begin() + (ptrdiff_t)cur_);
+                cur_ = 0;
+            }
+            if (!z_.next(buf_)) return false;
+        }
+        return true;
+    }
+    const uint8_t *ptr() const { return buf_.data() + cur_; }
+    void skip(size_t n) { cur_ += n; }
+
+  private:
+    BgzfReader z_;
+    std::vector<uint8_t> buf_;
+    size_t cur_ = 0;
+};
+
+inline int32_t rd32(const uint8_t *p) { int32_t v; memcpy(&v, p, 4); return v; }
+inline uint32_t rdu32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+inline uint16_t rdu16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
+
+bool is_bgzf(const std::string &path) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) throw std::runtime_error("cannot open " + path);
+    uint8_t h[4] = {0, 0, 0, 0};
+    const size_t n = fread(h, 1, 4, f);
+    fclose(f);
+    return n == 4 && h[0] == 31 && h[1] == 139;
+}
+
+void bam_header(BamStream &s, spp_file *f) {
+    if (!s.need(12) || memcmp(s.ptr(), "BAM\1", 4) != 0) throw std::runtime_error("not a BAM file");
+    const int32_t l_text = rd32(s.ptr() + 4);
+    s.skip(8);
+    if (!s.need((size_t)l_text + 4)) throw std::runtime_error("truncated BAM header");
+    s.skip((size_t)l_text);
+    const int32_t n_ref = rd32(s.ptr());
+    s.skip(4);
+    for (int32_t i = 0; i < n_ref; i++) {
+        if (!s.need(4)) throw std::runtime_error("truncated BAM header");
+        const int32_t l_name = rd32(s.ptr());
+        if (!s.need((size_t)l_name + 8)) throw std::runtime_error("truncated BAM header");
+        Target t;
+        t.name.assign((const char *)s.ptr() + 4, (size_t)std::max(0, l_name - 1));
+        t.len = rd32(s.ptr() + 4 + l_name);
+        s.skip((size_t)l_name + 8);
+        f->tid_of[t.name] = (int32_t)f->targets.size();
+        f->targets.push_back(t);
+    }
+}
+
+int64_t ref_len(const uint32_t *cig, uint32_t n) {
+    int64_t l = 0;
+    for (uint32_t i = 0; i < n; i++)
+        if (consumes_ref(cig[i] & 0xF)) l += cig[i] >> 4;
+    return l;
+}
+
+void push_read(Reads &R, int64_t pos, uint16_t flag, uint8_t mapq, int32_t mtid, int64_t mpos, int64_t isize,
+               const uint32_t *cig, uint32_t n_cig, const char *name, size_t l_name) {
+    R.pos.push_back(pos);
+    R.end.push_back(pos + ref_len(cig, n_cig));
+    R.flag.push_back(flag);
+    R.mapq.push_back(mapq);
+    R.mtid.push_back(mtid);
+    R.mpos.push_back(mpos);
+    R.isize.push_back(isize);
+    R.cig_off.push_back(R.cigar.size());
+    R.n_cig.push_back(n_cig);
+    R.cigar.insert(R.cigar.end(), cig, cig + n_cig);
+    R.name_off.push_back(R.names.size());
+    R.names.insert(R.names.end(), name, name + l_name);
+    R.names.push_back('\0');
+}
+
+// stepper read filter (pysam __advance_all / __advance_nofilter / __advance_samtools) + htslib's
+// own unmapped skip in bam_plp_push
+bool stepper_keeps(const spp_params &p, uint16_t flag, uint8_t mapq) {
+    if (flag & F_UNMAP) return false;
+    if (p.stepper == SPP_STEPPER_NOFILTER) return true;
+    if (p.stepper == SPP_STEPPER_ALL) return !(flag & (F_UNMAP | F_SECONDARY | F_QCFAIL | F_DUP));
+    if (flag & p.flag_filter) return false;
+    if (mapq < p.min_mapping_quality) return false;
+    if ((flag & F_PAIRED) && !(flag & F_PROPER)) return false;   // orphan (ignore_orphans default)
+    return true;
+}
+
+void read_bam(const spp_file *f, int32_t tid, const spp_params &p, Reads &R) {
+    BamStream s(f->path, p.n_threads);
+    spp_file tmp;
+    bam_header(s, &tmp);
+    int64_t last_pos = -1;
+    while (s.need(4)) {
+        const uint32_t bs = rdu32(s.ptr());
+        if (!s.need(4 + (size_t)bs)) throw std::runtime_error("truncated BAM record");
+        const uint8_t *b = s.ptr() + 4;
+        const int32_t rtid = rd32(b);
+        const int64_t pos = rd32(b + 4);
+        const uint8_t l_name = b[8], mapq = b[9];
+        const uint16_t n_cig = rdu16(b + 12), flag = rdu16(b + 14);
+        const int32_t l_seq = rd32(b + 16), mtid = rd32(b + 20);
+        const int64_t mpos = rd32(b + 24), isize = rd32(b + 28);
+        if (rtid == tid) {
+            if (pos < last_pos) throw std::runtime_error("BAM is not coordinate-sorted");
+            last_pos = pos;
+            if (stepper_keeps(p, flag, mapq)) {
+                const uint8_t *name = b + 32;
+                std::vector<uint32_t> cig(n_cig);
+                memcpy(cig.data(), name + l_name, 4u * n_cig);
+                push_read(R, pos, flag, mapq, mtid, mpos, isize, cig.data(), n_cig, (const char *)name,
+                          l_name ? l_name - 1u : 0u);
+                const uint8_t *sq = name + l_name + 4u * n_cig;
+                const uint8_t *ql = sq + (l_seq + 1) / 2;
+                const size_t so = R.seq.size();
+                R.seq_off.push_back(so);
+                R.l_seq.push_back((uint32_t)l_seq);
+                R.seq.resize(so + (size_t)l_seq);
+                uint8_t *dst = R.seq.data() + so;
+                for (int32_t i = 0; i < l_seq; i++) dst[i] = (sq[i >> 1] >> ((~i & 1) << 2)) & 0xF;
+                R.qual.insert(R.qual.end(), ql, ql + l_seq);
+            }
+        }
+        s.skip(4 + (size_t)bs);
+    }
+}
+
+void sam_header_line(spp_file *f, const std::string &line) {
+    if (line.compare(0, 3, "@SQ") != 0) return;
+    Target t;
+    t.len = 0;
+    size_t p = 0;
+    while ((p = line.find('\t', p)) != std::string::npos) {
+        ++p;
+        const size_t q = line.find('\t', p);
+        const std::string fld = line.substr(p, q == std::string::npos ? std::string::npos : q - p);
+        if (fld.compare(0, 3, "SN:") == 0) t.name = fld.substr(3);
+        if (fld.compare(0, 3, "LN:") == 0) t.len = atoll(fld.c_str() + 3);
+    }
+    f->tid_of[t.name] = (int32_t)f->targets.size();
+    f->targets.push_back(t);
+}
+
+template <class F>
+void for_lines(const std::string &path, F &&fn) {
+    FILE *fp = fopen(path.c_str(), "rb");
+    if (!fp) throw std::runtime_error("cannot open " + path);
+    std::string line;
+    std::vector<char> buf(1 << 20);
+    std::string carry;
+    size_t n;
+    bool stop = false;
+    while (!stop && (n = fread(buf.data(), 1, buf.size(), fp)) > 0) {
+        size_t s = 0;
+        for (size_t i = 0; i < n; i++)
+            if (buf[i] == '\n') {
+                carry.append(buf.data() + s, i - s);
+                if (!carry.empty() && carry.back() == '\r') carry.pop_back();
+                if (!fn(carry)) { stop = true; break; }
+                carry.clear();
+                s = i + 1;
+            }
+        if (!stop) carry.append(buf.data() + s, n - s);
+    }
+    if (!stop && !carry.empty()) fn(carry);
+    fclose(fp);
+}
+
+void read_sam(const spp_file *f, int32_t tid, const spp_params &p, Reads &R) {
+    const std::string &want = f->targets[(size_t)tid].name;
+    int64_t last_pos = -1;
+    std::vector<uint32_t> cig;
+    for_lines(f->path, [&](const std::string &line) {
+        if (line.empty() || line[0] == '@') return true;
+        const char *fld[11];
+        size_t len[11];
+        size_t s = 0;
+        for (int k = 0; k < 11; k++) {
+            const size_t e = line.find('\t', s);
+            if (e == std::string::npos && k < 10) throw std::runtime_error("SAM record with < 11 fields");
+            fld[k] = line.data() + s;
+            len[k] = (e == std::string::npos ? line.size() : e) - s;
+            s = e + 1;
+        }
+        if (std::string(fld[2], len[2]) != want) return true;
+        const uint16_t flag = (uint16_t)atoi(fld[1]);
+        const int64_t pos = atoll(fld[3]) - 1;
+        const uint8_t mapq = (uint8_t)atoi(fld[4]);
+        if (pos < last_pos) throw std::runtime_error("SAM is not coordinate-sorted");
+        last_pos = pos;
+        if (!stepper_keeps(p, flag, mapq)) return true;
+        cig.clear();
+        if (!(len[5] == 1 && fld[5][0] == '*')) {
+            uint32_t v = 0;
+            for (size_t i = 0; i < len[5]; i++) {
+                const char c = fld[5][i];
+                if (c >= '0' && c <= '9') { v = v * 10 + (uint32_t)(c - '0'); continue; }
+                const char *ops = "MIDNSHP=X";
+                const char *o = strchr(ops, c);
+                if (!o || !*o) throw std::runtime_error("bad CIGAR");
+                cig.push_back(v << 4 | (uint32_t)(o - ops));
+                v = 0;
+            }
+        }
+        const std::string rnext(fld[6], len[6]);
+        int32_t mtid = -1;
+        if (rnext == "=") mtid = tid;
+        else if (rnext != "*") { auto it = f->tid_of.find(rnext); mtid = it == f->tid_of.end() ? -1 : it->second; }
+        const int64_t mpos = atoll(fld[7]) - 1, isize = atoll(fld[8]);
+        push_read(R, pos, flag, mapq, mtid, mpos, isize, cig.data(), (uint32_t)cig.size(), fld[0], len[0]);
+        const bool noseq = len[9] == 1 && fld[9][0] == '*';
+        const uint32_t l_seq = noseq ? 0u : (uint32_t)len[9];
+        R.seq_off.push_back(R.seq.size());
+        R.l_seq.push_back(l_seq);
+        for (uint32_t i = 0; i < l_seq; i++) R.seq.push_back(NT16.t[(uint8_t)fld[9][i]]);
+        const bool noq = len[10] == 1 && fld[10][0] == '*';
+        if (!noq && len[10] != l_seq) throw std::runtime_error("SAM QUAL length differs from SEQ");
+        for (uint32_t i = 0; i < l_seq; i++) R.qual.push_back(noq ? 0xFF : (uint8_t)(fld[10][i] - 33));
+        return true;
+    });
+}
+
+// htslib mate-overlap quality tweak (sam.c tweak_overlap_quality): at every reference position
+// where both mates have an aligned M/=/X base, equal bases -> a.q = min(a.q + b.q, 200), b.q = 0;
+// different bases -> the higher (a on ties) keeps 0.8 * q (truncated), the other gets 0.
+void tweak_overlap(Reads &R, size_t a, size_t b) {
+    auto aligned = [&](size_t r, std::vector<std::pair<int64_t, uint32_t>> &out) {
+        int64_t x = R.pos[r];
+        uint32_t y = 0;
+        const uint32_t *c = R.cigar.data() + R.cig_off[r];
+        for (uint32_t i = 0; i < R.n_cig[r]; i++) {
+            const uint32_t op = c[i] & 0xF, l = c[i] >> 4;
+            if (op == C_M || op == C_EQ || op == C_X)
+                for (uint32_t k = 0; k < l; k++) out.emplace_back(x + k, y + k);
+            if (consumes_ref(op)) x += l;
+            if (consumes_query(op)) y += l;
+        }
+    };
+    std::vector<std::pair<int64_t, uint32_t>> pa, pb;
+    aligned(a, pa);
+    aligned(b, pb);
+    size_t i = 0, j = 0;
+    while (i < pa.size() && j < pb.size()) {
+        if (pa[i].first < pb[j].first) { i++; continue; }
+        if (pb[j].first < pa[i].first) { j++; continue; }
+        const uint32_t ia = pa[i].second, ib = pb[j].second;
+        if (ia >= R.l_seq[a] || ib >= R.l_seq[b]) return;
+        uint8_t &qa = R.qual[R.seq_off[a] + ia], &qb = R.qual[R.seq_off[b] + ib];
+        if (R.seq[R.seq_off[a] + ia] == R.seq[R.seq_off[b] + ib]) {
+            const int q = qa + qb;
+            qa = (uint8_t)(q > 200 ? 200 : q);
+            qb = 0;
+        } else if (qa >= qb) {
+            qa = (uint8_t)(0.8 * qa);
+            qb = 0;
+        } else {
+            qb = (uint8_t)(0.8 * qb);
+            qa = 0;
+        }
+        i++;
+        j++;
+    }
+}
+
+// Overlap tweaks happen when the second mate is pushed; columns before the iterator's pending
+// position were already handed out by then (pysam reads qual[qpos] at that time).  Only the D/N
+// entries of the first mate can point (next query base) at a tweaked base in such a column, so
+// the first mate's original qualities are kept for the columns before `col`.
+struct Tweaks {
+    std::vector<int64_t> col;                                   // per read; INT64_MAX = none
+    std::unordered_map<size_t, std::vector<uint8_t>> orig;      // first mate -> qualities before
+};
+
+// Replay of bam_plp_push / bam_plp_next: which reads enter the buffer (maxcnt) and the overlap
+// pairing.  Returns keep[r].
+std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks &T) {
+    const size_t n = R.size();
+    std::vector<uint8_t> keep(n, 0);
+    T.col.assign(n, INT64_MAX);
+    const int64_t maxcnt = p.max_depth > 0 ? p.max_depth : INT64_MAX;
+    // live buffer: reads pushed and not yet freed.  Freed while scanning column c when end <= c.
+    std::priority_queue<std::pair<int64_t, size_t>, std::vector<std::pair<int64_t, size_t>>,
+                        std::greater<std::pair<int64_t, size_t>>> by_end;
+    std::vector<uint8_t> freed(n, 0);
+    size_t head = 0;                          // oldest pushed read not yet freed (list head)
+    std::vector<size_t> pushed;               // kept reads in push order
+    // bam_plp_init leaves iter->tid = iter->pos = 0: for contig 0 the depth check is live from the
+    // first read; for a later contig the first push sees another tid and the iterator then jumps
+    // to that read's position.
+    int64_t it_pos = 0, max_pos = -1;
+    bool started = tid == 0;
+    std::unordered_map<std::string, size_t> olap;
+    auto name = [&](size_t r) { return std::string(R.names.data() + R.name_off[r]); };
+    auto olap_remove = [&](size_t r) {
+        if (!p.ignore_overlaps || olap.empty()) return;
+        auto itr = olap.find(name(r));
+        if (itr != olap.end()) olap.erase(itr);
+    };
+    auto scan = [&](int64_t col) {            // free reads with end <= col (bam_plp_next)
+        while (!by_end.empty() && by_end.top().first <= col) {
+            const size_t r = by_end.top().second;
+            by_end.pop();
+            freed[r] = 1;
+            olap_remove(r);
+        }
+        while (head < pushed.size() && freed[pushed[head]]) head++;
+    };
+    auto advance = [&]() {                     // bam_plp_next loop while max_pos > pos
+        while (max_pos > it_pos) {
+            scan(it_pos);
+            if (head < pushed.size()) {
+                const int64_t hb = R.pos[pushed[head]];
+                if (it_pos < hb) it_pos = hb;
+                else ++it_pos;
+            } else break;
+        }
+    };
+    for (size_t r = 0; r < n; r++) {
+        // bam_plp_push
+        const int64_t cnt = (int64_t)by_end.size() + 1;      // mempool nodes: buffered + tail
+        if (started && it_pos == R.pos[r] && cnt > maxcnt) { olap_remove(r); continue; }
+        max_pos = R.pos[r];
+        if (R.end[r] > it_pos || !started) {
+            keep[r] = 1;
+            pushed.push_back(r);
+            by_end.emplace(R.end[r], r);
+            if (p.ignore_overlaps) {            // overlap_push
+                const uint16_t fl = R.flag[r];
+                const bool cand = !(fl & F_MUNMAP) && (fl & F_PROPER) &&
+                                  !(R.mtid[r] >= 0 && R.mtid[r] != tid) &&
+                                  !(std::llabs(R.isize[r]) >= 2 * (int64_t)R.l_seq[r] && R.mpos[r] >= R.end[r]);
+                if (cand) {
+                    const std::string nm = name(r);
+                    auto itr = olap.find(nm);
+                    if (itr == olap.end()) {
+                        if (R.mpos[r] >= R.pos[r] || ((fl & F_PAIRED) && R.mpos[r] == -1)) olap.emplace(nm, r);
+                    } else {
+                        const size_t a = itr->second;
+                        T.orig.emplace(a, std::vector<uint8_t>(R.qual.begin() + (ptrdiff_t)R.seq_off[a],
+                                                               R.qual.begin() + (ptrdiff_t)(R.seq_off[a] + R.l_seq[a])));
+                        T.col[a] = it_pos;
+                        tweak_overlap(R, a, r);
+                        olap.erase(itr);
+                    }
+                }
+            }
+        }
+        if (!started) {                        // first read: the iterator jumps to its contig/pos
+            started = true;
+            if (head < pushed.size()) it_pos = R.pos[pushed[head]];
+        }
+        advance();
+    }
+    return keep;
+}
+
+void fill_csr(const Reads &R, const std::vector<uint8_t> &keep, const Tweaks &T, spp_batch *B, int threads) {
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (size_t r = 0; r < R.size(); r++)
+        if (keep[r] && R.end[r] > R.pos[r]) { lo = std::min(lo, R.pos[r]); hi = std::max(hi, R.end[r]); }
+    if (lo == INT64_MAX) { lo = 0; hi = 0; }
+    const int64_t C = hi - lo;
+    B->pos_begin = lo;
+    B->n_cols = C;
+    std::vector<int64_t> diff((size_t)C + 1, 0);
+    for (size_t r = 0; r < R.size(); r++)
+        if (keep[r] && R.end[r] > R.pos[r]) { diff[(size_t)(R.pos[r] - lo)]++; diff[(size_t)(R.end[r] - lo)]--; }
+    B->off.assign((size_t)C + 1, 0);
+    int64_t run = 0;
+    for (int64_t c = 0; c < C; c++) {
+        run += diff[(size_t)c];
+        B->off[(size_t)c + 1] = B->off[(size_t)c] + (uint64_t)run;
+    }
+    const uint64_t E = B->off[(size_t)C];
+    B->n_entries = E;
+    B->code = (uint8_t *)malloc(E + 16);
+    B->qual = (uint8_t *)malloc(E + 16);
+    if (!B->code || !B->qual) throw std::runtime_error("out of host memory for the pileup");
+    memset(B->code + E, 0xFF, 16);
+    memset(B->qual + E, 0, 16);
+    // Column-range parallel fill: a thread owns columns [c0, c1) and walks the reads overlapping
+    // them in read order, so each column's entries keep htslib's order.
+    std::vector<size_t> kept;
+    for (size_t r = 0; r < R.size(); r++)
+        if (keep[r] && R.end[r] > R.pos[r]) kept.push_back(r);
+    const int nt = std::max(1, std::min(threads, 64));
+    auto work = [&](int t) {
+        const int64_t c0 = C * t / nt, c1 = C * (t + 1) / nt;
+        if (c0 >= c1) return;
+        std::vector<uint64_t> cur(B->off.begin() + c0, B->off.begin() + c1);
+        // reads are sorted by pos: those starting before lo + c1 can overlap
+        const auto last = std::lower_bound(kept.begin(), kept.end(), lo + c1,
+                                           [&](size_t r, int64_t v) { return R.pos[r] < v; });
+        for (auto itr = kept.begin(); itr != last; ++itr) {
+            const size_t r = *itr;
+            if (R.end[r] <= lo + c0) continue;
+            int64_t x = R.pos[r];
+            uint32_t y = 0;
+            const uint32_t *cg = R.cigar.data() + R.cig_off[r];
+            const uint8_t *sq = R.seq.data() + R.seq_off[r], *ql = R.qual.data() + R.seq_off[r];
+            const uint32_t ls = R.l_seq[r];
+            const int64_t tcol = T.col[r];
+            const uint8_t *ql0 = tcol == INT64_MAX ? ql : T.orig.at(r).data();
+            for (uint32_t i = 0; i < R.n_cig[r] && x < lo + c1; i++) {
+                const uint32_t op = cg[i] & 0xF, l = cg[i] >> 4;
+                if (consumes_ref(op)) {
+                    const int64_t a = std::max<int64_t>(x, lo + c0), e = std::min<int64_t>(x + l, lo + c1);
+                    for (int64_t col = a; col < e; col++) {
+                        const size_t k = (size_t)(col - lo - c0);
+                        uint8_t code, q;
+                        if (op == C_D || op == C_N) {            // resolve_cigar2: qpos = next query base
+                            code = op == C_D ? 16 : 17;
+                            q = y < ls ? (col < tcol ? ql0[y] : ql[y]) : 0;
+                        } else {
+                            const uint32_t qp = y + (uint32_t)(col - x);
+                            code = qp < ls ? sq[qp] : 15;
+                            q = qp < ls ? ql[qp] : 0;
+                        }
+                        B->code[cur[k]] = code;
+                        B->qual[cur[k]] = q;
+                        cur[k]++;
+                    }
+                    x += l;
+                }
+                if (consumes_query(op)) y += l;
+            }
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; t++) pool.emplace_back(work, t);
+    work(0);
+    for (auto &t : pool) t.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *spp_last_error(void) { return g_err.c_str(); }
+
+void spp_default_params(spp_params *p) {
+    memset(p, 0, sizeof(*p));
+    p->stepper = SPP_STEPPER_ALL;
+    p->min_mapping_quality = 0;
+    p->max_depth = 8000;
+    p->ignore_overlaps = 1;
+    p->flag_filter = F_UNMAP | F_SECONDARY | F_QCFAIL | F_DUP;
+    p->n_threads = 1;
+}
+
+int spp_open(const char *path, spp_file **out) {
+    if (!path || !out) return fail("spp_open: null argument");
+    *out = nullptr;
+    try {
+        auto *f = new spp_file();
+        f->path = path;
+        f->bam = is_bgzf(path);
+        if (f->bam) {
+            BamStream s(path, 1);
+            bam_header(s, f);
+        } else {
+            for_lines(path, [&](const std::string &line) {
+                if (line.empty() || line[0] != '@') return false;
+                sam_header_line(f, line);
+                return true;
+            });
+        }
+        *out = f;
+        return 0;
+    } catch (const std::exception &e) {
+        return fail(std::string("spp_open: ") + e.what());
+    }
+}
+
+int spp_close(spp_file *f) {
+    delete f;
+    return 0;
+}
+
+int spp_n_targets(spp_file *f, int32_t *n) {
+    if (!f || !n) return fail("spp_n_targets: null argument");
+    *n = (int32_t)f->targets.size();
+    return 0;
+}
+
+int spp_target(spp_file *f, int32_t tid, const char **name, int64_t *length) {
+    if (!f) return fail("spp_target: null file");
+    if (tid < 0 || (size_t)tid >= f->targets.size()) return fail("spp_target: tid out of range");
+    if (name) *name = f->targets[(size_t)tid].name.c_str();
+    if (length) *length = f->targets[(size_t)tid].len;
+    return 0;
+}
+
+int spp_target_id(spp_file *f, const char *name, int32_t *tid) {
+    if (!f || !name || !tid) return fail("spp_target_id: null argument");
+    auto it = f->tid_of.find(name);
+    if (it == f->tid_of.end()) return fail(std::string("invalid contig `") + name + "`");
+    *tid = it->second;
+    return 0;
+}
+
+int spp_pileup(spp_file *f, int32_t tid, const spp_params *p, spp_batch **out) {
+    if (!f || !p || !out) return fail("spp_pileup: null argument");
+    if (tid < 0 || (size_t)tid >= f->targets.size()) return fail("spp_pileup: tid out of range");
+    *out = nullptr;
+    try {
+        Reads R;
+        if (f->bam) read_bam(f, tid, *p, R);
+        else read_sam(f, tid, *p, R);
+        Tweaks T;
+        const std::vector<uint8_t> keep = simulate(R, *p, tid, T);
+        auto *B = new spp_batch();
+        int64_t used = 0;
+        for (uint8_t k : keep) used += k;
+        B->n_used = used;
+        B->n_dropped = (int64_t)R.size() - used;
+        fill_csr(R, keep, T, B, std::max(1, p->n_threads));
+        *out = B;
+        return 0;
+    } catch (const std::exception &e) {
+        return fail(std::string("spp_pileup: ") + e.what());
+    }
+}
+
+int spp_batch_info(spp_batch *b, int64_t *pos_begin, int64_t *n_cols, uint64_t *n_entries, int64_t *n_reads_used,
+                   int64_t *n_reads_dropped) {
+    if (!b) return fail("spp_batch_info: null batch");
+    if (pos_begin) *pos_begin = b->pos_begin;
+    if (n_cols) *n_cols = b->n_cols;
+    if (n_entries) *n_entries = b->n_entries;
+    if (n_reads_used) *n_reads_used = b->n_used;
+    if (n_reads_dropped) *n_reads_dropped = b->n_dropped;
+    return 0;
+}
+
+int spp_batch_arrays(spp_batch *b, const uint64_t **offsets, const uint8_t **base_code, const uint8_t **qual) {
+    if (!b) return fail("spp_batch_arrays: null batch");
+    if (offsets) *offsets = b->off.data();
+    if (base_code) *base_code = b->code;
+    if (qual) *qual = b->qual;
+    return 0;
+}
+
+int spp_batch_free(spp_batch *b) {
+    delete b;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,122 @@
+"""Pileup front end: BAM/SAM contig -> CSR batch for the GPU engine.
+
+Replaces ``pysam.AlignmentFile(path).pileup(min_mapping_quality=..., min_base_quality=...,
+reference=contig)`` as called by ``LiveVariantCaller.process_bam``
+(variant_caller/live_variant_caller.py:55-60).  The reading, read filtering, htslib depth cap
+and CIGAR walk run in the host C++ library (include/spings_pileup.h); the base-quality filter
+is applied by the GPU engine.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Tuple
+
+import numpy as np
+
+from . import _native as N
+
+
+@dataclass
+class PileupParams:
+    """pysam pileup() keyword defaults (stepper 'all', max_depth 8000, ignore_overlaps True)."""
+    stepper: str = "all"
+    min_mapping_quality: int = 0
+    max_depth: int = 8000
+    ignore_overlaps: bool = True
+    flag_filter: int = 0x704
+    n_threads: int = 8
+
+    def native(self) -> N.SppParams:
+        p = N.SppParams()
+        N.pileup_lib().spp_default_params(C.byref(p))
+        p.stepper = N.SPP_STEPPER[self.stepper]
+        p.min_mapping_quality = int(self.min_mapping_quality)
+        p.max_depth = int(self.max_depth)
+        p.ignore_overlaps = 1 if self.ignore_overlaps else 0
+        p.flag_filter = int(self.flag_filter)
+        p.n_threads = int(self.n_threads)
+        return p
+
+
+class PileupBatch:
+    """CSR batch owned by the native library: ``offsets`` u64[n_cols+1], ``codes``/``quals`` u8[E]
+    (16 padding bytes follow both arrays), columns [pos_begin, pos_begin + n_cols)."""
+
+    def __init__(self, handle):
+        L = N.pileup_lib()
+        self._h = C.c_void_p(handle)
+        pb, nc, ne, nu, nd = C.c_int64(), C.c_int64(), C.c_uint64(), C.c_int64(), C.c_int64()
+        N.pcheck(L.spp_batch_info(self._h, C.byref(pb), C.byref(nc), C.byref(ne), C.byref(nu), C.byref(nd)),
+                 "spp_batch_info")
+        self.pos_begin, self.n_cols, self.n_entries = pb.value, nc.value, ne.value
+        self.n_reads_used, self.n_reads_dropped = nu.value, nd.value
+        po, pc, pq = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        N.pcheck(L.spp_batch_arrays(self._h, C.byref(po), C.byref(pc), C.byref(pq)), "spp_batch_arrays")
+        E = self.n_entries
+        self.offsets = np.ctypeslib.as_array(C.cast(po, C.POINTER(C.c_uint64)), (self.n_cols + 1,))
+        self.codes_padded = np.ctypeslib.as_array(C.cast(pc, C.POINTER(C.c_uint8)), (E + 16,))
+        self.quals_padded = np.ctypeslib.as_array(C.cast(pq, C.POINTER(C.c_uint8)), (E + 16,))
+        self.codes = self.codes_padded[:E]
+        self.quals = self.quals_padded[:E]
+
+    def close(self):
+        if self._h:
+            N.pileup_lib().spp_batch_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def arrays(self) -> Tuple[int, np.ndarray, np.ndarray, np.ndarray]:
+        return self.pos_begin, self.offsets, self.codes, self.quals
+
+
+class AlignmentFile:
+    """Minimal pysam.AlignmentFile stand-in for the hot path: header targets + contig pileup."""
+
+    def __init__(self, path: str, mode: str = "rb"):
+        L = N.pileup_lib()
+        h = C.c_void_p()
+        N.pcheck(L.spp_open(str(path).encode(), C.byref(h)), f"open {path}")
+        self._h = h
+        n = C.c_int32()
+        N.pcheck(L.spp_n_targets(h, C.byref(n)))
+        self.references: List[str] = []
+        self.lengths: List[int] = []
+        for t in range(n.value):
+            nm, ln = C.c_char_p(), C.c_int64()
+            N.pcheck(L.spp_target(h, t, C.byref(nm), C.byref(ln)))
+            self.references.append(nm.value.decode())
+            self.lengths.append(ln.value)
+
+    def get_reference_length(self, reference: str) -> int:
+        return self.lengths[self.references.index(reference)]
+
+    def pileup_batch(self, reference: str, params: PileupParams | None = None) -> PileupBatch:
+        L = N.pileup_lib()
+        tid = C.c_int32()
+        N.pcheck(L.spp_target_id(self._h, reference.encode(), C.byref(tid)), "pileup")
+        b = C.c_void_p()
+        N.pcheck(L.spp_pileup(self._h, tid.value, C.byref((params or PileupParams()).native()), C.byref(b)), "pileup")
+        return PileupBatch(b.value)
+
+    def close(self):
+        if self._h:
+            N.pileup_lib().spp_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -21,7 +21,9 @@ def to_phred_scale(probability: float, threshold: int = 99) -> int:
 
 def _fold(xs):
     it = iter(xs)
-    p = next(it)
+    p = next(it, None)
+    if p is None:
+        return 1.0                      # np.prod([]) == 1.0
     for x in it:
         p = p * x
     return p

@@ -1,0 +1,75 @@
+/*
+ * spings_pileup.h — C-ABI of the host BAM/SAM reader and pileup emulator (libspings_pileup.so).
+ *
+ * Replaces the third-party pysam/htslib pileup that LiveVariantCaller.process_bam drives
+ * (variant_caller/live_variant_caller.py:54-72): it turns one contig of a
+ * coordinate-sorted BAM (or SAM) file into the CSR batch that spg_accumulate consumes
+ * (include/spings_gpu.h): offsets u64[n_cols+1], base_code u8[E], qual u8[E].
+ *
+ * Semantics restated from htslib sam.c / pysam libcalignmentfile.pyx (not vendored, absent from
+ * this image — parity unpinned):
+ *   - reads of the contig in file order; the stepper's read filter (pysam "all": skip
+ *     flag & (UNMAP|SECONDARY|QCFAIL|DUP); "samtools": also MAPQ < min_mapping_quality and
+ *     paired-but-not-proper reads; "nofilter": none); htslib itself skips unmapped reads;
+ *   - htslib's depth cap (bam_plp_push): a read starting at the pending column is dropped when
+ *     the iterator's node count (buffered reads + 1) exceeds max_depth (pysam default 8000);
+ *   - htslib's mate-overlap quality tweak when ignore_overlaps is set (pysam default True);
+ *   - per column, the buffered reads covering it in buffer (file) order: CIGAR M/=/X give the
+ *     base (BAM nibble) and its quality; D gives code 16, N code 17, each with the quality of
+ *     the next query base (0 when past the end) — the value pysam's min_base_quality filter
+ *     tests.  The base-quality filter itself is applied by the GPU engine.
+ *   - columns with no buffered read are not emitted (offsets[c] == offsets[c+1]).
+ * Every function returns 0 on success, < 0 on error (message: spp_last_error()).
+ */
+#ifndef SPINGS_PILEUP_H
+#define SPINGS_PILEUP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPP_STEPPER_ALL 0        /* pysam stepper="all" (its default) */
+#define SPP_STEPPER_NOFILTER 1   /* stepper="nofilter" */
+#define SPP_STEPPER_SAMTOOLS 2   /* stepper="samtools" (MAPQ + orphan filter; no BAQ: no fastafile) */
+
+typedef struct {
+    int32_t stepper;               /* SPP_STEPPER_* */
+    int32_t min_mapping_quality;   /* applied by the samtools stepper (pileup(min_mapping_quality=)) */
+    int32_t max_depth;             /* htslib maxcnt; pysam default 8000; <= 0 = unlimited (extension) */
+    int32_t ignore_overlaps;       /* 1 = htslib overlap quality tweak (pysam default) */
+    uint32_t flag_filter;          /* samtools stepper flag filter (pysam default 0x704) */
+    int32_t n_threads;             /* BGZF inflate / CSR fill threads (<= 0: 1) */
+    int64_t reserved[2];
+} spp_params;
+
+typedef struct spp_file spp_file;
+typedef struct spp_batch spp_batch;
+
+const char *spp_last_error(void);
+void spp_default_params(spp_params *p);
+
+/* Open a BAM (BGZF) or SAM file and parse its header. */
+int spp_open(const char *path, spp_file **out);
+int spp_close(spp_file *f);
+int spp_n_targets(spp_file *f, int32_t *n);
+/* name pointer valid until spp_close */
+int spp_target(spp_file *f, int32_t tid, const char **name, int64_t *length);
+int spp_target_id(spp_file *f, const char *name, int32_t *tid);
+
+/* AlignmentFile.pileup(reference=<contig tid>, ...) over the whole contig -> one CSR batch.
+ * The batch covers columns [pos_begin, pos_begin + n_cols) (first..last emitted column). */
+int spp_pileup(spp_file *f, int32_t tid, const spp_params *p, spp_batch **out);
+int spp_batch_info(spp_batch *b, int64_t *pos_begin, int64_t *n_cols, uint64_t *n_entries,
+                   int64_t *n_reads_used, int64_t *n_reads_dropped);
+/* Arrays owned by the batch (valid until spp_batch_free).  base_code and qual are allocated
+ * with 16 bytes of padding past n_entries (code 0xFF, qual 0) so they can be handed to the GPU
+ * engine without a copy. */
+int spp_batch_arrays(spp_batch *b, const uint64_t **offsets, const uint8_t **base_code, const uint8_t **qual);
+int spp_batch_free(spp_batch *b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPINGS_PILEUP_H */

@@ -1,0 +1,134 @@
+"""Pileup front end (include/spings_pileup.h) vs the pure-Python restatement oracle/pileup_port.py.
+
+pysam/htslib is absent here and on the GPU box, so both sides restate htslib/pysam behaviour
+(parity unpinned); they are built differently (C++ post-hoc CSR fill vs a
+column-by-column simulation of bam_plp_next) and must agree bit-exactly."""
+import os
+
+import numpy as np
+import pytest
+
+import spings  # noqa: F401
+from covid_spings_variant_caller_amd import build as B
+from covid_spings_variant_caller_amd.pileup import AlignmentFile, PileupParams
+from oracle import pileup_port as pp
+import samgen
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TESTFILE = os.path.join(GOLD, "testfile.sam")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    B.build_pileup()
+
+
+def product(path, contig, **kw):
+    with AlignmentFile(path) as f:
+        b = f.pileup_batch(contig, PileupParams(n_threads=kw.pop("n_threads", 3), **kw))
+        return b.pos_begin, b.offsets.copy(), b.codes.copy(), b.quals.copy()
+
+
+def oracle(path, contig, **kw):
+    return pp.to_csr(pp.pileup_columns(path, contig, **kw))
+
+
+def assert_same(a, b):
+    assert a[0] == b[0], (a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[2], b[2])
+    np.testing.assert_array_equal(a[3], b[3])
+
+
+def test_testfile_sam_counts():
+    """Config 1 input (test/testdata/testfile.sam): 4 reads, 421 columns, 1,642 entries."""
+    got = product(TESTFILE, "NC_045512.2")
+    exp = oracle(TESTFILE, "NC_045512.2")
+    assert_same(got, exp)
+    assert got[0] == 10 and len(got[1]) - 1 == 421 and int(got[1][-1]) == 1642
+    passing = int((got[3] >= 30).sum())
+    assert passing == 202            # 202 of 1,642 entries pass Q>=30
+
+
+def test_testfile_golden():
+    z = np.load(os.path.join(GOLD, "testfile_pileup.npz"))
+    got = product(TESTFILE, "NC_045512.2")
+    assert got[0] == int(z["pos_begin"])
+    np.testing.assert_array_equal(got[1], z["offsets"])
+    np.testing.assert_array_equal(got[2], z["codes"])
+    np.testing.assert_array_equal(got[3], z["quals"])
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("kw", [dict(), dict(max_depth=4), dict(max_depth=1), dict(max_depth=0),
+                                dict(stepper="samtools", min_mapping_quality=20, max_depth=6),
+                                dict(stepper="nofilter"), dict(ignore_overlaps=False, max_depth=3)])
+def test_random_sam_vs_port(tmp_path, seed, kw):
+    contigs = [("chrA", 700), ("chrB", 700)]
+    recs = samgen.random_records(seed, contigs)
+    sam = str(tmp_path / "r.sam")
+    samgen.write_sam(sam, contigs, recs)
+    for c, _ in contigs:
+        assert_same(product(sam, c, **kw), oracle(sam, c, **kw))
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_bam_equals_sam(tmp_path, seed):
+    contigs = [("chrA", 700), ("chrB", 700)]
+    recs = samgen.random_records(seed, contigs, n_reads=500)
+    sam, bam = str(tmp_path / "r.sam"), str(tmp_path / "r.bam")
+    samgen.write_sam(sam, contigs, recs)
+    samgen.write_bam(bam, contigs, recs, block=7000)       # many BGZF blocks
+    with AlignmentFile(bam) as f:
+        assert f.references == ["chrA", "chrB"] and f.lengths == [700, 700]
+    for c, _ in contigs:
+        for kw in (dict(), dict(max_depth=5)):
+            assert_same(product(bam, c, **kw), product(sam, c, **kw))
+
+
+def test_threads_do_not_change_order(tmp_path):
+    contigs = [("chrA", 700)]
+    recs = samgen.random_records(9, contigs, n_reads=800)
+    sam = str(tmp_path / "r.sam")
+    samgen.write_sam(sam, contigs, recs)
+    a = product(sam, "chrA", n_threads=1)
+    for t in (2, 7, 16):
+        assert_same(product(sam, "chrA", n_threads=t), a)
+
+
+def test_depth_cap_rule(tmp_path):
+    """htslib maxcnt: reads starting at the pending position are dropped once buffered reads + 1 >
+    max_depth; reads starting later are always taken (the cap is per start position)."""
+    recs = []
+    for i in range(10):                       # 10 reads at pos 1, then 10 at pos 5
+        recs.append(dict(qname=f"a{i}", flag=0, rname="c", pos=1, mapq=60, cigar="20M", rnext="*", pnext=0,
+                         tlen=0, seq="A" * 20, qual="I" * 20))
+    for i in range(10):
+        recs.append(dict(qname=f"b{i}", flag=0, rname="c", pos=5, mapq=60, cigar="20M", rnext="*", pnext=0,
+                         tlen=0, seq="C" * 20, qual="I" * 20))
+    sam = str(tmp_path / "cap.sam")
+    samgen.write_sam(sam, [("c", 100)], recs)
+    pb, off, codes, quals = product(sam, "c", max_depth=4)
+    assert_same((pb, off, codes, quals), oracle(sam, "c", max_depth=4))
+    depth = np.diff(off.astype(np.int64))
+    # contig 0: iterator starts at pos 0 -> first read at 0 kept while cnt (= buffered + 1) <= 4:
+    # 4 reads kept at pos 0; at pos 4 the first read is always kept (pending position differs), then
+    # the buffer already holds 5 -> the other 9 are dropped
+    assert pb == 0 and depth[0] == 4 and depth[4] == 5
+
+
+def test_unsorted_raises(tmp_path):
+    recs = [dict(qname="x", flag=0, rname="c", pos=50, mapq=60, cigar="10M", rnext="*", pnext=0, tlen=0,
+                 seq="A" * 10, qual="I" * 10),
+            dict(qname="y", flag=0, rname="c", pos=10, mapq=60, cigar="10M", rnext="*", pnext=0, tlen=0,
+                 seq="A" * 10, qual="I" * 10)]
+    sam = str(tmp_path / "u.sam")
+    samgen.write_sam(sam, [("c", 100)], recs)
+    with pytest.raises(RuntimeError, match="sorted"):
+        product(sam, "c")
+
+
+def test_unknown_contig_raises():
+    with AlignmentFile(TESTFILE) as f:
+        with pytest.raises(RuntimeError, match="contig"):
+            f.pileup_batch("chrZ")
