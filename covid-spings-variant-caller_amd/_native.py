@@ -86,6 +86,9 @@ def gpu_lib():
     _sig(L.spg_copy_candidates_device, i32, vp, vp, i64)
     _sig(L.spg_last_kernel_ms, i32, vp, C.POINTER(C.c_float), C.POINTER(C.c_float))
     _sig(L.spg_kernel_times, i32, vp, vp, vp, i64, C.POINTER(i64))
+    _sig(L.spg_history_count, i32, vp, C.POINTER(i64))
+    _sig(L.spg_history_info, i32, vp, i64, C.POINTER(i64), C.POINTER(i64), C.POINTER(u64))
+    _sig(L.spg_history_copy, i32, vp, i64, vp, vp, vp)
     _sig(L.spg_device_count, i32, C.POINTER(i32))
     _sig(L.spg_sizeof_candidate, C.c_size_t)
     _sig(L.spg_sizeof_detail, C.c_size_t)

@@ -36,6 +36,7 @@ static int fail(const std::string &m) {
 
 struct HistBatch {
     int64_t pos_begin, n_cols;
+    uint64_t n_entries;
     uint64_t *off;
     uint8_t *code, *qual;
     bool owned;
@@ -257,7 +258,7 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
     HIPCHK(hipSetDevice(c->device));
     const bool dev = flags & SPG_IN_DEVICE;
     const bool borrow = dev && (flags & SPG_IN_BORROW);
-    HistBatch hb{pos_begin, n_cols, nullptr, nullptr, nullptr, !borrow};
+    HistBatch hb{pos_begin, n_cols, n_entries, nullptr, nullptr, nullptr, !borrow};
     if (!dev) {
         // validate the host CSR (cheap, O(n_cols)); device inputs are trusted
         if (offsets[0] != 0 || offsets[n_cols] != n_entries) return fail("spg_accumulate: offsets[0] must be 0 and offsets[n_cols] == n_entries");
@@ -519,6 +520,34 @@ int spg_kernel_times(spg_ctx *c, float *acc_ms, float *fin_ms, int64_t cap, int6
     }
     c->ring_r += n;
     *n_out = n;
+    return 0;
+}
+
+int spg_history_count(spg_ctx *c, int64_t *n_batches) {
+    if (!c || !n_batches) return fail("spg_history_count: null argument");
+    *n_batches = (int64_t)c->hist.size();
+    return 0;
+}
+
+int spg_history_info(spg_ctx *c, int64_t i, int64_t *pos_begin, int64_t *n_cols, uint64_t *n_entries) {
+    if (!c) return fail("spg_history_info: null ctx");
+    if (i < 0 || i >= (int64_t)c->hist.size()) return fail("spg_history_info: batch index out of range");
+    const HistBatch &h = c->hist[(size_t)i];
+    if (pos_begin) *pos_begin = h.pos_begin;
+    if (n_cols) *n_cols = h.n_cols;
+    if (n_entries) *n_entries = h.n_entries;
+    return 0;
+}
+
+int spg_history_copy(spg_ctx *c, int64_t i, uint64_t *offsets, uint8_t *base_code, uint8_t *qual) {
+    if (!c) return fail("spg_history_copy: null ctx");
+    if (i < 0 || i >= (int64_t)c->hist.size()) return fail("spg_history_copy: batch index out of range");
+    HIPCHK(hipSetDevice(c->device));
+    const HistBatch &h = c->hist[(size_t)i];
+    if (offsets) HIPCHK(hipMemcpyAsync(offsets, h.off, sizeof(uint64_t) * (h.n_cols + 1), hipMemcpyDeviceToHost, c->stream));
+    if (base_code && h.n_entries) HIPCHK(hipMemcpyAsync(base_code, h.code, h.n_entries, hipMemcpyDeviceToHost, c->stream));
+    if (qual && h.n_entries) HIPCHK(hipMemcpyAsync(qual, h.qual, h.n_entries, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
 

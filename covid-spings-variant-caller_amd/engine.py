@@ -134,6 +134,24 @@ class PileupEngine:
             N.check(self._L.spg_kernel_times(self._h, N.ptr(a), N.ptr(f), int(cap), C.byref(n)), "spg_kernel_times")
         return a[:n.value].astype(np.float64), f[:n.value].astype(np.float64)
 
+    def history(self):
+        """The accumulated batches since reset(), as host copies: [(pos_begin, offsets, codes, quals)]."""
+        out = []
+        with self._lock:
+            n = C.c_int64()
+            N.check(self._L.spg_history_count(self._h, C.byref(n)), "spg_history_count")
+            for i in range(n.value):
+                pb, nc, ne = C.c_int64(), C.c_int64(), C.c_uint64()
+                N.check(self._L.spg_history_info(self._h, i, C.byref(pb), C.byref(nc), C.byref(ne)),
+                        "spg_history_info")
+                off = np.zeros(nc.value + 1, np.uint64)
+                codes = np.zeros(ne.value, np.uint8)
+                quals = np.zeros(ne.value, np.uint8)
+                N.check(self._L.spg_history_copy(self._h, i, N.ptr(off), N.ptr(codes), N.ptr(quals)),
+                        "spg_history_copy")
+                out.append((pb.value, off, codes, quals))
+        return out
+
     # -- results ------------------------------------------------------------------------------
     def table(self, pos0: int = 0, n: Optional[int] = None) -> Dict[str, np.ndarray]:
         n = self.n_pos - pos0 if n is None else n

@@ -1,0 +1,277 @@
+"""Drop-in ``LiveVariantCaller`` (variant_caller/live_variant_caller.py:21-297) on the MI355X engine.
+
+Same constructor arguments, methods and semantics as the reference class:
+
+* ``process_bam(inputBam, referenceIndex=0)`` (:54-72) — the contig's pileup is built by the host
+  emulator (``pileup.AlignmentFile``, include/spings_pileup.h) with pysam's pileup() defaults and
+  the caller's min_mapping_quality, then accumulated on the GPU (``spg_accumulate``) where the
+  base-quality filter, ``process_pileup_column`` and ``process_svn`` (:74-103) run.  Accumulates
+  across calls like ``memory``; positions are keyed by coordinate only, as in the reference.
+* ``prepare_variants()`` (:120-231) — ``spg_finalize`` on the GPU; returns the reference's
+  ``List[Variant]`` (start, stop, alleles, qual, info{DP, AD, GL, PL, SCORE}) in memory order.
+* ``write_vcf(outputVfc)`` (:233-297) — same header, records sorted by (start, SCORE); written by
+  pysam when it is importable, otherwise by a writer that emits the text htslib produces for this
+  header (float32 QUAL/Float INFO printed with %g).
+* ``reset_memory()`` (:37-38), ``create_checkpoint`` / ``load_checkpoint`` (:40-52) — the
+  checkpoint holds the accumulated batches (the engine's exact state) instead of a pickle.
+* ``memory`` (:32) — read-only view rebuilt from the device table and batch history.
+
+Exceptions propagate like the reference's (missing files -> OSError, unknown contig ->
+ValueError, engine/library failures -> RuntimeError).  There is no CPU path: without
+libspings_gpu.so or a GPU the constructor raises.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from . import _native as N
+from .engine import PileupEngine
+from .pileup import AlignmentFile, PileupParams
+from .structs import Site, Variant
+
+log = logging.getLogger("covid_spings_variant_caller_amd")
+
+
+class FastaFile:
+    """The part of pysam.FastaFile the caller uses: references, lengths, fetch(reference=)."""
+
+    def __init__(self, path: str):
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"could not open fasta file `{path}`")
+        self.filename = path
+        self.references: List[str] = []
+        self._seq: Dict[str, str] = {}
+        name, parts = None, []
+        with open(path) as f:
+            for line in f:
+                line = line.rstrip("\r\n")
+                if line.startswith(">"):
+                    if name is not None:
+                        self._seq[name] = "".join(parts)
+                    name, parts = line[1:].split()[0] if line[1:].split() else "", []
+                    self.references.append(name)
+                elif line:
+                    parts.append(line.strip())
+        if name is not None:
+            self._seq[name] = "".join(parts)
+        self.lengths = [len(self._seq[r]) for r in self.references]
+
+    def fetch(self, reference: str) -> str:
+        if reference not in self._seq:
+            raise KeyError(f"sequence '{reference}' not present")
+        return self._seq[reference]
+
+    def get_reference_length(self, reference: str) -> int:
+        return len(self.fetch(reference))
+
+    def close(self):
+        pass
+
+
+class LiveVariantCaller:
+    def __init__(self, referenceFasta: str, minBaseQuality: int, minMappingQuality: int, minTotalDepth: int,
+                 minAlleleDepth: int, minEvidenceRatio: float, maxVariants: int, device: Optional[int] = None,
+                 max_depth: int = 8000, stepper: str = "all", ignore_overlaps: bool = True,
+                 n_threads: Optional[int] = None):
+        self.minBaseQuality = minBaseQuality
+        self.minMappingQuality = minMappingQuality
+        self.minTotalDepth = minTotalDepth
+        self.minAlleleDepth = minAlleleDepth
+        self.minEvidenceRatio = minEvidenceRatio
+        self.maxVariants = maxVariants
+        self.fastaFile = FastaFile(referenceFasta)
+        self.pileup_params = PileupParams(stepper=stepper, min_mapping_quality=minMappingQuality, max_depth=max_depth,
+                                          ignore_overlaps=ignore_overlaps,
+                                          n_threads=n_threads or min(16, len(os.sched_getaffinity(0))))
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0"))
+        n_pos = max(self.fastaFile.lengths) if self.fastaFile.lengths else 1
+        self.engine = PileupEngine(max(1, n_pos), minBaseQuality, minTotalDepth, minAlleleDepth, minEvidenceRatio,
+                                   device=device)
+        self._lock = threading.RLock()
+        self._batch_contig: List[int] = []       # FASTA reference index of each accumulated batch
+        self.reset_memory()
+
+    def __del__(self):
+        try:
+            self.fastaFile.close()
+            self.engine.close()
+        except Exception:
+            pass
+
+    # -- memory -------------------------------------------------------------------------------
+    def reset_memory(self):
+        """:37-38"""
+        with self._lock:
+            self.engine.reset()
+            self._batch_contig = []
+            self._current_ref = None
+
+    def _use_reference(self, index: int):
+        if self._current_ref != index:
+            self.engine.set_reference(self.fastaFile.fetch(self.fastaFile.references[index]))
+            self._current_ref = index
+
+    @property
+    def memory(self) -> Dict[int, Site]:
+        """Read-only view of the reference's ``memory`` (dict[int, Site], insertion order):
+        reference char and totalDepth from the device table, per-allele quality lists (bq-filtered,
+        BAM order) regrouped from the batch history."""
+        with self._lock:
+            self.engine.finalize()
+            t = self.engine.table()
+            hist = self.engine.history()
+            minbq = self.minBaseQuality
+            present = np.nonzero(t["flags"] & N.SPG_F_PRESENT)[0]
+            order = present[np.lexsort((present, t["first_batch"][present]))]
+            mem: Dict[int, Site] = {}
+            refs = [self.fastaFile.fetch(self.fastaFile.references[i]) for i in self._batch_contig]
+            for p in order.tolist():
+                b = int(t["first_batch"][p]) - 1
+                mem[p] = {"reference": refs[b][p], "totalDepth": int(t["depth"][p]), "snvs": {}, "indels": {}}
+            for pb, off, codes, quals in hist:
+                for c in range(len(off) - 1):
+                    lo, hi = int(off[c]), int(off[c + 1])
+                    if lo == hi:
+                        continue
+                    snvs = mem[pb + c]["snvs"]
+                    for code, q in zip(codes[lo:hi].tolist(), quals[lo:hi].tolist()):
+                        if q < minbq or code >= 16:
+                            continue
+                        snvs.setdefault(N.NIBBLE[code], []).append(q)
+            return mem
+
+    # -- hot path -----------------------------------------------------------------------------
+    def process_bam(self, inputBam: str, referenceIndex=0):
+        """:54-72 — pileup of references[referenceIndex] accumulated on the GPU."""
+        if not os.path.exists(inputBam):
+            raise FileNotFoundError(f"[Errno 2] could not open alignment file `{inputBam}`: No such file or directory")
+        contig = self.fastaFile.references[referenceIndex]
+        with AlignmentFile(inputBam) as bam:
+            if contig not in bam.references:
+                raise ValueError(f"invalid contig `{contig}`")
+            batch = bam.pileup_batch(contig, self.pileup_params)
+        with self._lock:
+            if batch.n_cols == 0:
+                return
+            self._use_reference(referenceIndex)
+            self.engine.accumulate(batch.pos_begin, batch.offsets, batch.codes, batch.quals)
+            self._batch_contig.append(referenceIndex)
+        batch.close()
+
+    def prepare_variants(self) -> List[Variant]:
+        """:120-231"""
+        with self._lock:
+            self.engine.finalize()
+            return self.engine.variants()
+
+    # -- checkpoint ---------------------------------------------------------------------------
+    def create_checkpoint(self, filename):
+        """:40-45 — the accumulated batches (exact engine state), numpy .npz."""
+        log.info("Creating checkpoint %s", filename)
+        with self._lock:
+            hist = self.engine.history()
+            arrays = {"contig": np.array(self._batch_contig, np.int64),
+                      "names": np.array(self.fastaFile.references)}
+            for i, (pb, off, codes, quals) in enumerate(hist):
+                arrays[f"b{i}_pos"] = np.int64(pb)
+                arrays[f"b{i}_off"] = off
+                arrays[f"b{i}_codes"] = codes
+                arrays[f"b{i}_quals"] = quals
+            with open(filename, "wb") as f:
+                np.savez(f, **arrays)
+
+    def load_checkpoint(self, filename):
+        """:47-52 — replaces memory with the checkpoint's (replays its batches)."""
+        log.info("Loading checkpoint %s", filename)
+        with np.load(filename, allow_pickle=False) as z:
+            contig = z["contig"].tolist()
+            names = z["names"].tolist()
+            if names != self.fastaFile.references:
+                raise ValueError("checkpoint was made with a different reference FASTA")
+            batches = [(int(z[f"b{i}_pos"]), z[f"b{i}_off"], z[f"b{i}_codes"], z[f"b{i}_quals"])
+                       for i in range(len(contig))]
+        with self._lock:
+            self.reset_memory()
+            for ci, (pb, off, codes, quals) in zip(contig, batches):
+                self._use_reference(ci)
+                self.engine.accumulate(pb, off, codes, quals)
+                self._batch_contig.append(ci)
+
+    # -- output ------------------------------------------------------------------------------
+    def write_vcf(self, outputVfc: str):
+        """:233-297"""
+        print("VFC output", outputVfc)
+        variants = self.prepare_variants()
+        records = sorted(variants, key=lambda v: (v["start"], v["info"]["SCORE"]))
+        contigs = [(r, self.fastaFile.get_reference_length(r)) for r in self.fastaFile.references]
+        try:
+            import pysam  # noqa: F401
+        except ImportError:
+            pysam = None
+        if pysam is not None:
+            _write_vcf_pysam(pysam, outputVfc, contigs, records)
+        else:
+            write_vcf_text(outputVfc, contigs, records)
+
+
+INFO_META = [
+    ("DP", "1", "Integer", "Total Depth"),
+    ("AD", "1", "Integer", "Allele Depth"),
+    ("GL", "1", "Float", "Genotype likelihoods comprised of comma separated floating point log10-scaled "
+                         "likelihoods for all possible genotypes given the set of alleles defined in the REF "
+                         "and ALT fields"),
+    ("PL", "1", "Integer", "The phred-scaled genotype likelihoods rounded to the closest integer (and otherwise "
+                           "defined precisely as the GL field)"),
+    ("SCORE", "1", "Float", "Custom scoring function"),
+]
+
+
+def _hval(v: str) -> str:
+    """htslib header value quoting as pysam's add_meta does it (quote when it holds ' ;,"\\t<>')."""
+    return f'"{v}"' if any(ch in v for ch in ' ;,"\t<>') else v
+
+
+def _f32(x) -> str:
+    """A Float field as htslib prints it: stored as float32, printed with %g."""
+    return "%g" % float(np.float32(x))
+
+
+def write_vcf_text(path: str, contigs, records: List[Variant]):
+    """The VCF text pysam.VariantFile(mode='w') writes for the reference's header (:235-278)."""
+    out = ["##fileformat=VCFv4.2", '##FILTER=<ID=PASS,Description="All filters passed">']
+    for i, n, t, d in INFO_META:
+        out.append(f"##INFO=<ID={i},Number={n},Type={t},Description={_hval(d)}>")
+    for name, length in contigs:
+        out.append(f"##contig=<ID={name},length={length}>")
+    out.append("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO")
+    chrom = contigs[0][0] if contigs else "."          # new_record() without contig -> rid 0
+    for v in records:
+        info = v["info"]
+        fields = []
+        for key, _, typ, _ in INFO_META:
+            if key not in info:
+                continue
+            val = info[key]
+            fields.append(f"{key}={int(val)}" if typ == "Integer" else f"{key}={_f32(val)}")
+        out.append("\t".join([chrom, str(v["start"] + 1), ".", v["alleles"][0], v["alleles"][1], _f32(v["qual"]), ".",
+                              ";".join(fields)]))
+    with open(path, "w") as f:
+        f.write("\n".join(out) + "\n")
+
+
+def _write_vcf_pysam(pysam, path, contigs, records):
+    h = pysam.VariantHeader()
+    for i, n, t, d in INFO_META:
+        h.add_meta("INFO", items=[("ID", i), ("Number", int(n)), ("Type", t), ("Description", d)])
+    for name, length in contigs:
+        h.contigs.add(name, length)
+    vf = pysam.VariantFile(path, mode="w", header=h)
+    for v in records:
+        vf.write(vf.new_record(start=v["start"], stop=v["stop"], alleles=v["alleles"], qual=v["qual"], info=v["info"]))
+    vf.close()

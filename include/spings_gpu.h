@@ -153,6 +153,14 @@ int spg_device_results(spg_ctx *ctx, void **candidates, void **n_candidates);
  * another stream (e.g. an RCCL gather) may read dst afterwards. */
 int spg_copy_candidates_device(spg_ctx *ctx, void *dst, int64_t cap);
 
+/* The accumulated batches (replay history) since the last spg_reset, in accumulate order: the
+ * exact state behind LiveVariantCaller.memory, used for create_checkpoint (:40-45) and the
+ * memory view.  spg_history_copy copies batch i to host buffers (offsets n_cols+1, base_code /
+ * qual n_entries each; any may be NULL) and synchronises. */
+int spg_history_count(spg_ctx *ctx, int64_t *n_batches);
+int spg_history_info(spg_ctx *ctx, int64_t i, int64_t *pos_begin, int64_t *n_cols, uint64_t *n_entries);
+int spg_history_copy(spg_ctx *ctx, int64_t i, uint64_t *offsets, uint8_t *base_code, uint8_t *qual);
+
 /* Timing hooks (bench): HIP events around the accumulate launches of one finalize step (first
  * begin .. last end) and around the finalize launch, ms.  spg_last_kernel_ms: the latest step.
  * spg_kernel_times: every step completed since the previous spg_kernel_times call (at most 64

@@ -162,3 +162,44 @@ def random_records(seed, contigs, n_reads=300, L=600, read_len=60, pair_frac=0.3
         recs_c = [r for r in recs if r["rname"] == cname]
         recs = [r for r in recs if r["rname"] != cname] + sorted(recs_c, key=lambda r: r["pos"])
     return recs
+
+
+def snv_records(contig, ref, n_reads, read_len=60, snvs=None, seed=0, del_frac=0.05, qual_choices=None):
+    """Single-end reads sampled from `ref` with planted SNVs {pos: (alt, af)} (0-based), random
+    errors, a few 2-base deletions; coordinate-sorted SAM records."""
+    rng = random.Random(seed)
+    snvs = snvs or {}
+    qual_choices = qual_choices or [12, 20, 28, 30, 32, 35, 37, 38, 40, 41]
+    L = len(ref)
+    starts = sorted(rng.randrange(0, L - read_len) for _ in range(n_reads))
+    recs = []
+    for i, s in enumerate(starts):
+        if rng.random() < del_frac:
+            k = rng.randrange(10, read_len - 12)
+            cig = [("M", k), ("D", 2), ("M", read_len - k)]
+        else:
+            cig = [("M", read_len)]
+        seq, x = [], s
+        for op, n in cig:
+            if op == "M":
+                for j in range(n):
+                    b = ref[x + j].upper()
+                    if (x + j) in snvs and rng.random() < snvs[x + j][1]:
+                        b = snvs[x + j][0]
+                    if rng.random() < 0.01:
+                        b = rng.choice("ACGTN")
+                    seq.append(b)
+            x += n
+        qual = "".join(chr(33 + rng.choice(qual_choices)) for _ in seq)
+        recs.append(dict(qname=f"q{i}", flag=0, rname=contig, pos=s + 1, mapq=60,
+                         cigar="".join(f"{n}{op}" for op, n in cig), rnext="*", pnext=0, tlen=0,
+                         seq="".join(seq), qual=qual))
+    return recs
+
+
+def write_fasta(path, seqs, width=60):
+    with open(path, "w") as f:
+        for name, s in seqs:
+            f.write(f">{name} synthetic\n")
+            for i in range(0, len(s), width):
+                f.write(s[i:i + width] + "\n")

@@ -1,0 +1,145 @@
+"""LiveVariantCaller drop-in (covid-spings-variant-caller_amd/live_variant_caller.py) on the GPU,
+end to end from SAM/BAM files: pileup emulator -> spg_accumulate -> spg_finalize, against the
+oracle chain oracle/pileup_port.py -> oracle/reference_port.OracleCaller on the same files."""
+import os
+
+import numpy as np
+import pytest
+
+import spings  # noqa: F401
+import samgen
+from oracle_util import compare_variants
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+RTOL = 1e-9
+
+
+def _ref(L, seed):
+    from covid_spings_variant_caller_amd import synth
+    return synth.reference(L, seed=seed)
+
+
+def _oracle(ref, files, contig="chrS", minbq=30, **pk):
+    from oracle import pileup_port as pp
+    from oracle.reference_port import OracleCaller
+    o = OracleCaller(ref, minbq, 10, 5, 0.10)
+    for f in files:
+        o.accumulate(*pp.to_csr(pp.pileup_columns(f, contig, **pk)))
+    return o
+
+
+def _caller(fasta, **kw):
+    from covid_spings_variant_caller_amd.live_variant_caller import LiveVariantCaller
+    return LiveVariantCaller(fasta, 30, 20, 10, 5, 0.10, 1, **kw)
+
+
+@pytest.fixture(scope="module")
+def planted(tmp_path_factory):
+    d = tmp_path_factory.mktemp("lvc")
+    L = 800
+    ref = _ref(L, 11)
+    ref = ref[:100] + ref[100:200].lower() + ref[200:]          # lowercase REF chars are kept
+    fasta = str(d / "ref.fa")
+    samgen.write_fasta(fasta, [("chrS", ref)])
+    snvs = {150: ("T" if ref[150].upper() != "T" else "A", 0.5), 300: ("G" if ref[300] != "G" else "C", 0.3),
+            301: ("C" if ref[301] != "C" else "G", 0.9), 555: ("A" if ref[555] != "A" else "T", 0.12)}
+    files = []
+    for k, (n, fmt) in enumerate([(900, "sam"), (700, "bam")]):
+        recs = samgen.snv_records("chrS", ref, n, snvs=snvs, seed=20 + k)
+        p = str(d / f"s{k}.{fmt}")
+        (samgen.write_sam if fmt == "sam" else samgen.write_bam)(p, [("chrS", L)], recs)
+        files.append(p)
+    return d, ref, fasta, files
+
+
+def test_testfile_sam_no_variants(tmp_path):
+    """Config 1: the reference's test fixture yields no variants (depth <= 4 < minTotalDepth)."""
+    fasta = str(tmp_path / "cov.fa")
+    samgen.write_fasta(fasta, [("NC_045512.2", _ref(29903, 1))])
+    c = _caller(fasta)
+    c.process_bam(os.path.join(GOLD, "testfile.sam"))
+    assert c.prepare_variants() == []
+    o = _oracle(_ref(29903, 1), [os.path.join(GOLD, "testfile.sam")], contig="NC_045512.2")
+    mem = c.memory
+    assert list(mem.keys()) == list(o.memory.keys())
+    for p, s in o.memory.items():
+        assert mem[p]["totalDepth"] == s["totalDepth"] and mem[p]["snvs"] == s["snvs"], p
+    out = tmp_path / "o.vcf"
+    c.write_vcf(str(out))
+    assert out.read_text().splitlines()[-1].startswith("#CHROM")
+
+
+def test_process_bam_two_files_vs_oracle(planted):
+    d, ref, fasta, files = planted
+    c = _caller(fasta)
+    for f in files:
+        c.process_bam(f)
+    got = c.prepare_variants()
+    exp = _oracle(ref, files).prepare_variants()
+    assert len(exp) >= 3
+    compare_variants(got, exp, RTOL)
+    assert any(v["info"]["GL"] != 0 for v in got)
+    mem, omem = c.memory, _oracle(ref, files).memory
+    assert list(mem) == list(omem)
+    assert all(mem[p] == omem[p] for p in omem)
+
+
+def test_write_vcf_sorted_and_formatted(planted):
+    d, ref, fasta, files = planted
+    c = _caller(fasta)
+    for f in files:
+        c.process_bam(f)
+    out = d / "calls.vcf"
+    c.write_vcf(str(out))
+    lines = [ln for ln in out.read_text().splitlines() if not ln.startswith("#")]
+    exp = sorted(_oracle(ref, files).prepare_variants(), key=lambda v: (v["start"], v["info"]["SCORE"]))
+    assert len(lines) == len(exp)
+    for ln, v in zip(lines, exp):
+        f = ln.split("\t")
+        assert f[0] == "chrS" and int(f[1]) == v["start"] + 1 and (f[3], f[4]) == v["alleles"]
+        assert float(f[5]) == pytest.approx(float(np.float32(v["qual"])), rel=1e-5)
+
+
+def test_checkpoint_roundtrip(planted):
+    d, ref, fasta, files = planted
+    a = _caller(fasta)
+    a.process_bam(files[0])
+    ck = str(d / "ck.npz")
+    a.create_checkpoint(ck)
+    b = _caller(fasta)
+    b.load_checkpoint(ck)
+    b.process_bam(files[1])                      # resume: live mode (vc_queue.py:134-144)
+    a.process_bam(files[1])
+    compare_variants(b.prepare_variants(), a.prepare_variants(), 0.0)
+
+
+def test_reset_memory(planted):
+    d, ref, fasta, files = planted
+    c = _caller(fasta)
+    c.process_bam(files[0])
+    c.reset_memory()
+    assert c.prepare_variants() == [] and c.memory == {}
+    c.process_bam(files[1])
+    compare_variants(c.prepare_variants(), _oracle(ref, files[1:]).prepare_variants(), RTOL)
+
+
+def test_depth_cap_parity_mode(planted):
+    """max_depth (pysam default 8000) is applied by the emulator: a small cap changes depths the same
+    way in the product and in the oracle chain."""
+    d, ref, fasta, files = planted
+    c = _caller(fasta, max_depth=20)
+    c.process_bam(files[0])
+    compare_variants(c.prepare_variants(), _oracle(ref, files[:1], max_depth=20).prepare_variants(), RTOL)
+
+
+def test_errors(planted, tmp_path):
+    d, ref, fasta, files = planted
+    c = _caller(fasta)
+    with pytest.raises(OSError):
+        c.process_bam(str(tmp_path / "missing.bam"))
+    other = str(tmp_path / "o.sam")
+    samgen.write_sam(other, [("chrX", 800)], samgen.snv_records("chrX", ref, 5, seed=1))
+    with pytest.raises(ValueError):
+        c.process_bam(other)
