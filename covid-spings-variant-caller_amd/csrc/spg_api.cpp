@@ -282,6 +282,8 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
         }
         HIPCHK(hipMemsetAsync(hb.code + n_entries, 0xFF, pad - n_entries, c->stream));
         HIPCHK(hipMemsetAsync(hb.qual + n_entries, 0, pad - n_entries, c->stream));
+        // host buffers may be pageable and are the caller's again on return
+        if (!dev) HIPCHK(hipStreamSynchronize(c->stream));
     }
     if (!dev) {
         for (uint64_t i = 0; i < n_entries; i++)

@@ -21,11 +21,15 @@ def _ref(L, seed):
     return synth.reference(L, seed=seed)
 
 
+SAMS = {}
+
+
 def _oracle(ref, files, contig="chrS", minbq=30, **pk):
     from oracle import pileup_port as pp
     from oracle.reference_port import OracleCaller
     o = OracleCaller(ref, minbq, 10, 5, 0.10)
     for f in files:
+        f = f[:-4] + ".sam" if f.endswith(".bam") else f
         o.accumulate(*pp.to_csr(pp.pileup_columns(f, contig, **pk)))
     return o
 
@@ -45,12 +49,16 @@ def planted(tmp_path_factory):
     samgen.write_fasta(fasta, [("chrS", ref)])
     snvs = {150: ("T" if ref[150].upper() != "T" else "A", 0.5), 300: ("G" if ref[300] != "G" else "C", 0.3),
             301: ("C" if ref[301] != "C" else "G", 0.9), 555: ("A" if ref[555] != "A" else "T", 0.12)}
-    files = []
+    files, sams = [], []
     for k, (n, fmt) in enumerate([(900, "sam"), (700, "bam")]):
         recs = samgen.snv_records("chrS", ref, n, snvs=snvs, seed=20 + k)
         p = str(d / f"s{k}.{fmt}")
         (samgen.write_sam if fmt == "sam" else samgen.write_bam)(p, [("chrS", L)], recs)
         files.append(p)
+        sams.append(str(d / f"s{k}.sam"))
+        if fmt == "bam":
+            samgen.write_sam(sams[-1], [("chrS", L)], recs)      # the oracle reads SAM text
+    SAMS[tuple(files)] = sams
     return d, ref, fasta, files
 
 
