@@ -18,6 +18,10 @@ namespace spg {
 constexpr int NSLOT = SPG_NSLOT;          // A C G T N
 constexpr uint32_t INF32 = 0xFFFFFFFFu;
 constexpr uint32_t MISC_EXOTIC = 0x100u;  // acc.misc bit: an allele outside A,C,G,T,N was seen
+// acc.misc bits 9..13: slot k's sum of eps is incomplete (the deep kernel skips it for a column's
+// major allele when that allele is the REF char — never a candidate, so QUAL is never needed; a
+// position where such a slot does become a candidate is resolved by the exact replay)
+constexpr int MISC_SE_SKIP_SHIFT = 9;
 
 // Accumulators replacing Site (structs.py:2-6).  The q lists are replaced by sufficient
 // statistics: counts, the integer sum of q (log10 of the eps product up to fp64 rounding), the sum

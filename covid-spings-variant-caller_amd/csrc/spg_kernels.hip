@@ -220,13 +220,14 @@ struct __align__(8) WaveRare {
     double sl[NSLOT], se[NSLOT];
     uint32_t depth, n_del, n_skip, n_other;
     uint32_t cnt[NSLOT], sq[NSLOT], qf[NSLOT], first[NSLOT];
+    uint32_t se_skip, pad;
 };
-static_assert(sizeof(WaveRare) == 176, "WaveRare");
+static_assert(sizeof(WaveRare) == 184, "WaveRare");
 
 __device__ __forceinline__ void rare_init(WaveRare *R, int lane) {
     uint32_t *w = reinterpret_cast<uint32_t *>(R);
-    // words 0..19 doubles, 20..23 counters, 24..33 cnt/sq: 0; 34..38 qf: 255; 39..43 first: INF
-    if (lane < 44) w[lane] = lane < 34 ? 0u : (lane < 39 ? 255u : INF32);
+    // words 0..19 doubles, 20..23 counters, 24..33 cnt/sq: 0; 34..38 qf: 255; 39..43 first: INF; 44 se_skip
+    if (lane < 45) w[lane] = lane < 34 ? 0u : (lane < 39 ? 255u : (lane < 44 ? INF32 : 0u));
 }
 
 __device__ __forceinline__ void rare_entry(WaveRare *R, uint32_t code, uint32_t q, uint32_t idx,
@@ -240,7 +241,7 @@ __device__ __forceinline__ void rare_entry(WaveRare *R, uint32_t code, uint32_t 
     atomicAdd(&R->sq[sl], q);
     atomicMin(&R->qf[sl], q);
     atomicMin(&R->first[sl], idx);
-    const double2 t = lut[q];                          // {ln(1-eps), eps}; row 0 holds {0, 0}
+    const double2 t = lut[q < 128u ? q : q + 128u];    // {ln(1-eps), eps}; row 0 holds {0, 0}
     atomicAdd(&R->sl[sl], t.x);
     atomicAdd(&R->se[sl], q == 0 ? 1.0 : t.y);         // eps(Q0) = 1
 }
@@ -280,6 +281,7 @@ __device__ __forceinline__ void merge_column(Acc *__restrict__ A, const WaveRare
         h0.x += R->depth;                                           // :87
         h1.x += R->n_del; h1.y += R->n_skip; h1.z += R->n_other; h1.w = epoch;
         if (R->n_other) h0.w |= MISC_EXOTIC;
+        h0.w |= R->se_skip << MISC_SE_SKIP_SHIFT;
         const uint32_t have = order_mask(h0.z);
         uint32_t newmask = 0, first[NSLOT];
 #pragma unroll
@@ -315,6 +317,12 @@ __device__ __forceinline__ void merge_column(Acc *__restrict__ A, const WaveRare
     }
 }
 
+struct RareItem {            // one lane's chunk slice (up to 16 entries) holding rare entries
+    uint32_t c[4], q[4];
+    int32_t o;              // column-relative offset of its first entry
+    uint32_t pad[3];
+};
+
 struct Dual2 {              // per-lane partial sums of a wave's second fast allele
     double sl[64], se[64];
     uint32_t cnt[64], sq[64];
@@ -334,13 +342,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     using V = typename Vec<W>::T;
     constexpr uint32_t ALIGN = 4 * W;
     constexpr uint32_t STEP = 64 * ALIGN;               // entries per chunk
-    constexpr uint32_t QCAP = 512;                     // per-wave rare-entry queue (LDS)
-    __shared__ double2 lut[256];
+    constexpr uint32_t QCAP = 64;                      // per-wave queue of lane slices holding rare entries
+    // LUT rows 0..127: {ln(1-eps), eps} for q < 128; rows 128..255: {0, 0} (the fast path's index
+    // for entries that are not fast); rows 256..383: q = 128..255 for the rare path
+    __shared__ double2 lut[384];
     __shared__ WaveRare rare[4];
-    __shared__ uint2 rqueue[4][QCAP];
+    __shared__ RareItem rqueue[4][QCAP];
     __shared__ Dual2 dual2[4];
     write_hist(P);
-    lut[threadIdx.x] = make_double2(T->fast[threadIdx.x][0], T->fast[threadIdx.x][1]);
+    {
+        const uint32_t q = threadIdx.x;
+        lut[q] = q < 128u ? make_double2(T->fast[q][0], T->fast[q][1]) : make_double2(0.0, 0.0);
+        if (q >= 128u) lut[q + 128u] = make_double2(T->fast[q][0], T->fast[q][1]);
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -349,15 +363,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const int ng = (int)min((int64_t)P.G, P.n_cols - g0);
     WaveRare *R = rare + (threadIdx.x >> 6);
     Dual2 *D2 = dual2 + (threadIdx.x >> 6);
-    uint2 *Q = rqueue[threadIdx.x >> 6];
-    uint32_t qn = 0;                                   // queued entries (wave-uniform)
+    RareItem *Q = rqueue[threadIdx.x >> 6];
+    uint32_t qn = 0;                                   // queued lane slices (wave-uniform)
     // drain the queue into the LDS record: every lane takes one entry per round (LDS atomics)
-    auto drain = [&]() {                     // drain the queue into the LDS record (LDS atomics)
+    // Drain: lane k decodes queued slice k (its rare entries are few) into the column's LDS record
+    // with LDS atomics.  Runs at column end (or when the queue is full), so the column's bounds,
+    // major / second allele are the current ones.
+    int32_t bl = 0, el = 0;                    // column bounds relative to its first chunk
+    uint32_t mrep = 0, M = 1;
+    bool dual = false;
+    uint32_t mrep2 = 0, M2 = 0;
+    bool sem = true;                           // accumulate sum(eps) of the major (not when it is REF)
+    auto drain = [&]() {
         wave_sync();
         for (uint32_t b0 = 0; b0 < qn; b0 += 64) {
             if (b0 + lane < qn) {
-                const uint2 e = Q[b0 + lane];
-                rare_entry(R, e.x >> 8, e.x & 0xFFu, e.y, lut);
+                const RareItem *it = Q + b0 + lane;
+                const int32_t o = it->o;
+#pragma unroll 1
+                for (int d = 0; d < W; d++) {          // rolled: one copy of the decode, data stays in LDS
+                    const uint32_t cw = it->c[d], qw = it->q[d];
+                    const uint32_t v = valid80(o + 4 * d, bl, el);
+                    uint32_t f80, r80, g80, r2;
+                    swar4(cw, qw, v, mrep, P.kpass, P.kok, f80, r80);
+                    swar4(cw, qw, v, mrep2, P.kpass, P.kok, g80, r2);   // mrep2 matches nothing unless dual
+                    r80 &= ~g80;
+                    while (r80) {
+                        const int sh = __builtin_ctz(r80) - 7;
+                        r80 &= r80 - 1;
+                        const uint32_t c = (cw >> sh) & 0xFFu, q = (qw >> sh) & 0xFFu;
+                        if ((int)q >= P.min_bq)
+                            rare_entry(R, c, q, (uint32_t)(o + 4 * d - bl) + (uint32_t)(sh >> 3), lut);
+                    }
+                }
             }
         }
         qn = 0;
@@ -406,15 +444,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     // per-column state
     int cj = 0;
     uint32_t cs = 0, cpre = 0, cn = 0;
-    int32_t bl = 0, el = 0;                    // column bounds relative to its first chunk
-    uint32_t mrep = 0, M = 1;
     uint32_t fcnt = 0, fsq = 0, ffirst = INF32;
     double fsl = 0.0, fse = 0.0;
     bool found = false;
-    // second fast allele (dual mode): a frequent minor allele (an SNV, an indel's D entries) would
-    // otherwise push thousands of entries through the rare path and stall its wave
-    bool dual = false;
-    uint32_t mrep2 = 0, M2 = 0;
+    // second fast allele (dual mode, state above): a frequent minor allele (an SNV, an indel's D
+    // entries) would otherwise push thousands of entries through the rare path and stall its wave
     uint32_t ffirst2 = INF32;
     bool found2 = false;
 
@@ -442,6 +476,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             for (int k = 0; k < 7; k++) if (k != b1 && cnt7[k] > c2n) { c2n = cnt7[k]; b2 = k; }
             M = VC[b1];
             mrep = M * 0x01010101u;
+            sem = nibble_char(M) != (uint8_t)__builtin_amdgcn_readlane(refc, cj);
             dual = b2 >= 0;
             M2 = dual ? VC[b2] : 0u;
             mrep2 = dual ? M2 * 0x01010101u : 0xFFFFFFFFu;
@@ -469,8 +504,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                 r80 &= ~g80;
             }
         };
-        auto body = [&](auto full_tag, auto dual_tag) {
+        auto body = [&](auto full_tag, auto dual_tag, auto se_tag) {
             constexpr bool DUAL = decltype(dual_tag)::value;
+            constexpr bool SE = decltype(se_tag)::value;
             uint32_t rany = 0;
             uint32_t fcnt2 = 0, fsq2 = 0;
             double fsl2 = 0.0, fse2 = 0.0;
@@ -482,7 +518,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                 if constexpr (DUAL) {           // the second allele's entries leave the rare set
                     fcnt2 += __popc(g80);
                     fsq2 = __builtin_amdgcn_udot4(qw, g80 >> 7, fsq2, false);
-                    const uint32_t idx2 = qw & (g80 | (g80 - (g80 >> 7)));
+                    const uint32_t idx2 = (qw & 0x7F7F7F7Fu) ^ g80 ^ 0x80808080u;
                     const double2 u0 = lut[idx2 & 0xFFu], u1 = lut[(idx2 >> 8) & 0xFFu];
                     fsl2 += u0.x + u1.x;
                     fse2 += u0.y + u1.y;
@@ -494,11 +530,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                 }
                 fcnt += __popc(f80);
                 fsq = __builtin_amdgcn_udot4(qw, f80 >> 7, fsq, false);
-                const uint32_t idx = qw & (f80 | (f80 - (f80 >> 7)));     // q where fast, 0 elsewhere
-                const double2 t0 = lut[idx & 0xFFu], t1 = lut[(idx >> 8) & 0xFFu];
-                const double2 t2 = lut[(idx >> 16) & 0xFFu], t3 = lut[idx >> 24];
-                fsl += (t0.x + t1.x) + (t2.x + t3.x);
-                fse += (t0.y + t1.y) + (t2.y + t3.y);
+                // fast entries have q < 128: their row is q; every other byte gets bit 7 -> a zero row
+                const uint32_t idx = (qw & 0x7F7F7F7Fu) ^ f80 ^ 0x80808080u;
+                if constexpr (SE) {
+                    const double2 t0 = lut[idx & 0xFFu], t1 = lut[(idx >> 8) & 0xFFu];
+                    const double2 t2 = lut[(idx >> 16) & 0xFFu], t3 = lut[idx >> 24];
+                    fsl += (t0.x + t1.x) + (t2.x + t3.x);
+                    fse += (t0.y + t1.y) + (t2.y + t3.y);
+                } else {                       // REF major: no eps sum, half the LDS traffic
+                    const double t0 = lut[idx & 0xFFu].x, t1 = lut[(idx >> 8) & 0xFFu].x;
+                    const double t2 = lut[(idx >> 16) & 0xFFu].x, t3 = lut[idx >> 24].x;
+                    fsl += (t0 + t1) + (t2 + t3);
+                }
                 rany |= r80;
                 asm volatile("" : "+v"(fsl), "+v"(fse) :: "memory");   // keep each dword's lookups together
             }
@@ -518,63 +561,56 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                     if (f80) mine = (uint32_t)(o + 4 * d - bl) + ((uint32_t)__builtin_ctz(f80) >> 3);
                     if (DUAL && g80) mine2 = (uint32_t)(o + 4 * d - bl) + ((uint32_t)__builtin_ctz(g80) >> 3);
                 }
+                // lanes cover increasing offsets: the first fast entry is the lowest one of the
+                // lowest lane that has any
                 if (!found) {
-                    const uint32_t w = wmin(mine);
-                    if (w != INF32) { ffirst = w; found = true; }
+                    const uint64_t b = __ballot(mine != INF32);
+                    if (b) { ffirst = __builtin_amdgcn_readlane(mine, (int)__builtin_ctzll(b)); found = true; }
                 }
                 if (DUAL && !found2) {
-                    const uint32_t w = wmin(mine2);
-                    if (w != INF32) { ffirst2 = w; found2 = true; }
+                    const uint64_t b = __ballot(mine2 != INF32);
+                    if (b) { ffirst2 = __builtin_amdgcn_readlane(mine2, (int)__builtin_ctzll(b)); found2 = true; }
                 }
             }
-            if (__ballot(rany != 0)) {         // rare entries: append to the wave's LDS queue
-                uint32_t m = 0;
+            if (__ballot(rany != 0)) {         // rare entries: queue this lane slice for the drain
+                const uint64_t bal = __ballot(rany != 0);
+                const uint32_t n = (uint32_t)__popcll(bal);
+                if (qn + n > QCAP) drain();
+                if (rany) {
+                    const uint32_t slot = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                    RareItem &it = Q[slot];
 #pragma unroll
-                for (int d = 0; d < W; d++) {
-                    uint32_t f80, g80, r80;
-                    classify(full_tag, dual_tag, d, f80, g80, r80, true);
-                    const uint32_t t = r80 >> 7;
-                    m |= ((t | (t >> 7) | (t >> 14) | (t >> 21)) & 0xFu) << (4 * d);
-                }
-                while (__ballot(m != 0)) {
-                    const int j = m ? __builtin_ctz(m) : 0;
-                    const int d = j >> 2, sh = (j & 3) * 8;
-                    uint32_t cw = dw<W>(cc, 0), qw = dw<W>(qq, 0);
-#pragma unroll
-                    for (int dd = 1; dd < W; dd++)
-                        if (d == dd) { cw = dw<W>(cc, dd); qw = dw<W>(qq, dd); }
-                    const uint32_t c = (cw >> sh) & 0xFFu, q = (qw >> sh) & 0xFFu;
-                    const bool ok = m != 0 && (int)q >= P.min_bq;
-                    m &= m - 1;
-                    const uint64_t bal = __ballot(ok);
-                    const uint32_t n = (uint32_t)__popcll(bal);
-                    if (qn + n > QCAP) drain();
-                    if (ok) {
-                        const uint32_t slot = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                        Q[slot] = make_uint2((c << 8) | q, (uint32_t)(o + j - bl));
+                    for (int d = 0; d < W; d++) {
+                        it.c[d] = dw<W>(cc, d);
+                        it.q[d] = dw<W>(qq, d);
                     }
-                    qn += n;
+                    it.o = o;
                 }
+                qn += n;
             }
         };
+        using T_ = std::true_type;
+        using F_ = std::false_type;
         if (dual) {
-            if (full) body(std::true_type{}, std::true_type{});
-            else body(std::false_type{}, std::true_type{});
+            if (full) body(T_{}, T_{}, T_{});
+            else body(F_{}, T_{}, T_{});
+        } else if (full) {
+            if (sem) body(T_{}, F_{}, T_{});
+            else body(T_{}, F_{}, F_{});
         } else {
-            if (full) body(std::true_type{}, std::false_type{});
-            else body(std::false_type{}, std::false_type{});
+            body(F_{}, F_{}, T_{});
         }
         if (cs + 1 == cn) {                    // ---- column end ----
             if (qn) drain();
-            const uint32_t fc = wsum(fcnt), fs = wsum(fsq);
-            const double fl = wsumd(fsl), fe = wsumd(fse);
+            const uint32_t fc = dsum_u32(fcnt), fs = dsum_u32(fsq);
+            const double fl = dsum_f64(fsl), fe = dsum_f64(fse);
             uint32_t fc2 = 0, fs2 = 0;
             double fl2 = 0.0, fe2 = 0.0;
             if (dual) {
                 wave_sync();
-                fc2 = wsum(D2->cnt[lane]); fs2 = wsum(D2->sq[lane]);
-                fl2 = wsumd(D2->sl[lane]); fe2 = wsumd(D2->se[lane]);
+                fc2 = dsum_u32(D2->cnt[lane]); fs2 = dsum_u32(D2->sq[lane]);
+                fl2 = dsum_f64(D2->sl[lane]); fe2 = dsum_f64(D2->se[lane]);
             }
             wave_sync();
             if (lane == 0) {
@@ -584,6 +620,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                     R->cnt[Ms] += fc; R->sq[Ms] += fs; R->sl[Ms] += fl; R->se[Ms] += fe;
                     R->qf[Ms] = min(R->qf[Ms], (uint32_t)P.qlo);
                     R->first[Ms] = min(R->first[Ms], ffirst);
+                    if (!sem) R->se_skip |= 1u << Ms;   // full chunks skipped the eps sum
                 }
                 if (fc2) {
                     const int s2 = slot_of(M2);
@@ -826,6 +863,18 @@ __global__ __launch_bounds__(256) void k_finalize(FParams F, const Acc *__restri
         atomicAdd(&O.ctr[F.cslot].n_band, 1u);
         replay_position(F, H, a, T, O, pos);
         return;
+    }
+    // a candidate whose sum of eps was skipped (its allele was REF when accumulated, but the REF
+    // stored at the first visit differs): QUAL comes from the exact replay
+    const uint32_t skip = (a.misc >> MISC_SE_SKIP_SHIFT) & 0x1Fu;
+    if (skip) {
+#pragma unroll
+        for (int k = 0; k < NSLOT; k++)
+            if (k < n && ((skip >> slot[k]) & 1u) && is_candidate(F, a, slot_code((int)slot[k]), cnts[k])) {
+                O.flags[pos] = flags | SPG_F_REPLAYED;
+                replay_position(F, H, a, T, O, pos);
+                return;
+            }
     }
     double S = 0.0;
 #pragma unroll

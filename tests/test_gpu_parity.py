@@ -192,3 +192,29 @@ def test_empty_and_degenerate_batches():
         eng.accumulate(199, np.array([0, 1, 2], np.uint64), np.array([1, 1], np.uint8), np.array([30, 30], np.uint8))
     with pytest.raises(Exception):
         eng.accumulate(0, np.array([0, 1], np.uint64), np.array([18], np.uint8), np.array([30], np.uint8))
+
+
+def test_reference_switch_between_batches_replays_skipped_eps():
+    """Positions are keyed by coordinate only (live_variant_caller.py:77-87): a later batch read
+    against another contig's sequence keeps the REF char of the first visit.  The deep kernel skips
+    the eps sum of a column's major allele when it equals the *current* REF char; when that allele
+    is a candidate against the stored REF, the position must come out of the exact replay."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from oracle.reference_port import OracleCaller
+    L = 400
+    r1 = synth.reference(L, seed=31)
+    r2 = "".join("G" if (i % 7 == 3) else ch for i, ch in enumerate(synth.reference(L, seed=32)))
+    b1 = synth.pileup(L, 40, seed=33, ref=r1, lo=0, hi=L, read_len=50)
+    b2 = synth.pileup(L, 4000, seed=34, ref=r2, lo=60, hi=340, read_len=50)     # deep: k_acc_seg<4>
+    eng = PileupEngine(L, 30, 10, 5, 0.10, device=0, reference=r1)
+    eng.accumulate(*b1)
+    eng.set_reference(r2)
+    eng.accumulate(*b2)
+    eng.finalize()
+    o = OracleCaller(r1, 30, 10, 5, 0.10)
+    o.accumulate(*b1)
+    o.accumulate(*b2)
+    exp = o.prepare_variants()
+    assert len(exp) > 20
+    compare_variants(eng.variants(), exp, RTOL)

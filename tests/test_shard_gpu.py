@@ -27,5 +27,9 @@ def test_sharded_engines_match_single():
             e.accumulate(*b)
     got = shard.merge_candidates([e.local_candidates() for e in engines])
     assert len(exp) > 20
-    for k in exp.dtype.names:
+    for k in ("pos", "dp", "ad", "pl", "score", "ref", "alt", "gl_zero", "rank", "first_batch"):
         np.testing.assert_array_equal(got[k], exp[k], err_msg=k)
+    # fp64 sums: a shard's CSR slice starts at another byte alignment, so entries meet the 16-byte
+    # chunk lanes in another grouping and the sums round differently (parity bar: 1e-9 relative)
+    for k in ("gl", "gl_linear", "qual"):
+        np.testing.assert_allclose(got[k], exp[k], rtol=1e-12, atol=0, err_msg=k)
