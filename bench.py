@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--max-depth", type=int, default=0, help="0 = uncapped; 8000 = pysam parity cap")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-positions", type=int, default=8000)
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end BAM -> calls leg")
+    ap.add_argument("--e2e-threads", type=int, default=16)
     return ap.parse_args()
 
 
@@ -85,6 +87,46 @@ def cpu_baseline(args):
                       f"pysam pileup/BAM decode not included (absent)",
             "c_restatement": {"value": n_c / t_c, "unit": "positions/s", "cores": 1,
                               "sample": f"oracle/spg_oracle.c on {n_c} positions ({int(off2[-1])} entries), {t_c:.2f} s"}}
+
+
+def end_to_end(args, device):
+    """BAM -> host pileup (libspings_pileup: BGZF inflate, htslib-rule pileup, CSR) -> H2D ->
+    accumulate -> finalize -> call table, on one synthetic 10,000x BAM written by the C++ read
+    simulator.  Reported beside `value` (never as it): it includes the host front end and PCIe."""
+    import tempfile
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.pileup import AlignmentFile, PileupParams, simulate_bam
+    ref = synth.reference(L_SARS, seed=1)
+    d = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
+    bam = os.path.join(d, "sars_e2e.bam")
+    t0 = time.perf_counter()
+    n_reads = simulate_bam(bam, "NC_045512.2", ref, depth=args.depth, seed=5, n_threads=args.e2e_threads)
+    t_sim = time.perf_counter() - t0
+    eng = PileupEngine(L_SARS, 30, 10, 5, 0.10, device=device, reference=ref)
+    res = {}
+    for cap, tag in ((8000, "parity_mode_max_depth_8000"), (0, "uncapped")):
+        eng.reset()
+        t0 = time.perf_counter()
+        with AlignmentFile(bam) as f:
+            b = f.pileup_batch("NC_045512.2", PileupParams(max_depth=cap, n_threads=args.e2e_threads))
+        t1 = time.perf_counter()
+        eng.accumulate(b.pos_begin, b.offsets, b.codes, b.quals)
+        eng.finalize()
+        n_calls = len(eng.candidates())
+        t2 = time.perf_counter()
+        res[tag] = {"positions_per_s": L_SARS / (t2 - t0), "host_pileup_s": t1 - t0, "h2d_gpu_s": t2 - t1,
+                    "entries": int(b.n_entries), "reads_used": int(b.n_reads_used), "calls": n_calls,
+                    "pcie_inclusive_gpu_positions_per_s": L_SARS / (t2 - t1)}
+        b.close()
+    eng.close()
+    res["bam_bytes"] = os.path.getsize(bam)
+    res["reads"] = n_reads
+    res["simulate_s"] = t_sim
+    res["host_threads"] = args.e2e_threads
+    os.remove(bam)
+    os.rmdir(d)
+    return res
 
 
 def pmc_traffic(E):
@@ -186,6 +228,8 @@ def main():
                      "kernel": "k_acc_seg<4,true> (spg_accumulate)", "kernel_ms": t_acc * 1e3, "algorithmic_bytes": algo_bytes},
         "finalize_ms": t_fin * 1e3, "candidates_per_gpu_step": n_cand, "datagen_s": t_gen,
     }
+    if rank == 0 and world == 1 and not args.no_e2e:
+        res["end_to_end"] = end_to_end(args, 0)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args)
         res["cpu_baseline"]["cores_available"] = len(os.sched_getaffinity(0))

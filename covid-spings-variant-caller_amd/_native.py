@@ -126,6 +126,13 @@ class SppParams(C.Structure):
                 ("reserved", C.c_int64 * 2)]
 
 
+class SimParams(C.Structure):
+    _fields_ = [("depth", C.c_double), ("read_len", C.c_int32), ("snv_every", C.c_int32), ("q_mean", C.c_double),
+                ("q_sd", C.c_double), ("q_min", C.c_int32), ("q_max", C.c_int32), ("del_frac", C.c_double),
+                ("ins_frac", C.c_double), ("n_rate", C.c_double), ("seed", C.c_uint64), ("n_threads", C.c_int32),
+                ("level", C.c_int32), ("reserved", C.c_int64 * 2)]
+
+
 def pileup_lib():
     """Load libspings_pileup.so (host-only; raises if it has not been built)."""
     global _pileup
@@ -147,6 +154,9 @@ def pileup_lib():
          C.POINTER(i64), C.POINTER(i64))
     _sig(L.spp_batch_arrays, C.c_int, vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp))
     _sig(L.spp_batch_free, C.c_int, vp)
+    _sig(L.spp_default_sim_params, None, C.POINTER(SimParams))
+    _sig(L.spp_simulate_bam, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, i64, C.POINTER(SimParams),
+         C.POINTER(i64))
     _pileup = L
     return L
 

@@ -20,6 +20,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <queue>
+#include <random>
+#include <cmath>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -621,6 +623,79 @@ void fill_csr(const Reads &R, const std::vector<uint8_t> &keep, const Tweaks &T,
     for (auto &t : pool) t.join();
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Read simulator -> BGZF BAM
+// ---------------------------------------------------------------------------------------------
+class BgzfWriter {
+  public:
+    BgzfWriter(const std::string &path, int threads, int level) : threads_(std::max(1, threads)), level_(level) {
+        f_ = fopen(path.c_str(), "wb");
+        if (!f_) throw std::runtime_error("cannot create " + path);
+    }
+    ~BgzfWriter() {
+        if (f_) fclose(f_);
+    }
+    void write(const void *p, size_t n) {
+        const uint8_t *b = (const uint8_t *)p;
+        buf_.insert(buf_.end(), b, b + n);
+        if (buf_.size() >= kFlush) flush(false);
+    }
+    void close() {
+        flush(true);
+        static const uint8_t eof[28] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0, 27, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        fwrite(eof, 1, 28, f_);
+        fclose(f_);
+        f_ = nullptr;
+    }
+
+  private:
+    static constexpr size_t kBlock = 65280, kFlush = 64u << 20;
+    void flush(bool all) {
+        const size_t nb = all ? (buf_.size() + kBlock - 1) / kBlock : buf_.size() / kBlock;
+        if (!nb) return;
+        std::vector<std::vector<uint8_t>> out(nb);
+        std::atomic<size_t> next{0};
+        std::atomic<bool> bad{false};
+        auto work = [&]() {
+            for (size_t i; (i = next++) < nb;) {
+                const size_t off = i * kBlock, len = std::min(kBlock, buf_.size() - off);
+                z_stream zs;
+                memset(&zs, 0, sizeof(zs));
+                if (deflateInit2(&zs, level_, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) { bad = true; return; }
+                std::vector<uint8_t> &o = out[i];
+                o.resize(18 + deflateBound(&zs, len) + 8);
+                zs.next_in = buf_.data() + off;
+                zs.avail_in = (uInt)len;
+                zs.next_out = o.data() + 18;
+                zs.avail_out = (uInt)(o.size() - 26);
+                if (deflate(&zs, Z_FINISH) != Z_STREAM_END) bad = true;
+                const size_t clen = zs.total_out;
+                deflateEnd(&zs);
+                const size_t bsize = clen + 26;
+                const uint8_t hdr[18] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0,
+                                         (uint8_t)((bsize - 1) & 0xFF), (uint8_t)((bsize - 1) >> 8)};
+                memcpy(o.data(), hdr, 18);
+                const uint32_t crc = (uint32_t)crc32(0, buf_.data() + off, (uInt)len), isz = (uint32_t)len;
+                memcpy(o.data() + 18 + clen, &crc, 4);
+                memcpy(o.data() + 22 + clen, &isz, 4);
+                o.resize(bsize);
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < threads_; t++) pool.emplace_back(work);
+        work();
+        for (auto &t : pool) t.join();
+        if (bad) throw std::runtime_error("BGZF deflate failed");
+        for (auto &o : out) fwrite(o.data(), 1, o.size(), f_);
+        const size_t used = std::min(buf_.size(), nb * kBlock);
+        buf_.erase(buf_.begin(), buf_.begin() + (ptrdiff_t)used);
+    }
+    FILE *f_ = nullptr;
+    int threads_, level_;
+    std::vector<uint8_t> buf_;
+};
+
 }  // namespace
 
 extern "C" {
@@ -733,6 +808,175 @@ int spp_batch_arrays(spp_batch *b, const uint64_t **offsets, const uint8_t **bas
 int spp_batch_free(spp_batch *b) {
     delete b;
     return 0;
+}
+
+}  // extern "C"
+
+namespace {
+
+int reg2bin(int64_t beg, int64_t end) {
+    --end;
+    if (beg >> 14 == end >> 14) return (int)(((1 << 15) - 1) / 7 + (beg >> 14));
+    if (beg >> 17 == end >> 17) return (int)(((1 << 12) - 1) / 7 + (beg >> 17));
+    if (beg >> 20 == end >> 20) return (int)(((1 << 9) - 1) / 7 + (beg >> 20));
+    if (beg >> 23 == end >> 23) return (int)(((1 << 6) - 1) / 7 + (beg >> 23));
+    if (beg >> 26 == end >> 26) return (int)(((1 << 3) - 1) / 7 + (beg >> 26));
+    return 0;
+}
+
+// One chunk of reads (consecutive in sorted order) -> BAM records; its own RNG stream, so the
+// output does not depend on the thread count.
+void sim_chunk(const spp_sim_params &p, const char *ref, int64_t L, const std::vector<int64_t> &starts, size_t r0,
+               size_t r1, uint64_t seed, std::vector<uint8_t> &out) {
+    std::mt19937_64 rng(seed);
+    std::uniform_real_distribution<double> U(0.0, 1.0);
+    std::normal_distribution<double> Nq(p.q_mean, p.q_sd);
+    static const char ACGT[4] = {'A', 'C', 'G', 'T'};
+    auto idx_of = [](char c) { c = (char)toupper(c); return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : -1; };
+    const int R = p.read_len;
+    std::vector<char> seq((size_t)R + 8);
+    std::vector<uint8_t> qual((size_t)R + 8);
+    for (size_t r = r0; r < r1; r++) {
+        int64_t pos = starts[r];
+        const double u = U(rng);
+        int kind = u < p.del_frac ? 1 : (u < p.del_frac + p.ins_frac ? 2 : 0);
+        if (R < 74) kind = 0;
+        if (kind == 1 && pos + R + 2 > L) kind = 0;
+        uint32_t cig[3];
+        int ncig = 1;
+        if (kind == 0) cig[0] = (uint32_t)R << 4 | C_M;
+        else if (kind == 1) { cig[0] = 70u << 4 | C_M; cig[1] = 2u << 4 | C_D; cig[2] = (uint32_t)(R - 70) << 4 | C_M; ncig = 3; }
+        else { cig[0] = 70u << 4 | C_M; cig[1] = 2u << 4 | C_I; cig[2] = (uint32_t)(R - 72) << 4 | C_M; ncig = 3; }
+        // query bases
+        int y = 0;
+        int64_t x = pos;
+        for (int k = 0; k < ncig; k++) {
+            const uint32_t op = cig[k] & 0xF, l = cig[k] >> 4;
+            for (uint32_t j = 0; j < l; j++) {
+                if (op == C_D) { x++; continue; }
+                char b;
+                if (op == C_I) b = ACGT[rng() & 3];
+                else {
+                    b = (char)toupper(ref[x]);
+                    if (p.snv_every > 0 && x % p.snv_every == p.snv_every / 2) {
+                        static const double afs[4] = {1.0, 0.5, 0.2, 0.05};
+                        const int bi = idx_of(b);
+                        if (bi >= 0 && U(rng) < afs[(x / p.snv_every) % 4]) b = ACGT[(bi + 1 + (int)(x % 3)) % 4];
+                    }
+                    x++;
+                }
+                int q = (int)std::lround(Nq(rng));
+                q = std::min(std::max(q, p.q_min), p.q_max);
+                const int bi = idx_of(b);
+                if (bi >= 0 && U(rng) < std::pow(10.0, -q / 10.0)) b = ACGT[(bi + 1 + (int)(rng() % 3)) % 4];
+                if (U(rng) < p.n_rate) b = 'N';
+                seq[(size_t)y] = b;
+                qual[(size_t)y] = (uint8_t)q;
+                y++;
+            }
+        }
+        const int64_t end = x;
+        char name[32];
+        const int ln = snprintf(name, sizeof(name), "r%zu", r) + 1;
+        const int lseq = y;
+        const uint32_t bs = 32 + (uint32_t)ln + 4u * (uint32_t)ncig + (uint32_t)((lseq + 1) / 2) + (uint32_t)lseq;
+        const size_t o = out.size();
+        out.resize(o + 4 + bs);
+        uint8_t *b = out.data() + o;
+        auto w32 = [&](size_t at, uint32_t v) { memcpy(b + at, &v, 4); };
+        auto w16 = [&](size_t at, uint16_t v) { memcpy(b + at, &v, 2); };
+        w32(0, bs);
+        w32(4, 0);                                     // refID
+        w32(8, (uint32_t)pos);
+        b[12] = (uint8_t)ln;
+        b[13] = 60;                                    // MAPQ
+        w16(14, (uint16_t)reg2bin(pos, std::max(end, pos + 1)));
+        w16(16, (uint16_t)ncig);
+        w16(18, 0);                                    // flag
+        w32(20, (uint32_t)lseq);
+        w32(24, 0xFFFFFFFFu);                          // next refID
+        w32(28, 0xFFFFFFFFu);                          // next pos
+        w32(32, 0);                                    // tlen
+        memcpy(b + 36, name, (size_t)ln);
+        size_t at = 36 + (size_t)ln;
+        for (int k = 0; k < ncig; k++, at += 4) w32(at, cig[k]);
+        for (int i = 0; i < lseq; i += 2) {
+            const uint8_t hi = NT16.t[(uint8_t)seq[(size_t)i]], lo = i + 1 < lseq ? NT16.t[(uint8_t)seq[(size_t)i + 1]] : 0;
+            b[at++] = (uint8_t)(hi << 4 | lo);
+        }
+        memcpy(b + at, qual.data(), (size_t)lseq);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+void spp_default_sim_params(spp_sim_params *p) {
+    memset(p, 0, sizeof(*p));
+    p->depth = 1000.0;
+    p->read_len = 150;
+    p->snv_every = 997;
+    p->q_mean = 33.0;
+    p->q_sd = 6.0;
+    p->q_min = 2;
+    p->q_max = 41;
+    p->del_frac = 0.01;
+    p->ins_frac = 0.01;
+    p->n_rate = 1e-4;
+    p->seed = 2;
+    p->n_threads = 8;
+    p->level = 1;
+}
+
+int spp_simulate_bam(const char *path, const char *contig, const char *ref_seq, int64_t ref_len,
+                     const spp_sim_params *p, int64_t *n_reads_out) {
+    if (!path || !contig || !ref_seq || !p) return fail("spp_simulate_bam: null argument");
+    if (ref_len < p->read_len + 4 || p->read_len < 1) return fail("spp_simulate_bam: reference shorter than a read");
+    try {
+        const int64_t L = ref_len;
+        const int64_t n = (int64_t)std::llround(p->depth * (double)L / p->read_len);
+        std::vector<int64_t> starts((size_t)n);
+        {
+            std::mt19937_64 rng(p->seed);
+            std::uniform_int_distribution<int64_t> S(0, L - p->read_len);
+            for (auto &s : starts) s = S(rng);
+            std::sort(starts.begin(), starts.end());
+        }
+        BgzfWriter w(path, p->n_threads, p->level);
+        const std::string text = std::string("@HD\tVN:1.6\tSO:coordinate\n@SQ\tSN:") + contig + "\tLN:" +
+                                 std::to_string(L) + "\n";
+        std::vector<uint8_t> hdr;
+        auto put32 = [&](uint32_t v) { const uint8_t *q = (const uint8_t *)&v; hdr.insert(hdr.end(), q, q + 4); };
+        hdr.insert(hdr.end(), {'B', 'A', 'M', 1});
+        put32((uint32_t)text.size());
+        hdr.insert(hdr.end(), text.begin(), text.end());
+        put32(1);
+        put32((uint32_t)strlen(contig) + 1);
+        hdr.insert(hdr.end(), contig, contig + strlen(contig) + 1);
+        put32((uint32_t)L);
+        w.write(hdr.data(), hdr.size());
+        const size_t chunk = 1 << 16;
+        const size_t nchunks = ((size_t)n + chunk - 1) / chunk;
+        const int nt = std::max(1, p->n_threads);
+        for (size_t c0 = 0; c0 < nchunks; c0 += (size_t)nt) {         // nt chunks in parallel, written in order
+            const size_t c1 = std::min(nchunks, c0 + (size_t)nt);
+            std::vector<std::vector<uint8_t>> bufs(c1 - c0);
+            std::vector<std::thread> pool;
+            for (size_t c = c0; c < c1; c++)
+                pool.emplace_back([&, c]() {
+                    sim_chunk(*p, ref_seq, L, starts, c * chunk, std::min((size_t)n, (c + 1) * chunk),
+                              p->seed * 1000003ull + c, bufs[c - c0]);
+                });
+            for (auto &t : pool) t.join();
+            for (auto &b : bufs) w.write(b.data(), b.size());
+        }
+        w.close();
+        if (n_reads_out) *n_reads_out = n;
+        return 0;
+    } catch (const std::exception &e) {
+        return fail(std::string("spp_simulate_bam: ") + e.what());
+    }
 }
 
 }  // extern "C"

@@ -120,3 +120,20 @@ class AlignmentFile:
             self.close()
         except Exception:
             pass
+
+
+def simulate_bam(path: str, contig: str, reference: str, depth: float, seed: int = 2, n_threads: int = 8,
+                 **kw) -> int:
+    """Write a synthetic coordinate-sorted BAM (include/spings_pileup.h spp_simulate_bam; SURVEY §8 d
+    read model).  Extra keywords override spp_sim_params fields.  Returns the number of reads."""
+    L = N.pileup_lib()
+    p = N.SimParams()
+    L.spp_default_sim_params(C.byref(p))
+    p.depth, p.seed, p.n_threads = float(depth), int(seed), int(n_threads)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    n = C.c_int64()
+    ref = reference.encode()
+    N.pcheck(L.spp_simulate_bam(str(path).encode(), contig.encode(), ref, len(ref), C.byref(p), C.byref(n)),
+             "spp_simulate_bam")
+    return n.value

@@ -69,6 +69,29 @@ int spp_batch_info(spp_batch *b, int64_t *pos_begin, int64_t *n_cols, uint64_t *
 int spp_batch_arrays(spp_batch *b, const uint64_t **offsets, const uint8_t **base_code, const uint8_t **qual);
 int spp_batch_free(spp_batch *b);
 
+/* Synthetic read simulator (SURVEY.md §8 d "Synthetic inputs"): writes a coordinate-sorted BGZF
+ * BAM of single-end reads (flag 0, MAPQ 60) over one contig — starts uniform on [0, L-read_len],
+ * CIGAR read_len M (a del_frac share "70M2D..M", an ins_frac share "70M2I..M"), q =
+ * clip(round(N(q_mean, q_sd)), q_min, q_max), a sequencing error replaces the base with a uniform
+ * other base with probability eps(q), N with probability n_rate, planted SNVs every snv_every-th
+ * position (offset snv_every/2) with allele fractions cycling {1.0, 0.5, 0.2, 0.05}.  Seeded. */
+typedef struct {
+    double depth;          /* mean coverage */
+    int32_t read_len;      /* 150 */
+    int32_t snv_every;     /* 997; 0 = none */
+    double q_mean, q_sd;   /* 33, 6 */
+    int32_t q_min, q_max;  /* 2, 41 */
+    double del_frac, ins_frac, n_rate;   /* 0.01, 0.01, 1e-4 */
+    uint64_t seed;
+    int32_t n_threads;     /* BGZF deflate threads */
+    int32_t level;         /* zlib level (1 = fast) */
+    int64_t reserved[2];
+} spp_sim_params;
+
+void spp_default_sim_params(spp_sim_params *p);
+int spp_simulate_bam(const char *path, const char *contig, const char *ref_seq, int64_t ref_len,
+                     const spp_sim_params *p, int64_t *n_reads_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -203,3 +203,38 @@ def write_fasta(path, seqs, width=60):
             f.write(f">{name} synthetic\n")
             for i in range(0, len(s), width):
                 f.write(s[i:i + width] + "\n")
+
+
+def read_bam_as_sam(bam_path, sam_path):
+    """BAM -> SAM text (test helper: lets the SAM-only Python oracle read simulator output)."""
+    import gzip
+    data = gzip.open(bam_path, "rb").read()
+    assert data[:4] == b"BAM\1"
+    l_text = struct.unpack_from("<i", data, 4)[0]
+    p = 8 + l_text
+    n_ref = struct.unpack_from("<i", data, p)[0]
+    p += 4
+    targets = []
+    for _ in range(n_ref):
+        ln = struct.unpack_from("<i", data, p)[0]
+        name = data[p + 4:p + 4 + ln - 1].decode()
+        targets.append((name, struct.unpack_from("<i", data, p + 4 + ln)[0]))
+        p += 8 + ln
+    recs = []
+    while p < len(data):
+        bs = struct.unpack_from("<i", data, p)[0]
+        b = data[p + 4:p + 4 + bs]
+        p += 4 + bs
+        tid, pos, l_name, mapq, _bin, n_cig, flag, l_seq, mt, mp, tlen = struct.unpack_from("<iiBBHHHiiii", b, 0)
+        name = b[32:32 + l_name - 1].decode()
+        o = 32 + l_name
+        cig = "".join(f"{c >> 4}{OPS[c & 15]}" for c in struct.unpack_from(f"<{n_cig}I", b, o)) or "*"
+        o += 4 * n_cig
+        seq = "".join(NT16[(b[o + i // 2] >> (4 if i % 2 == 0 else 0)) & 15] for i in range(l_seq))
+        o += (l_seq + 1) // 2
+        qual = "".join(chr(33 + min(q, 93)) for q in b[o:o + l_seq])
+        recs.append(dict(qname=name, flag=flag, rname=targets[tid][0], pos=pos + 1, mapq=mapq, cigar=cig,
+                         rnext="*" if mt < 0 else ("=" if mt == tid else targets[mt][0]), pnext=mp + 1, tlen=tlen,
+                         seq=seq or "*", qual=qual or "*"))
+    write_sam(sam_path, targets, recs)
+    return targets, recs
