@@ -78,6 +78,7 @@ def gpu_lib():
     _sig(L.spg_accumulate_ex, i32, vp, i64, i64, vp, vp, vp, u64, C.c_uint32)
     _sig(L.spg_finalize, i32, vp)
     _sig(L.spg_sync, i32, vp)
+    _sig(L.spg_stream, i32, vp, C.POINTER(vp))
     _sig(L.spg_get_table, i32, vp, i64, i64, vp, vp, vp, vp, vp, vp)
     _sig(L.spg_count, i32, vp, C.POINTER(i64), C.POINTER(i64))
     _sig(L.spg_get_candidates, i32, vp, vp, i64, C.POINTER(i64))
@@ -86,6 +87,7 @@ def gpu_lib():
     _sig(L.spg_copy_candidates_device, i32, vp, vp, i64)
     _sig(L.spg_last_kernel_ms, i32, vp, C.POINTER(C.c_float), C.POINTER(C.c_float))
     _sig(L.spg_kernel_times, i32, vp, vp, vp, i64, C.POINTER(i64))
+    _sig(L.spg_set_timing, i32, vp, i32)
     _sig(L.spg_history_count, i32, vp, C.POINTER(i64))
     _sig(L.spg_history_info, i32, vp, i64, C.POINTER(i64), C.POINTER(i64), C.POINTER(u64))
     _sig(L.spg_history_copy, i32, vp, i64, vp, vp, vp)

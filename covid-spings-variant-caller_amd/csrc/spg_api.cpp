@@ -34,6 +34,13 @@ static int fail(const std::string &m) {
         if (e_ != hipSuccess) return fail(std::string(#x) + ": " + hipGetErrorString(e_));              \
     } while (0)
 
+// Timing events: 2 (default) around accumulate and finalize, 1 accumulate only, 0 none.  Each
+// timestamped event costs a few microseconds of GPU idle between launches.
+static int default_timing() {
+    static const int lvl = [] { const char *e = getenv("SPG_TIMING"); return e ? atoi(e) : 2; }();
+    return lvl;
+}
+
 struct HistBatch {
     int64_t pos_begin, n_cols;
     uint64_t n_entries;
@@ -75,9 +82,14 @@ struct spg_ctx {
     static constexpr int NRING = 64;
     hipEvent_t ev[NRING][4] = {};
     int64_t ring_w = 0, ring_r = 0;     // entries [ring_r, ring_w) are complete
+    uint8_t ring_tm[NRING] = {};        // bit 0: accumulate events recorded, bit 1: finalize events
     bool acc_open = false, acc_any = false;
     bool last_acc = false, last_fin = false;
+    int timing = default_timing();
+    int acc_timing = 0;                 // level the open / last accumulate interval was recorded at
+    int fin_timing = 0;
 };
+
 
 extern "C" {
 
@@ -323,9 +335,11 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
     P.G = G;
     P.t_deep = deep_batch ? 1u : 128u;
     hipEvent_t *ev = c->ev[c->ring_w % spg_ctx::NRING];
-    if (!c->acc_open) HIPCHK(hipEventRecord(ev[0], c->stream));
+    if (!c->acc_open) c->acc_timing = c->timing;
+    const int tm = c->acc_timing;
+    if (tm >= 1 && !c->acc_open) HIPCHK(hipEventRecord(ev[0], c->stream));
     HIPCHK(launch_accumulate(P, hb.off, hb.code, hb.qual, c->ref, c->tables, c->acc, c->stream));
-    HIPCHK(hipEventRecord(ev[1], c->stream));
+    if (tm >= 1) HIPCHK(hipEventRecord(ev[1], c->stream));
     c->acc_open = true;
     c->acc_any = true;
     c->finalized = false;
@@ -368,18 +382,29 @@ int spg_finalize(spg_ctx *c) {
     c->cslot ^= 1u;            // this call counts in slot cslot (zeroed by the previous call / creation)
     hipEvent_t *ev = c->ev[c->ring_w % spg_ctx::NRING];
     if (!c->acc_open) {        // no accumulate since the last finalize: empty accumulate interval
-        HIPCHK(hipEventRecord(ev[0], c->stream));
-        HIPCHK(hipEventRecord(ev[1], c->stream));
+        c->acc_timing = c->timing;
+        if (c->acc_timing >= 1) {
+            HIPCHK(hipEventRecord(ev[0], c->stream));
+            HIPCHK(hipEventRecord(ev[1], c->stream));
+        }
     }
-    HIPCHK(hipEventRecord(ev[2], c->stream));
+    const int ft = c->timing;
+    if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
     HIPCHK(launch_finalize(make_fparams(c), c->acc, c->tables, make_out(c), c->d_hist, c->stream));
-    HIPCHK(hipEventRecord(ev[3], c->stream));
-    c->last_acc = c->acc_open;
-    c->last_fin = true;
+    if (ft >= 2) HIPCHK(hipEventRecord(ev[3], c->stream));
+    c->last_acc = c->acc_open && c->acc_timing >= 1;
+    c->last_fin = ft >= 2;
+    c->ring_tm[c->ring_w % spg_ctx::NRING] = (c->last_acc ? 1 : 0) | (c->last_fin ? 2 : 0);
     c->acc_open = false;
     c->ring_w++;
     if (c->ring_w - c->ring_r > spg_ctx::NRING) c->ring_r = c->ring_w - spg_ctx::NRING;
     c->finalized = true;
+    return 0;
+}
+
+int spg_stream(spg_ctx *c, void **stream) {
+    if (!c || !stream) return fail("spg_stream: null argument");
+    *stream = (void *)c->stream;
     return 0;
 }
 
@@ -488,7 +513,6 @@ int spg_copy_candidates_device(spg_ctx *c, void *dst, int64_t cap) {
     HIPCHK(hipMemcpyAsync(dst, &c->ctr[c->cslot].n_cand, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
     const int64_t n = std::min<int64_t>(cap, c->cand_cap);
     if (n) HIPCHK(hipMemcpyAsync((char *)dst + 8, c->cand, sizeof(spg_candidate) * n, hipMemcpyDeviceToDevice, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
 
@@ -499,7 +523,7 @@ int spg_last_kernel_ms(spg_ctx *c, float *acc_ms, float *fin_ms) {
     if (acc_ms) *acc_ms = 0.f;
     if (fin_ms) *fin_ms = 0.f;
     if (c->acc_open) {         // accumulates since the last finalize
-        if (acc_ms) HIPCHK(hipEventElapsedTime(acc_ms, c->ev[c->ring_w % spg_ctx::NRING][0],
+        if (acc_ms && c->acc_timing >= 1) HIPCHK(hipEventElapsedTime(acc_ms, c->ev[c->ring_w % spg_ctx::NRING][0],
                                                c->ev[c->ring_w % spg_ctx::NRING][1]));
         return 0;
     }
@@ -510,6 +534,13 @@ int spg_last_kernel_ms(spg_ctx *c, float *acc_ms, float *fin_ms) {
     return 0;
 }
 
+int spg_set_timing(spg_ctx *c, int level) {
+    if (!c) return fail("spg_set_timing: null ctx");
+    if (level < 0 || level > 2) return fail("spg_set_timing: level must be 0, 1 or 2");
+    c->timing = level;
+    return 0;
+}
+
 int spg_kernel_times(spg_ctx *c, float *acc_ms, float *fin_ms, int64_t cap, int64_t *n_out) {
     if (!c || !n_out) return fail("spg_kernel_times: null argument");
     HIPCHK(hipSetDevice(c->device));
@@ -517,8 +548,15 @@ int spg_kernel_times(spg_ctx *c, float *acc_ms, float *fin_ms, int64_t cap, int6
     int64_t n = 0;
     for (int64_t i = c->ring_r; i < c->ring_w && n < cap; i++, n++) {
         hipEvent_t *ev = c->ev[i % spg_ctx::NRING];
-        if (acc_ms) HIPCHK(hipEventElapsedTime(acc_ms + n, ev[0], ev[1]));
-        if (fin_ms) HIPCHK(hipEventElapsedTime(fin_ms + n, ev[2], ev[3]));
+        const uint8_t tm = c->ring_tm[i % spg_ctx::NRING];
+        if (acc_ms) {
+            acc_ms[n] = 0.f;
+            if (tm & 1) HIPCHK(hipEventElapsedTime(acc_ms + n, ev[0], ev[1]));
+        }
+        if (fin_ms) {
+            fin_ms[n] = 0.f;
+            if (tm & 2) HIPCHK(hipEventElapsedTime(fin_ms + n, ev[2], ev[3]));
+        }
     }
     c->ring_r += n;
     *n_out = n;

@@ -46,6 +46,7 @@ class PileupEngine:
     # -- lifecycle --------------------------------------------------------------------------
     def close(self):
         with self._lock:
+            self._ext = None
             if getattr(self, "_h", None):
                 self._L.spg_destroy(self._h)
                 self._h = None
@@ -92,7 +93,9 @@ class PileupEngine:
                         raise ValueError("device inputs must be contiguous tensors on the engine's device")
                 if offsets.dtype not in (torch.int64, torch.uint64) or codes.dtype != torch.uint8 or quals.dtype != torch.uint8:
                     raise ValueError("device inputs: offsets int64, codes/quals uint8")
-                torch.cuda.current_stream(self.device).synchronize()
+                # order the engine's stream after the producer's work on torch's current stream
+                # (a device-side wait, no host synchronisation)
+                self._torch_stream().wait_stream(torch.cuda.current_stream(self.device))
                 flags = N.SPG_IN_DEVICE | (N.SPG_IN_BORROW if borrow else 0)
                 n_cols = offsets.numel() - 1
                 if n_entries is None:
@@ -103,6 +106,14 @@ class PileupEngine:
                                                   N.ptr(quals), int(n_entries), flags), "spg_accumulate_ex")
                 if borrow:
                     self._borrowed.append((offsets, codes, quals))
+
+    def _torch_stream(self):
+        if getattr(self, "_ext", None) is None:
+            import torch
+            st = C.c_void_p()
+            N.check(self._L.spg_stream(self._h, C.byref(st)), "spg_stream")
+            self._ext = torch.cuda.ExternalStream(st.value, device=torch.device("cuda", self.device))
+        return self._ext
 
     def finalize(self):
         """prepare_variants (:120-231): per-position table + candidates, on device."""
@@ -116,14 +127,22 @@ class PileupEngine:
     def copy_candidates_device(self, dst, cap=None):
         """Call table -> a torch uint8 device tensor (u64 count, then spg_candidate records)."""
         cap = (dst.numel() - 8) // N.CANDIDATE_DTYPE.itemsize if cap is None else cap
+        import torch
         with self._lock:
             N.check(self._L.spg_copy_candidates_device(self._h, N.ptr(dst), int(cap)), "spg_copy_candidates_device")
+            # consumers on torch's current stream (e.g. a torch.distributed gather) wait on the copy
+            torch.cuda.current_stream(self.device).wait_stream(self._torch_stream())
 
     def last_kernel_ms(self):
         a, f = C.c_float(), C.c_float()
         with self._lock:
             N.check(self._L.spg_last_kernel_ms(self._h, C.byref(a), C.byref(f)), "spg_last_kernel_ms")
         return a.value, f.value
+
+    def set_timing(self, level: int):
+        """Timing events recorded from now on: 2 accumulate + finalize, 1 accumulate only, 0 none."""
+        with self._lock:
+            N.check(self._L.spg_set_timing(self._h, int(level)), "spg_set_timing")
 
     def kernel_times(self, cap: int = 64):
         """(accumulate_ms, finalize_ms) arrays of every step finalized since the previous call."""

@@ -131,6 +131,9 @@ int spg_accumulate_ex(spg_ctx *ctx, int64_t pos_begin, int64_t n_cols, const uin
 int spg_finalize(spg_ctx *ctx);
 
 int spg_sync(spg_ctx *ctx);
+/* The context's HIP stream (hipStream_t as void*), so a caller can order its own work against the
+ * engine's without host synchronisation (e.g. torch.cuda.ExternalStream + wait_stream). */
+int spg_stream(spg_ctx *ctx, void **stream);
 
 /* Copy table rows [pos0, pos0+n) to host; any pointer may be NULL.
  *   depth[n] u32; counts[n*8] u32 (A C G T N DEL REFSKIP OTHER); gl[n*5] f64 (A C G T N,
@@ -149,8 +152,8 @@ int spg_get_details(spg_ctx *ctx, spg_detail *out, int64_t cap, int64_t *n_out);
 int spg_device_results(spg_ctx *ctx, void **candidates, void **n_candidates);
 
 /* Device-to-device copy of the call table into caller memory on the ctx device: dst[0..8) gets the
- * candidate count (u64), dst + 8 up to `cap` spg_candidate records; synchronises the ctx stream so
- * another stream (e.g. an RCCL gather) may read dst afterwards. */
+ * candidate count (u64), dst + 8 up to `cap` spg_candidate records.  Enqueued on the ctx stream:
+ * order a consumer on another stream (e.g. an RCCL gather) after it through spg_stream. */
 int spg_copy_candidates_device(spg_ctx *ctx, void *dst, int64_t cap);
 
 /* The accumulated batches (replay history) since the last spg_reset, in accumulate order: the
@@ -166,6 +169,10 @@ int spg_history_copy(spg_ctx *ctx, int64_t i, uint64_t *offsets, uint8_t *base_c
  * spg_kernel_times: every step completed since the previous spg_kernel_times call (at most 64
  * are kept), oldest first, without timing-induced stalls between steps.  Both synchronise. */
 int spg_last_kernel_ms(spg_ctx *ctx, float *accumulate_ms, float *finalize_ms);
+/* Which timing events are recorded from now on: 2 = accumulate + finalize (default, or env
+ * SPG_TIMING), 1 = accumulate only, 0 = none; unrecorded intervals read as 0 ms.  Each event pair
+ * costs a few microseconds of GPU idle time between launches. */
+int spg_set_timing(spg_ctx *ctx, int level);
 int spg_kernel_times(spg_ctx *ctx, float *accumulate_ms, float *finalize_ms, int64_t cap, int64_t *n_out);
 
 /* Introspection for tests. */

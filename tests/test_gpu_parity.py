@@ -218,3 +218,30 @@ def test_reference_switch_between_batches_replays_skipped_eps():
     exp = o.prepare_variants()
     assert len(exp) > 20
     compare_variants(eng.variants(), exp, RTOL)
+
+
+def test_copy_candidates_device_orders_torch_stream():
+    """spg_copy_candidates_device + spg_stream: the call table lands in a torch tensor and torch's
+    stream waits for it without a host sync (the path bench.py's RCCL gather uses)."""
+    import torch
+    from covid_spings_variant_caller_amd import _native as N
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    L = 5000
+    ref = synth.reference(L, seed=8)
+    pb, off, c, q = synth.pileup(L, 400, seed=9, ref=ref, snv_every=53)
+    do, dc, dq = synth.to_device(off, c, q)
+    eng = PileupEngine(L, 30, 10, 5, 0.10, device=0, reference=ref)
+    buf = torch.zeros(8 + 4096 * 56, dtype=torch.uint8, device="cuda:0")
+    for _ in range(3):
+        eng.reset()
+        eng.accumulate(pb, do, dc, dq, borrow=True, n_entries=len(c))
+        eng.finalize()
+        eng.copy_candidates_device(buf)
+        host = buf.cpu().numpy()                     # torch's stream, ordered after the copy
+        n = int(host[:8].view(np.uint64)[0])
+        got = host[8:8 + n * 56].view(N.CANDIDATE_DTYPE)
+        exp = eng.candidates()
+        assert n == len(exp) > 10
+        got = got[np.lexsort((got["rank"], got["pos"], got["first_batch"]))]
+        assert got.tobytes() == exp.tobytes()
