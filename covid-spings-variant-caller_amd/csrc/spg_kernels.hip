@@ -730,13 +730,19 @@ __device__ __forceinline__ bool is_candidate(const FParams &F, const Acc &a, uin
 
 // Exact sequential recomputation of one position over the batch history (rare: subnormal band,
 // IUPAC alleles).  np.prod left folds in BAM order, dict-order chains, exactly as utils.py:16-24.
-__device__ __noinline__ void replay_position(const FParams &F, const Hist *__restrict__ H, const Acc &a,
-                                             const Tables *__restrict__ T, const Out &O, int64_t pos) {
+// Its per-allele tables live in the block's LDS (ReplayWs, one per thread) rather than in scratch:
+// a kernel with a private segment pays for it on every launch.
+struct ReplayWs {
     uint32_t cnt[16], ord[16];
-    double P[16], Hh[16], se[16];
+    double P[16], Hh[16], se[16], G[16];
+};
+
+__device__ __forceinline__ void replay_position(const FParams &F, const Hist *__restrict__ H, const Acc &a,
+                                             const Tables *__restrict__ T, const Out &O, int64_t pos,
+                                             ReplayWs *__restrict__ w) {
     int n = 0;
     uint32_t depth = 0;
-    for (int c = 0; c < 16; c++) { cnt[c] = 0; P[c] = 1.0; Hh[c] = 1.0; se[c] = 0.0; }
+    for (int c = 0; c < 16; c++) { w->cnt[c] = 0; w->P[c] = 1.0; w->Hh[c] = 1.0; w->se[c] = 0.0; }
     for (int b = 0; b < F.n_hist; b++) {
         const Hist h = H[b];
         const int64_t col = pos - h.pos_begin;
@@ -748,31 +754,31 @@ __device__ __noinline__ void replay_position(const FParams &F, const Hist *__res
             depth++;
             if (c >= 16) continue;                         // D / N: depth only
             const double e = T->eps[q];
-            if (cnt[c] == 0) { ord[n++] = c; P[c] = e; Hh[c] = 1.0 - e; }   // np.prod: x0, then *=
-            else { P[c] = P[c] * e; Hh[c] = Hh[c] * (1.0 - e); }
-            cnt[c]++;
-            se[c] += e;
+            if (w->cnt[c] == 0) { w->ord[n++] = c; w->P[c] = e; w->Hh[c] = 1.0 - e; }   // np.prod: x0, then *=
+            else { w->P[c] = w->P[c] * e; w->Hh[c] = w->Hh[c] * (1.0 - e); }
+            w->cnt[c]++;
+            w->se[c] += e;
         }
     }
     const bool evaluated = (int64_t)depth >= (int64_t)F.min_td;
-    double G[16];
     double S = 0.0;
     for (int h = 0; h < n; h++) {
         double non = 1.0;
         for (int j = 0; j < n; j++)
-            if (j != h) non = non * P[ord[j]];
-        G[h] = Hh[ord[h]] * non;
-        S = S + G[h];
+            if (j != h) non = non * w->P[w->ord[j]];
+        w->G[h] = w->Hh[w->ord[h]] * non;
+        S = S + w->G[h];
     }
     if (S == 0) S = 1.0;
     uint8_t flags = O.flags[pos];
     if (evaluated) {
         double *gl = O.gl + pos * NSLOT;
         for (int h = 0; h < n; h++) {
-            const int s = slot_of(ord[h]);
-            if (s >= 0) gl[s] = G[h];
-            if (is_candidate(F, a, ord[h], cnt[ord[h]])) {
-                write_candidate(F, O, pos, a, h, ord[h], cnt[ord[h]], G[h], S, se[ord[h]] / (double)cnt[ord[h]]);
+            const uint32_t c = w->ord[h];
+            const int s = slot_of(c);
+            if (s >= 0) gl[s] = w->G[h];
+            if (is_candidate(F, a, c, w->cnt[c])) {
+                write_candidate(F, O, pos, a, h, c, w->cnt[c], w->G[h], S, w->se[c] / (double)w->cnt[c]);
                 flags |= SPG_F_CANDIDATE;
             }
         }
@@ -781,20 +787,21 @@ __device__ __noinline__ void replay_position(const FParams &F, const Hist *__res
     if (depth != a.depth) atomicOr(&O.ctr[F.cslot].err, 1u);   // history / accumulator mismatch
     const uint32_t at = atomicAdd(&O.ctr[F.cslot].n_detail, 1u);
     if (at < (uint32_t)F.detail_cap) {
-        spg_detail d;
-        d.pos = pos; d.depth = depth; d.n_alleles = (uint8_t)n;
-        d.pad[0] = d.pad[1] = d.pad[2] = 0;
+        spg_detail *d = O.detail + at;
+        d->pos = pos; d->depth = depth; d->n_alleles = (uint8_t)n;
+        d->pad[0] = d->pad[1] = d->pad[2] = 0;
         for (int k = 0; k < 16; k++) {
-            d.code[k] = k < n ? (uint8_t)ord[k] : 0xFF;
-            d.count[k] = k < n ? cnt[ord[k]] : 0;
-            d.gl[k] = (k < n && evaluated) ? G[k] : __builtin_nan("");
+            d->code[k] = k < n ? (uint8_t)w->ord[k] : 0xFF;
+            d->count[k] = k < n ? w->cnt[w->ord[k]] : 0;
+            d->gl[k] = (k < n && evaluated) ? w->G[k] : __builtin_nan("");
         }
-        O.detail[at] = d;
     }
 }
 
-__global__ __launch_bounds__(256) void k_finalize(FParams F, const Acc *__restrict__ acc,
+__global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restrict__ acc,
                                                   const Tables *__restrict__ T, const Hist *__restrict__ H, Out O) {
+    __shared__ ReplayWs ws[64];
+    ReplayWs *my_ws = ws + (threadIdx.x & 63);
     if (blockIdx.x == 0 && threadIdx.x == 0) O.ctr[F.cslot ^ 1u] = Counters{0, 0, 0, 0};   // next call's slot
     const int64_t pos = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (pos >= F.n_pos) return;
@@ -815,86 +822,90 @@ __global__ __launch_bounds__(256) void k_finalize(FParams F, const Acc *__restri
     if (evaluated) flags |= SPG_F_EVALUATED;
     if (a.misc & MISC_EXOTIC) {       // IUPAC / '=' alleles: the exact replay tabulates every allele
         O.flags[pos] = flags | SPG_F_EXOTIC | SPG_F_REPLAYED;
-        replay_position(F, H, a, T, O, pos);
-        return;
+        goto replay;
     }
     if (!evaluated) { O.flags[pos] = flags; return; }
+    {   // normal path; every exit that needs the exact replay jumps past this block
 
-    const int n = (int)(a.order & 7u);
-    uint32_t slot[NSLOT], cnts[NSLOT];
-    LV Pv[NSLOT], Hv[NSLOT];
-    double Qv[NSLOT];
-    // per-allele P (= prod eps, utils.py:19) and H (= prod 1-eps, utils.py:17) in dict order
-#pragma unroll
-    for (int k = 0; k < NSLOT; k++) {
-        slot[k] = (a.order >> (3 + 3 * k)) & 7u;
-        uint32_t c_ = 0, sq = 0, qf = 0; double sl = 0.0, se = 0.0;
-#pragma unroll
-        for (int j = 0; j < NSLOT; j++)
-            if (slot[k] == (uint32_t)j) { c_ = a.cnt[j]; sq = a.sq[j]; qf = a.qf[j]; sl = a.sl[j]; se = a.se[j]; }
-        cnts[k] = c_;
-        Qv[k] = k < n ? se / (double)c_ : 0.0;
-        // P: log10 P = -sum(q)/10 up to (n+2) ulp; exact zero proven when every factor < 1/2
-        if (sq <= 3076u) Pv[k] = lv_normal(T->p10k[sq / 10u] * T->eps[sq % 10u], -(double)sq * LOG2_10_OVER_10);
-        else if (sq >= 3245u && qf >= 4u) Pv[k] = lv_zero();
-        else Pv[k] = lv_band(-1022.0 + 2 * MARGIN);
-        // H: exp(sum ln(1-eps)); exactly 0 when a Q0 entry is present (1 - 1.0 == 0)
-        if (qf == 0u) Hv[k] = lv_zero();
-        else {
-            const double l2 = sl * INV_LN2;
-            Hv[k] = l2 > -1022.0 + MARGIN ? lv_normal(exp(sl), l2) : lv_band(-1022.0 + 2 * MARGIN);
+        const int n = (int)(a.order & 7u);
+        uint32_t slot[NSLOT], cnts[NSLOT];
+        LV Pv[NSLOT], Hv[NSLOT];
+        double Sv[NSLOT];
+        // per-allele P (= prod eps, utils.py:19) and H (= prod 1-eps, utils.py:17) in dict order
+    #pragma unroll
+        for (int k = 0; k < NSLOT; k++) {
+            slot[k] = (a.order >> (3 + 3 * k)) & 7u;
+            cnts[k] = 0; Sv[k] = 0.0; Pv[k] = lv_normal(1.0, 0.0); Hv[k] = lv_normal(1.0, 0.0);
+            if (k >= n) continue;              // only the alleles present (no exp for empty slots)
+            uint32_t c_ = 0, sq = 0, qf = 0; double sl = 0.0, se = 0.0;
+    #pragma unroll
+            for (int j = 0; j < NSLOT; j++)
+                if (slot[k] == (uint32_t)j) { c_ = a.cnt[j]; sq = a.sq[j]; qf = a.qf[j]; sl = a.sl[j]; se = a.se[j]; }
+            cnts[k] = c_;
+            Sv[k] = se;
+            // P: log10 P = -sum(q)/10 up to (n+2) ulp; exact zero proven when every factor < 1/2
+            if (sq <= 3076u) Pv[k] = lv_normal(T->p10k[sq / 10u] * T->eps[sq % 10u], -(double)sq * LOG2_10_OVER_10);
+            else if (sq >= 3245u && qf >= 4u) Pv[k] = lv_zero();
+            else Pv[k] = lv_band(-1022.0 + 2 * MARGIN);
+            // H: exp(sum ln(1-eps)); exactly 0 when a Q0 entry is present (1 - 1.0 == 0)
+            if (qf == 0u) Hv[k] = lv_zero();
+            else {
+                const double l2 = sl * INV_LN2;
+                Hv[k] = l2 > -1022.0 + MARGIN ? lv_normal(exp(sl), l2) : lv_band(-1022.0 + 2 * MARGIN);
+            }
         }
-    }
-    double G[NSLOT];
-    bool band = false;
-#pragma unroll
-    for (int h = 0; h < NSLOT; h++) {
-        // N = ((1.0 * P_a1) * P_a2) ... over a != h in dict order (utils.py:18-22), GL = H * N
-        LV c = lv_normal(1.0, 0.0);
-#pragma unroll
-        for (int j = 0; j < NSLOT; j++)
-            if (j != h && j < n) c = lv_mul(c, Pv[j]);
-        const LV g = lv_mul(Hv[h], c);
-        if (h < n && g.s == 2) band = true;
-        G[h] = g.s == 0 ? g.v : 0.0;
-    }
-    if (band) {
-        O.flags[pos] = flags | SPG_F_REPLAYED;
-        atomicAdd(&O.ctr[F.cslot].n_band, 1u);
-        replay_position(F, H, a, T, O, pos);
+        double G[NSLOT];
+        bool band = false;
+    #pragma unroll
+        for (int h = 0; h < NSLOT; h++) {
+            // N = ((1.0 * P_a1) * P_a2) ... over a != h in dict order (utils.py:18-22), GL = H * N
+            LV c = lv_normal(1.0, 0.0);
+    #pragma unroll
+            for (int j = 0; j < NSLOT; j++)
+                if (j != h && j < n) c = lv_mul(c, Pv[j]);
+            const LV g = lv_mul(Hv[h], c);
+            if (h < n && g.s == 2) band = true;
+            G[h] = g.s == 0 ? g.v : 0.0;
+        }
+        if (band) {
+            O.flags[pos] = flags | SPG_F_REPLAYED;
+            atomicAdd(&O.ctr[F.cslot].n_band, 1u);
+            goto replay;
+        }
+        // a candidate whose sum of eps was skipped (its allele was REF when accumulated, but the REF
+        // stored at the first visit differs): QUAL comes from the exact replay
+        const uint32_t skip = (a.misc >> MISC_SE_SKIP_SHIFT) & 0x1Fu;
+        if (skip) {
+    #pragma unroll
+            for (int k = 0; k < NSLOT; k++)
+                if (k < n && ((skip >> slot[k]) & 1u) && is_candidate(F, a, slot_code((int)slot[k]), cnts[k])) {
+                    O.flags[pos] = flags | SPG_F_REPLAYED;
+                    goto replay;
+                }
+        }
+        double S = 0.0;
+    #pragma unroll
+        for (int k = 0; k < NSLOT; k++)
+            if (k < n) S = S + G[k];                             // :145
+        if (S == 0) S = 1.0;                                     // :146
+    #pragma unroll
+        for (int k = 0; k < NSLOT; k++) {
+            if (k < n) {
+    #pragma unroll
+                for (int j = 0; j < NSLOT; j++)
+                    if (slot[k] == (uint32_t)j) gl[j] = G[k];
+                const uint32_t code = slot_code((int)slot[k]);
+                if (is_candidate(F, a, code, cnts[k])) {
+                    write_candidate(F, O, pos, a, k, code, cnts[k], G[k], S, Sv[k] / (double)cnts[k]);
+                    flags |= SPG_F_CANDIDATE;
+                }
+            }
+        }
+        O.flags[pos] = flags;
         return;
     }
-    // a candidate whose sum of eps was skipped (its allele was REF when accumulated, but the REF
-    // stored at the first visit differs): QUAL comes from the exact replay
-    const uint32_t skip = (a.misc >> MISC_SE_SKIP_SHIFT) & 0x1Fu;
-    if (skip) {
-#pragma unroll
-        for (int k = 0; k < NSLOT; k++)
-            if (k < n && ((skip >> slot[k]) & 1u) && is_candidate(F, a, slot_code((int)slot[k]), cnts[k])) {
-                O.flags[pos] = flags | SPG_F_REPLAYED;
-                replay_position(F, H, a, T, O, pos);
-                return;
-            }
-    }
-    double S = 0.0;
-#pragma unroll
-    for (int k = 0; k < NSLOT; k++)
-        if (k < n) S = S + G[k];                             // :145
-    if (S == 0) S = 1.0;                                     // :146
-#pragma unroll
-    for (int k = 0; k < NSLOT; k++) {
-        if (k < n) {
-#pragma unroll
-            for (int j = 0; j < NSLOT; j++)
-                if (slot[k] == (uint32_t)j) gl[j] = G[k];
-            const uint32_t code = slot_code((int)slot[k]);
-            if (is_candidate(F, a, code, cnts[k])) {
-                write_candidate(F, O, pos, a, k, code, cnts[k], G[k], S, Qv[k]);
-                flags |= SPG_F_CANDIDATE;
-            }
-        }
-    }
-    O.flags[pos] = flags;
+replay:
+    replay_position(F, H, a, T, O, pos, my_ws);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -920,9 +931,8 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
 
 hipError_t launch_finalize(const FParams &F, const Acc *acc, const Tables *T, const Out &O, const Hist *H,
                            hipStream_t st) {
-    static const int bs = [] { const char *e = getenv("SPG_FIN_BLOCK"); return e ? atoi(e) : 64; }();
-    const int64_t blocks = (F.n_pos + bs - 1) / bs;
-    hipLaunchKernelGGL(k_finalize, dim3((unsigned)blocks), dim3(bs), 0, st, F, acc, T, H, O);
+    const int64_t blocks = (F.n_pos + 63) / 64;      // 64-thread blocks: one wave, one ReplayWs per lane
+    hipLaunchKernelGGL(k_finalize, dim3((unsigned)blocks), dim3(64), 0, st, F, acc, T, H, O);
     return hipGetLastError();
 }
 
