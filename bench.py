@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--cpu-positions", type=int, default=8000)
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end BAM -> calls leg")
     ap.add_argument("--e2e-threads", type=int, default=16)
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
+                                                      "gloo only to exercise the path on one GPU)")
     return ap.parse_args()
 
 
@@ -157,11 +159,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.backend != "nccl":                  # functional runs of the N > 1 path on fewer GPUs
+        local = local % max(1, torch.cuda.device_count())
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
 
@@ -173,17 +180,29 @@ def main():
     d_off, d_c, d_q = synth.to_device(off, codes, quals, device=local if world > 1 else 0)
     eng = PileupEngine(C, 30, 10, 5, 0.10, device=local if world > 1 else 0, reference=vref)
 
-    cand_cap = 1 << 14
+    # call-table gather buffer: u64 count + records, sized from a first (untimed) pass so the
+    # per-step gather moves KBs, not the engine's full candidate capacity
+    eng.reset()
+    eng.accumulate(0, d_off, d_c, d_q, borrow=True, n_entries=E)
+    eng.finalize()
+    cand_cap = max(64, 4 * eng.counts()[0])
+    if dist is not None:
+        t = torch.tensor([cand_cap], dtype=torch.int64, device=d_c.device if args.backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        cand_cap = int(t.item())
     gather_buf = torch.zeros(cand_cap * 56 + 8, dtype=torch.uint8, device=d_c.device)
+    gather_out = [torch.empty_like(gather_buf) for _ in range(world)] if rank == 0 else None
 
     def step():
         eng.reset()
         eng.accumulate(0, d_off, d_c, d_q, borrow=True, n_entries=E)
         eng.finalize()
         if dist is not None:
-            eng.copy_candidates_device(gather_buf)
-            out = [torch.empty_like(gather_buf) for _ in range(world)] if rank == 0 else None
-            dist.gather(gather_buf, out, dst=0)
+            eng.copy_candidates_device(gather_buf, cap=cand_cap)
+            if args.backend == "nccl":
+                dist.gather(gather_buf, gather_out, dst=0)           # RCCL over xGMI
+            else:
+                dist.gather(gather_buf.cpu(), [o.cpu() for o in gather_out] if rank == 0 else None, dst=0)
 
     for _ in range(args.warmup):
         step()
@@ -203,7 +222,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=d_c.device)
+        t = torch.tensor([dt], dtype=torch.float64, device=d_c.device if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     acc_ms, _ = eng.kernel_times(max(64, args.steps))   # HIP events of the timed steps (last <= 64)
@@ -213,6 +232,11 @@ def main():
     eng.sync()
     _, fin_ms = eng.kernel_times()
     n_cand = eng.counts()[0]
+    gathered = None
+    if dist is not None and rank == 0:
+        gathered = [int(o[:8].cpu().numpy().view(np.uint64)[0]) for o in gather_out]
+        if max(gathered) > cand_cap:
+            raise RuntimeError(f"call table larger than the gather buffer ({max(gathered)} > {cand_cap})")
     positions_per_step = world * L_SARS
     value = positions_per_step * args.steps / dt
     t_acc = float(np.mean(acc_ms)) * 1e-3
@@ -233,6 +257,7 @@ def main():
                      "frac": achieved / PEAK_HBM, "traffic": pmc_traffic(E),
                      "kernel": "k_acc_seg<4,true> (spg_accumulate)", "kernel_ms": t_acc * 1e3, "algorithmic_bytes": algo_bytes},
         "finalize_ms": t_fin * 1e3, "candidates_per_gpu_step": n_cand, "datagen_s": t_gen,
+        "calls_gathered_per_step": sum(gathered) if gathered is not None else n_cand,
     }
     if rank == 0 and world == 1 and not args.no_e2e:
         res["end_to_end"] = end_to_end(args, 0)
