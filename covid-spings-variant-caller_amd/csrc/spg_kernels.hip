@@ -269,6 +269,39 @@ __device__ __forceinline__ void write_hist(const KParams &P) {
 // Merge the column record R (LDS) into its Acc.  Cooperative: lane 0 writes the header and the dict
 // order, lanes 1..5 one allele slot each.  FRESH (first batch since reset): every record belongs to
 // an older epoch, so nothing is read back — the merge is pure stores.
+// FRESH merge: the record is assembled in LDS and written as ten 16-byte stores (one per lane), so
+// each column costs exactly its 160 bytes of HBM writes instead of a scatter of partial lines.
+__device__ __forceinline__ void merge_fresh(Acc *__restrict__ A, const WaveRare *R, Acc *img, uint32_t batch_seq,
+                                            uint32_t epoch, uint8_t refc, int lane) {
+    if (lane == 0) {
+        uint32_t newmask = 0, first[NSLOT];
+#pragma unroll
+        for (int k = 0; k < NSLOT; k++) {
+            first[k] = R->first[k];
+            if (R->cnt[k]) newmask |= 1u << k;
+        }
+        img->depth = R->depth;
+        img->first_batch = batch_seq;                                // first visit (:77-85)
+        img->order = merge_order(0u, newmask, first);
+        img->misc = refc | (R->n_other ? MISC_EXOTIC : 0u) | (R->se_skip << MISC_SE_SKIP_SHIFT);
+        img->n_del = R->n_del;
+        img->n_skip = R->n_skip;
+        img->n_other = R->n_other;
+        img->epoch = epoch;
+    }
+    if (lane < NSLOT) {
+        const int k = lane;
+        const uint32_t c = R->cnt[k];
+        img->cnt[k] = c;
+        img->sq[k] = c ? (R->sq[k] > 0x80000000u ? 0x80000000u : R->sq[k]) : 0u;
+        img->sl[k] = c ? R->sl[k] : 0.0;
+        img->se[k] = c ? R->se[k] : 0.0;
+    }
+    if (lane < 8) img->qf[lane] = (uint8_t)(lane < NSLOT && R->cnt[lane] ? R->qf[lane] : 0u);
+    wave_sync();
+    if (lane < 10) reinterpret_cast<uint4 *>(A)[lane] = reinterpret_cast<const uint4 *>(img)[lane];
+}
+
 template <bool FRESH>
 __device__ __forceinline__ void merge_column(Acc *__restrict__ A, const WaveRare *R, uint32_t batch_seq,
                                              uint32_t epoch, uint8_t refc, int lane) {
@@ -317,6 +350,10 @@ __device__ __forceinline__ void merge_column(Acc *__restrict__ A, const WaveRare
     }
 }
 
+struct ColDesc {             // one column of a wave's segment (LDS)
+    uint32_t a, pre, n, b, e, idx, refc, pad;   // 16-B aligned first chunk, first chunk index, chunks,
+};                                              // bounds rel. to a, column within the group, REF char
+
 struct RareItem {            // one lane's chunk slice (up to 16 entries) holding rare entries
     uint32_t c[4], q[4];
     int32_t o;              // column-relative offset of its first entry
@@ -349,6 +386,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     __shared__ WaveRare rare[4];
     __shared__ RareItem rqueue[4][QCAP];
     __shared__ Dual2 dual2[4];
+    __shared__ Acc accimg[4];
+    __shared__ ColDesc coldesc[4][64];
     write_hist(P);
     {
         const uint32_t q = threadIdx.x;
@@ -363,6 +402,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const int ng = (int)min((int64_t)P.G, P.n_cols - g0);
     WaveRare *R = rare + (threadIdx.x >> 6);
     Dual2 *D2 = dual2 + (threadIdx.x >> 6);
+    Acc *img = accimg + (threadIdx.x >> 6);
+    ColDesc *CD = coldesc[threadIdx.x >> 6];
     RareItem *Q = rqueue[threadIdx.x >> 6];
     uint32_t qn = 0;                                   // queued lane slices (wave-uniform)
     // drain the queue into the LDS record: every lane takes one entry per round (LDS atomics)
@@ -417,7 +458,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const uint32_t a_rel = b_rel & ~(ALIGN - 1);
     const uint32_t len = (uint32_t)(oe - ob);
     const uint32_t nch = (lane < ng && len > 0 && len >= P.t_deep) ? (e_rel - a_rel + STEP - 1) / STEP : 0u;
-    // exclusive prefix of the chunk counts: chunk i belongs to column popcount(pre <= i) - 1
+    // exclusive prefix of the chunk counts
     uint32_t pre = nch;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -427,22 +468,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const uint32_t total = __builtin_amdgcn_readlane(pre, 63);   // SGPR: loop bounds stay scalar
     pre -= nch;
     if (total == 0) return;
+    // Column descriptors of the columns with chunks, compacted into LDS; the loop walks them with
+    // two scalar cursors (consumption and prefetch), so no per-lane descriptor stays in a VGPR.
+    {
+        const uint64_t nz = __ballot(nch > 0);
+        if (nch > 0) {
+            const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
+            CD[k] = ColDesc{a_rel, pre, nch, b_rel - a_rel, e_rel - a_rel, (uint32_t)lane, refc, 0u};
+        }
+        wave_sync();
+    }
     const uint32_t lo = (uint32_t)lane * ALIGN;
-    const uint32_t pre_m = lane < ng ? pre : 0xFFFFFFFFu;   // lanes without a column never count
-    auto col_of = [&](uint32_t i) -> int {       // wave-uniform: one v_cmp into an SGPR mask
-        return (int)__popcll(__ballot(pre_m <= i)) - 1;
+    auto cd = [&](uint32_t k, int f) -> uint32_t {      // uniform LDS read of descriptor field f
+        return __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t *>(CD + k)[f]);
     };
-    auto chunk_off = [&](uint32_t i) -> uint32_t {   // branch-free: chunks past the end are loaded and ignored
-        const int j = col_of(min(i, total - 1));
-        return __builtin_amdgcn_readlane(a_rel, j) + (i - __builtin_amdgcn_readlane(pre, j)) * STEP + lo;
+    // prefetch cursor: column of the chunk being loaded (chunk indices only grow, by one per call)
+    uint32_t pk = 0, p_a = cd(0, 0), p_pre = cd(0, 1), p_end = p_pre + cd(0, 2);
+    auto chunk_off = [&](uint32_t i) -> uint32_t {   // chunks past the end reload the last one (ignored)
+        if (i >= p_end && i < total) {
+            pk++;
+            p_a = cd(pk, 0);
+            p_pre = cd(pk, 1);
+            p_end = p_pre + cd(pk, 2);
+        }
+        const uint32_t ii = i < p_end ? i : p_end - 1;
+        return p_a + (ii - p_pre) * STEP + lo;
     };
 
     V c0 = bload<W>(rc, chunk_off(0)), q0 = bload<W>(rq, chunk_off(0));
     V c1 = bload<W>(rc, chunk_off(1)), q1 = bload<W>(rq, chunk_off(1));
     V c2, q2;
 
-    // per-column state
-    int cj = 0;
+    // per-column state (consumption cursor)
+    uint32_t ck = 0xFFFFFFFFu, cj = 0, crefc = 0;
     uint32_t cs = 0, cpre = 0, cn = 0;
     uint32_t fcnt = 0, fsq = 0, ffirst = INF32;
     double fsl = 0.0, fse = 0.0;
@@ -453,14 +511,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     bool found2 = false;
 
     auto process = [&](const V &cc, const V &qq, uint32_t i) {
-        cj = col_of(i);
-        cpre = __builtin_amdgcn_readlane(pre, cj);
+        if (i == cpre + cn) {                  // next column with chunks
+            ck++;
+            cpre = cd(ck, 1);
+            cn = cd(ck, 2);
+            bl = (int32_t)cd(ck, 3);
+            el = (int32_t)cd(ck, 4);
+            cj = cd(ck, 5);
+            crefc = cd(ck, 6);
+        }
         cs = i - cpre;
         if (cs == 0) {                         // ---- column begin ----
-            cn = __builtin_amdgcn_readlane(nch, cj);
-            const uint32_t a = __builtin_amdgcn_readlane(a_rel, cj);
-            bl = (int32_t)(__builtin_amdgcn_readlane(b_rel, cj) - a);
-            el = (int32_t)(__builtin_amdgcn_readlane(e_rel, cj) - a);
             rare_init(R, lane);
             const uint32_t v0 = dw<W>(cc, 0) & 0xFFu;
             const int vote = ((int32_t)lo >= bl && (int32_t)lo < el) ? (int)v0 : -1;
@@ -476,7 +537,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             for (int k = 0; k < 7; k++) if (k != b1 && cnt7[k] > c2n) { c2n = cnt7[k]; b2 = k; }
             M = VC[b1];
             mrep = M * 0x01010101u;
-            sem = nibble_char(M) != (uint8_t)__builtin_amdgcn_readlane(refc, cj);
+            sem = nibble_char(M) != (uint8_t)crefc;
             dual = b2 >= 0;
             M2 = dual ? VC[b2] : 0u;
             mrep2 = dual ? M2 * 0x01010101u : 0xFFFFFFFFu;
@@ -634,8 +695,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                 }
             }
             wave_sync();
-            merge_column<FRESH>(acc + P.pos_begin + g0 + cj, R, P.batch_seq, P.epoch,
-                                (uint8_t)__builtin_amdgcn_readlane(refc, cj), lane);
+            if constexpr (FRESH)
+                merge_fresh(acc + P.pos_begin + g0 + cj, R, img, P.batch_seq, P.epoch, (uint8_t)crefc, lane);
+            else
+                merge_column<false>(acc + P.pos_begin + g0 + cj, R, P.batch_seq, P.epoch, (uint8_t)crefc, lane);
             wave_sync();
         }
     };
