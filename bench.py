@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--cpu-positions", type=int, default=8000)
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end BAM -> calls leg")
     ap.add_argument("--e2e-threads", type=int, default=16)
+    ap.add_argument("--full-table", action="store_true", help="also accumulate every table GL term")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
                                                       "gloo only to exercise the path on one GPU)")
     return ap.parse_args()
@@ -105,7 +106,7 @@ def end_to_end(args, device):
     t0 = time.perf_counter()
     n_reads = simulate_bam(bam, "NC_045512.2", ref, depth=args.depth, seed=5, n_threads=args.e2e_threads)
     t_sim = time.perf_counter() - t0
-    eng = PileupEngine(L_SARS, 30, 10, 5, 0.10, device=device, reference=ref)
+    eng = PileupEngine(L_SARS, 30, 10, 5, 0.10, device=device, reference=ref, calls_only=True)
     res = {}
     for cap, tag in ((8000, "parity_mode_max_depth_8000"), (0, "uncapped")):
         eng.reset()
@@ -178,7 +179,10 @@ def main():
     C = len(off) - 1
     t_gen = time.perf_counter() - t_gen
     d_off, d_c, d_q = synth.to_device(off, codes, quals, device=local if world > 1 else 0)
-    eng = PileupEngine(C, 30, 10, 5, 0.10, device=local if world > 1 else 0, reference=vref)
+    # calls-only engine (SPG_P_CALLS_ONLY): the call table prepare_variants() returns, exactly; see
+    # DESIGN.md §3 — the per-position GL table's REF-major entries are not accumulated
+    eng = PileupEngine(C, 30, 10, 5, 0.10, device=local if world > 1 else 0, reference=vref,
+                       calls_only=not args.full_table)
 
     # call-table gather buffer: u64 count + records, sized from a first (untimed) pass so the
     # per-step gather moves KBs, not the engine's full candidate capacity
@@ -252,7 +256,8 @@ def main():
                                + ("uncapped" if not args.max_depth else f"max_depth {args.max_depth}")
                                + ", 1 sample per GPU per step (coordinate-sharded)",
                    "positions_per_step": positions_per_step, "entries_per_gpu_step": E, "columns_per_gpu": C,
-                   "parallelism": f"coord-shard x{world}"},
+                   "parallelism": f"coord-shard x{world}",
+                   "engine_mode": "full_table" if args.full_table else "calls_only"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM, "traffic": pmc_traffic(E),
                      "kernel": "k_acc_seg<4,true> (spg_accumulate)", "kernel_ms": t_acc * 1e3, "algorithmic_bytes": algo_bytes},

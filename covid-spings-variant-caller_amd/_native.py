@@ -18,7 +18,8 @@ SPG_NSLOT = 5
 SPG_NCOUNT = 8
 SPG_CODE_DEL = 16
 SPG_CODE_SKIP = 17
-SPG_F_PRESENT, SPG_F_EVALUATED, SPG_F_REPLAYED, SPG_F_EXOTIC, SPG_F_CANDIDATE = 1, 2, 4, 8, 16
+SPG_F_PRESENT, SPG_F_EVALUATED, SPG_F_REPLAYED, SPG_F_EXOTIC, SPG_F_CANDIDATE, SPG_F_PARTIAL = 1, 2, 4, 8, 16, 32
+SPG_P_CALLS_ONLY = 1
 SPG_IN_DEVICE, SPG_IN_BORROW = 1, 2
 NIBBLE = "=ACMGRSVTWYHKDBN"
 SLOT_CHARS = "ACGTN"
@@ -27,7 +28,7 @@ SLOT_CODES = (1, 2, 4, 8, 15)
 
 class SpgParams(C.Structure):
     _fields_ = [("min_base_quality", C.c_int32), ("min_total_depth", C.c_int32),
-                ("min_allele_depth", C.c_int32), ("reserved0", C.c_int32),
+                ("min_allele_depth", C.c_int32), ("flags", C.c_int32),
                 ("min_evidence_ratio", C.c_double), ("reserved1", C.c_int64 * 4)]
 
 

@@ -18,10 +18,10 @@ namespace spg {
 constexpr int NSLOT = SPG_NSLOT;          // A C G T N
 constexpr uint32_t INF32 = 0xFFFFFFFFu;
 constexpr uint32_t MISC_EXOTIC = 0x100u;  // acc.misc bit: an allele outside A,C,G,T,N was seen
-// acc.misc bits 9..13: slot k's sum of eps is incomplete (the deep kernel skips it for a column's
-// major allele when that allele is the REF char — never a candidate, so QUAL is never needed; a
-// position where such a slot does become a candidate is resolved by the exact replay)
-constexpr int MISC_SE_SKIP_SHIFT = 9;
+// acc.misc bits 9..13: slot k's sum(ln(1-eps)) and sum(eps) are incomplete (SPG_P_CALLS_ONLY: the deep
+// kernel skips them for a column's major allele when it is the REF char; finalize treats that
+// allele's hypothesis product as unknown and replays a position whose calls would depend on it)
+constexpr int MISC_SKIP_SHIFT = 9;
 
 // Accumulators replacing Site (structs.py:2-6).  The q lists are replaced by sufficient
 // statistics: counts, the integer sum of q (log10 of the eps product up to fp64 rounding), the sum
@@ -67,6 +67,7 @@ struct KParams {
     uint32_t epoch;
     uint32_t G;            // columns per wave group
     uint32_t t_deep;       // columns with >= t_deep raw entries are processed wave-wide
+    uint32_t calls_only;   // SPG_P_CALLS_ONLY
     Hist hdesc;            // this batch's history descriptor ...
     Hist *hslot;           // ... written here by the first thread of the launch
 };

@@ -220,13 +220,13 @@ struct __align__(8) WaveRare {
     double sl[NSLOT], se[NSLOT];
     uint32_t depth, n_del, n_skip, n_other;
     uint32_t cnt[NSLOT], sq[NSLOT], qf[NSLOT], first[NSLOT];
-    uint32_t se_skip, pad;
+    uint32_t skip, pad;
 };
 static_assert(sizeof(WaveRare) == 184, "WaveRare");
 
 __device__ __forceinline__ void rare_init(WaveRare *R, int lane) {
     uint32_t *w = reinterpret_cast<uint32_t *>(R);
-    // words 0..19 doubles, 20..23 counters, 24..33 cnt/sq: 0; 34..38 qf: 255; 39..43 first: INF; 44 se_skip
+    // words 0..19 doubles, 20..23 counters, 24..33 cnt/sq: 0; 34..38 qf: 255; 39..43 first: INF; 44 skip
     if (lane < 45) w[lane] = lane < 34 ? 0u : (lane < 39 ? 255u : (lane < 44 ? INF32 : 0u));
 }
 
@@ -283,7 +283,7 @@ __device__ __forceinline__ void merge_fresh(Acc *__restrict__ A, const WaveRare 
         img->depth = R->depth;
         img->first_batch = batch_seq;                                // first visit (:77-85)
         img->order = merge_order(0u, newmask, first);
-        img->misc = refc | (R->n_other ? MISC_EXOTIC : 0u) | (R->se_skip << MISC_SE_SKIP_SHIFT);
+        img->misc = refc | (R->n_other ? MISC_EXOTIC : 0u) | (R->skip << MISC_SKIP_SHIFT);
         img->n_del = R->n_del;
         img->n_skip = R->n_skip;
         img->n_other = R->n_other;
@@ -314,7 +314,7 @@ __device__ __forceinline__ void merge_column(Acc *__restrict__ A, const WaveRare
         h0.x += R->depth;                                           // :87
         h1.x += R->n_del; h1.y += R->n_skip; h1.z += R->n_other; h1.w = epoch;
         if (R->n_other) h0.w |= MISC_EXOTIC;
-        h0.w |= R->se_skip << MISC_SE_SKIP_SHIFT;
+        h0.w |= R->skip << MISC_SKIP_SHIFT;
         const uint32_t have = order_mask(h0.z);
         uint32_t newmask = 0, first[NSLOT];
 #pragma unroll
@@ -414,7 +414,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     uint32_t mrep = 0, M = 1;
     bool dual = false;
     uint32_t mrep2 = 0, M2 = 0;
-    bool sem = true;                           // accumulate sum(eps) of the major (not when it is REF)
+    bool sem = true;                           // the major is not the REF char (calls-only mode skips REF sums)
+    bool skipped = false;                      // this column's major skipped its likelihood sums
     auto drain = [&]() {
         wave_sync();
         for (uint32_t b0 = 0; b0 < qn; b0 += 64) {
@@ -538,6 +539,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             M = VC[b1];
             mrep = M * 0x01010101u;
             sem = nibble_char(M) != (uint8_t)crefc;
+            skipped = false;
             dual = b2 >= 0;
             M2 = dual ? VC[b2] : 0u;
             mrep2 = dual ? M2 * 0x01010101u : 0xFFFFFFFFu;
@@ -565,9 +567,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                 r80 &= ~g80;
             }
         };
-        auto body = [&](auto full_tag, auto dual_tag, auto se_tag) {
+        auto body = [&](auto full_tag, auto dual_tag, auto sl_tag) {
             constexpr bool DUAL = decltype(dual_tag)::value;
-            constexpr bool SE = decltype(se_tag)::value;
+            constexpr bool SL = decltype(sl_tag)::value;     // false: counts / sum(q) only (calls-only REF major)
             uint32_t rany = 0;
             uint32_t fcnt2 = 0, fsq2 = 0;
             double fsl2 = 0.0, fse2 = 0.0;
@@ -593,18 +595,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                 fsq = __builtin_amdgcn_udot4(qw, f80 >> 7, fsq, false);
                 // fast entries have q < 128: their row is q; every other byte gets bit 7 -> a zero row
                 const uint32_t idx = (qw & 0x7F7F7F7Fu) ^ f80 ^ 0x80808080u;
-                if constexpr (SE) {
+                if constexpr (SL) {
                     const double2 t0 = lut[idx & 0xFFu], t1 = lut[(idx >> 8) & 0xFFu];
                     const double2 t2 = lut[(idx >> 16) & 0xFFu], t3 = lut[idx >> 24];
                     fsl += (t0.x + t1.x) + (t2.x + t3.x);
                     fse += (t0.y + t1.y) + (t2.y + t3.y);
-                } else {                       // REF major: no eps sum, half the LDS traffic
-                    const double t0 = lut[idx & 0xFFu].x, t1 = lut[(idx >> 8) & 0xFFu].x;
-                    const double t2 = lut[(idx >> 16) & 0xFFu].x, t3 = lut[idx >> 24].x;
-                    fsl += (t0 + t1) + (t2 + t3);
+                    asm volatile("" : "+v"(fsl), "+v"(fse) :: "memory");   // keep each dword's lookups together
+                } else {
+                    (void)idx;
                 }
                 rany |= r80;
-                asm volatile("" : "+v"(fsl), "+v"(fse) :: "memory");   // keep each dword's lookups together
             }
             if constexpr (DUAL) {
                 // second allele: lane-private LDS accumulators (no registers held across chunks)
@@ -657,8 +657,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             if (full) body(T_{}, T_{}, T_{});
             else body(F_{}, T_{}, T_{});
         } else if (full) {
-            if (sem) body(T_{}, F_{}, T_{});
-            else body(T_{}, F_{}, F_{});
+            if (sem || !P.calls_only) body(T_{}, F_{}, T_{});
+            else { body(T_{}, F_{}, F_{}); skipped = true; }
         } else {
             body(F_{}, F_{}, T_{});
         }
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                     R->cnt[Ms] += fc; R->sq[Ms] += fs; R->sl[Ms] += fl; R->se[Ms] += fe;
                     R->qf[Ms] = min(R->qf[Ms], (uint32_t)P.qlo);
                     R->first[Ms] = min(R->first[Ms], ffirst);
-                    if (!sem) R->se_skip |= 1u << Ms;   // full chunks skipped the eps sum
+                    if (skipped) R->skip |= 1u << Ms;   // full chunks skipped its likelihood sums
                 }
                 if (fc2) {
                     const int s2 = slot_of(M2);
@@ -752,8 +752,10 @@ struct LV { int s; double v, l2; };
 __device__ __forceinline__ LV lv_normal(double v, double l2) { return LV{0, v, l2}; }
 __device__ __forceinline__ LV lv_zero() { return LV{1, 0.0, -1e300}; }
 __device__ __forceinline__ LV lv_band(double ub) { return LV{2, 0.0, ub}; }
+__device__ __forceinline__ LV lv_unknown() { return LV{3, 0.0, 0.0}; }   // not accumulated (calls-only)
 __device__ __forceinline__ LV lv_mul(const LV &a, const LV &b) {
     if (a.s == 1 || b.s == 1) return lv_zero();                   // 0 * finite == 0
+    if (a.s == 3 || b.s == 3) return lv_unknown();
     const double l2 = a.l2 + b.l2;
     if (a.s == 0 && b.s == 0) {
         if (l2 > -1022.0 + MARGIN) return lv_normal(a.v * b.v, l2);  // stays normal: one rounding
@@ -891,6 +893,7 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
     {   // normal path; every exit that needs the exact replay jumps past this block
 
         const int n = (int)(a.order & 7u);
+        const uint32_t skip = (a.misc >> MISC_SKIP_SHIFT) & 0x1Fu;
         uint32_t slot[NSLOT], cnts[NSLOT];
         LV Pv[NSLOT], Hv[NSLOT];
         double Sv[NSLOT];
@@ -912,13 +915,14 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
             else Pv[k] = lv_band(-1022.0 + 2 * MARGIN);
             // H: exp(sum ln(1-eps)); exactly 0 when a Q0 entry is present (1 - 1.0 == 0)
             if (qf == 0u) Hv[k] = lv_zero();
+            else if ((skip >> slot[k]) & 1u) Hv[k] = lv_unknown();
             else {
                 const double l2 = sl * INV_LN2;
                 Hv[k] = l2 > -1022.0 + MARGIN ? lv_normal(exp(sl), l2) : lv_band(-1022.0 + 2 * MARGIN);
             }
         }
         double G[NSLOT];
-        bool band = false;
+        bool band = false, unknown = false, cand_needs_s = false;
     #pragma unroll
         for (int h = 0; h < NSLOT; h++) {
             // N = ((1.0 * P_a1) * P_a2) ... over a != h in dict order (utils.py:18-22), GL = H * N
@@ -928,29 +932,26 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
                 if (j != h && j < n) c = lv_mul(c, Pv[j]);
             const LV g = lv_mul(Hv[h], c);
             if (h < n && g.s == 2) band = true;
-            G[h] = g.s == 0 ? g.v : 0.0;
+            G[h] = g.s == 0 ? g.v : (g.s == 3 ? NaN : 0.0);
+            if (h < n && g.s == 3) unknown = true;
+            // a candidate needs S = sum(GL) unless its own GL is exactly 0 (SCORE = 0 for any S)
+            if (h < n && g.s != 1 && is_candidate(F, a, slot_code((int)slot[h]), cnts[h])) {
+                cand_needs_s = true;
+                if (g.s == 3) band = true;        // its own GL depends on terms not accumulated
+            }
         }
-        if (band) {
+        // unknown (not accumulated) GL terms only matter if a call needs S: then replay exactly
+        if (band || (unknown && cand_needs_s)) {
             O.flags[pos] = flags | SPG_F_REPLAYED;
             atomicAdd(&O.ctr[F.cslot].n_band, 1u);
             goto replay;
         }
-        // a candidate whose sum of eps was skipped (its allele was REF when accumulated, but the REF
-        // stored at the first visit differs): QUAL comes from the exact replay
-        const uint32_t skip = (a.misc >> MISC_SE_SKIP_SHIFT) & 0x1Fu;
-        if (skip) {
-    #pragma unroll
-            for (int k = 0; k < NSLOT; k++)
-                if (k < n && ((skip >> slot[k]) & 1u) && is_candidate(F, a, slot_code((int)slot[k]), cnts[k])) {
-                    O.flags[pos] = flags | SPG_F_REPLAYED;
-                    goto replay;
-                }
-        }
+        if (unknown) flags |= SPG_F_PARTIAL;
         double S = 0.0;
     #pragma unroll
         for (int k = 0; k < NSLOT; k++)
-            if (k < n) S = S + G[k];                             // :145
-        if (S == 0) S = 1.0;                                     // :146
+            if (k < n && !unknown) S = S + G[k];                 // :145
+        if (S == 0) S = 1.0;                                     // :146 (every call has GL 0 if unknown)
     #pragma unroll
         for (int k = 0; k < NSLOT; k++) {
             if (k < n) {

@@ -26,13 +26,16 @@ def eps_lut() -> np.ndarray:
 class PileupEngine:
     def __init__(self, n_pos: int, min_base_quality: int = 30, min_total_depth: int = 10,
                  min_allele_depth: int = 5, min_evidence_ratio: float = 0.10, device: int = 0,
-                 reference: Optional[str] = None):
+                 reference: Optional[str] = None, calls_only: bool = False):
+        """``calls_only`` (SPG_P_CALLS_ONLY): compute exactly what prepare_variants() emits; table GLs
+        that only the engine's own per-position table would show may read NaN (SPG_F_PARTIAL)."""
         self._L = N.gpu_lib()
         self._lock = threading.RLock()
         self.n_pos = int(n_pos)
         self.device = int(device)
-        self.params = N.SpgParams(int(min_base_quality), int(min_total_depth), int(min_allele_depth), 0,
-                                  float(min_evidence_ratio))
+        self.calls_only = bool(calls_only)
+        self.params = N.SpgParams(int(min_base_quality), int(min_total_depth), int(min_allele_depth),
+                                  N.SPG_P_CALLS_ONLY if calls_only else 0, float(min_evidence_ratio))
         h = C.c_void_p()
         N.check(self._L.spg_create(self.device, self.n_pos, C.byref(self.params), C.byref(h)), "spg_create")
         self._h = h

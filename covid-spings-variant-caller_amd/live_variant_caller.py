@@ -91,8 +91,9 @@ class LiveVariantCaller:
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         n_pos = max(self.fastaFile.lengths) if self.fastaFile.lengths else 1
+        # calls-only engine: prepare_variants() is the class's only statistical output
         self.engine = PileupEngine(max(1, n_pos), minBaseQuality, minTotalDepth, minAlleleDepth, minEvidenceRatio,
-                                   device=device)
+                                   device=device, calls_only=True)
         self._lock = threading.RLock()
         self._batch_contig: List[int] = []       # FASTA reference index of each accumulated batch
         self.reset_memory()

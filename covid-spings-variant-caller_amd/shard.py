@@ -94,11 +94,12 @@ class ShardedEngine:
     batch; its candidates go to the rank-0 call table with absolute positions."""
 
     def __init__(self, lo: int, hi: int, reference: str, min_base_quality=30, min_total_depth=10,
-                 min_allele_depth=5, min_evidence_ratio=0.10, device=0):
+                 min_allele_depth=5, min_evidence_ratio=0.10, device=0, calls_only=True):
         from .engine import PileupEngine
         self.lo, self.hi = lo, hi
         self.engine = PileupEngine(max(1, hi - lo), min_base_quality, min_total_depth, min_allele_depth,
-                                   min_evidence_ratio, device=device, reference=reference[lo:max(hi, lo + 1)])
+                                   min_evidence_ratio, device=device, reference=reference[lo:max(hi, lo + 1)],
+                                   calls_only=calls_only)
 
         self.n_batches = 0          # batches seen by the job (global sequence)
         self._global_seq = []       # local engine batch seq - 1 -> global batch seq

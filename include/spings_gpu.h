@@ -51,6 +51,7 @@ extern "C" {
 #define SPG_F_REPLAYED 0x04   /* resolved by the exact sequential replay (subnormal band / exotic) */
 #define SPG_F_EXOTIC 0x08     /* has alleles outside A,C,G,T,N (see spg_detail) */
 #define SPG_F_CANDIDATE 0x10  /* produced >= 1 variant */
+#define SPG_F_PARTIAL 0x20    /* SPG_P_CALLS_ONLY: some table GL of this position not computed (NaN) */
 
 /* accumulate flags */
 #define SPG_IN_DEVICE 0x1     /* offsets/base_code/qual are device pointers on the ctx device */
@@ -58,13 +59,21 @@ extern "C" {
                                  history without copying; they must stay valid until
                                  spg_reset/spg_destroy */
 
+/* spg_params.flags */
+#define SPG_P_CALLS_ONLY 0x1  /* compute what prepare_variants() emits and nothing it cannot see: the
+                                 deep kernel does not accumulate sum(ln(1-eps)) / sum(eps) of a
+                                 column's major allele when it is the REF char (never a candidate).
+                                 Candidates stay exact (positions whose calls would depend on the
+                                 missing terms are replayed); table GL entries that depend on them
+                                 read NaN and the position carries SPG_F_PARTIAL. */
+
 /* LiveVariantCaller ctor thresholds (live_variant_caller.py:22-29); minMappingQuality and
  * maxVariants act before the boundary / are unused by the reference, so they are not here. */
 typedef struct {
     int32_t min_base_quality;    /* pileup min_base_quality -> pysam pileup_base_qual_skip */
     int32_t min_total_depth;     /* :131 */
     int32_t min_allele_depth;    /* :153 */
-    int32_t reserved0;
+    int32_t flags;               /* SPG_P_* */
     double min_evidence_ratio;   /* :154 */
     int64_t reserved1[4];
 } spg_params;
