@@ -32,7 +32,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--depth", type=float, default=10000.0)
+    ap.add_argument("--workload", default="sars10k", choices=sorted(WORKLOADS) if False else
+                    ["sars10k", "sars1k", "sars100k", "chr1_30x"])
+    ap.add_argument("--depth", type=float, default=0.0, help="override the workload's depth")
+    ap.add_argument("--length", type=int, default=0, help="override the workload's reference length")
     ap.add_argument("--max-depth", type=int, default=0, help="0 = uncapped; 8000 = pysam parity cap")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-positions", type=int, default=8000)
@@ -44,23 +47,40 @@ def parse():
     return ap.parse_args()
 
 
-def build_shard(rank, world, depth, max_depth):
-    """CSR of this rank's coordinate range of each of `world` samples, concatenated."""
+WORKLOADS = {   # BASELINE.json configs (the metric is quoted on sars10k; the others are optional runs)
+    "sars10k": (L_SARS, 10000.0, "NC_045512.2"),
+    "sars1k": (L_SARS, 1000.0, "NC_045512.2"),
+    "sars100k": (L_SARS, 100000.0, "NC_045512.2"),
+    "chr1_30x": (248956422, 30.0, "chr1"),
+}
+
+
+def build_shard(rank, world, L, depth, max_depth, device):
+    """This rank's coordinate range of each of `world` samples, generated natively
+    (libspings_pileup spp_synth_batch: SURVEY §8 d read model) and concatenated in HBM."""
+    import torch
     from covid_spings_variant_caller_amd import synth
-    ref = synth.reference(L_SARS, seed=1)
-    shard = (L_SARS + world - 1) // world
-    lo, hi = rank * shard, min(L_SARS, (rank + 1) * shard)
-    offs, codes, quals, refs = [np.zeros(1, np.uint64)], [], [], []
+    from covid_spings_variant_caller_amd.pileup import synth_batch
+    ref = synth.reference(L, seed=1)
+    shard = (L + world - 1) // world
+    lo, hi = rank * shard, min(L, (rank + 1) * shard)
+    offs, dc, dq, refs = [np.zeros(1, np.uint64)], [], [], []
     base = 0
+    threads = min(16, len(os.sched_getaffinity(0)))
     for s in range(world):
-        _, o, c, q = synth.pileup(L_SARS, depth, seed=2 + s, ref=ref, lo=lo, hi=hi, max_depth=max_depth)
-        offs.append(o[1:] + np.uint64(base))
-        base += len(c)
-        codes.append(c)
-        quals.append(q)
+        b = synth_batch(ref, depth, lo=lo, hi=hi, seed=2 + s, n_threads=threads, max_depth=max_depth)
+        offs.append(b.offsets[1:] + np.uint64(base))
+        base += b.n_entries
+        dc.append(torch.from_numpy(b.codes).to(device))
+        dq.append(torch.from_numpy(b.quals).to(device))
         refs.append(ref[lo:hi])
+        b.close()
+    pad = torch.zeros(16, dtype=torch.uint8, device=device)
+    d_c = torch.cat(dc + [pad + 0xFF])
+    d_q = torch.cat(dq + [pad])
     off = np.concatenate(offs)
-    return ref, "".join(refs), off, np.concatenate(codes), np.concatenate(quals), hi - lo
+    d_off = torch.from_numpy(off.view(np.int64).copy()).to(device)
+    return ref, "".join(refs), off, d_off, d_c, d_q, int(base)
 
 
 def cpu_baseline(args):
@@ -68,17 +88,19 @@ def cpu_baseline(args):
     from covid_spings_variant_caller_amd import synth
     from oracle import reference_port as rp
     from oracle.c_oracle import COracle
-    ref = synth.reference(L_SARS, seed=1)
+    Lw, depth = args.eff_L, args.eff_depth
+    ref = synth.reference(min(Lw, 10_000_000), seed=1)
     lo = 8000
-    n = args.cpu_positions
-    _, off, c, q = synth.pileup(L_SARS, args.depth, seed=2, ref=ref, lo=lo, hi=lo + n, max_depth=args.max_depth)
+    # about 8e7 entries (~13 s in the numpy port) whatever the depth
+    n = int(min(max(args.cpu_positions * 10000.0 / depth, 100), len(ref) - lo))
+    _, off, c, q = synth.pileup(len(ref), depth, seed=2, ref=ref, lo=lo, hi=lo + n, max_depth=args.max_depth)
     t0 = time.perf_counter()
     o = rp.OracleCaller(ref, 30, 10, 5, 0.10)
     o.accumulate(lo, off, c, q)
     o.prepare_variants()
     t_py = time.perf_counter() - t0
-    n_c = L_SARS                              # the C restatement takes the whole genome
-    _, off2, c2, q2 = synth.pileup(L_SARS, args.depth, seed=2, ref=ref, max_depth=args.max_depth)
+    n_c = min(len(ref), max(n, int(3e8 / depth)))   # the C restatement: ~3e8 entries (the whole SARS genome)
+    _, off2, c2, q2 = synth.pileup(len(ref), depth, seed=2, ref=ref, hi=n_c, max_depth=args.max_depth)
     t0 = time.perf_counter()
     co = COracle(ref, 30, 10, 5, 0.10)
     co.accumulate(0, off2, c2, q2)
@@ -86,7 +108,7 @@ def cpu_baseline(args):
     t_c = time.perf_counter() - t0
     return {"value": n / t_py, "unit": "positions/s", "cores": 1, "kind": "port",
             "sample": f"oracle/reference_port.py (Python/numpy restatement of live_variant_caller.py:74-185) "
-                      f"on {n} positions x {args.depth:.0f}x ({int(off[-1])} entries), {t_py:.2f} s, 1 core; "
+                      f"on {n} positions x {depth:.0f}x ({int(off[-1])} entries), {t_py:.2f} s, 1 core; "
                       f"pysam pileup/BAM decode not included (absent)",
             "c_restatement": {"value": n_c / t_c, "unit": "positions/s", "cores": 1,
                               "sample": f"oracle/spg_oracle.c on {n_c} positions ({int(off2[-1])} entries), {t_c:.2f} s"}}
@@ -104,7 +126,7 @@ def end_to_end(args, device):
     d = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
     bam = os.path.join(d, "sars_e2e.bam")
     t0 = time.perf_counter()
-    n_reads = simulate_bam(bam, "NC_045512.2", ref, depth=args.depth, seed=5, n_threads=args.e2e_threads)
+    n_reads = simulate_bam(bam, "NC_045512.2", ref, depth=args.eff_depth, seed=5, n_threads=args.e2e_threads)
     t_sim = time.perf_counter() - t0
     eng = PileupEngine(L_SARS, 30, 10, 5, 0.10, device=device, reference=ref, calls_only=True)
     res = {}
@@ -173,12 +195,15 @@ def main():
     else:
         torch.cuda.set_device(0)
 
+    L, depth, contig = WORKLOADS[args.workload]
+    L = args.length or L
+    depth = args.depth or depth
+    args.eff_L, args.eff_depth = L, depth
+    dev = torch.device("cuda", local if world > 1 else 0)
     t_gen = time.perf_counter()
-    ref, vref, off, codes, quals, shard_len = build_shard(rank, world, args.depth, args.max_depth)
-    E = len(codes)
+    ref, vref, off, d_off, d_c, d_q, E = build_shard(rank, world, L, depth, args.max_depth, dev)
     C = len(off) - 1
     t_gen = time.perf_counter() - t_gen
-    d_off, d_c, d_q = synth.to_device(off, codes, quals, device=local if world > 1 else 0)
     # calls-only engine (SPG_P_CALLS_ONLY): the call table prepare_variants() returns, exactly; see
     # DESIGN.md §3 — the per-position GL table's REF-major entries are not accumulated
     eng = PileupEngine(C, 30, 10, 5, 0.10, device=local if world > 1 else 0, reference=vref,
@@ -241,18 +266,20 @@ def main():
         gathered = [int(o[:8].cpu().numpy().view(np.uint64)[0]) for o in gather_out]
         if max(gathered) > cand_cap:
             raise RuntimeError(f"call table larger than the gather buffer ({max(gathered)} > {cand_cap})")
-    positions_per_step = world * L_SARS
+    positions_per_step = world * L
     value = positions_per_step * args.steps / dt
     t_acc = float(np.mean(acc_ms)) * 1e-3
     t_fin = float(np.mean(fin_ms)) * 1e-3
     algo_bytes = 2 * E + 8 * (C + 1)          # base_code + qual + u64 offsets read by the accumulate kernel
     achieved = algo_bytes / t_acc
     res = {
-        "metric": "pileup positions/s at 10,000x depth (SARS-CoV-2, synthetic)",
+        "metric": ("pileup positions/s at 10,000x depth (SARS-CoV-2, synthetic)" if args.workload == "sars10k"
+                   and depth == 10000 and L == L_SARS else f"pileup positions/s at {depth:,.0f}x depth ({contig} "
+                   f"L={L:,}, synthetic)"),
         "value": value, "unit": "positions/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "u8/f64", "data": "synthetic",
-        "config": {"workload": f"SARS-CoV-2 L={L_SARS}, {args.depth:.0f}x, 150-bp reads, "
+        "config": {"workload": f"{args.workload}: {contig} L={L}, {depth:.0f}x, 150-bp reads, "
                                + ("uncapped" if not args.max_depth else f"max_depth {args.max_depth}")
                                + ", 1 sample per GPU per step (coordinate-sharded)",
                    "positions_per_step": positions_per_step, "entries_per_gpu_step": E, "columns_per_gpu": C,
@@ -264,7 +291,7 @@ def main():
         "finalize_ms": t_fin * 1e3, "candidates_per_gpu_step": n_cand, "datagen_s": t_gen,
         "calls_gathered_per_step": sum(gathered) if gathered is not None else n_cand,
     }
-    if rank == 0 and world == 1 and not args.no_e2e:
+    if rank == 0 and world == 1 and not args.no_e2e and L == L_SARS:
         res["end_to_end"] = end_to_end(args, 0)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args)

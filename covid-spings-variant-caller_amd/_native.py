@@ -160,6 +160,7 @@ def pileup_lib():
     _sig(L.spp_default_sim_params, None, C.POINTER(SimParams))
     _sig(L.spp_simulate_bam, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, i64, C.POINTER(SimParams),
          C.POINTER(i64))
+    _sig(L.spp_synth_batch, C.c_int, C.c_char_p, i64, i64, i64, C.POINTER(SimParams), i64, C.POINTER(vp))
     _pileup = L
     return L
 

@@ -85,6 +85,7 @@ struct spg_ctx {
     uint8_t ring_tm[NRING] = {};        // bit 0: accumulate events recorded, bit 1: finalize events
     bool acc_open = false, acc_any = false;
     bool last_acc = false, last_fin = false;
+    bool table_valid = false;           // the SoA table matches the last finalize
     int timing = default_timing();
     int acc_timing = 0;                 // level the open / last accumulate interval was recorded at
     int fin_timing = 0;
@@ -318,7 +319,8 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
         const char *e = getenv("SPG_TARGET_WAVES");
         return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)16384;
     }();
-    const bool deep_batch = avg >= 2048.0;
+    static const double deep_min = [] { const char *e = getenv("SPG_DEEP_MIN"); return e ? atof(e) : 256.0; }();
+    const bool deep_batch = avg >= deep_min;
     const uint32_t G = (uint32_t)std::min<int64_t>(64, std::max<int64_t>(1, (n_cols + target_waves - 1) / target_waves));
     KParams P{};
     P.pos_begin = pos_begin;
@@ -376,8 +378,15 @@ static FParams make_fparams(spg_ctx *c) {
     return F;
 }
 
+static int finalize_impl(spg_ctx *c, bool table);
+
 int spg_finalize(spg_ctx *c) {
     if (!c) return fail("spg_finalize: null ctx");
+    // calls-only contexts write the per-position table lazily (spg_get_table)
+    return finalize_impl(c, !(c->p.flags & SPG_P_CALLS_ONLY));
+}
+
+static int finalize_impl(spg_ctx *c, bool table) {
     if (!c->lut_set) return fail("spg_finalize: spg_set_eps_lut not called");
     HIPCHK(hipSetDevice(c->device));
     c->cslot ^= 1u;            // this call counts in slot cslot (zeroed by the previous call / creation)
@@ -391,7 +400,10 @@ int spg_finalize(spg_ctx *c) {
     }
     const int ft = c->timing;
     if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
-    HIPCHK(launch_finalize(make_fparams(c), c->acc, c->tables, make_out(c), c->d_hist, c->stream));
+    FParams F = make_fparams(c);
+    F.table = table ? 1u : 0u;
+    HIPCHK(launch_finalize(F, c->acc, c->tables, make_out(c), c->d_hist, c->stream));
+    c->table_valid = table;
     if (ft >= 2) HIPCHK(hipEventRecord(ev[3], c->stream));
     c->last_acc = c->acc_open && c->acc_timing >= 1;
     c->last_fin = ft >= 2;
@@ -438,7 +450,7 @@ static int settle(spg_ctx *c, Counters &h) {
             again = true;
         }
         if (!again) return 0;
-        int rc = spg_finalize(c);
+        int rc = finalize_impl(c, c->table_valid);
         if (rc) return rc;
     }
     return fail("spg: result buffers did not settle");
@@ -489,6 +501,12 @@ int spg_get_table(spg_ctx *c, int64_t pos0, int64_t n, uint32_t *depth, uint32_t
     Counters h{};
     int rc = settle(c, h);
     if (rc) return rc;
+    if (!c->table_valid) {                  // calls-only finalize: build the table now
+        rc = finalize_impl(c, true);
+        if (rc) return rc;
+        rc = settle(c, h);
+        if (rc) return rc;
+    }
     const hipMemcpyKind k = hipMemcpyDeviceToHost;
     if (depth) HIPCHK(hipMemcpyAsync(depth, c->o_depth + pos0, 4 * n, k, c->stream));
     if (counts) HIPCHK(hipMemcpyAsync(counts, c->o_counts + pos0 * SPG_NCOUNT, 4 * SPG_NCOUNT * n, k, c->stream));

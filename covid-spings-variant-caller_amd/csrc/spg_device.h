@@ -83,6 +83,8 @@ struct FParams {
     int64_t cand_cap, band_cap, detail_cap;
     int32_t min_bq, n_hist;
     uint32_t epoch, cslot;
+    uint32_t table;        // write the per-position SoA table (else: calls only, early exits)
+    uint32_t pad_;
 };
 
 struct Out {                // SoA result table

@@ -144,9 +144,11 @@ __device__ __forceinline__ uint32_t order_mask(uint32_t order) {
 }
 
 // Merge one column's batch statistics into its Acc record (single lane; shallow path).
-__device__ void merge_acc(Acc *__restrict__ A, const ColState &c, uint32_t batch_seq, uint32_t epoch, uint8_t refc) {
-    Acc a = *A;
-    if (a.epoch != epoch) {                         // record of an older sample: start afresh
+__device__ void merge_acc(Acc *__restrict__ A, const ColState &c, uint32_t batch_seq, uint32_t epoch, uint8_t refc,
+                          uint32_t skip = 0u, bool fresh = false) {
+    Acc a;
+    if (!fresh) a = *A;                             // FRESH (first batch of the epoch): nothing to read
+    if (fresh || a.epoch != epoch) {                // record of an older sample: start afresh
         a = Acc{};
         a.epoch = epoch;
     }
@@ -159,6 +161,7 @@ __device__ void merge_acc(Acc *__restrict__ A, const ColState &c, uint32_t batch
     a.n_skip += c.n_skip;
     a.n_other += c.n_other;
     if (c.n_other) a.misc |= MISC_EXOTIC;
+    a.misc |= skip << MISC_SKIP_SHIFT;
     const uint32_t have = order_mask(a.order);
     uint32_t newmask = 0;
 #pragma unroll
@@ -715,26 +718,92 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
 }
 
-// Short columns (< t_deep raw entries): one lane per column, sequential, registers only.
-__global__ __launch_bounds__(256) void k_acc_shallow(KParams P, const uint64_t *__restrict__ off,
+// Short columns (< t_deep raw entries): one lane per column.  The lane walks its column in
+// aligned dwords (4 entries per load, columns of neighbouring lanes share cache lines), classifies
+// them with the SWAR test against the column's REF allele (the major allele of a shallow column in
+// practice), sums the fast entries in registers (LDS LUT) and sends the rest through the per-slot
+// register state one by one.
+__device__ __forceinline__ uint32_t code_of_ref(uint8_t c) {
+    c = (uint8_t)(c & 0xDFu);                     // upper case
+    return c == 'A' ? 1u : c == 'C' ? 2u : c == 'G' ? 4u : c == 'T' ? 8u : c == 'N' ? 15u : 1u;
+}
+
+__device__ __forceinline__ void entry_update_lut(ColState &s, uint32_t code, uint32_t q, uint32_t idx,
+                                                 const double2 *__restrict__ lut) {
+    s.depth++;
+    if (code == SPG_CODE_DEL) { s.n_del++; return; }
+    if (code == SPG_CODE_SKIP) { s.n_skip++; return; }
+    const int sl = slot_of(code);
+    if (sl < 0) { s.n_other++; return; }
+    const double2 t = lut[q < 128u ? q : q + 128u];
+    s.cnt[sl] += 1u; s.sq[sl] += q; s.qf[sl] = min(s.qf[sl], q); s.first[sl] = min(s.first[sl], idx);
+    s.sl[sl] += t.x; s.se[sl] += q == 0 ? 1.0 : t.y;        // state in LDS: indexed directly
+}
+
+__global__ __launch_bounds__(128) void k_acc_shallow(KParams P, const uint64_t *__restrict__ off,
                                                      const uint8_t *__restrict__ code,
                                                      const uint8_t *__restrict__ qual,
                                                      const uint8_t *__restrict__ ref, const Tables *__restrict__ T,
                                                      Acc *__restrict__ acc) {
+    __shared__ double2 lut[384];                  // same layout as k_acc_seg's
+    __shared__ ColState lane_state[128];          // per-lane state of the non-fast alleles (indexed by slot)
     write_hist(P);
+    for (uint32_t q = threadIdx.x; q < 256u; q += blockDim.x) {
+        lut[q] = q < 128u ? make_double2(T->fast[q][0], T->fast[q][1]) : make_double2(0.0, 0.0);
+        if (q >= 128u) lut[q + 128u] = make_double2(T->fast[q][0], T->fast[q][1]);
+    }
+    __syncthreads();
     const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (col >= P.n_cols) return;
     const uint64_t ob = off[col], oe = off[col + 1];
     const uint64_t len = oe - ob;
     if (len == 0 || len >= P.t_deep) return;
-    ColState st;
-    cs_init(st);
-    for (uint64_t i = ob; i < oe; i++) {
-        const uint32_t c = code[i], q = qual[i];
-        if ((int)q >= P.min_bq) entry_update(st, c, q, (uint32_t)(i - ob), T);
-    }
     const int64_t pos = P.pos_begin + col;
-    merge_acc(acc + pos, st, P.batch_seq, P.epoch, ref[pos]);
+    const uint8_t refc = ref[pos];
+    const uint32_t M = code_of_ref(refc);
+    const uint32_t mrep = M * 0x01010101u;
+    const bool sums = !P.calls_only || nibble_char(M) != refc;   // calls-only: no sums for the REF allele
+    ColState &st = lane_state[threadIdx.x];
+    cs_init(st);
+    uint32_t fcnt = 0, fsq = 0, ffirst = INF32;
+    double fsl = 0.0, fse = 0.0;
+    const uint64_t a0 = ob & ~(uint64_t)3, a1 = (oe + 3) & ~(uint64_t)3;
+    const uint32_t *cw4 = reinterpret_cast<const uint32_t *>(code + a0);
+    const uint32_t *qw4 = reinterpret_cast<const uint32_t *>(qual + a0);
+    const int32_t lead = (int32_t)(ob - a0);
+    const uint32_t nd = (uint32_t)((a1 - a0) >> 2);
+    for (uint32_t d = 0; d < nd; d++) {
+        const uint32_t cw = cw4[d], qw = qw4[d];
+        const int32_t x = (int32_t)(4 * d) - lead;           // column index of this dword's byte 0
+        const uint32_t v = valid80(x, 0, (int32_t)len);
+        uint32_t f80, r80;
+        swar4(cw, qw, v, mrep, P.kpass, P.kok, f80, r80);
+        fcnt += __popc(f80);
+        fsq = __builtin_amdgcn_udot4(qw, f80 >> 7, fsq, false);
+        if (sums) {
+            const uint32_t idx = (qw & 0x7F7F7F7Fu) ^ f80 ^ 0x80808080u;
+            const double2 t0 = lut[idx & 0xFFu], t1 = lut[(idx >> 8) & 0xFFu];
+            const double2 t2 = lut[(idx >> 16) & 0xFFu], t3 = lut[idx >> 24];
+            fsl += (t0.x + t1.x) + (t2.x + t3.x);
+            fse += (t0.y + t1.y) + (t2.y + t3.y);
+        }
+        if (f80 && ffirst == INF32) ffirst = (uint32_t)(x + (int32_t)(__builtin_ctz(f80) >> 3));
+        while (r80) {
+            const int sh = __builtin_ctz(r80) - 7;
+            r80 &= r80 - 1;
+            const uint32_t c = (cw >> sh) & 0xFFu, q = (qw >> sh) & 0xFFu;
+            if ((int)q >= P.min_bq) entry_update_lut(st, c, q, (uint32_t)(x + (sh >> 3)), lut);
+        }
+    }
+    uint32_t skip = 0;
+    if (fcnt) {
+        const int Ms = slot_of(M);
+        st.depth += fcnt;
+        st.cnt[Ms] += fcnt; st.sq[Ms] += fsq; st.qf[Ms] = min(st.qf[Ms], (uint32_t)P.qlo);
+        st.first[Ms] = min(st.first[Ms], ffirst); st.sl[Ms] += fsl; st.se[Ms] += fse;
+        if (!sums) skip = 1u << Ms;
+    }
+    merge_acc(acc + pos, st, P.batch_seq, P.epoch, refc, skip, P.batch_seq == 1);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -835,20 +904,20 @@ __device__ __forceinline__ void replay_position(const FParams &F, const Hist *__
         S = S + w->G[h];
     }
     if (S == 0) S = 1.0;
-    uint8_t flags = O.flags[pos];
+    uint8_t flags = F.table ? O.flags[pos] : 0;
     if (evaluated) {
         double *gl = O.gl + pos * NSLOT;
         for (int h = 0; h < n; h++) {
             const uint32_t c = w->ord[h];
             const int s = slot_of(c);
-            if (s >= 0) gl[s] = w->G[h];
+            if (s >= 0 && F.table) gl[s] = w->G[h];
             if (is_candidate(F, a, c, w->cnt[c])) {
                 write_candidate(F, O, pos, a, h, c, w->cnt[c], w->G[h], S, w->se[c] / (double)w->cnt[c]);
                 flags |= SPG_F_CANDIDATE;
             }
         }
     }
-    O.flags[pos] = flags;
+    if (F.table) O.flags[pos] = flags;
     if (depth != a.depth) atomicOr(&O.ctr[F.cslot].err, 1u);   // history / accumulator mismatch
     const uint32_t at = atomicAdd(&O.ctr[F.cslot].n_detail, 1u);
     if (at < (uint32_t)F.detail_cap) {
@@ -870,26 +939,48 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
     if (blockIdx.x == 0 && threadIdx.x == 0) O.ctr[F.cslot ^ 1u] = Counters{0, 0, 0, 0};   // next call's slot
     const int64_t pos = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (pos >= F.n_pos) return;
+    const double NaN = __builtin_nan("");
+    if (!F.table) {
+        // calls only: the header and the counts (first 48 bytes) decide whether this position can
+        // produce a call at all; only then is the rest of the record read
+        const uint4 h0 = reinterpret_cast<const uint4 *>(acc + pos)[0];
+        const uint4 h1 = reinterpret_cast<const uint4 *>(acc + pos)[1];
+        if (h1.w != F.epoch || h0.y == 0) return;                       // not in memory
+        if ((int64_t)h0.x < (int64_t)F.min_td) return;                  // not evaluated (:131)
+        if (!(h0.w & MISC_EXOTIC)) {
+            const uint4 c4 = reinterpret_cast<const uint4 *>(acc + pos)[2];
+            const uint32_t c5 = reinterpret_cast<const uint32_t *>(acc + pos)[12];
+            const uint32_t cnt[NSLOT] = {c4.x, c4.y, c4.z, c4.w, c5};
+            const uint8_t refc = (uint8_t)(h0.w & 0xFFu);
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < NSLOT; k++)
+                any |= cnt[k] != 0 && refc != nibble_char(slot_code(k)) && (int64_t)cnt[k] >= F.min_ad &&
+                       (double)cnt[k] / (double)h0.x >= F.ratio;                         // :151-157
+            if (!any) return;
+        }
+    }
     const Acc a = acc[pos];
     const bool live = a.epoch == F.epoch && a.first_batch != 0;
-    const double NaN = __builtin_nan("");
-    O.depth[pos] = live ? a.depth : 0u;
-    O.order[pos] = live ? a.order : 0u;
-    O.first[pos] = live ? a.first_batch : 0u;
     uint32_t *cnt8 = O.counts + pos * SPG_NCOUNT;
-    double *gl = O.gl + pos * NSLOT;
+    double *gl = F.table ? O.gl + pos * NSLOT : reinterpret_cast<double *>(my_ws->G);   // scratch-free sink
+    if (F.table) {
+        O.depth[pos] = live ? a.depth : 0u;
+        O.order[pos] = live ? a.order : 0u;
+        O.first[pos] = live ? a.first_batch : 0u;
 #pragma unroll
-    for (int k = 0; k < NSLOT; k++) { cnt8[k] = live ? a.cnt[k] : 0u; gl[k] = NaN; }
-    cnt8[5] = live ? a.n_del : 0u; cnt8[6] = live ? a.n_skip : 0u; cnt8[7] = live ? a.n_other : 0u;
-    if (!live) { O.flags[pos] = 0; return; }
+        for (int k = 0; k < NSLOT; k++) { cnt8[k] = live ? a.cnt[k] : 0u; gl[k] = NaN; }
+        cnt8[5] = live ? a.n_del : 0u; cnt8[6] = live ? a.n_skip : 0u; cnt8[7] = live ? a.n_other : 0u;
+    }
+    if (!live) { if (F.table) O.flags[pos] = 0; return; }
     uint8_t flags = SPG_F_PRESENT;
     const bool evaluated = (int64_t)a.depth >= (int64_t)F.min_td;   // :131
     if (evaluated) flags |= SPG_F_EVALUATED;
     if (a.misc & MISC_EXOTIC) {       // IUPAC / '=' alleles: the exact replay tabulates every allele
-        O.flags[pos] = flags | SPG_F_EXOTIC | SPG_F_REPLAYED;
+        if (F.table) O.flags[pos] = flags | SPG_F_EXOTIC | SPG_F_REPLAYED;
         goto replay;
     }
-    if (!evaluated) { O.flags[pos] = flags; return; }
+    if (!evaluated) { if (F.table) O.flags[pos] = flags; return; }
     {   // normal path; every exit that needs the exact replay jumps past this block
 
         const int n = (int)(a.order & 7u);
@@ -942,7 +1033,7 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
         }
         // unknown (not accumulated) GL terms only matter if a call needs S: then replay exactly
         if (band || (unknown && cand_needs_s)) {
-            O.flags[pos] = flags | SPG_F_REPLAYED;
+            if (F.table) O.flags[pos] = flags | SPG_F_REPLAYED;
             atomicAdd(&O.ctr[F.cslot].n_band, 1u);
             goto replay;
         }
@@ -965,7 +1056,7 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
                 }
             }
         }
-        O.flags[pos] = flags;
+        if (F.table) O.flags[pos] = flags;
         return;
     }
 replay:
@@ -979,8 +1070,8 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
                              const uint8_t *ref, const Tables *T, Acc *acc, hipStream_t st) {
     if (P.n_cols == 0) return hipSuccess;
     if (P.t_deep > 1) {      // mixed / shallow batches: lane-per-column pass for the short columns
-        const int64_t blocks = (P.n_cols + 255) / 256;
-        hipLaunchKernelGGL(k_acc_shallow, dim3((unsigned)blocks), dim3(256), 0, st, P, off, code, qual, ref, T, acc);
+        const int64_t blocks = (P.n_cols + 127) / 128;
+        hipLaunchKernelGGL(k_acc_shallow, dim3((unsigned)blocks), dim3(128), 0, st, P, off, code, qual, ref, T, acc);
     }
     const int64_t waves = (P.n_cols + P.G - 1) / P.G;
     const int64_t blocks = (waves + 3) / 4;

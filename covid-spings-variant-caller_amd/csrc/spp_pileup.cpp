@@ -980,3 +980,88 @@ int spp_simulate_bam(const char *path, const char *contig, const char *ref_seq, 
 }
 
 }  // extern "C"
+
+extern "C" int spp_synth_batch(const char *ref_seq, int64_t ref_len, int64_t lo, int64_t hi, const spp_sim_params *p,
+                               int64_t max_depth, spp_batch **out) {
+    if (!ref_seq || !p || !out) return fail("spp_synth_batch: null argument");
+    if (lo < 0 || hi > ref_len || hi < lo) return fail("spp_synth_batch: bad column range");
+    *out = nullptr;
+    try {
+        const int64_t L = ref_len, R = p->read_len, C = hi - lo;
+        const int64_t n = (int64_t)std::llround(p->depth * (double)L / (double)R);
+        std::vector<int64_t> starts((size_t)n);
+        {
+            std::mt19937_64 rng(p->seed);
+            std::uniform_int_distribution<int64_t> S(0, std::max<int64_t>(0, L - R));
+            for (auto &x : starts) x = S(rng);
+            std::sort(starts.begin(), starts.end());
+        }
+        auto *B = new spp_batch();
+        B->pos_begin = lo;
+        B->n_cols = C;
+        B->off.assign((size_t)C + 1, 0);
+        for (int64_t c = 0; c < C; c++) {          // reads covering lo + c: starts in [lo+c-R+1, lo+c]
+            const int64_t col = lo + c;
+            const auto a = std::lower_bound(starts.begin(), starts.end(), col - R + 1);
+            const auto b = std::upper_bound(starts.begin(), starts.end(), col);
+            int64_t d = b - a;
+            if (max_depth > 0) d = std::min(d, max_depth);
+            B->off[(size_t)c + 1] = B->off[(size_t)c] + (uint64_t)d;
+        }
+        const uint64_t E = B->off[(size_t)C];
+        B->n_entries = E;
+        B->n_used = n;
+        B->code = (uint8_t *)malloc(E + 16);
+        B->qual = (uint8_t *)malloc(E + 16);
+        if (!B->code || !B->qual) { delete B; return fail("spp_synth_batch: out of host memory"); }
+        memset(B->code + E, 0xFF, 16);
+        memset(B->qual + E, 0, 16);
+        // quality -> error probability, the discrete q distribution (clip(round(N(mean, sd))))
+        double eps[256];
+        for (int q = 0; q < 256; q++) eps[q] = std::pow(10.0, -q / 10.0);
+        const int nt = std::max(1, p->n_threads);
+        const int64_t blk = 4096;                  // columns per RNG stream: deterministic for any nt
+        const int64_t nblk = (C + blk - 1) / blk;
+        std::atomic<int64_t> next{0};
+        auto work = [&]() {
+            static const uint8_t ACGT[4] = {1, 2, 4, 8};
+            for (int64_t bi; (bi = next++) < nblk;) {
+                std::mt19937_64 rng(p->seed * 0x9E3779B97F4A7C15ull + (uint64_t)bi * 7919u + 17u);
+                std::uniform_real_distribution<double> U(0.0, 1.0);
+                std::normal_distribution<double> Nq(p->q_mean, p->q_sd);
+                const double del_rate = p->del_frac * 2.0 / (double)R;
+                for (int64_t c = bi * blk; c < std::min(C, (bi + 1) * blk); c++) {
+                    const int64_t col = lo + c;
+                    const char rc = (char)toupper(ref_seq[col]);
+                    const int ri = rc == 'A' ? 0 : rc == 'C' ? 1 : rc == 'G' ? 2 : rc == 'T' ? 3 : -1;
+                    const bool planted = p->snv_every > 0 && col % p->snv_every == p->snv_every / 2 && ri >= 0;
+                    static const double afs[4] = {1.0, 0.5, 0.2, 0.05};
+                    const double af = planted ? afs[(col / p->snv_every) % 4] : 0.0;
+                    const uint8_t alt = planted ? ACGT[(ri + 1 + (int)(col % 3)) % 4] : 0;
+                    for (uint64_t e = B->off[(size_t)c]; e < B->off[(size_t)c + 1]; e++) {
+                        uint8_t b = ri >= 0 ? ACGT[ri] : 15;
+                        if (planted && U(rng) < af) b = alt;
+                        int q = (int)std::lround(Nq(rng));
+                        q = std::min(std::max(q, p->q_min), p->q_max);
+                        if (b != 15 && U(rng) < eps[q]) {
+                            const int bi2 = b == 1 ? 0 : b == 2 ? 1 : b == 4 ? 2 : 3;
+                            b = ACGT[(bi2 + 1 + (int)(rng() % 3)) % 4];
+                        }
+                        if (U(rng) < p->n_rate) b = 15;
+                        if (U(rng) < del_rate) b = 16;
+                        B->code[e] = b;
+                        B->qual[e] = (uint8_t)q;
+                    }
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nt; t++) pool.emplace_back(work);
+        work();
+        for (auto &t : pool) t.join();
+        *out = B;
+        return 0;
+    } catch (const std::exception &e) {
+        return fail(std::string("spp_synth_batch: ") + e.what());
+    }
+}

@@ -137,3 +137,21 @@ def simulate_bam(path: str, contig: str, reference: str, depth: float, seed: int
     N.pcheck(L.spp_simulate_bam(str(path).encode(), contig.encode(), ref, len(ref), C.byref(p), C.byref(n)),
              "spp_simulate_bam")
     return n.value
+
+
+def synth_batch(reference: str, depth: float, lo: int = 0, hi: int | None = None, seed: int = 2, n_threads: int = 16,
+                max_depth: int = 0, **kw) -> PileupBatch:
+    """Synthetic CSR pileup of columns [lo, hi) generated natively (spp_synth_batch): the read model
+    of SURVEY §8 d at column level, for configs too large for numpy (100,000x, chr1 30x)."""
+    L = N.pileup_lib()
+    p = N.SimParams()
+    L.spp_default_sim_params(C.byref(p))
+    p.depth, p.seed, p.n_threads = float(depth), int(seed), int(n_threads)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    ref = reference.encode()
+    hi = len(ref) if hi is None else hi
+    b = C.c_void_p()
+    N.pcheck(L.spp_synth_batch(ref, len(ref), int(lo), int(hi), C.byref(p), int(max_depth), C.byref(b)),
+             "spp_synth_batch")
+    return PileupBatch(b.value)

@@ -20,7 +20,7 @@ CODE_OF = {"A": 1, "C": 2, "G": 4, "T": 8, "N": 15}
 
 def reference(L: int, seed: int = 1) -> str:
     rng = np.random.default_rng(seed)
-    return "".join(np.array(list("ACGT"))[rng.integers(0, 4, size=L)].tolist())
+    return np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size=L)].tobytes().decode("ascii")
 
 
 def pileup(L: int, depth: float, seed: int = 2, read_len: int = 150, ref: str | None = None,

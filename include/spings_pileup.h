@@ -92,6 +92,14 @@ void spp_default_sim_params(spp_sim_params *p);
 int spp_simulate_bam(const char *path, const char *contig, const char *ref_seq, int64_t ref_len,
                      const spp_sim_params *p, int64_t *n_reads_out);
 
+/* Synthetic pileup straight to CSR (no BAM), for the large benchmark configs (100,000x, chr1 30x):
+ * the read model of spp_simulate_bam at column level — reads of read_len start uniformly (sorted),
+ * column c holds the reads covering it in start order; per entry q, sequencing error, N and planted
+ * SNVs as above, CIGAR D entries (code 16, quality of the next base) at rate del_frac*2/read_len.
+ * Columns [lo, hi) of a reference of ref_len; multi-threaded, deterministic for a seed. */
+int spp_synth_batch(const char *ref_seq, int64_t ref_len, int64_t lo, int64_t hi, const spp_sim_params *p,
+                    int64_t max_depth, spp_batch **out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -149,3 +149,20 @@ def test_simulated_bam_vs_port(tmp_path):
     pb, off, codes, quals = product(bam, "chrS", max_depth=0)
     assert (codes == 16).sum() > 0 and set(np.unique(codes).tolist()) <= {1, 2, 4, 8, 15, 16}
     assert 2 <= quals.min() and quals.max() <= 41
+
+
+def test_synth_batch_deterministic_and_shaped():
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.pileup import synth_batch
+    ref = synth.reference(5000, seed=3)
+    a = synth_batch(ref, 200, lo=100, hi=4900, seed=5, n_threads=1)
+    b = synth_batch(ref, 200, lo=100, hi=4900, seed=5, n_threads=7)
+    assert a.pos_begin == 100 and a.n_cols == 4800
+    np.testing.assert_array_equal(a.offsets, b.offsets)
+    np.testing.assert_array_equal(a.codes, b.codes)
+    np.testing.assert_array_equal(a.quals, b.quals)
+    depth = np.diff(a.offsets.astype(np.int64))
+    assert 150 < depth.mean() < 250
+    assert set(np.unique(a.codes).tolist()) <= {1, 2, 4, 8, 15, 16}
+    capped = synth_batch(ref, 200, lo=100, hi=4900, seed=5, n_threads=2, max_depth=50)
+    assert np.diff(capped.offsets.astype(np.int64)).max() <= 50
