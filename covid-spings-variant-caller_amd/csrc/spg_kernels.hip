@@ -169,16 +169,33 @@ __device__ void merge_acc(Acc *__restrict__ A, const ColState &c, uint32_t batch
         if (c.cnt[k]) {
             if (a.cnt[k] == 0) a.qf[k] = (uint8_t)c.qf[k];
             else a.qf[k] = (uint8_t)min((uint32_t)a.qf[k], c.qf[k]);
+            const bool had = a.cnt[k] != 0;      // absent slots' sums may hold stale bytes
             a.cnt[k] += c.cnt[k];
             const uint64_t s = (uint64_t)a.sq[k] + c.sq[k];
             a.sq[k] = s > 0x80000000ull ? 0x80000000u : (uint32_t)s;
-            a.sl[k] += c.sl[k];
-            a.se[k] += c.se[k];
+            a.sl[k] = had ? a.sl[k] + c.sl[k] : c.sl[k];
+            a.se[k] = had ? a.se[k] + c.se[k] : c.se[k];
             if (!((have >> k) & 1u)) newmask |= 1u << k;
         }
     }
     a.order = merge_order(a.order, newmask, c.first);
-    *A = a;
+    if (!fresh) {
+        *A = a;
+        return;
+    }
+    // FRESH record: sl/se (bytes 80..159) are read only for slots that hold sums; a column whose
+    // present slots all skipped them (calls-only REF) writes 80 bytes instead of 160
+    bool sums = false;
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) sums |= c.cnt[k] != 0 && !((skip >> k) & 1u);
+    const uint4 *src = reinterpret_cast<const uint4 *>(&a);
+    uint4 *dst = reinterpret_cast<uint4 *>(A);
+#pragma unroll
+    for (int i = 0; i < 5; i++) dst[i] = src[i];
+    if (sums) {
+#pragma unroll
+        for (int i = 5; i < 10; i++) dst[i] = src[i];
+    }
 }
 
 // ------------------------------------------------------------------------------------------

@@ -78,8 +78,8 @@ def test_band_case_is_replayed_exactly():
                 assert t["flags"][pos] & 4, pos
 
 
-def _vs_oracle(reference, batches, p, check_mem=True, calls_only=False):
-    eng = _engine(reference, p, calls_only=calls_only)
+def _vs_oracle(reference, batches, p, check_mem=True, calls_only=False, eng=None):
+    eng = eng if eng is not None else _engine(reference, p, calls_only=calls_only)
     orc = COracle(reference, p["minBaseQuality"], p["minTotalDepth"], p["minAlleleDepth"], p["minEvidenceRatio"])
     for pb, off, c, q in batches:
         eng.accumulate(pb, off, c, q)
@@ -160,13 +160,32 @@ def test_min_base_quality_sweep(bq):
     _vs_oracle(ref, [(lo, off, c, q)], dict(DEF, minBaseQuality=bq, minEvidenceRatio=0.02, minAlleleDepth=2))
 
 
-def test_multibatch_accumulation_and_order():
+@pytest.mark.parametrize("calls_only", [False, True])
+def test_multibatch_accumulation_and_order(calls_only):
     from covid_spings_variant_caller_amd import synth
     L = 5000
     ref = synth.reference(L, seed=10)
     batches = [synth.pileup(L, 300, seed=20 + i, ref=ref, snv_every=17, lo=lo, hi=hi)
                for i, (lo, hi) in enumerate([(2000, 4000), (0, 2500), (3500, 5000), (1000, 1200)])]
-    _vs_oracle(ref, batches, DEF)
+    _vs_oracle(ref, batches, DEF, calls_only=calls_only)
+
+
+@pytest.mark.parametrize("calls_only", [False, True])
+def test_shallow_then_deep_then_shallow(calls_only):
+    """Lane-kernel (shallow) FRESH records written partially, then merged by the deep kernel and the
+    lane kernel again: stale bytes of absent slots must never leak into the sums."""
+    from covid_spings_variant_caller_amd import synth
+    L = 3000
+    ref = synth.reference(L, seed=40)
+    batches = [synth.pileup(L, 30, seed=41, ref=ref, snv_every=13, lo=0, hi=2000, read_len=40),
+               synth.pileup(L, 3000, seed=42, ref=ref, snv_every=13, lo=500, hi=2500, read_len=60),
+               synth.pileup(L, 20, seed=43, ref=ref, snv_every=13, lo=1000, hi=3000, read_len=40)]
+    # a first epoch leaves stale records behind (reset is an epoch bump, not a memset)
+    eng = _engine(ref, DEF, calls_only=calls_only)
+    eng.accumulate(*synth.pileup(L, 500, seed=44, ref=ref, snv_every=7, lo=0, hi=L))
+    eng.finalize()
+    eng.reset()
+    _vs_oracle(ref, batches, DEF, calls_only=calls_only, eng=eng)
 
 
 def test_device_borrowed_input_matches_host_input():
