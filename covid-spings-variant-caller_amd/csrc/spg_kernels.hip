@@ -1,17 +1,20 @@
 // spg_kernels.hip — CDNA4 (gfx950) kernels of the pileup + genotype-likelihood engine.
 //
-//   k_acc_deep<W>  process_pileup_column / process_svn (live_variant_caller.py:74-103) + pysam's
-//                  base-quality filter for one CSR batch, one wave64 per column: coalesced dwordx4
-//                  (W=4) or dword (W=1) loads of base_code and qual two steps ahead, SWAR byte tests,
-//                  v_dot4_u32_u8 quality sums, v_bcnt counts and an LDS {ln(1-eps), eps} table for the
-//                  column's major allele; the rare entries (minor alleles, D/N, q < 4, q >= 128, IUPAC)
-//                  go exactly, one by one, into a per-wave LDS record (LDS atomics).
-//   k_acc_shallow  the same for short columns, one lane per column, sequential.
+//   k_acc_seg<W,FRESH>  process_pileup_column / process_svn (live_variant_caller.py:74-103) + pysam's
+//                  base-quality filter for one CSR batch: a wave64 owns G consecutive columns and
+//                  streams them as one sequence of 64 x 4W-entry chunks (buffer loads two chunks ahead,
+//                  column descriptors in LDS behind scalar cursors).  SWAR byte tests classify 4
+//                  entries per dword; the column's major (and, when frequent, second) allele takes the
+//                  fast path (v_bcnt counts, v_dot4_u32_u8 quality sums, LDS {ln(1-eps), eps} table);
+//                  the rare entries (other alleles, D/N, q < 4, q >= 128, IUPAC) are queued as lane
+//                  slices and decoded exactly into a per-wave LDS record at column end.
+//   k_acc_shallow  short columns (< t_deep entries), one lane per column, SWAR against the REF allele.
 //   k_finalize     prepare_variants (:120-185) + genotype_likelihood / to_phred_scale
 //                  (utils.py:12-24): per-position GL in fp64 with the reference's underflow decisions,
 //                  candidate filters, GL/PL/SCORE/QUAL.  A position whose result depends on the order
-//                  of fp64 roundings in the subnormal range (or that holds IUPAC alleles) is recomputed
-//                  exactly by walking the batch history (np.prod left folds in BAM order).
+//                  of fp64 roundings in the subnormal range (or that holds IUPAC alleles, or whose calls
+//                  need terms calls-only mode did not accumulate) is recomputed exactly by walking the
+//                  batch history (np.prod left folds in BAM order).
 #include <type_traits>
 
 #include "spg_device.h"
@@ -36,43 +39,9 @@ __device__ __forceinline__ void cs_init(ColState &s) {
     }
 }
 
-// One pileup entry that passed the base-quality filter (:89-103).
-__device__ __forceinline__ void entry_update(ColState &s, uint32_t code, uint32_t q, uint32_t idx,
-                                             const Tables *__restrict__ T) {
-    s.depth++;
-    if (code == SPG_CODE_DEL) { s.n_del++; return; }
-    if (code == SPG_CODE_SKIP) { s.n_skip++; return; }
-    const int sl = slot_of(code);
-    if (sl < 0) { s.n_other++; return; }
-    const double l = T->l1m[q], e = T->eps[q];
-#pragma unroll
-    for (int k = 0; k < NSLOT; k++) {
-        if (sl == k) {
-            s.cnt[k] += 1u; s.sq[k] += q; s.qf[k] = min(s.qf[k], q); s.first[k] = min(s.first[k], idx);
-            s.sl[k] += l; s.se[k] += e;
-        }
-    }
-}
-
 // ------------------------------------------------------------------------------------------
-// wave64 reductions (butterfly; every lane ends with the result)
+// wave helpers
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wsum(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-__device__ __forceinline__ uint32_t wmin(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor(v, o));
-    return v;
-}
-__device__ __forceinline__ double wsumd(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -95,12 +64,6 @@ __device__ __forceinline__ uint32_t dsum_u32(uint32_t v) {
     for (int c = 0; c < 4; c++) v += dpp_u32(v, c);
     return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
            __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
-}
-__device__ __forceinline__ uint32_t dmin_u32(uint32_t v) {
-#pragma unroll
-    for (int c = 0; c < 4; c++) v = min(v, dpp_u32(v, c));
-    return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
-               min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
 }
 __device__ __forceinline__ double rl_f64(double v, int l) {
     const uint64_t b = __builtin_bit_cast(uint64_t, v);

@@ -325,3 +325,19 @@ def test_calls_only_mode_matches_oracle(case):
         o.accumulate(*b1)
         o.accumulate(*b2)
         compare_variants(eng.variants(), o.prepare_variants(), RTOL)
+
+
+def test_many_bams_accumulated():
+    """BASELINE config 4 in miniature: 64 BAM-sized batches (100x, own seeds, pysam-style per-BAM
+    depth cap) accumulated in one context — memory insertion order, first visits, dict order and
+    calls vs the oracle."""
+    from covid_spings_variant_caller_amd import synth
+    L = 2500
+    ref = synth.reference(L, seed=50)
+    batches = []
+    for i in range(64):
+        lo = (i * 37) % 900
+        batches.append(synth.pileup(L, 100, seed=1000 + i, ref=ref, snv_every=23, lo=lo, hi=min(L, lo + 1600),
+                                    max_depth=80))
+    for calls_only in (False, True):
+        _vs_oracle(ref, batches, DEF, calls_only=calls_only)
