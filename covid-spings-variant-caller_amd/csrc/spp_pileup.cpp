@@ -12,6 +12,7 @@
 // parity unpinned; oracle/pileup_port.py is the independent restatement the tests compare with).
 #include "spings_pileup.h"
 
+#include <sys/mman.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -19,6 +20,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <exception>
 #include <queue>
 #include <random>
 #include <cmath>
@@ -59,16 +62,56 @@ struct Nt16 {
     }
 } const NT16;
 
+// resize() without value-initialisation: the parallel decoders write every element, and the first
+// touch of fresh pages then happens on those threads rather than in a serial zero fill.
+template <class T>
+struct NoInit : std::allocator<T> {
+    template <class U> struct rebind { using other = NoInit<U>; };
+    NoInit() = default;
+    template <class U> NoInit(const NoInit<U> &) {}
+    template <class U, class... A> void construct(U *p, A &&...a) {
+        if constexpr (sizeof...(A) == 0) ::new ((void *)p) U;
+        else ::new ((void *)p) U(std::forward<A>(a)...);
+    }
+};
+template <class T> using Vec = std::vector<T, NoInit<T>>;
+
 struct Reads {                 // one contig's reads, structure of arrays
-    std::vector<int64_t> pos, end, mpos, isize;
-    std::vector<int32_t> mtid;
-    std::vector<uint16_t> flag;
-    std::vector<uint8_t> mapq;
-    std::vector<uint64_t> cig_off, seq_off, name_off;
-    std::vector<uint32_t> n_cig, l_seq;
-    std::vector<uint32_t> cigar;
-    std::vector<uint8_t> seq, qual;   // one nibble code / quality per query base
-    std::vector<char> names;
+    Vec<int64_t> pos, end, mpos, isize;
+    Vec<int32_t> mtid;
+    Vec<uint16_t> flag;
+    Vec<uint8_t> mapq;
+    Vec<uint64_t> cig_off, name_off;
+    Vec<uint32_t> n_cig, l_seq;
+    Vec<uint32_t> cigar;
+    Vec<uint8_t *> bases;     // per read: l_seq nibble codes, then l_seq qualities (in `arena`)
+    Vec<char> names;
+    // bases storage: 2 MiB-aligned blocks (transparent huge pages requested), never moved, so the
+    // decoders can fill a window's records in parallel without a serial grow-and-copy
+    struct Arena {
+        std::vector<uint8_t *> blocks;
+        uint8_t *cur = nullptr;
+        size_t left = 0;
+        ~Arena() {
+            for (uint8_t *b : blocks) free(b);
+        }
+        uint8_t *alloc(size_t n) {
+            if (n > left) {
+                const size_t sz = std::max<size_t>(n + (2u << 20) - 1, 64u << 20) & ~(size_t)((2u << 20) - 1);
+                cur = (uint8_t *)aligned_alloc(2u << 20, sz);
+                if (!cur) throw std::runtime_error("out of host memory for the reads");
+                madvise(cur, sz, MADV_HUGEPAGE);
+                blocks.push_back(cur);
+                left = sz;
+            }
+            uint8_t *r = cur;
+            cur += n;
+            left -= n;
+            return r;
+        }
+    } arena;
+    uint8_t *seq(size_t r) const { return bases[r]; }
+    uint8_t *qual(size_t r) const { return bases[r] + l_seq[r]; }
     size_t size() const { return pos.size(); }
 };
 
@@ -100,24 +143,28 @@ struct spp_batch {
 
 namespace {
 
+
 // ---------------------------------------------------------------------------------------------
 // BGZF: blocks are independent raw-deflate members; inflate a window of blocks in parallel.
 // ---------------------------------------------------------------------------------------------
 class BgzfReader {
   public:
     BgzfReader(const std::string &path, int threads) : threads_(std::max(1, threads)) {
+        // SPP_BGZF_WINDOW (bytes, >= 65554): a smaller read window, for the boundary tests
+        if (const char *w = getenv("SPP_BGZF_WINDOW")) window_ = std::max<size_t>(strtoull(w, nullptr, 10), 65554);
         f_ = fopen(path.c_str(), "rb");
         if (!f_) throw std::runtime_error("cannot open " + path);
     }
     ~BgzfReader() {
         if (f_) fclose(f_);
     }
-    // Append the next window of decompressed bytes to `out`; false at EOF.
-    bool next(std::vector<uint8_t> &out) {
-        std::vector<uint8_t> comp(kWindow);
+    // Inflate the next window of blocks into out[gap:] (out is resized); false at EOF.
+    bool next(Vec<uint8_t> &out, size_t gap) {
+        Vec<uint8_t> &comp = comp_;
+        comp.resize(window_);
         size_t n = carry_.size();
         std::copy(carry_.begin(), carry_.end(), comp.begin());
-        n += fread(comp.data() + n, 1, kWindow - n, f_);
+        n += fread(comp.data() + n, 1, window_ - n, f_);
         if (n == 0) return false;
         struct Blk { size_t off, clen, ulen; };
         std::vector<Blk> blks;
@@ -149,7 +196,7 @@ class BgzfReader {
         carry_.assign(comp.begin() + p, comp.begin() + n);
         std::vector<size_t> uoff(blks.size() + 1, 0);
         for (size_t i = 0; i < blks.size(); i++) uoff[i + 1] = uoff[i] + blks[i].ulen;
-        const size_t base = out.size();
+        const size_t base = gap;
         out.resize(base + uoff.back());
         std::atomic<size_t> next_blk{0};
         std::atomic<bool> bad{false};
@@ -178,33 +225,70 @@ class BgzfReader {
     }
 
   private:
-    static constexpr size_t kWindow = 16u << 20;
+    size_t window_ = 16u << 20;      // compressed bytes read per window
     FILE *f_ = nullptr;
     int threads_;
     std::vector<uint8_t> carry_;
+    Vec<uint8_t> comp_;
 };
 
-// Sequential byte source over the decompressed BAM stream.
+// Byte source over the decompressed BAM stream.  The next window is inflated on a helper thread
+// while the caller parses the current one (refill() joins it); windows are inflated behind a
+// kGap-byte head room into which the unparsed tail of the previous window (a partial record) is
+// copied, so a refill swaps buffers instead of moving the window.
 class BamStream {
   public:
-    BamStream(const std::string &path, int threads) : z_(path, threads) {}
+    BamStream(const std::string &path, int threads) : z_(path, threads) { launch(); }
+    ~BamStream() {
+        if (pending_.joinable()) pending_.join();
+    }
+    size_t avail() const { return buf_.size() - cur_; }
     bool need(size_t n) {            // ensure n bytes available at cur_
-        while (buf_.size() - cur_ < n) {
-            if (cur_ > (64u << 20)) {
-                buf_.erase(buf_.begin(), buf_.begin() + (ptrdiff_t)cur_);
-                cur_ = 0;
-            }
-            if (!z_.next(buf_)) return false;
+        while (avail() < n)
+            if (!refill()) return false;
+        return true;
+    }
+    // Append the next inflated window (dropping the consumed prefix); false at EOF.  Pointers
+    // from ptr() are invalidated.
+    bool refill() {
+        pending_.join();
+        if (err_) std::rethrow_exception(err_);
+        if (!more_) return false;
+        const size_t carry = avail();
+        if (carry <= kGap) {
+            memcpy(next_.data() + kGap - carry, ptr(), carry);
+            buf_.swap(next_);
+            cur_ = kGap - carry;
+        } else {                        // a record longer than the head room: concatenate
+            Vec<uint8_t> joined(carry + next_.size() - kGap);
+            memcpy(joined.data(), ptr(), carry);
+            memcpy(joined.data() + carry, next_.data() + kGap, next_.size() - kGap);
+            buf_.swap(joined);
+            cur_ = 0;
         }
+        launch();
         return true;
     }
     const uint8_t *ptr() const { return buf_.data() + cur_; }
     void skip(size_t n) { cur_ += n; }
 
   private:
+    void launch() {
+        pending_ = std::thread([this] {
+            try {
+                more_ = z_.next(next_, kGap);
+            } catch (...) {
+                err_ = std::current_exception();
+            }
+        });
+    }
+    static constexpr size_t kGap = 1u << 20;
     BgzfReader z_;
-    std::vector<uint8_t> buf_;
+    Vec<uint8_t> buf_, next_;
     size_t cur_ = 0;
+    bool more_ = false;
+    std::exception_ptr err_;
+    std::thread pending_;
 };
 
 inline int32_t rd32(const uint8_t *p) { int32_t v; memcpy(&v, p, 4); return v; }
@@ -277,43 +361,91 @@ bool stepper_keeps(const spp_params &p, uint16_t flag, uint8_t mapq) {
     return true;
 }
 
+// BAM records: the complete records of each inflated window are located serially (block_size
+// hops; contig, sort order and the stepper filter read from the fixed header), then decoded into
+// the Reads arrays in parallel.
 void read_bam(const spp_file *f, int32_t tid, const spp_params &p, Reads &R) {
-    BamStream s(f->path, p.n_threads);
+    const int nt = std::max(1, std::min(p.n_threads, 64));
+    BamStream s(f->path, nt);
     spp_file tmp;
     bam_header(s, &tmp);
+    // two 4-bit codes per packed byte, high nibble first
+    static const auto pair_tab = [] {
+        std::vector<uint16_t> t(256);
+        for (int v = 0; v < 256; v++) t[(size_t)v] = (uint16_t)((v >> 4) | ((v & 0xF) << 8));
+        return t;
+    }();
     int64_t last_pos = -1;
-    while (s.need(4)) {
-        const uint32_t bs = rdu32(s.ptr());
-        if (!s.need(4 + (size_t)bs)) throw std::runtime_error("truncated BAM record");
-        const uint8_t *b = s.ptr() + 4;
-        const int32_t rtid = rd32(b);
-        const int64_t pos = rd32(b + 4);
-        const uint8_t l_name = b[8], mapq = b[9];
-        const uint16_t n_cig = rdu16(b + 12), flag = rdu16(b + 14);
-        const int32_t l_seq = rd32(b + 16), mtid = rd32(b + 20);
-        const int64_t mpos = rd32(b + 24), isize = rd32(b + 28);
-        if (rtid == tid) {
-            if (pos < last_pos) throw std::runtime_error("BAM is not coordinate-sorted");
-            last_pos = pos;
-            if (stepper_keeps(p, flag, mapq)) {
-                const uint8_t *name = b + 32;
-                std::vector<uint32_t> cig(n_cig);
-                memcpy(cig.data(), name + l_name, 4u * n_cig);
-                push_read(R, pos, flag, mapq, mtid, mpos, isize, cig.data(), n_cig, (const char *)name,
-                          l_name ? l_name - 1u : 0u);
-                const uint8_t *sq = name + l_name + 4u * n_cig;
-                const uint8_t *ql = sq + (l_seq + 1) / 2;
-                const size_t so = R.seq.size();
-                R.seq_off.push_back(so);
-                R.l_seq.push_back((uint32_t)l_seq);
-                R.seq.resize(so + (size_t)l_seq);
-                uint8_t *dst = R.seq.data() + so;
-                for (int32_t i = 0; i < l_seq; i++) dst[i] = (sq[i >> 1] >> ((~i & 1) << 2)) & 0xF;
-                R.qual.insert(R.qual.end(), ql, ql + l_seq);
+    std::vector<const uint8_t *> recs;
+    for (;;) {
+        recs.clear();
+        while (s.avail() >= 4) {
+            const uint32_t bs = rdu32(s.ptr());
+            if (s.avail() < 4 + (size_t)bs) break;
+            const uint8_t *b = s.ptr() + 4;
+            if (bs < 32) throw std::runtime_error("truncated BAM record");
+            if (rd32(b) == tid) {
+                const int64_t pos = rd32(b + 4);
+                if (pos < last_pos) throw std::runtime_error("BAM is not coordinate-sorted");
+                last_pos = pos;
+                if (stepper_keeps(p, rdu16(b + 14), b[9])) recs.push_back(b);
             }
+            s.skip(4 + (size_t)bs);
         }
-        s.skip(4 + (size_t)bs);
+        const size_t k = recs.size(), n0 = R.size();
+        if (k) {
+            // per-read offsets into the variable-length arrays (serial prefix sums)
+            R.pos.resize(n0 + k); R.end.resize(n0 + k); R.flag.resize(n0 + k); R.mapq.resize(n0 + k);
+            R.mtid.resize(n0 + k); R.mpos.resize(n0 + k); R.isize.resize(n0 + k);
+            R.cig_off.resize(n0 + k); R.n_cig.resize(n0 + k); R.name_off.resize(n0 + k);
+            R.bases.resize(n0 + k); R.l_seq.resize(n0 + k);
+            size_t co = R.cigar.size(), so = 0, no = R.names.size();
+            for (size_t i = 0; i < k; i++) {
+                const uint8_t *b = recs[i];
+                const uint32_t n_cig = rdu16(b + 12), l_seq = (uint32_t)rd32(b + 16), l_name = b[8];
+                R.cig_off[n0 + i] = co; R.n_cig[n0 + i] = n_cig; co += n_cig;
+                R.l_seq[n0 + i] = l_seq; so += 2 * (size_t)l_seq;
+                R.name_off[n0 + i] = no; no += (l_name ? l_name - 1u : 0u) + 1u;
+            }
+            R.cigar.resize(co); R.names.resize(no);
+            uint8_t *bp = R.arena.alloc(so);
+            for (size_t i = 0; i < k; i++) { R.bases[n0 + i] = bp; bp += 2 * (size_t)R.l_seq[n0 + i]; }
+            auto work = [&](size_t i0, size_t i1) {
+                for (size_t i = i0; i < i1; i++) {
+                    const uint8_t *b = recs[i];
+                    const size_t r = n0 + i;
+                    const uint8_t l_name = b[8];
+                    const uint32_t n_cig = R.n_cig[r], l_seq = R.l_seq[r];
+                    R.pos[r] = rd32(b + 4);
+                    R.mapq[r] = b[9];
+                    R.flag[r] = rdu16(b + 14);
+                    R.mtid[r] = rd32(b + 20);
+                    R.mpos[r] = rd32(b + 24);
+                    R.isize[r] = rd32(b + 28);
+                    const uint8_t *name = b + 32;
+                    const size_t ln = l_name ? l_name - 1u : 0u;
+                    memcpy(R.names.data() + R.name_off[r], name, ln);
+                    R.names[R.name_off[r] + ln] = '\0';
+                    uint32_t *cg = R.cigar.data() + R.cig_off[r];
+                    memcpy(cg, name + l_name, 4u * n_cig);
+                    R.end[r] = R.pos[r] + ref_len(cg, n_cig);
+                    const uint8_t *sq = name + l_name + 4u * n_cig;
+                    const uint8_t *ql = sq + (l_seq + 1) / 2;
+                    uint8_t *dst = R.seq(r);
+                    for (uint32_t j = 0; j < l_seq / 2; j++) memcpy(dst + 2 * j, &pair_tab[sq[j]], 2);
+                    if (l_seq & 1) dst[l_seq - 1] = sq[l_seq / 2] >> 4;
+                    memcpy(R.qual(r), ql, l_seq);
+                }
+            };
+            const size_t nw = std::min<size_t>((size_t)nt, (k + 4095) / 4096);
+            std::vector<std::thread> pool;
+            for (size_t t = 1; t < nw; t++) pool.emplace_back(work, k * t / nw, k * (t + 1) / nw);
+            work(0, nw ? k / nw : k);
+            for (auto &t : pool) t.join();
+        }
+        if (!s.refill()) break;
     }
+    if (s.avail()) throw std::runtime_error("truncated BAM record");
 }
 
 void sam_header_line(spp_file *f, const std::string &line) {
@@ -401,12 +533,13 @@ void read_sam(const spp_file *f, int32_t tid, const spp_params &p, Reads &R) {
         push_read(R, pos, flag, mapq, mtid, mpos, isize, cig.data(), (uint32_t)cig.size(), fld[0], len[0]);
         const bool noseq = len[9] == 1 && fld[9][0] == '*';
         const uint32_t l_seq = noseq ? 0u : (uint32_t)len[9];
-        R.seq_off.push_back(R.seq.size());
         R.l_seq.push_back(l_seq);
-        for (uint32_t i = 0; i < l_seq; i++) R.seq.push_back(NT16.t[(uint8_t)fld[9][i]]);
+        uint8_t *bp = R.arena.alloc(2 * (size_t)l_seq);
+        R.bases.push_back(bp);
+        for (uint32_t i = 0; i < l_seq; i++) bp[i] = NT16.t[(uint8_t)fld[9][i]];
         const bool noq = len[10] == 1 && fld[10][0] == '*';
         if (!noq && len[10] != l_seq) throw std::runtime_error("SAM QUAL length differs from SEQ");
-        for (uint32_t i = 0; i < l_seq; i++) R.qual.push_back(noq ? 0xFF : (uint8_t)(fld[10][i] - 33));
+        for (uint32_t i = 0; i < l_seq; i++) bp[l_seq + i] = noq ? 0xFF : (uint8_t)(fld[10][i] - 33);
         return true;
     });
 }
@@ -436,8 +569,8 @@ void tweak_overlap(Reads &R, size_t a, size_t b) {
         if (pb[j].first < pa[i].first) { j++; continue; }
         const uint32_t ia = pa[i].second, ib = pb[j].second;
         if (ia >= R.l_seq[a] || ib >= R.l_seq[b]) return;
-        uint8_t &qa = R.qual[R.seq_off[a] + ia], &qb = R.qual[R.seq_off[b] + ib];
-        if (R.seq[R.seq_off[a] + ia] == R.seq[R.seq_off[b] + ib]) {
+        uint8_t &qa = R.qual(a)[ia], &qb = R.qual(b)[ib];
+        if (R.seq(a)[ia] == R.seq(b)[ib]) {
             const int q = qa + qb;
             qa = (uint8_t)(q > 200 ? 200 : q);
             qb = 0;
@@ -462,6 +595,31 @@ struct Tweaks {
     std::unordered_map<size_t, std::vector<uint8_t>> orig;      // first mate -> qualities before
 };
 
+// Min-queue of (end, read) for the live buffer.  Reads arrive in start order, so their ends are
+// mostly non-decreasing (equal-length reads): those go to a FIFO, the rest to a heap.  The order
+// among equal ends is immaterial (scan frees every read with end <= col).
+struct EndQueue {
+    using E = std::pair<int64_t, size_t>;
+    std::deque<E> fifo;
+    std::priority_queue<E, std::vector<E>, std::greater<E>> heap;
+    size_t size() const { return fifo.size() + heap.size(); }
+    bool empty() const { return fifo.empty() && heap.empty(); }
+    void emplace(int64_t end, size_t r) {
+        if (fifo.empty() || fifo.back().first <= end) fifo.emplace_back(end, r);
+        else heap.emplace(end, r);
+    }
+    const E &top() const {
+        if (heap.empty()) return fifo.front();
+        if (fifo.empty()) return heap.top();
+        return heap.top().first < fifo.front().first ? heap.top() : fifo.front();
+    }
+    void pop() {
+        if (heap.empty()) fifo.pop_front();
+        else if (fifo.empty() || heap.top().first < fifo.front().first) heap.pop();
+        else fifo.pop_front();
+    }
+};
+
 // Replay of bam_plp_push / bam_plp_next: which reads enter the buffer (maxcnt) and the overlap
 // pairing.  Returns keep[r].
 std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks &T) {
@@ -470,8 +628,7 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
     T.col.assign(n, INT64_MAX);
     const int64_t maxcnt = p.max_depth > 0 ? p.max_depth : INT64_MAX;
     // live buffer: reads pushed and not yet freed.  Freed while scanning column c when end <= c.
-    std::priority_queue<std::pair<int64_t, size_t>, std::vector<std::pair<int64_t, size_t>>,
-                        std::greater<std::pair<int64_t, size_t>>> by_end;
+    EndQueue by_end;
     std::vector<uint8_t> freed(n, 0);
     size_t head = 0;                          // oldest pushed read not yet freed (list head)
     std::vector<size_t> pushed;               // kept reads in push order
@@ -527,8 +684,7 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
                         if (R.mpos[r] >= R.pos[r] || ((fl & F_PAIRED) && R.mpos[r] == -1)) olap.emplace(nm, r);
                     } else {
                         const size_t a = itr->second;
-                        T.orig.emplace(a, std::vector<uint8_t>(R.qual.begin() + (ptrdiff_t)R.seq_off[a],
-                                                               R.qual.begin() + (ptrdiff_t)(R.seq_off[a] + R.l_seq[a])));
+                        T.orig.emplace(a, std::vector<uint8_t>(R.qual(a), R.qual(a) + R.l_seq[a]));
                         T.col[a] = it_pos;
                         tweak_overlap(R, a, r);
                         olap.erase(itr);
@@ -588,7 +744,7 @@ void fill_csr(const Reads &R, const std::vector<uint8_t> &keep, const Tweaks &T,
             int64_t x = R.pos[r];
             uint32_t y = 0;
             const uint32_t *cg = R.cigar.data() + R.cig_off[r];
-            const uint8_t *sq = R.seq.data() + R.seq_off[r], *ql = R.qual.data() + R.seq_off[r];
+            const uint8_t *sq = R.seq(r), *ql = R.qual(r);
             const uint32_t ls = R.l_seq[r];
             const int64_t tcol = T.col[r];
             const uint8_t *ql0 = tcol == INT64_MAX ? ql : T.orig.at(r).data();

@@ -166,3 +166,28 @@ def test_synth_batch_deterministic_and_shaped():
     assert set(np.unique(a.codes).tolist()) <= {1, 2, 4, 8, 15, 16}
     capped = synth_batch(ref, 200, lo=100, hi=4900, seed=5, n_threads=2, max_depth=50)
     assert np.diff(capped.offsets.astype(np.int64)).max() <= 50
+
+
+def test_bam_window_boundaries(tmp_path, monkeypatch):
+    """Records straddling the reader's inflate windows, including one longer than the 1 MiB head
+    room a window keeps for the previous window's partial record (the concatenating refill)."""
+    rng = np.random.default_rng(11)
+    L = 900_000
+    long_len = 800_000
+    recs = [dict(qname="long", flag=0, rname="c", pos=1, mapq=60, cigar=f"{long_len}M", rnext="*", pnext=0,
+                 tlen=0, seq="".join(rng.choice(list("ACGT"), long_len)),
+                 qual="".join(chr(33 + int(q)) for q in rng.integers(2, 41, long_len)))]
+    for i in range(3000):
+        p = int(rng.integers(1, L - 100))
+        recs.append(dict(qname=f"r{i}", flag=0, rname="c", pos=p, mapq=60, cigar="100M", rnext="*", pnext=0,
+                         tlen=0, seq="".join(rng.choice(list("ACGT"), 100)),
+                         qual="".join(chr(33 + int(q)) for q in rng.integers(2, 41, 100))))
+    recs.sort(key=lambda r: r["pos"])
+    sam, bam = str(tmp_path / "w.sam"), str(tmp_path / "w.bam")
+    samgen.write_sam(sam, [("c", L)], recs)
+    samgen.write_bam(bam, [("c", L)], recs, block=30000)
+    want = product(sam, "c")
+    for window in ("65554", "200000"):
+        monkeypatch.setenv("SPP_BGZF_WINDOW", window)
+        assert_same(product(bam, "c"), want)
+        assert_same(product(bam, "c", n_threads=1), want)
