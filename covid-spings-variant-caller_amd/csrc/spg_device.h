@@ -104,8 +104,9 @@ __host__ __device__ __forceinline__ uint32_t slot_code(int s) {
     return s == 0 ? 1u : s == 1 ? 2u : s == 2 ? 4u : s == 3 ? 8u : 15u;
 }
 __host__ __device__ __forceinline__ uint8_t nibble_char(uint32_t c) {
-    const char *t = "=ACMGRSVTWYHKDBN";
-    return (uint8_t)t[c & 15u];
+    // "=ACMGRSVTWYHKDBN"[c & 15] from two immediates (no memory load in the device code)
+    const uint64_t t = (c & 8u) ? 0x4E42444B48595754ull : 0x565352474D43413Dull;
+    return (uint8_t)(t >> (8u * (c & 7u)));
 }
 
 }  // namespace spg

@@ -214,7 +214,7 @@ __device__ __forceinline__ void rare_init(WaveRare *R, int lane) {
 }
 
 __device__ __forceinline__ void rare_entry(WaveRare *R, uint32_t code, uint32_t q, uint32_t idx,
-                                           const double2 *__restrict__ lut) {
+                                           const double2 *__restrict__ lut, const Tables *__restrict__ T) {
     atomicAdd(&R->depth, 1u);
     if (code == SPG_CODE_DEL) { atomicAdd(&R->n_del, 1u); return; }
     if (code == SPG_CODE_SKIP) { atomicAdd(&R->n_skip, 1u); return; }
@@ -224,7 +224,14 @@ __device__ __forceinline__ void rare_entry(WaveRare *R, uint32_t code, uint32_t 
     atomicAdd(&R->sq[sl], q);
     atomicMin(&R->qf[sl], q);
     atomicMin(&R->first[sl], idx);
-    const double2 t = lut[q < 128u ? q : q + 128u];    // {ln(1-eps), eps}; row 0 holds {0, 0}
+    // {ln(1-eps), eps}; row 0 holds {0, 0}; q >= 128 (never a fast entry) from the global table,
+    // in a branch of its own: volatile, or hipcc merges the two loads into a flat load of a selected
+    // pointer that every rare entry would pay, with a vmcnt(0) that drains the chunk prefetch
+    double2 t = lut[q & 127u];
+    if (q >= 128u) {
+        const volatile double *g = &T->fast[q][0];
+        t = make_double2(g[0], g[1]);
+    }
     atomicAdd(&R->sl[sl], t.x);
     atomicAdd(&R->se[sl], q == 0 ? 1.0 : t.y);         // eps(Q0) = 1
 }
@@ -333,14 +340,13 @@ __device__ __forceinline__ void merge_column(Acc *__restrict__ A, const WaveRare
     }
 }
 
-struct ColDesc {             // one column of a wave's segment (LDS)
-    uint32_t a, pre, n, b, e, idx, refc, pad;   // 16-B aligned first chunk, first chunk index, chunks,
-};                                              // bounds rel. to a, column within the group, REF char
+struct ColDesc {             // one column of a wave's segment (LDS, 16 B)
+    uint32_t a, pre, e;     // 4W-aligned first chunk, first chunk index, end rel. to a (chunks = ceil(e / STEP))
+    uint32_t bic;           // start rel. to a (bits 0-3) | column within the group (4-9) | REF char (10-17)
+};
 
 struct RareItem {            // one lane's chunk slice (up to 16 entries) holding rare entries
-    uint32_t c[4], q[4];
-    int32_t o;              // column-relative offset of its first entry
-    uint32_t pad[3];
+    uint32_t c[4], q[4];    // (its column-relative offset is kept beside, in rqo)
 };
 
 struct Dual2 {              // per-lane partial sums of a wave's second fast allele
@@ -362,12 +368,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     using V = typename Vec<W>::T;
     constexpr uint32_t ALIGN = 4 * W;
     constexpr uint32_t STEP = 64 * ALIGN;               // entries per chunk
-    constexpr uint32_t QCAP = 64;                      // per-wave queue of lane slices holding rare entries
+    constexpr uint32_t QCAP = 64;                      // per-wave queue of lane slices holding rare entries (>= 64:
+                                                       // a drain must leave room for every lane's slice)
     // LUT rows 0..127: {ln(1-eps), eps} for q < 128; rows 128..255: {0, 0} (the fast path's index
-    // for entries that are not fast); rows 256..383: q = 128..255 for the rare path
-    __shared__ double2 lut[384];
+    // for entries that are not fast; the rare path reads q >= 128 from the global table)
+    __shared__ double2 lut[256];
     __shared__ WaveRare rare[4];
     __shared__ RareItem rqueue[4][QCAP];
+    __shared__ int32_t rqo[4][QCAP];
     __shared__ Dual2 dual2[4];
     __shared__ Acc accimg[4];
     __shared__ ColDesc coldesc[4][64];
@@ -375,7 +383,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     {
         const uint32_t q = threadIdx.x;
         lut[q] = q < 128u ? make_double2(T->fast[q][0], T->fast[q][1]) : make_double2(0.0, 0.0);
-        if (q >= 128u) lut[q + 128u] = make_double2(T->fast[q][0], T->fast[q][1]);
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -388,6 +395,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     Acc *img = accimg + (threadIdx.x >> 6);
     ColDesc *CD = coldesc[threadIdx.x >> 6];
     RareItem *Q = rqueue[threadIdx.x >> 6];
+    int32_t *QO = rqo[threadIdx.x >> 6];
     uint32_t qn = 0;                                   // queued lane slices (wave-uniform)
     // drain the queue into the LDS record: every lane takes one entry per round (LDS atomics)
     // Drain: lane k decodes queued slice k (its rare entries are few) into the column's LDS record
@@ -404,7 +412,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         for (uint32_t b0 = 0; b0 < qn; b0 += 64) {
             if (b0 + lane < qn) {
                 const RareItem *it = Q + b0 + lane;
-                const int32_t o = it->o;
+                const int32_t o = QO[b0 + lane];
 #pragma unroll 1
                 for (int d = 0; d < W; d++) {          // rolled: one copy of the decode, data stays in LDS
                     const uint32_t cw = it->c[d], qw = it->q[d];
@@ -418,7 +426,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                         r80 &= r80 - 1;
                         const uint32_t c = (cw >> sh) & 0xFFu, q = (qw >> sh) & 0xFFu;
                         if ((int)q >= P.min_bq)
-                            rare_entry(R, c, q, (uint32_t)(o + 4 * d - bl) + (uint32_t)(sh >> 3), lut);
+                            rare_entry(R, c, q, (uint32_t)(o + 4 * d - bl) + (uint32_t)(sh >> 3), lut, T);
                     }
                 }
             }
@@ -458,7 +466,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         const uint64_t nz = __ballot(nch > 0);
         if (nch > 0) {
             const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
-            CD[k] = ColDesc{a_rel, pre, nch, b_rel - a_rel, e_rel - a_rel, (uint32_t)lane, refc, 0u};
+            CD[k] = ColDesc{a_rel, pre, e_rel - a_rel, (b_rel - a_rel) | ((uint32_t)lane << 4) | (refc << 10)};
         }
         wave_sync();
     }
@@ -467,13 +475,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         return __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t *>(CD + k)[f]);
     };
     // prefetch cursor: column of the chunk being loaded (chunk indices only grow, by one per call)
-    uint32_t pk = 0, p_a = cd(0, 0), p_pre = cd(0, 1), p_end = p_pre + cd(0, 2);
+    uint32_t pk = 0, p_a = cd(0, 0), p_pre = cd(0, 1), p_end = p_pre + (cd(0, 2) + STEP - 1) / STEP;
     auto chunk_off = [&](uint32_t i) -> uint32_t {   // chunks past the end reload the last one (ignored)
         if (i >= p_end && i < total) {
             pk++;
             p_a = cd(pk, 0);
             p_pre = cd(pk, 1);
-            p_end = p_pre + cd(pk, 2);
+            p_end = p_pre + (cd(pk, 2) + STEP - 1) / STEP;
         }
         const uint32_t ii = i < p_end ? i : p_end - 1;
         return p_a + (ii - p_pre) * STEP + lo;
@@ -498,11 +506,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         if (i == cpre + cn) {                  // next column with chunks
             ck++;
             cpre = cd(ck, 1);
-            cn = cd(ck, 2);
-            bl = (int32_t)cd(ck, 3);
-            el = (int32_t)cd(ck, 4);
-            cj = cd(ck, 5);
-            crefc = cd(ck, 6);
+            const uint32_t e = cd(ck, 2), bic = cd(ck, 3);
+            cn = (e + STEP - 1) / STEP;
+            bl = (int32_t)(bic & 15u);
+            el = (int32_t)e;
+            cj = (bic >> 4) & 63u;
+            crefc = bic >> 10;
         }
         cs = i - cpre;
         if (cs == 0) {                         // ---- column begin ----
@@ -629,7 +638,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                         it.c[d] = dw<W>(cc, d);
                         it.q[d] = dw<W>(qq, d);
                     }
-                    it.o = o;
+                    QO[slot] = o;
                 }
                 qn += n;
             }
@@ -685,6 +694,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             wave_sync();
         }
     };
+
 
     for (uint32_t i = 0; i < total; i += 3) {
         c2 = bload<W>(rc, chunk_off(i + 2)); q2 = bload<W>(rq, chunk_off(i + 2));

@@ -1,0 +1,8 @@
+set -e
+cd /root/repo
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python tools/kbench.py --tag head --calls-only --iters 40
+SPG_GPU_LIB=tools/_variants/lib_e1.so timeout -k 10 300 python tools/kbench.py --tag e1_stream_only --calls-only --iters 40

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--max-depth", type=int, default=0)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tag", default=os.environ.get("SPG_GPU_LIB", "default"))
+    ap.add_argument("--calls-only", action="store_true")
     a = ap.parse_args()
     import torch
     import spings  # noqa: F401
@@ -38,7 +39,7 @@ def main():
     torch.cuda.set_device(0)
     ref, off, c, q = data(a.depth, a.max_depth)
     do, dc, dq = synth.to_device(off, c, q)
-    eng = PileupEngine(len(off) - 1, 30, 10, 5, 0.10, device=0, reference=ref)
+    eng = PileupEngine(len(off) - 1, 30, 10, 5, 0.10, device=0, reference=ref, calls_only=a.calls_only)
     accs, fins, steps = [], [], []
     for it in range(a.iters + 3):
         t0 = time.perf_counter()
@@ -54,7 +55,7 @@ def main():
     E = len(c)
     B = 2 * E + 8 * len(off)
     acc = float(np.median(accs))
-    print(json.dumps({"tag": a.tag, "acc_ms": acc, "acc_min_ms": float(np.min(accs)), "fin_ms": float(np.median(fins)),
+    print(json.dumps({"tag": a.tag, "calls_only": a.calls_only, "acc_ms": acc, "acc_min_ms": float(np.min(accs)), "fin_ms": float(np.median(fins)),
                       "step_ms": float(np.median(steps)), "GBps": B / acc / 1e6, "frac": B / acc / 1e6 / 8000,
                       "n_cand": eng.counts()[0]}))
 
