@@ -337,6 +337,7 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
     P.G = G;
     P.t_deep = deep_batch ? 1u : 128u;
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
+    P.n_entries = n_entries;
     hipEvent_t *ev = c->ev[c->ring_w % spg_ctx::NRING];
     if (!c->acc_open) c->acc_timing = c->timing;
     const int tm = c->acc_timing;

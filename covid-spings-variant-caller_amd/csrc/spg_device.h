@@ -68,6 +68,7 @@ struct KParams {
     uint32_t G;            // columns per wave group
     uint32_t t_deep;       // columns with >= t_deep raw entries are processed wave-wide
     uint32_t calls_only;   // SPG_P_CALLS_ONLY
+    uint64_t n_entries;    // entries of the batch (launch shape only)
     Hist hdesc;            // this batch's history descriptor ...
     Hist *hslot;           // ... written here by the first thread of the launch
 };

@@ -259,37 +259,20 @@ __device__ __forceinline__ void write_hist(const KParams &P) {
 // Merge the column record R (LDS) into its Acc.  Cooperative: lane 0 writes the header and the dict
 // order, lanes 1..5 one allele slot each.  FRESH (first batch since reset): every record belongs to
 // an older epoch, so nothing is read back — the merge is pure stores.
-// FRESH merge: the record is assembled in LDS and written as ten 16-byte stores (one per lane), so
-// each column costs exactly its 160 bytes of HBM writes instead of a scatter of partial lines.
-__device__ __forceinline__ void merge_fresh(Acc *__restrict__ A, const WaveRare *R, Acc *img, uint32_t batch_seq,
-                                            uint32_t epoch, uint8_t refc, int lane) {
-    if (lane == 0) {
-        uint32_t newmask = 0, first[NSLOT];
-#pragma unroll
-        for (int k = 0; k < NSLOT; k++) {
-            first[k] = R->first[k];
-            if (R->cnt[k]) newmask |= 1u << k;
-        }
-        img->depth = R->depth;
-        img->first_batch = batch_seq;                                // first visit (:77-85)
-        img->order = merge_order(0u, newmask, first);
-        img->misc = refc | (R->n_other ? MISC_EXOTIC : 0u) | (R->skip << MISC_SKIP_SHIFT);
-        img->n_del = R->n_del;
-        img->n_skip = R->n_skip;
-        img->n_other = R->n_other;
-        img->epoch = epoch;
-    }
-    if (lane < NSLOT) {
-        const int k = lane;
-        const uint32_t c = R->cnt[k];
-        img->cnt[k] = c;
-        img->sq[k] = c ? (R->sq[k] > 0x80000000u ? 0x80000000u : R->sq[k]) : 0u;
-        img->sl[k] = c ? R->sl[k] : 0.0;
-        img->se[k] = c ? R->se[k] : 0.0;
-    }
-    if (lane < 8) img->qf[lane] = (uint8_t)(lane < NSLOT && R->cnt[lane] ? R->qf[lane] : 0u);
+// FRESH merge (k_acc_seg): the record is assembled in LDS (img) and later written with the wave's
+// other finished records as 16-byte stores, ten lanes per record (flush_records), so each column
+// costs exactly its 160 bytes of HBM writes and the wave issues one store instruction per RB columns.
+constexpr int RB = 6;        // finished FRESH records a wave buffers before one 60-lane store
+
+// Write the wave's n buffered records (img[0..n), to acc + col[r]); lanes 10 r .. 10 r + 9 store
+// record r.  A store costs the chunk prefetch a vmcnt drain, so the wave batches them.
+__device__ __forceinline__ void flush_records(Acc *__restrict__ acc, const Acc *img, const uint32_t *col, uint32_t n,
+                                              int lane) {
     wave_sync();
-    if (lane < 10) reinterpret_cast<uint4 *>(A)[lane] = reinterpret_cast<const uint4 *>(img)[lane];
+    if ((uint32_t)lane < 10u * n) {
+        const uint32_t r = (uint32_t)lane / 10u, piece = (uint32_t)lane - 10u * r;
+        reinterpret_cast<uint4 *>(acc + col[r])[piece] = reinterpret_cast<const uint4 *>(img + r)[piece];
+    }
 }
 
 template <bool FRESH>
@@ -360,8 +343,11 @@ struct Dual2 {              // per-lane partial sums of a wave's second fast all
 // Loads go through one wave-uniform buffer descriptor per array over the segment (range-checked:
 // chunks past the end read zeros).  Per column: allele vote on its first chunk, SWAR/LUT fast path
 // for the major allele, exact rare path into the wave's LDS record, then a cooperative merge.
-template <int W, bool FRESH>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_acc_seg(KParams P, const uint64_t *__restrict__ off,
+// WPE: minimum waves per SIMD the register allocation must allow.  4 (128 VGPRs) for mid-depth
+// batches, whose waves stream few chunks per column and need occupancy to hide the column starts;
+// 3 (up to 168 VGPRs, no spills) for deep batches, where the chunk loop dominates.
+template <int W, bool FRESH, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_acc_seg(KParams P, const uint64_t *__restrict__ off,
                                                  const uint8_t *__restrict__ code, const uint8_t *__restrict__ qual,
                                                  const uint8_t *__restrict__ ref, const Tables *__restrict__ T,
                                                  Acc *__restrict__ acc) {
@@ -376,8 +362,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     __shared__ WaveRare rare[4];
     __shared__ RareItem rqueue[4][QCAP];
     __shared__ int32_t rqo[4][QCAP];
+    __shared__ uint32_t rqr[4][QCAP];
     __shared__ Dual2 dual2[4];
-    __shared__ Acc accimg[4];
+    __shared__ Acc accimg[4][FRESH ? RB : 1];
+    __shared__ uint32_t acccol[4][RB];
     __shared__ ColDesc coldesc[4][64];
     write_hist(P);
     {
@@ -392,10 +380,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     const int ng = (int)min((int64_t)P.G, P.n_cols - g0);
     WaveRare *R = rare + (threadIdx.x >> 6);
     Dual2 *D2 = dual2 + (threadIdx.x >> 6);
-    Acc *img = accimg + (threadIdx.x >> 6);
+    Acc *img = accimg[threadIdx.x >> 6];
+    uint32_t *imgcol = acccol[threadIdx.x >> 6];
+    uint32_t nrec = 0;                                 // FRESH: finished records buffered in img (uniform)
     ColDesc *CD = coldesc[threadIdx.x >> 6];
     RareItem *Q = rqueue[threadIdx.x >> 6];
     int32_t *QO = rqo[threadIdx.x >> 6];
+    uint32_t *QR = rqr[threadIdx.x >> 6];
     uint32_t qn = 0;                                   // queued lane slices (wave-uniform)
     // drain the queue into the LDS record: every lane takes one entry per round (LDS atomics)
     // Drain: lane k decodes queued slice k (its rare entries are few) into the column's LDS record
@@ -413,21 +404,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
             if (b0 + lane < qn) {
                 const RareItem *it = Q + b0 + lane;
                 const int32_t o = QO[b0 + lane];
-#pragma unroll 1
-                for (int d = 0; d < W; d++) {          // rolled: one copy of the decode, data stays in LDS
-                    const uint32_t cw = it->c[d], qw = it->q[d];
-                    const uint32_t v = valid80(o + 4 * d, bl, el);
-                    uint32_t f80, r80, g80, r2;
-                    swar4(cw, qw, v, mrep, P.kpass, P.kok, f80, r80);
-                    swar4(cw, qw, v, mrep2, P.kpass, P.kok, g80, r2);   // mrep2 matches nothing unless dual
-                    r80 &= ~g80;
-                    while (r80) {
-                        const int sh = __builtin_ctz(r80) - 7;
-                        r80 &= r80 - 1;
-                        const uint32_t c = (cw >> sh) & 0xFFu, q = (qw >> sh) & 0xFFu;
-                        if ((int)q >= P.min_bq)
-                            rare_entry(R, c, q, (uint32_t)(o + 4 * d - bl) + (uint32_t)(sh >> 3), lut, T);
-                    }
+                uint32_t rb = QR[b0 + lane];           // bit 8 b + 7 - d: byte b of dword d is rare
+                while (rb) {
+                    const uint32_t p = (uint32_t)__builtin_ctz(rb);
+                    rb &= rb - 1;
+                    const uint32_t b = p >> 3, d = 7u - (p & 7u);
+                    const uint32_t c = (it->c[d] >> (8u * b)) & 0xFFu, q = (it->q[d] >> (8u * b)) & 0xFFu;
+                    if ((int)q >= P.min_bq)
+                        rare_entry(R, c, q, (uint32_t)(o + 4 * (int32_t)d - bl) + b, lut, T);
                 }
             }
         }
@@ -562,7 +546,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         auto body = [&](auto full_tag, auto dual_tag, auto sl_tag) {
             constexpr bool DUAL = decltype(dual_tag)::value;
             constexpr bool SL = decltype(sl_tag)::value;     // false: counts / sum(q) only (calls-only REF major)
-            uint32_t rany = 0;
+            uint32_t rany = 0;                  // the chunk slice's rare entries: bit 8 b + 7 - d
             uint32_t fcnt2 = 0, fsq2 = 0;
             double fsl2 = 0.0, fse2 = 0.0;
 #pragma unroll
@@ -596,7 +580,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                 } else {
                     (void)idx;
                 }
-                rany |= r80;
+                rany |= d == 0 ? r80 : r80 >> d;
             }
             if constexpr (DUAL) {
                 // second allele: lane-private LDS accumulators (no registers held across chunks)
@@ -639,6 +623,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                         it.q[d] = dw<W>(qq, d);
                     }
                     QO[slot] = o;
+                    QR[slot] = rany;
                 }
                 qn += n;
             }
@@ -648,16 +633,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         if (dual) {
             if (full) body(T_{}, T_{}, T_{});
             else body(F_{}, T_{}, T_{});
-        } else if (full) {
-            if (sem || !P.calls_only) body(T_{}, F_{}, T_{});
-            else { body(T_{}, F_{}, F_{}); skipped = true; }
-        } else {
-            body(F_{}, F_{}, T_{});
+        } else if (sem || !P.calls_only) {
+            if (full) body(T_{}, F_{}, T_{});
+            else body(F_{}, F_{}, T_{});
+        } else {                               // calls-only, REF major: counts and sum(q) only
+            if (full) body(T_{}, F_{}, F_{});
+            else body(F_{}, F_{}, F_{});
+            skipped = true;
         }
         if (cs + 1 == cn) {                    // ---- column end ----
             if (qn) drain();
             const uint32_t fc = dsum_u32(fcnt), fs = dsum_u32(fsq);
-            const double fl = dsum_f64(fsl), fe = dsum_f64(fse);
+            double fl = 0.0, fe = 0.0;
+            if (!skipped) { fl = dsum_f64(fsl); fe = dsum_f64(fse); }   // skipped: no chunk summed them
             uint32_t fc2 = 0, fs2 = 0;
             double fl2 = 0.0, fe2 = 0.0;
             if (dual) {
@@ -666,6 +654,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                 fl2 = dsum_f64(D2->sl[lane]); fe2 = dsum_f64(D2->se[lane]);
             }
             wave_sync();
+            if constexpr (FRESH) {
+                // lane k < NSLOT assembles slot k (the LDS record plus this column's fast sums), the
+                // dict order comes from a rank by (first entry, slot), lane 0 writes the header
+                Acc *a = img + nrec;
+                const int Ms = slot_of(M);
+                const bool base2 = fc2 != 0 && M2 != SPG_CODE_DEL && M2 != SPG_CODE_SKIP;
+                const int s2 = base2 ? slot_of(M2) : -1;
+                uint32_t c = 0, first = INF32, qf = 0;
+                if (lane < NSLOT) {
+                    c = R->cnt[lane];
+                    uint32_t sq = R->sq[lane];
+                    qf = R->qf[lane];
+                    first = R->first[lane];
+                    double sl = R->sl[lane], se = R->se[lane];
+                    if (lane == Ms && fc) {
+                        c += fc; sq += fs; sl += fl; se += fe;
+                        qf = min(qf, (uint32_t)P.qlo); first = min(first, ffirst);
+                    }
+                    if (lane == s2) {
+                        c += fc2; sq += fs2; sl += fl2; se += fe2;
+                        qf = min(qf, (uint32_t)P.qlo); first = min(first, ffirst2);
+                    }
+                    a->cnt[lane] = c;
+                    a->sq[lane] = c ? (sq > 0x80000000u ? 0x80000000u : sq) : 0u;
+                    a->sl[lane] = c ? sl : 0.0;
+                    a->se[lane] = c ? se : 0.0;
+                }
+                if (lane < 8) a->qf[lane] = (uint8_t)(c ? qf : 0u);
+                const uint32_t hm = (uint32_t)__ballot(lane < NSLOT && c != 0);
+                uint32_t rank = 0;
+#pragma unroll
+                for (int j = 0; j < NSLOT; j++) {
+                    const uint32_t fj = __builtin_amdgcn_readlane(first, j);
+                    rank += ((hm >> j) & 1u) && (fj < first || (fj == first && j < lane)) ? 1u : 0u;
+                }
+                uint32_t order = (uint32_t)__popc(hm);
+#pragma unroll
+                for (int j = 0; j < NSLOT; j++) {
+                    const uint32_t rj = __builtin_amdgcn_readlane(rank, j);
+                    if ((hm >> j) & 1u) order |= (uint32_t)j << (3 + 3 * rj);
+                }
+                if (lane == 0) {
+                    a->depth = R->depth + fc + fc2;
+                    a->first_batch = P.batch_seq;                          // first visit (:77-85)
+                    a->order = order;
+                    const uint32_t skip = R->skip | (skipped && fc ? 1u << Ms : 0u);
+                    a->misc = crefc | (R->n_other ? MISC_EXOTIC : 0u) | (skip << MISC_SKIP_SHIFT);
+                    a->n_del = R->n_del + (M2 == SPG_CODE_DEL ? fc2 : 0u);
+                    a->n_skip = R->n_skip + (M2 == SPG_CODE_SKIP ? fc2 : 0u);
+                    a->n_other = R->n_other;
+                    a->epoch = P.epoch;
+                    imgcol[nrec] = cj;
+                }
+                if (++nrec == RB) { flush_records(acc + P.pos_begin + g0, img, imgcol, nrec, lane); nrec = 0; }
+                wave_sync();
+                return;
+            }
             if (lane == 0) {
                 R->depth += fc + fc2;
                 if (fc) {
@@ -673,7 +718,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                     R->cnt[Ms] += fc; R->sq[Ms] += fs; R->sl[Ms] += fl; R->se[Ms] += fe;
                     R->qf[Ms] = min(R->qf[Ms], (uint32_t)P.qlo);
                     R->first[Ms] = min(R->first[Ms], ffirst);
-                    if (skipped) R->skip |= 1u << Ms;   // full chunks skipped its likelihood sums
+                    if (skipped) R->skip |= 1u << Ms;   // its chunks skipped the likelihood sums
                 }
                 if (fc2) {
                     const int s2 = slot_of(M2);
@@ -687,10 +732,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
                 }
             }
             wave_sync();
-            if constexpr (FRESH)
-                merge_fresh(acc + P.pos_begin + g0 + cj, R, img, P.batch_seq, P.epoch, (uint8_t)crefc, lane);
-            else
-                merge_column<false>(acc + P.pos_begin + g0 + cj, R, P.batch_seq, P.epoch, (uint8_t)crefc, lane);
+            merge_column<FRESH>(acc + P.pos_begin + g0 + cj, R, P.batch_seq, P.epoch, (uint8_t)crefc, lane);
             wave_sync();
         }
     };
@@ -705,6 +747,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         if (i + 2 >= total) break;
         c1 = bload<W>(rc, chunk_off(i + 4)); q1 = bload<W>(rq, chunk_off(i + 4));
         process(c2, q2, i + 2);
+    }
+    if constexpr (FRESH) {
+        if (nrec) flush_records(acc + P.pos_begin + g0, img, imgcol, nrec, lane);
     }
 }
 
@@ -1067,9 +1112,14 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
     const int64_t blocks = (waves + 3) / 4;
     const bool fresh = P.batch_seq == 1;
     const bool w4 = P.t_deep <= 1;
-#define SPG_SEG(WW, FF) hipLaunchKernelGGL((k_acc_seg<WW, FF>), dim3((unsigned)blocks), dim3(256), 0, st, P, off, code, qual, ref, T, acc)
-    if (w4) { if (fresh) SPG_SEG(4, true); else SPG_SEG(4, false); }
-    else { if (fresh) SPG_SEG(1, true); else SPG_SEG(1, false); }
+#define SPG_SEG(WW, FF, OO) hipLaunchKernelGGL((k_acc_seg<WW, FF, OO>), dim3((unsigned)blocks), dim3(256), 0, st, P, off, code, qual, ref, T, acc)
+    const bool deep = P.n_entries >= (uint64_t)P.n_cols * 4096u;    // >= 4 chunks per column on average
+    if (w4) {
+        if (deep) { if (fresh) SPG_SEG(4, true, 3); else SPG_SEG(4, false, 3); }
+        else { if (fresh) SPG_SEG(4, true, 4); else SPG_SEG(4, false, 4); }
+    } else {
+        if (fresh) SPG_SEG(1, true, 4); else SPG_SEG(1, false, 4);
+    }
 #undef SPG_SEG
     return hipGetLastError();
 }

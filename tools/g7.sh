@@ -1,0 +1,9 @@
+set -e
+cd /root/repo
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -1 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python tools/kbench.py --tag head --calls-only --iters 40
+timeout -k 10 300 python tools/kbench.py --tag head --iters 40
+timeout -k 10 300 python tools/kbench.py --tag head1000 --depth 1000 --calls-only --iters 40
