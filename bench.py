@@ -164,7 +164,7 @@ def pmc_traffic(E):
         return None
     try:
         d = json.load(open(files[-1]))
-        rec = d.get("spg::k_acc_seg<4, true>")
+        rec = next((v for k, v in d.items() if k.startswith("spg::k_acc_seg<4, true")), None)
         if rec is None or rec.get("entries") not in (None, E):
             return None
         return rec.get("hbm_bytes_per_launch")
@@ -287,7 +287,7 @@ def main():
                    "engine_mode": "full_table" if args.full_table else "calls_only"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM, "traffic": pmc_traffic(E),
-                     "kernel": "k_acc_seg<4,true> (spg_accumulate)", "kernel_ms": t_acc * 1e3, "algorithmic_bytes": algo_bytes},
+                     "kernel": "k_acc_seg<4,true,3> (spg_accumulate)", "kernel_ms": t_acc * 1e3, "algorithmic_bytes": algo_bytes},
         "finalize_ms": t_fin * 1e3, "candidates_per_gpu_step": n_cand, "datagen_s": t_gen,
         "calls_gathered_per_step": sum(gathered) if gathered is not None else n_cand,
     }
