@@ -185,6 +185,20 @@ __device__ __forceinline__ uint32_t valid80(int32_t x, int32_t b, int32_t e) {  
     return (uint32_t)((0x80808080ull << (8 * lead)) & (0x80808080ull >> (8 * (4 - end))));
 }
 
+// Validity of a lane's 4W entries o .. o + 4W - 1 against the column [b, e), one 0x80-per-byte mask
+// per dword: the byte at slice position p is valid iff lead <= p < end.  With K_d holding
+// 0x80 + p in each byte, K_d - lead (broadcast) has bit 7 iff p >= lead (no borrow: p, lead <= 16).
+template <int W>
+__device__ __forceinline__ void valid_masks(int32_t o, int32_t b, int32_t e, uint32_t (&v)[W]) {
+    const uint32_t lead = (uint32_t)min(max(b - o, 0), 4 * W), end = (uint32_t)min(max(e - o, 0), 4 * W);
+    const uint32_t lb = __builtin_amdgcn_perm(0u, lead, 0u), eb = __builtin_amdgcn_perm(0u, end, 0u);
+#pragma unroll
+    for (int d = 0; d < W; d++) {
+        const uint32_t K = 0x80808080u + (uint32_t)(4 * d) * 0x01010101u + 0x03020100u;
+        v[d] = (K - lb) & ~(K - eb) & 0x80808080u;
+    }
+}
+
 template <int W>   // W dwords per lane per step: 4 (16 entries, dwordx4) or 1 (4 entries)
 struct Vec;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -526,34 +540,61 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         }
         const int32_t o = (int32_t)(cs * STEP + lo);
         const bool full = (int32_t)(cs * STEP) >= bl && (int32_t)(cs * STEP + STEP) <= el;   // wave-uniform
+        // Lean chunks: no byte of the chunk has bit 7 set (q < 128, code < 128) and min_bq >= 4, so
+        // one SWAR add per dword tests q >= min_bq (no carry) and one xor-add tests code != M
+        // (codes < 128: no carry); q >= 128 or a stray code byte sends the chunk down the exact
+        // generic path.
+        bool lean = false;
+        if (P.kpass == P.kok) {
+            uint32_t h = 0;
+#pragma unroll
+            for (int d = 0; d < W; d++) h |= dw<W>(cc, d) | dw<W>(qq, d);
+            lean = __ballot((h & 0x80808080u) != 0u) == 0;
+        }
+        uint32_t vm[W];                         // partial chunks and every generic non-dual chunk
+        if (!full || (!lean && !dual)) valid_masks<W>(o, bl, el, vm);
         // SWAR classes of dword d: fast (major), second (dual mode) and rare.  Recomputed where
         // needed instead of kept in registers across the chunk.
-        auto classify = [&](auto full_tag, auto dual_tag, int d, uint32_t &f80, uint32_t &g80, uint32_t &r80,
-                            bool again = false) {
+        auto classify = [&](auto full_tag, auto dual_tag, auto lean_tag, int d, uint32_t &f80, uint32_t &g80,
+                            uint32_t &r80, bool again = false) {
             constexpr bool FULL = decltype(full_tag)::value;
             constexpr bool DUAL = decltype(dual_tag)::value;
+            constexpr bool LEAN = decltype(lean_tag)::value;
             uint32_t cw = dw<W>(cc, d), qw = dw<W>(qq, d);
             if (again) asm volatile("" : "+v"(cw), "+v"(qw));   // a recomputation, not a value kept live
-            const uint32_t v = FULL ? 0x80808080u : valid80(o + 4 * d, bl, el);
-            swar4(cw, qw, v, mrep, P.kpass, P.kok, f80, r80);
+            const uint32_t v = FULL ? 0x80808080u : vm[d];
             g80 = 0;
-            if constexpr (DUAL) {
-                uint32_t r2;
-                swar4(cw, qw, v, mrep2, P.kpass, P.kok, g80, r2);
-                r80 &= ~g80;
+            if constexpr (LEAN) {
+                const uint32_t t = qw + P.kpass;                      // bit 7: q >= min_bq
+                const uint32_t n = (cw ^ mrep) + 0x7F7F7F7Fu;         // bit 7: code != M
+                f80 = t & ~n & v;
+                r80 = t & n & v;
+                if constexpr (DUAL) {
+                    const uint32_t n2 = (cw ^ mrep2) + 0x7F7F7F7Fu;
+                    g80 = t & ~n2 & v;
+                    r80 &= n2;
+                }
+            } else {
+                swar4(cw, qw, v, mrep, P.kpass, P.kok, f80, r80);
+                if constexpr (DUAL) {
+                    uint32_t r2;
+                    swar4(cw, qw, v, mrep2, P.kpass, P.kok, g80, r2);
+                    r80 &= ~g80;
+                }
             }
         };
-        auto body = [&](auto full_tag, auto dual_tag, auto sl_tag) {
+        auto body = [&](auto full_tag, auto dual_tag, auto sl_tag, auto lean_tag) {
             constexpr bool DUAL = decltype(dual_tag)::value;
             constexpr bool SL = decltype(sl_tag)::value;     // false: counts / sum(q) only (calls-only REF major)
+            constexpr bool LEAN = decltype(lean_tag)::value;
             uint32_t rany = 0;                  // the chunk slice's rare entries: bit 8 b + 7 - d
-            uint32_t fcnt2 = 0, fsq2 = 0;
+            uint32_t fcnt2 = 0, fsq2 = 0, lsq = 0;
             double fsl2 = 0.0, fse2 = 0.0;
 #pragma unroll
             for (int d = 0; d < W; d++) {
                 const uint32_t qw = dw<W>(qq, d);
                 uint32_t f80, g80, r80;
-                classify(full_tag, dual_tag, d, f80, g80, r80);
+                classify(full_tag, dual_tag, lean_tag, d, f80, g80, r80);
                 if constexpr (DUAL) {           // the second allele's entries leave the rare set
                     fcnt2 += __popc(g80);
                     fsq2 = __builtin_amdgcn_udot4(qw, g80 >> 7, fsq2, false);
@@ -568,9 +609,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                     asm volatile("" : "+v"(fsl2), "+v"(fse2) :: "memory");
                 }
                 fcnt += __popc(f80);
-                fsq = __builtin_amdgcn_udot4(qw, f80 >> 7, fsq, false);
+                // lean: q < 128, so q * 0x80 sums of one chunk fit (16 x 127 x 128), shifted once below
+                if constexpr (LEAN) lsq = __builtin_amdgcn_udot4(qw, f80, lsq, false);
+                else fsq = __builtin_amdgcn_udot4(qw, f80 >> 7, fsq, false);
                 // fast entries have q < 128: their row is q; every other byte gets bit 7 -> a zero row
-                const uint32_t idx = (qw & 0x7F7F7F7Fu) ^ f80 ^ 0x80808080u;
+                const uint32_t idx = (LEAN ? qw : (qw & 0x7F7F7F7Fu)) ^ f80 ^ 0x80808080u;
                 if constexpr (SL) {
                     const double2 t0 = lut[idx & 0xFFu], t1 = lut[(idx >> 8) & 0xFFu];
                     const double2 t2 = lut[(idx >> 16) & 0xFFu], t3 = lut[idx >> 24];
@@ -582,6 +625,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 }
                 rany |= d == 0 ? r80 : r80 >> d;
             }
+            if constexpr (LEAN) fsq += lsq >> 7;
             if constexpr (DUAL) {
                 // second allele: lane-private LDS accumulators (no registers held across chunks)
                 __hip_atomic_fetch_add(&D2->cnt[lane], fcnt2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -594,7 +638,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
 #pragma unroll
                 for (int d = W - 1; d >= 0; d--) {
                     uint32_t f80, g80, r80;
-                    classify(full_tag, dual_tag, d, f80, g80, r80, true);
+                    classify(full_tag, dual_tag, lean_tag, d, f80, g80, r80, true);
                     if (f80) mine = (uint32_t)(o + 4 * d - bl) + ((uint32_t)__builtin_ctz(f80) >> 3);
                     if (DUAL && g80) mine2 = (uint32_t)(o + 4 * d - bl) + ((uint32_t)__builtin_ctz(g80) >> 3);
                 }
@@ -631,14 +675,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         using T_ = std::true_type;
         using F_ = std::false_type;
         if (dual) {
-            if (full) body(T_{}, T_{}, T_{});
-            else body(F_{}, T_{}, T_{});
+            if (full) body(T_{}, T_{}, T_{}, F_{});
+            else body(F_{}, T_{}, T_{}, F_{});
         } else if (sem || !P.calls_only) {
-            if (full) body(T_{}, F_{}, T_{});
-            else body(F_{}, F_{}, T_{});
+            if (lean) {
+                if (full) body(T_{}, F_{}, T_{}, T_{});
+                else body(F_{}, F_{}, T_{}, T_{});
+            } else {
+                body(F_{}, F_{}, T_{}, F_{});
+            }
         } else {                               // calls-only, REF major: counts and sum(q) only
-            if (full) body(T_{}, F_{}, F_{});
-            else body(F_{}, F_{}, F_{});
+            if (lean) {
+                if (full) body(T_{}, F_{}, F_{}, T_{});
+                else body(F_{}, F_{}, F_{}, T_{});
+            } else {
+                body(F_{}, F_{}, F_{}, F_{});
+            }
             skipped = true;
         }
         if (cs + 1 == cn) {                    // ---- column end ----
