@@ -270,71 +270,81 @@ __device__ __forceinline__ void write_hist(const KParams &P) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *P.hslot = P.hdesc;
 }
 
-// Merge the column record R (LDS) into its Acc.  Cooperative: lane 0 writes the header and the dict
-// order, lanes 1..5 one allele slot each.  FRESH (first batch since reset): every record belongs to
-// an older epoch, so nothing is read back — the merge is pure stores.
-// FRESH merge (k_acc_seg): the record is assembled in LDS (img) and later written with the wave's
-// other finished records as 16-byte stores, ten lanes per record (flush_records), so each column
-// costs exactly its 160 bytes of HBM writes and the wave issues one store instruction per RB columns.
-constexpr int RB = 6;        // finished FRESH records a wave buffers before one 60-lane store
+// Column finishing is batched: at a column's end the wave only reduces its fast-path sums into a
+// ColSum (lane 0) next to the column's rare record (both in a per-wave LDS ring of NB slots).  When
+// the ring is full (and at the wave's end) lane j < NB assembles column j's 160-B Acc record — the
+// merge of rare record, fast sums and (not FRESH) the record already in HBM — in LDS, and the wave
+// writes the records with 16-B stores, ten lanes per record.  The serial per-column work of
+// process_pileup_column / process_svn's dict bookkeeping (:77-101) thus runs lane-parallel.
+constexpr int NB = 8;        // columns a wave finishes together
 
-// Write the wave's n buffered records (img[0..n), to acc + col[r]); lanes 10 r .. 10 r + 9 store
-// record r.  A store costs the chunk prefetch a vmcnt drain, so the wave batches them.
-__device__ __forceinline__ void flush_records(Acc *__restrict__ acc, const Acc *img, const uint32_t *col, uint32_t n,
-                                              int lane) {
-    wave_sync();
-    if ((uint32_t)lane < 10u * n) {
-        const uint32_t r = (uint32_t)lane / 10u, piece = (uint32_t)lane - 10u * r;
-        reinterpret_cast<uint4 *>(acc + col[r])[piece] = reinterpret_cast<const uint4 *>(img + r)[piece];
-    }
-}
+struct ColSum {              // one finished column's fast-path statistics (written by lane 0)
+    uint32_t M, M2, fc, fs, fc2, fs2, ffirst, ffirst2;
+    uint32_t skipped, cj, crefc, pad;
+    double fl, fe, fl2, fe2;
+};
+static_assert(sizeof(ColSum) == 80, "ColSum");
 
+// Lane-per-column record assembly (lane j of the finisher; R / S in LDS, out = the LDS image).
 template <bool FRESH>
-__device__ __forceinline__ void merge_column(Acc *__restrict__ A, const WaveRare *R, uint32_t batch_seq,
-                                             uint32_t epoch, uint8_t refc, int lane) {
+__device__ __forceinline__ void assemble_record(const KParams &P, const Acc *__restrict__ A, const WaveRare *R,
+                                                const ColSum *S, Acc *out) {
+    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = make_uint4(0, 0, 0, 0);
     bool fresh = FRESH;
-    if constexpr (!FRESH) fresh = A->epoch != epoch;    // read by every lane before any lane writes
-    if (lane == 0) {
-        uint4 h0 = make_uint4(0, 0, 0, 0), h1 = make_uint4(0, 0, 0, 0);
-        if (!fresh) { h0 = reinterpret_cast<const uint4 *>(A)[0]; h1 = reinterpret_cast<const uint4 *>(A)[1]; }
-        if (h0.y == 0) { h0.y = batch_seq; h0.w = refc; }          // first visit (:77-85)
-        h0.x += R->depth;                                           // :87
-        h1.x += R->n_del; h1.y += R->n_skip; h1.z += R->n_other; h1.w = epoch;
-        if (R->n_other) h0.w |= MISC_EXOTIC;
-        h0.w |= R->skip << MISC_SKIP_SHIFT;
-        const uint32_t have = order_mask(h0.z);
-        uint32_t newmask = 0, first[NSLOT];
+    if constexpr (!FRESH) {
+        h0 = reinterpret_cast<const uint4 *>(A)[0];
+        h1 = reinterpret_cast<const uint4 *>(A)[1];
+        fresh = h1.w != P.epoch;                    // record of an older sample: start afresh
+        if (fresh) { h0 = make_uint4(0, 0, 0, 0); h1 = make_uint4(0, 0, 0, 0); }
+    }
+    const uint32_t M = S->M, M2 = S->M2, fc = S->fc, fc2 = S->fc2;
+    const int Ms = fc ? slot_of(M) : -1;
+    const int s2 = (fc2 && M2 != SPG_CODE_DEL && M2 != SPG_CODE_SKIP) ? slot_of(M2) : -1;
+    const uint32_t have = order_mask(h0.z);
+    uint32_t newmask = 0, first[NSLOT];
 #pragma unroll
-        for (int k = 0; k < NSLOT; k++) {
-            first[k] = R->first[k];
-            if (R->cnt[k] && !((have >> k) & 1u)) newmask |= 1u << k;
+    for (int k = 0; k < NSLOT; k++) {
+        uint32_t c = R->cnt[k], sq = R->sq[k], qf = R->qf[k];
+        double sl = R->sl[k], se = R->se[k];
+        first[k] = R->first[k];
+        if (k == Ms) {
+            c += fc; sq += S->fs; sl += S->fl; se += S->fe;
+            qf = min(qf, (uint32_t)P.qlo); first[k] = min(first[k], S->ffirst);
         }
-        h0.z = merge_order(h0.z, newmask, first);
-        reinterpret_cast<uint4 *>(A)[0] = h0;
-        reinterpret_cast<uint4 *>(A)[1] = h1;
-    } else if (lane <= NSLOT) {
-        const int k = lane - 1;
-        const uint32_t c = R->cnt[k];
-        uint32_t old = 0;
-        if (!fresh) old = A->cnt[k];
+        if (k == s2) {
+            c += fc2; sq += S->fs2; sl += S->fl2; se += S->fe2;
+            qf = min(qf, (uint32_t)P.qlo); first[k] = min(first[k], S->ffirst2);
+        }
+        uint32_t oc = 0, osq = 0, oqf = 0;
+        double osl = 0.0, ose = 0.0;
+        if (!fresh) { oc = A->cnt[k]; osq = A->sq[k]; oqf = A->qf[k]; osl = A->sl[k]; ose = A->se[k]; }
         if (c) {
-            if (old) {
-                A->qf[k] = (uint8_t)min((uint32_t)A->qf[k], R->qf[k]);
-                const uint64_t sq = (uint64_t)A->sq[k] + R->sq[k];
-                A->sq[k] = sq > 0x80000000ull ? 0x80000000u : (uint32_t)sq;
-                A->sl[k] = A->sl[k] + R->sl[k];
-                A->se[k] = A->se[k] + R->se[k];
+            if (!((have >> k) & 1u)) newmask |= 1u << k;
+            if (oc) {                                // absent slots' sums may hold stale bytes
+                qf = min(oqf, qf);
+                const uint64_t t = (uint64_t)osq + sq;
+                sq = t > 0x80000000ull ? 0x80000000u : (uint32_t)t;
+                sl = osl + sl; se = ose + se;
             } else {
-                A->qf[k] = (uint8_t)R->qf[k];
-                A->sq[k] = R->sq[k] > 0x80000000u ? 0x80000000u : R->sq[k];
-                A->sl[k] = R->sl[k];
-                A->se[k] = R->se[k];
+                sq = sq > 0x80000000u ? 0x80000000u : sq;
             }
-            A->cnt[k] = old + c;
-        } else if (fresh) {
-            A->cnt[k] = 0;
+            out->cnt[k] = oc + c; out->sq[k] = sq; out->qf[k] = (uint8_t)qf; out->sl[k] = sl; out->se[k] = se;
+        } else {
+            out->cnt[k] = oc; out->sq[k] = osq; out->qf[k] = (uint8_t)oqf; out->sl[k] = osl; out->se[k] = ose;
         }
     }
+    out->qf[5] = out->qf[6] = out->qf[7] = 0;
+    if (h0.y == 0) { h0.y = P.batch_seq; h0.w = S->crefc; }          // first visit (:77-85)
+    h0.x += R->depth + fc + fc2;                                      // :87
+    h0.z = merge_order(h0.z, newmask, first);
+    if (R->n_other) h0.w |= MISC_EXOTIC;
+    if (S->skipped && Ms >= 0) h0.w |= (1u << Ms) << MISC_SKIP_SHIFT;
+    h1.x += R->n_del + (M2 == SPG_CODE_DEL ? fc2 : 0u);
+    h1.y += R->n_skip + (M2 == SPG_CODE_SKIP ? fc2 : 0u);
+    h1.z += R->n_other;
+    h1.w = P.epoch;
+    reinterpret_cast<uint4 *>(out)[0] = h0;
+    reinterpret_cast<uint4 *>(out)[1] = h1;
 }
 
 struct ColDesc {             // one column of a wave's segment (LDS, 16 B)
@@ -373,13 +383,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     // LUT rows 0..127: {ln(1-eps), eps} for q < 128; rows 128..255: {0, 0} (the fast path's index
     // for entries that are not fast; the rare path reads q >= 128 from the global table)
     __shared__ double2 lut[256];
-    __shared__ WaveRare rare[4];
+    __shared__ WaveRare rare[4][NB];
+    __shared__ ColSum csum[4][NB];
     __shared__ RareItem rqueue[4][QCAP];
     __shared__ int32_t rqo[4][QCAP];
     __shared__ uint32_t rqr[4][QCAP];
     __shared__ Dual2 dual2[4];
-    __shared__ Acc accimg[4][FRESH ? RB : 1];
-    __shared__ uint32_t acccol[4][RB];
+    __shared__ Acc accimg[4][NB];
     __shared__ ColDesc coldesc[4][64];
     write_hist(P);
     {
@@ -392,20 +402,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     const int64_t g0 = wave * P.G;
     if (g0 >= P.n_cols) return;
     const int ng = (int)min((int64_t)P.G, P.n_cols - g0);
-    WaveRare *R = rare + (threadIdx.x >> 6);
+    WaveRare *RR = rare[threadIdx.x >> 6];             // rare records of the ring's columns
+    ColSum *CS = csum[threadIdx.x >> 6];
     Dual2 *D2 = dual2 + (threadIdx.x >> 6);
     Acc *img = accimg[threadIdx.x >> 6];
-    uint32_t *imgcol = acccol[threadIdx.x >> 6];
-    uint32_t nrec = 0;                                 // FRESH: finished records buffered in img (uniform)
+    uint32_t nb = 0;                                   // columns in the finishing ring (uniform)
     ColDesc *CD = coldesc[threadIdx.x >> 6];
     RareItem *Q = rqueue[threadIdx.x >> 6];
     int32_t *QO = rqo[threadIdx.x >> 6];
     uint32_t *QR = rqr[threadIdx.x >> 6];
     uint32_t qn = 0;                                   // queued lane slices (wave-uniform)
-    // drain the queue into the LDS record: every lane takes one entry per round (LDS atomics)
-    // Drain: lane k decodes queued slice k (its rare entries are few) into the column's LDS record
-    // with LDS atomics.  Runs at column end (or when the queue is full), so the column's bounds,
-    // major / second allele are the current ones.
+    // Drain: lane k decodes queued slice k (its rare entries are few) into its column's LDS rare
+    // record with LDS atomics.  A queued slice carries its column-relative offset (QO) and its ring
+    // slot (QR bits 0-2), so the drain runs only when the queue is full or the ring is finished.
     int32_t bl = 0, el = 0;                    // column bounds relative to its first chunk
     uint32_t mrep = 0, M = 1;
     bool dual = false;
@@ -419,17 +428,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 const RareItem *it = Q + b0 + lane;
                 const int32_t o = QO[b0 + lane];
                 uint32_t rb = QR[b0 + lane];           // bit 8 b + 7 - d: byte b of dword d is rare
+                WaveRare *R = RR + (rb & 7u);
+                rb &= ~15u;
                 while (rb) {
                     const uint32_t p = (uint32_t)__builtin_ctz(rb);
                     rb &= rb - 1;
                     const uint32_t b = p >> 3, d = 7u - (p & 7u);
                     const uint32_t c = (it->c[d] >> (8u * b)) & 0xFFu, q = (it->q[d] >> (8u * b)) & 0xFFu;
                     if ((int)q >= P.min_bq)
-                        rare_entry(R, c, q, (uint32_t)(o + 4 * (int32_t)d - bl) + b, lut, T);
+                        rare_entry(R, c, q, (uint32_t)(o + 4 * (int32_t)d) + b, lut, T);
                 }
             }
         }
         qn = 0;
+        wave_sync();
+    };
+
+    // Finish the ring: drain the queue, lane j assembles column j's record in LDS, the wave stores the
+    // records (16 B per lane, ten lanes per record).
+    auto finish = [&]() {
+        if (qn) drain();
+        else wave_sync();
+        if ((uint32_t)lane < nb) {
+            const ColSum *S = CS + lane;
+            assemble_record<FRESH>(P, acc + P.pos_begin + g0 + S->cj, RR + lane, S, img + lane);
+        }
+        wave_sync();
+        Acc *base = acc + P.pos_begin + g0;
+        for (uint32_t t = (uint32_t)lane; t < 10u * nb; t += 64u) {
+            const uint32_t r = t / 10u, piece = t - 10u * r;
+            reinterpret_cast<uint4 *>(base + CS[r].cj)[piece] = reinterpret_cast<const uint4 *>(img + r)[piece];
+        }
+        nb = 0;
         wave_sync();
     };
 
@@ -513,7 +543,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         }
         cs = i - cpre;
         if (cs == 0) {                         // ---- column begin ----
-            rare_init(R, lane);
+            rare_init(RR + nb, lane);
             const uint32_t v0 = dw<W>(cc, 0) & 0xFFu;
             const int vote = ((int32_t)lo >= bl && (int32_t)lo < el) ? (int)v0 : -1;
             int cnt7[7];
@@ -666,8 +696,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                         it.c[d] = dw<W>(cc, d);
                         it.q[d] = dw<W>(qq, d);
                     }
-                    QO[slot] = o;
-                    QR[slot] = rany;
+                    QO[slot] = o - bl;
+                    QR[slot] = rany | nb;           // rany bits 0-3 are free: ring slot
                 }
                 qn += n;
             }
@@ -694,7 +724,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
             skipped = true;
         }
         if (cs + 1 == cn) {                    // ---- column end ----
-            if (qn) drain();
             const uint32_t fc = dsum_u32(fcnt), fs = dsum_u32(fsq);
             double fl = 0.0, fe = 0.0;
             if (!skipped) { fl = dsum_f64(fsl); fe = dsum_f64(fse); }   // skipped: no chunk summed them
@@ -705,90 +734,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 fc2 = dsum_u32(D2->cnt[lane]); fs2 = dsum_u32(D2->sq[lane]);
                 fl2 = dsum_f64(D2->sl[lane]); fe2 = dsum_f64(D2->se[lane]);
             }
-            wave_sync();
-            if constexpr (FRESH) {
-                // lane k < NSLOT assembles slot k (the LDS record plus this column's fast sums), the
-                // dict order comes from a rank by (first entry, slot), lane 0 writes the header
-                Acc *a = img + nrec;
-                const int Ms = slot_of(M);
-                const bool base2 = fc2 != 0 && M2 != SPG_CODE_DEL && M2 != SPG_CODE_SKIP;
-                const int s2 = base2 ? slot_of(M2) : -1;
-                uint32_t c = 0, first = INF32, qf = 0;
-                if (lane < NSLOT) {
-                    c = R->cnt[lane];
-                    uint32_t sq = R->sq[lane];
-                    qf = R->qf[lane];
-                    first = R->first[lane];
-                    double sl = R->sl[lane], se = R->se[lane];
-                    if (lane == Ms && fc) {
-                        c += fc; sq += fs; sl += fl; se += fe;
-                        qf = min(qf, (uint32_t)P.qlo); first = min(first, ffirst);
-                    }
-                    if (lane == s2) {
-                        c += fc2; sq += fs2; sl += fl2; se += fe2;
-                        qf = min(qf, (uint32_t)P.qlo); first = min(first, ffirst2);
-                    }
-                    a->cnt[lane] = c;
-                    a->sq[lane] = c ? (sq > 0x80000000u ? 0x80000000u : sq) : 0u;
-                    a->sl[lane] = c ? sl : 0.0;
-                    a->se[lane] = c ? se : 0.0;
-                }
-                if (lane < 8) a->qf[lane] = (uint8_t)(c ? qf : 0u);
-                const uint32_t hm = (uint32_t)__ballot(lane < NSLOT && c != 0);
-                uint32_t rank = 0;
-#pragma unroll
-                for (int j = 0; j < NSLOT; j++) {
-                    const uint32_t fj = __builtin_amdgcn_readlane(first, j);
-                    rank += ((hm >> j) & 1u) && (fj < first || (fj == first && j < lane)) ? 1u : 0u;
-                }
-                uint32_t order = (uint32_t)__popc(hm);
-#pragma unroll
-                for (int j = 0; j < NSLOT; j++) {
-                    const uint32_t rj = __builtin_amdgcn_readlane(rank, j);
-                    if ((hm >> j) & 1u) order |= (uint32_t)j << (3 + 3 * rj);
-                }
-                if (lane == 0) {
-                    a->depth = R->depth + fc + fc2;
-                    a->first_batch = P.batch_seq;                          // first visit (:77-85)
-                    a->order = order;
-                    const uint32_t skip = R->skip | (skipped && fc ? 1u << Ms : 0u);
-                    a->misc = crefc | (R->n_other ? MISC_EXOTIC : 0u) | (skip << MISC_SKIP_SHIFT);
-                    a->n_del = R->n_del + (M2 == SPG_CODE_DEL ? fc2 : 0u);
-                    a->n_skip = R->n_skip + (M2 == SPG_CODE_SKIP ? fc2 : 0u);
-                    a->n_other = R->n_other;
-                    a->epoch = P.epoch;
-                    imgcol[nrec] = cj;
-                }
-                if (++nrec == RB) { flush_records(acc + P.pos_begin + g0, img, imgcol, nrec, lane); nrec = 0; }
-                wave_sync();
-                return;
-            }
             if (lane == 0) {
-                R->depth += fc + fc2;
-                if (fc) {
-                    const int Ms = slot_of(M);
-                    R->cnt[Ms] += fc; R->sq[Ms] += fs; R->sl[Ms] += fl; R->se[Ms] += fe;
-                    R->qf[Ms] = min(R->qf[Ms], (uint32_t)P.qlo);
-                    R->first[Ms] = min(R->first[Ms], ffirst);
-                    if (skipped) R->skip |= 1u << Ms;   // its chunks skipped the likelihood sums
-                }
-                if (fc2) {
-                    const int s2 = slot_of(M2);
-                    if (M2 == SPG_CODE_DEL) R->n_del += fc2;
-                    else if (M2 == SPG_CODE_SKIP) R->n_skip += fc2;
-                    else {
-                        R->cnt[s2] += fc2; R->sq[s2] += fs2; R->sl[s2] += fl2; R->se[s2] += fe2;
-                        R->qf[s2] = min(R->qf[s2], (uint32_t)P.qlo);
-                        R->first[s2] = min(R->first[s2], ffirst2);
-                    }
-                }
+                ColSum *S = CS + nb;
+                S->M = M; S->M2 = dual ? M2 : 0u; S->fc = fc; S->fs = fs; S->fc2 = fc2; S->fs2 = fs2;
+                S->ffirst = ffirst; S->ffirst2 = ffirst2; S->skipped = skipped ? 1u : 0u; S->cj = cj;
+                S->crefc = crefc; S->fl = fl; S->fe = fe; S->fl2 = fl2; S->fe2 = fe2;
             }
-            wave_sync();
-            merge_column<FRESH>(acc + P.pos_begin + g0 + cj, R, P.batch_seq, P.epoch, (uint8_t)crefc, lane);
-            wave_sync();
+            if (++nb == NB) finish();
         }
     };
-
 
     for (uint32_t i = 0; i < total; i += 3) {
         c2 = bload<W>(rc, chunk_off(i + 2)); q2 = bload<W>(rq, chunk_off(i + 2));
@@ -800,9 +754,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         c1 = bload<W>(rc, chunk_off(i + 4)); q1 = bload<W>(rq, chunk_off(i + 4));
         process(c2, q2, i + 2);
     }
-    if constexpr (FRESH) {
-        if (nrec) flush_records(acc + P.pos_begin + g0, img, imgcol, nrec, lane);
-    }
+    if (nb) finish();
 }
 
 // Short columns (< t_deep raw entries): one lane per column.  The lane walks its column in
@@ -1030,13 +982,14 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
     if (!F.table) {
         // calls only: the header and the counts (first 48 bytes) decide whether this position can
         // produce a call at all; only then is the rest of the record read
+        // header and counts in one round trip (the 52 bytes are loaded together)
         const uint4 h0 = reinterpret_cast<const uint4 *>(acc + pos)[0];
         const uint4 h1 = reinterpret_cast<const uint4 *>(acc + pos)[1];
+        const uint4 c4 = reinterpret_cast<const uint4 *>(acc + pos)[2];
+        const uint32_t c5 = reinterpret_cast<const uint32_t *>(acc + pos)[12];
         if (h1.w != F.epoch || h0.y == 0) return;                       // not in memory
         if ((int64_t)h0.x < (int64_t)F.min_td) return;                  // not evaluated (:131)
         if (!(h0.w & MISC_EXOTIC)) {
-            const uint4 c4 = reinterpret_cast<const uint4 *>(acc + pos)[2];
-            const uint32_t c5 = reinterpret_cast<const uint32_t *>(acc + pos)[12];
             const uint32_t cnt[NSLOT] = {c4.x, c4.y, c4.z, c4.w, c5};
             const uint8_t refc = (uint8_t)(h0.w & 0xFFu);
             bool any = false;
