@@ -321,7 +321,10 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
     }();
     static const double deep_min = [] { const char *e = getenv("SPG_DEEP_MIN"); return e ? atof(e) : 256.0; }();
     const bool deep_batch = avg >= deep_min;
-    const uint32_t G = (uint32_t)std::min<int64_t>(64, std::max<int64_t>(1, (n_cols + target_waves - 1) / target_waves));
+    #ifndef SPG_GMAX
+#define SPG_GMAX 64
+#endif
+    const uint32_t G = (uint32_t)std::min<int64_t>(SPG_GMAX, std::max<int64_t>(1, (n_cols + target_waves - 1) / target_waves));
     KParams P{};
     P.pos_begin = pos_begin;
     P.n_cols = n_cols;

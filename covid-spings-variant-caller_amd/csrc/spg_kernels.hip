@@ -165,17 +165,18 @@ __device__ void merge_acc(Acc *__restrict__ A, const ColState &c, uint32_t batch
 // SWAR classification of 4 entries (one dword of base_code, one of qual)
 //   fast  = valid & q >= max(min_bq,4) & q < 128 & code == M      (the column's major allele)
 //   rare  = valid & (q >= min_bq | q >= 128) & !fast                (exact per-entry path)
+// Eight VALU ops: the q adds cannot carry across bytes (q & 127 plus at most 0x80); the code
+// compare (code ^ M) + 0x7F can only carry out of a byte whose code is >= 128, which is never
+// fast, and a carry can only turn the next byte's "equal" into "not equal" (rare, exact path).
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ void swar4(uint32_t cw, uint32_t qw, uint32_t v80, uint32_t mrep, uint32_t kpass,
                                       uint32_t kok, uint32_t &fast80, uint32_t &rare80) {
     const uint32_t q7 = qw & 0x7F7F7F7Fu;
-    const uint32_t hi80 = qw & 0x80808080u;
-    const uint32_t pass80 = (q7 + kpass) & 0x80808080u;
-    const uint32_t ok80 = (q7 + kok) & 0x80808080u;
-    const uint32_t x = cw ^ mrep;
-    const uint32_t ne80 = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
-    fast80 = ok80 & ~(ne80 | hi80) & v80;
-    rare80 = (pass80 | hi80) & ~fast80 & v80;
+    const uint32_t pass = q7 + kpass;                  // bit 7: (q & 127) >= min_bq
+    const uint32_t ok = q7 + kok;                      // bit 7: (q & 127) >= max(min_bq, 4)
+    const uint32_t ne = (cw ^ mrep) + 0x7F7F7F7Fu;     // bit 7: code != M (codes < 128)
+    fast80 = ok & ~(ne | qw | cw) & v80;
+    rare80 = (pass | qw) & ~fast80 & v80;
 }
 
 __device__ __forceinline__ uint32_t valid80(int32_t x, int32_t b, int32_t e) {   // bytes x..x+3 in [b,e)
@@ -260,10 +261,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t column_rsrc(const uint8_t *p, 
     return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)__builtin_amdgcn_readfirstlane(n), 0x00020000);
 }
 
-template <int W>
+// NT: non-temporal loads (aux = 2) for batches far larger than the 256 MiB Infinity Cache, which a
+// default-policy stream only thrashes (10,000x: 6 % faster; batches that fit lose ~2 %)
+template <int W, bool NT>
 __device__ __forceinline__ typename Vec<W>::T bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    if constexpr (W == 4) return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
-    else return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+    if constexpr (W == 4) return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, NT ? 2 : 0);
+    else return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, NT ? 2 : 0);
 }
 
 __device__ __forceinline__ void write_hist(const KParams &P) {
@@ -276,7 +279,17 @@ __device__ __forceinline__ void write_hist(const KParams &P) {
 // merge of rare record, fast sums and (not FRESH) the record already in HBM — in LDS, and the wave
 // writes the records with 16-B stores, ten lanes per record.  The serial per-column work of
 // process_pileup_column / process_svn's dict bookkeeping (:77-101) thus runs lane-parallel.
-constexpr int NB = 8;        // columns a wave finishes together
+#ifndef SPG_NB
+#define SPG_NB 8
+#endif
+#ifndef SPG_SEG_WPE
+#define SPG_SEG_WPE 4
+#endif
+#ifndef SPG_GMAX
+#define SPG_GMAX 64
+#endif
+constexpr int NB = SPG_NB;   // columns a wave finishes together
+constexpr int KW = 4;        // waves per k_acc_seg workgroup
 
 struct ColSum {              // one finished column's fast-path statistics (written by lane 0)
     uint32_t M, M2, fc, fs, fc2, fs2, ffirst, ffirst2;
@@ -370,7 +383,7 @@ struct Dual2 {              // per-lane partial sums of a wave's second fast all
 // WPE: minimum waves per SIMD the register allocation must allow.  4 (128 VGPRs) for mid-depth
 // batches, whose waves stream few chunks per column and need occupancy to hide the column starts;
 // 3 (up to 168 VGPRs, no spills) for deep batches, where the chunk loop dominates.
-template <int W, bool FRESH, int WPE>
+template <int W, bool FRESH, int WPE, bool NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_acc_seg(KParams P, const uint64_t *__restrict__ off,
                                                  const uint8_t *__restrict__ code, const uint8_t *__restrict__ qual,
                                                  const uint8_t *__restrict__ ref, const Tables *__restrict__ T,
@@ -383,22 +396,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     // LUT rows 0..127: {ln(1-eps), eps} for q < 128; rows 128..255: {0, 0} (the fast path's index
     // for entries that are not fast; the rare path reads q >= 128 from the global table)
     __shared__ double2 lut[256];
-    __shared__ WaveRare rare[4][NB];
-    __shared__ ColSum csum[4][NB];
-    __shared__ RareItem rqueue[4][QCAP];
-    __shared__ int32_t rqo[4][QCAP];
-    __shared__ uint32_t rqr[4][QCAP];
-    __shared__ Dual2 dual2[4];
-    __shared__ Acc accimg[4][NB];
-    __shared__ ColDesc coldesc[4][64];
+    __shared__ WaveRare rare[KW][NB];
+    __shared__ ColSum csum[KW][NB];
+    __shared__ RareItem rqueue[KW][QCAP];
+    __shared__ int32_t rqo[KW][QCAP];
+    __shared__ uint32_t rqr[KW][QCAP];
+    __shared__ Dual2 dual2[KW];
+    __shared__ Acc accimg[KW][NB];
+    __shared__ ColDesc coldesc[KW][SPG_GMAX];
     write_hist(P);
-    {
-        const uint32_t q = threadIdx.x;
+    for (uint32_t q = threadIdx.x; q < 256u; q += 64u * KW)
         lut[q] = q < 128u ? make_double2(T->fast[q][0], T->fast[q][1]) : make_double2(0.0, 0.0);
-    }
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t wave = (int64_t)blockIdx.x * KW + (threadIdx.x >> 6);
     const int64_t g0 = wave * P.G;
     if (g0 >= P.n_cols) return;
     const int ng = (int)min((int64_t)P.G, P.n_cols - g0);
@@ -515,9 +526,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         return p_a + (ii - p_pre) * STEP + lo;
     };
 
-    V c0 = bload<W>(rc, chunk_off(0)), q0 = bload<W>(rq, chunk_off(0));
-    V c1 = bload<W>(rc, chunk_off(1)), q1 = bload<W>(rq, chunk_off(1));
-    V c2, q2;
+    // register ring of three chunks: two loads stay in flight while one chunk is processed
+    V c0, q0, c1, q1, c2, q2;
+#define SPG_LD(C, Q, I) do { const uint32_t o_ = chunk_off(I); C = bload<W, NT>(rc, o_); Q = bload<W, NT>(rq, o_); } while (0)
+    SPG_LD(c0, q0, 0u);
+    SPG_LD(c1, q1, 1u);
 
     // per-column state (consumption cursor)
     uint32_t ck = 0xFFFFFFFFu, cj = 0, crefc = 0;
@@ -530,6 +543,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     uint32_t ffirst2 = INF32;
     bool found2 = false;
 
+    // rare entries of a chunk (bit 8 b + 7 - d of rany: byte b of dword d): queue the lane slices
+    // that hold any for the drain
+    auto enqueue = [&](const V &cc, const V &qq, uint32_t rany, int32_t rel) {
+        const uint64_t bal = __ballot(rany != 0);
+        if (bal) {
+            const uint32_t n = (uint32_t)__popcll(bal);
+            if (qn + n > QCAP) drain();
+            if (rany) {
+                const uint32_t slot = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                RareItem &it = Q[slot];
+#pragma unroll
+                for (int d = 0; d < W; d++) {
+                    it.c[d] = dw<W>(cc, d);
+                    it.q[d] = dw<W>(qq, d);
+                }
+                QO[slot] = rel;
+                QR[slot] = rany | nb;           // rany bits 0-3 are free: ring slot
+            }
+            qn += n;
+        }
+    };
+
+    // One chunk.  Every chunk takes the same generic SWAR path (validity masks, exact q >= 128
+    // handling): specialised bodies for full / all-q<128 chunks measured slower, their extra code
+    // and registers costing more occupancy than the instructions they save.
     auto process = [&](const V &cc, const V &qq, uint32_t i) {
         if (i == cpre + cn) {                  // next column with chunks
             ck++;
@@ -569,54 +608,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
             wave_sync();
         }
         const int32_t o = (int32_t)(cs * STEP + lo);
-        const bool full = (int32_t)(cs * STEP) >= bl && (int32_t)(cs * STEP + STEP) <= el;   // wave-uniform
-        // Lean chunks: no byte of the chunk has bit 7 set (q < 128, code < 128) and min_bq >= 4, so
-        // one SWAR add per dword tests q >= min_bq (no carry) and one xor-add tests code != M
-        // (codes < 128: no carry); q >= 128 or a stray code byte sends the chunk down the exact
-        // generic path.
-        bool lean = false;
-        if (P.kpass == P.kok) {
-            uint32_t h = 0;
+        uint32_t vm[W];                         // entries of the lane slice inside the column
+        if ((int32_t)(cs * STEP) >= bl && (int32_t)(cs * STEP + STEP) <= el) {   // full chunk (uniform)
 #pragma unroll
-            for (int d = 0; d < W; d++) h |= dw<W>(cc, d) | dw<W>(qq, d);
-            lean = __ballot((h & 0x80808080u) != 0u) == 0;
+            for (int d = 0; d < W; d++) vm[d] = 0x80808080u;
+        } else {
+            valid_masks<W>(o, bl, el, vm);
         }
-        uint32_t vm[W];                         // partial chunks and every generic non-dual chunk
-        if (!full || (!lean && !dual)) valid_masks<W>(o, bl, el, vm);
         // SWAR classes of dword d: fast (major), second (dual mode) and rare.  Recomputed where
         // needed instead of kept in registers across the chunk.
-        auto classify = [&](auto full_tag, auto dual_tag, auto lean_tag, int d, uint32_t &f80, uint32_t &g80,
-                            uint32_t &r80, bool again = false) {
-            constexpr bool FULL = decltype(full_tag)::value;
+        auto classify = [&](auto dual_tag, int d, uint32_t &f80, uint32_t &g80, uint32_t &r80, bool again = false) {
             constexpr bool DUAL = decltype(dual_tag)::value;
-            constexpr bool LEAN = decltype(lean_tag)::value;
             uint32_t cw = dw<W>(cc, d), qw = dw<W>(qq, d);
             if (again) asm volatile("" : "+v"(cw), "+v"(qw));   // a recomputation, not a value kept live
-            const uint32_t v = FULL ? 0x80808080u : vm[d];
             g80 = 0;
-            if constexpr (LEAN) {
-                const uint32_t t = qw + P.kpass;                      // bit 7: q >= min_bq
-                const uint32_t n = (cw ^ mrep) + 0x7F7F7F7Fu;         // bit 7: code != M
-                f80 = t & ~n & v;
-                r80 = t & n & v;
-                if constexpr (DUAL) {
-                    const uint32_t n2 = (cw ^ mrep2) + 0x7F7F7F7Fu;
-                    g80 = t & ~n2 & v;
-                    r80 &= n2;
-                }
-            } else {
-                swar4(cw, qw, v, mrep, P.kpass, P.kok, f80, r80);
-                if constexpr (DUAL) {
-                    uint32_t r2;
-                    swar4(cw, qw, v, mrep2, P.kpass, P.kok, g80, r2);
-                    r80 &= ~g80;
-                }
+            swar4(cw, qw, vm[d], mrep, P.kpass, P.kok, f80, r80);
+            if constexpr (DUAL) {
+                uint32_t r2;
+                swar4(cw, qw, vm[d], mrep2, P.kpass, P.kok, g80, r2);
+                r80 &= ~g80;
             }
         };
-        auto body = [&](auto full_tag, auto dual_tag, auto sl_tag, auto lean_tag) {
+        auto body = [&](auto dual_tag, auto sl_tag) {
             constexpr bool DUAL = decltype(dual_tag)::value;
             constexpr bool SL = decltype(sl_tag)::value;     // false: counts / sum(q) only (calls-only REF major)
-            constexpr bool LEAN = decltype(lean_tag)::value;
             uint32_t rany = 0;                  // the chunk slice's rare entries: bit 8 b + 7 - d
             uint32_t fcnt2 = 0, fsq2 = 0, lsq = 0;
             double fsl2 = 0.0, fse2 = 0.0;
@@ -624,7 +639,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
             for (int d = 0; d < W; d++) {
                 const uint32_t qw = dw<W>(qq, d);
                 uint32_t f80, g80, r80;
-                classify(full_tag, dual_tag, lean_tag, d, f80, g80, r80);
+                classify(dual_tag, d, f80, g80, r80);
                 if constexpr (DUAL) {           // the second allele's entries leave the rare set
                     fcnt2 += __popc(g80);
                     fsq2 = __builtin_amdgcn_udot4(qw, g80 >> 7, fsq2, false);
@@ -639,23 +654,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                     asm volatile("" : "+v"(fsl2), "+v"(fse2) :: "memory");
                 }
                 fcnt += __popc(f80);
-                // lean: q < 128, so q * 0x80 sums of one chunk fit (16 x 127 x 128), shifted once below
-                if constexpr (LEAN) lsq = __builtin_amdgcn_udot4(qw, f80, lsq, false);
-                else fsq = __builtin_amdgcn_udot4(qw, f80 >> 7, fsq, false);
-                // fast entries have q < 128: their row is q; every other byte gets bit 7 -> a zero row
-                const uint32_t idx = (LEAN ? qw : (qw & 0x7F7F7F7Fu)) ^ f80 ^ 0x80808080u;
+                // fast entries have q < 128: q * 0x80 sums of one chunk fit, shifted once below
+                lsq = __builtin_amdgcn_udot4(qw, f80, lsq, false);
                 if constexpr (SL) {
+                    // fast entries have q < 128: their row is q; every other byte gets bit 7 -> a zero row
+                    const uint32_t idx = (qw & 0x7F7F7F7Fu) ^ f80 ^ 0x80808080u;
                     const double2 t0 = lut[idx & 0xFFu], t1 = lut[(idx >> 8) & 0xFFu];
                     const double2 t2 = lut[(idx >> 16) & 0xFFu], t3 = lut[idx >> 24];
                     fsl += (t0.x + t1.x) + (t2.x + t3.x);
                     fse += (t0.y + t1.y) + (t2.y + t3.y);
                     asm volatile("" : "+v"(fsl), "+v"(fse) :: "memory");   // keep each dword's lookups together
-                } else {
-                    (void)idx;
                 }
                 rany |= d == 0 ? r80 : r80 >> d;
             }
-            if constexpr (LEAN) fsq += lsq >> 7;
+            fsq += lsq >> 7;
             if constexpr (DUAL) {
                 // second allele: lane-private LDS accumulators (no registers held across chunks)
                 __hip_atomic_fetch_add(&D2->cnt[lane], fcnt2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -668,7 +680,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
 #pragma unroll
                 for (int d = W - 1; d >= 0; d--) {
                     uint32_t f80, g80, r80;
-                    classify(full_tag, dual_tag, lean_tag, d, f80, g80, r80, true);
+                    classify(dual_tag, d, f80, g80, r80, true);
                     if (f80) mine = (uint32_t)(o + 4 * d - bl) + ((uint32_t)__builtin_ctz(f80) >> 3);
                     if (DUAL && g80) mine2 = (uint32_t)(o + 4 * d - bl) + ((uint32_t)__builtin_ctz(g80) >> 3);
                 }
@@ -683,44 +695,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                     if (b) { ffirst2 = __builtin_amdgcn_readlane(mine2, (int)__builtin_ctzll(b)); found2 = true; }
                 }
             }
-            if (__ballot(rany != 0)) {         // rare entries: queue this lane slice for the drain
-                const uint64_t bal = __ballot(rany != 0);
-                const uint32_t n = (uint32_t)__popcll(bal);
-                if (qn + n > QCAP) drain();
-                if (rany) {
-                    const uint32_t slot = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
-                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                    RareItem &it = Q[slot];
-#pragma unroll
-                    for (int d = 0; d < W; d++) {
-                        it.c[d] = dw<W>(cc, d);
-                        it.q[d] = dw<W>(qq, d);
-                    }
-                    QO[slot] = o - bl;
-                    QR[slot] = rany | nb;           // rany bits 0-3 are free: ring slot
-                }
-                qn += n;
-            }
+            enqueue(cc, qq, rany, o - bl);
         };
         using T_ = std::true_type;
         using F_ = std::false_type;
-        if (dual) {
-            if (full) body(T_{}, T_{}, T_{}, F_{});
-            else body(F_{}, T_{}, T_{}, F_{});
-        } else if (sem || !P.calls_only) {
-            if (lean) {
-                if (full) body(T_{}, F_{}, T_{}, T_{});
-                else body(F_{}, F_{}, T_{}, T_{});
-            } else {
-                body(F_{}, F_{}, T_{}, F_{});
-            }
-        } else {                               // calls-only, REF major: counts and sum(q) only
-            if (lean) {
-                if (full) body(T_{}, F_{}, F_{}, T_{});
-                else body(F_{}, F_{}, F_{}, T_{});
-            } else {
-                body(F_{}, F_{}, F_{}, F_{});
-            }
+        if (dual) body(T_{}, T_{});
+        else if (sem || !P.calls_only) body(F_{}, T_{});
+        else {                                 // calls-only, REF major: counts and sum(q) only
+            body(F_{}, F_{});
             skipped = true;
         }
         if (cs + 1 == cn) {                    // ---- column end ----
@@ -745,15 +727,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     };
 
     for (uint32_t i = 0; i < total; i += 3) {
-        c2 = bload<W>(rc, chunk_off(i + 2)); q2 = bload<W>(rq, chunk_off(i + 2));
-        process(c0, q0, i);
-        if (i + 1 >= total) break;
-        c0 = bload<W>(rc, chunk_off(i + 3)); q0 = bload<W>(rq, chunk_off(i + 3));
-        process(c1, q1, i + 1);
-        if (i + 2 >= total) break;
-        c1 = bload<W>(rc, chunk_off(i + 4)); q1 = bload<W>(rq, chunk_off(i + 4));
-        process(c2, q2, i + 2);
+        SPG_LD(c2, q2, i + 2); process(c0, q0, i); if (i + 1 >= total) break;
+        SPG_LD(c0, q0, i + 3); process(c1, q1, i + 1); if (i + 2 >= total) break;
+        SPG_LD(c1, q1, i + 4); process(c2, q2, i + 2);
     }
+#undef SPG_LD
     if (nb) finish();
 }
 
@@ -1114,16 +1092,17 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
         hipLaunchKernelGGL(k_acc_shallow, dim3((unsigned)blocks), dim3(128), 0, st, P, off, code, qual, ref, T, acc);
     }
     const int64_t waves = (P.n_cols + P.G - 1) / P.G;
-    const int64_t blocks = (waves + 3) / 4;
+    const int64_t blocks = (waves + KW - 1) / KW;
     const bool fresh = P.batch_seq == 1;
     const bool w4 = P.t_deep <= 1;
-#define SPG_SEG(WW, FF, OO) hipLaunchKernelGGL((k_acc_seg<WW, FF, OO>), dim3((unsigned)blocks), dim3(256), 0, st, P, off, code, qual, ref, T, acc)
-    const bool deep = P.n_entries >= (uint64_t)P.n_cols * 4096u;    // >= 4 chunks per column on average
+    // batches far beyond the 256 MiB Infinity Cache stream with non-temporal loads
+    const bool nt = 2 * P.n_entries > (192ull << 20);
+#define SPG_SEG(WW, FF, NN) hipLaunchKernelGGL((k_acc_seg<WW, FF, SPG_SEG_WPE, NN>), dim3((unsigned)blocks), dim3(64 * KW), 0, st, P, off, code, qual, ref, T, acc)
     if (w4) {
-        if (deep) { if (fresh) SPG_SEG(4, true, 3); else SPG_SEG(4, false, 3); }
-        else { if (fresh) SPG_SEG(4, true, 4); else SPG_SEG(4, false, 4); }
+        if (nt) { if (fresh) SPG_SEG(4, true, true); else SPG_SEG(4, false, true); }
+        else { if (fresh) SPG_SEG(4, true, false); else SPG_SEG(4, false, false); }
     } else {
-        if (fresh) SPG_SEG(1, true, 4); else SPG_SEG(1, false, 4);
+        if (fresh) SPG_SEG(1, true, false); else SPG_SEG(1, false, false);
     }
 #undef SPG_SEG
     return hipGetLastError();
