@@ -154,6 +154,14 @@ def end_to_end(args, device):
     return res
 
 
+def kernel_name(E, C):
+    """The accumulate instantiation launch_accumulate (csrc/spg_kernels.hip) picks for this batch."""
+    if E < 256 * C:
+        return "k_acc_shallow + k_acc_seg<1,true,4,false> (spg_accumulate)"
+    nt = 2 * E > (192 << 20)
+    return f"k_acc_seg<4,true,4,{'true' if nt else 'false'}> (spg_accumulate{'; non-temporal loads' if nt else ''})"
+
+
 def pmc_traffic(E):
     """HBM bytes per launch of the accumulate kernel from the newest committed PMC summary
     (profiles/rNN_bench_pmc.json, written by tools/summarize_prof.py from rocprofv3 --pmc passes of
@@ -287,7 +295,7 @@ def main():
                    "engine_mode": "full_table" if args.full_table else "calls_only"},
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM, "traffic": pmc_traffic(E),
-                     "kernel": "k_acc_seg<4,true,3> (spg_accumulate)", "kernel_ms": t_acc * 1e3, "algorithmic_bytes": algo_bytes},
+                     "kernel": kernel_name(E, C), "kernel_ms": t_acc * 1e3, "algorithmic_bytes": algo_bytes},
         "finalize_ms": t_fin * 1e3, "candidates_per_gpu_step": n_cand, "datagen_s": t_gen,
         "calls_gathered_per_step": sum(gathered) if gathered is not None else n_cand,
     }
