@@ -239,6 +239,56 @@ int spg_set_reference(spg_ctx *c, const char *seq, int64_t len) {
     return 0;
 }
 
+// SPG_TRACE=1 (debugging): synchronise after every launch and name the kernel that failed
+static bool trace_on() {
+    static const bool on = [] { const char *e = getenv("SPG_TRACE"); return e && atoi(e) > 0; }();
+    return on;
+}
+static uint32_t *trace_dbg() {      // device words the kernels record range violations in
+    static uint32_t *d = [] { uint32_t *p = nullptr; if (hipMalloc(&p, 64) == hipSuccess) (void)hipMemset(p, 0, 64); return p; }();
+    return d;
+}
+static uint4 *g_prog = nullptr;      // SPG_TRACE: host-mapped per-wave progress of the last accumulate
+static size_t g_prog_n = 0;
+static uint4 *trace_prog(int64_t n_waves) {
+    if (!trace_on()) return nullptr;
+    if ((size_t)n_waves > g_prog_n) {
+        if (g_prog) (void)hipHostFree(g_prog);
+        g_prog = nullptr;
+        g_prog_n = 0;
+        if (hipHostMalloc((void **)&g_prog, sizeof(uint4) * n_waves, hipHostMallocMapped) != hipSuccess) return nullptr;
+        g_prog_n = (size_t)n_waves;
+    }
+    memset(g_prog, 0, sizeof(uint4) * g_prog_n);
+    uint4 *d = nullptr;
+    if (hipHostGetDevicePointer((void **)&d, g_prog, 0) != hipSuccess) return nullptr;
+    return d;
+}
+static int trace_sync(spg_ctx *c, const char *what) {
+    if (!trace_on()) return 0;
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    if (g_prog && e != hipSuccess) {     // which waves were where when the kernel faulted
+        size_t hist[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        int shown = 0;
+        for (size_t w = 0; w < g_prog_n; w++) {
+            const volatile uint32_t *r = reinterpret_cast<volatile uint32_t *>(g_prog + w);
+            const uint32_t st = r[0];
+            hist[st < 8 ? st : 7]++;
+            if (st != 0 && st != 6 && shown < 32) {
+                fprintf(stderr, "[spg trace] wave %zu stage %u: %u %u %u\n", w, st, r[1], r[2], r[3]);
+                shown++;
+            }
+        }
+        fprintf(stderr, "[spg trace] stages 0-7: %zu %zu %zu %zu %zu %zu %zu %zu\n", hist[0], hist[1], hist[2],
+                hist[3], hist[4], hist[5], hist[6], hist[7]);
+    }
+    uint32_t h[4] = {0, 0, 0, 0};
+    if (e == hipSuccess && trace_dbg()) (void)hipMemcpy(h, trace_dbg(), sizeof(h), hipMemcpyDeviceToHost);
+    fprintf(stderr, "[spg trace] %s: %s dbg %u %u %u %08x\n", what, hipGetErrorString(e), h[0], h[1], h[2], h[3]);
+    fflush(stderr);
+    return e == hipSuccess ? 0 : fail(std::string("spg trace: ") + what + ": " + hipGetErrorString(e));
+}
+
 static int grow_history_table(spg_ctx *c) {
     const int64_t n = (int64_t)c->hist.size();
     if (n <= c->d_hist_cap) return 0;
@@ -341,11 +391,14 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
     P.t_deep = deep_batch ? 1u : 128u;
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
     P.n_entries = n_entries;
+    P.dbg = trace_on() ? trace_dbg() : nullptr;
+    P.prog = trace_prog((n_cols + G - 1) / G + 4);
     hipEvent_t *ev = c->ev[c->ring_w % spg_ctx::NRING];
     if (!c->acc_open) c->acc_timing = c->timing;
     const int tm = c->acc_timing;
     if (tm >= 1 && !c->acc_open) HIPCHK(hipEventRecord(ev[0], c->stream));
     HIPCHK(launch_accumulate(P, hb.off, hb.code, hb.qual, c->ref, c->tables, c->acc, c->stream));
+    if (trace_sync(c, "accumulate")) return -1;
     if (tm >= 1) HIPCHK(hipEventRecord(ev[1], c->stream));
     c->acc_open = true;
     c->acc_any = true;
@@ -407,6 +460,7 @@ static int finalize_impl(spg_ctx *c, bool table) {
     FParams F = make_fparams(c);
     F.table = table ? 1u : 0u;
     HIPCHK(launch_finalize(F, c->acc, c->tables, make_out(c), c->d_hist, c->stream));
+    if (trace_sync(c, "finalize")) return -1;
     c->table_valid = table;
     if (ft >= 2) HIPCHK(hipEventRecord(ev[3], c->stream));
     c->last_acc = c->acc_open && c->acc_timing >= 1;

@@ -239,14 +239,10 @@ __device__ __forceinline__ void rare_entry(WaveRare *R, uint32_t code, uint32_t 
     atomicAdd(&R->sq[sl], q);
     atomicMin(&R->qf[sl], q);
     atomicMin(&R->first[sl], idx);
-    // {ln(1-eps), eps}; row 0 holds {0, 0}; q >= 128 (never a fast entry) from the global table,
-    // in a branch of its own: volatile, or hipcc merges the two loads into a flat load of a selected
-    // pointer that every rare entry would pay, with a vmcnt(0) that drains the chunk prefetch
-    double2 t = lut[q & 127u];
-    if (q >= 128u) {
-        const volatile double *g = &T->fast[q][0];
-        t = make_double2(g[0], g[1]);
-    }
+    // {ln(1-eps), eps}; row 0 holds {0, 0}; q >= 128 (never a fast entry) from rows 256..383, so the
+    // drain touches no global memory (a global load here would also wait for the chunk prefetch)
+    (void)T;
+    const double2 t = lut[q < 128u ? q : q + 128u];
     atomicAdd(&R->sl[sl], t.x);
     atomicAdd(&R->se[sl], q == 0 ? 1.0 : t.y);         // eps(Q0) = 1
 }
@@ -394,8 +390,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     constexpr uint32_t QCAP = 64;                      // per-wave queue of lane slices holding rare entries (>= 64:
                                                        // a drain must leave room for every lane's slice)
     // LUT rows 0..127: {ln(1-eps), eps} for q < 128; rows 128..255: {0, 0} (the fast path's index
-    // for entries that are not fast; the rare path reads q >= 128 from the global table)
-    __shared__ double2 lut[256];
+    // for entries that are not fast); rows 256..383: q = 128..255 for the rare path
+    __shared__ double2 lut[384];
     __shared__ WaveRare rare[KW][NB];
     __shared__ ColSum csum[KW][NB];
     __shared__ RareItem rqueue[KW][QCAP];
@@ -405,14 +401,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     __shared__ Acc accimg[KW][NB];
     __shared__ ColDesc coldesc[KW][SPG_GMAX];
     write_hist(P);
-    for (uint32_t q = threadIdx.x; q < 256u; q += 64u * KW)
+    for (uint32_t q = threadIdx.x; q < 256u; q += 64u * KW) {
         lut[q] = q < 128u ? make_double2(T->fast[q][0], T->fast[q][1]) : make_double2(0.0, 0.0);
+        if (q >= 128u) lut[q + 128u] = make_double2(T->fast[q][0], T->fast[q][1]);
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * KW + (threadIdx.x >> 6);
     const int64_t g0 = wave * P.G;
     if (g0 >= P.n_cols) return;
     const int ng = (int)min((int64_t)P.G, P.n_cols - g0);
+    // SPG_TRACE: lane 0 posts (stage, a, b, c) to host-mapped memory, so a fault leaves each wave's
+    // last step readable by the host
+    auto prog = [&](uint32_t stage, uint32_t a, uint32_t b, uint32_t c) {
+        if (P.prog && lane == 0) {
+            uint32_t *pp = reinterpret_cast<uint32_t *>(P.prog + wave);
+            __hip_atomic_store(pp + 1, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(pp + 2, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(pp + 3, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(pp, stage, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    };
+    prog(1, (uint32_t)g0, (uint32_t)ng, 0);
     WaveRare *RR = rare[threadIdx.x >> 6];             // rare records of the ring's columns
     ColSum *CS = csum[threadIdx.x >> 6];
     Dual2 *D2 = dual2 + (threadIdx.x >> 6);
@@ -432,7 +442,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     uint32_t mrep2 = 0, M2 = 0;
     bool sem = true;                           // the major is not the REF char (calls-only mode skips REF sums)
     bool skipped = false;                      // this column's major skipped its likelihood sums
-    auto drain = [&]() {
+    auto drain = [&]() __attribute__((always_inline)) {
+        prog(3, qn, nb, 0);
         wave_sync();
         for (uint32_t b0 = 0; b0 < qn; b0 += 64) {
             if (b0 + lane < qn) {
@@ -457,7 +468,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
 
     // Finish the ring: drain the queue, lane j assembles column j's record in LDS, the wave stores the
     // records (16 B per lane, ten lanes per record).
-    auto finish = [&]() {
+    auto finish = [&]() __attribute__((always_inline)) {
         if (qn) drain();
         else wave_sync();
         if ((uint32_t)lane < nb) {
@@ -465,9 +476,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
             assemble_record<FRESH>(P, acc + P.pos_begin + g0 + S->cj, RR + lane, S, img + lane);
         }
         wave_sync();
+        prog(4, nb, CS[0].cj, CS[nb - 1].cj);
         Acc *base = acc + P.pos_begin + g0;
         for (uint32_t t = (uint32_t)lane; t < 10u * nb; t += 64u) {
             const uint32_t r = t / 10u, piece = t - 10u * r;
+            if (P.dbg && CS[r].cj >= (uint32_t)ng) {                   // SPG_TRACE: record outside the group
+                atomicAdd(P.dbg + 2, 1u);
+                P.dbg[3] = CS[r].cj | ((uint32_t)ng << 8) | (r << 16) | (nb << 24);
+                continue;
+            }
             reinterpret_cast<uint4 *>(base + CS[r].cj)[piece] = reinterpret_cast<const uint4 *>(img + r)[piece];
         }
         nb = 0;
@@ -478,6 +495,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     uint64_t ob = 0, oe = 0;
     uint32_t refc = 0;
     if (lane < ng) { ob = off[g0 + lane]; oe = off[g0 + lane + 1]; refc = ref[P.pos_begin + g0 + lane]; }
+    if (P.dbg && lane < ng && (oe < ob || oe > P.n_entries)) {       // SPG_TRACE: bad CSR offsets
+        atomicAdd(P.dbg, 1u);
+        P.dbg[1] = (uint32_t)(g0 + lane);
+        ob = oe = 0;
+    }
     const uint64_t sb = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)ob) |
                         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ob >> 32)) << 32);
     const uint64_t base = sb & ~(uint64_t)(ALIGN - 1);
@@ -582,6 +604,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         }
         cs = i - cpre;
         if (cs == 0) {                         // ---- column begin ----
+            prog(2, ck, i, cn);
             rare_init(RR + nb, lane);
             const uint32_t v0 = dw<W>(cc, 0) & 0xFFu;
             const int vote = ((int32_t)lo >= bl && (int32_t)lo < el) ? (int)v0 : -1;
@@ -732,7 +755,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         SPG_LD(c1, q1, i + 4); process(c2, q2, i + 2);
     }
 #undef SPG_LD
+    prog(5, total, nb, qn);
     if (nb) finish();
+    prog(6, 0, 0, 0);
 }
 
 // Short columns (< t_deep raw entries): one lane per column.  The lane walks its column in
