@@ -62,8 +62,8 @@ __device__ __forceinline__ uint32_t dpp_u32(uint32_t v, int ctrl) {
 __device__ __forceinline__ uint32_t dsum_u32(uint32_t v) {
 #pragma unroll
     for (int c = 0; c < 4; c++) v += dpp_u32(v, c);
-    return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) +
-           __builtin_amdgcn_readlane(v, 32) + __builtin_amdgcn_readlane(v, 48);
+    return (uint32_t)__builtin_amdgcn_readlane(v, 0) + (uint32_t)__builtin_amdgcn_readlane(v, 16) +
+           (uint32_t)__builtin_amdgcn_readlane(v, 32) + (uint32_t)__builtin_amdgcn_readlane(v, 48);
 }
 __device__ __forceinline__ double rl_f64(double v, int l) {
     const uint64_t b = __builtin_bit_cast(uint64_t, v);
@@ -500,11 +500,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         P.dbg[1] = (uint32_t)(g0 + lane);
         ob = oe = 0;
     }
-    const uint64_t sb = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)ob) |
-                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ob >> 32)) << 32);
+    // (the lane builtins return int: widen through uint32_t, or offsets >= 2^31 sign-extend into a
+    // wild segment base)
+    const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ob) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(ob >> 32)) << 32);
     const uint64_t base = sb & ~(uint64_t)(ALIGN - 1);
-    const uint64_t send = (uint64_t)__builtin_amdgcn_readlane((uint32_t)oe, ng - 1) |
-                          ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(oe >> 32), ng - 1) << 32);
+    const uint64_t send = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)oe, ng - 1) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(oe >> 32), ng - 1) << 32);
     const uint32_t nbytes = (uint32_t)(((send - base) + ALIGN - 1) & ~(uint64_t)(ALIGN - 1));
     const __amdgpu_buffer_rsrc_t rc = column_rsrc(code + base, nbytes), rq = column_rsrc(qual + base, nbytes);
     const uint32_t b_rel = (uint32_t)(ob - base), e_rel = (uint32_t)(oe - base);

@@ -215,6 +215,38 @@ def test_device_borrowed_input_matches_host_input():
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("calls_only", [False, True])
+def test_offsets_beyond_2_31(calls_only):
+    """Device CSR whose entries sit past byte 2^31 of the code/qual buffers (a 100,000x SARS-CoV-2
+    batch reaches 3e9): the deep kernel's segment base must widen the CSR offsets unsigned."""
+    import torch
+    from covid_spings_variant_caller_amd import synth
+    L = 2000
+    ref = synth.reference(L, seed=8)
+    lo, off, c, q = synth.pileup(L, 10000, seed=9, ref=ref, snv_every=7, lo=900, hi=1020)
+    E = len(c)
+    host = _engine(ref, DEF, calls_only=calls_only)
+    host.accumulate(lo, off, c, q)
+    host.finalize()
+    base = (1 << 31) - 4 * 1024 - 5           # columns straddle 2^31; unaligned start
+    n = base + E + 64
+    dc = torch.empty(n, dtype=torch.uint8, device="cuda")
+    dq = torch.empty(n, dtype=torch.uint8, device="cuda")
+    dc[base:base + E] = torch.from_numpy(c).cuda()
+    dq[base:base + E] = torch.from_numpy(q).cuda()
+    dc[base + E:].fill_(0xFF)
+    dq[base + E:].zero_()
+    do = torch.from_numpy((off.astype(np.int64) + base)).cuda()
+    dev = _engine(ref, DEF, calls_only=calls_only)
+    dev.accumulate(lo, do, dc, dq, borrow=True, n_entries=E)
+    dev.finalize()
+    assert dev.memory_summary() == host.memory_summary()
+    # another 16-B alignment of the entries regroups the fp64 sums (QUAL / GL): tolerance, not bits
+    compare_variants(dev.variants(), host.variants(), rtol=RTOL)
+    del dc, dq
+    torch.cuda.empty_cache()
+
+
 def test_empty_and_degenerate_batches():
     ref = "ACGT" * 50
     eng = _engine(ref, DEF)
