@@ -360,10 +360,13 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
     if (rc) return rc;
     c->batch_seq++;
     // Work decomposition from the batch's mean depth (no per-column host pass, so device inputs
-    // need no host copy of the offsets).  Deep batches (mean >= 2048 entries per column) stream every
+    // need no host copy of the offsets).  Deep batches (mean >= 256 entries per column) stream every
     // column through k_acc_seg<4> (16 entries/lane/chunk); shallower batches run a lane-per-column
     // pass for columns below t_deep = 128 and k_acc_seg<1> (4 entries/lane/chunk) for the rest.
-    // Each wave owns G consecutive columns; G targets ~one resident wave per slot.
+    // Each wave owns G consecutive columns.  A wave's setup (CSR offsets, then its first chunk) costs
+    // two memory round trips, so a deep wave gets ~16 chunks where that still leaves one grid
+    // generation of <= 4,096 waves (16 per CU) to fill the chip (1,000x: G = 8, 3,738 waves:
+    // 40 -> 36 us); otherwise G targets 16,384 waves (10,000x: G = 2, measured best).
     const double avg = (double)n_entries / (double)n_cols;
     static const int64_t target_waves = [] {
         const char *e = getenv("SPG_TARGET_WAVES");
@@ -374,7 +377,13 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
     #ifndef SPG_GMAX
 #define SPG_GMAX 64
 #endif
-    const uint32_t G = (uint32_t)std::min<int64_t>(SPG_GMAX, std::max<int64_t>(1, (n_cols + target_waves - 1) / target_waves));
+    int64_t g = std::max<int64_t>(1, (n_cols + target_waves - 1) / target_waves);
+    if (deep_batch && !getenv("SPG_TARGET_WAVES")) {
+        const int64_t g_chunks = (int64_t)std::ceil(16384.0 / std::max(avg, 1.0));    // ~16 chunks per wave
+        const int64_t g_fill = std::max<int64_t>(1, (n_cols + 4095) / 4096);           // one generation
+        g = std::max<int64_t>(g, std::min(g_chunks, g_fill));
+    }
+    const uint32_t G = (uint32_t)std::min<int64_t>(SPG_GMAX, g);
     KParams P{};
     P.pos_begin = pos_begin;
     P.n_cols = n_cols;
