@@ -373,3 +373,41 @@ def test_many_bams_accumulated():
                                     max_depth=80))
     for calls_only in (False, True):
         _vs_oracle(ref, batches, DEF, calls_only=calls_only)
+
+
+@pytest.mark.parametrize("depth", [10000, 100000])
+def test_full_size_count_conservation(depth):
+    """BASELINE sizes (SARS-CoV-2 at 10,000x: E = 3.0e8; 100,000x: E = 3.0e9, past 2^31) through a
+    size-independent property: every entry with q >= minBaseQuality lands in exactly one position's
+    totalDepth and one allele / D / N bucket (process_pileup_column :75-101), so per-position depth
+    and per-code totals equal direct counts of the CSR."""
+    import torch
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.pileup import synth_batch
+    L = 29903
+    ref = synth.reference(L, seed=1)
+    b = synth_batch(ref, depth, seed=2, n_threads=16)
+    E = b.n_entries
+    keep = b.quals >= 30
+    want_depth = np.add.reduceat(keep, b.offsets[:-1].astype(np.int64)).astype(np.int64)
+    want_depth[np.diff(b.offsets.astype(np.int64)) == 0] = 0
+    want_codes = np.bincount(b.codes[keep], minlength=256)
+    del keep
+    dc = torch.from_numpy(b.codes_padded).cuda()
+    dq = torch.from_numpy(b.quals_padded).cuda()
+    do = torch.from_numpy(b.offsets.view(np.int64).copy()).cuda()
+    eng = PileupEngine(L, 30, 10, 5, 0.10, device=0, reference=ref, calls_only=True)
+    eng.accumulate(0, do, dc, dq, borrow=True, n_entries=E)
+    eng.finalize()
+    t = eng.table()
+    np.testing.assert_array_equal(t["depth"].astype(np.int64), want_depth)
+    cnt = t["counts"].astype(np.int64).sum(axis=0)
+    assert [int(x) for x in cnt[:5]] == [int(want_codes[k]) for k in (1, 2, 4, 8, 15)]
+    assert int(cnt[5]) == int(want_codes[16]) and int(cnt[6]) == int(want_codes[17])
+    assert int(cnt[7]) == int(want_codes.sum() - want_codes[[1, 2, 4, 8, 15, 16, 17]].sum())
+    assert eng.counts()[0] > 0
+    eng.close()
+    del dc, dq, do
+    b.close()
+    torch.cuda.empty_cache()
