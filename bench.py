@@ -173,7 +173,7 @@ def pmc_traffic(E):
     try:
         d = json.load(open(files[-1]))
         rec = next((v for k, v in d.items() if k.startswith("spg::k_acc_seg<4, true")), None)
-        if rec is None or rec.get("entries") not in (None, E):
+        if rec is None or rec.get("entries") != E:
             return None
         return rec.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
