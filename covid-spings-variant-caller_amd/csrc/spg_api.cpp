@@ -79,7 +79,7 @@ struct spg_ctx {
     bool finalized = false;
     // timing ring: one entry per finalize; events around the accumulate launches (first begin ..
     // last end) and around the finalize launch.  Read back without stalling the pipeline.
-    static constexpr int NRING = 64;
+    static constexpr int NRING = 256;
     hipEvent_t ev[NRING][4] = {};
     int64_t ring_w = 0, ring_r = 0;     // entries [ring_r, ring_w) are complete
     uint8_t ring_tm[NRING] = {};        // bit 0: accumulate events recorded, bit 1: finalize events
