@@ -276,7 +276,7 @@ def main():
         step()
     eng.sync()
     _, fin_ms = eng.kernel_times()
-    n_cand = eng.counts()[0]
+    n_cand, n_replay = eng.counts()
     gathered = None
     if dist is not None and rank == 0:
         gathered = [int(o[:8].cpu().numpy().view(np.uint64)[0]) for o in gather_out]
@@ -304,7 +304,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM, "traffic": pmc_traffic(E),
                      "kernel": kernel_name(E, C), "kernel_ms": t_acc * 1e3, "algorithmic_bytes": algo_bytes},
-        "finalize_ms": t_fin * 1e3, "candidates_per_gpu_step": n_cand, "datagen_s": t_gen,
+        "finalize_ms": t_fin * 1e3, "candidates_per_gpu_step": n_cand,
+        "replayed_positions_per_gpu_step": n_replay, "datagen_s": t_gen,
         "calls_gathered_per_step": sum(gathered) if gathered is not None else n_cand,
     }
     if rank == 0 and world == 1 and not args.no_e2e and L == L_SARS:
