@@ -35,6 +35,9 @@ class SpgParams(C.Structure):
 CANDIDATE_DTYPE = np.dtype([("pos", "<i8"), ("dp", "<i4"), ("ad", "<i4"), ("pl", "<i4"), ("score", "<i4"),
                             ("ref", "u1"), ("alt", "u1"), ("gl_zero", "u1"), ("rank", "u1"),
                             ("first_batch", "<u4"), ("gl", "<f8"), ("gl_linear", "<f8"), ("qual", "<f8")])
+# spg_batch (include/spings_gpu.h): one CSR batch of spg_accumulate_batches
+BATCH_DTYPE = np.dtype([("pos_begin", "<i8"), ("n_cols", "<i8"), ("offsets", "<u8"), ("base_code", "<u8"),
+                        ("qual", "<u8"), ("n_entries", "<u8")])
 DETAIL_DTYPE = np.dtype([("pos", "<i8"), ("depth", "<u4"), ("n_alleles", "u1"), ("pad", "u1", 3),
                          ("code", "u1", 16), ("count", "<u4", 16), ("gl", "<f8", 16)])
 
@@ -77,6 +80,10 @@ def gpu_lib():
     _sig(L.spg_set_reference, i32, vp, C.c_char_p, i64)
     _sig(L.spg_accumulate, i32, vp, i64, i64, vp, vp, vp, u64)
     _sig(L.spg_accumulate_ex, i32, vp, i64, i64, vp, vp, vp, u64, C.c_uint32)
+    _sig(L.spg_accumulate_batches, i32, vp, vp, i64, C.c_uint32)
+    _sig(L.spg_host_alloc, i32, C.c_size_t, C.POINTER(vp))
+    _sig(L.spg_host_free, i32, vp)
+    _sig(L.spg_wait_input, i32, vp)
     _sig(L.spg_finalize, i32, vp)
     _sig(L.spg_sync, i32, vp)
     _sig(L.spg_stream, i32, vp, C.POINTER(vp))

@@ -3,6 +3,8 @@
 // libspings_gpu.so.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -17,6 +19,8 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
                              const uint8_t *ref, const Tables *T, Acc *acc, hipStream_t st);
 hipError_t launch_finalize(const FParams &F, const Acc *acc, const Tables *T, const Out &O, const Hist *H,
                            hipStream_t st);
+hipError_t launch_multi(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, bool nt,
+                        int64_t max_blocks, hipStream_t st);
 }  // namespace spg
 
 using namespace spg;
@@ -46,22 +50,72 @@ struct HistBatch {
     uint64_t n_entries;
     uint64_t *off;
     uint8_t *code, *qual;
-    bool owned;
+    bool owned;            // in the context's arena (else borrowed device buffers)
+};
+
+// Device arena for the owned batch copies (the replay history): slabs allocated once and bump-
+// allocated per batch, recycled at spg_reset (no hipMalloc / hipFree per batch).  Copies into a
+// recycled slab are ordered after the kernels that read its old content (reset_fence below).
+struct Arena {
+    struct Slab { uint8_t *base; size_t cap, used; };
+    std::vector<Slab> slabs;
+    size_t cur = 0;
+    hipError_t alloc(size_t n, uint8_t **out) {
+        n = (n + 255) & ~size_t(255);
+        while (cur < slabs.size()) {
+            Slab &s = slabs[cur];
+            if (s.cap - s.used >= n) { *out = s.base + s.used; s.used += n; return hipSuccess; }
+            cur++;
+        }
+        // geometric slabs: 256 MiB, 512 MiB, 1 GiB, ... 8 GiB
+        size_t cap = (size_t)256 << 20;
+        for (size_t i = 0; i < slabs.size() && cap < ((size_t)8 << 30); i++) cap <<= 1;
+        cap = std::max(cap, n);
+        Slab s{nullptr, cap, 0};
+        hipError_t e = hipMalloc(&s.base, cap);
+        if (e != hipSuccess) return e;
+        slabs.push_back(s);
+        cur = slabs.size() - 1;
+        slabs[cur].used = n;
+        *out = s.base;
+        return hipSuccess;
+    }
+    void recycle() { for (auto &s : slabs) s.used = 0; cur = 0; }
+    void release() { for (auto &s : slabs) (void)hipFree(s.base); slabs.clear(); cur = 0; }
 };
 
 struct spg_ctx {
     int device = 0;
     int64_t n_pos = 0;
     spg_params p{};
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;       // kernels
+    hipStream_t copy_stream = nullptr;  // host -> device batch copies
+    hipEvent_t copy_ev = nullptr;       // after the latest batch copy
+    hipEvent_t compute_ev = nullptr;    // reset fence: recycled arena copies wait for the old kernels
+    bool copy_pending = false;          // the compute stream has not waited on copy_ev yet
     Acc *acc = nullptr;
     Tables *tables = nullptr;
     bool lut_set = false;
     uint8_t *ref = nullptr;
     int64_t ref_len = 0;
     std::vector<HistBatch> hist;
-    Hist *d_hist = nullptr;
+    Arena arena;
+    Hist *d_hist = nullptr;             // device descriptors of every history batch
     int64_t d_hist_cap = 0;
+    Hist *h_hist = nullptr;             // pinned host mirror (uploaded per run; append-only)
+    int64_t h_hist_cap = 0;
+    int64_t pend0 = 0;                  // history batches [pend0, size) are not accumulated yet (a run)
+    uint64_t pend_entries = 0;
+    MState *part = nullptr;             // split-run partial states
+    size_t part_bytes = 0;
+    // replay index: history batches per 2^RIDX_SHIFT-position bucket
+    std::vector<std::vector<int32_t>> buckets;
+    bool ridx_dirty = false;
+    int64_t ridx_items = 0;
+    uint32_t *h_ridx = nullptr, *d_ridx = nullptr;   // [n_buckets + 1 offsets | items]
+    size_t ridx_cap = 0;
+    hipEvent_t ridx_ev = nullptr;
+    bool ridx_valid = false;
     uint32_t batch_seq = 0;
     uint32_t epoch = 1;        // Acc records of other epochs read as empty (reset = epoch bump)
     uint32_t cslot = 0;        // Counters slot of the last finalize
@@ -83,12 +137,11 @@ struct spg_ctx {
     hipEvent_t ev[NRING][4] = {};
     int64_t ring_w = 0, ring_r = 0;     // entries [ring_r, ring_w) are complete
     uint8_t ring_tm[NRING] = {};        // bit 0: accumulate events recorded, bit 1: finalize events
-    bool acc_open = false, acc_any = false;
+    bool acc_open = false;
     bool last_acc = false, last_fin = false;
     bool table_valid = false;           // the SoA table matches the last finalize
     int timing = default_timing();
     int acc_timing = 0;                 // level the open / last accumulate interval was recorded at
-    int fin_timing = 0;
 };
 
 
@@ -103,6 +156,18 @@ size_t spg_sizeof_acc(void) { return sizeof(Acc); }
 int spg_device_count(int *n) {
     if (!n) return fail("spg_device_count: null");
     HIPCHK(hipGetDeviceCount(n));
+    return 0;
+}
+
+int spg_host_alloc(size_t bytes, void **out) {
+    if (!out) return fail("spg_host_alloc: null argument");
+    *out = nullptr;
+    HIPCHK(hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+    return 0;
+}
+
+int spg_host_free(void *p) {
+    if (p) HIPCHK(hipHostFree(p));
     return 0;
 }
 
@@ -136,8 +201,13 @@ int spg_create(int device, int64_t n_pos, const spg_params *p, spg_ctx **out) {
     int rc = 0;
     auto bail = [&](int r) { spg_destroy(c); return r; };
     if (hipSetDevice(device) != hipSuccess) return bail(fail("spg_create: hipSetDevice failed"));
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail("spg_create: stream"));
+    if (hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->compute_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ridx_ev, hipEventDisableTiming) != hipSuccess)
+        return bail(fail("spg_create: event"));
     if (hipMalloc(&c->acc, sizeof(Acc) * n_pos) != hipSuccess) return bail(fail("spg_create: acc alloc"));
     if (hipMalloc(&c->tables, sizeof(Tables)) != hipSuccess) return bail(fail("spg_create: tables alloc"));
     if (hipMemsetAsync(c->acc, 0, sizeof(Acc) * n_pos, c->stream) != hipSuccess) return bail(fail("memset"));
@@ -145,33 +215,41 @@ int spg_create(int device, int64_t n_pos, const spg_params *p, spg_ctx **out) {
     for (auto &row : c->ev)
         for (auto &e : row)
             if (hipEventCreate(&e) != hipSuccess) return bail(fail("spg_create: event"));
+    c->buckets.resize((size_t)((n_pos + (1 << RIDX_SHIFT) - 1) >> RIDX_SHIFT));
     *out = c;
     return 0;
 }
 
-static void free_history(spg_ctx *c) {
-    for (auto &h : c->hist)
-        if (h.owned) {
-            (void)hipFree(h.off);
-            (void)hipFree(h.code);
-            (void)hipFree(h.qual);
-        }
+static void clear_history(spg_ctx *c) {
     c->hist.clear();
+    c->arena.recycle();
+    c->pend0 = 0;
+    c->pend_entries = 0;
+    for (auto &b : c->buckets) b.clear();
+    c->ridx_items = 0;
+    c->ridx_dirty = false;
+    c->ridx_valid = false;
 }
 
 int spg_destroy(spg_ctx *c) {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    free_history(c);
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    c->arena.release();
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
-                    c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr};
+                    c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
+    if (c->h_hist) (void)hipHostFree(c->h_hist);
+    if (c->h_ridx) (void)hipHostFree(c->h_ridx);
     for (auto &row : c->ev)
         for (auto &e : row)
             if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {c->copy_ev, c->compute_ev, c->ridx_ev})
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     delete c;
     return 0;
 }
@@ -179,10 +257,11 @@ int spg_destroy(spg_ctx *c) {
 int spg_reset(spg_ctx *c) {
     if (!c) return fail("spg_reset: null ctx");
     HIPCHK(hipSetDevice(c->device));
-    bool owned = false;
-    for (auto &h : c->hist) owned |= h.owned;
-    if (owned) HIPCHK(hipStreamSynchronize(c->stream));
-    free_history(c);
+    // batches still pending belong to the old sample: dropped.  Copies into the recycled arena are
+    // ordered after every kernel enqueued so far.
+    HIPCHK(hipEventRecord(c->compute_ev, c->stream));
+    HIPCHK(hipStreamWaitEvent(c->copy_stream, c->compute_ev, 0));
+    clear_history(c);
     if (++c->epoch == 0) {     // wrapped: clear the records once and restart at epoch 1
         HIPCHK(hipMemsetAsync(c->acc, 0, sizeof(Acc) * c->n_pos, c->stream));
         c->epoch = 1;
@@ -224,9 +303,13 @@ int spg_set_eps_lut(spg_ctx *c, const double lut[256]) {
     return 0;
 }
 
+static int flush_run(spg_ctx *c, int64_t h1 = -1);
+
 int spg_set_reference(spg_ctx *c, const char *seq, int64_t len) {
     if (!c || !seq || len < 0) return fail("spg_set_reference: bad argument");
     HIPCHK(hipSetDevice(c->device));
+    // pending batches take their first-visit REF chars from the reference they were accumulated under
+    if (int rc = flush_run(c)) return rc;
     if (c->ref) {
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipFree(c->ref));
@@ -289,94 +372,86 @@ static int trace_sync(spg_ctx *c, const char *what) {
     return e == hipSuccess ? 0 : fail(std::string("spg trace: ") + what + ": " + hipGetErrorString(e));
 }
 
+#ifndef SPG_GMAX
+#define SPG_GMAX 64
+#endif
+
+static int64_t env_i64(const char *name, int64_t dflt) {
+    const char *e = getenv(name);
+    return e ? std::max<int64_t>(1, atoll(e)) : dflt;
+}
+
+// Device descriptor table and its pinned host mirror, grown geometrically.
 static int grow_history_table(spg_ctx *c) {
     const int64_t n = (int64_t)c->hist.size();
-    if (n <= c->d_hist_cap) return 0;
-    int64_t cap = std::max<int64_t>(64, c->d_hist_cap * 2);
-    while (cap < n) cap *= 2;
-    Hist *nh = nullptr;
-    HIPCHK(hipMalloc(&nh, sizeof(Hist) * cap));
-    if (c->d_hist) {
-        HIPCHK(hipMemcpyAsync(nh, c->d_hist, sizeof(Hist) * (n - 1), hipMemcpyDeviceToDevice, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        HIPCHK(hipFree(c->d_hist));
+    if (n > c->h_hist_cap) {
+        int64_t cap = std::max<int64_t>(64, c->h_hist_cap * 2);
+        while (cap < n) cap *= 2;
+        Hist *nh = nullptr;
+        HIPCHK(hipHostMalloc((void **)&nh, sizeof(Hist) * cap, hipHostMallocDefault));
+        if (c->h_hist) {
+            memcpy(nh, c->h_hist, sizeof(Hist) * c->h_hist_cap);
+            HIPCHK(hipStreamSynchronize(c->stream));      // in-flight uploads may still read the old mirror
+            HIPCHK(hipHostFree(c->h_hist));
+        }
+        c->h_hist = nh;
+        c->h_hist_cap = cap;
     }
-    c->d_hist = nh;
-    c->d_hist_cap = cap;
+    if (n > c->d_hist_cap) {
+        int64_t cap = std::max<int64_t>(64, c->d_hist_cap * 2);
+        while (cap < n) cap *= 2;
+        Hist *nd = nullptr;
+        HIPCHK(hipMalloc(&nd, sizeof(Hist) * cap));
+        if (c->d_hist) {
+            HIPCHK(hipMemcpyAsync(nd, c->d_hist, sizeof(Hist) * c->d_hist_cap, hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            HIPCHK(hipFree(c->d_hist));
+        }
+        c->d_hist = nd;
+        c->d_hist_cap = cap;
+    }
     return 0;
 }
 
-int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
-                      const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags) {
-    if (!c) return fail("spg_accumulate: null ctx");
-    if (!c->lut_set) return fail("spg_accumulate: spg_set_eps_lut not called");
-    if (!c->ref) return fail("spg_accumulate: spg_set_reference not called");
-    if (n_cols < 0 || pos_begin < 0 || pos_begin + n_cols > c->n_pos)
-        return fail("spg_accumulate: column range outside the context's positions");
-    if (pos_begin + n_cols > c->ref_len)
-        return fail("spg_accumulate: column range beyond the reference sequence (IndexError in the reference)");
-    if (n_cols == 0) return 0;
-    if (!offsets || (n_entries && (!base_code || !qual))) return fail("spg_accumulate: null buffer");
-    if (n_entries >= (1ull << 40)) return fail("spg_accumulate: batch too large");
-    HIPCHK(hipSetDevice(c->device));
-    const bool dev = flags & SPG_IN_DEVICE;
-    const bool borrow = dev && (flags & SPG_IN_BORROW);
-    HistBatch hb{pos_begin, n_cols, n_entries, nullptr, nullptr, nullptr, !borrow};
-    if (!dev) {
-        // validate the host CSR (cheap, O(n_cols)); device inputs are trusted
-        if (offsets[0] != 0 || offsets[n_cols] != n_entries) return fail("spg_accumulate: offsets[0] must be 0 and offsets[n_cols] == n_entries");
-        for (int64_t i = 0; i < n_cols; i++)
-            if (offsets[i + 1] < offsets[i]) return fail("spg_accumulate: offsets not monotone");
-    }
-    const size_t pad = (n_entries + 16 + 15) & ~size_t(15);
-    if (borrow) {
-        hb.off = const_cast<uint64_t *>(offsets);
-        hb.code = const_cast<uint8_t *>(base_code);
-        hb.qual = const_cast<uint8_t *>(qual);
-    } else {
-        HIPCHK(hipMalloc(&hb.off, sizeof(uint64_t) * (n_cols + 1)));
-        HIPCHK(hipMalloc(&hb.code, pad));
-        HIPCHK(hipMalloc(&hb.qual, pad));
-        const hipMemcpyKind k = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-        HIPCHK(hipMemcpyAsync(hb.off, offsets, sizeof(uint64_t) * (n_cols + 1), k, c->stream));
-        if (n_entries) {
-            HIPCHK(hipMemcpyAsync(hb.code, base_code, n_entries, k, c->stream));
-            HIPCHK(hipMemcpyAsync(hb.qual, qual, n_entries, k, c->stream));
-        }
-        HIPCHK(hipMemsetAsync(hb.code + n_entries, 0xFF, pad - n_entries, c->stream));
-        HIPCHK(hipMemsetAsync(hb.qual + n_entries, 0, pad - n_entries, c->stream));
-        // host buffers may be pageable and are the caller's again on return
-        if (!dev) HIPCHK(hipStreamSynchronize(c->stream));
-    }
-    if (!dev) {
-        for (uint64_t i = 0; i < n_entries; i++)
-            if (base_code[i] > SPG_CODE_SKIP) {
-                if (!borrow) { (void)hipStreamSynchronize(c->stream); (void)hipFree(hb.off); (void)hipFree(hb.code); (void)hipFree(hb.qual); }
-                return fail("spg_accumulate: base_code > 17 at entry " + std::to_string(i));
-            }
-    }
-    c->hist.push_back(hb);
-    int rc = grow_history_table(c);
-    if (rc) return rc;
-    c->batch_seq++;
-    // Work decomposition from the batch's mean depth (no per-column host pass, so device inputs
-    // need no host copy of the offsets).  Deep batches (mean >= 256 entries per column) stream every
-    // column through k_acc_seg<4> (16 entries/lane/chunk); shallower batches run a lane-per-column
-    // pass for columns below t_deep = 128 and k_acc_seg<1> (4 entries/lane/chunk) for the rest.
+// accumulate timing interval: ev[0] before the first accumulate launch since the last finalize
+static int acc_begin(spg_ctx *c) {
+    if (c->acc_open) return 0;
+    c->acc_timing = c->timing;
+    if (c->acc_timing >= 1) HIPCHK(hipEventRecord(c->ev[c->ring_w % spg_ctx::NRING][0], c->stream));
+    c->acc_open = true;
+    return 0;
+}
+static int acc_end(spg_ctx *c) {
+    if (c->acc_timing >= 1) HIPCHK(hipEventRecord(c->ev[c->ring_w % spg_ctx::NRING][1], c->stream));
+    return 0;
+}
+
+// kernels read batch data only after its copy (copy stream) has landed
+static int wait_copies(spg_ctx *c) {
+    if (!c->copy_pending) return 0;
+    HIPCHK(hipStreamWaitEvent(c->stream, c->copy_ev, 0));
+    c->copy_pending = false;
+    return 0;
+}
+
+static void fill_swar(const spg_ctx *c, int32_t &min_bq, int32_t &qlo, uint32_t &kpass, uint32_t &kok) {
+    const int mb = c->p.min_base_quality;
+    min_bq = mb;
+    qlo = std::max(mb, 4);
+    kpass = mb <= 0 ? 0x80808080u : (mb >= 128 ? 0u : (uint32_t)(0x80 - mb) * 0x01010101u);
+    kok = qlo >= 128 ? 0u : (uint32_t)(0x80 - qlo) * 0x01010101u;
+}
+
+// k_acc_seg over one batch (every column of a deep batch; the long columns of a shallow one)
+static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch) {
+    const HistBatch &hb = c->hist[(size_t)idx];
+    const int64_t n_cols = hb.n_cols;
+    const double avg = (double)hb.n_entries / (double)n_cols;
     // Each wave owns G consecutive columns.  A wave's setup (CSR offsets, then its first chunk) costs
     // two memory round trips, so a deep wave gets ~16 chunks where that still leaves one grid
     // generation of <= 4,096 waves (16 per CU) to fill the chip (1,000x: G = 8, 3,738 waves:
     // 40 -> 36 us); otherwise G targets 16,384 waves (10,000x: G = 2, measured best).
-    const double avg = (double)n_entries / (double)n_cols;
-    static const int64_t target_waves = [] {
-        const char *e = getenv("SPG_TARGET_WAVES");
-        return e ? std::max<int64_t>(1, atoll(e)) : (int64_t)16384;
-    }();
-    static const double deep_min = [] { const char *e = getenv("SPG_DEEP_MIN"); return e ? atof(e) : 256.0; }();
-    const bool deep_batch = avg >= deep_min;
-    #ifndef SPG_GMAX
-#define SPG_GMAX 64
-#endif
+    static const int64_t target_waves = env_i64("SPG_TARGET_WAVES", 16384);
     int64_t g = std::max<int64_t>(1, (n_cols + target_waves - 1) / target_waves);
     if (deep_batch && !getenv("SPG_TARGET_WAVES")) {
         const int64_t g_chunks = (int64_t)std::ceil(16384.0 / std::max(avg, 1.0));    // ~16 chunks per wave
@@ -385,39 +460,244 @@ int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint6
     }
     const uint32_t G = (uint32_t)std::min<int64_t>(SPG_GMAX, g);
     KParams P{};
-    P.pos_begin = pos_begin;
+    P.pos_begin = hb.pos_begin;
     P.n_cols = n_cols;
-    P.min_bq = c->p.min_base_quality;
-    P.qlo = std::max(c->p.min_base_quality, 4);
-    const int mb = c->p.min_base_quality;
-    P.kpass = mb <= 0 ? 0x80808080u : (mb >= 128 ? 0u : (uint32_t)(0x80 - mb) * 0x01010101u);
-    P.kok = P.qlo >= 128 ? 0u : (uint32_t)(0x80 - P.qlo) * 0x01010101u;
-    P.batch_seq = c->batch_seq;
+    fill_swar(c, P.min_bq, P.qlo, P.kpass, P.kok);
+    P.batch_seq = (uint32_t)(idx + 1);
     P.epoch = c->epoch;
-    P.hdesc = Hist{pos_begin, n_cols, hb.off, hb.code, hb.qual};
-    P.hslot = c->d_hist + (c->hist.size() - 1);
+    P.hdesc = Hist{hb.pos_begin, n_cols, hb.off, hb.code, hb.qual};
+    P.hslot = c->d_hist + idx;
     P.G = G;
     P.t_deep = deep_batch ? 1u : 128u;
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
-    P.n_entries = n_entries;
+    P.n_entries = hb.n_entries;
     P.dbg = trace_on() ? trace_dbg() : nullptr;
     P.prog = trace_prog((n_cols + G - 1) / G + 4);
-    hipEvent_t *ev = c->ev[c->ring_w % spg_ctx::NRING];
-    if (!c->acc_open) c->acc_timing = c->timing;
-    const int tm = c->acc_timing;
-    if (tm >= 1 && !c->acc_open) HIPCHK(hipEventRecord(ev[0], c->stream));
     HIPCHK(launch_accumulate(P, hb.off, hb.code, hb.qual, c->ref, c->tables, c->acc, c->stream));
-    if (trace_sync(c, "accumulate")) return -1;
-    if (tm >= 1) HIPCHK(hipEventRecord(ev[1], c->stream));
-    c->acc_open = true;
-    c->acc_any = true;
+    return trace_sync(c, "accumulate (k_acc_seg)");
+}
+
+// Fold the pending run [pend0, size) into the records: k_acc_multi (+ k_merge_parts when split), and
+// for a single batch the long columns through k_acc_seg<1>.
+static int flush_run(spg_ctx *c, int64_t h1) {
+    if (h1 < 0) h1 = (int64_t)c->hist.size();
+    const int64_t h0 = c->pend0;
+    if (h1 <= h0) return 0;
+    const int32_t K = (int32_t)(h1 - h0);
+    int64_t u0 = INT64_MAX, u1 = INT64_MIN;
+    for (int64_t i = h0; i < h1; i++) {
+        u0 = std::min(u0, c->hist[(size_t)i].pos_begin);
+        u1 = std::max(u1, c->hist[(size_t)i].pos_begin + c->hist[(size_t)i].n_cols);
+    }
+    const bool nt = 2 * c->pend_entries > (192ull << 20);
+    c->pend0 = h1;
+    c->pend_entries = 0;
+    if (int rc = wait_copies(c)) return rc;
+    if (int rc = acc_begin(c)) return rc;
+    // descriptors of the run (pinned mirror -> device table)
+    HIPCHK(hipMemcpyAsync(c->d_hist + h0, c->h_hist + h0, sizeof(Hist) * K, hipMemcpyHostToDevice, c->stream));
+    MParams P{};
+    P.u0 = u0;
+    P.u1 = u1;
+    P.h0 = (int32_t)h0;
+    P.K = K;
+    P.n_groups = (int32_t)((u1 - u0 + 63) / 64);
+    // split the run over batch ranges when its positions alone cannot fill the chip
+    static const int64_t target_items = env_i64("SPG_MULTI_ITEMS", 8192);
+    int64_t S = std::min<int64_t>(K, std::max<int64_t>(1, target_items / std::max<int32_t>(1, P.n_groups)));
+    const int64_t kper = (K + S - 1) / S;
+    S = (K + kper - 1) / kper;
+    P.S = (int32_t)S;
+    P.kper = (int32_t)kper;
+    fill_swar(c, P.min_bq, P.qlo, P.kpass, P.kok);
+    P.seq0 = (uint32_t)(h0 + 1);
+    P.epoch = c->epoch;
+    P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
+    P.t_deep = K == 1 ? 128u : 0u;
+    P.fresh = h0 == 0 ? 1u : 0u;
+    if (S > 1) {
+        const size_t need = sizeof(MState) * (size_t)S * (size_t)P.n_groups * 64;
+        if (need > c->part_bytes) {
+            if (c->part) { HIPCHK(hipStreamSynchronize(c->stream)); HIPCHK(hipFree(c->part)); }
+            c->part = nullptr;
+            c->part_bytes = 0;
+            HIPCHK(hipMalloc(&c->part, need));
+            c->part_bytes = need;
+        }
+        P.part = c->part;
+    }
+    static const int64_t max_blocks = env_i64("SPG_MULTI_BLOCKS", 6144);
+    HIPCHK(launch_multi(P, c->d_hist, c->ref, c->tables, c->acc, nt, max_blocks, c->stream));
+    if (int rc = trace_sync(c, "accumulate (k_acc_multi)")) return rc;
+    if (K == 1) {
+        // a single shallow batch: its long columns (>= 128 entries) go through the wave-wide kernel
+        if (int rc = launch_seg(c, h0, false)) return rc;
+    }
+    return acc_end(c);
+}
+
+static bool is_pinned(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
+    return a.type == hipMemoryTypeHost;
+}
+
+// One batch: validation, its history copy (arena) or borrowed device buffers, descriptors, bucket
+// index; a deep batch is accumulated right away, a shallow one joins the pending run.
+static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
+                     const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags,
+                     bool *pageable_copy) {
+    if (n_cols < 0 || pos_begin < 0 || pos_begin + n_cols > c->n_pos)
+        return fail("spg_accumulate: column range outside the context's positions");
+    if (pos_begin + n_cols > c->ref_len)
+        return fail("spg_accumulate: column range beyond the reference sequence (IndexError in the reference)");
+    if (n_cols == 0) return 0;
+    if (!offsets || (n_entries && (!base_code || !qual))) return fail("spg_accumulate: null buffer");
+    if (n_entries >= (1ull << 40)) return fail("spg_accumulate: batch too large");
+    const bool dev = flags & SPG_IN_DEVICE;
+    const bool borrow = dev && (flags & SPG_IN_BORROW);
+    if (!dev) {
+        // validate the host CSR (offsets O(n_cols), codes O(E)); device inputs are trusted
+        if (offsets[0] != 0 || offsets[n_cols] != n_entries)
+            return fail("spg_accumulate: offsets[0] must be 0 and offsets[n_cols] == n_entries");
+        for (int64_t i = 0; i < n_cols; i++)
+            if (offsets[i + 1] < offsets[i]) return fail("spg_accumulate: offsets not monotone");
+        uint8_t hi = 0;
+        for (uint64_t i = 0; i < n_entries; i++) hi = std::max(hi, base_code[i]);
+        if (hi > SPG_CODE_SKIP) {
+            for (uint64_t i = 0; i < n_entries; i++)
+                if (base_code[i] > SPG_CODE_SKIP) return fail("spg_accumulate: base_code > 17 at entry " + std::to_string(i));
+        }
+    }
+    HistBatch hb{pos_begin, n_cols, n_entries, nullptr, nullptr, nullptr, !borrow};
+    if (borrow) {
+        hb.off = const_cast<uint64_t *>(offsets);
+        hb.code = const_cast<uint8_t *>(base_code);
+        hb.qual = const_cast<uint8_t *>(qual);
+    } else {
+        const size_t pad = (n_entries + 16 + 15) & ~size_t(15);
+        uint8_t *m = nullptr;
+        HIPCHK(c->arena.alloc(sizeof(uint64_t) * (n_cols + 1) + 2 * pad, &m));
+        hb.code = m;
+        hb.qual = m + pad;
+        hb.off = reinterpret_cast<uint64_t *>(m + 2 * pad);
+        const hipMemcpyKind k = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+        hipStream_t cs = c->copy_stream;
+        HIPCHK(hipMemcpyAsync(hb.off, offsets, sizeof(uint64_t) * (n_cols + 1), k, cs));
+        if (n_entries) {
+            HIPCHK(hipMemcpyAsync(hb.code, base_code, n_entries, k, cs));
+            HIPCHK(hipMemcpyAsync(hb.qual, qual, n_entries, k, cs));
+        }
+        HIPCHK(hipMemsetAsync(hb.code + n_entries, 0xFF, pad - n_entries, cs));
+        HIPCHK(hipMemsetAsync(hb.qual + n_entries, 0, pad - n_entries, cs));
+        HIPCHK(hipEventRecord(c->copy_ev, cs));
+        c->copy_pending = true;
+        // pageable host buffers are the caller's again on return; pinned ones after spg_wait_input
+        if (!dev && !(is_pinned(offsets) && (!n_entries || (is_pinned(base_code) && is_pinned(qual)))))
+            *pageable_copy = true;
+    }
+    c->hist.push_back(hb);
+    const int64_t idx = (int64_t)c->hist.size() - 1;
+    if (int rc = grow_history_table(c)) return rc;
+    c->h_hist[idx] = Hist{pos_begin, n_cols, hb.off, hb.code, hb.qual};
+    for (int64_t b = pos_begin >> RIDX_SHIFT; b <= (pos_begin + n_cols - 1) >> RIDX_SHIFT; b++) {
+        c->buckets[(size_t)b].push_back((int32_t)idx);
+        c->ridx_items++;
+    }
+    c->ridx_dirty = true;
+    c->batch_seq++;
     c->finalized = false;
+    static const double deep_min = [] { const char *e = getenv("SPG_DEEP_MIN"); return e ? atof(e) : 256.0; }();
+    const double avg = (double)n_entries / (double)n_cols;
+    if (avg >= deep_min) {
+        // a deep batch: the run before it first (accumulate order), then k_acc_seg<4> on its own
+        if (int rc = flush_run(c, idx)) return rc;
+        c->pend0 = idx + 1;
+        if (int rc = wait_copies(c)) return rc;
+        if (int rc = acc_begin(c)) return rc;
+        if (int rc = launch_seg(c, idx, true)) return rc;
+        return acc_end(c);
+    }
+    c->pend_entries += n_entries;
+    static const int64_t run_max = env_i64("SPG_RUN_MAX", 4096);
+    if ((int64_t)c->hist.size() - c->pend0 >= run_max) return flush_run(c);
     return 0;
+}
+
+static int accumulate_many(spg_ctx *c, const spg_batch *b, int64_t n, uint32_t flags) {
+    if (!c) return fail("spg_accumulate: null ctx");
+    if (!c->lut_set) return fail("spg_accumulate: spg_set_eps_lut not called");
+    if (!c->ref) return fail("spg_accumulate: spg_set_reference not called");
+    if (n < 0 || (n > 0 && !b)) return fail("spg_accumulate_batches: bad batch list");
+    HIPCHK(hipSetDevice(c->device));
+    bool pageable = false;
+    int rc = 0;
+    for (int64_t i = 0; i < n && rc == 0; i++)
+        rc = add_batch(c, b[i].pos_begin, b[i].n_cols, b[i].offsets, b[i].base_code, b[i].qual, b[i].n_entries,
+                       flags, &pageable);
+    if (pageable) HIPCHK(hipStreamSynchronize(c->copy_stream));
+    return rc;
+}
+
+int spg_accumulate_ex(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
+                      const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags) {
+    const spg_batch b{pos_begin, n_cols, offsets, base_code, qual, n_entries};
+    return accumulate_many(c, &b, 1, flags);
 }
 
 int spg_accumulate(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets, const uint8_t *base_code,
                    const uint8_t *qual, uint64_t n_entries) {
     return spg_accumulate_ex(c, pos_begin, n_cols, offsets, base_code, qual, n_entries, 0);
+}
+
+int spg_accumulate_batches(spg_ctx *c, const spg_batch *batches, int64_t n, uint32_t flags) {
+    return accumulate_many(c, batches, n, flags);
+}
+
+int spg_wait_input(spg_ctx *c) {
+    if (!c) return fail("spg_wait_input: null ctx");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->copy_stream));
+    return 0;
+}
+
+// Replay index upload: CSR of the bucket lists (only when more than a few batches are kept: with
+// few, the replay scans them all).
+static int upload_ridx(spg_ctx *c, RIndex &R) {
+    R = RIndex{nullptr, nullptr, 0};
+    if ((int64_t)c->hist.size() <= 8) return 0;
+    if (c->ridx_dirty || !c->ridx_valid) {
+        const int64_t nb = (int64_t)c->buckets.size();
+        const size_t words = (size_t)(nb + 1 + c->ridx_items);
+        if (c->h_ridx) HIPCHK(hipEventSynchronize(c->ridx_ev));   // the previous upload has read it
+        if (words > c->ridx_cap) {
+            size_t cap = std::max<size_t>(words, c->ridx_cap * 2);
+            if (c->h_ridx) HIPCHK(hipHostFree(c->h_ridx));
+            if (c->d_ridx) { HIPCHK(hipStreamSynchronize(c->stream)); HIPCHK(hipFree(c->d_ridx)); }
+            c->h_ridx = nullptr;
+            c->d_ridx = nullptr;
+            c->ridx_cap = 0;
+            HIPCHK(hipHostMalloc((void **)&c->h_ridx, sizeof(uint32_t) * cap, hipHostMallocDefault));
+            HIPCHK(hipMalloc(&c->d_ridx, sizeof(uint32_t) * cap));
+            c->ridx_cap = cap;
+        }
+        uint32_t *off = c->h_ridx;
+        int32_t *items = reinterpret_cast<int32_t *>(c->h_ridx + nb + 1);
+        uint32_t at = 0;
+        for (int64_t b = 0; b < nb; b++) {
+            off[b] = at;
+            for (int32_t i : c->buckets[(size_t)b]) items[at++] = i;
+        }
+        off[nb] = at;
+        HIPCHK(hipMemcpyAsync(c->d_ridx, c->h_ridx, sizeof(uint32_t) * words, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipEventRecord(c->ridx_ev, c->stream));
+        c->ridx_dirty = false;
+        c->ridx_valid = true;
+    }
+    R.off = c->d_ridx;
+    R.items = reinterpret_cast<const int32_t *>(c->d_ridx + c->buckets.size() + 1);
+    R.n_buckets = (int64_t)c->buckets.size();
+    return 0;
 }
 
 static Out make_out(spg_ctx *c) {
@@ -455,6 +735,7 @@ int spg_finalize(spg_ctx *c) {
 static int finalize_impl(spg_ctx *c, bool table) {
     if (!c->lut_set) return fail("spg_finalize: spg_set_eps_lut not called");
     HIPCHK(hipSetDevice(c->device));
+    if (int rc = flush_run(c)) return rc;     // the pending run of shallow batches
     c->cslot ^= 1u;            // this call counts in slot cslot (zeroed by the previous call / creation)
     hipEvent_t *ev = c->ev[c->ring_w % spg_ctx::NRING];
     if (!c->acc_open) {        // no accumulate since the last finalize: empty accumulate interval
@@ -468,6 +749,7 @@ static int finalize_impl(spg_ctx *c, bool table) {
     if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
     FParams F = make_fparams(c);
     F.table = table ? 1u : 0u;
+    if (int rc = upload_ridx(c, F.ridx)) return rc;
     HIPCHK(launch_finalize(F, c->acc, c->tables, make_out(c), c->d_hist, c->stream));
     if (trace_sync(c, "finalize")) return -1;
     c->table_valid = table;
@@ -491,6 +773,7 @@ int spg_stream(spg_ctx *c, void **stream) {
 int spg_sync(spg_ctx *c) {
     if (!c) return fail("spg_sync: null ctx");
     HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->copy_stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -669,6 +952,7 @@ int spg_history_copy(spg_ctx *c, int64_t i, uint64_t *offsets, uint8_t *base_cod
     if (!c) return fail("spg_history_copy: null ctx");
     if (i < 0 || i >= (int64_t)c->hist.size()) return fail("spg_history_copy: batch index out of range");
     HIPCHK(hipSetDevice(c->device));
+    if (int rc = wait_copies(c)) return rc;
     const HistBatch &h = c->hist[(size_t)i];
     if (offsets) HIPCHK(hipMemcpyAsync(offsets, h.off, sizeof(uint64_t) * (h.n_cols + 1), hipMemcpyDeviceToHost, c->stream));
     if (base_code && h.n_entries) HIPCHK(hipMemcpyAsync(base_code, h.code, h.n_entries, hipMemcpyDeviceToHost, c->stream));

@@ -75,8 +75,48 @@ struct KParams {
     uint4 *prog;           // SPG_TRACE: per-wave progress records in host-mapped memory (else null)
 };
 
+// Per-position state of one lane of k_acc_multi over a run of batches (lane-private, in LDS), and
+// the partial record one batch split hands to k_merge_parts (same 176-B layout in HBM).
+struct __align__(16) MState {
+    uint32_t depth, n_del, n_skip, n_other;
+    uint32_t cnt[NSLOT], sq[NSLOT];
+    uint32_t first[NSLOT];   // stream index (raw entries of this position in the split) of the slot's
+                             // first entry; INF32 if absent
+    uint32_t fb;             // launch-relative index of the first batch holding raw entries (INF32: none)
+    uint8_t qf[NSLOT];       // q lower bound per slot (255 = none)
+    uint8_t skip;            // slots whose sum(ln(1-eps)) / sum(eps) were skipped (calls-only REF)
+    uint8_t flags;           // image bits after the record is assembled: 1 write, 2 write the sums half
+    uint8_t pad0;
+    uint32_t pad1[2];
+    double sl[NSLOT], se[NSLOT];
+};
+static_assert(sizeof(MState) == 176, "MState layout");
+
+struct MParams {             // one k_acc_multi launch: history batches [h0, h0 + K) over positions [u0, u1)
+    int64_t u0, u1;
+    int32_t h0, K;
+    int32_t S, kper;         // batch splits (partial records merged by k_merge_parts when S > 1)
+    int32_t n_groups;        // 64-position groups
+    int32_t min_bq, qlo;
+    uint32_t kpass, kok;
+    uint32_t seq0;           // batch_seq of batch h0 (1-based within the epoch)
+    uint32_t epoch;
+    uint32_t calls_only;
+    uint32_t t_deep;         // K == 1: columns with >= t_deep entries are left to k_acc_seg (0 = none)
+    uint32_t fresh;          // seq0 == 1: no record of this epoch exists yet
+    MState *part;            // S > 1: partial records [S][n_groups * 64]
+};
+
+// Replay index: history batches overlapping each 2^RIDX_SHIFT-position bucket, in accumulate order.
+constexpr int RIDX_SHIFT = 12;
+struct RIndex {
+    const uint32_t *off;     // [n_buckets + 1]
+    const int32_t *items;    // history indices
+    int64_t n_buckets;       // 0: no index, scan every batch
+};
+
 struct Counters {           // per finalize; two slots, the kernel zeroes the other one
-    uint32_t n_cand, n_band, n_detail, err;
+    uint32_t n_cand, n_band, n_detail, err;   // n_band: positions queued for the exact replay
 };
 
 struct FParams {
@@ -88,6 +128,7 @@ struct FParams {
     uint32_t epoch, cslot;
     uint32_t table;        // write the per-position SoA table (else: calls only, early exits)
     uint32_t pad_;
+    RIndex ridx;
 };
 
 struct Out {                // SoA result table
@@ -95,7 +136,7 @@ struct Out {                // SoA result table
     double *gl;
     uint8_t *flags;
     spg_candidate *cand;
-    int64_t *band;
+    int64_t *band;          // positions queued for the exact replay (k_replay); n_band of them
     spg_detail *detail;
     Counters *ctr;          // Counters[2]
 };

@@ -1,43 +1,29 @@
 // spg_kernels.hip — CDNA4 (gfx950) kernels of the pileup + genotype-likelihood engine.
 //
 //   k_acc_seg<W,FRESH>  process_pileup_column / process_svn (live_variant_caller.py:74-103) + pysam's
-//                  base-quality filter for one CSR batch: a wave64 owns G consecutive columns and
+//                  base-quality filter for one deep CSR batch: a wave64 owns G consecutive columns and
 //                  streams them as one sequence of 64 x 4W-entry chunks (buffer loads two chunks ahead,
 //                  column descriptors in LDS behind scalar cursors).  SWAR byte tests classify 4
 //                  entries per dword; the column's major (and, when frequent, second) allele takes the
 //                  fast path (v_bcnt counts, v_dot4_u32_u8 quality sums, LDS {ln(1-eps), eps} table);
 //                  the rare entries (other alleles, D/N, q < 4, q >= 128, IUPAC) are queued as lane
 //                  slices and decoded exactly into a per-wave LDS record at column end.
-//   k_acc_shallow  short columns (< t_deep entries), one lane per column, SWAR against the REF allele.
+//   k_acc_multi    shallow batches, one lane per position, a run of K batches (BAMs) per launch: the
+//                  record of a position is read and written once per run (k_merge_parts folds split
+//                  runs).
 //   k_finalize     prepare_variants (:120-185) + genotype_likelihood / to_phred_scale
 //                  (utils.py:12-24): per-position GL in fp64 with the reference's underflow decisions,
 //                  candidate filters, GL/PL/SCORE/QUAL.  A position whose result depends on the order
 //                  of fp64 roundings in the subnormal range (or that holds IUPAC alleles, or whose calls
-//                  need terms calls-only mode did not accumulate) is recomputed exactly by walking the
-//                  batch history (np.prod left folds in BAM order).
+//                  need terms calls-only mode did not accumulate) is recomputed exactly by its wave,
+//                  walking the batch history (np.prod left folds in BAM order).
+#include <algorithm>
 #include <type_traits>
 
 #include "spg_device.h"
 #include <stdlib.h>
 
 namespace spg {
-
-// ------------------------------------------------------------------------------------------
-// per-lane column state (shallow columns)
-// ------------------------------------------------------------------------------------------
-struct ColState {
-    uint32_t depth, n_del, n_skip, n_other;
-    uint32_t cnt[NSLOT], sq[NSLOT], qf[NSLOT], first[NSLOT];
-    double sl[NSLOT], se[NSLOT];
-};
-
-__device__ __forceinline__ void cs_init(ColState &s) {
-    s.depth = s.n_del = s.n_skip = s.n_other = 0;
-#pragma unroll
-    for (int k = 0; k < NSLOT; k++) {
-        s.cnt[k] = 0; s.sq[k] = 0; s.qf[k] = 255u; s.first[k] = INF32; s.sl[k] = 0.0; s.se[k] = 0.0;
-    }
-}
 
 // ------------------------------------------------------------------------------------------
 // wave helpers
@@ -80,8 +66,10 @@ __device__ __forceinline__ double dsum_f64(double v) {
     return (rl_f64(v, 0) + rl_f64(v, 16)) + (rl_f64(v, 32) + rl_f64(v, 48));
 }
 
-// New alleles join the dict in order of first appearance in this batch (:100-101).
-__device__ __forceinline__ uint32_t merge_order(uint32_t order, uint32_t newmask, const uint32_t *first) {
+// New alleles join the dict in order of first appearance in this batch (:100-101).  `first` holds each
+// slot's first-entry key in the accumulated stream (u32 within one run, u64 across batch splits).
+template <typename KeyT>
+__device__ __forceinline__ uint32_t merge_order(uint32_t order, uint32_t newmask, const KeyT *first) {
     uint32_t n = order & 7u;
 #pragma unroll
     for (int k = 0; k < NSLOT; k++) {
@@ -106,17 +94,27 @@ __device__ __forceinline__ uint32_t order_mask(uint32_t order) {
     return have;
 }
 
-// Merge one column's batch statistics into its Acc record (single lane; shallow path).
-__device__ void merge_acc(Acc *__restrict__ A, const ColState &c, uint32_t batch_seq, uint32_t epoch, uint8_t refc,
-                          uint32_t skip = 0u, bool fresh = false) {
-    Acc a;
-    if (!fresh) a = *A;                             // FRESH (first batch of the epoch): nothing to read
-    if (fresh || a.epoch != epoch) {                // record of an older sample: start afresh
-        a = Acc{};
-        a.epoch = epoch;
+__device__ __forceinline__ uint32_t sat_add31(uint32_t a, uint32_t b) {   // sum q, saturating at 2^31
+    const uint64_t s = (uint64_t)a + b;
+    return s > 0x80000000ull ? 0x80000000u : (uint32_t)s;
+}
+
+__device__ __forceinline__ void ms_init(MState &S) {
+    S.depth = S.n_del = S.n_skip = S.n_other = 0;
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) {
+        S.cnt[k] = 0; S.sq[k] = 0; S.first[k] = INF32; S.qf[k] = 255; S.sl[k] = 0.0; S.se[k] = 0.0;
     }
+    S.fb = INF32; S.skip = 0; S.flags = 0;
+}
+
+// Merge one run of batches (state c, first-entry keys per slot) into the position's record `a` (already
+// reset when it belongs to an older epoch): process_pileup_column's first visit (:77-85), totalDepth
+// (:87) and process_svn's dict appends (:100-101) for a whole run at once.
+template <typename KeyT>
+__device__ __forceinline__ void merge_state(Acc &a, const MState &c, const KeyT *key, uint32_t first_seq, uint8_t refc) {
     if (a.first_batch == 0) {                       // first visit (:77-85)
-        a.first_batch = batch_seq;
+        a.first_batch = first_seq;
         a.misc = refc;
     }
     a.depth += c.depth;                             // :87
@@ -124,43 +122,32 @@ __device__ void merge_acc(Acc *__restrict__ A, const ColState &c, uint32_t batch
     a.n_skip += c.n_skip;
     a.n_other += c.n_other;
     if (c.n_other) a.misc |= MISC_EXOTIC;
-    a.misc |= skip << MISC_SKIP_SHIFT;
+    a.misc |= (uint32_t)c.skip << MISC_SKIP_SHIFT;
     const uint32_t have = order_mask(a.order);
     uint32_t newmask = 0;
 #pragma unroll
     for (int k = 0; k < NSLOT; k++) {
         if (c.cnt[k]) {
-            if (a.cnt[k] == 0) a.qf[k] = (uint8_t)c.qf[k];
-            else a.qf[k] = (uint8_t)min((uint32_t)a.qf[k], c.qf[k]);
-            const bool had = a.cnt[k] != 0;      // absent slots' sums may hold stale bytes
+            const bool had = a.cnt[k] != 0;         // absent slots' sums may hold stale bytes
+            a.qf[k] = had ? (uint8_t)min((uint32_t)a.qf[k], (uint32_t)c.qf[k]) : c.qf[k];
             a.cnt[k] += c.cnt[k];
-            const uint64_t s = (uint64_t)a.sq[k] + c.sq[k];
-            a.sq[k] = s > 0x80000000ull ? 0x80000000u : (uint32_t)s;
+            a.sq[k] = sat_add31(a.sq[k], c.sq[k]);
             a.sl[k] = had ? a.sl[k] + c.sl[k] : c.sl[k];
             a.se[k] = had ? a.se[k] + c.se[k] : c.se[k];
             if (!((have >> k) & 1u)) newmask |= 1u << k;
         }
     }
-    a.order = merge_order(a.order, newmask, c.first);
-    if (!fresh) {
-        *A = a;
-        return;
-    }
-    // FRESH record: sl/se (bytes 80..159) are read only for slots that hold sums; a column whose
-    // present slots all skipped them (calls-only REF) writes 80 bytes instead of 160
-    bool sums = false;
-#pragma unroll
-    for (int k = 0; k < NSLOT; k++) sums |= c.cnt[k] != 0 && !((skip >> k) & 1u);
-    const uint4 *src = reinterpret_cast<const uint4 *>(&a);
-    uint4 *dst = reinterpret_cast<uint4 *>(A);
-#pragma unroll
-    for (int i = 0; i < 5; i++) dst[i] = src[i];
-    if (sums) {
-#pragma unroll
-        for (int i = 5; i < 10; i++) dst[i] = src[i];
-    }
+    a.order = merge_order(a.order, newmask, key);
 }
 
+// A FRESH record needs its sl/se half (bytes 80..159) only when some present slot holds sums
+__device__ __forceinline__ bool record_has_sums(const Acc &a) {
+    const uint32_t skip = (a.misc >> MISC_SKIP_SHIFT) & 0x1Fu;
+    bool sums = false;
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) sums |= a.cnt[k] != 0 && !((skip >> k) & 1u);
+    return sums;
+}
 // ------------------------------------------------------------------------------------------
 // SWAR classification of 4 entries (one dword of base_code, one of qual)
 //   fast  = valid & q >= max(min_bq,4) & q < 128 & code == M      (the column's major allele)
@@ -762,92 +749,271 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     prog(6, 0, 0, 0);
 }
 
-// Short columns (< t_deep raw entries): one lane per column.  The lane walks its column in
-// aligned dwords (4 entries per load, columns of neighbouring lanes share cache lines), classifies
-// them with the SWAR test against the column's REF allele (the major allele of a shallow column in
-// practice), sums the fast entries in registers (LDS LUT) and sends the rest through the per-slot
-// register state one by one.
+// ------------------------------------------------------------------------------------------
+// k_acc_multi: shallow batches.  One lane per reference position, one wave per 64 consecutive
+// positions, and a RUN of K batches per launch: for every batch in accumulate order the wave reads
+// the 64 columns' CSR offsets (one coalesced 520-B load) and then each lane streams its column's
+// entries in 16-B blocks (the wave's blocks of one batch cover one contiguous ~64-column range, so
+// consecutive block loads of neighbouring lanes share cache lines).  Per lane: SWAR counts / sum(q)
+// against the REF allele, a second SWAR allele promoted once a non-REF base is frequent (an SNV),
+// and every other entry decoded exactly into the lane's LDS state.  The Acc record is read and
+// written ONCE per run instead of once per batch: the reference's per-BAM appends
+// (process_pileup_column / process_svn, live_variant_caller.py:74-103, repeated by process_bam for
+// every BAM, :54-72) become one pass.  When the run's positions are too few to fill the chip (a
+// 29.9-kb genome), the run is split into S batch ranges whose partial states k_merge_parts folds in
+// order.
+// ------------------------------------------------------------------------------------------
+constexpr int MW = 4;          // waves per k_acc_multi workgroup
+constexpr int MBLK = 4;        // 16-B blocks per lane per load round (64 entries)
+
 __device__ __forceinline__ uint32_t code_of_ref(uint8_t c) {
     c = (uint8_t)(c & 0xDFu);                     // upper case
     return c == 'A' ? 1u : c == 'C' ? 2u : c == 'G' ? 4u : c == 'T' ? 8u : c == 'N' ? 15u : 1u;
 }
 
-__device__ __forceinline__ void entry_update_lut(ColState &s, uint32_t code, uint32_t q, uint32_t idx,
-                                                 const double2 *__restrict__ lut) {
-    s.depth++;
-    if (code == SPG_CODE_DEL) { s.n_del++; return; }
-    if (code == SPG_CODE_SKIP) { s.n_skip++; return; }
+// One entry outside the SWAR paths (lane-private LDS state; q >= 128 rows from global: rare)
+__device__ __forceinline__ void ms_rare(MState &S, uint32_t code, uint32_t q, uint32_t idx,
+                                        const double2 *__restrict__ lut, const Tables *__restrict__ T) {
+    S.depth++;
+    if (code == SPG_CODE_DEL) { S.n_del++; return; }
+    if (code == SPG_CODE_SKIP) { S.n_skip++; return; }
     const int sl = slot_of(code);
-    if (sl < 0) { s.n_other++; return; }
-    const double2 t = lut[q < 128u ? q : q + 128u];
-    s.cnt[sl] += 1u; s.sq[sl] += q; s.qf[sl] = min(s.qf[sl], q); s.first[sl] = min(s.first[sl], idx);
-    s.sl[sl] += t.x; s.se[sl] += q == 0 ? 1.0 : t.y;        // state in LDS: indexed directly
+    if (sl < 0) { S.n_other++; return; }
+    S.cnt[sl]++;
+    S.sq[sl] = sat_add31(S.sq[sl], q);
+    S.qf[sl] = (uint8_t)min((uint32_t)S.qf[sl], q);
+    S.first[sl] = min(S.first[sl], idx);
+    const double2 t = q < 128u ? lut[q] : make_double2(T->fast[q][0], T->fast[q][1]);
+    S.sl[sl] += t.x;
+    S.se[sl] += q == 0 ? 1.0 : t.y;                // eps(Q0) = 1
 }
 
-__global__ __launch_bounds__(128) void k_acc_shallow(KParams P, const uint64_t *__restrict__ off,
-                                                     const uint8_t *__restrict__ code,
-                                                     const uint8_t *__restrict__ qual,
-                                                     const uint8_t *__restrict__ ref, const Tables *__restrict__ T,
-                                                     Acc *__restrict__ acc) {
-    __shared__ double2 lut[384];                  // same layout as k_acc_seg's
-    __shared__ ColState lane_state[128];          // per-lane state of the non-fast alleles (indexed by slot)
-    write_hist(P);
-    for (uint32_t q = threadIdx.x; q < 256u; q += blockDim.x) {
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
+    const u32x4 *v = reinterpret_cast<const u32x4 *>(p);
+    if constexpr (NT) return __builtin_nontemporal_load(v);
+    else return *v;
+}
+
+// sum over a fast allele's entries of a dword: {ln(1-eps), eps} rows of the LDS LUT (row q for the
+// selected bytes, a zero row for every other byte)
+__device__ __forceinline__ void lut_sums(uint32_t qw, uint32_t sel80, const double2 *__restrict__ lut, double &sl,
+                                         double &se) {
+    const uint32_t idx = (qw & 0x7F7F7F7Fu) ^ sel80 ^ 0x80808080u;
+    const double2 t0 = lut[idx & 0xFFu], t1 = lut[(idx >> 8) & 0xFFu];
+    const double2 t2 = lut[(idx >> 16) & 0xFFu], t3 = lut[idx >> 24];
+    sl += (t0.x + t1.x) + (t2.x + t3.x);
+    se += (t0.y + t1.y) + (t2.y + t3.y);
+}
+
+template <bool NT>
+__global__ __launch_bounds__(64 * MW) void k_acc_multi(MParams P, const Hist *__restrict__ H,
+                                                       const uint8_t *__restrict__ ref,
+                                                       const Tables *__restrict__ T, Acc *__restrict__ acc) {
+    // rows 0..127 {ln(1-eps), eps} for q < 128; rows 128..255 zero (the index of non-selected bytes)
+    __shared__ double2 lut[256];
+    __shared__ MState st[MW][64];
+    for (uint32_t q = threadIdx.x; q < 256u; q += 64u * MW)
         lut[q] = q < 128u ? make_double2(T->fast[q][0], T->fast[q][1]) : make_double2(0.0, 0.0);
-        if (q >= 128u) lut[q + 128u] = make_double2(T->fast[q][0], T->fast[q][1]);
-    }
     __syncthreads();
-    const int64_t col = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (col >= P.n_cols) return;
-    const uint64_t ob = off[col], oe = off[col + 1];
-    const uint64_t len = oe - ob;
-    if (len == 0 || len >= P.t_deep) return;
-    const int64_t pos = P.pos_begin + col;
-    const uint8_t refc = ref[pos];
-    const uint32_t M = code_of_ref(refc);
-    const uint32_t mrep = M * 0x01010101u;
-    const bool sums = !P.calls_only || nibble_char(M) != refc;   // calls-only: no sums for the REF allele
-    ColState &st = lane_state[threadIdx.x];
-    cs_init(st);
-    uint32_t fcnt = 0, fsq = 0, ffirst = INF32;
-    double fsl = 0.0, fse = 0.0;
-    const uint64_t a0 = ob & ~(uint64_t)3, a1 = (oe + 3) & ~(uint64_t)3;
-    const uint32_t *cw4 = reinterpret_cast<const uint32_t *>(code + a0);
-    const uint32_t *qw4 = reinterpret_cast<const uint32_t *>(qual + a0);
-    const int32_t lead = (int32_t)(ob - a0);
-    const uint32_t nd = (uint32_t)((a1 - a0) >> 2);
-    for (uint32_t d = 0; d < nd; d++) {
-        const uint32_t cw = cw4[d], qw = qw4[d];
-        const int32_t x = (int32_t)(4 * d) - lead;           // column index of this dword's byte 0
-        const uint32_t v = valid80(x, 0, (int32_t)len);
-        uint32_t f80, r80;
-        swar4(cw, qw, v, mrep, P.kpass, P.kok, f80, r80);
-        fcnt += __popc(f80);
-        fsq = __builtin_amdgcn_udot4(qw, f80 >> 7, fsq, false);
-        if (sums) {
-            const uint32_t idx = (qw & 0x7F7F7F7Fu) ^ f80 ^ 0x80808080u;
-            const double2 t0 = lut[idx & 0xFFu], t1 = lut[(idx >> 8) & 0xFFu];
-            const double2 t2 = lut[(idx >> 16) & 0xFFu], t3 = lut[idx >> 24];
-            fsl += (t0.x + t1.x) + (t2.x + t3.x);
-            fse += (t0.y + t1.y) + (t2.y + t3.y);
-        }
-        if (f80 && ffirst == INF32) ffirst = (uint32_t)(x + (int32_t)(__builtin_ctz(f80) >> 3));
-        while (r80) {
-            const int sh = __builtin_ctz(r80) - 7;
-            r80 &= r80 - 1;
-            const uint32_t c = (cw >> sh) & 0xFFu, q = (qw >> sh) & 0xFFu;
-            if ((int)q >= P.min_bq) entry_update_lut(st, c, q, (uint32_t)(x + (sh >> 3)), lut);
-        }
-    }
-    uint32_t skip = 0;
-    if (fcnt) {
+    const int lane = threadIdx.x & 63;
+    MState *ST = st[threadIdx.x >> 6];
+    MState &S = ST[lane];
+    const int64_t n_items = (int64_t)P.n_groups * P.S;
+    // grid-stride over (position group, batch split) items: the LUT is loaded once per workgroup
+    for (int64_t item = (int64_t)blockIdx.x * MW + (threadIdx.x >> 6); item < n_items;
+         item += (int64_t)gridDim.x * MW) {
+        const int32_t g = (int32_t)(item % P.n_groups), s = (int32_t)(item / P.n_groups);
+        const int64_t p0 = P.u0 + (int64_t)g * 64;
+        const int64_t p = p0 + lane;
+        const bool inr = p < P.u1;
+        ms_init(S);
+        const uint8_t refc = inr ? ref[p] : (uint8_t)'A';
+        const uint32_t M = code_of_ref(refc), mrep = M * 0x01010101u;
         const int Ms = slot_of(M);
-        st.depth += fcnt;
-        st.cnt[Ms] += fcnt; st.sq[Ms] += fsq; st.qf[Ms] = min(st.qf[Ms], (uint32_t)P.qlo);
-        st.first[Ms] = min(st.first[Ms], ffirst); st.sl[Ms] += fsl; st.se[Ms] += fse;
-        if (!sums) skip = 1u << Ms;
+        // calls-only: no likelihood sums for a REF-char major (never a candidate)
+        const bool msum = !P.calls_only || nibble_char(M) != refc;
+        const bool any_msum = __ballot(msum && inr) != 0;
+        int s2 = -1;                                   // slot of the promoted second allele
+        // no second allele: code 0x7F matches nothing (the SWAR compare needs code ^ M < 0x80)
+        uint32_t mrep2 = 0x7F7F7F7Fu;
+        uint32_t fcnt = 0, fsq = 0, ffirst = INF32;
+        double fsl = 0.0, fse = 0.0;
+        uint32_t gcnt = 0, gsq = 0, gfirst = INF32;
+        double gsl = 0.0, gse = 0.0;
+        bool deep = false;
+        uint32_t sidx = 0;                             // raw entries of this position in earlier batches
+        const int32_t k0 = s * P.kper, k1 = min(P.K, k0 + P.kper);
+        for (int32_t k = k0; k < k1; k++) {
+            const Hist h = H[P.h0 + k];
+            const int64_t col = p - h.pos_begin;
+            const bool cov = inr && col >= 0 && col < h.n_cols;
+            if (__ballot(cov) == 0) continue;
+            uint64_t ob = 0, oe = 0;
+            if (cov) { ob = h.off[col]; oe = h.off[col + 1]; }
+            uint32_t len = (uint32_t)(oe - ob);
+            if (P.t_deep && len >= P.t_deep) { deep = true; len = 0; }   // k_acc_seg takes this column
+            if (len && S.fb == INF32) S.fb = (uint32_t)k;
+            const uint64_t a0 = ob & ~(uint64_t)15;
+            const int32_t lead = (int32_t)(ob - a0);
+            const uint32_t nblk = len ? (uint32_t)(((uint64_t)lead + len + 15) >> 4) : 0u;
+            uint32_t mx = nblk;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+            mx = __builtin_amdgcn_readfirstlane(mx);
+            const uint8_t *cb = h.code + a0, *qb = h.qual + a0;
+            const bool dual = __ballot(s2 >= 0) != 0;
+            for (uint32_t j = 0; j < mx; j += MBLK) {
+                u32x4 cw[MBLK], qw[MBLK];
+#pragma unroll
+                for (int u = 0; u < MBLK; u++) {
+                    if (j + u < nblk) {
+                        cw[u] = ld16<NT>(cb + 16u * (j + u));
+                        qw[u] = ld16<NT>(qb + 16u * (j + u));
+                    } else {
+                        cw[u] = u32x4{0u, 0u, 0u, 0u};
+                        qw[u] = u32x4{0u, 0u, 0u, 0u};
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < MBLK; u++) {
+                    if (j + u >= mx) break;
+                    const int32_t x0 = (int32_t)(16u * (j + u)) - lead;   // segment index of the block's byte 0
+                    uint32_t vm[4];
+                    valid_masks<4>(x0, 0, (int32_t)len, vm);
+#pragma unroll
+                    for (int d = 0; d < 4; d++) {
+                        const uint32_t c_ = dw<4>(cw[u], d), q_ = dw<4>(qw[u], d);
+                        uint32_t f80, r80, g80 = 0;
+                        swar4(c_, q_, vm[d], mrep, P.kpass, P.kok, f80, r80);
+                        if (dual) {
+                            uint32_t r2;
+                            swar4(c_, q_, vm[d], mrep2, P.kpass, P.kok, g80, r2);
+                            r80 &= ~g80;
+                            gcnt += __popc(g80);
+                            gsq = __builtin_amdgcn_udot4(q_, g80 >> 7, gsq, false);
+                            lut_sums(q_, g80, lut, gsl, gse);
+                            if (gfirst == INF32 && g80)
+                                gfirst = sidx + (uint32_t)(x0 + 4 * d) + ((uint32_t)__builtin_ctz(g80) >> 3);
+                        }
+                        fcnt += __popc(f80);
+                        fsq = __builtin_amdgcn_udot4(q_, f80 >> 7, fsq, false);
+                        if (any_msum) lut_sums(q_, msum ? f80 : 0u, lut, fsl, fse);
+                        if (ffirst == INF32 && f80)
+                            ffirst = sidx + (uint32_t)(x0 + 4 * d) + ((uint32_t)__builtin_ctz(f80) >> 3);
+                        while (r80) {
+                            const int sh = __builtin_ctz(r80) - 7;
+                            r80 &= r80 - 1;
+                            const uint32_t c = (c_ >> sh) & 0xFFu, q = (q_ >> sh) & 0xFFu;
+                            if ((int)q >= P.min_bq)
+                                ms_rare(S, c, q, sidx + (uint32_t)(x0 + 4 * d + (sh >> 3)), lut, T);
+                        }
+                    }
+                }
+            }
+            sidx += len;
+            if (fsq) { S.sq[Ms] = sat_add31(S.sq[Ms], fsq); fsq = 0; }
+            if (gsq) { S.sq[s2] = sat_add31(S.sq[s2], gsq); gsq = 0; }
+            if (s2 < 0) {                              // promote a frequent non-REF base (SNV) to SWAR
+                uint32_t best = 3;
+#pragma unroll
+                for (int k2 = 0; k2 < 4; k2++)
+                    if (k2 != Ms && S.cnt[k2] > best) { best = S.cnt[k2]; s2 = k2; }
+                if (s2 >= 0) mrep2 = slot_code(s2) * 0x01010101u;
+            }
+        }
+        if (fcnt) {
+            S.depth += fcnt;
+            S.cnt[Ms] += fcnt;
+            S.qf[Ms] = (uint8_t)min((uint32_t)S.qf[Ms], (uint32_t)P.qlo);
+            S.first[Ms] = min(S.first[Ms], ffirst);
+            if (msum) { S.sl[Ms] += fsl; S.se[Ms] += fse; }
+            else S.skip |= (uint8_t)(1u << Ms);
+        }
+        if (gcnt) {
+            S.depth += gcnt;
+            S.cnt[s2] += gcnt;
+            S.qf[s2] = (uint8_t)min((uint32_t)S.qf[s2], (uint32_t)P.qlo);
+            S.first[s2] = min(S.first[s2], gfirst);
+            S.sl[s2] += gsl;
+            S.se[s2] += gse;
+        }
+        if (P.S > 1) {
+            // partial state of this split -> k_merge_parts (11 x 16 B per lane, coalesced)
+            wave_sync();
+            const uint4 *src = reinterpret_cast<const uint4 *>(ST);
+            uint4 *dst = reinterpret_cast<uint4 *>(P.part + ((int64_t)s * P.n_groups + g) * 64);
+            for (int t = lane; t < 64 * 11; t += 64) dst[t] = src[t];
+            wave_sync();
+            continue;
+        }
+        // one run: assemble the record in the lane's own LDS slot, then store the wave's records
+        // with 16-B pieces (ten lanes per record)
+        uint32_t fl = 0;
+        if (inr && !deep && S.fb != INF32) {
+            const MState c = S;
+            Acc a;
+            if (!P.fresh) a = acc[p];
+            if (P.fresh || a.epoch != P.epoch) { a = Acc{}; a.epoch = P.epoch; }
+            merge_state(a, c, c.first, P.seq0 + c.fb, refc);
+            fl = 1u | ((!P.fresh || record_has_sums(a)) ? 2u : 0u);
+            *reinterpret_cast<Acc *>(&S) = a;
+        }
+        reinterpret_cast<uint32_t *>(&S)[40] = fl;     // byte 160: past the 160-B image
+        wave_sync();
+        for (int t = lane; t < 640; t += 64) {
+            const int r = t / 10, piece = t - 10 * r;
+            const uint32_t f = reinterpret_cast<const uint32_t *>(ST + r)[40];
+            if ((f & 1u) && (piece < 5 || (f & 2u)))
+                reinterpret_cast<uint4 *>(acc + p0 + r)[piece] = reinterpret_cast<const uint4 *>(ST + r)[piece];
+        }
+        wave_sync();
     }
-    merge_acc(acc + pos, st, P.batch_seq, P.epoch, refc, skip, P.batch_seq == 1);
+}
+
+// Fold the S partial states of a split run in batch order (first-entry keys (split, stream index)) and
+// merge them into the records.  One thread per position.
+__global__ __launch_bounds__(256) void k_merge_parts(MParams P, const uint8_t *__restrict__ ref,
+                                                     Acc *__restrict__ acc) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t p = P.u0 + i;
+    if (p >= P.u1) return;
+    MState c;
+    ms_init(c);
+    uint64_t key[NSLOT];
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) key[k] = ~0ull;
+    const int64_t stride = (int64_t)P.n_groups * 64;
+    for (int32_t s = 0; s < P.S; s++) {
+        const MState &q = P.part[(int64_t)s * stride + i];
+        const uint32_t fb = q.fb;
+        if (fb == INF32) continue;
+        if (c.fb == INF32) c.fb = fb;
+        c.depth += q.depth; c.n_del += q.n_del; c.n_skip += q.n_skip; c.n_other += q.n_other;
+        c.skip |= q.skip;
+#pragma unroll
+        for (int k = 0; k < NSLOT; k++) {
+            const uint32_t n = q.cnt[k];
+            if (!n) continue;
+            if (!c.cnt[k]) { key[k] = ((uint64_t)(uint32_t)s << 32) | q.first[k]; c.qf[k] = q.qf[k]; }
+            else c.qf[k] = (uint8_t)min((uint32_t)c.qf[k], (uint32_t)q.qf[k]);
+            c.cnt[k] += n;
+            c.sq[k] = sat_add31(c.sq[k], q.sq[k]);
+            c.sl[k] += q.sl[k];
+            c.se[k] += q.se[k];
+        }
+    }
+    if (c.fb == INF32) return;
+    Acc a;
+    if (!P.fresh) a = acc[p];
+    if (P.fresh || a.epoch != P.epoch) { a = Acc{}; a.epoch = P.epoch; }
+    merge_state(a, c, key, P.seq0 + c.fb, ref[p]);
+    const uint4 *src = reinterpret_cast<const uint4 *>(&a);
+    uint4 *dst = reinterpret_cast<uint4 *>(acc + p);
+    const bool sums = !P.fresh || record_has_sums(a);
+#pragma unroll
+    for (int t = 0; t < 10; t++)
+        if (t < 5 || sums) dst[t] = src[t];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -906,94 +1072,172 @@ __device__ __forceinline__ bool is_candidate(const FParams &F, const Acc &a, uin
            (double)ad / (double)a.depth >= F.ratio;                            // :151-157
 }
 
-// Exact sequential recomputation of one position over the batch history (rare: subnormal band,
-// IUPAC alleles).  np.prod left folds in BAM order, dict-order chains, exactly as utils.py:16-24.
-// Its per-allele tables live in the block's LDS (ReplayWs, one per thread) rather than in scratch:
-// a kernel with a private segment pays for it on every launch.
+// Exact sequential recomputation of one position over the batch history (rare: subnormal band, IUPAC
+// alleles, calls-only terms that were not accumulated).  np.prod is a strict left fold (utils.py:17,19)
+// and N a dict-order fold (:18-22): sequential per allele, but the 16 allele codes' folds are
+// independent.  The wave walks the position's entries 64 at a time (coalesced byte loads, one entry per
+// lane) over the batches the replay index lists for the position; lane c owns code c's fold and takes
+// the chunk's code-c factors in order through readlane, so no fold step waits on a memory load.
+// Pass 1: counts, first appearance (dict order), sum(eps) and the P folds (stopped at 0: P only
+// shrinks).  Pass 2: the H folds, only for alleles whose GL is not already exactly 0 through N == 0
+// (H is finite, so H * 0 == 0), each stopped at 0.
 struct ReplayWs {
     uint32_t cnt[16], ord[16];
-    double P[16], Hh[16], se[16], G[16];
+    uint64_t first[16];
+    double P[16], Hh[16], se[16], G[16], non[16];
+    uint32_t needH, n;
 };
 
-__device__ __forceinline__ void replay_position(const FParams &F, const Hist *__restrict__ H, const Acc &a,
-                                             const Tables *__restrict__ T, const Out &O, int64_t pos,
-                                             ReplayWs *__restrict__ w) {
-    int n = 0;
-    uint32_t depth = 0;
-    for (int c = 0; c < 16; c++) { w->cnt[c] = 0; w->P[c] = 1.0; w->Hh[c] = 1.0; w->se[c] = 0.0; }
-    for (int b = 0; b < F.n_hist; b++) {
+template <typename Fn>
+__device__ __forceinline__ void replay_walk(const FParams &F, const Hist *__restrict__ H, int64_t pos, int lane,
+                                            Fn &&fn) {
+    const bool indexed = F.ridx.n_buckets > 0;
+    uint32_t i0 = 0, i1 = (uint32_t)F.n_hist;
+    if (indexed) {
+        const int64_t bk = pos >> RIDX_SHIFT;
+        i0 = F.ridx.off[bk];
+        i1 = F.ridx.off[bk + 1];
+    }
+    uint64_t ord = 0;                                  // raw entries of this position in earlier batches
+    for (uint32_t i = i0; i < i1; i++) {
+        const int32_t b = indexed ? F.ridx.items[i] : (int32_t)i;
         const Hist h = H[b];
         const int64_t col = pos - h.pos_begin;
         if (col < 0 || col >= h.n_cols) continue;
         const uint64_t lo = h.off[col], hi = h.off[col + 1];
-        for (uint64_t i = lo; i < hi; i++) {
-            const uint32_t q = h.qual[i], c = h.code[i];
-            if ((int)q < F.min_bq) continue;
-            depth++;
-            if (c >= 16) continue;                         // D / N: depth only
-            const double e = T->eps[q];
-            if (w->cnt[c] == 0) { w->ord[n++] = c; w->P[c] = e; w->Hh[c] = 1.0 - e; }   // np.prod: x0, then *=
-            else { w->P[c] = w->P[c] * e; w->Hh[c] = w->Hh[c] * (1.0 - e); }
-            w->cnt[c]++;
-            w->se[c] += e;
+        for (uint64_t e0 = lo; e0 < hi; e0 += 64) {
+            const uint64_t e = e0 + (uint64_t)lane;
+            const bool valid = e < hi;
+            const uint32_t c = valid ? h.code[e] : 0xFFu, q = valid ? h.qual[e] : 0u;
+            fn(c, q, valid, ord + (e0 - lo));
         }
-    }
-    const bool evaluated = (int64_t)depth >= (int64_t)F.min_td;
-    double S = 0.0;
-    for (int h = 0; h < n; h++) {
-        double non = 1.0;
-        for (int j = 0; j < n; j++)
-            if (j != h) non = non * w->P[w->ord[j]];
-        w->G[h] = w->Hh[w->ord[h]] * non;
-        S = S + w->G[h];
-    }
-    if (S == 0) S = 1.0;
-    uint8_t flags = F.table ? O.flags[pos] : 0;
-    if (evaluated) {
-        double *gl = O.gl + pos * NSLOT;
-        for (int h = 0; h < n; h++) {
-            const uint32_t c = w->ord[h];
-            const int s = slot_of(c);
-            if (s >= 0 && F.table) gl[s] = w->G[h];
-            if (is_candidate(F, a, c, w->cnt[c])) {
-                write_candidate(F, O, pos, a, h, c, w->cnt[c], w->G[h], S, w->se[c] / (double)w->cnt[c]);
-                flags |= SPG_F_CANDIDATE;
-            }
-        }
-    }
-    if (F.table) O.flags[pos] = flags;
-    if (depth != a.depth) atomicOr(&O.ctr[F.cslot].err, 1u);   // history / accumulator mismatch
-    const uint32_t at = atomicAdd(&O.ctr[F.cslot].n_detail, 1u);
-    if (at < (uint32_t)F.detail_cap) {
-        spg_detail *d = O.detail + at;
-        d->pos = pos; d->depth = depth; d->n_alleles = (uint8_t)n;
-        d->pad[0] = d->pad[1] = d->pad[2] = 0;
-        for (int k = 0; k < 16; k++) {
-            d->code[k] = k < n ? (uint8_t)w->ord[k] : 0xFF;
-            d->count[k] = k < n ? w->cnt[w->ord[k]] : 0;
-            d->gl[k] = (k < n && evaluated) ? w->G[k] : __builtin_nan("");
-        }
+        ord += hi - lo;
     }
 }
 
-__global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restrict__ acc,
-                                                  const Tables *__restrict__ T, const Hist *__restrict__ H, Out O) {
-    __shared__ ReplayWs ws[64];
-    ReplayWs *my_ws = ws + (threadIdx.x & 63);
-    if (blockIdx.x == 0 && threadIdx.x == 0) O.ctr[F.cslot ^ 1u] = Counters{0, 0, 0, 0};   // next call's slot
-    const int64_t pos = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (pos >= F.n_pos) return;
+__device__ __forceinline__ void replay_wave(const FParams &F, const Hist *__restrict__ H, const Acc *__restrict__ acc,
+                                         const Out &O, int64_t pos, ReplayWs *w, const double *eps_s) {
+    const int lane = threadIdx.x & 63;
+    const Acc a = acc[pos];
+    uint32_t cnt = 0, depth = 0;
+    uint64_t first = ~0ull;
+    double P = 1.0, Hh = 1.0, se = 0.0;
+    replay_walk(F, H, pos, lane, [&](uint32_t c, uint32_t q, bool valid, uint64_t base) {
+        const bool pass = valid && (int)q >= F.min_bq;
+        depth += (uint32_t)__popcll(__ballot(pass));
+        const bool isc = pass && c < 16u;
+        const double e = isc ? eps_s[q] : 0.0;
+        uint64_t todo = __ballot(isc);
+        while (todo) {
+            const int j0 = (int)__builtin_ctzll(todo);
+            const uint32_t cc = __builtin_amdgcn_readlane(c, j0);
+            const bool mine = isc && c == cc;
+            const uint64_t bm = __ballot(mine);
+            todo &= ~bm;
+            const double es = dsum_f64(mine ? e : 0.0);
+            double pc = rl_f64(P, (int)cc);
+            for (uint64_t m = bm; m && pc != 0.0; m &= m - 1) pc = pc * rl_f64(e, (int)__builtin_ctzll(m));
+            if (lane == (int)cc) {
+                if (cnt == 0) first = base + (uint64_t)j0;
+                cnt += (uint32_t)__popcll(bm);
+                se += es;
+                P = pc;
+            }
+        }
+    });
+    if (lane < 16) { w->cnt[lane] = cnt; w->first[lane] = first; w->P[lane] = P; w->se[lane] = se; }
+    wave_sync();
+    if (lane == 0) {
+        int n = 0;                                     // dict order: codes by first appearance
+        for (int c = 0; c < 16; c++) {
+            if (!w->cnt[c]) continue;
+            int at = n++;
+            while (at > 0 && w->first[w->ord[at - 1]] > w->first[c]) { w->ord[at] = w->ord[at - 1]; at--; }
+            w->ord[at] = (uint32_t)c;
+        }
+        uint32_t need = 0;
+        for (int h = 0; h < n; h++) {                  // N_h = ((1.0 * P_a1) * P_a2) ... over a != h
+            double non = 1.0;
+            for (int j = 0; j < n; j++)
+                if (j != h) non = non * w->P[w->ord[j]];
+            w->non[h] = non;
+            if (non != 0.0) need |= 1u << w->ord[h];
+        }
+        w->n = (uint32_t)n;
+        w->needH = need;
+    }
+    wave_sync();
+    const uint32_t needH = w->needH;
+    if (needH) {
+        replay_walk(F, H, pos, lane, [&](uint32_t c, uint32_t q, bool valid, uint64_t) {
+            const bool isc = valid && (int)q >= F.min_bq && c < 16u && ((needH >> c) & 1u);
+            const double om = isc ? 1.0 - eps_s[q] : 0.0;
+            uint64_t todo = __ballot(isc);
+            while (todo) {
+                const uint32_t cc = __builtin_amdgcn_readlane(c, (int)__builtin_ctzll(todo));
+                const uint64_t bm = __ballot(isc && c == cc);
+                todo &= ~bm;
+                double hc = rl_f64(Hh, (int)cc);
+                for (uint64_t m = bm; m && hc != 0.0; m &= m - 1) hc = hc * rl_f64(om, (int)__builtin_ctzll(m));
+                if (lane == (int)cc) Hh = hc;
+            }
+        });
+    }
+    if (lane < 16) w->Hh[lane] = Hh;
+    wave_sync();
+    if (lane == 0) {
+        const int n = (int)w->n;
+        const bool evaluated = (int64_t)depth >= (int64_t)F.min_td;
+        double S = 0.0;
+        for (int h = 0; h < n; h++) {
+            w->G[h] = w->Hh[w->ord[h]] * w->non[h];
+            S = S + w->G[h];
+        }
+        if (S == 0) S = 1.0;
+        uint8_t flags = F.table ? O.flags[pos] : 0;
+        if (evaluated) {
+            double *gl = O.gl + pos * NSLOT;
+            for (int h = 0; h < n; h++) {
+                const uint32_t c = w->ord[h];
+                const int s = slot_of(c);
+                if (s >= 0 && F.table) gl[s] = w->G[h];
+                if (is_candidate(F, a, c, w->cnt[c])) {
+                    write_candidate(F, O, pos, a, h, c, w->cnt[c], w->G[h], S, w->se[c] / (double)w->cnt[c]);
+                    flags |= SPG_F_CANDIDATE;
+                }
+            }
+        }
+        if (F.table) O.flags[pos] = flags;
+        if (depth != a.depth) atomicOr(&O.ctr[F.cslot].err, 1u);   // history / accumulator mismatch
+        const uint32_t at = atomicAdd(&O.ctr[F.cslot].n_detail, 1u);
+        if (at < (uint32_t)F.detail_cap) {
+            spg_detail *d = O.detail + at;
+            d->pos = pos; d->depth = depth; d->n_alleles = (uint8_t)n;
+            d->pad[0] = d->pad[1] = d->pad[2] = 0;
+            for (int k = 0; k < 16; k++) {
+                d->code[k] = k < n ? (uint8_t)w->ord[k] : 0xFF;
+                d->count[k] = k < n ? w->cnt[w->ord[k]] : 0;
+                d->gl[k] = (k < n && evaluated) ? w->G[k] : __builtin_nan("");
+            }
+        }
+    }
+    wave_sync();
+}
+
+// prepare_variants for one position (one lane).  Returns true when the position needs the exact replay.
+__device__ __forceinline__ bool finalize_position(const FParams &F, const Acc *__restrict__ acc,
+                                                  const Tables *__restrict__ T, const Out &O, int64_t pos,
+                                                  double *sink) {
     const double NaN = __builtin_nan("");
     if (!F.table) {
-        // calls only: the header and the counts (first 48 bytes) decide whether this position can
-        // produce a call at all; only then is the rest of the record read
-        // header and counts in one round trip (the 52 bytes are loaded together)
+        // calls only: the header and the counts (first 52 bytes, one round trip) decide whether this
+        // position can produce a call at all; only then is the rest of the record read
         const uint4 h0 = reinterpret_cast<const uint4 *>(acc + pos)[0];
         const uint4 h1 = reinterpret_cast<const uint4 *>(acc + pos)[1];
         const uint4 c4 = reinterpret_cast<const uint4 *>(acc + pos)[2];
         const uint32_t c5 = reinterpret_cast<const uint32_t *>(acc + pos)[12];
-        if (h1.w != F.epoch || h0.y == 0) return;                       // not in memory
-        if ((int64_t)h0.x < (int64_t)F.min_td) return;                  // not evaluated (:131)
+        if (h1.w != F.epoch || h0.y == 0) return false;                  // not in memory
+        if ((int64_t)h0.x < (int64_t)F.min_td) return false;             // not evaluated (:131)
         if (!(h0.w & MISC_EXOTIC)) {
             const uint32_t cnt[NSLOT] = {c4.x, c4.y, c4.z, c4.w, c5};
             const uint8_t refc = (uint8_t)(h0.w & 0xFFu);
@@ -1002,13 +1246,13 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
             for (int k = 0; k < NSLOT; k++)
                 any |= cnt[k] != 0 && refc != nibble_char(slot_code(k)) && (int64_t)cnt[k] >= F.min_ad &&
                        (double)cnt[k] / (double)h0.x >= F.ratio;                         // :151-157
-            if (!any) return;
+            if (!any) return false;
         }
     }
     const Acc a = acc[pos];
     const bool live = a.epoch == F.epoch && a.first_batch != 0;
     uint32_t *cnt8 = O.counts + pos * SPG_NCOUNT;
-    double *gl = F.table ? O.gl + pos * NSLOT : reinterpret_cast<double *>(my_ws->G);   // scratch-free sink
+    double *gl = F.table ? O.gl + pos * NSLOT : sink;     // scratch-free sink
     if (F.table) {
         O.depth[pos] = live ? a.depth : 0u;
         O.order[pos] = live ? a.order : 0u;
@@ -1017,107 +1261,122 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
         for (int k = 0; k < NSLOT; k++) { cnt8[k] = live ? a.cnt[k] : 0u; gl[k] = NaN; }
         cnt8[5] = live ? a.n_del : 0u; cnt8[6] = live ? a.n_skip : 0u; cnt8[7] = live ? a.n_other : 0u;
     }
-    if (!live) { if (F.table) O.flags[pos] = 0; return; }
+    if (!live) { if (F.table) O.flags[pos] = 0; return false; }
     uint8_t flags = SPG_F_PRESENT;
     const bool evaluated = (int64_t)a.depth >= (int64_t)F.min_td;   // :131
     if (evaluated) flags |= SPG_F_EVALUATED;
     if (a.misc & MISC_EXOTIC) {       // IUPAC / '=' alleles: the exact replay tabulates every allele
         if (F.table) O.flags[pos] = flags | SPG_F_EXOTIC | SPG_F_REPLAYED;
-        goto replay;
+        return true;
     }
-    if (!evaluated) { if (F.table) O.flags[pos] = flags; return; }
-    {   // normal path; every exit that needs the exact replay jumps past this block
+    if (!evaluated) { if (F.table) O.flags[pos] = flags; return false; }
+    const int n = (int)(a.order & 7u);
+    const uint32_t skip = (a.misc >> MISC_SKIP_SHIFT) & 0x1Fu;
+    uint32_t slot[NSLOT], cnts[NSLOT];
+    LV Pv[NSLOT], Hv[NSLOT];
+    double Sv[NSLOT];
+    // per-allele P (= prod eps, utils.py:19) and H (= prod 1-eps, utils.py:17) in dict order
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) {
+        slot[k] = (a.order >> (3 + 3 * k)) & 7u;
+        cnts[k] = 0; Sv[k] = 0.0; Pv[k] = lv_normal(1.0, 0.0); Hv[k] = lv_normal(1.0, 0.0);
+        if (k >= n) continue;              // only the alleles present (no exp for empty slots)
+        uint32_t c_ = 0, sq = 0, qf = 0; double sl = 0.0, se = 0.0;
+#pragma unroll
+        for (int j = 0; j < NSLOT; j++)
+            if (slot[k] == (uint32_t)j) { c_ = a.cnt[j]; sq = a.sq[j]; qf = a.qf[j]; sl = a.sl[j]; se = a.se[j]; }
+        cnts[k] = c_;
+        Sv[k] = se;
+        // P: log10 P = -sum(q)/10 up to (n+2) ulp; exact zero proven when every factor < 1/2
+        if (sq <= 3076u) Pv[k] = lv_normal(T->p10k[sq / 10u] * T->eps[sq % 10u], -(double)sq * LOG2_10_OVER_10);
+        else if (sq >= 3245u && qf >= 4u) Pv[k] = lv_zero();
+        else Pv[k] = lv_band(-1022.0 + 2 * MARGIN);
+        // H: exp(sum ln(1-eps)); exactly 0 when a Q0 entry is present (1 - 1.0 == 0)
+        if (qf == 0u) Hv[k] = lv_zero();
+        else if ((skip >> slot[k]) & 1u) Hv[k] = lv_unknown();
+        else {
+            const double l2 = sl * INV_LN2;
+            Hv[k] = l2 > -1022.0 + MARGIN ? lv_normal(exp(sl), l2) : lv_band(-1022.0 + 2 * MARGIN);
+        }
+    }
+    double G[NSLOT];
+    bool band = false, unknown = false, cand_needs_s = false;
+#pragma unroll
+    for (int h = 0; h < NSLOT; h++) {
+        // N = ((1.0 * P_a1) * P_a2) ... over a != h in dict order (utils.py:18-22), GL = H * N
+        LV c = lv_normal(1.0, 0.0);
+#pragma unroll
+        for (int j = 0; j < NSLOT; j++)
+            if (j != h && j < n) c = lv_mul(c, Pv[j]);
+        const LV g = lv_mul(Hv[h], c);
+        if (h < n && g.s == 2) band = true;
+        G[h] = g.s == 0 ? g.v : (g.s == 3 ? NaN : 0.0);
+        if (h < n && g.s == 3) unknown = true;
+        // a candidate needs S = sum(GL) unless its own GL is exactly 0 (SCORE = 0 for any S)
+        if (h < n && g.s != 1 && is_candidate(F, a, slot_code((int)slot[h]), cnts[h])) {
+            cand_needs_s = true;
+            if (g.s == 3) band = true;        // its own GL depends on terms not accumulated
+        }
+    }
+    // unknown (not accumulated) GL terms only matter if a call needs S: then replay exactly
+    if (band || (unknown && cand_needs_s)) {
+        if (F.table) O.flags[pos] = flags | SPG_F_REPLAYED;
+        return true;
+    }
+    if (unknown) flags |= SPG_F_PARTIAL;
+    double S = 0.0;
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++)
+        if (k < n && !unknown) S = S + G[k];                 // :145
+    if (S == 0) S = 1.0;                                     // :146 (every call has GL 0 if unknown)
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) {
+        if (k < n) {
+#pragma unroll
+            for (int j = 0; j < NSLOT; j++)
+                if (slot[k] == (uint32_t)j) gl[j] = G[k];
+            const uint32_t code = slot_code((int)slot[k]);
+            if (is_candidate(F, a, code, cnts[k])) {
+                write_candidate(F, O, pos, a, k, code, cnts[k], G[k], S, Sv[k] / (double)cnts[k]);
+                flags |= SPG_F_CANDIDATE;
+            }
+        }
+    }
+    if (F.table) O.flags[pos] = flags;
+    return false;
+}
 
-        const int n = (int)(a.order & 7u);
-        const uint32_t skip = (a.misc >> MISC_SKIP_SHIFT) & 0x1Fu;
-        uint32_t slot[NSLOT], cnts[NSLOT];
-        LV Pv[NSLOT], Hv[NSLOT];
-        double Sv[NSLOT];
-        // per-allele P (= prod eps, utils.py:19) and H (= prod 1-eps, utils.py:17) in dict order
-    #pragma unroll
-        for (int k = 0; k < NSLOT; k++) {
-            slot[k] = (a.order >> (3 + 3 * k)) & 7u;
-            cnts[k] = 0; Sv[k] = 0.0; Pv[k] = lv_normal(1.0, 0.0); Hv[k] = lv_normal(1.0, 0.0);
-            if (k >= n) continue;              // only the alleles present (no exp for empty slots)
-            uint32_t c_ = 0, sq = 0, qf = 0; double sl = 0.0, se = 0.0;
-    #pragma unroll
-            for (int j = 0; j < NSLOT; j++)
-                if (slot[k] == (uint32_t)j) { c_ = a.cnt[j]; sq = a.sq[j]; qf = a.qf[j]; sl = a.sl[j]; se = a.se[j]; }
-            cnts[k] = c_;
-            Sv[k] = se;
-            // P: log10 P = -sum(q)/10 up to (n+2) ulp; exact zero proven when every factor < 1/2
-            if (sq <= 3076u) Pv[k] = lv_normal(T->p10k[sq / 10u] * T->eps[sq % 10u], -(double)sq * LOG2_10_OVER_10);
-            else if (sq >= 3245u && qf >= 4u) Pv[k] = lv_zero();
-            else Pv[k] = lv_band(-1022.0 + 2 * MARGIN);
-            // H: exp(sum ln(1-eps)); exactly 0 when a Q0 entry is present (1 - 1.0 == 0)
-            if (qf == 0u) Hv[k] = lv_zero();
-            else if ((skip >> slot[k]) & 1u) Hv[k] = lv_unknown();
-            else {
-                const double l2 = sl * INV_LN2;
-                Hv[k] = l2 > -1022.0 + MARGIN ? lv_normal(exp(sl), l2) : lv_band(-1022.0 + 2 * MARGIN);
-            }
-        }
-        double G[NSLOT];
-        bool band = false, unknown = false, cand_needs_s = false;
-    #pragma unroll
-        for (int h = 0; h < NSLOT; h++) {
-            // N = ((1.0 * P_a1) * P_a2) ... over a != h in dict order (utils.py:18-22), GL = H * N
-            LV c = lv_normal(1.0, 0.0);
-    #pragma unroll
-            for (int j = 0; j < NSLOT; j++)
-                if (j != h && j < n) c = lv_mul(c, Pv[j]);
-            const LV g = lv_mul(Hv[h], c);
-            if (h < n && g.s == 2) band = true;
-            G[h] = g.s == 0 ? g.v : (g.s == 3 ? NaN : 0.0);
-            if (h < n && g.s == 3) unknown = true;
-            // a candidate needs S = sum(GL) unless its own GL is exactly 0 (SCORE = 0 for any S)
-            if (h < n && g.s != 1 && is_candidate(F, a, slot_code((int)slot[h]), cnts[h])) {
-                cand_needs_s = true;
-                if (g.s == 3) band = true;        // its own GL depends on terms not accumulated
-            }
-        }
-        // unknown (not accumulated) GL terms only matter if a call needs S: then replay exactly
-        if (band || (unknown && cand_needs_s)) {
-            if (F.table) O.flags[pos] = flags | SPG_F_REPLAYED;
-            atomicAdd(&O.ctr[F.cslot].n_band, 1u);
-            goto replay;
-        }
-        if (unknown) flags |= SPG_F_PARTIAL;
-        double S = 0.0;
-    #pragma unroll
-        for (int k = 0; k < NSLOT; k++)
-            if (k < n && !unknown) S = S + G[k];                 // :145
-        if (S == 0) S = 1.0;                                     // :146 (every call has GL 0 if unknown)
-    #pragma unroll
-        for (int k = 0; k < NSLOT; k++) {
-            if (k < n) {
-    #pragma unroll
-                for (int j = 0; j < NSLOT; j++)
-                    if (slot[k] == (uint32_t)j) gl[j] = G[k];
-                const uint32_t code = slot_code((int)slot[k]);
-                if (is_candidate(F, a, code, cnts[k])) {
-                    write_candidate(F, O, pos, a, k, code, cnts[k], G[k], S, Sv[k] / (double)cnts[k]);
-                    flags |= SPG_F_CANDIDATE;
-                }
-            }
-        }
-        if (F.table) O.flags[pos] = flags;
-        return;
+// One wave per 64 positions: each lane runs prepare_variants' per-position logic; positions that need
+// the exact replay are then replayed one after another by the whole wave.
+__global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restrict__ acc,
+                                                  const Tables *__restrict__ T, const Hist *__restrict__ H, Out O) {
+    __shared__ double sink[64][NSLOT];
+    __shared__ double eps_s[256];
+    __shared__ ReplayWs ws;
+    const int lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && threadIdx.x == 0) O.ctr[F.cslot ^ 1u] = Counters{0, 0, 0, 0};   // next call's slot
+    const int64_t pos = (int64_t)blockIdx.x * 64 + lane;
+    const bool need = pos < F.n_pos && finalize_position(F, acc, T, O, pos, sink[lane]);
+    uint64_t rb = __ballot(need);
+    if (rb == 0) return;
+    if (need) atomicAdd(&O.ctr[F.cslot].n_band, 1u);
+    for (int q = lane; q < 256; q += 64) eps_s[q] = T->eps[q];
+    wave_sync();
+    while (rb) {
+        const int j = (int)__builtin_ctzll(rb);
+        rb &= rb - 1;
+        replay_wave(F, H, acc, O, (int64_t)blockIdx.x * 64 + j, &ws, eps_s);
     }
-replay:
-    replay_position(F, H, a, T, O, pos, my_ws);
 }
 
 // ------------------------------------------------------------------------------------------
 // launchers (called from spg_api.cpp)
 // ------------------------------------------------------------------------------------------
+// k_acc_seg over one batch: every column of a deep batch (W = 4), or the long columns (>= t_deep) of a
+// shallow one (W = 1; k_acc_multi takes the rest)
 hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_t *code, const uint8_t *qual,
                              const uint8_t *ref, const Tables *T, Acc *acc, hipStream_t st) {
     if (P.n_cols == 0) return hipSuccess;
-    if (P.t_deep > 1) {      // mixed / shallow batches: lane-per-column pass for the short columns
-        const int64_t blocks = (P.n_cols + 127) / 128;
-        hipLaunchKernelGGL(k_acc_shallow, dim3((unsigned)blocks), dim3(128), 0, st, P, off, code, qual, ref, T, acc);
-    }
     const int64_t waves = (P.n_cols + P.G - 1) / P.G;
     const int64_t blocks = (waves + KW - 1) / KW;
     const bool fresh = P.batch_seq == 1;
@@ -1135,9 +1394,24 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
     return hipGetLastError();
 }
 
+// k_acc_multi over a run of shallow batches (+ k_merge_parts when the run is split)
+hipError_t launch_multi(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, bool nt,
+                        int64_t max_blocks, hipStream_t st) {
+    const int64_t items = (int64_t)P.n_groups * P.S;
+    if (items == 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>((items + MW - 1) / MW, max_blocks);
+    if (nt) hipLaunchKernelGGL(k_acc_multi<true>, dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
+    else hipLaunchKernelGGL(k_acc_multi<false>, dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
+    if (P.S > 1) {
+        const int64_t mb = (P.u1 - P.u0 + 255) / 256;
+        hipLaunchKernelGGL(k_merge_parts, dim3((unsigned)mb), dim3(256), 0, st, P, ref, acc);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_finalize(const FParams &F, const Acc *acc, const Tables *T, const Out &O, const Hist *H,
                            hipStream_t st) {
-    const int64_t blocks = (F.n_pos + 63) / 64;      // 64-thread blocks: one wave, one ReplayWs per lane
+    const int64_t blocks = (F.n_pos + 63) / 64;      // 64-thread blocks: one wave
     hipLaunchKernelGGL(k_finalize, dim3((unsigned)blocks), dim3(64), 0, st, F, acc, T, H, O);
     return hipGetLastError();
 }

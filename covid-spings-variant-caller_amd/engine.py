@@ -11,6 +11,7 @@ from __future__ import annotations
 import ctypes as C
 import math
 import threading
+import weakref
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -109,6 +110,41 @@ class PileupEngine:
                                                   N.ptr(quals), int(n_entries), flags), "spg_accumulate_ex")
                 if borrow:
                     self._borrowed.append((offsets, codes, quals))
+
+    def accumulate_batches(self, batches, device: bool = False, borrow: bool = False):
+        """Many batches in one call (spg_accumulate_batches): ``batches`` is a sequence of
+        (pos_begin, offsets, codes, quals[, n_entries]) — numpy host arrays, or (``device=True``) torch
+        tensors on this engine's device (``borrow`` keeps them as history without a copy; the caller
+        keeps them alive until reset()).  Same result as one accumulate() per batch, in order."""
+        with self._lock:
+            rec = np.zeros(len(batches), N.BATCH_DTYPE)
+            keep = []
+            for i, b in enumerate(batches):
+                pb, off, c, q = b[:4]
+                if device:
+                    n = int(b[4]) if len(b) > 4 else int(off[-1].item())
+                    rec[i] = (int(pb), off.numel() - 1, off.data_ptr(), c.data_ptr(), q.data_ptr(), n)
+                else:
+                    off = np.ascontiguousarray(off, dtype=np.uint64)
+                    c = np.ascontiguousarray(c, dtype=np.uint8)
+                    q = np.ascontiguousarray(q, dtype=np.uint8)
+                    if len(c) != len(q):
+                        raise ValueError("codes and quals differ in length")
+                    rec[i] = (int(pb), len(off) - 1, off.ctypes.data, c.ctypes.data, q.ctypes.data, len(c))
+                keep.append((off, c, q))
+            flags = 0
+            if device:
+                import torch
+                self._torch_stream().wait_stream(torch.cuda.current_stream(self.device))
+                flags = N.SPG_IN_DEVICE | (N.SPG_IN_BORROW if borrow else 0)
+            N.check(self._L.spg_accumulate_batches(self._h, N.ptr(rec), len(rec), flags), "spg_accumulate_batches")
+            if device and borrow:
+                self._borrowed.extend(keep)
+
+    def wait_input(self):
+        """Block until every input copy enqueued so far has landed (pinned host buffers are free)."""
+        with self._lock:
+            N.check(self._L.spg_wait_input(self._h), "spg_wait_input")
 
     def _torch_stream(self):
         if getattr(self, "_ext", None) is None:
@@ -259,6 +295,19 @@ class PileupEngine:
                 out[p] = {N.SLOT_CHARS[(o >> (3 + 3 * i)) & 7]: float(t["gl"][p][(o >> (3 + 3 * i)) & 7])
                           for i in range(o & 7)}
         return out
+
+
+def pinned_empty(n: int, dtype=np.uint8) -> np.ndarray:
+    """A numpy array in pinned (page-locked) host memory (spg_host_alloc): CSR inputs staged here are
+    copied to HBM asynchronously (engine.wait_input() before reusing the buffer)."""
+    dtype = np.dtype(dtype)
+    nbytes = max(1, int(n) * dtype.itemsize)
+    L = N.gpu_lib()
+    p = C.c_void_p()
+    N.check(L.spg_host_alloc(nbytes, C.byref(p)), "spg_host_alloc")
+    buf = (C.c_uint8 * nbytes).from_address(p.value)
+    weakref.finalize(buf, L.spg_host_free, C.c_void_p(p.value))
+    return np.frombuffer(buf, dtype=dtype, count=int(n))
 
 
 def device_count() -> int:

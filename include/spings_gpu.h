@@ -30,6 +30,7 @@
 #ifndef SPINGS_GPU_H
 #define SPINGS_GPU_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -134,6 +135,28 @@ int spg_accumulate(spg_ctx *ctx, int64_t pos_begin, int64_t n_cols, const uint64
                    const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries);
 int spg_accumulate_ex(spg_ctx *ctx, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
                       const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags);
+
+/* Many batches (BAMs) in one call: exactly n successive spg_accumulate_ex calls, without n trips
+ * through the binding (process_bam over a list of BAMs, vc_queue.py:142-144 repeated).  Shallow
+ * batches (mean < 256 entries per column) are not launched one by one: the context folds a run of
+ * them per position in one pass (each record read and written once per run), when the run reaches
+ * SPG_RUN_MAX (env, default 4096) batches, before a deep batch, and at spg_finalize. */
+typedef struct {
+    int64_t pos_begin, n_cols;
+    const uint64_t *offsets;       /* n_cols + 1 */
+    const uint8_t *base_code, *qual;
+    uint64_t n_entries;
+} spg_batch;
+int spg_accumulate_batches(spg_ctx *ctx, const spg_batch *batches, int64_t n, uint32_t flags);
+
+/* Pinned (page-locked) host staging buffers for the CSR inputs (north_star: "SoA pinned buffers").
+ * Inputs in pinned memory are copied asynchronously on the context's copy stream: spg_accumulate
+ * returns after enqueue and the caller must not modify them until spg_wait_input (or spg_sync)
+ * returns.  Pageable inputs are copied before spg_accumulate returns. */
+int spg_host_alloc(size_t bytes, void **out);
+int spg_host_free(void *p);
+/* Block until every input copy enqueued so far has completed (the host buffers are free again). */
+int spg_wait_input(spg_ctx *ctx);
 
 /* prepare_variants (:120-231) + genotype_likelihood / to_phred_scale (utils.py:12-24):
  * per-position table and the candidate list, on device.  Returns after enqueue. */

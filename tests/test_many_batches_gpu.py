@@ -1,0 +1,173 @@
+"""GPU parity of the many-BAM path (BASELINE config 4: many BAMs accumulated into one `memory`,
+live_variant_caller.py:54-103 once per BAM, vc_queue.py:142-144) against the bit-exact C oracle.
+
+Shallow batches are folded per position in runs (k_acc_multi): a run of K batches reads and writes
+each record once, split over batch ranges (k_merge_parts) when the positions alone cannot fill the
+chip.  These tests drive >= 1,000 batches through that path, through the one-call entry point
+(spg_accumulate_batches) and per-batch calls, with heterogeneous column ranges, depth caps, planted
+SNVs, an IUPAC allele and a position whose P product lands in the subnormal band after the run (so
+the exact wave-parallel replay walks 1,000 batches through the replay index).
+"""
+import numpy as np
+import pytest
+
+import spings  # noqa: F401
+from oracle.c_oracle import COracle
+from oracle_util import compare_variants
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-9
+DEF = {"minBaseQuality": 30, "minTotalDepth": 10, "minAlleleDepth": 5, "minEvidenceRatio": 0.10}
+
+
+def _engine(ref, calls_only, n_pos=None):
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    return PileupEngine(n_pos or len(ref), DEF["minBaseQuality"], DEF["minTotalDepth"], DEF["minAlleleDepth"],
+                        DEF["minEvidenceRatio"], device=0, reference=ref, calls_only=calls_only)
+
+
+def _oracle(ref):
+    return COracle(ref, DEF["minBaseQuality"], DEF["minTotalDepth"], DEF["minAlleleDepth"], DEF["minEvidenceRatio"])
+
+
+def _plant(batch, pos, code, q):
+    """Append one entry (code, q) at the end of column `pos` of a CSR batch."""
+    pb, off, c, qq = batch
+    col = pos - pb
+    if col < 0 or col >= len(off) - 1:
+        return batch
+    at = int(off[col + 1])
+    c = np.insert(c, at, np.uint8(code))
+    qq = np.insert(qq, at, np.uint8(q))
+    off = off.copy()
+    off[col + 1:] += np.uint64(1)
+    return pb, off, c, qq
+
+
+def _many(L, n, depth, seed0, span, band_pos=None, iupac_pos=None, cap=0):
+    from covid_spings_variant_caller_amd import synth
+    ref = synth.reference(L, seed=seed0)
+    out = []
+    for i in range(n):
+        lo = (i * 131) % max(1, L - span)
+        b = synth.pileup(L, depth, seed=seed0 + 1 + i, ref=ref, snv_every=41, lo=lo, hi=min(L, lo + span),
+                         max_depth=cap)
+        if band_pos is not None and i < 98:
+            # 98 x Q31 of a non-REF base: sum(q) >= 3038, at or past the subnormal band
+            b = _plant(b, band_pos, 2 if ref[band_pos] != "C" else 4, 31)
+        if iupac_pos is not None and i == n // 2:
+            b = _plant(b, iupac_pos, 5, 35)         # one 'R' (IUPAC): exotic position, exact replay
+        out.append(b)
+    return ref, out
+
+
+def _check(eng, orc, check_mem=True):
+    eng.finalize()
+    orc.finalize()
+    if check_mem:
+        assert eng.memory_summary() == orc.memory_summary()
+    compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
+
+
+@pytest.mark.parametrize("calls_only", [True, False])
+def test_1000_batches_one_call_vs_oracle(calls_only):
+    L = 1500
+    ref, batches = _many(L, 1000, 40, 7000, span=1100, band_pos=700, iupac_pos=710, cap=35)
+    # the band position: REF at 700 must not be C for the planted allele to be an extra allele
+    eng = _engine(ref, calls_only)
+    orc = _oracle(ref)
+    eng.accumulate_batches(batches)
+    for b in batches:
+        orc.accumulate(*b)
+    _check(eng, orc)
+    t = eng.table()
+    assert t["flags"][710] & 12 == 12, "IUPAC position not replayed (exact walk over 1,000 batches)"
+    assert eng.counts()[1] >= 1
+    assert len(eng.variants()) > 10
+    eng.close()
+
+
+def test_1000_batches_per_call_and_live_finalize():
+    """Per-batch accumulate() calls (the live path) with a finalize every 125 BAMs (write_vcf after
+    BAMs, vc_queue.py:142-144): each intermediate call table equals the oracle's."""
+    L = 1200
+    ref, batches = _many(L, 1000, 30, 9100, span=900, band_pos=450)
+    eng = _engine(ref, True)
+    orc = _oracle(ref)
+    for i, b in enumerate(batches):
+        eng.accumulate(*b)
+        orc.accumulate(*b)
+        if (i + 1) % 125 == 0:
+            eng.finalize()
+            orc.finalize()
+            compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
+    _check(eng, orc)
+    eng.close()
+
+
+def test_unsplit_run_wide_range():
+    """A run over enough positions that it is not split over batch ranges (S = 1): 2 batches x 600 kb
+    at 30x, plus a deep batch in between (run, k_acc_seg, run)."""
+    from covid_spings_variant_caller_amd import synth
+    L = 600_000
+    ref = synth.reference(L, seed=77)
+    b1 = synth.pileup(L, 30, seed=78, ref=ref, snv_every=997, lo=0, hi=L)
+    b2 = synth.pileup(L, 25, seed=79, ref=ref, snv_every=991, lo=1000, hi=L - 5000, max_depth=20)
+    b3 = synth.pileup(L, 600, seed=80, ref=ref, snv_every=97, lo=200_000, hi=203_000)
+    b4 = synth.pileup(L, 30, seed=81, ref=ref, snv_every=997, lo=100, hi=L)
+    eng = _engine(ref, True)
+    orc = _oracle(ref)
+    eng.accumulate_batches([b1, b2])
+    eng.accumulate(*b3)
+    eng.accumulate(*b4)
+    for b in (b1, b2, b3, b4):
+        orc.accumulate(*b)
+    _check(eng, orc, check_mem=False)
+    # counts and dict order at every position (memory_summary at this size is slow in Python)
+    got = eng.table()
+    m = orc.memory_arrays()
+    pos = m["pos"].astype(np.int64)
+    np.testing.assert_array_equal(got["depth"][pos].astype(np.uint64), m["depth"])
+    eng.close()
+
+
+def test_device_borrowed_many_batches():
+    """Borrowed HBM batches through spg_accumulate_batches (no copy): same calls as host input."""
+    import torch
+    from covid_spings_variant_caller_amd import synth
+    L = 1000
+    ref, batches = _many(L, 300, 50, 4200, span=800)
+    dev = []
+    for pb, off, c, q in batches:
+        o, dc, dq = synth.to_device(off, c, q)
+        dev.append((pb, o, dc, dq, len(c)))
+    torch.cuda.synchronize()
+    eng = _engine(ref, True)
+    eng.accumulate_batches(dev, device=True, borrow=True)
+    orc = _oracle(ref)
+    for b in batches:
+        orc.accumulate(*b)
+    _check(eng, orc)
+    eng.close()
+
+
+def test_pinned_host_batches():
+    """Inputs in pinned host memory (spg_host_alloc) are copied asynchronously on the copy stream."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import pinned_empty
+    L = 1000
+    ref, batches = _many(L, 64, 60, 5200, span=900)
+    pinned = []
+    for pb, off, c, q in batches:
+        po, pc, pq = pinned_empty(len(off), np.uint64), pinned_empty(len(c), np.uint8), pinned_empty(len(q), np.uint8)
+        po[:], pc[:], pq[:] = off, c, q
+        pinned.append((pb, po, pc, pq))
+    eng = _engine(ref, True)
+    eng.accumulate_batches(pinned)
+    eng.wait_input()
+    orc = _oracle(ref)
+    for b in batches:
+        orc.accumulate(*b)
+    _check(eng, orc)
+    eng.close()
