@@ -1,20 +1,30 @@
 """Benchmark: pileup positions/s at 10,000x depth on 1..8 MI355X (BASELINE.json metric).
 
 One step = one pass of the hot path over one batch: reset the accumulators (new sample), accumulate
-the batch's CSR pileup (HBM-resident, borrowed), finalize (per-position table + call table), and —
-for N > 1 — gather the call tables to rank 0 over RCCL.  Workload (BASELINE config 2/"metric
-point"): synthetic SARS-CoV-2 reference (L = 29,903), 10,000x depth, 150-bp reads, uncapped
-(max_depth 0).  Weak scaling: with N GPUs a step processes N samples; rank r owns the r-th
-coordinate range of every sample (one engine over the concatenated shards).
+the batch's CSR pileup (HBM-resident, borrowed), finalize (call table), and — for N > 1 — gather the
+call tables to rank 0 (RCCL over xGMI).  Headline workload (BASELINE metric point): synthetic
+SARS-CoV-2 (L = 29,903), 10,000x depth, 150-bp reads, uncapped.  Weak scaling: with N GPUs a step
+processes N samples; rank r owns the r-th coordinate range of every sample.
 
-Timing: W untimed warm-up steps, then K steps between barrier + device synchronize; max over
-ranks.  The dominant kernel's duration is measured with HIP events on the engine's stream.
+Also on the same line (nested, never `value`):
+* ``parity_mode``: the metric point with pysam's max_depth 8,000 (E = 2.36e8);
+* ``config4``: BASELINE config 4 — 10,000 BAM-sized 100x SARS-CoV-2 samples accumulated into one
+  memory per step (live_variant_caller.py:54-103 once per BAM) and finalized; coordinate-sharded over
+  the N ranks (each rank: its range of every BAM);
+* ``end_to_end`` (host BAM -> calls) and ``cpu_baseline`` (the oracle restatements on host cores).
+
+Timing: W untimed warm-up steps; then 20 measurements, each of K steps (K = max(--steps, enough
+steps for >= 100 ms)) between barrier + device synchronize, max over ranks; the median measurement is
+reported.  The dominant kernel's duration comes from HIP events on the engine's stream (every
+--time-every-th step, so the events do not idle the GPU between steps).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import subprocess
 import sys
 import time
 
@@ -30,19 +40,22 @@ L_SARS = 29903
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--steps", type=int, default=20, help="minimum steps per timed measurement")
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", default="sars10k", choices=sorted(WORKLOADS) if False else
-                    ["sars10k", "sars1k", "sars100k", "chr1_30x"])
+    ap.add_argument("--reps", type=int, default=20, help="timed measurements (median reported)")
+    ap.add_argument("--min-ms", type=float, default=100.0, help="minimum duration of one measurement")
+    ap.add_argument("--workload", default="sars10k", choices=["sars10k", "sars1k", "sars100k", "chr1_30x"])
     ap.add_argument("--depth", type=float, default=0.0, help="override the workload's depth")
     ap.add_argument("--length", type=int, default=0, help="override the workload's reference length")
     ap.add_argument("--max-depth", type=int, default=0, help="0 = uncapped; 8000 = pysam parity cap")
+    ap.add_argument("--no-parity", action="store_true", help="skip the max_depth 8000 nested line")
+    ap.add_argument("--many-batches", type=int, default=10000, help="config 4 samples (0 = skip)")
+    ap.add_argument("--many-depth", type=float, default=100.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-positions", type=int, default=8000)
+    ap.add_argument("--cpu-positions", type=int, default=6000)
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end BAM -> calls leg")
     ap.add_argument("--time-every", type=int, default=8,
-                    help="HIP events around the accumulate kernel on every K-th timed step (each event "
-                         "pair idles the GPU for microseconds; 1 = every step)")
+                    help="HIP events around the accumulate kernel on every K-th timed step")
     ap.add_argument("--e2e-threads", type=int, default=16)
     ap.add_argument("--full-table", action="store_true", help="also accumulate every table GL term")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
@@ -50,12 +63,87 @@ def parse():
     return ap.parse_args()
 
 
-WORKLOADS = {   # BASELINE.json configs (the metric is quoted on sars10k; the others are optional runs)
+WORKLOADS = {   # BASELINE.json configs (the metric is quoted on sars10k)
     "sars10k": (L_SARS, 10000.0, "NC_045512.2"),
     "sars1k": (L_SARS, 1000.0, "NC_045512.2"),
     "sars100k": (L_SARS, 100000.0, "NC_045512.2"),
     "chr1_30x": (248956422, 30.0, "chr1"),
 }
+
+
+class Dist:
+    """torch.distributed helpers (no-ops at N = 1)."""
+
+    def __init__(self, world, rank, backend, device):
+        self.world, self.rank, self.backend, self.device = world, rank, backend, device
+        self.dist = None
+        if world > 1:
+            import torch
+            import torch.distributed as dist
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=device)
+            else:
+                dist.init_process_group(backend)
+            self.dist = dist
+            self.tdev = device if backend == "nccl" else torch.device("cpu")
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64, device=self.tdev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def measure(D, step, eng, K_min, reps, min_ms, every):
+    """reps measurements of K steps each (K >= K_min, >= min_ms of steps); max over ranks.  Returns
+    (K, per-measurement seconds, accumulate-kernel ms samples)."""
+    import torch
+    eng.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(3):
+        step(k)
+    eng.sync()
+    est = D.max((time.perf_counter() - t0) / 3)
+    K = max(K_min, int(math.ceil(min_ms * 1e-3 / max(est, 1e-7))))
+    eng.kernel_times(4096)
+    times, acc = [], []
+    for _ in range(reps):
+        eng.set_timing(0)
+        torch.cuda.synchronize()
+        D.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(K):
+            eng.set_timing(1 if k % every == 0 else 0)
+            step(k)
+        eng.sync()
+        torch.cuda.synchronize()
+        D.barrier()
+        times.append(D.max(time.perf_counter() - t0))
+        a, _ = eng.kernel_times(4096)
+        acc.extend(a[a > 0].tolist())
+    return K, np.array(times), np.array(acc)
+
+
+def finalize_ms(step, eng, n=8):
+    eng.set_timing(2)
+    for k in range(n):
+        step(k)
+    eng.sync()
+    _, f = eng.kernel_times(4096)
+    eng.set_timing(0)
+    return float(np.mean(f[f > 0])) if (f > 0).any() else 0.0
 
 
 def build_shard(rank, world, L, depth, max_depth, device):
@@ -86,15 +174,190 @@ def build_shard(rank, world, L, depth, max_depth, device):
     return ref, "".join(refs), off, d_off, d_c, d_q, int(base)
 
 
+def kernel_name(E, C):
+    """The accumulate instantiation the engine picks for this batch (csrc/spg_api.cpp add_batch)."""
+    if E < 256 * C:
+        return "k_acc_multi (+ k_acc_seg<1> for columns >= 128 entries)"
+    nt = 2 * E > (192 << 20)
+    return f"k_acc_seg<4,true,4,{'true' if nt else 'false'}> (spg_accumulate{'; non-temporal loads' if nt else ''})"
+
+
+def pmc_traffic(key, E):
+    """HBM bytes per launch of the accumulate kernel from the newest committed PMC summary
+    (profiles/rNN_*pmc.json, tools/summarize_prof.py over rocprofv3 --pmc passes of this bench:
+    FETCH_SIZE x2 + WRITE_SIZE), when it was measured on this workload; else None."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for k, v in d.items():
+            if k.startswith(key) and v.get("entries") == E:
+                return v.get("hbm_bytes_per_launch")
+    return None
+
+
+def run_point(args, D, L, depth, max_depth, local, world, rank, contig):
+    """The metric point (one sample per GPU per step, coordinate-sharded): returns the result dict."""
+    import torch
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    dev = torch.device("cuda", local)
+    t_gen = time.perf_counter()
+    ref, vref, off, d_off, d_c, d_q, E = build_shard(rank, world, L, depth, max_depth, dev)
+    C = len(off) - 1
+    t_gen = time.perf_counter() - t_gen
+    # calls-only engine (SPG_P_CALLS_ONLY): the call table prepare_variants() returns, exactly
+    eng = PileupEngine(C, 30, 10, 5, 0.10, device=local, reference=vref, calls_only=not args.full_table)
+    eng.reset()
+    eng.accumulate(0, d_off, d_c, d_q, borrow=True, n_entries=E)
+    eng.finalize()
+    n_cand, n_replay = eng.counts()
+    # call-table gather: persistent buffers, sized from this first pass (KBs per step)
+    cap = max(64, 4 * n_cand)
+    cap = int(D.max(cap))
+    rec = 56
+    gather_buf = torch.zeros(cap * rec + 8, dtype=torch.uint8, device=dev)
+    gdev = dev if args.backend == "nccl" else torch.device("cpu")
+    send = gather_buf if args.backend == "nccl" else torch.zeros_like(gather_buf, device="cpu")
+    recv = [torch.zeros_like(send) for _ in range(world)] if (world > 1 and rank == 0) else None
+
+    def step(k):
+        eng.reset()
+        eng.accumulate(0, d_off, d_c, d_q, borrow=True, n_entries=E)
+        eng.finalize()
+        if world > 1:
+            eng.copy_candidates_device(gather_buf, cap=cap)
+            if args.backend != "nccl":
+                send.copy_(gather_buf)                  # device -> persistent host buffer (gloo)
+            D.dist.gather(send, recv, dst=0)            # RCCL over xGMI for nccl
+
+    for k in range(args.warmup):
+        step(k)
+    K, times, acc = measure(D, step, eng, args.steps, args.reps, args.min_ms, max(1, args.time_every))
+    fin = finalize_ms(step, eng)
+    gathered = None
+    if world > 1:
+        # the gathered table must equal every rank's own table (count and bytes)
+        step(0)
+        eng.sync()
+        torch.cuda.synchronize()
+        mine = np.frombuffer(send.cpu().numpy().tobytes(), np.uint8) if args.backend != "nccl" else \
+            gather_buf.cpu().numpy()
+        n_mine = int(mine[:8].view(np.uint64)[0])
+        allmine = [torch.from_numpy(mine[:8 + n_mine * rec].copy()).to(gdev)]
+        sizes = torch.tensor([8 + n_mine * rec], dtype=torch.int64, device=gdev)
+        all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
+        D.dist.all_gather(all_sizes, sizes)
+        if rank == 0:
+            gathered = 0
+            for r in range(world):
+                got = recv[r].cpu().numpy()
+                n = int(got[:8].view(np.uint64)[0])
+                assert 8 + n * rec == int(all_sizes[r].item()), "gathered count differs from the rank's table"
+                gathered += n
+            assert np.array_equal(recv[0].cpu().numpy()[:8 + n_mine * rec], mine[:8 + n_mine * rec]), \
+                "gathered bytes differ from rank 0's table"
+        # every rank sends its table bytes to rank 0 for a byte comparison
+        buf = torch.zeros(8 + cap * rec, dtype=torch.uint8, device=gdev)
+        buf[:8 + n_mine * rec] = allmine[0]
+        outs = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
+        D.dist.gather(buf, outs, dst=0)
+        if rank == 0:
+            for r in range(world):
+                a, b = outs[r].cpu().numpy(), recv[r].cpu().numpy()
+                n = int(a[:8].view(np.uint64)[0])
+                assert np.array_equal(a[:8 + n * rec], b[:8 + n * rec]), f"rank {r}: gathered bytes differ"
+    med = float(np.median(times))
+    t_acc = float(np.mean(acc)) * 1e-3 if len(acc) else float("nan")
+    algo_bytes = 2 * E + 8 * (C + 1)          # base_code + qual + u64 offsets read by the accumulate kernel
+    eng.close()
+    return {
+        "value": world * L * K / med, "ms_per_step": med / K * 1e3, "steps": K, "E": E, "C": C,
+        "measurements_ms": [round(t * 1e3, 3) for t in times], "t_gen": t_gen,
+        "kernel_ms": t_acc * 1e3, "kernel_ms_median": float(np.median(acc)) if len(acc) else None,
+        "kernel_samples": int(len(acc)), "algo_bytes": algo_bytes, "achieved": algo_bytes / t_acc,
+        "finalize_ms": fin, "n_cand": n_cand, "n_replay": n_replay, "gathered": gathered,
+    }
+
+
+def run_config4(args, D, local, world, rank):
+    """BASELINE config 4: args.many_batches BAM-sized samples (args.many_depth x, per-BAM cap 8,000)
+    accumulated into one memory per step, then finalized; this rank's coordinate range of every BAM."""
+    import torch
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.synth_device import many_bams
+    dev = torch.device("cuda", local)
+    L = L_SARS
+    ref = synth.reference(L, seed=1)
+    shard = (L + world - 1) // world
+    lo, hi = rank * shard, min(L, (rank + 1) * shard)
+    t0 = time.perf_counter()
+    data = many_bams(ref, args.many_batches, args.many_depth, seed=1000, lo=lo, hi=hi, max_depth=8000, device=dev)
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
+    recs = data.records()
+    E = int(data.n_entries.sum())
+    C = hi - lo
+    eng = PileupEngine(C, 30, 10, 5, 0.10, device=local, reference=ref[lo:hi], calls_only=True)
+
+    def step(k):
+        eng.reset()
+        eng.accumulate_records(recs)
+        eng.finalize()
+
+    step(0)
+    n_cand, n_replay = eng.counts()
+    for k in range(max(1, args.warmup // 4)):
+        step(k)
+    K, times, acc = measure(D, step, eng, 1, args.reps, args.min_ms, 1)
+    fin = finalize_ms(step, eng, 4)
+    med = float(np.median(times))
+    t_acc = float(np.mean(acc)) * 1e-3 if len(acc) else float("nan")
+    # SURVEY §8(d) canonical bytes: 2E + 4 x CSR columns read + 68 x positions output
+    canon = 2 * E + 4 * args.many_batches * C + 68 * C
+    read = 2 * E + 8 * args.many_batches * (C + 1)
+    eng.close()
+    del data
+    torch.cuda.empty_cache()
+    return {
+        "workload": f"{args.many_batches} synthetic SARS-CoV-2 BAMs x {args.many_depth:.0f}x (per-BAM cap 8000, "
+                    f"seeds 1000+i, generated in HBM), accumulated into one memory + finalize per step; "
+                    f"coordinate-sharded x{world}",
+        "value": args.many_batches * L * K / med, "unit": "positions/s (BAMs x L per step)",
+        "ms_per_step": med / K * 1e3, "steps": K, "measurements": len(times),
+        "entries_per_gpu_step": E, "columns_per_gpu": C, "datagen_s": t_gen,
+        "kernel": "k_acc_multi + k_merge_parts (runs of <= 4096 BAMs)",
+        "accumulate_ms": t_acc * 1e3, "accumulate_samples": int(len(acc)), "finalize_ms": fin,
+        "roofline": {"bound": "hbm", "achieved": canon / t_acc / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                     "frac": canon / t_acc / PEAK_HBM, "algorithmic_bytes": canon,
+                     "read_bytes_per_step": read, "traffic": pmc_traffic("spg::k_acc_multi", E)},
+        "candidates_per_gpu_step": n_cand, "replayed_positions_per_gpu_step": n_replay,
+    }
+
+
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return None
+
+
 def cpu_baseline(args):
-    """Oracle restatements of the reference path on a bounded sample of the same workload."""
+    """Oracle restatements of the reference path on a bounded sample of the same workload, on this
+    box's host cores: the Python/numpy port (1 core), the C restatement on 1 core and on every core
+    this process may use (OpenMP)."""
     from covid_spings_variant_caller_amd import synth
     from oracle import reference_port as rp
     from oracle.c_oracle import COracle
     Lw, depth = args.eff_L, args.eff_depth
     ref = synth.reference(min(Lw, 10_000_000), seed=1)
     lo = 8000
-    # about 8e7 entries (~13 s in the numpy port) whatever the depth
     n = int(min(max(args.cpu_positions * 10000.0 / depth, 100), len(ref) - lo))
     _, off, c, q = synth.pileup(len(ref), depth, seed=2, ref=ref, lo=lo, hi=lo + n, max_depth=args.max_depth)
     t0 = time.perf_counter()
@@ -104,17 +367,26 @@ def cpu_baseline(args):
     t_py = time.perf_counter() - t0
     n_c = min(len(ref), max(n, int(3e8 / depth)))   # the C restatement: ~3e8 entries (the whole SARS genome)
     _, off2, c2, q2 = synth.pileup(len(ref), depth, seed=2, ref=ref, hi=n_c, max_depth=args.max_depth)
-    t0 = time.perf_counter()
-    co = COracle(ref, 30, 10, 5, 0.10)
-    co.accumulate(0, off2, c2, q2)
-    co.finalize()
-    t_c = time.perf_counter() - t0
+    res = {}
+    cores = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or cores
+    for tag, threads in (("c_restatement", 1), ("c_restatement_all_cores", min(cores, omp))):
+        COracle.set_threads(threads)
+        t0 = time.perf_counter()
+        co = COracle(ref, 30, 10, 5, 0.10)
+        co.accumulate(0, off2, c2, q2)
+        co.finalize()
+        t_c = time.perf_counter() - t0
+        res[tag] = {"value": n_c / t_c, "unit": "positions/s", "cores": threads,
+                    "sample": f"oracle/spg_oracle.c ({'OpenMP' if threads > 1 else 'sequential'}) on {n_c} positions "
+                              f"({int(off2[-1])} entries), {t_c:.2f} s"}
+        del co
+    COracle.set_threads(1)
     return {"value": n / t_py, "unit": "positions/s", "cores": 1, "kind": "port",
             "sample": f"oracle/reference_port.py (Python/numpy restatement of live_variant_caller.py:74-185) "
                       f"on {n} positions x {depth:.0f}x ({int(off[-1])} entries), {t_py:.2f} s, 1 core; "
                       f"pysam pileup/BAM decode not included (absent)",
-            "c_restatement": {"value": n_c / t_c, "unit": "positions/s", "cores": 1,
-                              "sample": f"oracle/spg_oracle.c on {n_c} positions ({int(off2[-1])} entries), {t_c:.2f} s"}}
+            **res, "cores_available": cores, "cpu_model": cpu_model()}
 
 
 def end_to_end(args, device):
@@ -157,167 +429,65 @@ def end_to_end(args, device):
     return res
 
 
-def kernel_name(E, C):
-    """The accumulate instantiation launch_accumulate (csrc/spg_kernels.hip) picks for this batch."""
-    if E < 256 * C:
-        return "k_acc_shallow + k_acc_seg<1,true,4,false> (spg_accumulate)"
-    nt = 2 * E > (192 << 20)
-    return f"k_acc_seg<4,true,4,{'true' if nt else 'false'}> (spg_accumulate{'; non-temporal loads' if nt else ''})"
-
-
-def pmc_traffic(E):
-    """HBM bytes per launch of the accumulate kernel from the newest committed PMC summary
-    (profiles/rNN_bench_pmc.json, written by tools/summarize_prof.py from rocprofv3 --pmc passes of
-    this bench: FETCH_SIZE x2 + WRITE_SIZE), when it was measured on this workload; else None."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench_pmc.json")))
-    if not files:
-        return None
-    try:
-        d = json.load(open(files[-1]))
-        rec = next((v for k, v in d.items() if k.startswith("spg::k_acc_seg<4, true")), None)
-        if rec is None or rec.get("entries") != E:
-            return None
-        return rec.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        return None
-
-
 def main():
     args = parse()
     import torch
     import spings  # noqa: F401
-    from covid_spings_variant_caller_amd import synth
-    from covid_spings_variant_caller_amd.engine import PileupEngine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.backend != "nccl":                  # functional runs of the N > 1 path on fewer GPUs
         local = local % max(1, torch.cuda.device_count())
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(args.backend)
-    else:
-        torch.cuda.set_device(0)
+    torch.cuda.set_device(local)
+    D = Dist(world, rank, args.backend, torch.device("cuda", local))
 
     L, depth, contig = WORKLOADS[args.workload]
     L = args.length or L
     depth = args.depth or depth
     args.eff_L, args.eff_depth = L, depth
-    dev = torch.device("cuda", local if world > 1 else 0)
-    t_gen = time.perf_counter()
-    ref, vref, off, d_off, d_c, d_q, E = build_shard(rank, world, L, depth, args.max_depth, dev)
-    C = len(off) - 1
-    t_gen = time.perf_counter() - t_gen
-    # calls-only engine (SPG_P_CALLS_ONLY): the call table prepare_variants() returns, exactly; see
-    # DESIGN.md §3 — the per-position GL table's REF-major entries are not accumulated
-    eng = PileupEngine(C, 30, 10, 5, 0.10, device=local if world > 1 else 0, reference=vref,
-                       calls_only=not args.full_table)
-
-    # call-table gather buffer: u64 count + records, sized from a first (untimed) pass so the
-    # per-step gather moves KBs, not the engine's full candidate capacity
-    eng.reset()
-    eng.accumulate(0, d_off, d_c, d_q, borrow=True, n_entries=E)
-    eng.finalize()
-    cand_cap = max(64, 4 * eng.counts()[0])
-    if dist is not None:
-        t = torch.tensor([cand_cap], dtype=torch.int64, device=d_c.device if args.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        cand_cap = int(t.item())
-    gather_buf = torch.zeros(cand_cap * 56 + 8, dtype=torch.uint8, device=d_c.device)
-    gather_out = [torch.empty_like(gather_buf) for _ in range(world)] if rank == 0 else None
-
-    def step():
-        eng.reset()
-        eng.accumulate(0, d_off, d_c, d_q, borrow=True, n_entries=E)
-        eng.finalize()
-        if dist is not None:
-            eng.copy_candidates_device(gather_buf, cap=cand_cap)
-            if args.backend == "nccl":
-                dist.gather(gather_buf, gather_out, dst=0)           # RCCL over xGMI
-            else:
-                dist.gather(gather_buf.cpu(), [o.cpu() for o in gather_out] if rank == 0 else None, dst=0)
-
-    for _ in range(args.warmup):
-        step()
-    eng.sync()
-    eng.kernel_times()                   # drop the warm-up steps' timings
-    # timed region: HIP events around the accumulate kernel on every time_every-th step (a uniform
-    # sample of the timed steps; events on every step would idle the GPU between launches)
-    eng.set_timing(0)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    every = max(1, args.time_every)
-    for k in range(args.steps):
-        eng.set_timing(1 if k % every == 0 else 0)
-        step()
-    eng.sync()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=d_c.device if args.backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    acc_ms, _ = eng.kernel_times(max(256, args.steps))  # HIP events of the sampled timed steps
-    acc_ms = acc_ms[acc_ms > 0]
-    eng.set_timing(2)                    # finalize duration from a few extra (untimed) steps
-    for _ in range(8):
-        step()
-    eng.sync()
-    _, fin_ms = eng.kernel_times()
-    n_cand, n_replay = eng.counts()
-    gathered = None
-    if dist is not None and rank == 0:
-        gathered = [int(o[:8].cpu().numpy().view(np.uint64)[0]) for o in gather_out]
-        if max(gathered) > cand_cap:
-            raise RuntimeError(f"call table larger than the gather buffer ({max(gathered)} > {cand_cap})")
-    positions_per_step = world * L
-    value = positions_per_step * args.steps / dt
-    t_acc = float(np.mean(acc_ms)) * 1e-3
-    t_fin = float(np.mean(fin_ms)) * 1e-3
-    algo_bytes = 2 * E + 8 * (C + 1)          # base_code + qual + u64 offsets read by the accumulate kernel
-    achieved = algo_bytes / t_acc
+    main_pt = run_point(args, D, L, depth, args.max_depth, local, world, rank, contig)
+    E, C = main_pt["E"], main_pt["C"]
     res = {
         "metric": ("pileup positions/s at 10,000x depth (SARS-CoV-2, synthetic)" if args.workload == "sars10k"
                    and depth == 10000 and L == L_SARS else f"pileup positions/s at {depth:,.0f}x depth ({contig} "
                    f"L={L:,}, synthetic)"),
-        "value": value, "unit": "positions/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u8/f64", "data": "synthetic",
+        "value": main_pt["value"], "unit": "positions/s", "n_gpus": world, "steps": main_pt["steps"],
+        "warmup": args.warmup, "ms_per_step": main_pt["ms_per_step"], "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8/f64", "data": "synthetic",
         "config": {"workload": f"{args.workload}: {contig} L={L}, {depth:.0f}x, 150-bp reads, "
                                + ("uncapped" if not args.max_depth else f"max_depth {args.max_depth}")
                                + ", 1 sample per GPU per step (coordinate-sharded)",
-                   "positions_per_step": positions_per_step, "entries_per_gpu_step": E, "columns_per_gpu": C,
+                   "positions_per_step": world * L, "entries_per_gpu_step": E, "columns_per_gpu": C,
                    "parallelism": f"coord-shard x{world}",
                    "engine_mode": "full_table" if args.full_table else "calls_only"},
-        "roofline": {"bound": "hbm", "achieved": achieved / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM, "traffic": pmc_traffic(E),
-                     "kernel": kernel_name(E, C), "kernel_ms": t_acc * 1e3, "algorithmic_bytes": algo_bytes},
-        "finalize_ms": t_fin * 1e3, "candidates_per_gpu_step": n_cand,
-        "replayed_positions_per_gpu_step": n_replay, "datagen_s": t_gen,
-        "calls_gathered_per_step": sum(gathered) if gathered is not None else n_cand,
+        "timing": {"measurements": len(main_pt["measurements_ms"]), "steps_per_measurement": main_pt["steps"],
+                   "steps_requested": args.steps, "measurement_ms": main_pt["measurements_ms"],
+                   "statistic": "median measurement; max over ranks"},
+        "roofline": {"bound": "hbm", "achieved": main_pt["achieved"] / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                     "frac": main_pt["achieved"] / PEAK_HBM, "traffic": pmc_traffic("spg::k_acc_seg<4, true", E),
+                     "kernel": kernel_name(E, C), "kernel_ms": main_pt["kernel_ms"],
+                     "kernel_ms_median": main_pt["kernel_ms_median"], "kernel_samples": main_pt["kernel_samples"],
+                     "algorithmic_bytes": main_pt["algo_bytes"]},
+        "finalize_ms": main_pt["finalize_ms"], "candidates_per_gpu_step": main_pt["n_cand"],
+        "replayed_positions_per_gpu_step": main_pt["n_replay"], "datagen_s": main_pt["t_gen"],
+        "calls_gathered_per_step": main_pt["gathered"] if main_pt["gathered"] is not None else main_pt["n_cand"],
     }
+    if not args.no_parity and not args.max_depth and args.workload == "sars10k":
+        p = run_point(args, D, L, depth, 8000, local, world, rank, contig)
+        res["parity_mode"] = {"max_depth": 8000, "value": p["value"], "ms_per_step": p["ms_per_step"],
+                              "steps": p["steps"], "entries_per_gpu_step": p["E"], "kernel_ms": p["kernel_ms"],
+                              "roofline_frac": p["achieved"] / PEAK_HBM, "finalize_ms": p["finalize_ms"],
+                              "candidates_per_gpu_step": p["n_cand"], "kernel": kernel_name(p["E"], p["C"])}
+    if args.many_batches > 0 and args.workload == "sars10k":
+        res["config4"] = run_config4(args, D, local, world, rank)
     if rank == 0 and world == 1 and not args.no_e2e and L == L_SARS:
         res["end_to_end"] = end_to_end(args, 0)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args)
-        res["cpu_baseline"]["cores_available"] = len(os.sched_getaffinity(0))
     if rank == 0:
-        print(json.dumps(res))
-    eng.close()
-    if dist is not None:
-        dist.destroy_process_group()
+        print(json.dumps(res), flush=True)
+    D.close()
 
 
 if __name__ == "__main__":

@@ -141,6 +141,19 @@ class PileupEngine:
             if device and borrow:
                 self._borrowed.extend(keep)
 
+    def accumulate_records(self, rec: np.ndarray, device: bool = True, borrow: bool = True):
+        """spg_accumulate_batches over prebuilt spg_batch records (N.BATCH_DTYPE), e.g.
+        synth_device.DeviceBatches.records(): one binding call for thousands of batches.  The caller
+        keeps the buffers alive (borrowed device inputs) until reset()."""
+        rec = np.ascontiguousarray(rec, dtype=N.BATCH_DTYPE)
+        with self._lock:
+            flags = 0
+            if device:
+                import torch
+                self._torch_stream().wait_stream(torch.cuda.current_stream(self.device))
+                flags = N.SPG_IN_DEVICE | (N.SPG_IN_BORROW if borrow else 0)
+            N.check(self._L.spg_accumulate_batches(self._h, N.ptr(rec), len(rec), flags), "spg_accumulate_batches")
+
     def wait_input(self):
         """Block until every input copy enqueued so far has landed (pinned host buffers are free)."""
         with self._lock:

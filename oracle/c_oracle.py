@@ -47,6 +47,8 @@ def lib():
         L.spo_memory.argtypes = [C.c_void_p] + [C.c_void_p] * 8
         L.spo_variants.argtypes = [C.c_void_p, C.c_void_p]
         L.spo_variant_size.restype = C.c_int
+        L.spo_set_threads.argtypes = [C.c_int]
+        L.spo_max_threads.restype = C.c_int
         assert L.spo_variant_size() == VARIANT_DTYPE.itemsize
         _lib = L
     return _lib
@@ -78,6 +80,15 @@ class COracle:
 
     def reset(self):
         lib().spo_reset(self._h)
+
+    @staticmethod
+    def set_threads(n: int):
+        """OpenMP threads of accumulate/finalize (1 = sequential; outputs identical for any count)."""
+        lib().spo_set_threads(int(n))
+
+    @staticmethod
+    def max_threads() -> int:
+        return lib().spo_max_threads()
 
     def accumulate(self, pos_begin, offsets, codes, quals):
         o = np.ascontiguousarray(offsets, dtype=np.uint64)

@@ -21,6 +21,9 @@
  * Build: make -C oracle   (-> oracle/_build/libspg_oracle.so)
  */
 #include <math.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -125,36 +128,53 @@ static inline void site_append(site_t *s, uint8_t code, uint8_t q) {
     s->q[k][s->len[k]++] = q;                               /* :103 */
 }
 
+/* Threads for spo_accumulate / spo_finalize (OpenMP; 1 = the sequential restatement).  Positions are
+ * independent, so the per-position arithmetic (and every output bit) is the same for any count. */
+static int g_threads = 1;
+void spo_set_threads(int n) { g_threads = n > 0 ? n : 1; }
+int spo_max_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
 /* live_variant_caller.py:74-103 over one CSR batch */
 int spo_accumulate(spo_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64_t *off, const uint8_t *code,
                    const uint8_t *qual) {
     if (pos_begin < 0 || pos_begin + n_cols > c->n_pos) return -1;
+    /* first visits in column order (:77-85): memory insertion order */
+    for (int64_t i = 0; i < n_cols; i++) {
+        int64_t pos = pos_begin + i;
+        if (off[i + 1] == off[i] || c->present[pos]) continue;   /* htslib emits no empty column */
+        c->present[pos] = 1;
+        c->ins[c->n_ins++] = pos;
+        c->site[pos] = (site_t *)calloc(1, sizeof(site_t));
+    }
+    int err = 0;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 256) num_threads(g_threads) reduction(| : err)
+#endif
     for (int64_t i = 0; i < n_cols; i++) {
         uint64_t lo = off[i], hi = off[i + 1];
-        if (hi == lo) continue;                             /* htslib emits no empty column */
+        if (hi == lo) continue;
         int64_t pos = pos_begin + i;
         uint64_t total = 0;
         for (uint64_t e = lo; e < hi; e++)
             if (!(c->min_bq > 0 && qual[e] < c->min_bq)) total++;   /* :75 len(pileups) */
-        if (!c->present[pos]) {                             /* :77-85 */
-            c->present[pos] = 1;
-            c->ins[c->n_ins++] = pos;
-            c->site[pos] = (site_t *)calloc(1, sizeof(site_t));
-            c->depth[pos] = total;
-        } else {
-            c->depth[pos] += total;                         /* :87 */
-        }
+        c->depth[pos] += total;                             /* :81 / :87 */
         site_t *s = c->site[pos];
         for (uint64_t e = lo; e < hi; e++) {                /* :89-103 */
             uint8_t q = qual[e], cd = code[e];
             if (c->min_bq > 0 && q < c->min_bq) continue;
             if (cd == CODE_DEL) { c->n_del[pos]++; continue; }
             if (cd == CODE_SKIP) { c->n_skip[pos]++; continue; }
-            if (cd >= NCODE) return -2;
+            if (cd >= NCODE) { err = 1; break; }
             site_append(s, cd, q);
         }
     }
-    return 0;
+    return err ? -2 : 0;
 }
 
 /* numpy pairwise_sum_DOUBLE (PW_BLOCKSIZE 128, unroll 8) */
@@ -193,62 +213,88 @@ static void push_var(spo_ctx *c, spo_variant *v) {
     c->var[c->n_var++] = *v;
 }
 
-/* live_variant_caller.py:120-185 + utils.py:16-24; returns the number of variants */
-int64_t spo_finalize(spo_ctx *c) {
-    c->n_var = 0;
-    double *eps = NULL;
-    size_t eps_cap = 0;
-    for (int64_t ii = 0; ii < c->n_ins; ii++) {
-        int64_t pos = c->ins[ii];
-        double *glp = c->gl + pos * NCODE;
-        for (int k = 0; k < NCODE; k++) glp[k] = NAN;
-        if (c->depth[pos] < (uint64_t)(c->min_td < 0 ? 0 : c->min_td)) continue;   /* :131 */
-        site_t *s = c->site[pos];
-        int n = s->n_all;
-        double P[NCODE], H[NCODE], Q[NCODE];
-        for (int k = 0; k < n; k++) {
-            uint32_t m = s->len[k];
-            if (m > eps_cap) { eps_cap = m * 2; eps = (double *)realloc(eps, eps_cap * 8); }
-            for (uint32_t j = 0; j < m; j++) eps[j] = c->eps[s->q[k][j]];   /* :132-138 */
-            double p = eps[0], h = 1.0 - eps[0];                           /* np.prod left fold */
-            for (uint32_t j = 1; j < m; j++) { p *= eps[j]; h *= (1.0 - eps[j]); }
-            P[k] = p; H[k] = h;
-            Q[k] = pairwise(eps, m) / (double)m;                            /* np.mean */
-        }
-        double G[NCODE];
-        double S = 0.0;
-        for (int h = 0; h < n; h++) {                                      /* :140-143 */
-            double non = 1.0;
-            for (int a = 0; a < n; a++)
-                if (a != h) non = non * P[a];
-            G[h] = H[h] * non;
-            glp[h] = G[h];
-        }
-        for (int h = 0; h < n; h++) S = S + G[h];                          /* :145 */
-        if (S == 0) S = 1.0;                                               /* :146 */
-        char refc = c->ref[pos];
-        for (int k = 0; k < n; k++) {                                      /* :148-185 */
-            uint32_t ad = s->len[k];
-            char allele = NIBBLE[s->code[k]];
-            if (refc != allele && (int64_t)ad >= c->min_ad &&
-                (double)ad / (double)c->depth[pos] >= c->ratio) {
-                spo_variant v;
-                memset(&v, 0, sizeof(v));
-                v.start = pos;
-                v.dp = (int32_t)c->depth[pos];
-                v.ad = (int32_t)ad;
-                v.ref = (uint8_t)refc;
-                v.alt = (uint8_t)allele;
-                v.gl_linear = G[k];
-                if (G[k] != 0) { v.gl = log10(G[k]); v.pl = (int32_t)rint(-10.0 * v.gl); v.gl_zero = 0; }
-                else { v.gl = 0; v.pl = 0; v.gl_zero = 1; }
-                v.score = to_phred(1.0 - (G[k] / S));
-                v.qual = Q[k];
-                push_var(c, &v);
-            }
+/* One position of prepare_variants (:131-185): GL per allele (utils.py:16-24) into glp, the emitted
+ * variants into out (at most NCODE); returns their number. */
+static int finalize_pos(const spo_ctx *c, int64_t pos, double **eps, size_t *eps_cap, spo_variant *out) {
+    double *glp = c->gl + pos * NCODE;
+    for (int k = 0; k < NCODE; k++) glp[k] = NAN;
+    if (c->depth[pos] < (uint64_t)(c->min_td < 0 ? 0 : c->min_td)) return 0;   /* :131 */
+    const site_t *s = c->site[pos];
+    int n = s->n_all;
+    double P[NCODE], H[NCODE], Q[NCODE];
+    for (int k = 0; k < n; k++) {
+        uint32_t m = s->len[k];
+        if (m > *eps_cap) { *eps_cap = m * 2; *eps = (double *)realloc(*eps, *eps_cap * 8); }
+        double *e = *eps;
+        for (uint32_t j = 0; j < m; j++) e[j] = c->eps[s->q[k][j]];     /* :132-138 */
+        double p = e[0], h = 1.0 - e[0];                                /* np.prod left fold */
+        for (uint32_t j = 1; j < m; j++) { p *= e[j]; h *= (1.0 - e[j]); }
+        P[k] = p; H[k] = h;
+        Q[k] = pairwise(e, m) / (double)m;                               /* np.mean */
+    }
+    double G[NCODE];
+    double S = 0.0;
+    for (int h = 0; h < n; h++) {                                       /* :140-143 */
+        double non = 1.0;
+        for (int a = 0; a < n; a++)
+            if (a != h) non = non * P[a];
+        G[h] = H[h] * non;
+        glp[h] = G[h];
+    }
+    for (int h = 0; h < n; h++) S = S + G[h];                           /* :145 */
+    if (S == 0) S = 1.0;                                                /* :146 */
+    char refc = c->ref[pos];
+    int nv = 0;
+    for (int k = 0; k < n; k++) {                                       /* :148-185 */
+        uint32_t ad = s->len[k];
+        char allele = NIBBLE[s->code[k]];
+        if (refc != allele && (int64_t)ad >= c->min_ad &&
+            (double)ad / (double)c->depth[pos] >= c->ratio) {
+            spo_variant v;
+            memset(&v, 0, sizeof(v));
+            v.start = pos;
+            v.dp = (int32_t)c->depth[pos];
+            v.ad = (int32_t)ad;
+            v.ref = (uint8_t)refc;
+            v.alt = (uint8_t)allele;
+            v.gl_linear = G[k];
+            if (G[k] != 0) { v.gl = log10(G[k]); v.pl = (int32_t)rint(-10.0 * v.gl); v.gl_zero = 0; }
+            else { v.gl = 0; v.pl = 0; v.gl_zero = 1; }
+            v.score = to_phred(1.0 - (G[k] / S));
+            v.qual = Q[k];
+            out[nv++] = v;
         }
     }
-    free(eps);
+    return nv;
+}
+
+/* live_variant_caller.py:120-185 + utils.py:16-24; returns the number of variants.  Positions in
+ * memory insertion order, evaluated in chunks (in parallel when threads > 1), emitted in order. */
+int64_t spo_finalize(spo_ctx *c) {
+    c->n_var = 0;
+    enum { CHUNK = 65536 };
+    spo_variant *buf = (spo_variant *)malloc((size_t)CHUNK * NCODE * sizeof(spo_variant));
+    int *nv = (int *)malloc((size_t)CHUNK * sizeof(int));
+    for (int64_t c0 = 0; c0 < c->n_ins; c0 += CHUNK) {
+        int64_t c1 = c0 + CHUNK < c->n_ins ? c0 + CHUNK : c->n_ins;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(g_threads)
+#endif
+        {
+            double *eps = NULL;
+            size_t eps_cap = 0;
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 64)
+#endif
+            for (int64_t ii = c0; ii < c1; ii++)
+                nv[ii - c0] = finalize_pos(c, c->ins[ii], &eps, &eps_cap, buf + (ii - c0) * NCODE);
+            free(eps);
+        }
+        for (int64_t ii = c0; ii < c1; ii++)
+            for (int k = 0; k < nv[ii - c0]; k++) push_var(c, buf + (ii - c0) * NCODE + k);
+    }
+    free(buf);
+    free(nv);
     return c->n_var;
 }
 

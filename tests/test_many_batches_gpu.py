@@ -171,3 +171,35 @@ def test_pinned_host_batches():
         orc.accumulate(*b)
     _check(eng, orc)
     eng.close()
+
+
+def test_config4_device_generated_batches_vs_oracle():
+    """The bench's config-4 data path: BAM-sized 100x samples generated in HBM (synth_device), fed as
+    borrowed spg_batch records (one binding call), coordinate shard [lo, hi) of the genome — calls and
+    memory vs the oracle on host copies of the same batches."""
+    import torch
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.synth_device import many_bams
+    L = 29903
+    ref = synth.reference(L, seed=1)
+    lo, hi = 11000, 13500
+    data = many_bams(ref, 400, 100, seed=1000, lo=lo, hi=hi, max_depth=8000, device=torch.device("cuda", 0))
+    torch.cuda.synchronize()
+    eng = PileupEngine(hi - lo, 30, 10, 5, 0.10, device=0, reference=ref[lo:hi], calls_only=True)
+    eng.accumulate_records(data.records())
+    eng.finalize()
+    orc = COracle(ref[lo:hi], 30, 10, 5, 0.10)
+    for i in range(len(data)):
+        pb, off, c, q = data.host(i)
+        orc.accumulate(pb - lo, off, c, q)
+    orc.finalize()
+    assert eng.memory_summary() == orc.memory_summary()
+    compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
+    assert len(eng.variants()) >= 2
+    # twice in a row on the same context (the bench's step: reset + accumulate + finalize)
+    eng.reset()
+    eng.accumulate_records(data.records())
+    eng.finalize()
+    compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
+    eng.close()
