@@ -106,6 +106,7 @@ struct spg_ctx {
     int64_t h_hist_cap = 0;
     int64_t pend0 = 0;                  // history batches [pend0, size) are not accumulated yet (a run)
     uint64_t pend_entries = 0;
+    uint32_t *kerr = nullptr;           // k_acc_multi error word (a batch too deep for a run)
     MState *part = nullptr;             // split-run partial states
     size_t part_bytes = 0;
     // replay index: history batches per 2^RIDX_SHIFT-position bucket
@@ -187,6 +188,8 @@ static int alloc_outputs(spg_ctx *c) {
     HIPCHK(hipMalloc(&c->detail, sizeof(spg_detail) * c->detail_cap));
     HIPCHK(hipMalloc(&c->ctr, 2 * sizeof(Counters)));
     HIPCHK(hipMemsetAsync(c->ctr, 0, 2 * sizeof(Counters), c->stream));
+    HIPCHK(hipMalloc(&c->kerr, sizeof(uint32_t)));
+    HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));
     return 0;
 }
 
@@ -238,7 +241,7 @@ int spg_destroy(spg_ctx *c) {
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     c->arena.release();
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
-                    c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx};
+                    c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
@@ -515,6 +518,7 @@ static int flush_run(spg_ctx *c, int64_t h1) {
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
     P.t_deep = K == 1 ? 128u : 0u;
     P.fresh = h0 == 0 ? 1u : 0u;
+    P.err = c->kerr;
     if (S > 1) {
         const size_t need = sizeof(MState) * (size_t)S * (size_t)P.n_groups * 64;
         if (need > c->part_bytes) {
@@ -786,6 +790,10 @@ static int settle(spg_ctx *c, Counters &h) {
         HIPCHK(hipMemcpyAsync(&h, c->ctr + c->cslot, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (h.err) return fail("spg: replay found a depth mismatch between history and accumulators");
+        uint32_t kerr = 0;
+        HIPCHK(hipMemcpy(&kerr, c->kerr, sizeof(kerr), hipMemcpyDeviceToHost));
+        if (kerr) return fail("spg: a shallow batch held >= 2^30 entries in 64 consecutive columns; accumulate it "
+                              "on its own as a deep batch (spg_accumulate on a context without a pending run)");
         bool again = false;
         if ((int64_t)h.n_cand > c->cand_cap) {
             HIPCHK(hipFree(c->cand));

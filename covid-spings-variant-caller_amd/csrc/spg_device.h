@@ -105,6 +105,7 @@ struct MParams {             // one k_acc_multi launch: history batches [h0, h0 
     uint32_t t_deep;         // K == 1: columns with >= t_deep entries are left to k_acc_seg (0 = none)
     uint32_t fresh;          // seq0 == 1: no record of this epoch exists yet
     MState *part;            // S > 1: partial records [S][n_groups * 64]
+    uint32_t *err;           // bit 0: a 64-column window of a run's batch held >= 2^30 entries (not run)
 };
 
 // Replay index: history batches overlapping each 2^RIDX_SHIFT-position bucket, in accumulate order.
@@ -136,7 +137,7 @@ struct Out {                // SoA result table
     double *gl;
     uint8_t *flags;
     spg_candidate *cand;
-    int64_t *band;          // positions queued for the exact replay (k_replay); n_band of them
+    int64_t *band;
     spg_detail *detail;
     Counters *ctr;          // Counters[2]
 };

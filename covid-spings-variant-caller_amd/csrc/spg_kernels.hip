@@ -764,7 +764,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
 // order.
 // ------------------------------------------------------------------------------------------
 constexpr int MW = 4;          // waves per k_acc_multi workgroup
-constexpr int MBLK = 4;        // 16-B blocks per lane per load round (64 entries)
 
 __device__ __forceinline__ uint32_t code_of_ref(uint8_t c) {
     c = (uint8_t)(c & 0xDFu);                     // upper case
@@ -788,13 +787,6 @@ __device__ __forceinline__ void ms_rare(MState &S, uint32_t code, uint32_t q, ui
     S.se[sl] += q == 0 ? 1.0 : t.y;                // eps(Q0) = 1
 }
 
-template <bool NT>
-__device__ __forceinline__ u32x4 ld16(const uint8_t *p) {
-    const u32x4 *v = reinterpret_cast<const u32x4 *>(p);
-    if constexpr (NT) return __builtin_nontemporal_load(v);
-    else return *v;
-}
-
 // sum over a fast allele's entries of a dword: {ln(1-eps), eps} rows of the LDS LUT (row q for the
 // selected bytes, a zero row for every other byte)
 __device__ __forceinline__ void lut_sums(uint32_t qw, uint32_t sel80, const double2 *__restrict__ lut, double &sl,
@@ -806,7 +798,8 @@ __device__ __forceinline__ void lut_sums(uint32_t qw, uint32_t sel80, const doub
     se += (t0.y + t1.y) + (t2.y + t3.y);
 }
 
-template <bool NT>
+// MBLK: 16-B blocks per lane per load round (MBLK x 16 entries)
+template <bool NT, int MBLK>
 __global__ __launch_bounds__(64 * MW) void k_acc_multi(MParams P, const Hist *__restrict__ H,
                                                        const uint8_t *__restrict__ ref,
                                                        const Tables *__restrict__ T, Acc *__restrict__ acc) {
@@ -844,13 +837,29 @@ __global__ __launch_bounds__(64 * MW) void k_acc_multi(MParams P, const Hist *__
         bool deep = false;
         uint32_t sidx = 0;                             // raw entries of this position in earlier batches
         const int32_t k0 = s * P.kper, k1 = min(P.K, k0 + P.kper);
+        // batch k's descriptor and this lane's CSR bounds, loaded one batch ahead so the next batch's
+        // offsets are in flight while this one streams
+        uint64_t obn = 0, oen = 0;
+        if (k0 < k1) {
+            const Hist hn = H[P.h0 + k0];
+            const int64_t cn = p - hn.pos_begin;
+            if (inr && cn >= 0 && cn < hn.n_cols) { obn = hn.off[cn]; oen = hn.off[cn + 1]; }
+        }
         for (int32_t k = k0; k < k1; k++) {
             const Hist h = H[P.h0 + k];
+            const uint64_t ob = obn, oe = oen;
+            if (k + 1 < k1) {
+                const Hist hn = H[P.h0 + k + 1];
+                const int64_t cn = p - hn.pos_begin;
+                obn = oen = 0;
+                if (inr && cn >= 0 && cn < hn.n_cols) {
+                    obn = __builtin_nontemporal_load(hn.off + cn);
+                    oen = __builtin_nontemporal_load(hn.off + cn + 1);
+                }
+            }
             const int64_t col = p - h.pos_begin;
             const bool cov = inr && col >= 0 && col < h.n_cols;
             if (__ballot(cov) == 0) continue;
-            uint64_t ob = 0, oe = 0;
-            if (cov) { ob = h.off[col]; oe = h.off[col + 1]; }
             uint32_t len = (uint32_t)(oe - ob);
             if (P.t_deep && len >= P.t_deep) { deep = true; len = 0; }   // k_acc_seg takes this column
             if (len && S.fb == INF32) S.fb = (uint32_t)k;
@@ -861,19 +870,32 @@ __global__ __launch_bounds__(64 * MW) void k_acc_multi(MParams P, const Hist *__
 #pragma unroll
             for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
             mx = __builtin_amdgcn_readfirstlane(mx);
-            const uint8_t *cb = h.code + a0, *qb = h.qual + a0;
+            // one buffer descriptor per array over the wave's byte range of this batch (the 64 columns
+            // are consecutive, so their segments are): lanes past their column read zeros, no branch
+            const uint64_t covm = __ballot(nblk != 0);
+            if (covm == 0) { sidx += len; continue; }
+            const int lf = (int)__builtin_ctzll(covm), ll = 63 - (int)__builtin_clzll(covm);
+            const uint64_t a1 = a0 + 16ull * nblk;
+            const uint64_t wb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)a0, lf) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(a0 >> 32), lf) << 32);
+            const uint64_t we = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)a1, ll) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(a1 >> 32), ll) << 32);
+            if (we - wb >= (1ull << 30)) {            // > 2^30 entries in 64 columns: not a shallow batch
+                if (lane == 0) atomicOr(P.err, 1u);
+                sidx += len;
+                continue;
+            }
+            const __amdgpu_buffer_rsrc_t rc = column_rsrc(h.code + wb, (uint32_t)(we - wb));
+            const __amdgpu_buffer_rsrc_t rq = column_rsrc(h.qual + wb, (uint32_t)(we - wb));
+            const uint32_t vo = (uint32_t)(a0 - wb);
             const bool dual = __ballot(s2 >= 0) != 0;
             for (uint32_t j = 0; j < mx; j += MBLK) {
                 u32x4 cw[MBLK], qw[MBLK];
 #pragma unroll
                 for (int u = 0; u < MBLK; u++) {
-                    if (j + u < nblk) {
-                        cw[u] = ld16<NT>(cb + 16u * (j + u));
-                        qw[u] = ld16<NT>(qb + 16u * (j + u));
-                    } else {
-                        cw[u] = u32x4{0u, 0u, 0u, 0u};
-                        qw[u] = u32x4{0u, 0u, 0u, 0u};
-                    }
+                    const uint32_t o = (j + u < nblk) ? vo + 16u * (j + u) : 0x80000000u;   // OOB -> 0
+                    cw[u] = __builtin_amdgcn_raw_buffer_load_b128(rc, (int)o, 0, 0);
+                    qw[u] = __builtin_amdgcn_raw_buffer_load_b128(rq, (int)o, 0, 0);
                 }
 #pragma unroll
                 for (int u = 0; u < MBLK; u++) {
@@ -1400,8 +1422,13 @@ hipError_t launch_multi(const MParams &P, const Hist *H, const uint8_t *ref, con
     const int64_t items = (int64_t)P.n_groups * P.S;
     if (items == 0) return hipSuccess;
     const int64_t blocks = std::min<int64_t>((items + MW - 1) / MW, max_blocks);
-    if (nt) hipLaunchKernelGGL(k_acc_multi<true>, dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
-    else hipLaunchKernelGGL(k_acc_multi<false>, dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
+    // Default-policy loads: a lane's 16-B blocks of one column are strided ~depth bytes from its
+    // neighbours', so one cache line serves several consecutive load instructions of the wave and must
+    // stay in L2 until they have all read it (non-temporal loads re-fetched such lines: 1.7x HBM bytes)
+    (void)nt;
+    static const int mblk = [] { const char *e = getenv("SPG_MBLK"); return e ? atoi(e) : 4; }();
+    if (mblk == 4) hipLaunchKernelGGL((k_acc_multi<false, 4>), dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
+    else hipLaunchKernelGGL((k_acc_multi<false, 8>), dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
     if (P.S > 1) {
         const int64_t mb = (P.u1 - P.u0 + 255) / 256;
         hipLaunchKernelGGL(k_merge_parts, dim3((unsigned)mb), dim3(256), 0, st, P, ref, acc);

@@ -42,12 +42,13 @@ class DeviceBatches:
         b, e = int(self.base[i]), int(self.n_entries[i])
         return (self.pos_begin, self.offsets[i], self.codes[b:b + e + 16], self.quals[b:b + e + 16], e)
 
-    def records(self):
-        """spg_batch records (include/spings_gpu.h) of every batch, for PileupEngine.accumulate_records."""
+    def records(self, pos_begin=None):
+        """spg_batch records (include/spings_gpu.h) of every batch, for PileupEngine.accumulate_records;
+        ``pos_begin`` overrides the first column's position (0 for an engine over this shard only)."""
         from . import _native as N
         rec = np.zeros(len(self), N.BATCH_DTYPE)
         C = self.n_cols
-        rec["pos_begin"] = self.pos_begin
+        rec["pos_begin"] = self.pos_begin if pos_begin is None else pos_begin
         rec["n_cols"] = C
         rec["offsets"] = self.offsets.data_ptr() + np.arange(len(self), dtype=np.uint64) * np.uint64(8 * (C + 1))
         rec["base_code"] = np.uint64(self.codes.data_ptr()) + self.base.astype(np.uint64)

@@ -187,7 +187,7 @@ def test_config4_device_generated_batches_vs_oracle():
     data = many_bams(ref, 400, 100, seed=1000, lo=lo, hi=hi, max_depth=8000, device=torch.device("cuda", 0))
     torch.cuda.synchronize()
     eng = PileupEngine(hi - lo, 30, 10, 5, 0.10, device=0, reference=ref[lo:hi], calls_only=True)
-    eng.accumulate_records(data.records())
+    eng.accumulate_records(data.records(pos_begin=0))
     eng.finalize()
     orc = COracle(ref[lo:hi], 30, 10, 5, 0.10)
     for i in range(len(data)):
@@ -199,7 +199,7 @@ def test_config4_device_generated_batches_vs_oracle():
     assert len(eng.variants()) >= 2
     # twice in a row on the same context (the bench's step: reset + accumulate + finalize)
     eng.reset()
-    eng.accumulate_records(data.records())
+    eng.accumulate_records(data.records(pos_begin=0))
     eng.finalize()
     compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
     eng.close()
