@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--no-parity", action="store_true", help="skip the max_depth 8000 nested line")
     ap.add_argument("--many-batches", type=int, default=10000, help="config 4 samples (0 = skip)")
     ap.add_argument("--many-depth", type=float, default=100.0)
+    ap.add_argument("--runs-batches", type=int, default=2000,
+                    help="config 4 as per-BAM batches folded in runs (k_acc_multi); 0 = skip")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-positions", type=int, default=6000)
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end BAM -> calls leg")
@@ -284,23 +286,83 @@ def run_point(args, D, L, depth, max_depth, local, world, rank, contig):
 
 def run_config4(args, D, local, world, rank):
     """BASELINE config 4: args.many_batches BAM-sized samples (args.many_depth x, per-BAM cap 8,000)
-    accumulated into one memory per step, then finalized; this rank's coordinate range of every BAM."""
+    accumulated into one memory per step, then finalized; this rank's coordinate range of every BAM.
+
+    Main figure: the batched layout a multi-BAM pileup emits (column-major: each position's entries of
+    every BAM concatenated, spg_accumulate_samples) - one deep column per position, k_acc_seg.
+    ``live_runs``: the same kind of samples as per-BAM CSR batches (what process_bam produces one BAM
+    at a time), folded in runs by k_acc_multi (args.runs_batches BAMs, spg_accumulate_batches)."""
     import torch
     from covid_spings_variant_caller_amd import synth
     from covid_spings_variant_caller_amd.engine import PileupEngine
-    from covid_spings_variant_caller_amd.synth_device import many_bams
+    from covid_spings_variant_caller_amd.synth_device import many_bams, many_bams_columns
     dev = torch.device("cuda", local)
     L = L_SARS
     ref = synth.reference(L, seed=1)
     shard = (L + world - 1) // world
     lo, hi = rank * shard, min(L, (rank + 1) * shard)
+    C = hi - lo
+    B = args.many_batches
     t0 = time.perf_counter()
-    data = many_bams(ref, args.many_batches, args.many_depth, seed=1000, lo=lo, hi=hi, max_depth=8000, device=dev)
+    d = many_bams_columns(ref, B, args.many_depth, seed=1000, lo=lo, hi=hi, max_depth=8000, device=dev)
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
+    E = d.n_entries
+    eng = PileupEngine(C, 30, 10, 5, 0.10, device=local, reference=ref[lo:hi], calls_only=True)
+
+    def step(k):
+        eng.reset()
+        eng.accumulate_samples(0, d.offsets, d.first_sample, d.codes, d.quals, B, borrow=True, n_entries=E)
+        eng.finalize()
+
+    step(0)
+    n_cand, n_replay = eng.counts()
+    for k in range(args.warmup):
+        step(k)
+    K, times, acc = measure(D, step, eng, args.steps, args.reps, args.min_ms, max(1, args.time_every))
+    fin = finalize_ms(step, eng)
+    med = float(np.median(times))
+    t_acc = float(np.mean(acc)) * 1e-3 if len(acc) else float("nan")
+    # SURVEY §8(d) canonical bytes: 2E + 4 x CSR columns read + 68 x positions output (the BAMs'
+    # per-BAM columns B x C count as read, although the batched layout reads only C + 1 offsets)
+    canon = 2 * E + 4 * B * C + 68 * C
+    read = 2 * E + 8 * (C + 1) + 4 * C
+    eng.close()
+    del d
+    torch.cuda.empty_cache()
+    res = {
+        "workload": f"{B} synthetic SARS-CoV-2 BAMs x {args.many_depth:.0f}x (per-BAM cap 8000, generated in HBM) "
+                    f"as one column-major multi-BAM batch (spg_accumulate_samples), accumulated into one memory + "
+                    f"finalize per step; coordinate-sharded x{world}",
+        "value": B * L * K / med, "unit": "positions/s (BAMs x L per step)",
+        "ms_per_step": med / K * 1e3, "steps": K, "measurements": len(times),
+        "entries_per_gpu_step": E, "columns_per_gpu": C, "datagen_s": t_gen,
+        "kernel": kernel_name(E, C), "accumulate_ms": t_acc * 1e3, "accumulate_samples": int(len(acc)),
+        "finalize_ms": fin,
+        "roofline": {"bound": "hbm", "achieved": canon / t_acc / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                     "frac": canon / t_acc / PEAK_HBM, "algorithmic_bytes": canon, "read_bytes_per_step": read,
+                     "frac_of_bytes_read": read / t_acc / PEAK_HBM,
+                     "traffic": pmc_traffic("spg::k_acc_seg<4, true", E)},
+        "candidates_per_gpu_step": n_cand, "replayed_positions_per_gpu_step": n_replay,
+    }
+    if args.runs_batches > 0:
+        res["live_runs"] = run_config4_runs(args, D, local, world, rank, ref, lo, hi)
+    return res
+
+
+def run_config4_runs(args, D, local, world, rank, ref, lo, hi):
+    """Config 4 as per-BAM CSR batches (batch-major), folded in runs by k_acc_multi."""
+    import torch
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.synth_device import many_bams
+    dev = torch.device("cuda", local)
+    B, C, L = args.runs_batches, hi - lo, L_SARS
+    t0 = time.perf_counter()
+    data = many_bams(ref, B, args.many_depth, seed=1000, lo=lo, hi=hi, max_depth=8000, device=dev)
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
     recs = data.records(pos_begin=0)   # the engine covers this shard only
     E = int(data.n_entries.sum())
-    C = hi - lo
     eng = PileupEngine(C, 30, 10, 5, 0.10, device=local, reference=ref[lo:hi], calls_only=True)
 
     def step(k):
@@ -309,33 +371,19 @@ def run_config4(args, D, local, world, rank):
         eng.finalize()
 
     step(0)
-    n_cand, n_replay = eng.counts()
-    for k in range(max(1, args.warmup // 4)):
-        step(k)
-    K, times, acc = measure(D, step, eng, 1, args.reps, args.min_ms, 1)
-    fin = finalize_ms(step, eng, 4)
+    n_cand = eng.counts()[0]
+    K, times, acc = measure(D, step, eng, 1, max(5, args.reps // 4), args.min_ms, 1)
     med = float(np.median(times))
     t_acc = float(np.mean(acc)) * 1e-3 if len(acc) else float("nan")
-    # SURVEY §8(d) canonical bytes: 2E + 4 x CSR columns read + 68 x positions output
-    canon = 2 * E + 4 * args.many_batches * C + 68 * C
-    read = 2 * E + 8 * args.many_batches * (C + 1)
+    canon = 2 * E + 4 * B * C + 68 * C
     eng.close()
     del data
     torch.cuda.empty_cache()
-    return {
-        "workload": f"{args.many_batches} synthetic SARS-CoV-2 BAMs x {args.many_depth:.0f}x (per-BAM cap 8000, "
-                    f"seeds 1000+i, generated in HBM), accumulated into one memory + finalize per step; "
-                    f"coordinate-sharded x{world}",
-        "value": args.many_batches * L * K / med, "unit": "positions/s (BAMs x L per step)",
-        "ms_per_step": med / K * 1e3, "steps": K, "measurements": len(times),
-        "entries_per_gpu_step": E, "columns_per_gpu": C, "datagen_s": t_gen,
-        "kernel": "k_acc_multi + k_merge_parts (runs of <= 4096 BAMs)",
-        "accumulate_ms": t_acc * 1e3, "accumulate_samples": int(len(acc)), "finalize_ms": fin,
-        "roofline": {"bound": "hbm", "achieved": canon / t_acc / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                     "frac": canon / t_acc / PEAK_HBM, "algorithmic_bytes": canon,
-                     "read_bytes_per_step": read, "traffic": pmc_traffic("spg::k_acc_multi", E)},
-        "candidates_per_gpu_step": n_cand, "replayed_positions_per_gpu_step": n_replay,
-    }
+    return {"bams": B, "value": B * L * K / med, "ms_per_step": med / K * 1e3, "measurements": len(times),
+            "entries_per_gpu_step": E, "datagen_s": t_gen, "kernel": "k_acc_multi + k_merge_parts",
+            "accumulate_ms": t_acc * 1e3, "candidates_per_gpu_step": n_cand,
+            "roofline": {"achieved": canon / t_acc / 1e9, "frac": canon / t_acc / PEAK_HBM,
+                         "algorithmic_bytes": canon, "traffic": pmc_traffic("spg::k_acc_multi", E)}}
 
 
 def cpu_model():

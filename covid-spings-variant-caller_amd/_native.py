@@ -81,6 +81,8 @@ def gpu_lib():
     _sig(L.spg_accumulate, i32, vp, i64, i64, vp, vp, vp, u64)
     _sig(L.spg_accumulate_ex, i32, vp, i64, i64, vp, vp, vp, u64, C.c_uint32)
     _sig(L.spg_accumulate_batches, i32, vp, vp, i64, C.c_uint32)
+    _sig(L.spg_accumulate_samples, i32, vp, i64, i64, i64, vp, vp, vp, vp, u64, C.c_uint32)
+    _sig(L.spg_history_samples, i32, vp, i64, C.POINTER(i64), vp)
     _sig(L.spg_host_alloc, i32, C.c_size_t, C.POINTER(vp))
     _sig(L.spg_host_free, i32, vp)
     _sig(L.spg_wait_input, i32, vp)

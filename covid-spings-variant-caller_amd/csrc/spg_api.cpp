@@ -51,6 +51,9 @@ struct HistBatch {
     uint64_t *off;
     uint8_t *code, *qual;
     bool owned;            // in the context's arena (else borrowed device buffers)
+    uint32_t seq0;         // batch_seq of its (first) sample
+    int64_t n_samples;     // > 1: a multi-sample column-major batch (spg_accumulate_samples)
+    uint32_t *fsamp;       // multi-sample: first sample holding entries, per column (device)
 };
 
 // Device arena for the owned batch copies (the replay history): slabs allocated once and bump-
@@ -466,7 +469,8 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch) {
     P.pos_begin = hb.pos_begin;
     P.n_cols = n_cols;
     fill_swar(c, P.min_bq, P.qlo, P.kpass, P.kok);
-    P.batch_seq = (uint32_t)(idx + 1);
+    P.batch_seq = hb.seq0;
+    P.fsamp = hb.fsamp;
     P.epoch = c->epoch;
     P.hdesc = Hist{hb.pos_begin, n_cols, hb.off, hb.code, hb.qual};
     P.hslot = c->d_hist + idx;
@@ -513,7 +517,7 @@ static int flush_run(spg_ctx *c, int64_t h1) {
     P.S = (int32_t)S;
     P.kper = (int32_t)kper;
     fill_swar(c, P.min_bq, P.qlo, P.kpass, P.kok);
-    P.seq0 = (uint32_t)(h0 + 1);
+    P.seq0 = c->hist[(size_t)h0].seq0;
     P.epoch = c->epoch;
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
     P.t_deep = K == 1 ? 128u : 0u;
@@ -550,7 +554,8 @@ static bool is_pinned(const void *p) {
 // index; a deep batch is accumulated right away, a shallow one joins the pending run.
 static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
                      const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags,
-                     bool *pageable_copy) {
+                     bool *pageable_copy, int64_t n_samples = 1, const uint32_t *first_sample = nullptr) {
+    if (n_samples < 1 || n_samples > (1 << 30)) return fail("spg_accumulate_samples: n_samples out of range");
     if (n_cols < 0 || pos_begin < 0 || pos_begin + n_cols > c->n_pos)
         return fail("spg_accumulate: column range outside the context's positions");
     if (pos_begin + n_cols > c->ref_len)
@@ -573,11 +578,16 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
                 if (base_code[i] > SPG_CODE_SKIP) return fail("spg_accumulate: base_code > 17 at entry " + std::to_string(i));
         }
     }
-    HistBatch hb{pos_begin, n_cols, n_entries, nullptr, nullptr, nullptr, !borrow};
+    HistBatch hb{pos_begin, n_cols, n_entries, nullptr, nullptr, nullptr, !borrow, c->batch_seq + 1, n_samples, nullptr};
+    if (first_sample && !dev) {
+        for (int64_t i = 0; i < n_cols; i++)
+            if (first_sample[i] >= (uint64_t)n_samples) return fail("spg_accumulate_samples: first_sample >= n_samples");
+    }
     if (borrow) {
         hb.off = const_cast<uint64_t *>(offsets);
         hb.code = const_cast<uint8_t *>(base_code);
         hb.qual = const_cast<uint8_t *>(qual);
+        hb.fsamp = const_cast<uint32_t *>(first_sample);
     } else {
         const size_t pad = (n_entries + 16 + 15) & ~size_t(15);
         uint8_t *m = nullptr;
@@ -594,6 +604,12 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
         }
         HIPCHK(hipMemsetAsync(hb.code + n_entries, 0xFF, pad - n_entries, cs));
         HIPCHK(hipMemsetAsync(hb.qual + n_entries, 0, pad - n_entries, cs));
+        if (first_sample) {
+            uint8_t *fs = nullptr;
+            HIPCHK(c->arena.alloc(sizeof(uint32_t) * n_cols, &fs));
+            hb.fsamp = reinterpret_cast<uint32_t *>(fs);
+            HIPCHK(hipMemcpyAsync(hb.fsamp, first_sample, sizeof(uint32_t) * n_cols, k, cs));
+        }
         HIPCHK(hipEventRecord(c->copy_ev, cs));
         c->copy_pending = true;
         // pageable host buffers are the caller's again on return; pinned ones after spg_wait_input
@@ -609,12 +625,13 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
         c->ridx_items++;
     }
     c->ridx_dirty = true;
-    c->batch_seq++;
+    c->batch_seq += (uint32_t)n_samples;
     c->finalized = false;
     static const double deep_min = [] { const char *e = getenv("SPG_DEEP_MIN"); return e ? atof(e) : 256.0; }();
     const double avg = (double)n_entries / (double)n_cols;
-    if (avg >= deep_min) {
-        // a deep batch: the run before it first (accumulate order), then k_acc_seg<4> on its own
+    if (avg >= deep_min || n_samples > 1 || first_sample) {
+        // a deep (or multi-sample) batch: the run before it first (accumulate order), then k_acc_seg on
+        // its own (a run folds single-sample batches with consecutive batch numbers)
         if (int rc = flush_run(c, idx)) return rc;
         c->pend0 = idx + 1;
         if (int rc = wait_copies(c)) return rc;
@@ -656,6 +673,38 @@ int spg_accumulate(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64_t
 
 int spg_accumulate_batches(spg_ctx *c, const spg_batch *batches, int64_t n, uint32_t flags) {
     return accumulate_many(c, batches, n, flags);
+}
+
+int spg_accumulate_samples(spg_ctx *c, int64_t pos_begin, int64_t n_cols, int64_t n_samples, const uint64_t *offsets,
+                           const uint32_t *first_sample, const uint8_t *base_code, const uint8_t *qual,
+                           uint64_t n_entries, uint32_t flags) {
+    if (!c) return fail("spg_accumulate_samples: null ctx");
+    if (!c->lut_set) return fail("spg_accumulate: spg_set_eps_lut not called");
+    if (!c->ref) return fail("spg_accumulate: spg_set_reference not called");
+    HIPCHK(hipSetDevice(c->device));
+    bool pageable = false;
+    int rc = add_batch(c, pos_begin, n_cols, offsets, base_code, qual, n_entries, flags, &pageable, n_samples,
+                       first_sample);
+    if (pageable) HIPCHK(hipStreamSynchronize(c->copy_stream));
+    return rc;
+}
+
+int spg_history_samples(spg_ctx *c, int64_t i, int64_t *n_samples, uint32_t *first_sample) {
+    if (!c) return fail("spg_history_samples: null ctx");
+    if (i < 0 || i >= (int64_t)c->hist.size()) return fail("spg_history_samples: batch index out of range");
+    HIPCHK(hipSetDevice(c->device));
+    const HistBatch &h = c->hist[(size_t)i];
+    if (n_samples) *n_samples = h.n_samples;
+    if (first_sample) {
+        if (h.fsamp) {
+            if (int rc = wait_copies(c)) return rc;
+            HIPCHK(hipMemcpyAsync(first_sample, h.fsamp, sizeof(uint32_t) * h.n_cols, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+        } else {
+            memset(first_sample, 0, sizeof(uint32_t) * h.n_cols);
+        }
+    }
+    return 0;
 }
 
 int spg_wait_input(spg_ctx *c) {

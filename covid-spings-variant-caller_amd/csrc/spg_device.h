@@ -71,6 +71,7 @@ struct KParams {
     uint64_t n_entries;    // entries of the batch (launch shape only)
     Hist hdesc;            // this batch's history descriptor ...
     Hist *hslot;           // ... written here by the first thread of the launch
+    const uint32_t *fsamp; // multi-sample batch: per column, the first sample holding entries (else null)
     uint32_t *dbg;         // SPG_TRACE: range violations recorded here instead of faulting (else null)
     uint4 *prog;           // SPG_TRACE: per-wave progress records in host-mapped memory (else null)
 };

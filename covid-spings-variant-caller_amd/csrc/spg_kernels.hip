@@ -276,7 +276,7 @@ constexpr int KW = 4;        // waves per k_acc_seg workgroup
 
 struct ColSum {              // one finished column's fast-path statistics (written by lane 0)
     uint32_t M, M2, fc, fs, fc2, fs2, ffirst, ffirst2;
-    uint32_t skipped, cj, crefc, pad;
+    uint32_t skipped, cj, crefc, fsamp;   // fsamp: first sample of a multi-sample column (0 otherwise)
     double fl, fe, fl2, fe2;
 };
 static_assert(sizeof(ColSum) == 80, "ColSum");
@@ -330,7 +330,7 @@ __device__ __forceinline__ void assemble_record(const KParams &P, const Acc *__r
         }
     }
     out->qf[5] = out->qf[6] = out->qf[7] = 0;
-    if (h0.y == 0) { h0.y = P.batch_seq; h0.w = S->crefc; }          // first visit (:77-85)
+    if (h0.y == 0) { h0.y = P.batch_seq + S->fsamp; h0.w = S->crefc; }   // first visit (:77-85)
     h0.x += R->depth + fc + fc2;                                      // :87
     h0.z = merge_order(h0.z, newmask, first);
     if (R->n_other) h0.w |= MISC_EXOTIC;
@@ -481,7 +481,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     // lane j < ng describes column g0 + j
     uint64_t ob = 0, oe = 0;
     uint32_t refc = 0;
-    if (lane < ng) { ob = off[g0 + lane]; oe = off[g0 + lane + 1]; refc = ref[P.pos_begin + g0 + lane]; }
+    uint32_t fsv = 0;                    // multi-sample batches: first sample holding entries of the column
+    if (lane < ng) {
+        ob = off[g0 + lane]; oe = off[g0 + lane + 1]; refc = ref[P.pos_begin + g0 + lane];
+        if (P.fsamp) fsv = P.fsamp[g0 + lane];
+    }
     if (P.dbg && lane < ng && (oe < ob || oe > P.n_entries)) {       // SPG_TRACE: bad CSR offsets
         atomicAdd(P.dbg, 1u);
         P.dbg[1] = (uint32_t)(g0 + lane);
@@ -728,11 +732,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 fc2 = dsum_u32(D2->cnt[lane]); fs2 = dsum_u32(D2->sq[lane]);
                 fl2 = dsum_f64(D2->sl[lane]); fe2 = dsum_f64(D2->se[lane]);
             }
+            const uint32_t fsc = (uint32_t)__builtin_amdgcn_readlane(fsv, (int)cj);
             if (lane == 0) {
                 ColSum *S = CS + nb;
                 S->M = M; S->M2 = dual ? M2 : 0u; S->fc = fc; S->fs = fs; S->fc2 = fc2; S->fs2 = fs2;
                 S->ffirst = ffirst; S->ffirst2 = ffirst2; S->skipped = skipped ? 1u : 0u; S->cj = cj;
                 S->crefc = crefc; S->fl = fl; S->fe = fe; S->fl2 = fl2; S->fe2 = fe2;
+                S->fsamp = fsc;
             }
             if (++nb == NB) finish();
         }

@@ -141,6 +141,34 @@ class PileupEngine:
             if device and borrow:
                 self._borrowed.extend(keep)
 
+    def accumulate_samples(self, pos_begin: int, offsets, first_sample, codes, quals, n_samples: int,
+                           borrow: bool = False, n_entries=None):
+        """spg_accumulate_samples: ``n_samples`` BAMs over one coordinate range as ONE column-major
+        batch (column c = sample 0's entries at c, then sample 1's, ...; see ``samples_to_columns``),
+        equal to one accumulate() per sample in order.  ``first_sample`` (u32 per column, or None)
+        names the first sample with an entry at each column.  numpy host arrays or torch tensors on
+        this engine's device (``borrow``: kept as history without a copy)."""
+        with self._lock:
+            if isinstance(offsets, np.ndarray):
+                o = np.ascontiguousarray(offsets, dtype=np.uint64)
+                c = np.ascontiguousarray(codes, dtype=np.uint8)
+                q = np.ascontiguousarray(quals, dtype=np.uint8)
+                fs = None if first_sample is None else np.ascontiguousarray(first_sample, dtype=np.uint32)
+                N.check(self._L.spg_accumulate_samples(self._h, int(pos_begin), len(o) - 1, int(n_samples), N.ptr(o),
+                                                       N.ptr(fs) if fs is not None else None, N.ptr(c), N.ptr(q),
+                                                       len(c), 0), "spg_accumulate_samples")
+            else:
+                import torch
+                self._torch_stream().wait_stream(torch.cuda.current_stream(self.device))
+                n = int(offsets[-1].item()) if n_entries is None else int(n_entries)
+                flags = N.SPG_IN_DEVICE | (N.SPG_IN_BORROW if borrow else 0)
+                N.check(self._L.spg_accumulate_samples(self._h, int(pos_begin), offsets.numel() - 1, int(n_samples),
+                                                       N.ptr(offsets),
+                                                       N.ptr(first_sample) if first_sample is not None else None,
+                                                       N.ptr(codes), N.ptr(quals), n, flags), "spg_accumulate_samples")
+                if borrow:
+                    self._borrowed.append((offsets, first_sample, codes, quals))
+
     def accumulate_records(self, rec: np.ndarray, device: bool = True, borrow: bool = True):
         """spg_accumulate_batches over prebuilt spg_batch records (N.BATCH_DTYPE), e.g.
         synth_device.DeviceBatches.records(): one binding call for thousands of batches.  The caller
@@ -308,6 +336,34 @@ class PileupEngine:
                 out[p] = {N.SLOT_CHARS[(o >> (3 + 3 * i)) & 7]: float(t["gl"][p][(o >> (3 + 3 * i)) & 7])
                           for i in range(o & 7)}
         return out
+
+
+def samples_to_columns(batches):
+    """Per-sample CSR batches over one range [(pos_begin, offsets, codes, quals)] -> the column-major
+    multi-sample batch of spg_accumulate_samples: (pos_begin, offsets, first_sample, codes, quals)."""
+    pbs = {int(b[0]) for b in batches}
+    ncs = {len(b[1]) - 1 for b in batches}
+    if len(pbs) != 1 or len(ncs) != 1:
+        raise ValueError("samples_to_columns: every sample batch must cover the same columns")
+    pb, C, S = pbs.pop(), ncs.pop(), len(batches)
+    lens = np.stack([np.diff(np.asarray(b[1], np.int64)) for b in batches])      # [S, C]
+    tot = lens.sum(axis=0)
+    off = np.zeros(C + 1, np.uint64)
+    np.cumsum(tot, out=off[1:])
+    # destination of sample s's column c: off[c] + lens[:s, c].sum()
+    start = off[:-1].astype(np.int64)[None, :] + np.cumsum(lens, axis=0) - lens
+    E = int(off[-1])
+    codes = np.empty(E, np.uint8)
+    quals = np.empty(E, np.uint8)
+    for s, b in enumerate(batches):
+        src_off = np.asarray(b[1], np.int64)
+        col = np.repeat(np.arange(C), lens[s])
+        dst = start[s][col] + (np.arange(len(col)) - src_off[:-1][col])
+        codes[dst] = b[2]
+        quals[dst] = b[3]
+    has = lens > 0
+    first = np.where(has.any(axis=0), has.argmax(axis=0), 0).astype(np.uint32)
+    return pb, off, first, codes, quals
 
 
 def pinned_empty(n: int, dtype=np.uint8) -> np.ndarray:

@@ -135,16 +135,29 @@ class LiveVariantCaller:
             for p in order.tolist():
                 b = int(t["first_batch"][p]) - 1
                 mem[p] = {"reference": refs[b][p], "totalDepth": int(t["depth"][p]), "snvs": {}, "indels": {}}
+            # every accumulated entry in accumulate order, then grouped per (position, allele) with a
+            # stable sort: each group is that allele's q list in BAM order (:103), groups of a position
+            # in order of their first entry (snvs dict order, :100-101)
+            pos_l, code_l, q_l = [], [], []
             for pb, off, codes, quals in hist:
-                for c in range(len(off) - 1):
-                    lo, hi = int(off[c]), int(off[c + 1])
-                    if lo == hi:
-                        continue
-                    snvs = mem[pb + c]["snvs"]
-                    for code, q in zip(codes[lo:hi].tolist(), quals[lo:hi].tolist()):
-                        if q < minbq or code >= 16:
-                            continue
-                        snvs.setdefault(N.NIBBLE[code], []).append(q)
+                lens = np.diff(off.astype(np.int64))
+                pos = np.repeat(np.arange(pb, pb + len(lens), dtype=np.int64), lens)
+                keep = (quals >= minbq) & (codes < 16)
+                pos_l.append(pos[keep]); code_l.append(codes[keep]); q_l.append(quals[keep])
+            if pos_l:
+                pos = np.concatenate(pos_l)
+                code = np.concatenate(code_l).astype(np.int64)
+                qs = np.concatenate(q_l)
+                key = pos * 16 + code
+                srt = np.argsort(key, kind="stable")
+                key_s = key[srt]
+                starts = np.flatnonzero(np.r_[True, key_s[1:] != key_s[:-1]])
+                ends = np.r_[starts[1:], len(key_s)]
+                first = srt[starts]                       # encounter index of each group's first entry
+                gpos, gcode = key_s[starts] // 16, key_s[starts] % 16
+                q_sorted = qs[srt]
+                for gi in np.lexsort((first, gpos)).tolist():
+                    mem[int(gpos[gi])]["snvs"][N.NIBBLE[int(gcode[gi])]] = q_sorted[starts[gi]:ends[gi]].tolist()
             return mem
 
     # -- hot path -----------------------------------------------------------------------------

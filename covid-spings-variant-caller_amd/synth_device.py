@@ -81,22 +81,8 @@ def many_bams(reference: str, n_batches: int, depth: float, seed: int = 1000, lo
     L = len(reference)
     hi = L if hi is None else hi
     C = hi - lo
-    ref_codes = np.zeros(256, np.uint8)
-    for ch, c in zip("ACGTN", (1, 2, 4, 8, 15)):
-        ref_codes[ord(ch)] = c
-        ref_codes[ord(ch.lower())] = c
-    rc = torch.from_numpy(ref_codes[np.frombuffer(reference[lo:hi].encode(), np.uint8)]).to(dev)
     cols = torch.arange(lo, hi, device=dev, dtype=torch.int64)
-    planted = (cols % snv_every) == (snv_every // 2)
-    af = torch.tensor([1.0, 0.5, 0.2, 0.05], device=dev)[((cols // snv_every) % 4)]
-    acgt = torch.tensor(ACGT, dtype=torch.uint8, device=dev)
-    log2 = {1: 0, 2: 1, 4: 2, 8: 3}
-    ref_idx = torch.zeros_like(rc, dtype=torch.int64)
-    for k, v in log2.items():
-        ref_idx[rc == k] = v
-    alt_idx = (ref_idx + 1 + (cols % 3)) % 4
-    qtab = _q_table(dev)
-    eps = torch.tensor([10.0 ** (-q / 10.0) for q in range(256)], device=dev, dtype=torch.float32)
+    gen = _EntryGen(reference, lo, hi, read_len, snv_every, seed, dev)
     n_reads = int(round(depth * L / read_len))
     per_sample = max(1.0, depth * C)
     chunk = max(1, min(n_batches, int(chunk_entries // per_sample)))
@@ -118,30 +104,121 @@ def many_bams(reference: str, n_batches: int, depth: float, seed: int = 1000, lo
     quals[E:] = 0
     for s0 in range(0, n_batches, chunk):
         s1 = min(n_batches, s0 + chunk)
-        g = torch.Generator(device=dev)
-        g.manual_seed(int(seed) * 1_000_003 + s0)
         lens = lens_cat[s0:s1]
         e0, e1 = int(base[s0]), int(base[s1 - 1] + n_entries[s1 - 1])
-        ne = e1 - e0
         flat = lens.reshape(-1)
         col = torch.repeat_interleave(torch.arange(C, device=dev).repeat(s1 - s0), flat)
-        q = qtab[torch.randint(0, 4096, (ne,), generator=g, device=dev)]
-        b = rc[col]
-        bi = ref_idx[col]
-        pl = planted[col]
-        if bool(pl.any()):
-            take = pl & (torch.rand(ne, generator=g, device=dev) < af[col])
-            b = torch.where(take, acgt[alt_idx[col]], b)
-            bi = torch.where(take, alt_idx[col], bi)
-        err = torch.rand(ne, generator=g, device=dev) < eps[q.long()]
-        shift = torch.randint(1, 4, (ne,), generator=g, device=dev)
-        b = torch.where(err, acgt[(bi + shift) % 4], b)
-        b = torch.where(torch.rand(ne, generator=g, device=dev) < 1e-4, torch.full_like(b, 15), b)
-        b = torch.where(torch.rand(ne, generator=g, device=dev) < (0.01 * 2 / read_len), torch.full_like(b, 16), b)
+        b, q = gen.draw(col, s0)
         codes[e0:e1] = b
         quals[e0:e1] = q
-        del col, q, b, bi, pl, err, shift
+        del col, q, b
     return DeviceBatches(lo, C, offsets, codes, quals, base, n_entries)
+
+
+@dataclass
+class DeviceColumns:
+    """n_samples BAMs as ONE column-major multi-sample batch (spg_accumulate_samples layout): column c
+    holds sample 0's entries at c, then sample 1's, ...; first_sample[c] is the first sample with any."""
+    pos_begin: int
+    n_cols: int
+    n_samples: int
+    offsets: "object"              # torch int64 [C+1]
+    first_sample: "object"         # torch int32 [C]
+    codes: "object"                # torch uint8 [E + 16]
+    quals: "object"
+    n_entries: int
+
+
+def many_bams_columns(reference: str, n_samples: int, depth: float, seed: int = 1000, lo: int = 0,
+                      hi: int | None = None, read_len: int = 150, max_depth: int = 0, snv_every: int = 997,
+                      device=None, chunk_entries: float = 2.0e8) -> DeviceColumns:
+    """Same samples as ``many_bams`` (read starts and per-BAM depth caps per sample, seeded per chunk of
+    samples), laid out column-major.  Entry values are i.i.d. given the column under the read model,
+    so each column's concatenated stream is drawn directly in HBM."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    L = len(reference)
+    hi = L if hi is None else hi
+    C = hi - lo
+    cols = torch.arange(lo, hi, device=dev, dtype=torch.int64)
+    n_reads = int(round(depth * L / read_len))
+    chunk = max(1, min(n_samples, int(chunk_entries // max(1.0, depth * C))))
+    tot = torch.zeros(C, dtype=torch.int64, device=dev)
+    first = torch.full((C,), -1, dtype=torch.int64, device=dev)
+    for s0 in range(0, n_samples, chunk):
+        s1 = min(n_samples, s0 + chunk)
+        lens = _lens(s0, s1, seed, n_reads, L, read_len, cols, max_depth, dev)[1]
+        tot += lens.sum(dim=0)
+        has = lens > 0
+        f = torch.where(has.any(dim=0), has.int().argmax(dim=0) + s0, torch.full_like(first, -1))
+        first = torch.where((first < 0) & (f >= 0), f, first)
+    offsets = torch.zeros(C + 1, dtype=torch.int64, device=dev)
+    offsets[1:] = torch.cumsum(tot, dim=0)
+    E = int(offsets[-1].item())
+    codes = torch.empty(E + 16, dtype=torch.uint8, device=dev)
+    quals = torch.empty(E + 16, dtype=torch.uint8, device=dev)
+    codes[E:] = 0xFF
+    quals[E:] = 0
+    # entries in column chunks of ~chunk_entries
+    gen = _EntryGen(reference, lo, hi, read_len, snv_every, seed, dev)
+    c0 = 0
+    off_h = offsets.cpu().numpy()
+    while c0 < C:
+        c1 = int(np.searchsorted(off_h, off_h[c0] + chunk_entries, side="right"))
+        c1 = min(C, max(c0 + 1, c1 - 1))
+        e0, e1 = int(off_h[c0]), int(off_h[c1])
+        if e1 > e0:
+            col = torch.repeat_interleave(torch.arange(c0, c1, device=dev), tot[c0:c1])
+            b, q = gen.draw(col, c0)
+            codes[e0:e1] = b
+            quals[e0:e1] = q
+            del col, b, q
+        c0 = c1
+    return DeviceColumns(lo, C, n_samples, offsets, first.clamp(min=0).to(torch.int32), codes, quals, E)
+
+
+class _EntryGen:
+    """Per-entry draws of the read model given each entry's column (shared by the generators)."""
+
+    def __init__(self, reference, lo, hi, read_len, snv_every, seed, dev):
+        import torch
+        ref_codes = np.zeros(256, np.uint8)
+        for ch, c in zip("ACGTN", (1, 2, 4, 8, 15)):
+            ref_codes[ord(ch)] = c
+            ref_codes[ord(ch.lower())] = c
+        self.rc = torch.from_numpy(ref_codes[np.frombuffer(reference[lo:hi].encode(), np.uint8)]).to(dev)
+        cols = torch.arange(lo, hi, device=dev, dtype=torch.int64)
+        self.planted = (cols % snv_every) == (snv_every // 2)
+        self.af = torch.tensor([1.0, 0.5, 0.2, 0.05], device=dev)[((cols // snv_every) % 4)]
+        self.acgt = torch.tensor(ACGT, dtype=torch.uint8, device=dev)
+        self.ref_idx = torch.zeros_like(self.rc, dtype=torch.int64)
+        for k, v in {1: 0, 2: 1, 4: 2, 8: 3}.items():
+            self.ref_idx[self.rc == k] = v
+        self.alt_idx = (self.ref_idx + 1 + (cols % 3)) % 4
+        self.qtab = _q_table(dev)
+        self.eps = torch.tensor([10.0 ** (-q / 10.0) for q in range(256)], device=dev, dtype=torch.float32)
+        self.read_len, self.seed, self.dev = read_len, seed, dev
+
+    def draw(self, col, salt):
+        import torch
+        dev = self.dev
+        g = torch.Generator(device=dev)
+        g.manual_seed(int(self.seed) * 1_000_003 + int(salt))
+        ne = col.numel()
+        q = self.qtab[torch.randint(0, 4096, (ne,), generator=g, device=dev)]
+        b = self.rc[col]
+        bi = self.ref_idx[col]
+        pl = self.planted[col]
+        if bool(pl.any()):
+            take = pl & (torch.rand(ne, generator=g, device=dev) < self.af[col])
+            b = torch.where(take, self.acgt[self.alt_idx[col]], b)
+            bi = torch.where(take, self.alt_idx[col], bi)
+        err = torch.rand(ne, generator=g, device=dev) < self.eps[q.long()]
+        shift = torch.randint(1, 4, (ne,), generator=g, device=dev)
+        b = torch.where(err, self.acgt[(bi + shift) % 4], b)
+        b = torch.where(torch.rand(ne, generator=g, device=dev) < 1e-4, torch.full_like(b, 15), b)
+        b = torch.where(torch.rand(ne, generator=g, device=dev) < (0.01 * 2 / self.read_len), torch.full_like(b, 16), b)
+        return b, q
 
 
 def _lens(s0, s1, seed, n_reads, L, read_len, cols, max_depth, dev):

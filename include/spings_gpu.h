@@ -149,6 +149,18 @@ typedef struct {
 } spg_batch;
 int spg_accumulate_batches(spg_ctx *ctx, const spg_batch *batches, int64_t n, uint32_t flags);
 
+/* BASELINE config 4 ingest: n_samples BAMs over one coordinate range in ONE column-major CSR batch,
+ * the layout a multi-BAM pileup (samtools mpileup style) emits: column c's entries are sample 0's
+ * pileup entries at that position, then sample 1's, ..., each in its own BAM order.  Accumulating it
+ * equals n_samples successive spg_accumulate calls, one per sample in sample order (the reference's
+ * process_bam per BAM, live_variant_caller.py:54-103): dict order follows the concatenated stream,
+ * batch numbers advance by n_samples, and a position first visited here gets first_batch =
+ * (first batch number) + first_sample[c], the first sample with an entry at c (NULL: 0 for every
+ * column).  Each position's stream is one long column, so the deep kernel streams it. */
+int spg_accumulate_samples(spg_ctx *ctx, int64_t pos_begin, int64_t n_cols, int64_t n_samples,
+                           const uint64_t *offsets, const uint32_t *first_sample, const uint8_t *base_code,
+                           const uint8_t *qual, uint64_t n_entries, uint32_t flags);
+
 /* Pinned (page-locked) host staging buffers for the CSR inputs (north_star: "SoA pinned buffers").
  * Inputs in pinned memory are copied asynchronously on the context's copy stream: spg_accumulate
  * returns after enqueue and the caller must not modify them until spg_wait_input (or spg_sync)
@@ -195,6 +207,9 @@ int spg_copy_candidates_device(spg_ctx *ctx, void *dst, int64_t cap);
 int spg_history_count(spg_ctx *ctx, int64_t *n_batches);
 int spg_history_info(spg_ctx *ctx, int64_t i, int64_t *pos_begin, int64_t *n_cols, uint64_t *n_entries);
 int spg_history_copy(spg_ctx *ctx, int64_t i, uint64_t *offsets, uint8_t *base_code, uint8_t *qual);
+/* Samples of history batch i (1 unless it came from spg_accumulate_samples) and, if first_sample is
+ * not NULL, its per-column first samples (n_cols; zeros for a single-sample batch). */
+int spg_history_samples(spg_ctx *ctx, int64_t i, int64_t *n_samples, uint32_t *first_sample);
 
 /* Timing hooks (bench): HIP events around the accumulate launches of one finalize step (first
  * begin .. last end) and around the finalize launch, ms.  spg_last_kernel_ms: the latest step.

@@ -203,3 +203,83 @@ def test_config4_device_generated_batches_vs_oracle():
     eng.finalize()
     compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
     eng.close()
+
+
+def _drop_cols(batch, c0, c1):
+    """A sample batch with no entries in columns [c0, c1) (the sample does not cover them)."""
+    pb, off, c, q = batch
+    off = np.asarray(off, np.int64)
+    e0, e1 = int(off[c0]), int(off[c1])
+    keep = np.r_[np.arange(0, e0), np.arange(e1, len(c))].astype(np.int64)
+    off2 = off.copy()
+    off2[c0 + 1:c1 + 1] = e0
+    off2[c1 + 1:] -= (e1 - e0)
+    return pb, off2.astype(np.uint64), c[keep], q[keep]
+
+
+@pytest.mark.parametrize("calls_only", [True, False])
+def test_multisample_batch_equals_sequential_samples(calls_only):
+    """spg_accumulate_samples (n BAMs as one column-major batch, the multi-BAM pileup layout) equals n
+    per-sample accumulates: memory (first visits by sample, dict order), calls; mixed with ordinary
+    batches before and after (batch numbering)."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import samples_to_columns
+    L = 3000
+    ref = synth.reference(L, seed=31)
+    lo, hi = 200, 2600
+    samples = [synth.pileup(L, 60, seed=3100 + s, ref=ref, snv_every=29, lo=lo, hi=hi, max_depth=50)
+               for s in range(24)]
+    samples[0] = _drop_cols(samples[0], 100, 300)        # columns first visited by sample 1 (or later)
+    samples[1] = _drop_cols(samples[1], 150, 300)
+    samples[2] = _drop_cols(samples[2], 280, 300)
+    samples[5] = _plant(samples[5], 900, 5, 35)          # IUPAC in sample 5: exact replay of the batch
+    before = synth.pileup(L, 40, seed=3050, ref=ref, snv_every=29, lo=1500, hi=L)
+    after = synth.pileup(L, 40, seed=3051, ref=ref, snv_every=29, lo=1000, hi=L)
+    pb, off, first, codes, quals = samples_to_columns(samples)
+    assert first[150] == 2 and first[290] == 3
+    eng = _engine(ref, calls_only)
+    orc = _oracle(ref)
+    eng.accumulate(*before)
+    eng.accumulate_samples(pb, off, first, codes, quals, len(samples))
+    eng.accumulate(*after)
+    for b in [before] + samples + [after]:
+        orc.accumulate(*b)
+    _check(eng, orc)
+    t = eng.table()
+    assert t["first_batch"][lo + 290] == 1 + 1 + 3       # batch 1 = `before`, samples from batch 2
+    assert t["flags"][900] & 8
+    from covid_spings_variant_caller_amd import _native as N
+    import ctypes as C
+    ns = C.c_int64()
+    fs = np.zeros(hi - lo, np.uint32)
+    N.check(eng._L.spg_history_samples(eng._h, 1, C.byref(ns), N.ptr(fs)))
+    assert ns.value == len(samples) and np.array_equal(fs, first)
+    eng.close()
+
+
+def test_multisample_device_columns_vs_oracle():
+    """The bench's config-4 layout generated in HBM (many_bams_columns), borrowed: calls and memory vs
+    the oracle fed the same column-major stream (every column's first sample is 0 here)."""
+    import torch
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.synth_device import many_bams_columns
+    L = 29903
+    ref = synth.reference(L, seed=1)
+    lo, hi = 20000, 21500
+    d = many_bams_columns(ref, 300, 100, seed=1000, lo=lo, hi=hi, max_depth=8000, device=torch.device("cuda", 0))
+    torch.cuda.synchronize()
+    first = d.first_sample.cpu().numpy()
+    assert (first == 0).all()
+    eng = PileupEngine(hi - lo, 30, 10, 5, 0.10, device=0, reference=ref[lo:hi], calls_only=True)
+    eng.accumulate_samples(0, d.offsets, d.first_sample, d.codes, d.quals, d.n_samples, borrow=True,
+                           n_entries=d.n_entries)
+    eng.finalize()
+    orc = COracle(ref[lo:hi], 30, 10, 5, 0.10)
+    orc.accumulate(0, d.offsets.cpu().numpy().view(np.uint64), d.codes[:d.n_entries].cpu().numpy(),
+                   d.quals[:d.n_entries].cpu().numpy())
+    orc.finalize()
+    assert eng.memory_summary() == orc.memory_summary()
+    compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
+    assert len(eng.variants()) >= 1
+    eng.close()
