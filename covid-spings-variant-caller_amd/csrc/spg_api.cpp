@@ -20,7 +20,7 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
 hipError_t launch_finalize(const FParams &F, const Acc *acc, const Tables *T, const Out &O, const Hist *H,
                            hipStream_t st);
 hipError_t launch_multi(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, bool nt,
-                        int64_t max_blocks, hipStream_t st);
+                        int64_t max_blocks, bool fused, hipStream_t st);
 }  // namespace spg
 
 using namespace spg;
@@ -110,6 +110,9 @@ struct spg_ctx {
     int64_t pend0 = 0;                  // history batches [pend0, size) are not accumulated yet (a run)
     uint64_t pend_entries = 0;
     uint32_t *kerr = nullptr;           // k_acc_multi error word (a batch too deep for a run)
+    uint32_t *nlist = nullptr;          // fused run: positions listed for the sparse finalize (in `band`)
+    bool stale = false;                 // records of history [0, stale_end) not written (fused run)
+    int64_t stale_end = 0;
     MState *part = nullptr;             // split-run partial states
     size_t part_bytes = 0;
     // replay index: history batches per 2^RIDX_SHIFT-position bucket
@@ -192,6 +195,7 @@ static int alloc_outputs(spg_ctx *c) {
     HIPCHK(hipMalloc(&c->ctr, 2 * sizeof(Counters)));
     HIPCHK(hipMemsetAsync(c->ctr, 0, 2 * sizeof(Counters), c->stream));
     HIPCHK(hipMalloc(&c->kerr, sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&c->nlist, sizeof(uint32_t)));
     HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));
     return 0;
 }
@@ -244,7 +248,7 @@ int spg_destroy(spg_ctx *c) {
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     c->arena.release();
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
-                    c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr};
+                    c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
@@ -263,6 +267,7 @@ int spg_destroy(spg_ctx *c) {
 int spg_reset(spg_ctx *c) {
     if (!c) return fail("spg_reset: null ctx");
     HIPCHK(hipSetDevice(c->device));
+    c->stale = false;
     // batches still pending belong to the old sample: dropped.  Copies into the recycled arena are
     // ordered after every kernel enqueued so far.
     HIPCHK(hipEventRecord(c->compute_ev, c->stream));
@@ -309,7 +314,7 @@ int spg_set_eps_lut(spg_ctx *c, const double lut[256]) {
     return 0;
 }
 
-static int flush_run(spg_ctx *c, int64_t h1 = -1);
+static int flush_run(spg_ctx *c, int64_t h1 = -1, bool fused = false);
 
 int spg_set_reference(spg_ctx *c, const char *seq, int64_t len) {
     if (!c || !seq || len < 0) return fail("spg_set_reference: bad argument");
@@ -486,7 +491,7 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch) {
 
 // Fold the pending run [pend0, size) into the records: k_acc_multi (+ k_merge_parts when split), and
 // for a single batch the long columns through k_acc_seg<1>.
-static int flush_run(spg_ctx *c, int64_t h1) {
+static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
     if (h1 < 0) h1 = (int64_t)c->hist.size();
     const int64_t h0 = c->pend0;
     if (h1 <= h0) return 0;
@@ -523,6 +528,15 @@ static int flush_run(spg_ctx *c, int64_t h1) {
     P.t_deep = K == 1 ? 128u : 0u;
     P.fresh = h0 == 0 ? 1u : 0u;
     P.err = c->kerr;
+    if (fused) {
+        if (S != 1 || h0 != 0) return fail("spg: internal: fused run must be one FRESH unsplit run");
+        P.min_td = c->p.min_total_depth;
+        P.min_ad = c->p.min_allele_depth;
+        P.ratio_lo = c->p.min_evidence_ratio * (1.0 - 1e-9);
+        P.list = c->band;
+        P.n_list = c->nlist;
+        HIPCHK(hipMemsetAsync(c->nlist, 0, sizeof(uint32_t), c->stream));
+    }
     if (S > 1) {
         const size_t need = sizeof(MState) * (size_t)S * (size_t)P.n_groups * 64;
         if (need > c->part_bytes) {
@@ -535,13 +549,40 @@ static int flush_run(spg_ctx *c, int64_t h1) {
         P.part = c->part;
     }
     static const int64_t max_blocks = env_i64("SPG_MULTI_BLOCKS", 6144);
-    HIPCHK(launch_multi(P, c->d_hist, c->ref, c->tables, c->acc, nt, max_blocks, c->stream));
+    HIPCHK(launch_multi(P, c->d_hist, c->ref, c->tables, c->acc, nt, max_blocks, fused, c->stream));
     if (int rc = trace_sync(c, "accumulate (k_acc_multi)")) return rc;
     if (K == 1) {
         // a single shallow batch: its long columns (>= 128 entries) go through the wave-wide kernel
         if (int rc = launch_seg(c, h0, false)) return rc;
     }
     return acc_end(c);
+}
+
+// A fused run at spg_finalize wrote records only for positions that could produce a call: before
+// anything reads the records again (another batch, the table, a full finalize), fold the run once more
+// with every record written.
+static int materialize(spg_ctx *c) {
+    if (!c->stale) return 0;
+    c->stale = false;
+    const int64_t keep = c->pend0;
+    c->pend0 = 0;
+    const int rc = flush_run(c, c->stale_end, false);
+    c->pend0 = keep;
+    return rc;
+}
+
+// split count of a run, as flush_run computes it
+static int64_t run_splits(const spg_ctx *c, int64_t h0, int64_t h1) {
+    int64_t u0 = INT64_MAX, u1 = INT64_MIN;
+    for (int64_t i = h0; i < h1; i++) {
+        u0 = std::min(u0, c->hist[(size_t)i].pos_begin);
+        u1 = std::max(u1, c->hist[(size_t)i].pos_begin + c->hist[(size_t)i].n_cols);
+    }
+    const int64_t K = h1 - h0, groups = (u1 - u0 + 63) / 64;
+    static const int64_t target_items = env_i64("SPG_MULTI_ITEMS", 8192);
+    int64_t S = std::min<int64_t>(K, std::max<int64_t>(1, target_items / std::max<int64_t>(1, groups)));
+    const int64_t kper = (K + S - 1) / S;
+    return (K + kper - 1) / kper;
 }
 
 static bool is_pinned(const void *p) {
@@ -556,6 +597,7 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
                      const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags,
                      bool *pageable_copy, int64_t n_samples = 1, const uint32_t *first_sample = nullptr) {
     if (n_samples < 1 || n_samples > (1 << 30)) return fail("spg_accumulate_samples: n_samples out of range");
+    if (int rc = materialize(c)) return rc;
     if (n_cols < 0 || pos_begin < 0 || pos_begin + n_cols > c->n_pos)
         return fail("spg_accumulate: column range outside the context's positions");
     if (pos_begin + n_cols > c->ref_len)
@@ -788,7 +830,21 @@ int spg_finalize(spg_ctx *c) {
 static int finalize_impl(spg_ctx *c, bool table) {
     if (!c->lut_set) return fail("spg_finalize: spg_set_eps_lut not called");
     HIPCHK(hipSetDevice(c->device));
-    if (int rc = flush_run(c)) return rc;     // the pending run of shallow batches
+    // A calls-only finalize of a sample whose every batch is still pending (one FRESH run): fold and
+    // pre-filter in one pass, finalize only the listed positions.  Otherwise: records complete, every
+    // position.
+    const int64_t nh = (int64_t)c->hist.size();
+    static const bool no_fuse = getenv("SPG_NO_FUSE") != nullptr;
+    const bool fused = !table && !no_fuse && (c->p.flags & SPG_P_CALLS_ONLY) && c->pend0 == 0 && nh > 0 &&
+                       run_splits(c, 0, nh) == 1;
+    if (fused) {
+        if (int rc = flush_run(c, -1, true)) return rc;
+        c->stale = true;
+        c->stale_end = nh;
+    } else {
+        if (int rc = materialize(c)) return rc;
+        if (int rc = flush_run(c)) return rc;     // the pending run of shallow batches
+    }
     c->cslot ^= 1u;            // this call counts in slot cslot (zeroed by the previous call / creation)
     hipEvent_t *ev = c->ev[c->ring_w % spg_ctx::NRING];
     if (!c->acc_open) {        // no accumulate since the last finalize: empty accumulate interval
@@ -802,6 +858,7 @@ static int finalize_impl(spg_ctx *c, bool table) {
     if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
     FParams F = make_fparams(c);
     F.table = table ? 1u : 0u;
+    if (fused) { F.list = c->band; F.n_list = c->nlist; }
     if (int rc = upload_ridx(c, F.ridx)) return rc;
     HIPCHK(launch_finalize(F, c->acc, c->tables, make_out(c), c->d_hist, c->stream));
     if (trace_sync(c, "finalize")) return -1;

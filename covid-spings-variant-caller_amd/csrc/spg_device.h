@@ -107,6 +107,13 @@ struct MParams {             // one k_acc_multi launch: history batches [h0, h0 
     uint32_t fresh;          // seq0 == 1: no record of this epoch exists yet
     MState *part;            // S > 1: partial records [S][n_groups * 64]
     uint32_t *err;           // bit 0: a 64-column window of a run's batch held >= 2^30 entries (not run)
+    // FUSED (a FRESH run folded at spg_finalize, calls-only): a record is written only for positions that
+    // can produce a call (prepare_variants' filters :131, :151-157) or need the exact replay; they are
+    // listed for the sparse finalize
+    int32_t min_td, min_ad;
+    double ratio_lo;         // min_evidence_ratio * (1 - 1e-9): the conservative AD/DP pre-check
+    int64_t *list;           // positions whose record was written (the sparse finalize's input)
+    uint32_t *n_list;
 };
 
 // Replay index: history batches overlapping each 2^RIDX_SHIFT-position bucket, in accumulate order.
@@ -131,6 +138,8 @@ struct FParams {
     uint32_t table;        // write the per-position SoA table (else: calls only, early exits)
     uint32_t pad_;
     RIndex ridx;
+    const int64_t *list;   // sparse finalize: only these positions (*n_list of them); null = every position
+    const uint32_t *n_list;
 };
 
 struct Out {                // SoA result table

@@ -805,8 +805,27 @@ __device__ __forceinline__ void lut_sums(uint32_t qw, uint32_t sel80, const doub
 }
 
 // MBLK: 16-B blocks per lane per load round (MBLK x 16 entries)
-template <bool NT, int MBLK>
-__global__ __launch_bounds__(64 * MW) void k_acc_multi(MParams P, const Hist *__restrict__ H,
+// prepare_variants' filters on a position's totals (:131, :151-157), a superset of the early exit
+// k_finalize takes in calls-only mode: false = the position can produce no call and needs no replay
+__device__ __forceinline__ bool may_call(const MState &c, uint8_t refc, const MParams &P) {
+    if (c.n_other) return true;                                  // exotic: exact replay
+    const uint32_t depth = c.depth;
+    if ((int64_t)depth < (int64_t)P.min_td) return false;
+    // AD / DP >= ratio, conservatively without a division: fl(n / d) >= r implies n >= d * r (1 - 2^-52),
+    // and P.ratio_lo = r (1 - 1e-9) keeps fl(d * ratio_lo) below that; the sparse finalize then applies
+    // the exact test to the listed positions
+    const double dlo = (double)depth * P.ratio_lo;
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) {
+        const uint32_t n = c.cnt[k];
+        any |= n != 0 && refc != nibble_char(slot_code(k)) && (int64_t)n >= P.min_ad && (double)n >= dlo;
+    }
+    return any;
+}
+
+template <bool NT, int MBLK, bool FUSED>
+__global__ __launch_bounds__(64 * MW) __attribute__((amdgpu_waves_per_eu(FUSED ? 2 : 3, 8))) void k_acc_multi(MParams P, const Hist *__restrict__ H,
                                                        const uint8_t *__restrict__ ref,
                                                        const Tables *__restrict__ T, Acc *__restrict__ acc) {
     // rows 0..127 {ln(1-eps), eps} for q < 128; rows 128..255 zero (the index of non-selected bytes)
@@ -820,14 +839,43 @@ __global__ __launch_bounds__(64 * MW) void k_acc_multi(MParams P, const Hist *__
     MState &S = ST[lane];
     const int64_t n_items = (int64_t)P.n_groups * P.S;
     // grid-stride over (position group, batch split) items: the LUT is loaded once per workgroup
-    for (int64_t item = (int64_t)blockIdx.x * MW + (threadIdx.x >> 6); item < n_items;
-         item += (int64_t)gridDim.x * MW) {
+    // an item's REF chars and first-batch CSR bounds (per lane), issued one item ahead: while a wave
+    // streams item i, the loads that start item i + 1 are in flight
+    const int64_t istride = (int64_t)gridDim.x * MW;
+#define SPG_ITEM_HEAD(IT)                                                                              \
+    do {                                                                                               \
+        const int64_t it_ = (IT);                                                                      \
+        rc_next = (uint8_t)'A';                                                                        \
+        ob_next = oe_next = 0;                                                                         \
+        if (it_ < n_items) {                                                                           \
+            const int32_t g_ = (int32_t)(it_ % P.n_groups), k_ = (int32_t)(it_ / P.n_groups) * P.kper;  \
+            const int64_t p_ = P.u0 + (int64_t)g_ * 64 + lane;                                          \
+            if (p_ < P.u1) {                                                                           \
+                rc_next = ref[p_];                                                                     \
+                if (k_ < P.K) {                                                                        \
+                    const Hist hn = H[P.h0 + k_];                                                      \
+                    const int64_t cn = p_ - hn.pos_begin;                                              \
+                    if (cn >= 0 && cn < hn.n_cols) {                                                   \
+                        ob_next = __builtin_nontemporal_load(hn.off + cn);                             \
+                        oe_next = __builtin_nontemporal_load(hn.off + cn + 1);                         \
+                    }                                                                                  \
+                }                                                                                      \
+            }                                                                                          \
+        }                                                                                              \
+    } while (0)
+    int64_t item = (int64_t)blockIdx.x * MW + (threadIdx.x >> 6);
+    uint8_t rc_next;
+    uint64_t ob_next, oe_next;
+    SPG_ITEM_HEAD(item);
+    for (; item < n_items; item += istride) {
         const int32_t g = (int32_t)(item % P.n_groups), s = (int32_t)(item / P.n_groups);
         const int64_t p0 = P.u0 + (int64_t)g * 64;
         const int64_t p = p0 + lane;
         const bool inr = p < P.u1;
         ms_init(S);
-        const uint8_t refc = inr ? ref[p] : (uint8_t)'A';
+        const uint8_t refc = rc_next;
+        uint64_t obn = ob_next, oen = oe_next;
+        SPG_ITEM_HEAD(item + istride);
         const uint32_t M = code_of_ref(refc), mrep = M * 0x01010101u;
         const int Ms = slot_of(M);
         // calls-only: no likelihood sums for a REF-char major (never a candidate)
@@ -843,14 +891,7 @@ __global__ __launch_bounds__(64 * MW) void k_acc_multi(MParams P, const Hist *__
         bool deep = false;
         uint32_t sidx = 0;                             // raw entries of this position in earlier batches
         const int32_t k0 = s * P.kper, k1 = min(P.K, k0 + P.kper);
-        // batch k's descriptor and this lane's CSR bounds, loaded one batch ahead so the next batch's
-        // offsets are in flight while this one streams
-        uint64_t obn = 0, oen = 0;
-        if (k0 < k1) {
-            const Hist hn = H[P.h0 + k0];
-            const int64_t cn = p - hn.pos_begin;
-            if (inr && cn >= 0 && cn < hn.n_cols) { obn = hn.off[cn]; oen = hn.off[cn + 1]; }
-        }
+        // later batches' CSR bounds are loaded one batch ahead as well
         for (int32_t k = k0; k < k1; k++) {
             const Hist h = H[P.h0 + k];
             const uint64_t ob = obn, oe = oen;
@@ -978,6 +1019,20 @@ __global__ __launch_bounds__(64 * MW) void k_acc_multi(MParams P, const Hist *__
         // one run: assemble the record in the lane's own LDS slot, then store the wave's records
         // with 16-B pieces (ten lanes per record)
         uint32_t fl = 0;
+        if constexpr (FUSED) {
+            // most positions cannot produce a call: no record, no listing (the context re-materializes
+            // the records from the history if anything needs them later); deep columns: k_acc_seg writes
+            // their records, listed here
+            const bool want = inr && (deep || (S.fb != INF32 && may_call(S, refc, P)));
+            const uint64_t wm = __ballot(want);
+            if (!wm) continue;
+            uint32_t at = 0;                               // one list slot reservation per wave
+            if (lane == 0) at = atomicAdd(P.n_list, (uint32_t)__popcll(wm));
+            at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
+            if (want)
+                P.list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u))] = p;
+            if (!want) S.fb = INF32;
+        }
         if (inr && !deep && S.fb != INF32) {
             const MState c = S;
             Acc a;
@@ -997,6 +1052,7 @@ __global__ __launch_bounds__(64 * MW) void k_acc_multi(MParams P, const Hist *__
         }
         wave_sync();
     }
+#undef SPG_ITEM_HEAD
 }
 
 // Fold the S partial states of a split run in batch order (first-entry keys (split, stream index)) and
@@ -1376,6 +1432,7 @@ __device__ __forceinline__ bool finalize_position(const FParams &F, const Acc *_
 
 // One wave per 64 positions: each lane runs prepare_variants' per-position logic; positions that need
 // the exact replay are then replayed one after another by the whole wave.
+template <bool SPARSE>
 __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restrict__ acc,
                                                   const Tables *__restrict__ T, const Hist *__restrict__ H, Out O) {
     __shared__ double sink[64][NSLOT];
@@ -1383,6 +1440,32 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
     __shared__ ReplayWs ws;
     const int lane = threadIdx.x & 63;
     if (blockIdx.x == 0 && threadIdx.x == 0) O.ctr[F.cslot ^ 1u] = Counters{0, 0, 0, 0};   // next call's slot
+    if constexpr (SPARSE) {
+        // sparse finalize: the positions the fused accumulate listed, 64 per wave iteration
+        const int64_t n = (int64_t)*F.n_list;
+        bool eps_loaded = false;
+        for (int64_t i0 = (int64_t)blockIdx.x * 64; i0 < n; i0 += (int64_t)gridDim.x * 64) {
+            const int64_t i = i0 + lane;
+            const int64_t pos = i < n ? F.list[i] : 0;
+            const bool need = i < n && finalize_position(F, acc, T, O, pos, sink[lane]);
+            uint64_t rb = __ballot(need);
+            if (rb == 0) continue;
+            if (need) atomicAdd(&O.ctr[F.cslot].n_band, 1u);
+            if (!eps_loaded) {
+                for (int q = lane; q < 256; q += 64) eps_s[q] = T->eps[q];
+                wave_sync();
+                eps_loaded = true;
+            }
+            while (rb) {
+                const int j = (int)__builtin_ctzll(rb);
+                rb &= rb - 1;
+                const int64_t pj = (int64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)pos, j) |
+                                   ((int64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)((uint64_t)pos >> 32), j) << 32);
+                replay_wave(F, H, acc, O, pj, &ws, eps_s);
+            }
+        }
+        return;
+    }
     const int64_t pos = (int64_t)blockIdx.x * 64 + lane;
     const bool need = pos < F.n_pos && finalize_position(F, acc, T, O, pos, sink[lane]);
     uint64_t rb = __ballot(need);
@@ -1424,7 +1507,7 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
 
 // k_acc_multi over a run of shallow batches (+ k_merge_parts when the run is split)
 hipError_t launch_multi(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, bool nt,
-                        int64_t max_blocks, hipStream_t st) {
+                        int64_t max_blocks, bool fused, hipStream_t st) {
     const int64_t items = (int64_t)P.n_groups * P.S;
     if (items == 0) return hipSuccess;
     const int64_t blocks = std::min<int64_t>((items + MW - 1) / MW, max_blocks);
@@ -1432,9 +1515,9 @@ hipError_t launch_multi(const MParams &P, const Hist *H, const uint8_t *ref, con
     // neighbours', so one cache line serves several consecutive load instructions of the wave and must
     // stay in L2 until they have all read it (non-temporal loads re-fetched such lines: 1.7x HBM bytes)
     (void)nt;
-    static const int mblk = [] { const char *e = getenv("SPG_MBLK"); return e ? atoi(e) : 4; }();
-    if (mblk == 4) hipLaunchKernelGGL((k_acc_multi<false, 4>), dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
-    else hipLaunchKernelGGL((k_acc_multi<false, 8>), dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
+    // (8 blocks per round measured slower: 5.2 vs 4.5 ms per 2,000 BAMs, its registers cost occupancy)
+    if (fused) hipLaunchKernelGGL((k_acc_multi<false, 4, true>), dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
+    else hipLaunchKernelGGL((k_acc_multi<false, 4, false>), dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
     if (P.S > 1) {
         const int64_t mb = (P.u1 - P.u0 + 255) / 256;
         hipLaunchKernelGGL(k_merge_parts, dim3((unsigned)mb), dim3(256), 0, st, P, ref, acc);
@@ -1444,8 +1527,11 @@ hipError_t launch_multi(const MParams &P, const Hist *H, const uint8_t *ref, con
 
 hipError_t launch_finalize(const FParams &F, const Acc *acc, const Tables *T, const Out &O, const Hist *H,
                            hipStream_t st) {
-    const int64_t blocks = (F.n_pos + 63) / 64;      // 64-thread blocks: one wave
-    hipLaunchKernelGGL(k_finalize, dim3((unsigned)blocks), dim3(64), 0, st, F, acc, T, H, O);
+    // 64-thread blocks (one wave), one position per lane; the sparse form strides over the list (its
+    // length is on the device)
+    const int64_t blocks = F.list ? std::min<int64_t>((F.n_pos + 63) / 64, 8192) : (F.n_pos + 63) / 64;
+    if (F.list) hipLaunchKernelGGL(k_finalize<true>, dim3((unsigned)blocks), dim3(64), 0, st, F, acc, T, H, O);
+    else hipLaunchKernelGGL(k_finalize<false>, dim3((unsigned)blocks), dim3(64), 0, st, F, acc, T, H, O);
     return hipGetLastError();
 }
 

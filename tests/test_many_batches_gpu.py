@@ -283,3 +283,41 @@ def test_multisample_device_columns_vs_oracle():
     compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
     assert len(eng.variants()) >= 1
     eng.close()
+
+
+def test_fused_fresh_run_then_more_batches_and_table():
+    """A calls-only finalize of one FRESH run (chr1-like: wide range, unsplit) writes records only for
+    positions that can produce a call and finalizes just those; the context re-materializes every
+    record before it reads them again (another batch, the per-position table, memory)."""
+    from covid_spings_variant_caller_amd import synth
+    L = 400_000
+    ref = synth.reference(L, seed=91)
+    b1 = synth.pileup(L, 30, seed=92, ref=ref, snv_every=997, lo=0, hi=L)
+    b1 = _plant(b1, 123_456, 5, 35)                 # an IUPAC entry: exotic, replayed
+    b2 = synth.pileup(L, 20, seed=93, ref=ref, snv_every=501, lo=50_000, hi=350_000)
+    eng = _engine(ref, True)
+    orc = _oracle(ref)
+    eng.accumulate(*b1)
+    orc.accumulate(*b1)
+    eng.finalize()
+    orc.finalize()
+    compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
+    assert eng.counts()[1] >= 1                     # the exotic position went through the replay
+    eng.accumulate(*b2)                             # records re-materialized first
+    orc.accumulate(*b2)
+    eng.finalize()
+    orc.finalize()
+    compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
+    got = eng.table()                               # full table: every record present
+    m = orc.memory_arrays()
+    pos = m["pos"].astype(np.int64)
+    np.testing.assert_array_equal(got["depth"][pos].astype(np.uint64), m["depth"])
+    assert (got["flags"][pos] & 1).all()
+    eng.reset()                                     # and a fused step again on a fresh sample
+    eng.accumulate(*b2)
+    eng.finalize()
+    orc2 = _oracle(ref)
+    orc2.accumulate(*b2)
+    orc2.finalize()
+    compare_variants(eng.variants(), orc2.variants(), rtol=RTOL)
+    eng.close()
