@@ -162,6 +162,7 @@ def pileup_lib():
     _sig(L.spp_target, C.c_int, vp, i32, C.POINTER(C.c_char_p), C.POINTER(i64))
     _sig(L.spp_target_id, C.c_int, vp, C.c_char_p, C.POINTER(i32))
     _sig(L.spp_pileup, C.c_int, vp, i32, C.POINTER(SppParams), C.POINTER(vp))
+    _sig(L.spp_pileup_region, C.c_int, vp, i32, i64, i64, C.POINTER(SppParams), C.POINTER(vp))
     _sig(L.spp_batch_info, C.c_int, vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(C.c_uint64),
          C.POINTER(i64), C.POINTER(i64))
     _sig(L.spp_batch_arrays, C.c_int, vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp))

@@ -84,7 +84,11 @@ struct Reads {                 // one contig's reads, structure of arrays
     Vec<uint64_t> cig_off, name_off;
     Vec<uint32_t> n_cig, l_seq;
     Vec<uint32_t> cigar;
-    Vec<uint8_t *> bases;     // per read: l_seq nibble codes, then l_seq qualities (in `arena`)
+    Vec<uint8_t *> bases;     // per read: l_seq nibble codes, then l_seq qualities (in `arena`);
+                              // null for reads outside the decode window (spp_pileup_region)
+    int64_t dlo = INT64_MIN, dhi = INT64_MAX;   // decode window: reads overlapping it keep bases
+    int64_t max_span = 0;                       // longest reference span of any read of the contig
+    bool decode(int64_t pos, int64_t end) const { return end > dlo && pos < dhi; }
     Vec<char> names;
     // bases storage: 2 MiB-aligned blocks (transparent huge pages requested), never moved, so the
     // decoders can fill a window's records in parallel without a serial grow-and-copy
@@ -400,16 +404,33 @@ void read_bam(const spp_file *f, int32_t tid, const spp_params &p, Reads &R) {
             R.cig_off.resize(n0 + k); R.n_cig.resize(n0 + k); R.name_off.resize(n0 + k);
             R.bases.resize(n0 + k); R.l_seq.resize(n0 + k);
             size_t co = R.cigar.size(), so = 0, no = R.names.size();
+            std::vector<uint8_t> dec(k, 1);
             for (size_t i = 0; i < k; i++) {
                 const uint8_t *b = recs[i];
                 const uint32_t n_cig = rdu16(b + 12), l_seq = (uint32_t)rd32(b + 16), l_name = b[8];
                 R.cig_off[n0 + i] = co; R.n_cig[n0 + i] = n_cig; co += n_cig;
-                R.l_seq[n0 + i] = l_seq; so += 2 * (size_t)l_seq;
+                R.l_seq[n0 + i] = l_seq;
                 R.name_off[n0 + i] = no; no += (l_name ? l_name - 1u : 0u) + 1u;
+                if (R.dlo != INT64_MIN || R.dhi != INT64_MAX) {   // region: bases of the window's reads only
+                    uint32_t cg[64];
+                    int64_t span = 0;
+                    for (uint32_t c0 = 0; c0 < n_cig; c0 += 64) {
+                        const uint32_t m = std::min<uint32_t>(64, n_cig - c0);
+                        memcpy(cg, b + 32 + l_name + 4u * c0, 4u * m);
+                        span += ref_len(cg, m);
+                    }
+                    const int64_t pos = rd32(b + 4);
+                    R.max_span = std::max(R.max_span, span);
+                    dec[i] = R.decode(pos, pos + span) ? 1 : 0;
+                }
+                if (dec[i]) so += 2 * (size_t)l_seq;
             }
             R.cigar.resize(co); R.names.resize(no);
-            uint8_t *bp = R.arena.alloc(so);
-            for (size_t i = 0; i < k; i++) { R.bases[n0 + i] = bp; bp += 2 * (size_t)R.l_seq[n0 + i]; }
+            uint8_t *bp = so ? R.arena.alloc(so) : nullptr;
+            for (size_t i = 0; i < k; i++) {
+                R.bases[n0 + i] = dec[i] ? bp : nullptr;
+                if (dec[i]) bp += 2 * (size_t)R.l_seq[n0 + i];
+            }
             auto work = [&](size_t i0, size_t i1) {
                 for (size_t i = i0; i < i1; i++) {
                     const uint8_t *b = recs[i];
@@ -429,6 +450,7 @@ void read_bam(const spp_file *f, int32_t tid, const spp_params &p, Reads &R) {
                     uint32_t *cg = R.cigar.data() + R.cig_off[r];
                     memcpy(cg, name + l_name, 4u * n_cig);
                     R.end[r] = R.pos[r] + ref_len(cg, n_cig);
+                    if (!R.bases[r]) continue;                  // outside the decode window
                     const uint8_t *sq = name + l_name + 4u * n_cig;
                     const uint8_t *ql = sq + (l_seq + 1) / 2;
                     uint8_t *dst = R.seq(r);
@@ -534,6 +556,8 @@ void read_sam(const spp_file *f, int32_t tid, const spp_params &p, Reads &R) {
         const bool noseq = len[9] == 1 && fld[9][0] == '*';
         const uint32_t l_seq = noseq ? 0u : (uint32_t)len[9];
         R.l_seq.push_back(l_seq);
+        R.max_span = std::max(R.max_span, R.end.back() - pos);
+        if (!R.decode(pos, R.end.back())) { R.bases.push_back(nullptr); return true; }
         uint8_t *bp = R.arena.alloc(2 * (size_t)l_seq);
         R.bases.push_back(bp);
         for (uint32_t i = 0; i < l_seq; i++) bp[i] = NT16.t[(uint8_t)fld[9][i]];
@@ -684,9 +708,13 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
                         if (R.mpos[r] >= R.pos[r] || ((fl & F_PAIRED) && R.mpos[r] == -1)) olap.emplace(nm, r);
                     } else {
                         const size_t a = itr->second;
-                        T.orig.emplace(a, std::vector<uint8_t>(R.qual(a), R.qual(a) + R.l_seq[a]));
-                        T.col[a] = it_pos;
-                        tweak_overlap(R, a, r);
+                        // region pileups decode the reads within a read span of the region: a pair with
+                        // an undecoded mate shares no aligned base with the region's reads
+                        if (R.bases[a] && R.bases[r]) {
+                            T.orig.emplace(a, std::vector<uint8_t>(R.qual(a), R.qual(a) + R.l_seq[a]));
+                            T.col[a] = it_pos;
+                            tweak_overlap(R, a, r);
+                        }
                         olap.erase(itr);
                     }
                 }
@@ -701,17 +729,22 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
     return keep;
 }
 
-void fill_csr(const Reads &R, const std::vector<uint8_t> &keep, const Tweaks &T, spp_batch *B, int threads) {
+void fill_csr(const Reads &R, const std::vector<uint8_t> &keep, const Tweaks &T, spp_batch *B, int threads,
+              int64_t rlo = INT64_MIN, int64_t rhi = INT64_MAX) {
     int64_t lo = INT64_MAX, hi = INT64_MIN;
+    auto inreg = [&](size_t r) { return keep[r] && R.end[r] > R.pos[r] && R.end[r] > rlo && R.pos[r] < rhi; };
     for (size_t r = 0; r < R.size(); r++)
-        if (keep[r] && R.end[r] > R.pos[r]) { lo = std::min(lo, R.pos[r]); hi = std::max(hi, R.end[r]); }
+        if (inreg(r)) { lo = std::min(lo, std::max(R.pos[r], rlo)); hi = std::max(hi, std::min(R.end[r], rhi)); }
     if (lo == INT64_MAX) { lo = 0; hi = 0; }
     const int64_t C = hi - lo;
     B->pos_begin = lo;
     B->n_cols = C;
     std::vector<int64_t> diff((size_t)C + 1, 0);
     for (size_t r = 0; r < R.size(); r++)
-        if (keep[r] && R.end[r] > R.pos[r]) { diff[(size_t)(R.pos[r] - lo)]++; diff[(size_t)(R.end[r] - lo)]--; }
+        if (inreg(r)) {
+            diff[(size_t)(std::max(R.pos[r], lo) - lo)]++;
+            diff[(size_t)(std::min(R.end[r], hi) - lo)]--;
+        }
     B->off.assign((size_t)C + 1, 0);
     int64_t run = 0;
     for (int64_t c = 0; c < C; c++) {
@@ -729,7 +762,7 @@ void fill_csr(const Reads &R, const std::vector<uint8_t> &keep, const Tweaks &T,
     // them in read order, so each column's entries keep htslib's order.
     std::vector<size_t> kept;
     for (size_t r = 0; r < R.size(); r++)
-        if (keep[r] && R.end[r] > R.pos[r]) kept.push_back(r);
+        if (inreg(r)) kept.push_back(r);
     const int nt = std::max(1, std::min(threads, 64));
     auto work = [&](int t) {
         const int64_t c0 = C * t / nt, c1 = C * (t + 1) / nt;
@@ -919,27 +952,44 @@ int spp_target_id(spp_file *f, const char *name, int32_t *tid) {
     return 0;
 }
 
-int spp_pileup(spp_file *f, int32_t tid, const spp_params *p, spp_batch **out) {
+static int pileup_impl(spp_file *f, int32_t tid, const spp_params *p, int64_t lo, int64_t hi, spp_batch **out) {
     if (!f || !p || !out) return fail("spp_pileup: null argument");
     if (tid < 0 || (size_t)tid >= f->targets.size()) return fail("spp_pileup: tid out of range");
+    if (lo >= hi) return fail("spp_pileup_region: empty region");
     *out = nullptr;
     try {
-        Reads R;
-        if (f->bam) read_bam(f, tid, *p, R);
-        else read_sam(f, tid, *p, R);
-        Tweaks T;
-        const std::vector<uint8_t> keep = simulate(R, *p, tid, T);
-        auto *B = new spp_batch();
-        int64_t used = 0;
-        for (uint8_t k : keep) used += k;
-        B->n_used = used;
-        B->n_dropped = (int64_t)R.size() - used;
-        fill_csr(R, keep, T, B, std::max(1, p->n_threads));
-        *out = B;
-        return 0;
+        const bool region = lo != INT64_MIN || hi != INT64_MAX;
+        // region: bases of reads within a read span of [lo, hi) (mates that can overlap a region read);
+        // the span bound is checked against the longest read and the pass redone if it was too short
+        int64_t pad = 16384;
+        for (;;) {
+            Reads R;
+            if (region) { R.dlo = lo == INT64_MIN ? lo : lo - pad; R.dhi = hi == INT64_MAX ? hi : hi + pad; }
+            if (f->bam) read_bam(f, tid, *p, R);
+            else read_sam(f, tid, *p, R);
+            if (region && R.max_span > pad) { pad = 2 * R.max_span; continue; }
+            Tweaks T;
+            const std::vector<uint8_t> keep = simulate(R, *p, tid, T);   // every read: exact depth cap
+            auto *B = new spp_batch();
+            int64_t used = 0;
+            for (uint8_t k : keep) used += k;
+            B->n_used = used;
+            B->n_dropped = (int64_t)R.size() - used;
+            fill_csr(R, keep, T, B, std::max(1, p->n_threads), lo, hi);
+            *out = B;
+            return 0;
+        }
     } catch (const std::exception &e) {
         return fail(std::string("spp_pileup: ") + e.what());
     }
+}
+
+int spp_pileup(spp_file *f, int32_t tid, const spp_params *p, spp_batch **out) {
+    return pileup_impl(f, tid, p, INT64_MIN, INT64_MAX, out);
+}
+
+int spp_pileup_region(spp_file *f, int32_t tid, int64_t lo, int64_t hi, const spp_params *p, spp_batch **out) {
+    return pileup_impl(f, tid, p, lo, hi, out);
 }
 
 int spp_batch_info(spp_batch *b, int64_t *pos_begin, int64_t *n_cols, uint64_t *n_entries, int64_t *n_reads_used,

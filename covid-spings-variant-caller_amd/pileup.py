@@ -96,12 +96,21 @@ class AlignmentFile:
     def get_reference_length(self, reference: str) -> int:
         return self.lengths[self.references.index(reference)]
 
-    def pileup_batch(self, reference: str, params: PileupParams | None = None) -> PileupBatch:
+    def pileup_batch(self, reference: str, params: PileupParams | None = None, start: int | None = None,
+                     stop: int | None = None) -> PileupBatch:
+        """The contig's pileup as one CSR batch; with start/stop only the columns [start, stop) (a
+        coordinate shard: spp_pileup_region, identical to slicing the whole-contig batch)."""
         L = N.pileup_lib()
         tid = C.c_int32()
         N.pcheck(L.spp_target_id(self._h, reference.encode(), C.byref(tid)), "pileup")
         b = C.c_void_p()
-        N.pcheck(L.spp_pileup(self._h, tid.value, C.byref((params or PileupParams()).native()), C.byref(b)), "pileup")
+        prm = (params or PileupParams()).native()
+        if start is None and stop is None:
+            N.pcheck(L.spp_pileup(self._h, tid.value, C.byref(prm), C.byref(b)), "pileup")
+        else:
+            lo = -(1 << 62) if start is None else int(start)
+            hi = (1 << 62) if stop is None else int(stop)
+            N.pcheck(L.spp_pileup_region(self._h, tid.value, lo, hi, C.byref(prm), C.byref(b)), "pileup")
         return PileupBatch(b.value)
 
     def close(self):

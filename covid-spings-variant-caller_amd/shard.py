@@ -118,6 +118,19 @@ class ShardedEngine:
             self.engine.accumulate(pb - self.lo, off, c, q)
             self._global_seq.append(self.n_batches)
 
+    def process_bam(self, path: str, contig: str, params=None):
+        """process_bam (live_variant_caller.py:54-72) for this rank's range only: the host pileup builds
+        just the [lo, hi) columns (spp_pileup_region; the depth cap still sees every read), so each
+        rank inflates the BAM but decodes and flattens only its shard."""
+        from .pileup import AlignmentFile
+        self.n_batches += 1
+        with AlignmentFile(path) as f:
+            b = f.pileup_batch(contig, params, start=self.lo, stop=self.hi)
+            if b.n_cols and b.n_entries:
+                self.engine.accumulate(b.pos_begin - self.lo, b.offsets, b.codes, b.quals)
+                self._global_seq.append(self.n_batches)
+            b.close()
+
     def local_candidates(self) -> np.ndarray:
         self.engine.finalize()
         c = self.engine.candidates()

@@ -61,6 +61,11 @@ int spp_target_id(spp_file *f, const char *name, int32_t *tid);
 /* AlignmentFile.pileup(reference=<contig tid>, ...) over the whole contig -> one CSR batch.
  * The batch covers columns [pos_begin, pos_begin + n_cols) (first..last emitted column). */
 int spp_pileup(spp_file *f, int32_t tid, const spp_params *p, spp_batch **out);
+/* The columns [lo, hi) of spp_pileup's batch (bit-identical to slicing it), for a coordinate shard
+ * (SURVEY §8 e): every read's fixed fields are parsed (htslib's depth cap depends on all pushes), but
+ * bases and qualities are decoded only for reads within a read span of the region, and the CSR
+ * holds only the region's columns. */
+int spp_pileup_region(spp_file *f, int32_t tid, int64_t lo, int64_t hi, const spp_params *p, spp_batch **out);
 int spp_batch_info(spp_batch *b, int64_t *pos_begin, int64_t *n_cols, uint64_t *n_entries,
                    int64_t *n_reads_used, int64_t *n_reads_dropped);
 /* Arrays owned by the batch (valid until spp_batch_free).  base_code and qual are allocated

@@ -191,3 +191,41 @@ def test_bam_window_boundaries(tmp_path, monkeypatch):
         monkeypatch.setenv("SPP_BGZF_WINDOW", window)
         assert_same(product(bam, "c"), want)
         assert_same(product(bam, "c", n_threads=1), want)
+
+
+def _slice(b, lo, hi):
+    """Columns [lo, hi) of a whole-contig batch (the reference a region pileup must equal)."""
+    pb, off, c, q = b
+    c0, c1 = max(0, lo - pb), max(0, min(len(off) - 1, hi - pb))
+    if c1 <= c0:
+        return None
+    # trim empty edge columns the way the region pileup reports its range (first / last covered column)
+    lens = np.diff(off[c0:c1 + 1].astype(np.int64))
+    nz = np.nonzero(lens)[0]
+    if len(nz) == 0:
+        return None
+    c0, c1 = c0 + int(nz[0]), c0 + int(nz[-1]) + 1
+    e0, e1 = int(off[c0]), int(off[c1])
+    return pb + c0, off[c0:c1 + 1] - off[c0], c[e0:e1], q[e0:e1]
+
+
+@pytest.mark.parametrize("fmt", ["sam", "bam"])
+@pytest.mark.parametrize("kw", [dict(), dict(max_depth=4), dict(max_depth=2, ignore_overlaps=False)])
+def test_region_pileup_equals_whole_contig_slice(tmp_path, fmt, kw):
+    """spp_pileup_region(lo, hi) == the [lo, hi) columns of spp_pileup (depth cap decided over every
+    read, mate-overlap tweaks with mates decoded around the region), for shard cuts anywhere."""
+    contigs = [("chrA", 900), ("chrB", 900)]
+    recs = samgen.random_records(11, contigs, n_reads=700)
+    path = str(tmp_path / f"r.{fmt}")
+    (samgen.write_sam if fmt == "sam" else samgen.write_bam)(path, contigs, recs)
+    for contig in ("chrA", "chrB"):
+        whole = product(path, contig, **kw)
+        for lo, hi in ((0, 900), (0, 300), (300, 301), (301, 650), (650, 900), (123, 777)):
+            with AlignmentFile(path) as f:
+                b = f.pileup_batch(contig, PileupParams(n_threads=3, **kw), start=lo, stop=hi)
+                got = (b.pos_begin, b.offsets.copy(), b.codes.copy(), b.quals.copy())
+            exp = _slice(whole, lo, hi)
+            if exp is None:
+                assert len(got[1]) == 1 or int(got[1][-1]) == 0
+            else:
+                assert_same(got, exp)
