@@ -321,3 +321,55 @@ def test_fused_fresh_run_then_more_batches_and_table():
     orc2.finalize()
     compare_variants(eng.variants(), orc2.variants(), rtol=RTOL)
     eng.close()
+
+
+def test_chr1_30x_full_size_count_conservation():
+    """BASELINE config 5 at full size (chr1, L = 248,956,422, 30x: E = 7.5e9 > 2^32 entries, generated in
+    HBM): a calls-only finalize of the FRESH run (fused path) then the per-position table (records
+    re-materialized): every entry with q >= minBaseQuality lands in exactly one position's totalDepth
+    and one allele / D / N bucket (process_pileup_column :75-101), so depths equal direct per-column
+    counts of the CSR and per-code totals equal direct counts."""
+    import ctypes as C
+    import torch
+    from covid_spings_variant_caller_amd import _native as N, synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.synth_device import many_bams_columns
+    L = 248_956_422
+    ref = synth.reference(L, seed=1)
+    dev = torch.device("cuda", 0)
+    d = many_bams_columns(ref, 1, 30.0, seed=7, device=dev)
+    E = d.n_entries
+    assert E > (1 << 32)
+    eng = PileupEngine(L, 30, 10, 5, 0.10, device=0, reference=ref, calls_only=True)
+    eng.accumulate(0, d.offsets, d.codes, d.quals, borrow=True, n_entries=E)
+    eng.finalize()
+    n_calls = eng.counts()[0]
+    assert n_calls > 10_000
+    codes_tot = torch.zeros(32, dtype=torch.int64, device=dev)
+    got_tot = np.zeros(8, np.int64)
+    off_h = d.offsets.cpu().numpy()
+    step = 1 << 25
+    depth = np.zeros(step, np.uint32)
+    counts = np.zeros((step, 8), np.uint32)
+    for c0 in range(0, L, step):
+        c1 = min(L, c0 + step)
+        e0, e1 = int(off_h[c0]), int(off_h[c1])
+        keep = d.quals[e0:e1] >= 30
+        cs = torch.zeros(e1 - e0 + 1, dtype=torch.int64, device=dev)
+        cs[1:] = torch.cumsum(keep, 0)
+        o = d.offsets[c0:c1 + 1] - e0
+        want = (cs[o[1:]] - cs[o[:-1]]).cpu().numpy()
+        codes_tot += torch.bincount(d.codes[e0:e1][keep].long(), minlength=32)
+        n = c1 - c0
+        N.check(eng._L.spg_get_table(eng._h, c0, n, N.ptr(depth), N.ptr(counts), None, None, None, None), "table")
+        np.testing.assert_array_equal(depth[:n].astype(np.int64), want)
+        got_tot += counts[:n].astype(np.int64).sum(axis=0)
+        del keep, cs
+    want_codes = codes_tot.cpu().numpy()
+    assert [int(x) for x in got_tot[:5]] == [int(want_codes[k]) for k in (1, 2, 4, 8, 15)]
+    assert int(got_tot[5]) == int(want_codes[16]) and int(got_tot[6]) == int(want_codes[17])
+    eng.finalize()                                  # the full finalize agrees with the fused one
+    assert eng.counts()[0] == n_calls
+    eng.close()
+    del d
+    torch.cuda.empty_cache()
