@@ -8,10 +8,10 @@ mkdir -p $OUT
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
-    python3 $ROOT/bench.py --steps 50 --warmup 5 --no-cpu-baseline > $OUT/trace.log 2>&1
+    python3 $ROOT/bench.py --steps 50 --warmup 5 --reps 3 --no-cpu-baseline --no-parity --many-batches 0 --no-e2e > $OUT/trace.log 2>&1
 i=0
 for pass in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $pass -d $OUT/pmc$i -o run --output-format csv -- \
-      python3 $ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/pmc$i.log 2>&1
+      python3 $ROOT/bench.py --steps 10 --warmup 2 --reps 2 --min-ms 5 --no-cpu-baseline --no-parity --many-batches 0 --no-e2e > $OUT/pmc$i.log 2>&1
 done
