@@ -120,7 +120,7 @@ def measure(D, step, eng, K_min, reps, min_ms, every):
     est = D.max((time.perf_counter() - t0) / 3)
     K = max(K_min, int(math.ceil(min_ms * 1e-3 / max(est, 1e-7))))
     eng.kernel_times(4096)
-    times, acc = [], []
+    times, acc, enq = [], [], []
     for _ in range(reps):
         eng.set_timing(0)
         torch.cuda.synchronize()
@@ -130,12 +130,14 @@ def measure(D, step, eng, K_min, reps, min_ms, every):
         for k in range(K):
             eng.set_timing(1 if k % every == 0 else 0)
             step(k)
+        enq.append(time.perf_counter() - t0)       # host time to enqueue the K steps
         eng.sync()
         torch.cuda.synchronize()
         D.barrier()
         times.append(D.max(time.perf_counter() - t0))
         a, _ = eng.kernel_times(4096)
         acc.extend(a[a > 0].tolist())
+    measure.host_enqueue_ms_per_step = float(np.median(enq)) / K * 1e3
     return K, np.array(times), np.array(acc)
 
 
@@ -281,6 +283,7 @@ def run_point(args, D, L, depth, max_depth, local, world, rank, contig):
         "kernel_ms": t_acc * 1e3, "kernel_ms_median": float(np.median(acc)) if len(acc) else None,
         "kernel_samples": int(len(acc)), "algo_bytes": algo_bytes, "achieved": algo_bytes / t_acc,
         "finalize_ms": fin, "n_cand": n_cand, "n_replay": n_replay, "gathered": gathered,
+        "host_enqueue_ms_per_step": measure.host_enqueue_ms_per_step,
     }
 
 
@@ -529,7 +532,8 @@ def main():
                      "kernel": kernel_name(E, C), "kernel_ms": main_pt["kernel_ms"],
                      "kernel_ms_median": main_pt["kernel_ms_median"], "kernel_samples": main_pt["kernel_samples"],
                      "algorithmic_bytes": main_pt["algo_bytes"]},
-        "finalize_ms": main_pt["finalize_ms"], "candidates_per_gpu_step": main_pt["n_cand"],
+        "finalize_ms": main_pt["finalize_ms"], "host_enqueue_ms_per_step": main_pt["host_enqueue_ms_per_step"],
+        "candidates_per_gpu_step": main_pt["n_cand"],
         "replayed_positions_per_gpu_step": main_pt["n_replay"], "datagen_s": main_pt["t_gen"],
         "calls_gathered_per_step": main_pt["gathered"] if main_pt["gathered"] is not None else main_pt["n_cand"],
     }

@@ -96,6 +96,9 @@ struct spg_ctx {
     hipEvent_t copy_ev = nullptr;       // after the latest batch copy
     hipEvent_t compute_ev = nullptr;    // reset fence: recycled arena copies wait for the old kernels
     bool copy_pending = false;          // the compute stream has not waited on copy_ev yet
+    bool arena_fence = false;           // the arena was recycled: the next copy into it waits for the kernels
+                                        // enqueued before the reset (recorded lazily: an event record per
+                                        // step idled the GPU between steps)
     Acc *acc = nullptr;
     Tables *tables = nullptr;
     bool lut_set = false;
@@ -112,6 +115,9 @@ struct spg_ctx {
     uint32_t *kerr = nullptr;           // k_acc_multi error word (a batch too deep for a run)
     uint32_t *nlist = nullptr;          // fused run: positions listed for the sparse finalize (in `band`)
     bool stale = false;                 // records of history [0, stale_end) not written (fused run)
+    bool deep_pend = false;             // history batch 0 is a deep batch not accumulated yet: a calls-only
+                                        // finalize runs it fused (k_acc_seg<..., FUSE>), anything else first
+                                        // accumulates it on its own
     int64_t stale_end = 0;
     MState *part = nullptr;             // split-run partial states
     size_t part_bytes = 0;
@@ -137,6 +143,9 @@ struct spg_ctx {
     spg_detail *detail = nullptr;
     int64_t detail_cap = 0;
     Counters *ctr = nullptr;
+    FusedArgs *d_fused = nullptr;       // the fused accumulate's finalize parameters [2 slots] (device) ...
+    FusedArgs *h_fused = nullptr;       // ... and their pinned staging copy (re-uploaded when they change)
+    bool fused_valid = false;
     bool finalized = false;
     // timing ring: one entry per finalize; events around the accumulate launches (first begin ..
     // last end) and around the finalize launch.  Read back without stalling the pipeline.
@@ -193,6 +202,9 @@ static int alloc_outputs(spg_ctx *c) {
     c->detail_cap = std::max<int64_t>(1024, std::min<int64_t>(n + 1, 65536));
     HIPCHK(hipMalloc(&c->detail, sizeof(spg_detail) * c->detail_cap));
     HIPCHK(hipMalloc(&c->ctr, 2 * sizeof(Counters)));
+    HIPCHK(hipMalloc(&c->d_fused, 2 * sizeof(FusedArgs)));
+    HIPCHK(hipHostMalloc((void **)&c->h_fused, 2 * sizeof(FusedArgs), hipHostMallocDefault));
+    memset(c->h_fused, 0, 2 * sizeof(FusedArgs));
     HIPCHK(hipMemsetAsync(c->ctr, 0, 2 * sizeof(Counters), c->stream));
     HIPCHK(hipMalloc(&c->kerr, sizeof(uint32_t)));
     HIPCHK(hipMalloc(&c->nlist, sizeof(uint32_t)));
@@ -248,11 +260,13 @@ int spg_destroy(spg_ctx *c) {
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     c->arena.release();
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
-                    c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist};
+                    c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
+                    c->d_fused};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
     if (c->h_ridx) (void)hipHostFree(c->h_ridx);
+    if (c->h_fused) (void)hipHostFree(c->h_fused);
     for (auto &row : c->ev)
         for (auto &e : row)
             if (e) (void)hipEventDestroy(e);
@@ -268,10 +282,10 @@ int spg_reset(spg_ctx *c) {
     if (!c) return fail("spg_reset: null ctx");
     HIPCHK(hipSetDevice(c->device));
     c->stale = false;
+    c->deep_pend = false;
     // batches still pending belong to the old sample: dropped.  Copies into the recycled arena are
-    // ordered after every kernel enqueued so far.
-    HIPCHK(hipEventRecord(c->compute_ev, c->stream));
-    HIPCHK(hipStreamWaitEvent(c->copy_stream, c->compute_ev, 0));
+    // ordered after every kernel enqueued so far (add_batch records that fence before its first copy).
+    if (!c->arena.slabs.empty()) c->arena_fence = true;
     clear_history(c);
     if (++c->epoch == 0) {     // wrapped: clear the records once and restart at epoch 1
         HIPCHK(hipMemsetAsync(c->acc, 0, sizeof(Acc) * c->n_pos, c->stream));
@@ -315,11 +329,13 @@ int spg_set_eps_lut(spg_ctx *c, const double lut[256]) {
 }
 
 static int flush_run(spg_ctx *c, int64_t h1 = -1, bool fused = false);
+static int flush_deep(spg_ctx *c);
 
 int spg_set_reference(spg_ctx *c, const char *seq, int64_t len) {
     if (!c || !seq || len < 0) return fail("spg_set_reference: bad argument");
     HIPCHK(hipSetDevice(c->device));
     // pending batches take their first-visit REF chars from the reference they were accumulated under
+    if (int rc = flush_deep(c)) return rc;
     if (int rc = flush_run(c)) return rc;
     if (c->ref) {
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -386,6 +402,10 @@ static int trace_sync(spg_ctx *c, const char *what) {
 #ifndef SPG_GMAX
 #define SPG_GMAX 64
 #endif
+#ifndef SPG_NB
+#define SPG_NB 8
+#endif
+static constexpr int64_t NB_RING = SPG_NB;   // k_acc_seg's finishing ring (columns per wave when fused)
 
 static int64_t env_i64(const char *name, int64_t dflt) {
     const char *e = getenv(name);
@@ -453,8 +473,29 @@ static void fill_swar(const spg_ctx *c, int32_t &min_bq, int32_t &qlo, uint32_t 
     kok = qlo >= 128 ? 0u : (uint32_t)(0x80 - qlo) * 0x01010101u;
 }
 
-// k_acc_seg over one batch (every column of a deep batch; the long columns of a shallow one)
-static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch) {
+// k_acc_seg over one batch (every column of a deep batch; the long columns of a shallow one).  F/O:
+// fused with the calls-only finalize (FRESH deep batch, the sample's only one).
+static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F = nullptr, const Out *O = nullptr) {
+    if (F) {
+        // finalize parameters in device memory (the kernel reads them after its loop); epoch and Counters
+        // slot travel in KParams, everything else changes only when the result buffers grow
+        // finalize parameters in device memory (the kernel reads them after its loop), one copy per
+        // Counters slot; they change only when the result buffers grow
+        FusedArgs fa[2];
+        memset(fa, 0, sizeof fa);               // padding included: compared bytewise below
+        for (uint32_t k = 0; k < 2; k++) {
+            memcpy(&fa[k].F, F, sizeof *F);
+            memcpy(&fa[k].O, O, sizeof *O);
+            fa[k].F.epoch = 0;
+            fa[k].F.cslot = k;
+        }
+        if (!c->fused_valid || memcmp(fa, c->h_fused, sizeof fa) != 0) {
+            HIPCHK(hipStreamSynchronize(c->stream));        // an earlier upload may still read the staging copy
+            memcpy(c->h_fused, fa, sizeof fa);
+            HIPCHK(hipMemcpyAsync(c->d_fused, c->h_fused, sizeof fa, hipMemcpyHostToDevice, c->stream));
+            c->fused_valid = true;
+        }
+    }
     const HistBatch &hb = c->hist[(size_t)idx];
     const int64_t n_cols = hb.n_cols;
     const double avg = (double)hb.n_entries / (double)n_cols;
@@ -469,7 +510,8 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch) {
         const int64_t g_fill = std::max<int64_t>(1, (n_cols + 4095) / 4096);           // one generation
         g = std::max<int64_t>(g, std::min(g_chunks, g_fill));
     }
-    const uint32_t G = (uint32_t)std::min<int64_t>(SPG_GMAX, g);
+    // fused: a wave's columns fit its finishing ring (its records stay in LDS for the finalize)
+    const uint32_t G = (uint32_t)std::min<int64_t>(F ? NB_RING : SPG_GMAX, g);
     KParams P{};
     P.pos_begin = hb.pos_begin;
     P.n_cols = n_cols;
@@ -485,8 +527,23 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch) {
     P.n_entries = hb.n_entries;
     P.dbg = trace_on() ? trace_dbg() : nullptr;
     P.prog = trace_prog((n_cols + G - 1) / G + 4);
+    if (F) P.fused = c->d_fused + F->cslot;
+    P.min_td = c->p.min_total_depth;
+    P.min_ad = c->p.min_allele_depth;
+    P.ratio_lo = c->p.min_evidence_ratio * (1.0 - 1e-9);
     HIPCHK(launch_accumulate(P, hb.off, hb.code, hb.qual, c->ref, c->tables, c->acc, c->stream));
-    return trace_sync(c, "accumulate (k_acc_seg)");
+    return trace_sync(c, F ? "accumulate + finalize (k_acc_seg, fused)" : "accumulate (k_acc_seg)");
+}
+
+// The deferred deep batch, accumulated on its own (something other than a calls-only finalize of the
+// sample needs its records)
+static int flush_deep(spg_ctx *c) {
+    if (!c->deep_pend) return 0;
+    c->deep_pend = false;
+    if (int rc = wait_copies(c)) return rc;
+    if (int rc = acc_begin(c)) return rc;
+    if (int rc = launch_seg(c, 0, true)) return rc;
+    return acc_end(c);
 }
 
 // Fold the pending run [pend0, size) into the records: k_acc_multi (+ k_merge_parts when split), and
@@ -598,6 +655,7 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
                      bool *pageable_copy, int64_t n_samples = 1, const uint32_t *first_sample = nullptr) {
     if (n_samples < 1 || n_samples > (1 << 30)) return fail("spg_accumulate_samples: n_samples out of range");
     if (int rc = materialize(c)) return rc;
+    if (int rc = flush_deep(c)) return rc;
     if (n_cols < 0 || pos_begin < 0 || pos_begin + n_cols > c->n_pos)
         return fail("spg_accumulate: column range outside the context's positions");
     if (pos_begin + n_cols > c->ref_len)
@@ -633,6 +691,11 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
     } else {
         const size_t pad = (n_entries + 16 + 15) & ~size_t(15);
         uint8_t *m = nullptr;
+        if (c->arena_fence) {
+            HIPCHK(hipEventRecord(c->compute_ev, c->stream));
+            HIPCHK(hipStreamWaitEvent(c->copy_stream, c->compute_ev, 0));
+            c->arena_fence = false;
+        }
         HIPCHK(c->arena.alloc(sizeof(uint64_t) * (n_cols + 1) + 2 * pad, &m));
         hb.code = m;
         hb.qual = m + pad;
@@ -676,6 +739,11 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
         // its own (a run folds single-sample batches with consecutive batch numbers)
         if (int rc = flush_run(c, idx)) return rc;
         c->pend0 = idx + 1;
+        static const bool no_fuse = getenv("SPG_NO_FUSE") != nullptr;
+        if (idx == 0 && (c->p.flags & SPG_P_CALLS_ONLY) && !no_fuse) {
+            c->deep_pend = true;               // the sample's first batch: launched by spg_finalize
+            return 0;
+        }
         if (int rc = wait_copies(c)) return rc;
         if (int rc = acc_begin(c)) return rc;
         if (int rc = launch_seg(c, idx, true)) return rc;
@@ -835,9 +903,15 @@ static int finalize_impl(spg_ctx *c, bool table) {
     // position.
     const int64_t nh = (int64_t)c->hist.size();
     static const bool no_fuse = getenv("SPG_NO_FUSE") != nullptr;
-    const bool fused = !table && !no_fuse && (c->p.flags & SPG_P_CALLS_ONLY) && c->pend0 == 0 && nh > 0 &&
-                       run_splits(c, 0, nh) == 1;
-    if (fused) {
+    // one deep batch pending: accumulate + finalize in one launch
+    const bool fused_deep = !table && c->deep_pend && nh == 1;
+    if (!fused_deep)
+        if (int rc = flush_deep(c)) return rc;
+    const bool fused = !fused_deep && !table && !no_fuse && (c->p.flags & SPG_P_CALLS_ONLY) && c->pend0 == 0 &&
+                       nh > 0 && run_splits(c, 0, nh) == 1;
+    if (fused_deep) {
+        c->deep_pend = false;
+    } else if (fused) {
         if (int rc = flush_run(c, -1, true)) return rc;
         c->stale = true;
         c->stale_end = nh;
@@ -847,7 +921,7 @@ static int finalize_impl(spg_ctx *c, bool table) {
     }
     c->cslot ^= 1u;            // this call counts in slot cslot (zeroed by the previous call / creation)
     hipEvent_t *ev = c->ev[c->ring_w % spg_ctx::NRING];
-    if (!c->acc_open) {        // no accumulate since the last finalize: empty accumulate interval
+    if (!c->acc_open && !fused_deep) {   // no accumulate since the last finalize: empty accumulate interval
         c->acc_timing = c->timing;
         if (c->acc_timing >= 1) {
             HIPCHK(hipEventRecord(ev[0], c->stream));
@@ -855,13 +929,23 @@ static int finalize_impl(spg_ctx *c, bool table) {
         }
     }
     const int ft = c->timing;
-    if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
     FParams F = make_fparams(c);
     F.table = table ? 1u : 0u;
-    if (fused) { F.list = c->band; F.n_list = c->nlist; }
-    if (int rc = upload_ridx(c, F.ridx)) return rc;
-    HIPCHK(launch_finalize(F, c->acc, c->tables, make_out(c), c->d_hist, c->stream));
-    if (trace_sync(c, "finalize")) return -1;
+    if (fused_deep) {
+        // the accumulate interval holds the fused kernel; the finalize interval is empty
+        const Out O = make_out(c);
+        if (int rc = wait_copies(c)) return rc;
+        if (int rc = acc_begin(c)) return rc;
+        if (int rc = launch_seg(c, 0, true, &F, &O)) return rc;
+        if (int rc = acc_end(c)) return rc;
+        if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
+    } else {
+        if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
+        if (fused) { F.list = c->band; F.n_list = c->nlist; }
+        if (int rc = upload_ridx(c, F.ridx)) return rc;
+        HIPCHK(launch_finalize(F, c->acc, c->tables, make_out(c), c->d_hist, c->stream));
+        if (trace_sync(c, "finalize")) return -1;
+    }
     c->table_valid = table;
     if (ft >= 2) HIPCHK(hipEventRecord(ev[3], c->stream));
     c->last_acc = c->acc_open && c->acc_timing >= 1;

@@ -71,6 +71,10 @@ struct KParams {
     uint64_t n_entries;    // entries of the batch (launch shape only)
     Hist hdesc;            // this batch's history descriptor ...
     Hist *hslot;           // ... written here by the first thread of the launch
+    const struct FusedArgs *fused;   // k_acc_seg<..., FUSE>: finalize parameters of this Counters slot (device
+                                     // memory: read only for the positions that pass the pre-check below)
+    int32_t min_td, min_ad;          // FUSE: prepare_variants' filters (:131, :151-157) for the division-free
+    double ratio_lo;                 // pre-check (ratio_lo = min_evidence_ratio * (1 - 1e-9))
     const uint32_t *fsamp; // multi-sample batch: per column, the first sample holding entries (else null)
     uint32_t *dbg;         // SPG_TRACE: range violations recorded here instead of faulting (else null)
     uint4 *prog;           // SPG_TRACE: per-wave progress records in host-mapped memory (else null)
@@ -150,6 +154,11 @@ struct Out {                // SoA result table
     int64_t *band;
     spg_detail *detail;
     Counters *ctr;          // Counters[2]
+};
+
+struct FusedArgs {          // the fused accumulate's finalize (one per Counters slot; F.epoch unused)
+    FParams F;
+    Out O;
 };
 
 __device__ __forceinline__ int slot_of(uint32_t c) {

@@ -256,6 +256,343 @@ __device__ __forceinline__ void write_hist(const KParams &P) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *P.hslot = P.hdesc;
 }
 
+// ------------------------------------------------------------------------------------------
+// finalize: GL with the reference's underflow decisions
+// ------------------------------------------------------------------------------------------
+constexpr double LOG2_10_OVER_10 = 0.33219280948873623;   // log2(10)/10
+constexpr double INV_LN2 = 1.4426950408889634;
+constexpr double MARGIN = 1e-5;               // log2 margin around the band edges (>> rounding error)
+
+// A value of the reference's fp64 computation, known either exactly as 0 (state 1), or accurately
+// (state 0: normal, within ~1e-12 relative, l2 = its log2), or only by an upper bound (state 2,
+// "band": l2 bounds log2 of the reference's value, which depends on the order of roundings in the
+// subnormal range).  lv_mul follows one reference multiplication fl(a*b).
+struct LV { int s; double v, l2; };
+__device__ __forceinline__ LV lv_normal(double v, double l2) { return LV{0, v, l2}; }
+__device__ __forceinline__ LV lv_zero() { return LV{1, 0.0, -1e300}; }
+__device__ __forceinline__ LV lv_band(double ub) { return LV{2, 0.0, ub}; }
+__device__ __forceinline__ LV lv_unknown() { return LV{3, 0.0, 0.0}; }   // not accumulated (calls-only)
+__device__ __forceinline__ LV lv_mul(const LV &a, const LV &b) {
+    if (a.s == 1 || b.s == 1) return lv_zero();                   // 0 * finite == 0
+    if (a.s == 3 || b.s == 3) return lv_unknown();
+    const double l2 = a.l2 + b.l2;
+    if (a.s == 0 && b.s == 0) {
+        if (l2 > -1022.0 + MARGIN) return lv_normal(a.v * b.v, l2);  // stays normal: one rounding
+        if (l2 < -1075.0 - MARGIN) return lv_zero();                // exact product < 2^-1075 -> 0
+        return lv_band(fmax(l2 + MARGIN, -1075.0) + 1.0);
+    }
+    const double ub = l2 + MARGIN;                                 // bound on the exact product
+    if (ub < -1075.0 - MARGIN) return lv_zero();
+    return lv_band(fmax(ub, -1075.0) + 1.0);                       // + half a subnormal unit
+}
+
+__device__ __forceinline__ int to_phred(double p) {      // utils.py:12-13
+    if (!(p > 0.0)) return 99;
+    const double r = rint(-10.0 * log10(p));
+    return r < 99.0 ? (int)r : 99;
+}
+
+__device__ __forceinline__ void write_candidate(const FParams &F, const Out &O, int64_t pos, const Acc &a, int k,
+                                                uint32_t code, uint32_t ad, double g, double S, double qual) {
+    spg_candidate c;
+    c.pos = pos; c.dp = (int32_t)a.depth; c.ad = (int32_t)ad;
+    c.ref = (uint8_t)(a.misc & 0xFFu); c.alt = nibble_char(code); c.rank = (uint8_t)k;
+    c.first_batch = a.first_batch;
+    c.gl_linear = g;
+    if (g != 0) { c.gl = log10(g); c.pl = (int32_t)rint(-10.0 * c.gl); c.gl_zero = 0; }
+    else { c.gl = 0.0; c.pl = 0; c.gl_zero = 1; }
+    c.score = to_phred(1.0 - (g / S));
+    c.qual = qual;
+    const uint32_t at = atomicAdd(&O.ctr[F.cslot].n_cand, 1u);
+    if (at < (uint32_t)F.cand_cap) O.cand[at] = c;
+}
+
+__device__ __forceinline__ bool is_candidate(const FParams &F, const Acc &a, uint32_t code, uint32_t ad) {
+    return (uint8_t)(a.misc & 0xFFu) != nibble_char(code) && (int64_t)ad >= F.min_ad &&
+           (double)ad / (double)a.depth >= F.ratio;                            // :151-157
+}
+
+// Exact sequential recomputation of one position over the batch history (rare: subnormal band, IUPAC
+// alleles, calls-only terms that were not accumulated).  np.prod is a strict left fold (utils.py:17,19)
+// and N a dict-order fold (:18-22): sequential per allele, but the 16 allele codes' folds are
+// independent.  The wave walks the position's entries 64 at a time (coalesced byte loads, one entry per
+// lane) over the batches the replay index lists for the position; lane c owns code c's fold and takes
+// the chunk's code-c factors in order through readlane, so no fold step waits on a memory load.
+// Pass 1: counts, first appearance (dict order), sum(eps) and the P folds (stopped at 0: P only
+// shrinks).  Pass 2: the H folds, only for alleles whose GL is not already exactly 0 through N == 0
+// (H is finite, so H * 0 == 0), each stopped at 0.
+struct ReplayWs {
+    uint32_t cnt[16], ord[16];
+    uint64_t first[16];
+    double P[16], Hh[16], se[16], G[16], non[16];
+    uint32_t needH, n;
+};
+
+template <typename Fn>
+__device__ __forceinline__ void replay_walk(const FParams &F, const Hist *__restrict__ H, int64_t pos, int lane,
+                                            Fn &&fn) {
+    const bool indexed = F.ridx.n_buckets > 0;
+    uint32_t i0 = 0, i1 = (uint32_t)F.n_hist;
+    if (indexed) {
+        const int64_t bk = pos >> RIDX_SHIFT;
+        i0 = F.ridx.off[bk];
+        i1 = F.ridx.off[bk + 1];
+    }
+    uint64_t ord = 0;                                  // raw entries of this position in earlier batches
+    for (uint32_t i = i0; i < i1; i++) {
+        const int32_t b = indexed ? F.ridx.items[i] : (int32_t)i;
+        const Hist h = H[b];
+        const int64_t col = pos - h.pos_begin;
+        if (col < 0 || col >= h.n_cols) continue;
+        const uint64_t lo = h.off[col], hi = h.off[col + 1];
+        for (uint64_t e0 = lo; e0 < hi; e0 += 64) {
+            const uint64_t e = e0 + (uint64_t)lane;
+            const bool valid = e < hi;
+            const uint32_t c = valid ? h.code[e] : 0xFFu, q = valid ? h.qual[e] : 0u;
+            fn(c, q, valid, ord + (e0 - lo));
+        }
+        ord += hi - lo;
+    }
+}
+
+// rec: the position's record (HBM, or the fused accumulate's LDS image); eps(q): from_phred_scale(q)
+template <typename EpsFn>
+__device__ __forceinline__ void replay_wave(const FParams &F, const Hist *__restrict__ H, const Acc *rec,
+                                         const Out &O, int64_t pos, ReplayWs *w, EpsFn &&eps_s) {
+    const int lane = threadIdx.x & 63;
+    const Acc a = *rec;
+    uint32_t cnt = 0, depth = 0;
+    uint64_t first = ~0ull;
+    double P = 1.0, Hh = 1.0, se = 0.0;
+    replay_walk(F, H, pos, lane, [&](uint32_t c, uint32_t q, bool valid, uint64_t base) {
+        const bool pass = valid && (int)q >= F.min_bq;
+        depth += (uint32_t)__popcll(__ballot(pass));
+        const bool isc = pass && c < 16u;
+        const double e = isc ? eps_s(q) : 0.0;
+        uint64_t todo = __ballot(isc);
+        while (todo) {
+            const int j0 = (int)__builtin_ctzll(todo);
+            const uint32_t cc = __builtin_amdgcn_readlane(c, j0);
+            const bool mine = isc && c == cc;
+            const uint64_t bm = __ballot(mine);
+            todo &= ~bm;
+            const double es = dsum_f64(mine ? e : 0.0);
+            double pc = rl_f64(P, (int)cc);
+            for (uint64_t m = bm; m && pc != 0.0; m &= m - 1) pc = pc * rl_f64(e, (int)__builtin_ctzll(m));
+            if (lane == (int)cc) {
+                if (cnt == 0) first = base + (uint64_t)j0;
+                cnt += (uint32_t)__popcll(bm);
+                se += es;
+                P = pc;
+            }
+        }
+    });
+    if (lane < 16) { w->cnt[lane] = cnt; w->first[lane] = first; w->P[lane] = P; w->se[lane] = se; }
+    wave_sync();
+    if (lane == 0) {
+        int n = 0;                                     // dict order: codes by first appearance
+        for (int c = 0; c < 16; c++) {
+            if (!w->cnt[c]) continue;
+            int at = n++;
+            while (at > 0 && w->first[w->ord[at - 1]] > w->first[c]) { w->ord[at] = w->ord[at - 1]; at--; }
+            w->ord[at] = (uint32_t)c;
+        }
+        uint32_t need = 0;
+        for (int h = 0; h < n; h++) {                  // N_h = ((1.0 * P_a1) * P_a2) ... over a != h
+            double non = 1.0;
+            for (int j = 0; j < n; j++)
+                if (j != h) non = non * w->P[w->ord[j]];
+            w->non[h] = non;
+            if (non != 0.0) need |= 1u << w->ord[h];
+        }
+        w->n = (uint32_t)n;
+        w->needH = need;
+    }
+    wave_sync();
+    const uint32_t needH = w->needH;
+    if (needH) {
+        replay_walk(F, H, pos, lane, [&](uint32_t c, uint32_t q, bool valid, uint64_t) {
+            const bool isc = valid && (int)q >= F.min_bq && c < 16u && ((needH >> c) & 1u);
+            const double om = isc ? 1.0 - eps_s(q) : 0.0;
+            uint64_t todo = __ballot(isc);
+            while (todo) {
+                const uint32_t cc = __builtin_amdgcn_readlane(c, (int)__builtin_ctzll(todo));
+                const uint64_t bm = __ballot(isc && c == cc);
+                todo &= ~bm;
+                double hc = rl_f64(Hh, (int)cc);
+                for (uint64_t m = bm; m && hc != 0.0; m &= m - 1) hc = hc * rl_f64(om, (int)__builtin_ctzll(m));
+                if (lane == (int)cc) Hh = hc;
+            }
+        });
+    }
+    if (lane < 16) w->Hh[lane] = Hh;
+    wave_sync();
+    if (lane == 0) {
+        const int n = (int)w->n;
+        const bool evaluated = (int64_t)depth >= (int64_t)F.min_td;
+        double S = 0.0;
+        for (int h = 0; h < n; h++) {
+            w->G[h] = w->Hh[w->ord[h]] * w->non[h];
+            S = S + w->G[h];
+        }
+        if (S == 0) S = 1.0;
+        uint8_t flags = F.table ? O.flags[pos] : 0;
+        if (evaluated) {
+            double *gl = O.gl + pos * NSLOT;
+            for (int h = 0; h < n; h++) {
+                const uint32_t c = w->ord[h];
+                const int s = slot_of(c);
+                if (s >= 0 && F.table) gl[s] = w->G[h];
+                if (is_candidate(F, a, c, w->cnt[c])) {
+                    write_candidate(F, O, pos, a, h, c, w->cnt[c], w->G[h], S, w->se[c] / (double)w->cnt[c]);
+                    flags |= SPG_F_CANDIDATE;
+                }
+            }
+        }
+        if (F.table) O.flags[pos] = flags;
+        if (depth != a.depth) atomicOr(&O.ctr[F.cslot].err, 1u);   // history / accumulator mismatch
+        const uint32_t at = atomicAdd(&O.ctr[F.cslot].n_detail, 1u);
+        if (at < (uint32_t)F.detail_cap) {
+            spg_detail *d = O.detail + at;
+            d->pos = pos; d->depth = depth; d->n_alleles = (uint8_t)n;
+            d->pad[0] = d->pad[1] = d->pad[2] = 0;
+            for (int k = 0; k < 16; k++) {
+                d->code[k] = k < n ? (uint8_t)w->ord[k] : 0xFF;
+                d->count[k] = k < n ? w->cnt[w->ord[k]] : 0;
+                d->gl[k] = (k < n && evaluated) ? w->G[k] : __builtin_nan("");
+            }
+        }
+    }
+    wave_sync();
+}
+
+// prepare_variants for one position (one lane).  Returns true when the position needs the exact replay.
+// rec: the position's record (HBM, or the fused accumulate's LDS image).  CO: calls only at compile
+// time (no per-position table; the fused accumulate's instantiation).
+template <bool CO>
+__device__ __forceinline__ bool finalize_position(const FParams &F, const Acc *rec,
+                                                  const Tables *__restrict__ T, const Out &O, int64_t pos,
+                                                  double *sink) {
+    const double NaN = __builtin_nan("");
+    const bool table = !CO && F.table;
+    if (!table) {
+        // calls only: the header and the counts (first 52 bytes, one round trip) decide whether this
+        // position can produce a call at all; only then is the rest of the record read
+        const uint4 h0 = reinterpret_cast<const uint4 *>(rec)[0];
+        const uint4 h1 = reinterpret_cast<const uint4 *>(rec)[1];
+        const uint4 c4 = reinterpret_cast<const uint4 *>(rec)[2];
+        const uint32_t c5 = reinterpret_cast<const uint32_t *>(rec)[12];
+        // not in memory (CO: the fused accumulate's own LDS image, of this epoch by construction)
+        if ((!CO && h1.w != F.epoch) || h0.y == 0) return false;
+        if ((int64_t)h0.x < (int64_t)F.min_td) return false;             // not evaluated (:131)
+        if (!(h0.w & MISC_EXOTIC)) {
+            const uint32_t cnt[NSLOT] = {c4.x, c4.y, c4.z, c4.w, c5};
+            const uint8_t refc = (uint8_t)(h0.w & 0xFFu);
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < NSLOT; k++)
+                any |= cnt[k] != 0 && refc != nibble_char(slot_code(k)) && (int64_t)cnt[k] >= F.min_ad &&
+                       (double)cnt[k] / (double)h0.x >= F.ratio;                         // :151-157
+            if (!any) return false;
+        }
+    }
+    const Acc a = *rec;
+    const bool live = (CO || a.epoch == F.epoch) && a.first_batch != 0;
+    uint32_t *cnt8 = O.counts + pos * SPG_NCOUNT;
+    double *gl = table ? O.gl + pos * NSLOT : sink;     // scratch-free sink (CO: none)
+    if (table) {
+        O.depth[pos] = live ? a.depth : 0u;
+        O.order[pos] = live ? a.order : 0u;
+        O.first[pos] = live ? a.first_batch : 0u;
+#pragma unroll
+        for (int k = 0; k < NSLOT; k++) { cnt8[k] = live ? a.cnt[k] : 0u; gl[k] = NaN; }
+        cnt8[5] = live ? a.n_del : 0u; cnt8[6] = live ? a.n_skip : 0u; cnt8[7] = live ? a.n_other : 0u;
+    }
+    if (!live) { if (table) O.flags[pos] = 0; return false; }
+    uint8_t flags = SPG_F_PRESENT;
+    const bool evaluated = (int64_t)a.depth >= (int64_t)F.min_td;   // :131
+    if (evaluated) flags |= SPG_F_EVALUATED;
+    if (a.misc & MISC_EXOTIC) {       // IUPAC / '=' alleles: the exact replay tabulates every allele
+        if (table) O.flags[pos] = flags | SPG_F_EXOTIC | SPG_F_REPLAYED;
+        return true;
+    }
+    if (!evaluated) { if (table) O.flags[pos] = flags; return false; }
+    const int n = (int)(a.order & 7u);
+    const uint32_t skip = (a.misc >> MISC_SKIP_SHIFT) & 0x1Fu;
+    uint32_t slot[NSLOT], cnts[NSLOT];
+    LV Pv[NSLOT], Hv[NSLOT];
+    double Sv[NSLOT];
+    // per-allele P (= prod eps, utils.py:19) and H (= prod 1-eps, utils.py:17) in dict order
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) {
+        slot[k] = (a.order >> (3 + 3 * k)) & 7u;
+        cnts[k] = 0; Sv[k] = 0.0; Pv[k] = lv_normal(1.0, 0.0); Hv[k] = lv_normal(1.0, 0.0);
+        if (k >= n) continue;              // only the alleles present (no exp for empty slots)
+        uint32_t c_ = 0, sq = 0, qf = 0; double sl = 0.0, se = 0.0;
+#pragma unroll
+        for (int j = 0; j < NSLOT; j++)
+            if (slot[k] == (uint32_t)j) { c_ = a.cnt[j]; sq = a.sq[j]; qf = a.qf[j]; sl = a.sl[j]; se = a.se[j]; }
+        cnts[k] = c_;
+        Sv[k] = se;
+        // P: log10 P = -sum(q)/10 up to (n+2) ulp; exact zero proven when every factor < 1/2
+        if (sq <= 3076u) Pv[k] = lv_normal(T->p10k[sq / 10u] * T->eps[sq % 10u], -(double)sq * LOG2_10_OVER_10);
+        else if (sq >= 3245u && qf >= 4u) Pv[k] = lv_zero();
+        else Pv[k] = lv_band(-1022.0 + 2 * MARGIN);
+        // H: exp(sum ln(1-eps)); exactly 0 when a Q0 entry is present (1 - 1.0 == 0)
+        if (qf == 0u) Hv[k] = lv_zero();
+        else if ((skip >> slot[k]) & 1u) Hv[k] = lv_unknown();
+        else {
+            const double l2 = sl * INV_LN2;
+            Hv[k] = l2 > -1022.0 + MARGIN ? lv_normal(exp(sl), l2) : lv_band(-1022.0 + 2 * MARGIN);
+        }
+    }
+    double G[NSLOT];
+    bool band = false, unknown = false, cand_needs_s = false;
+#pragma unroll
+    for (int h = 0; h < NSLOT; h++) {
+        // N = ((1.0 * P_a1) * P_a2) ... over a != h in dict order (utils.py:18-22), GL = H * N
+        LV c = lv_normal(1.0, 0.0);
+#pragma unroll
+        for (int j = 0; j < NSLOT; j++)
+            if (j != h && j < n) c = lv_mul(c, Pv[j]);
+        const LV g = lv_mul(Hv[h], c);
+        if (h < n && g.s == 2) band = true;
+        G[h] = g.s == 0 ? g.v : (g.s == 3 ? NaN : 0.0);
+        if (h < n && g.s == 3) unknown = true;
+        // a candidate needs S = sum(GL) unless its own GL is exactly 0 (SCORE = 0 for any S)
+        if (h < n && g.s != 1 && is_candidate(F, a, slot_code((int)slot[h]), cnts[h])) {
+            cand_needs_s = true;
+            if (g.s == 3) band = true;        // its own GL depends on terms not accumulated
+        }
+    }
+    // unknown (not accumulated) GL terms only matter if a call needs S: then replay exactly
+    if (band || (unknown && cand_needs_s)) {
+        if (table) O.flags[pos] = flags | SPG_F_REPLAYED;
+        return true;
+    }
+    if (unknown) flags |= SPG_F_PARTIAL;
+    double S = 0.0;
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++)
+        if (k < n && !unknown) S = S + G[k];                 // :145
+    if (S == 0) S = 1.0;                                     // :146 (every call has GL 0 if unknown)
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) {
+        if (k < n) {
+#pragma unroll
+            for (int j = 0; j < NSLOT; j++)
+                if (!CO && slot[k] == (uint32_t)j) gl[j] = G[k];
+            const uint32_t code = slot_code((int)slot[k]);
+            if (is_candidate(F, a, code, cnts[k])) {
+                write_candidate(F, O, pos, a, k, code, cnts[k], G[k], S, Sv[k] / (double)cnts[k]);
+                flags |= SPG_F_CANDIDATE;
+            }
+        }
+    }
+    if (table) O.flags[pos] = flags;
+    return false;
+}
+
 // Column finishing is batched: at a column's end the wave only reduces its fast-path sums into a
 // ColSum (lane 0) next to the column's rare record (both in a per-wave LDS ring of NB slots).  When
 // the ring is full (and at the wave's end) lane j < NB assembles column j's 160-B Acc record — the
@@ -366,7 +703,36 @@ struct Dual2 {              // per-lane partial sums of a wave's second fast all
 // WPE: minimum waves per SIMD the register allocation must allow.  4 (128 VGPRs) for mid-depth
 // batches, whose waves stream few chunks per column and need occupancy to hide the column starts;
 // 3 (up to 168 VGPRs, no spills) for deep batches, where the chunk loop dominates.
-template <int W, bool FRESH, int WPE, bool NT>
+// The fused accumulate's finalize (k_acc_seg<..., FUSE>, after the wave's loop, for the lanes whose
+// column passed the pre-check): prepare_variants (:120-185) on the ring's records, whose images finish()
+// left in LDS; lane j evaluates column j,
+// candidates go straight to the call table, and the wave replays the few positions that need the
+// exact fold over this batch's column (the sample's only batch).
+__device__ __forceinline__ void fused_tail(const FParams &F, const Out &O, const Tables *__restrict__ T, int64_t pos0,
+                                         uint32_t nfin, const ColSum *CS, const Acc *img, ReplayWs *ws,
+                                         const Hist *hdl, const double2 *lut) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t cjl = (uint32_t)lane < nfin ? CS[lane].cj : 0u;
+    const int64_t pos = pos0 + (int64_t)cjl;
+    const bool need = (uint32_t)lane < nfin && finalize_position<true>(F, img + lane, T, O, pos, nullptr);
+    uint64_t rb = __ballot(need);
+    if (!rb) return;
+    if (need) atomicAdd(&O.ctr[F.cslot].n_band, 1u);
+    while (rb) {
+        const int j = (int)__builtin_ctzll(rb);
+        rb &= rb - 1;
+        const int64_t pj = pos0 + (int64_t)(uint32_t)__builtin_amdgcn_readlane(cjl, j);
+        replay_wave(F, hdl, img + j, O, pj, ws, [&](uint32_t q) {
+            return q == 0u ? 1.0 : lut[q < 128u ? q : q + 128u].y;     // from_phred_scale (eps(Q0) = 1)
+        });
+    }
+}
+
+// FUSE (a FRESH deep batch that is the sample's only batch, finalized calls-only: spg_finalize launches
+// it in place of accumulate + k_finalize): each wave owns G <= NB columns, so its one ring holds every
+// record it writes; after the loop lane j runs prepare_variants' per-position logic on record j's LDS
+// image and the wave replays the few positions that need the exact fold — one launch per sample.
+template <int W, bool FRESH, int WPE, bool NT, bool FUSE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_acc_seg(KParams P, const uint64_t *__restrict__ off,
                                                  const uint8_t *__restrict__ code, const uint8_t *__restrict__ qual,
                                                  const uint8_t *__restrict__ ref, const Tables *__restrict__ T,
@@ -381,13 +747,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     __shared__ double2 lut[384];
     __shared__ WaveRare rare[KW][NB];
     __shared__ ColSum csum[KW][NB];
-    __shared__ RareItem rqueue[KW][QCAP];
+    __shared__ __align__(16) RareItem rqueue[KW][QCAP];   // FUSE: the replay workspace after the loop
+    static_assert(sizeof(ReplayWs) <= sizeof(RareItem) * QCAP, "ReplayWs aliases a wave's queue");
     __shared__ int32_t rqo[KW][QCAP];
     __shared__ uint32_t rqr[KW][QCAP];
     __shared__ Dual2 dual2[KW];
     __shared__ Acc accimg[KW][NB];
     __shared__ ColDesc coldesc[KW][SPG_GMAX];
+    __shared__ Hist hdl;                                // FUSE: this batch's descriptor for the replay
     write_hist(P);
+    if (FUSE && threadIdx.x == 0) hdl = P.hdesc;
+    if constexpr (FUSE) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) P.fused->O.ctr[P.fused->F.cslot ^ 1u] = Counters{0, 0, 0, 0};   // next call's slot
+    }
     for (uint32_t q = threadIdx.x; q < 256u; q += 64u * KW) {
         lut[q] = q < 128u ? make_double2(T->fast[q][0], T->fast[q][1]) : make_double2(0.0, 0.0);
         if (q >= 128u) lut[q + 128u] = make_double2(T->fast[q][0], T->fast[q][1]);
@@ -740,7 +1112,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 S->crefc = crefc; S->fl = fl; S->fe = fe; S->fl2 = fl2; S->fe2 = fe2;
                 S->fsamp = fsc;
             }
-            if (++nb == NB) finish();
+            if (++nb == NB) {
+                if constexpr (!FUSE) finish();         // FUSE: G <= NB, the ring is finished after the loop
+            }
         }
     };
 
@@ -751,7 +1125,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     }
 #undef SPG_LD
     prog(5, total, nb, qn);
+    const uint32_t nfin = nb;                          // FUSE: every column of the wave (G <= NB)
     if (nb) finish();
+    if constexpr (FUSE) {
+        // Division-free pre-check from the images (LDS) and the kernel's scalar parameters: most positions
+        // cannot produce a call.  Only a wave holding a possible call reads the finalize parameters (vector
+        // loads from memory, whose wait would also wait for the record stores just issued).
+        bool maybe = false;
+        if ((uint32_t)lane < nfin) {
+            const Acc *r = img + lane;
+            const uint32_t depth = r->depth, misc = r->misc;
+            if (misc & MISC_EXOTIC) {
+                maybe = true;                              // exotic allele: exact replay
+            } else if ((int64_t)depth >= (int64_t)P.min_td) {
+                const double dlo = (double)depth * P.ratio_lo;
+                const uint8_t refc = (uint8_t)(misc & 0xFFu);
+#pragma unroll
+                for (int k = 0; k < NSLOT; k++) {
+                    const uint32_t n = r->cnt[k];
+                    maybe |= n != 0 && refc != nibble_char(slot_code(k)) && (int64_t)n >= P.min_ad && (double)n >= dlo;
+                }
+            }
+        }
+        if (__ballot(maybe))
+            fused_tail(P.fused->F, P.fused->O, T, P.pos_begin + g0, maybe ? nfin : 0u, CS, img,
+                       reinterpret_cast<ReplayWs *>(Q), &hdl, lut);
+    }
     prog(6, 0, 0, 0);
 }
 
@@ -1100,336 +1499,6 @@ __global__ __launch_bounds__(256) void k_merge_parts(MParams P, const uint8_t *_
         if (t < 5 || sums) dst[t] = src[t];
 }
 
-// ------------------------------------------------------------------------------------------
-// finalize: GL with the reference's underflow decisions
-// ------------------------------------------------------------------------------------------
-constexpr double LOG2_10_OVER_10 = 0.33219280948873623;   // log2(10)/10
-constexpr double INV_LN2 = 1.4426950408889634;
-constexpr double MARGIN = 1e-5;               // log2 margin around the band edges (>> rounding error)
-
-// A value of the reference's fp64 computation, known either exactly as 0 (state 1), or accurately
-// (state 0: normal, within ~1e-12 relative, l2 = its log2), or only by an upper bound (state 2,
-// "band": l2 bounds log2 of the reference's value, which depends on the order of roundings in the
-// subnormal range).  lv_mul follows one reference multiplication fl(a*b).
-struct LV { int s; double v, l2; };
-__device__ __forceinline__ LV lv_normal(double v, double l2) { return LV{0, v, l2}; }
-__device__ __forceinline__ LV lv_zero() { return LV{1, 0.0, -1e300}; }
-__device__ __forceinline__ LV lv_band(double ub) { return LV{2, 0.0, ub}; }
-__device__ __forceinline__ LV lv_unknown() { return LV{3, 0.0, 0.0}; }   // not accumulated (calls-only)
-__device__ __forceinline__ LV lv_mul(const LV &a, const LV &b) {
-    if (a.s == 1 || b.s == 1) return lv_zero();                   // 0 * finite == 0
-    if (a.s == 3 || b.s == 3) return lv_unknown();
-    const double l2 = a.l2 + b.l2;
-    if (a.s == 0 && b.s == 0) {
-        if (l2 > -1022.0 + MARGIN) return lv_normal(a.v * b.v, l2);  // stays normal: one rounding
-        if (l2 < -1075.0 - MARGIN) return lv_zero();                // exact product < 2^-1075 -> 0
-        return lv_band(fmax(l2 + MARGIN, -1075.0) + 1.0);
-    }
-    const double ub = l2 + MARGIN;                                 // bound on the exact product
-    if (ub < -1075.0 - MARGIN) return lv_zero();
-    return lv_band(fmax(ub, -1075.0) + 1.0);                       // + half a subnormal unit
-}
-
-__device__ __forceinline__ int to_phred(double p) {      // utils.py:12-13
-    if (!(p > 0.0)) return 99;
-    const double r = rint(-10.0 * log10(p));
-    return r < 99.0 ? (int)r : 99;
-}
-
-__device__ __forceinline__ void write_candidate(const FParams &F, const Out &O, int64_t pos, const Acc &a, int k,
-                                                uint32_t code, uint32_t ad, double g, double S, double qual) {
-    spg_candidate c;
-    c.pos = pos; c.dp = (int32_t)a.depth; c.ad = (int32_t)ad;
-    c.ref = (uint8_t)(a.misc & 0xFFu); c.alt = nibble_char(code); c.rank = (uint8_t)k;
-    c.first_batch = a.first_batch;
-    c.gl_linear = g;
-    if (g != 0) { c.gl = log10(g); c.pl = (int32_t)rint(-10.0 * c.gl); c.gl_zero = 0; }
-    else { c.gl = 0.0; c.pl = 0; c.gl_zero = 1; }
-    c.score = to_phred(1.0 - (g / S));
-    c.qual = qual;
-    const uint32_t at = atomicAdd(&O.ctr[F.cslot].n_cand, 1u);
-    if (at < (uint32_t)F.cand_cap) O.cand[at] = c;
-}
-
-__device__ __forceinline__ bool is_candidate(const FParams &F, const Acc &a, uint32_t code, uint32_t ad) {
-    return (uint8_t)(a.misc & 0xFFu) != nibble_char(code) && (int64_t)ad >= F.min_ad &&
-           (double)ad / (double)a.depth >= F.ratio;                            // :151-157
-}
-
-// Exact sequential recomputation of one position over the batch history (rare: subnormal band, IUPAC
-// alleles, calls-only terms that were not accumulated).  np.prod is a strict left fold (utils.py:17,19)
-// and N a dict-order fold (:18-22): sequential per allele, but the 16 allele codes' folds are
-// independent.  The wave walks the position's entries 64 at a time (coalesced byte loads, one entry per
-// lane) over the batches the replay index lists for the position; lane c owns code c's fold and takes
-// the chunk's code-c factors in order through readlane, so no fold step waits on a memory load.
-// Pass 1: counts, first appearance (dict order), sum(eps) and the P folds (stopped at 0: P only
-// shrinks).  Pass 2: the H folds, only for alleles whose GL is not already exactly 0 through N == 0
-// (H is finite, so H * 0 == 0), each stopped at 0.
-struct ReplayWs {
-    uint32_t cnt[16], ord[16];
-    uint64_t first[16];
-    double P[16], Hh[16], se[16], G[16], non[16];
-    uint32_t needH, n;
-};
-
-template <typename Fn>
-__device__ __forceinline__ void replay_walk(const FParams &F, const Hist *__restrict__ H, int64_t pos, int lane,
-                                            Fn &&fn) {
-    const bool indexed = F.ridx.n_buckets > 0;
-    uint32_t i0 = 0, i1 = (uint32_t)F.n_hist;
-    if (indexed) {
-        const int64_t bk = pos >> RIDX_SHIFT;
-        i0 = F.ridx.off[bk];
-        i1 = F.ridx.off[bk + 1];
-    }
-    uint64_t ord = 0;                                  // raw entries of this position in earlier batches
-    for (uint32_t i = i0; i < i1; i++) {
-        const int32_t b = indexed ? F.ridx.items[i] : (int32_t)i;
-        const Hist h = H[b];
-        const int64_t col = pos - h.pos_begin;
-        if (col < 0 || col >= h.n_cols) continue;
-        const uint64_t lo = h.off[col], hi = h.off[col + 1];
-        for (uint64_t e0 = lo; e0 < hi; e0 += 64) {
-            const uint64_t e = e0 + (uint64_t)lane;
-            const bool valid = e < hi;
-            const uint32_t c = valid ? h.code[e] : 0xFFu, q = valid ? h.qual[e] : 0u;
-            fn(c, q, valid, ord + (e0 - lo));
-        }
-        ord += hi - lo;
-    }
-}
-
-__device__ __forceinline__ void replay_wave(const FParams &F, const Hist *__restrict__ H, const Acc *__restrict__ acc,
-                                         const Out &O, int64_t pos, ReplayWs *w, const double *eps_s) {
-    const int lane = threadIdx.x & 63;
-    const Acc a = acc[pos];
-    uint32_t cnt = 0, depth = 0;
-    uint64_t first = ~0ull;
-    double P = 1.0, Hh = 1.0, se = 0.0;
-    replay_walk(F, H, pos, lane, [&](uint32_t c, uint32_t q, bool valid, uint64_t base) {
-        const bool pass = valid && (int)q >= F.min_bq;
-        depth += (uint32_t)__popcll(__ballot(pass));
-        const bool isc = pass && c < 16u;
-        const double e = isc ? eps_s[q] : 0.0;
-        uint64_t todo = __ballot(isc);
-        while (todo) {
-            const int j0 = (int)__builtin_ctzll(todo);
-            const uint32_t cc = __builtin_amdgcn_readlane(c, j0);
-            const bool mine = isc && c == cc;
-            const uint64_t bm = __ballot(mine);
-            todo &= ~bm;
-            const double es = dsum_f64(mine ? e : 0.0);
-            double pc = rl_f64(P, (int)cc);
-            for (uint64_t m = bm; m && pc != 0.0; m &= m - 1) pc = pc * rl_f64(e, (int)__builtin_ctzll(m));
-            if (lane == (int)cc) {
-                if (cnt == 0) first = base + (uint64_t)j0;
-                cnt += (uint32_t)__popcll(bm);
-                se += es;
-                P = pc;
-            }
-        }
-    });
-    if (lane < 16) { w->cnt[lane] = cnt; w->first[lane] = first; w->P[lane] = P; w->se[lane] = se; }
-    wave_sync();
-    if (lane == 0) {
-        int n = 0;                                     // dict order: codes by first appearance
-        for (int c = 0; c < 16; c++) {
-            if (!w->cnt[c]) continue;
-            int at = n++;
-            while (at > 0 && w->first[w->ord[at - 1]] > w->first[c]) { w->ord[at] = w->ord[at - 1]; at--; }
-            w->ord[at] = (uint32_t)c;
-        }
-        uint32_t need = 0;
-        for (int h = 0; h < n; h++) {                  // N_h = ((1.0 * P_a1) * P_a2) ... over a != h
-            double non = 1.0;
-            for (int j = 0; j < n; j++)
-                if (j != h) non = non * w->P[w->ord[j]];
-            w->non[h] = non;
-            if (non != 0.0) need |= 1u << w->ord[h];
-        }
-        w->n = (uint32_t)n;
-        w->needH = need;
-    }
-    wave_sync();
-    const uint32_t needH = w->needH;
-    if (needH) {
-        replay_walk(F, H, pos, lane, [&](uint32_t c, uint32_t q, bool valid, uint64_t) {
-            const bool isc = valid && (int)q >= F.min_bq && c < 16u && ((needH >> c) & 1u);
-            const double om = isc ? 1.0 - eps_s[q] : 0.0;
-            uint64_t todo = __ballot(isc);
-            while (todo) {
-                const uint32_t cc = __builtin_amdgcn_readlane(c, (int)__builtin_ctzll(todo));
-                const uint64_t bm = __ballot(isc && c == cc);
-                todo &= ~bm;
-                double hc = rl_f64(Hh, (int)cc);
-                for (uint64_t m = bm; m && hc != 0.0; m &= m - 1) hc = hc * rl_f64(om, (int)__builtin_ctzll(m));
-                if (lane == (int)cc) Hh = hc;
-            }
-        });
-    }
-    if (lane < 16) w->Hh[lane] = Hh;
-    wave_sync();
-    if (lane == 0) {
-        const int n = (int)w->n;
-        const bool evaluated = (int64_t)depth >= (int64_t)F.min_td;
-        double S = 0.0;
-        for (int h = 0; h < n; h++) {
-            w->G[h] = w->Hh[w->ord[h]] * w->non[h];
-            S = S + w->G[h];
-        }
-        if (S == 0) S = 1.0;
-        uint8_t flags = F.table ? O.flags[pos] : 0;
-        if (evaluated) {
-            double *gl = O.gl + pos * NSLOT;
-            for (int h = 0; h < n; h++) {
-                const uint32_t c = w->ord[h];
-                const int s = slot_of(c);
-                if (s >= 0 && F.table) gl[s] = w->G[h];
-                if (is_candidate(F, a, c, w->cnt[c])) {
-                    write_candidate(F, O, pos, a, h, c, w->cnt[c], w->G[h], S, w->se[c] / (double)w->cnt[c]);
-                    flags |= SPG_F_CANDIDATE;
-                }
-            }
-        }
-        if (F.table) O.flags[pos] = flags;
-        if (depth != a.depth) atomicOr(&O.ctr[F.cslot].err, 1u);   // history / accumulator mismatch
-        const uint32_t at = atomicAdd(&O.ctr[F.cslot].n_detail, 1u);
-        if (at < (uint32_t)F.detail_cap) {
-            spg_detail *d = O.detail + at;
-            d->pos = pos; d->depth = depth; d->n_alleles = (uint8_t)n;
-            d->pad[0] = d->pad[1] = d->pad[2] = 0;
-            for (int k = 0; k < 16; k++) {
-                d->code[k] = k < n ? (uint8_t)w->ord[k] : 0xFF;
-                d->count[k] = k < n ? w->cnt[w->ord[k]] : 0;
-                d->gl[k] = (k < n && evaluated) ? w->G[k] : __builtin_nan("");
-            }
-        }
-    }
-    wave_sync();
-}
-
-// prepare_variants for one position (one lane).  Returns true when the position needs the exact replay.
-__device__ __forceinline__ bool finalize_position(const FParams &F, const Acc *__restrict__ acc,
-                                                  const Tables *__restrict__ T, const Out &O, int64_t pos,
-                                                  double *sink) {
-    const double NaN = __builtin_nan("");
-    if (!F.table) {
-        // calls only: the header and the counts (first 52 bytes, one round trip) decide whether this
-        // position can produce a call at all; only then is the rest of the record read
-        const uint4 h0 = reinterpret_cast<const uint4 *>(acc + pos)[0];
-        const uint4 h1 = reinterpret_cast<const uint4 *>(acc + pos)[1];
-        const uint4 c4 = reinterpret_cast<const uint4 *>(acc + pos)[2];
-        const uint32_t c5 = reinterpret_cast<const uint32_t *>(acc + pos)[12];
-        if (h1.w != F.epoch || h0.y == 0) return false;                  // not in memory
-        if ((int64_t)h0.x < (int64_t)F.min_td) return false;             // not evaluated (:131)
-        if (!(h0.w & MISC_EXOTIC)) {
-            const uint32_t cnt[NSLOT] = {c4.x, c4.y, c4.z, c4.w, c5};
-            const uint8_t refc = (uint8_t)(h0.w & 0xFFu);
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < NSLOT; k++)
-                any |= cnt[k] != 0 && refc != nibble_char(slot_code(k)) && (int64_t)cnt[k] >= F.min_ad &&
-                       (double)cnt[k] / (double)h0.x >= F.ratio;                         // :151-157
-            if (!any) return false;
-        }
-    }
-    const Acc a = acc[pos];
-    const bool live = a.epoch == F.epoch && a.first_batch != 0;
-    uint32_t *cnt8 = O.counts + pos * SPG_NCOUNT;
-    double *gl = F.table ? O.gl + pos * NSLOT : sink;     // scratch-free sink
-    if (F.table) {
-        O.depth[pos] = live ? a.depth : 0u;
-        O.order[pos] = live ? a.order : 0u;
-        O.first[pos] = live ? a.first_batch : 0u;
-#pragma unroll
-        for (int k = 0; k < NSLOT; k++) { cnt8[k] = live ? a.cnt[k] : 0u; gl[k] = NaN; }
-        cnt8[5] = live ? a.n_del : 0u; cnt8[6] = live ? a.n_skip : 0u; cnt8[7] = live ? a.n_other : 0u;
-    }
-    if (!live) { if (F.table) O.flags[pos] = 0; return false; }
-    uint8_t flags = SPG_F_PRESENT;
-    const bool evaluated = (int64_t)a.depth >= (int64_t)F.min_td;   // :131
-    if (evaluated) flags |= SPG_F_EVALUATED;
-    if (a.misc & MISC_EXOTIC) {       // IUPAC / '=' alleles: the exact replay tabulates every allele
-        if (F.table) O.flags[pos] = flags | SPG_F_EXOTIC | SPG_F_REPLAYED;
-        return true;
-    }
-    if (!evaluated) { if (F.table) O.flags[pos] = flags; return false; }
-    const int n = (int)(a.order & 7u);
-    const uint32_t skip = (a.misc >> MISC_SKIP_SHIFT) & 0x1Fu;
-    uint32_t slot[NSLOT], cnts[NSLOT];
-    LV Pv[NSLOT], Hv[NSLOT];
-    double Sv[NSLOT];
-    // per-allele P (= prod eps, utils.py:19) and H (= prod 1-eps, utils.py:17) in dict order
-#pragma unroll
-    for (int k = 0; k < NSLOT; k++) {
-        slot[k] = (a.order >> (3 + 3 * k)) & 7u;
-        cnts[k] = 0; Sv[k] = 0.0; Pv[k] = lv_normal(1.0, 0.0); Hv[k] = lv_normal(1.0, 0.0);
-        if (k >= n) continue;              // only the alleles present (no exp for empty slots)
-        uint32_t c_ = 0, sq = 0, qf = 0; double sl = 0.0, se = 0.0;
-#pragma unroll
-        for (int j = 0; j < NSLOT; j++)
-            if (slot[k] == (uint32_t)j) { c_ = a.cnt[j]; sq = a.sq[j]; qf = a.qf[j]; sl = a.sl[j]; se = a.se[j]; }
-        cnts[k] = c_;
-        Sv[k] = se;
-        // P: log10 P = -sum(q)/10 up to (n+2) ulp; exact zero proven when every factor < 1/2
-        if (sq <= 3076u) Pv[k] = lv_normal(T->p10k[sq / 10u] * T->eps[sq % 10u], -(double)sq * LOG2_10_OVER_10);
-        else if (sq >= 3245u && qf >= 4u) Pv[k] = lv_zero();
-        else Pv[k] = lv_band(-1022.0 + 2 * MARGIN);
-        // H: exp(sum ln(1-eps)); exactly 0 when a Q0 entry is present (1 - 1.0 == 0)
-        if (qf == 0u) Hv[k] = lv_zero();
-        else if ((skip >> slot[k]) & 1u) Hv[k] = lv_unknown();
-        else {
-            const double l2 = sl * INV_LN2;
-            Hv[k] = l2 > -1022.0 + MARGIN ? lv_normal(exp(sl), l2) : lv_band(-1022.0 + 2 * MARGIN);
-        }
-    }
-    double G[NSLOT];
-    bool band = false, unknown = false, cand_needs_s = false;
-#pragma unroll
-    for (int h = 0; h < NSLOT; h++) {
-        // N = ((1.0 * P_a1) * P_a2) ... over a != h in dict order (utils.py:18-22), GL = H * N
-        LV c = lv_normal(1.0, 0.0);
-#pragma unroll
-        for (int j = 0; j < NSLOT; j++)
-            if (j != h && j < n) c = lv_mul(c, Pv[j]);
-        const LV g = lv_mul(Hv[h], c);
-        if (h < n && g.s == 2) band = true;
-        G[h] = g.s == 0 ? g.v : (g.s == 3 ? NaN : 0.0);
-        if (h < n && g.s == 3) unknown = true;
-        // a candidate needs S = sum(GL) unless its own GL is exactly 0 (SCORE = 0 for any S)
-        if (h < n && g.s != 1 && is_candidate(F, a, slot_code((int)slot[h]), cnts[h])) {
-            cand_needs_s = true;
-            if (g.s == 3) band = true;        // its own GL depends on terms not accumulated
-        }
-    }
-    // unknown (not accumulated) GL terms only matter if a call needs S: then replay exactly
-    if (band || (unknown && cand_needs_s)) {
-        if (F.table) O.flags[pos] = flags | SPG_F_REPLAYED;
-        return true;
-    }
-    if (unknown) flags |= SPG_F_PARTIAL;
-    double S = 0.0;
-#pragma unroll
-    for (int k = 0; k < NSLOT; k++)
-        if (k < n && !unknown) S = S + G[k];                 // :145
-    if (S == 0) S = 1.0;                                     // :146 (every call has GL 0 if unknown)
-#pragma unroll
-    for (int k = 0; k < NSLOT; k++) {
-        if (k < n) {
-#pragma unroll
-            for (int j = 0; j < NSLOT; j++)
-                if (slot[k] == (uint32_t)j) gl[j] = G[k];
-            const uint32_t code = slot_code((int)slot[k]);
-            if (is_candidate(F, a, code, cnts[k])) {
-                write_candidate(F, O, pos, a, k, code, cnts[k], G[k], S, Sv[k] / (double)cnts[k]);
-                flags |= SPG_F_CANDIDATE;
-            }
-        }
-    }
-    if (F.table) O.flags[pos] = flags;
-    return false;
-}
-
 // One wave per 64 positions: each lane runs prepare_variants' per-position logic; positions that need
 // the exact replay are then replayed one after another by the whole wave.
 template <bool SPARSE>
@@ -1447,7 +1516,7 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
         for (int64_t i0 = (int64_t)blockIdx.x * 64; i0 < n; i0 += (int64_t)gridDim.x * 64) {
             const int64_t i = i0 + lane;
             const int64_t pos = i < n ? F.list[i] : 0;
-            const bool need = i < n && finalize_position(F, acc, T, O, pos, sink[lane]);
+            const bool need = i < n && finalize_position<false>(F, acc + pos, T, O, pos, sink[lane]);
             uint64_t rb = __ballot(need);
             if (rb == 0) continue;
             if (need) atomicAdd(&O.ctr[F.cslot].n_band, 1u);
@@ -1461,13 +1530,13 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
                 rb &= rb - 1;
                 const int64_t pj = (int64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)pos, j) |
                                    ((int64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)((uint64_t)pos >> 32), j) << 32);
-                replay_wave(F, H, acc, O, pj, &ws, eps_s);
+                replay_wave(F, H, acc + pj, O, pj, &ws, [&](uint32_t q) { return eps_s[q]; });
             }
         }
         return;
     }
     const int64_t pos = (int64_t)blockIdx.x * 64 + lane;
-    const bool need = pos < F.n_pos && finalize_position(F, acc, T, O, pos, sink[lane]);
+    const bool need = pos < F.n_pos && finalize_position<false>(F, acc + pos, T, O, pos, sink[lane]);
     uint64_t rb = __ballot(need);
     if (rb == 0) return;
     if (need) atomicAdd(&O.ctr[F.cslot].n_band, 1u);
@@ -1476,7 +1545,8 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
     while (rb) {
         const int j = (int)__builtin_ctzll(rb);
         rb &= rb - 1;
-        replay_wave(F, H, acc, O, (int64_t)blockIdx.x * 64 + j, &ws, eps_s);
+        const int64_t pj = (int64_t)blockIdx.x * 64 + j;
+        replay_wave(F, H, acc + pj, O, pj, &ws, [&](uint32_t q) { return eps_s[q]; });
     }
 }
 
@@ -1494,14 +1564,19 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
     const bool w4 = P.t_deep <= 1;
     // batches far beyond the 256 MiB Infinity Cache stream with non-temporal loads
     const bool nt = 2 * P.n_entries > (192ull << 20);
-#define SPG_SEG(WW, FF, NN) hipLaunchKernelGGL((k_acc_seg<WW, FF, SPG_SEG_WPE, NN>), dim3((unsigned)blocks), dim3(64 * KW), 0, st, P, off, code, qual, ref, T, acc)
-    if (w4) {
+#define SPG_SEG(WW, FF, NN) hipLaunchKernelGGL((k_acc_seg<WW, FF, SPG_SEG_WPE, NN, false>), dim3((unsigned)blocks), dim3(64 * KW), 0, st, P, off, code, qual, ref, T, acc)
+#define SPG_SEGF(NN) hipLaunchKernelGGL((k_acc_seg<4, true, SPG_SEG_WPE, NN, true>), dim3((unsigned)blocks), dim3(64 * KW), 0, st, P, off, code, qual, ref, T, acc)
+    if (P.fused) {            // fused accumulate + calls-only finalize (FRESH deep batch, G <= NB)
+        if (!w4 || !fresh || P.G > (uint32_t)NB) return hipErrorInvalidValue;
+        if (nt) SPG_SEGF(true); else SPG_SEGF(false);
+    } else if (w4) {
         if (nt) { if (fresh) SPG_SEG(4, true, true); else SPG_SEG(4, false, true); }
         else { if (fresh) SPG_SEG(4, true, false); else SPG_SEG(4, false, false); }
     } else {
         if (fresh) SPG_SEG(1, true, false); else SPG_SEG(1, false, false);
     }
 #undef SPG_SEG
+#undef SPG_SEGF
     return hipGetLastError();
 }
 

@@ -86,6 +86,9 @@ def _vs_oracle(reference, batches, p, check_mem=True, calls_only=False, eng=None
         orc.accumulate(pb, off, c, q)
     eng.finalize()
     orc.finalize()
+    # calls-only: the call table of THIS finalize (a single deep batch runs it fused into k_acc_seg);
+    # table() below re-finalizes with the per-position table
+    first_calls = eng.variants() if calls_only else None
     if check_mem:
         assert eng.memory_summary() == orc.memory_summary()
     t = eng.table()
@@ -108,6 +111,8 @@ def _vs_oracle(reference, batches, p, check_mem=True, calls_only=False, eng=None
     else:
         _cmp_gl(eng.gl_table(), orc.gl_table(), replayed)
     compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
+    if first_calls is not None:
+        compare_variants(first_calls, orc.variants(), rtol=RTOL)
     return eng, orc
 
 
@@ -411,3 +416,47 @@ def test_full_size_count_conservation(depth):
     del dc, dq, do
     b.close()
     torch.cuda.empty_cache()
+
+
+def _plant_many(batch, pos, code, q, n):
+    """Append n entries (code, q) at the end of column `pos` of a CSR batch."""
+    pb, off, c, qq = batch
+    at = int(off[pos - pb + 1])
+    c = np.insert(c, at, np.full(n, code, np.uint8))
+    qq = np.insert(qq, at, np.full(n, q, np.uint8))
+    off = off.copy()
+    off[pos - pb + 1:] += np.uint64(n)
+    return pb, off, c, qq
+
+
+@pytest.mark.parametrize("depth", [1000, 10000])
+def test_fused_deep_finalize_replays(depth):
+    """A calls-only sample whose only batch is deep: spg_finalize runs accumulate + prepare_variants in
+    ONE launch (k_acc_seg<..., FUSE>).  Planted IUPAC alleles (a call 'R' and a lone 'M': exotic, exact
+    replay) and a P product in the subnormal band (exact replay) are resolved by the finishing waves;
+    calls equal the oracle's, the fused launch leaves the records complete for a later table, and a
+    second finalize (k_finalize) returns the same calls."""
+    from covid_spings_variant_caller_amd import synth
+    L = 4000
+    ref = synth.reference(L, seed=71)
+    b = synth.pileup(L, depth, seed=72, ref=ref, snv_every=53, lo=500, hi=1700)
+    d = depth // 5
+    b = _plant_many(b, 800, 5, 35, d)                        # 'R' x 20 %: an IUPAC call
+    b = _plant_many(b, 801, 3, 33, 1)                        # one 'M': exotic, replayed, no call
+    alt = 2 if ref[900] != "C" else 4
+    b = _plant_many(b, 900, alt, 31, 100)                    # sum q = 3100: P in the subnormal band
+    orc = COracle(ref, 30, 10, 5, 0.01)
+    eng = _engine(ref, dict(DEF, minEvidenceRatio=0.01), calls_only=True)
+    eng.accumulate(*b)
+    orc.accumulate(*b)
+    eng.finalize()
+    orc.finalize()
+    fused = eng.variants()
+    compare_variants(fused, orc.variants(), rtol=RTOL)
+    assert any(v["alleles"][1] == "R" for v in fused)
+    eng.finalize()                                           # records complete: the unfused finalize agrees
+    compare_variants(eng.variants(), fused, rtol=0)
+    assert eng.memory_summary() == orc.memory_summary()
+    t = eng.table()
+    assert t["flags"][800] & 12 == 12 and t["flags"][801] & 12 == 12   # exotic + replayed
+    eng.close()
