@@ -78,6 +78,7 @@ struct KParams {
     const uint32_t *fsamp; // multi-sample batch: per column, the first sample holding entries (else null)
     uint32_t *dbg;         // SPG_TRACE: range violations recorded here instead of faulting (else null)
     uint4 *prog;           // SPG_TRACE: per-wave progress records in host-mapped memory (else null)
+    uint4 *wtime;          // SPG_WAVE_TIMES: per wave {start, setup done, end} (s_memrealtime, 100 MHz), hw id
 };
 
 // Per-position state of one lane of k_acc_multi over a run of batches (lane-private, in LDS), and

@@ -782,6 +782,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         }
     };
     prog(1, (uint32_t)g0, (uint32_t)ng, 0);
+    // SPG_WAVE_TIMES (profiling): wave timeline in s_memrealtime ticks
+    const uint64_t wt0 = P.wtime ? __builtin_amdgcn_s_memrealtime() : 0;
+    uint64_t wt1 = 0;
     WaveRare *RR = rare[threadIdx.x >> 6];             // rare records of the ring's columns
     ColSum *CS = csum[threadIdx.x >> 6];
     Dual2 *D2 = dual2 + (threadIdx.x >> 6);
@@ -913,6 +916,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         return p_a + (ii - p_pre) * STEP + lo;
     };
 
+    if (P.wtime) wt1 = __builtin_amdgcn_s_memrealtime();
     // register ring of three chunks: two loads stay in flight while one chunk is processed
     V c0, q0, c1, q1, c2, q2;
 #define SPG_LD(C, Q, I) do { const uint32_t o_ = chunk_off(I); C = bload<W, NT>(rc, o_); Q = bload<W, NT>(rq, o_); } while (0)
@@ -1150,6 +1154,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         if (__ballot(maybe))
             fused_tail(P.fused->F, P.fused->O, T, P.pos_begin + g0, maybe ? nfin : 0u, CS, img,
                        reinterpret_cast<ReplayWs *>(Q), &hdl, lut);
+    }
+    if (P.wtime && lane == 0) {
+        const uint64_t wt2 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
+        P.wtime[wave] = make_uint4((uint32_t)wt0, (uint32_t)(wt1 - wt0), (uint32_t)(wt2 - wt0), (hw & 0xFFFFFu) | (xcc << 24));
     }
     prog(6, 0, 0, 0);
 }

@@ -121,6 +121,27 @@ def test_checkpoint_roundtrip(planted):
     b.process_bam(files[1])                      # resume: live mode (vc_queue.py:134-144)
     a.process_bam(files[1])
     compare_variants(b.prepare_variants(), a.prepare_variants(), 0.0)
+    # and against the oracle chain that never checkpointed: calls and the memory view after resume
+    o = _oracle(ref, files)
+    compare_variants(b.prepare_variants(), o.prepare_variants(), RTOL)
+    mem = b.memory
+    assert list(mem) == list(o.memory)
+    assert all(mem[p] == o.memory[p] for p in o.memory)
+
+
+def test_checkpoint_resume_into_fresh_process_state(planted):
+    """A checkpoint taken before any BAM, and one loaded into a caller that already holds data
+    (load_checkpoint replaces memory, live_variant_caller.py:48-52), both match the oracle."""
+    d, ref, fasta, files = planted
+    a = _caller(fasta)
+    ck0 = str(d / "ck0.npz")
+    a.create_checkpoint(ck0)
+    b = _caller(fasta)
+    b.process_bam(files[0])
+    b.load_checkpoint(ck0)                       # back to an empty memory
+    assert b.memory == {} and b.prepare_variants() == []
+    b.process_bam(files[1])
+    compare_variants(b.prepare_variants(), _oracle(ref, files[1:]).prepare_variants(), RTOL)
 
 
 def test_reset_memory(planted):

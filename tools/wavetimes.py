@@ -1,0 +1,88 @@
+"""Per-wave timeline of the deep accumulate kernel (profiling; SPG_WAVE_TIMES instrumentation).
+
+Runs the bench's 10,000x SARS-CoV-2 batch through the fused accumulate a few times with
+SPG_WAVE_TIMES=<file> (k_acc_seg records per wave: start, setup done, end in s_memrealtime ticks of
+10 ns, and HW_ID / XCC_ID), then reports the launch's span, the wave generations, setup and lifetime
+distributions, and how the tail ends.  Usage: python tools/wavetimes.py [depth] [out.json]
+"""
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def run(depth, path):
+    import torch
+    import spings  # noqa: F401
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.pileup import synth_batch
+    L = 29903
+    ref = synth.reference(L, seed=1)
+    b = synth_batch(ref, depth, seed=2, n_threads=16)
+    dc = torch.from_numpy(b.codes_padded).cuda()
+    dq = torch.from_numpy(b.quals_padded).cuda()
+    do = torch.from_numpy(b.offsets.view(np.int64).copy()).cuda()
+    eng = PileupEngine(L, 30, 10, 5, 0.10, device=0, reference=ref, calls_only=True)
+    for _ in range(4):
+        eng.reset()
+        eng.accumulate(0, do, dc, dq, borrow=True, n_entries=b.n_entries)
+        eng.finalize()
+    eng.sync()
+    eng.close()
+
+
+def analyse(path):
+    raw = open(path, "rb").read()
+    at, launches = 0, []
+    while at < len(raw):
+        n, g = np.frombuffer(raw[at:at + 16], np.int64)
+        at += 16
+        w = np.frombuffer(raw[at:at + 16 * n], np.uint32).reshape(n, 4)
+        at += 16 * int(n)
+        launches.append((int(g), w))
+    g, w = launches[-1]
+    t0 = w[:, 0].astype(np.int64)
+    t0 = (t0 - t0.min()) * 10e-3                     # us
+    setup = w[:, 1] * 10e-3
+    life = w[:, 2] * 10e-3
+    end = t0 + life
+    xcc = w[:, 3] >> 24
+    span = float(end.max())
+    q = lambda a: {p: round(float(np.percentile(a, p)), 2) for p in (5, 25, 50, 75, 95, 100)}
+    res = {"waves": int(len(w)), "G": g, "span_us": round(span, 2),
+           "start_us": q(t0), "setup_us": q(setup), "life_us": q(life), "end_us": q(end),
+           "waves_ending_after_span_minus_5us": int((end > span - 5).sum()),
+           "waves_starting_after_span_minus_10us": int((t0 > span - 10).sum()),
+           "busy_wave_us_over_span": round(float(life.sum()) / span, 1),
+           "per_xcc_span_us": {int(x): round(float(end[xcc == x].max() - t0[xcc == x].min()), 2)
+                               for x in np.unique(xcc)}}
+    hist, edges = np.histogram(t0, bins=20, range=(0, span))
+    res["start_histogram"] = hist.tolist()
+    conc = [int(((t0 <= t) & (end > t)).sum()) for t in np.linspace(0, span, 23)[1:-1]]
+    res["resident_waves_over_time"] = conc
+    return res
+
+
+if __name__ == "__main__":
+    depth = float(sys.argv[1]) if len(sys.argv) > 1 else 10000.0
+    out = sys.argv[2] if len(sys.argv) > 2 else None
+    path = os.environ.get("SPG_WAVE_TIMES")
+    if not path:
+        path = os.path.join(tempfile.mkdtemp(), "wt.bin")
+        os.environ["SPG_WAVE_TIMES"] = path
+        import subprocess
+        r = subprocess.run([sys.executable, __file__, str(depth)] + ([out] if out else []), env=os.environ)
+        sys.exit(r.returncode)
+    if os.path.exists(path):
+        os.remove(path)
+    run(depth, path)
+    res = analyse(path)
+    print(json.dumps(res, indent=1))
+    if out:
+        json.dump(res, open(out, "w"), indent=1)
