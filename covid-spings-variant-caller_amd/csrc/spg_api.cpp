@@ -527,11 +527,37 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     P.n_entries = hb.n_entries;
     P.dbg = trace_on() ? trace_dbg() : nullptr;
     P.prog = trace_prog((n_cols + G - 1) / G + 4);
+    // SPG_WAVE_TIMES=<file> (profiling, tools/wavetimes.py): per-wave timeline of each deep launch
+    // appended to <file> (the launch is synchronised)
+    static const char *wt_file = getenv("SPG_WAVE_TIMES");
+    static uint4 *wt_buf = nullptr;
+    static int64_t wt_cap = 0;
+    const int64_t n_waves = (n_cols + G - 1) / G;
+    if (wt_file && deep_batch) {
+        if (n_waves > wt_cap) {
+            if (wt_buf) HIPCHK(hipFree(wt_buf));
+            HIPCHK(hipMalloc(&wt_buf, sizeof(uint4) * n_waves));
+            wt_cap = n_waves;
+        }
+        HIPCHK(hipMemsetAsync(wt_buf, 0, sizeof(uint4) * n_waves, c->stream));
+        P.wtime = wt_buf;
+    }
     if (F) P.fused = c->d_fused + F->cslot;
     P.min_td = c->p.min_total_depth;
     P.min_ad = c->p.min_allele_depth;
     P.ratio_lo = c->p.min_evidence_ratio * (1.0 - 1e-9);
     HIPCHK(launch_accumulate(P, hb.off, hb.code, hb.qual, c->ref, c->tables, c->acc, c->stream));
+    if (P.wtime) {
+        std::vector<uint4> h((size_t)n_waves);
+        HIPCHK(hipMemcpyAsync(h.data(), P.wtime, sizeof(uint4) * n_waves, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (FILE *f = fopen(wt_file, "ab")) {
+            const int64_t hdr[2] = {n_waves, (int64_t)G};
+            fwrite(hdr, sizeof hdr, 1, f);
+            fwrite(h.data(), sizeof(uint4), h.size(), f);
+            fclose(f);
+        }
+    }
     return trace_sync(c, F ? "accumulate + finalize (k_acc_seg, fused)" : "accumulate (k_acc_seg)");
 }
 
