@@ -21,6 +21,8 @@ hipError_t launch_finalize(const FParams &F, const Acc *acc, const Tables *T, co
                            hipStream_t st);
 hipError_t launch_multi(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, bool nt,
                         int64_t max_blocks, bool fused, hipStream_t st);
+hipError_t launch_one(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc,
+                      int64_t max_blocks, bool fused, hipStream_t st);
 }  // namespace spg
 
 using namespace spg;
@@ -114,6 +116,9 @@ struct spg_ctx {
     uint64_t pend_entries = 0;
     uint32_t *kerr = nullptr;           // k_acc_multi error word (a batch too deep for a run)
     uint32_t *nlist = nullptr;          // fused run: positions listed for the sparse finalize (in `band`)
+    uint32_t *deep_list = nullptr;      // single shallow batch: its long columns (for k_acc_seg<1>) ...
+    int64_t deep_cap = 0;
+    uint32_t *deep_n = nullptr;         // ... and their count
     bool stale = false;                 // records of history [0, stale_end) not written (fused run)
     bool deep_pend = false;             // history batch 0 is a deep batch not accumulated yet: a calls-only
                                         // finalize runs it fused (k_acc_seg<..., FUSE>), anything else first
@@ -208,6 +213,7 @@ static int alloc_outputs(spg_ctx *c) {
     HIPCHK(hipMemsetAsync(c->ctr, 0, 2 * sizeof(Counters), c->stream));
     HIPCHK(hipMalloc(&c->kerr, sizeof(uint32_t)));
     HIPCHK(hipMalloc(&c->nlist, sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&c->deep_n, sizeof(uint32_t)));
     HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));
     return 0;
 }
@@ -261,7 +267,7 @@ int spg_destroy(spg_ctx *c) {
     c->arena.release();
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
-                    c->d_fused};
+                    c->d_fused, c->deep_list, c->deep_n};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
@@ -475,7 +481,8 @@ static void fill_swar(const spg_ctx *c, int32_t &min_bq, int32_t &qlo, uint32_t 
 
 // k_acc_seg over one batch (every column of a deep batch; the long columns of a shallow one).  F/O:
 // fused with the calls-only finalize (FRESH deep batch, the sample's only one).
-static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F = nullptr, const Out *O = nullptr) {
+static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F = nullptr, const Out *O = nullptr,
+                      bool listed = false) {
     if (F) {
         // finalize parameters in device memory (the kernel reads them after its loop); epoch and Counters
         // slot travel in KParams, everything else changes only when the result buffers grow
@@ -526,7 +533,12 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
     P.n_entries = hb.n_entries;
     P.dbg = trace_on() ? trace_dbg() : nullptr;
-    P.prog = trace_prog((n_cols + G - 1) / G + 4);
+    if (listed) {                 // the long columns k_acc_multi listed, one per wave
+        P.G = 1;
+        P.deep_list = c->deep_list;
+        P.deep_n = c->deep_n;
+    }
+    P.prog = trace_prog(listed ? 2048 * 4 + 4 : (n_cols + G - 1) / G + 4);
     // SPG_WAVE_TIMES=<file> (profiling, tools/wavetimes.py): per-wave timeline of each deep launch
     // appended to <file> (the launch is synchronised)
     static const char *wt_file = getenv("SPG_WAVE_TIMES");
@@ -610,6 +622,9 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
     P.t_deep = K == 1 ? 128u : 0u;
     P.fresh = h0 == 0 ? 1u : 0u;
+    uint64_t run_entries = 0;
+    for (int64_t i = h0; i < h1; i++) run_entries += c->hist[(size_t)i].n_entries;
+    P.ref_sl = P.calls_only && (double)run_entries < 200.0 * (double)(u1 - u0) ? 1u : 0u;
     P.err = c->kerr;
     if (fused) {
         if (S != 1 || h0 != 0) return fail("spg: internal: fused run must be one FRESH unsplit run");
@@ -631,12 +646,34 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
         }
         P.part = c->part;
     }
+    if (K == 1) {
+        // list of the batch's long columns (each has >= 128 entries: at most E / 128 of them)
+        const HistBatch &hb = c->hist[(size_t)h0];
+        const int64_t cap = std::min<int64_t>(hb.n_cols, (int64_t)(hb.n_entries / 128) + 1);
+        if (cap > c->deep_cap) {
+            if (c->deep_list) { HIPCHK(hipStreamSynchronize(c->stream)); HIPCHK(hipFree(c->deep_list)); }
+            c->deep_list = nullptr;
+            c->deep_cap = 0;
+            HIPCHK(hipMalloc(&c->deep_list, sizeof(uint32_t) * cap));
+            c->deep_cap = cap;
+        }
+        HIPCHK(hipMemsetAsync(c->deep_n, 0, sizeof(uint32_t), c->stream));
+        P.deep_list = c->deep_list;
+        P.deep_n = c->deep_n;
+    }
     static const int64_t max_blocks = env_i64("SPG_MULTI_BLOCKS", 6144);
-    HIPCHK(launch_multi(P, c->d_hist, c->ref, c->tables, c->acc, nt, max_blocks, fused, c->stream));
+    // a single shallow batch into a FRESH memory (mean column <= 40 entries: the pipelined blocks cover
+    // almost every column): k_acc_one; otherwise the run kernel
+    static const bool no_one = getenv("SPG_NO_ONE") != nullptr;
+    if (K == 1 && h0 == 0 && !no_one && (double)run_entries <= 40.0 * (double)(u1 - u0))
+        HIPCHK(launch_one(P, c->d_hist, c->ref, c->tables, c->acc, max_blocks, fused, c->stream));
+    else
+        HIPCHK(launch_multi(P, c->d_hist, c->ref, c->tables, c->acc, nt, max_blocks, fused, c->stream));
     if (int rc = trace_sync(c, "accumulate (k_acc_multi)")) return rc;
     if (K == 1) {
-        // a single shallow batch: its long columns (>= 128 entries) go through the wave-wide kernel
-        if (int rc = launch_seg(c, h0, false)) return rc;
+        // a single shallow batch: its long columns (>= 128 entries), listed by k_acc_multi, go through the
+        // wave-wide kernel
+        if (int rc = launch_seg(c, h0, false, nullptr, nullptr, true)) return rc;
     }
     return acc_end(c);
 }

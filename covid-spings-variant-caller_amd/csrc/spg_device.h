@@ -78,6 +78,8 @@ struct KParams {
     const uint32_t *fsamp; // multi-sample batch: per column, the first sample holding entries (else null)
     uint32_t *dbg;         // SPG_TRACE: range violations recorded here instead of faulting (else null)
     uint4 *prog;           // SPG_TRACE: per-wave progress records in host-mapped memory (else null)
+    const uint32_t *deep_list;   // W = 1: the long columns k_acc_multi listed (batch-relative) ...
+    const uint32_t *deep_n;      // ... and their count (null: one group of G columns per wave)
     uint4 *wtime;          // SPG_WAVE_TIMES: per wave {start, setup done, end} (s_memrealtime, 100 MHz), hw id
 };
 
@@ -110,8 +112,13 @@ struct MParams {             // one k_acc_multi launch: history batches [h0, h0 
     uint32_t calls_only;
     uint32_t t_deep;         // K == 1: columns with >= t_deep entries are left to k_acc_seg (0 = none)
     uint32_t fresh;          // seq0 == 1: no record of this epoch exists yet
+    uint32_t ref_sl;         // calls-only, shallow run: still sum ln(1-eps) for a REF-char major (at such
+                             // depths a call's GL is not 0, its SCORE needs S = sum(GL), which needs the
+                             // REF allele's H; skipping it would send every call to the exact replay)
     MState *part;            // S > 1: partial records [S][n_groups * 64]
     uint32_t *err;           // bit 0: a 64-column window of a run's batch held >= 2^30 entries (not run)
+    uint32_t *deep_list;     // K == 1: columns with >= t_deep entries, listed for k_acc_seg<1> ...
+    uint32_t *deep_n;        // ... and their count
     // FUSED (a FRESH run folded at spg_finalize, calls-only): a record is written only for positions that
     // can produce a call (prepare_variants' filters :131, :151-157) or need the exact replay; they are
     // listed for the sparse finalize

@@ -767,9 +767,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     __syncthreads();
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * KW + (threadIdx.x >> 6);
-    const int64_t g0 = wave * P.G;
-    if (g0 >= P.n_cols) return;
-    const int ng = (int)min((int64_t)P.G, P.n_cols - g0);
+    // deep_list (the long columns of a shallow batch): the waves stride over the listed columns, one
+    // column each; otherwise one group of G consecutive columns per wave
+    const bool listed = P.deep_n != nullptr;
+    const int64_t n_items = listed ? (int64_t)*P.deep_n : wave + 1;
+    const int64_t istride = listed ? (int64_t)gridDim.x * KW : 1;
+    for (int64_t item = wave; item < n_items; item += istride) {
+    const int64_t g0 = listed ? (int64_t)P.deep_list[item] : wave * P.G;
+    if (g0 >= P.n_cols) continue;
+    const int ng = listed ? 1 : (int)min((int64_t)P.G, P.n_cols - g0);
     // SPG_TRACE: lane 0 posts (stage, a, b, c) to host-mapped memory, so a fault leaves each wave's
     // last step readable by the host
     auto prog = [&](uint32_t stage, uint32_t a, uint32_t b, uint32_t c) {
@@ -888,7 +894,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     }
     const uint32_t total = __builtin_amdgcn_readlane(pre, 63);   // SGPR: loop bounds stay scalar
     pre -= nch;
-    if (total == 0) return;
+    if (total == 0) continue;
     // Column descriptors of the columns with chunks, compacted into LDS; the loop walks them with
     // two scalar cursors (consumption and prefetch), so no per-lane descriptor stays in a VGPR.
     {
@@ -1162,6 +1168,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         P.wtime[wave] = make_uint4((uint32_t)wt0, (uint32_t)(wt1 - wt0), (uint32_t)(wt2 - wt0), (hw & 0xFFFFFu) | (xcc << 24));
     }
     prog(6, 0, 0, 0);
+    }   // items
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1213,6 +1220,13 @@ __device__ __forceinline__ void lut_sums(uint32_t qw, uint32_t sel80, const doub
     se += (t0.y + t1.y) + (t2.y + t3.y);
 }
 
+// sum of ln(1-eps) only (calls-only REF major of a shallow run: its sum(eps) is never used, the REF
+// allele is never a call): 8-B rows, half the LDS traffic of lut_sums
+__device__ __forceinline__ void lut_sl(uint32_t qw, uint32_t sel80, const double *__restrict__ l1m, double &sl) {
+    const uint32_t idx = (qw & 0x7F7F7F7Fu) ^ sel80 ^ 0x80808080u;
+    sl += (l1m[idx & 0xFFu] + l1m[(idx >> 8) & 0xFFu]) + (l1m[(idx >> 16) & 0xFFu] + l1m[idx >> 24]);
+}
+
 // MBLK: 16-B blocks per lane per load round (MBLK x 16 entries)
 // prepare_variants' filters on a position's totals (:131, :151-157), a superset of the early exit
 // k_finalize takes in calls-only mode: false = the position can produce no call and needs no replay
@@ -1239,9 +1253,12 @@ __global__ __launch_bounds__(64 * MW) __attribute__((amdgpu_waves_per_eu(FUSED ?
                                                        const Tables *__restrict__ T, Acc *__restrict__ acc) {
     // rows 0..127 {ln(1-eps), eps} for q < 128; rows 128..255 zero (the index of non-selected bytes)
     __shared__ double2 lut[256];
+    __shared__ double l1m8[256];                       // ln(1-eps) rows of the same layout (P.ref_sl)
     __shared__ MState st[MW][64];
-    for (uint32_t q = threadIdx.x; q < 256u; q += 64u * MW)
+    for (uint32_t q = threadIdx.x; q < 256u; q += 64u * MW) {
         lut[q] = q < 128u ? make_double2(T->fast[q][0], T->fast[q][1]) : make_double2(0.0, 0.0);
+        l1m8[q] = q < 128u ? T->fast[q][0] : 0.0;
+    }
     __syncthreads();
     const int lane = threadIdx.x & 63;
     MState *ST = st[threadIdx.x >> 6];
@@ -1287,9 +1304,12 @@ __global__ __launch_bounds__(64 * MW) __attribute__((amdgpu_waves_per_eu(FUSED ?
         SPG_ITEM_HEAD(item + istride);
         const uint32_t M = code_of_ref(refc), mrep = M * 0x01010101u;
         const int Ms = slot_of(M);
-        // calls-only: no likelihood sums for a REF-char major (never a candidate)
+        // calls-only: no likelihood sums for a REF-char major (never a candidate) — except its
+        // sum(ln(1-eps)) in shallow runs (P.ref_sl)
         const bool msum = !P.calls_only || nibble_char(M) != refc;
         const bool any_msum = __ballot(msum && inr) != 0;
+        const bool rsl = !msum && P.ref_sl;
+        const bool any_rsl = __ballot(rsl && inr) != 0;
         int s2 = -1;                                   // slot of the promoted second allele
         // no second allele: code 0x7F matches nothing (the SWAR compare needs code ^ M < 0x80)
         uint32_t mrep2 = 0x7F7F7F7Fu;
@@ -1318,6 +1338,17 @@ __global__ __launch_bounds__(64 * MW) __attribute__((amdgpu_waves_per_eu(FUSED ?
             if (__ballot(cov) == 0) continue;
             uint32_t len = (uint32_t)(oe - ob);
             if (P.t_deep && len >= P.t_deep) { deep = true; len = 0; }   // k_acc_seg takes this column
+            if (P.deep_list) {                         // list the long columns for k_acc_seg<1>
+                const uint64_t dm = __ballot(cov && deep);
+                if (dm) {
+                    uint32_t at = 0;
+                    if (lane == 0) at = atomicAdd(P.deep_n, (uint32_t)__popcll(dm));
+                    at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
+                    if (cov && deep)
+                        P.deep_list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u))] = (uint32_t)col;
+                }
+            }
             if (len && S.fb == INF32) S.fb = (uint32_t)k;
             const uint64_t a0 = ob & ~(uint64_t)15;
             const int32_t lead = (int32_t)(ob - a0);
@@ -1377,6 +1408,7 @@ __global__ __launch_bounds__(64 * MW) __attribute__((amdgpu_waves_per_eu(FUSED ?
                         fcnt += __popc(f80);
                         fsq = __builtin_amdgcn_udot4(q_, f80 >> 7, fsq, false);
                         if (any_msum) lut_sums(q_, msum ? f80 : 0u, lut, fsl, fse);
+                        if (any_rsl) lut_sl(q_, rsl ? f80 : 0u, l1m8, fsl);
                         if (ffirst == INF32 && f80)
                             ffirst = sidx + (uint32_t)(x0 + 4 * d) + ((uint32_t)__builtin_ctz(f80) >> 3);
                         while (r80) {
@@ -1406,6 +1438,7 @@ __global__ __launch_bounds__(64 * MW) __attribute__((amdgpu_waves_per_eu(FUSED ?
             S.qf[Ms] = (uint8_t)min((uint32_t)S.qf[Ms], (uint32_t)P.qlo);
             S.first[Ms] = min(S.first[Ms], ffirst);
             if (msum) { S.sl[Ms] += fsl; S.se[Ms] += fse; }
+            else if (P.ref_sl) S.sl[Ms] += fsl;        // sum(eps) of the REF allele: never read (no call)
             else S.skip |= (uint8_t)(1u << Ms);
         }
         if (gcnt) {
@@ -1462,6 +1495,215 @@ __global__ __launch_bounds__(64 * MW) __attribute__((amdgpu_waves_per_eu(FUSED ?
         wave_sync();
     }
 #undef SPG_ITEM_HEAD
+}
+
+// ------------------------------------------------------------------------------------------
+// k_acc_one: a single shallow batch into a FRESH memory (the first BAM of a sample: process_bam's
+// columns, live_variant_caller.py:54-103, once).  One lane per position, one wave per 64-column tile,
+// like k_acc_multi, but with a two-tile software pipeline: a tile's CSR bounds are loaded two tiles
+// ahead and its first ONE_BLK 16-B blocks one tile ahead, so a wave keeps the next tile's data in
+// flight while it classifies the current one (k_acc_multi, built for runs of many batches, exposes one
+// memory latency per tile).  Longer columns take extra blocks synchronously; columns with >= t_deep
+// entries are listed for k_acc_seg<1>.  FUSED: records only for positions that may produce a call.
+// ------------------------------------------------------------------------------------------
+#ifndef SPG_ONE_BLK
+#define SPG_ONE_BLK 4
+#endif
+constexpr int ONE_BLK = SPG_ONE_BLK;
+
+template <bool FUSED>
+__global__ __launch_bounds__(64 * MW) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_acc_one(MParams P, const Hist *__restrict__ H,
+                                                       const uint8_t *__restrict__ ref,
+                                                       const Tables *__restrict__ T, Acc *__restrict__ acc) {
+    __shared__ double2 lut[256];                       // {ln(1-eps), eps}, rows 128..255 zero
+    __shared__ double l1m8[256];                       // ln(1-eps), rows 128..255 zero
+    __shared__ MState st[MW][64];
+    for (uint32_t q = threadIdx.x; q < 256u; q += 64u * MW) {
+        lut[q] = q < 128u ? make_double2(T->fast[q][0], T->fast[q][1]) : make_double2(0.0, 0.0);
+        l1m8[q] = q < 128u ? T->fast[q][0] : 0.0;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    MState &S = st[threadIdx.x >> 6][lane];
+    const Hist h = H[P.h0];
+    const int64_t n_tiles = P.n_groups;
+    const int64_t stride = (int64_t)gridDim.x * MW;
+    int64_t tile = (int64_t)blockIdx.x * MW + (threadIdx.x >> 6);
+
+    // a tile's head: this lane's REF char and column bounds
+    struct Head { uint64_t ob, oe; uint32_t rc; };
+    auto head = [&](int64_t t) -> Head {
+        Head hd{0, 0, (uint32_t)'A'};
+        if (t < n_tiles) {
+            const int64_t p = P.u0 + t * 64 + lane;
+            const int64_t col = p - h.pos_begin;
+            if (p < P.u1 && col >= 0 && col < h.n_cols) {
+                hd.rc = ref[p];
+                hd.ob = __builtin_nontemporal_load(h.off + col);
+                hd.oe = __builtin_nontemporal_load(h.off + col + 1);
+            }
+        }
+        return hd;
+    };
+    // a tile's data: one buffer descriptor per array over the wave's byte range (the 64 columns are
+    // consecutive), ONE_BLK 16-B blocks per lane (lanes past their column read zeros)
+    struct Seg { __amdgpu_buffer_rsrc_t rc, rq; uint32_t vo; };
+    auto seg = [&](const Head &hd, uint32_t &len, int32_t &lead, uint32_t &nblk) -> Seg {
+        len = (uint32_t)(hd.oe - hd.ob);
+        const uint64_t a0 = hd.ob & ~(uint64_t)15;
+        lead = (int32_t)(hd.ob - a0);
+        nblk = len ? (uint32_t)(((uint64_t)lead + len + 15) >> 4) : 0u;
+        const uint64_t covm = __ballot(nblk != 0);
+        Seg sg{column_rsrc(h.code, 0), column_rsrc(h.qual, 0), 0u};
+        if (covm == 0) return sg;
+        const int lf = (int)__builtin_ctzll(covm), ll = 63 - (int)__builtin_clzll(covm);
+        const uint64_t a1 = a0 + 16ull * nblk;
+        const uint64_t wb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)a0, lf) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(a0 >> 32), lf) << 32);
+        const uint64_t we = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)a1, ll) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(a1 >> 32), ll) << 32);
+        if (we - wb >= (1ull << 30)) {                // > 2^30 entries in 64 columns: not a shallow batch
+            if (lane == 0) atomicOr(P.err, 1u);
+            nblk = 0;
+            len = 0;
+            return sg;
+        }
+        sg.rc = column_rsrc(h.code + wb, (uint32_t)(we - wb));
+        sg.rq = column_rsrc(h.qual + wb, (uint32_t)(we - wb));
+        sg.vo = (uint32_t)(a0 - wb);
+        return sg;
+    };
+    auto blk = [&](const Seg &sg, uint32_t nblk, uint32_t u, u32x4 &cw, u32x4 &qw) {
+        const uint32_t o = u < nblk ? sg.vo + 16u * u : 0x80000000u;   // out of range -> zeros
+        cw = __builtin_amdgcn_raw_buffer_load_b128(sg.rc, (int)o, 0, 0);
+        qw = __builtin_amdgcn_raw_buffer_load_b128(sg.rq, (int)o, 0, 0);
+    };
+
+    Head h1 = head(tile), h2 = head(tile + stride);
+    uint32_t len1, nblk1;
+    int32_t lead1;
+    Seg s1 = seg(h1, len1, lead1, nblk1);
+    u32x4 c1[ONE_BLK], q1[ONE_BLK];
+#pragma unroll
+    for (int u = 0; u < ONE_BLK; u++) blk(s1, nblk1, u, c1[u], q1[u]);
+    for (; tile < n_tiles; tile += stride) {
+        // the pipeline: the tile after next's bounds, the next tile's blocks
+        const Head h3 = head(tile + 2 * stride);
+        uint32_t len2, nblk2;
+        int32_t lead2;
+        const Seg s2 = seg(h2, len2, lead2, nblk2);
+        u32x4 c2[ONE_BLK], q2[ONE_BLK];
+#pragma unroll
+        for (int u = 0; u < ONE_BLK; u++) blk(s2, nblk2, u, c2[u], q2[u]);
+
+        // ---- this tile ----
+        const int64_t p = P.u0 + tile * 64 + lane;
+        const bool inr = p < P.u1;
+        ms_init(S);
+        const uint32_t refc = h1.rc;
+        const uint32_t M = code_of_ref((uint8_t)refc), mrep = M * 0x01010101u;
+        const int Ms = slot_of(M);
+        // calls-only: no likelihood sums for a REF-char major (never a call), except its sum(ln(1-eps))
+        // in shallow runs (P.ref_sl)
+        const bool msum = !P.calls_only || nibble_char(M) != (uint8_t)refc;
+        const bool any_msum = __ballot(msum && inr) != 0;
+        const bool rsl = !msum && P.ref_sl;
+        const bool any_rsl = __ballot(rsl && inr) != 0;
+        uint32_t len = len1;
+        bool deep = false;
+        if (P.t_deep && len >= P.t_deep) { deep = true; len = 0; }   // k_acc_seg<1> takes this column
+        const uint64_t dm = __ballot(deep);
+        if (dm) {
+            uint32_t at = 0;
+            if (lane == 0) at = atomicAdd(P.deep_n, (uint32_t)__popcll(dm));
+            at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
+            if (deep)
+                P.deep_list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u))] =
+                    (uint32_t)(p - h.pos_begin);
+        }
+        if (len) S.fb = 0;
+        const uint32_t nblk = len ? nblk1 : 0u;
+        uint32_t mx = nblk;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        mx = __builtin_amdgcn_readfirstlane(mx);
+        uint32_t fcnt = 0, fsq = 0, ffirst = INF32;
+        double fsl = 0.0, fse = 0.0;
+        auto classify = [&](const u32x4 &cw, const u32x4 &qw, uint32_t u) {
+            const int32_t x0 = (int32_t)(16u * u) - lead1;    // column index of the block's byte 0
+            uint32_t vm[4];
+            valid_masks<4>(x0, 0, (int32_t)len, vm);
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                const uint32_t c_ = dw<4>(cw, d), q_ = dw<4>(qw, d);
+                uint32_t f80, r80;
+                swar4(c_, q_, vm[d], mrep, P.kpass, P.kok, f80, r80);
+                fcnt += __popc(f80);
+                fsq = __builtin_amdgcn_udot4(q_, f80 >> 7, fsq, false);
+                if (any_msum) lut_sums(q_, msum ? f80 : 0u, lut, fsl, fse);
+                if (any_rsl) lut_sl(q_, rsl ? f80 : 0u, l1m8, fsl);
+                if (ffirst == INF32 && f80) ffirst = (uint32_t)(x0 + 4 * d) + ((uint32_t)__builtin_ctz(f80) >> 3);
+                while (r80) {
+                    const int sh = __builtin_ctz(r80) - 7;
+                    r80 &= r80 - 1;
+                    const uint32_t c = (c_ >> sh) & 0xFFu, q = (q_ >> sh) & 0xFFu;
+                    if ((int)q >= P.min_bq) ms_rare(S, c, q, (uint32_t)(x0 + 4 * d + (sh >> 3)), lut, T);
+                }
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < ONE_BLK; u++)
+            if ((uint32_t)u < mx) classify(c1[u], q1[u], (uint32_t)u);
+        for (uint32_t u = ONE_BLK; u < mx; u++) {      // a longer column: its further blocks, unpipelined
+            u32x4 cw, qw;
+            blk(s1, nblk, u, cw, qw);
+            classify(cw, qw, u);
+        }
+        if (fcnt) {
+            S.depth += fcnt;
+            S.cnt[Ms] += fcnt;
+            S.qf[Ms] = (uint8_t)min((uint32_t)S.qf[Ms], (uint32_t)P.qlo);
+            S.first[Ms] = min(S.first[Ms], ffirst);
+            S.sq[Ms] = sat_add31(S.sq[Ms], fsq);
+            if (msum) { S.sl[Ms] += fsl; S.se[Ms] += fse; }
+            else if (P.ref_sl) S.sl[Ms] += fsl;        // sum(eps) of the REF allele: never read (no call)
+            else S.skip |= (uint8_t)(1u << Ms);
+        }
+        bool write = inr && !deep && S.fb != INF32;
+        if constexpr (FUSED) {
+            // most positions cannot produce a call: no record, no listing (the context re-materializes the
+            // records from the history if anything needs them later); deep columns are listed here
+            const bool want = inr && (deep || (S.fb != INF32 && may_call(S, (uint8_t)refc, P)));
+            const uint64_t wm = __ballot(want);
+            if (wm) {
+                uint32_t at = 0;                       // one list slot reservation per wave
+                if (lane == 0) at = atomicAdd(P.n_list, (uint32_t)__popcll(wm));
+                at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
+                if (want)
+                    P.list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u))] = p;
+            }
+            write = write && want;
+        }
+        if (write) {                                   // this lane's record (FRESH), 16-B stores
+            Acc a = Acc{};
+            a.epoch = P.epoch;
+            merge_state(a, S, S.first, P.seq0, (uint8_t)refc);
+            const bool sums = record_has_sums(a);
+            uint4 *dst = reinterpret_cast<uint4 *>(acc + p);
+            const uint4 *src = reinterpret_cast<const uint4 *>(&a);
+#pragma unroll
+            for (int t = 0; t < 10; t++)
+                if (t < 5 || sums) dst[t] = src[t];
+        }
+        h1 = h2;
+        h2 = h3;
+        s1 = s2;
+        len1 = len2;
+        lead1 = lead2;
+        nblk1 = nblk2;
+#pragma unroll
+        for (int u = 0; u < ONE_BLK; u++) { c1[u] = c2[u]; q1[u] = q2[u]; }
+    }
 }
 
 // Fold the S partial states of a split run in batch order (first-entry keys (split, stream index)) and
@@ -1569,12 +1811,13 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
                              const uint8_t *ref, const Tables *T, Acc *acc, hipStream_t st) {
     if (P.n_cols == 0) return hipSuccess;
     const int64_t waves = (P.n_cols + P.G - 1) / P.G;
-    const int64_t blocks = (waves + KW - 1) / KW;
+    // listed long columns: a fixed grid strides over the list (its length is on the device)
+    const int64_t blocks = P.deep_n ? std::min<int64_t>((P.n_cols + KW - 1) / KW, 2048) : (waves + KW - 1) / KW;
     const bool fresh = P.batch_seq == 1;
     const bool w4 = P.t_deep <= 1;
     // batches far beyond the 256 MiB Infinity Cache stream with non-temporal loads
     const bool nt = 2 * P.n_entries > (192ull << 20);
-#define SPG_SEG(WW, FF, NN) hipLaunchKernelGGL((k_acc_seg<WW, FF, SPG_SEG_WPE, NN, false>), dim3((unsigned)blocks), dim3(64 * KW), 0, st, P, off, code, qual, ref, T, acc)
+#define SPG_SEG(WW, FF, NN) hipLaunchKernelGGL((k_acc_seg<WW, FF, WW == 1 ? 3 : SPG_SEG_WPE, NN, false>), dim3((unsigned)blocks), dim3(64 * KW), 0, st, P, off, code, qual, ref, T, acc)
 #define SPG_SEGF(NN) hipLaunchKernelGGL((k_acc_seg<4, true, SPG_SEG_WPE, NN, true>), dim3((unsigned)blocks), dim3(64 * KW), 0, st, P, off, code, qual, ref, T, acc)
     if (P.fused) {            // fused accumulate + calls-only finalize (FRESH deep batch, G <= NB)
         if (!w4 || !fresh || P.G > (uint32_t)NB) return hipErrorInvalidValue;
@@ -1607,6 +1850,16 @@ hipError_t launch_multi(const MParams &P, const Hist *H, const uint8_t *ref, con
         const int64_t mb = (P.u1 - P.u0 + 255) / 256;
         hipLaunchKernelGGL(k_merge_parts, dim3((unsigned)mb), dim3(256), 0, st, P, ref, acc);
     }
+    return hipGetLastError();
+}
+
+// k_acc_one over a single shallow batch into a FRESH memory
+hipError_t launch_one(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc,
+                      int64_t max_blocks, bool fused, hipStream_t st) {
+    if (P.n_groups == 0) return hipSuccess;
+    const int64_t blocks = std::min<int64_t>(((int64_t)P.n_groups + MW - 1) / MW, max_blocks);
+    if (fused) hipLaunchKernelGGL(k_acc_one<true>, dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
+    else hipLaunchKernelGGL(k_acc_one<false>, dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
     return hipGetLastError();
 }
 
