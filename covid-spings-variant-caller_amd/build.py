@@ -7,7 +7,9 @@ The .so files are git-ignored but travel to the GPU box with the gpurun snapshot
 """
 from __future__ import annotations
 
+import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -35,6 +37,7 @@ def _run(cmd):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
 
 
 def build_gpu(force=False, verbose=False) -> str:
@@ -42,12 +45,48 @@ def build_gpu(force=False, verbose=False) -> str:
     out = os.path.join(LIBDIR, "libspings_gpu.so")
     deps = [os.path.join(CSRC, f) for f in GPU_SOURCES + GPU_HEADERS] + [os.path.join(INC, "spings_gpu.h")]
     if force or _stale(out, deps):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", f"-I{INC}", "-o", out + ".tmp"]
+        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", f"-I{INC}", "-o", out + ".tmp",
+               "-Rpass-analysis=kernel-resource-usage"]
         cmd += [os.path.join(CSRC, f) for f in GPU_SOURCES]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        _run(cmd)
+        r = _run(cmd)
         os.replace(out + ".tmp", out)
+        res = kernel_resources(r.stderr)
+        with open(os.path.join(LIBDIR, "kernel_resources.json"), "w") as f:
+            json.dump(res, f, indent=1, sort_keys=True)
+        for k, v in res.items():
+            if v.get("scratch", 0) and any(h in k for h in HOT_KERNELS):
+                print(f"WARNING: hot kernel {k} spills to scratch ({v['scratch']} B/lane)", file=sys.stderr)
+    return out
+
+
+# kernels on the measured paths: a scratch spill there costs occupancy and time (tests/test_cabi.py)
+HOT_KERNELS = ("k_acc_seg<4", "k_acc_one", "k_acc_multi", "k_finalize")
+
+
+def kernel_resources(remarks: str) -> dict:
+    """Per-kernel VGPRs / SGPR spills / scratch / occupancy / LDS from hipcc's kernel-resource-usage
+    remarks (demangled names)."""
+    out, cur = {}, None
+    for line in remarks.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+            try:
+                name = subprocess.run(["c++filt", name], capture_output=True, text=True).stdout.strip() or name
+            except OSError:
+                pass
+            cur = out.setdefault(name.split("(")[0].replace("void ", ""), {})
+            continue
+        if cur is None:
+            continue
+        for key, pat in (("vgpr", r"VGPRs: (\d+)"), ("sgpr_spill", r"SGPRs Spill: (\d+)"),
+                         ("vgpr_spill", r"VGPRs Spill: (\d+)"), ("scratch", r"ScratchSize \[bytes/lane\]: (\d+)"),
+                         ("waves_per_simd", r"Occupancy \[waves/SIMD\]: (\d+)"), ("lds", r"LDS Size \[bytes/block\]: (\d+)")):
+            m = re.search(pat, line)
+            if m:
+                cur[key] = int(m.group(1))
     return out
 
 

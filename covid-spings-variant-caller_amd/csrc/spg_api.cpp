@@ -529,6 +529,20 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     P.hdesc = Hist{hb.pos_begin, n_cols, hb.off, hb.code, hb.qual};
     P.hslot = c->d_hist + idx;
     P.G = G;
+    P.G2 = G;
+    P.w1 = (uint32_t)std::min<int64_t>(UINT32_MAX, (n_cols + G - 1) / G);
+    // Deep batches with G >= 2: the last grid generation (#CUs x 16 waves) gets groups of G / 2 columns,
+    // so the waves that start last end sooner (the launch's tail)
+    static const int64_t tail_waves = [] { const char *e = getenv("SPG_TAIL_WAVES"); return e ? atoll(e) : 4096ll; }();
+    if (deep_batch && G >= 2 && tail_waves > 0) {
+        const int64_t G2 = G / 2;
+        const int64_t tail_cols = std::min<int64_t>(n_cols, tail_waves * G2);
+        const int64_t w1 = (n_cols - tail_cols + G - 1) / G;
+        if (w1 > 0 && w1 * G < n_cols) {
+            P.w1 = (uint32_t)w1;
+            P.G2 = (uint32_t)G2;
+        }
+    }
     P.t_deep = deep_batch ? 1u : 128u;
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
     P.n_entries = hb.n_entries;
@@ -538,13 +552,14 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
         P.deep_list = c->deep_list;
         P.deep_n = c->deep_n;
     }
-    P.prog = trace_prog(listed ? 2048 * 4 + 4 : (n_cols + G - 1) / G + 4);
+    P.prog = trace_prog(listed ? 2048 * 4 + 4 : 2 * ((n_cols + G - 1) / G) + 4);   // tail split: <= 2x waves
     // SPG_WAVE_TIMES=<file> (profiling, tools/wavetimes.py): per-wave timeline of each deep launch
     // appended to <file> (the launch is synchronised)
     static const char *wt_file = getenv("SPG_WAVE_TIMES");
     static uint4 *wt_buf = nullptr;
     static int64_t wt_cap = 0;
-    const int64_t n_waves = (n_cols + G - 1) / G;
+    const int64_t n_waves = P.w1 >= (n_cols + G - 1) / G ? (n_cols + G - 1) / G
+                                                        : P.w1 + (n_cols - (int64_t)P.w1 * G + P.G2 - 1) / P.G2;
     if (wt_file && deep_batch) {
         if (n_waves > wt_cap) {
             if (wt_buf) HIPCHK(hipFree(wt_buf));

@@ -66,6 +66,8 @@ struct KParams {
     uint32_t batch_seq;    // 1-based within the epoch
     uint32_t epoch;
     uint32_t G;            // columns per wave group
+    uint32_t w1, G2;       // waves >= w1 own G2 (< G) columns: the last grid generation's waves are
+                           // shorter, so the launch's tail is (w1 = all waves: no split)
     uint32_t t_deep;       // columns with >= t_deep raw entries are processed wave-wide
     uint32_t calls_only;   // SPG_P_CALLS_ONLY
     uint64_t n_entries;    // entries of the batch (launch shape only)
@@ -80,7 +82,7 @@ struct KParams {
     uint4 *prog;           // SPG_TRACE: per-wave progress records in host-mapped memory (else null)
     const uint32_t *deep_list;   // W = 1: the long columns k_acc_multi listed (batch-relative) ...
     const uint32_t *deep_n;      // ... and their count (null: one group of G columns per wave)
-    uint4 *wtime;          // SPG_WAVE_TIMES: per wave {start, setup done, end} (s_memrealtime, 100 MHz), hw id
+    uint4 *wtime;          // SPG_WAVE_TIMES: per wave {start, first column, lifetime} (s_memrealtime, 100 MHz), hw id
 };
 
 // Per-position state of one lane of k_acc_multi over a run of batches (lane-private, in LDS), and

@@ -769,13 +769,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     const int64_t wave = (int64_t)blockIdx.x * KW + (threadIdx.x >> 6);
     // deep_list (the long columns of a shallow batch): the waves stride over the listed columns, one
     // column each; otherwise one group of G consecutive columns per wave
-    const bool listed = P.deep_n != nullptr;
+    const bool listed = W == 1 && P.deep_n != nullptr;  // (W = 4: compile-time off; the loop runs once)
     const int64_t n_items = listed ? (int64_t)*P.deep_n : wave + 1;
     const int64_t istride = listed ? (int64_t)gridDim.x * KW : 1;
     for (int64_t item = wave; item < n_items; item += istride) {
-    const int64_t g0 = listed ? (int64_t)P.deep_list[item] : wave * P.G;
+    const bool tail = !listed && wave >= (int64_t)P.w1;
+    const int64_t g0 = listed ? (int64_t)P.deep_list[item]
+                              : (tail ? (int64_t)P.w1 * P.G + (wave - P.w1) * P.G2 : wave * P.G);
     if (g0 >= P.n_cols) continue;
-    const int ng = listed ? 1 : (int)min((int64_t)P.G, P.n_cols - g0);
+    const int ng = listed ? 1 : (int)min((int64_t)(tail ? P.G2 : P.G), P.n_cols - g0);
     // SPG_TRACE: lane 0 posts (stage, a, b, c) to host-mapped memory, so a fault leaves each wave's
     // last step readable by the host
     auto prog = [&](uint32_t stage, uint32_t a, uint32_t b, uint32_t c) {
@@ -790,7 +792,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     prog(1, (uint32_t)g0, (uint32_t)ng, 0);
     // SPG_WAVE_TIMES (profiling): wave timeline in s_memrealtime ticks
     const uint64_t wt0 = P.wtime ? __builtin_amdgcn_s_memrealtime() : 0;
-    uint64_t wt1 = 0;
     WaveRare *RR = rare[threadIdx.x >> 6];             // rare records of the ring's columns
     ColSum *CS = csum[threadIdx.x >> 6];
     Dual2 *D2 = dual2 + (threadIdx.x >> 6);
@@ -922,7 +923,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         return p_a + (ii - p_pre) * STEP + lo;
     };
 
-    if (P.wtime) wt1 = __builtin_amdgcn_s_memrealtime();
     // register ring of three chunks: two loads stay in flight while one chunk is processed
     V c0, q0, c1, q1, c2, q2;
 #define SPG_LD(C, Q, I) do { const uint32_t o_ = chunk_off(I); C = bload<W, NT>(rc, o_); Q = bload<W, NT>(rq, o_); } while (0)
@@ -1097,8 +1097,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         };
         using T_ = std::true_type;
         using F_ = std::false_type;
-        if (dual) body(T_{}, T_{});
-        else if (sem || !P.calls_only) body(F_{}, T_{});
+        if (dual) {
+            if (sem || !P.calls_only) body(T_{}, T_{});
+            else {                             // calls-only, REF major: only the second allele's sums
+                body(T_{}, F_{});
+                skipped = true;
+            }
+        } else if (sem || !P.calls_only) body(F_{}, T_{});
         else {                                 // calls-only, REF major: counts and sum(q) only
             body(F_{}, F_{});
             skipped = true;
@@ -1165,7 +1170,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         const uint64_t wt2 = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
         const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
-        P.wtime[wave] = make_uint4((uint32_t)wt0, (uint32_t)(wt1 - wt0), (uint32_t)(wt2 - wt0), (hw & 0xFFFFFu) | (xcc << 24));
+        P.wtime[wave] = make_uint4((uint32_t)wt0, (uint32_t)g0, (uint32_t)(wt2 - wt0), (hw & 0xFFFFFu) | (xcc << 24));
     }
     prog(6, 0, 0, 0);
     }   // items
@@ -1810,7 +1815,8 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
 hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_t *code, const uint8_t *qual,
                              const uint8_t *ref, const Tables *T, Acc *acc, hipStream_t st) {
     if (P.n_cols == 0) return hipSuccess;
-    const int64_t waves = (P.n_cols + P.G - 1) / P.G;
+    const int64_t waves = P.w1 >= (P.n_cols + P.G - 1) / P.G ? (P.n_cols + P.G - 1) / P.G
+                                                             : P.w1 + (P.n_cols - (int64_t)P.w1 * P.G + P.G2 - 1) / P.G2;
     // listed long columns: a fixed grid strides over the list (its length is on the device)
     const int64_t blocks = P.deep_n ? std::min<int64_t>((P.n_cols + KW - 1) / KW, 2048) : (waves + KW - 1) / KW;
     const bool fresh = P.batch_seq == 1;

@@ -27,6 +27,7 @@
 #include <cmath>
 #include <stdexcept>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -963,19 +964,31 @@ static int pileup_impl(spp_file *f, int32_t tid, const spp_params *p, int64_t lo
         // the span bound is checked against the longest read and the pass redone if it was too short
         int64_t pad = 16384;
         for (;;) {
+            // SPP_TIMING=1: phase times on stderr (read / depth-cap simulation / CSR fill)
+            static const bool timing = getenv("SPP_TIMING") != nullptr;
+            auto now = [] { return std::chrono::steady_clock::now(); };
+            const auto t0 = now();
             Reads R;
             if (region) { R.dlo = lo == INT64_MIN ? lo : lo - pad; R.dhi = hi == INT64_MAX ? hi : hi + pad; }
             if (f->bam) read_bam(f, tid, *p, R);
             else read_sam(f, tid, *p, R);
             if (region && R.max_span > pad) { pad = 2 * R.max_span; continue; }
+            const auto t1 = now();
             Tweaks T;
             const std::vector<uint8_t> keep = simulate(R, *p, tid, T);   // every read: exact depth cap
+            const auto t2 = now();
             auto *B = new spp_batch();
             int64_t used = 0;
             for (uint8_t k : keep) used += k;
             B->n_used = used;
             B->n_dropped = (int64_t)R.size() - used;
             fill_csr(R, keep, T, B, std::max(1, p->n_threads), lo, hi);
+            if (timing) {
+                const auto t3 = now();
+                auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+                fprintf(stderr, "[spp timing] read %.1f ms, simulate %.1f ms, fill %.1f ms (%zu reads, %d threads)\n",
+                        ms(t0, t1), ms(t1, t2), ms(t2, t3), (size_t)R.size(), p->n_threads);
+            }
             *out = B;
             return 0;
         }

@@ -68,3 +68,21 @@ def test_pileup_library_exports_every_declared_symbol():
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
     assert ctypes.sizeof(N.SppParams) == 40
+
+
+def test_hot_kernels_do_not_spill_to_scratch():
+    """The build records hipcc's kernel-resource-usage remarks (_lib/kernel_resources.json): no kernel
+    on a measured path may spill to scratch (a spill there cost 60 % of the deep kernel's speed once),
+    and the deep accumulate keeps 4 waves per SIMD (16 per CU, the LDS limit)."""
+    import json
+    import os
+    from covid_spings_variant_caller_amd import build as B
+    path = os.path.join(B.LIBDIR, "kernel_resources.json")
+    if not os.path.exists(path):
+        pytest.skip("library built without the resource record")
+    res = json.load(open(path))
+    hot = {k: v for k, v in res.items() if any(h in k for h in B.HOT_KERNELS)}
+    assert hot, res
+    assert all(v.get("scratch", 0) == 0 for v in hot.values()), {k: v for k, v in hot.items() if v.get("scratch")}
+    deep = [v for k, v in hot.items() if k.startswith("spg::k_acc_seg<4, true")]
+    assert deep and all(v["waves_per_simd"] >= 4 for v in deep), deep

@@ -1,8 +1,8 @@
 """Per-wave timeline of the deep accumulate kernel (profiling; SPG_WAVE_TIMES instrumentation).
 
 Runs the bench's 10,000x SARS-CoV-2 batch through the fused accumulate a few times with
-SPG_WAVE_TIMES=<file> (k_acc_seg records per wave: start, setup done, end in s_memrealtime ticks of
-10 ns, and HW_ID / XCC_ID), then reports the launch's span, the wave generations, setup and lifetime
+SPG_WAVE_TIMES=<file> (k_acc_seg records per wave: start, lifetime in s_memrealtime ticks of
+10 ns, its first column, and HW_ID / XCC_ID), then reports the launch's span, the wave generations, setup and lifetime
 distributions, and how the tail ends.  Usage: python tools/wavetimes.py [depth] [out.json]
 """
 import json
@@ -49,14 +49,16 @@ def analyse(path):
     g, w = launches[-1]
     t0 = w[:, 0].astype(np.int64)
     t0 = (t0 - t0.min()) * 10e-3                     # us
-    setup = w[:, 1] * 10e-3
+    col = w[:, 1].astype(np.int64)
     life = w[:, 2] * 10e-3
     end = t0 + life
     xcc = w[:, 3] >> 24
     span = float(end.max())
     q = lambda a: {p: round(float(np.percentile(a, p)), 2) for p in (5, 25, 50, 75, 95, 100)}
     res = {"waves": int(len(w)), "G": g, "span_us": round(span, 2),
-           "start_us": q(t0), "setup_us": q(setup), "life_us": q(life), "end_us": q(end),
+           "start_us": q(t0), "life_us": q(life), "end_us": q(end),
+           "longest_waves": [{"first_column": int(col[i]), "life_us": round(float(life[i]), 2),
+                              "start_us": round(float(t0[i]), 2)} for i in np.argsort(-life)[:8]],
            "waves_ending_after_span_minus_5us": int((end > span - 5).sum()),
            "waves_starting_after_span_minus_10us": int((t0 > span - 10).sum()),
            "busy_wave_us_over_span": round(float(life.sum()) / span, 1),
