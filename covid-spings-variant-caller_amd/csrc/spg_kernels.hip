@@ -1823,7 +1823,9 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
     const bool w4 = P.t_deep <= 1;
     // batches far beyond the 256 MiB Infinity Cache stream with non-temporal loads
     const bool nt = 2 * P.n_entries > (192ull << 20);
-#define SPG_SEG(WW, FF, NN) hipLaunchKernelGGL((k_acc_seg<WW, FF, WW == 1 ? 3 : SPG_SEG_WPE, NN, false>), dim3((unsigned)blocks), dim3(64 * KW), 0, st, P, off, code, qual, ref, T, acc)
+    // (W = 1, and a deep batch into a memory that already holds records (the old record is read and
+    // merged): 3 waves per SIMD, so the register allocation needs no scratch)
+#define SPG_SEG(WW, FF, NN) hipLaunchKernelGGL((k_acc_seg<WW, FF, (WW == 1 || !FF) ? 3 : SPG_SEG_WPE, NN, false>), dim3((unsigned)blocks), dim3(64 * KW), 0, st, P, off, code, qual, ref, T, acc)
 #define SPG_SEGF(NN) hipLaunchKernelGGL((k_acc_seg<4, true, SPG_SEG_WPE, NN, true>), dim3((unsigned)blocks), dim3(64 * KW), 0, st, P, off, code, qual, ref, T, acc)
     if (P.fused) {            // fused accumulate + calls-only finalize (FRESH deep batch, G <= NB)
         if (!w4 || !fresh || P.G > (uint32_t)NB) return hipErrorInvalidValue;

@@ -84,5 +84,5 @@ def test_hot_kernels_do_not_spill_to_scratch():
     hot = {k: v for k, v in res.items() if any(h in k for h in B.HOT_KERNELS)}
     assert hot, res
     assert all(v.get("scratch", 0) == 0 for v in hot.values()), {k: v for k, v in hot.items() if v.get("scratch")}
-    deep = [v for k, v in hot.items() if k.startswith("spg::k_acc_seg<4, true")]
+    deep = [v for k, v in hot.items() if k.startswith("spg::k_acc_seg<4, true, 4")]
     assert deep and all(v["waves_per_simd"] >= 4 for v in deep), deep
