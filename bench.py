@@ -60,6 +60,7 @@ def parse():
     ap.add_argument("--time-every", type=int, default=8,
                     help="HIP events around the accumulate kernel on every K-th timed step")
     ap.add_argument("--e2e-threads", type=int, default=16)
+    ap.add_argument("--e2e-bams", type=int, default=4, help="BAMs per end-to-end stream")
     ap.add_argument("--full-table", action="store_true", help="also accumulate every table GL term")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
                                                       "gloo only to exercise the path on one GPU)")
@@ -442,41 +443,76 @@ def cpu_baseline(args):
 
 
 def end_to_end(args, device):
-    """BAM -> host pileup (libspings_pileup: BGZF inflate, htslib-rule pileup, CSR) -> H2D ->
-    accumulate -> finalize -> call table, on one synthetic 10,000x BAM written by the C++ read
-    simulator.  Reported beside `value` (never as it): it includes the host front end and PCIe."""
+    """BAM -> calls through the drop-in (LiveVariantCaller.process_bam, live_variant_caller.py:54-72):
+    host pileup (libspings_pileup: BGZF inflate, htslib-rule pileup, CSR offsets) -> entries written
+    into pinned, double-buffered staging -> async H2D on the engine's copy stream -> accumulate; the
+    next BAM's pileup overlaps the previous BAM's copy and kernels.  A stream of --e2e-bams synthetic
+    10,000x BAMs (written by the C++ read simulator) into one memory, then prepare_variants.  Reported
+    beside `value` (never as it): it includes the host front end and PCIe."""
     import tempfile
     from covid_spings_variant_caller_amd import synth
-    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.live_variant_caller import LiveVariantCaller
     from covid_spings_variant_caller_amd.pileup import AlignmentFile, PileupParams, simulate_bam
+    from covid_spings_variant_caller_amd.engine import pinned_empty
     ref = synth.reference(L_SARS, seed=1)
     d = tempfile.mkdtemp(dir=os.environ.get("TMPDIR", "/tmp"))
     bam = os.path.join(d, "sars_e2e.bam")
+    fasta = os.path.join(d, "ref.fa")
+    with open(fasta, "w") as f:
+        f.write(">NC_045512.2\n")
+        for i in range(0, L_SARS, 60):
+            f.write(ref[i:i + 60] + "\n")
     t0 = time.perf_counter()
     n_reads = simulate_bam(bam, "NC_045512.2", ref, depth=args.eff_depth, seed=5, n_threads=args.e2e_threads)
     t_sim = time.perf_counter() - t0
-    eng = PileupEngine(L_SARS, 30, 10, 5, 0.10, device=device, reference=ref, calls_only=True)
     res = {}
+    n_bams = max(1, args.e2e_bams)
     for cap, tag in ((8000, "parity_mode_max_depth_8000"), (0, "uncapped")):
-        eng.reset()
+        caller = LiveVariantCaller(fasta, 30, 20, 10, 5, 0.10, 1, device=device, max_depth=cap,
+                                   n_threads=args.e2e_threads)
+        caller.process_bam(bam)                    # warm-up: pinned staging, library state
+        caller.reset_memory()
+        caller.engine.sync()
         t0 = time.perf_counter()
-        with AlignmentFile(bam) as f:
-            b = f.pileup_batch("NC_045512.2", PileupParams(max_depth=cap, n_threads=args.e2e_threads))
+        for _ in range(n_bams):
+            caller.process_bam(bam)
+        t_in = time.perf_counter() - t0
+        calls = caller.prepare_variants()
+        caller.engine.sync()
         t1 = time.perf_counter()
-        eng.accumulate(b.pos_begin, b.offsets, b.codes, b.quals)
+        # breakdown of one more BAM: host pileup phases, then the GPU leg alone
+        p = caller.pileup_params
+        b0 = time.perf_counter()
+        with AlignmentFile(bam) as f:
+            b = f.pileup_plan("NC_045512.2", p)
+        b1 = time.perf_counter()
+        codes, quals = pinned_empty(b.n_entries + 16), pinned_empty(b.n_entries + 16)
+        b.fill(codes, quals)
+        b2 = time.perf_counter()
+        eng = caller.engine
+        eng.reset()
+        eng.sync()
+        g0 = time.perf_counter()
+        eng.accumulate(b.pos_begin, b.offsets, codes[:b.n_entries], quals[:b.n_entries], trusted=True)
         eng.finalize()
-        n_calls = len(eng.candidates())
-        t2 = time.perf_counter()
-        res[tag] = {"positions_per_s": L_SARS / (t2 - t0), "host_pileup_s": t1 - t0, "h2d_gpu_s": t2 - t1,
-                    "entries": int(b.n_entries), "reads_used": int(b.n_reads_used), "calls": n_calls,
-                    "pcie_inclusive_gpu_positions_per_s": L_SARS / (t2 - t1)}
+        eng.sync()
+        g1 = time.perf_counter()
+        E = b.n_entries
         b.close()
-    eng.close()
+        res[tag] = {"bams": n_bams, "positions_per_s_per_bam": n_bams * L_SARS / (t1 - t0),
+                    "s_per_bam": (t1 - t0) / n_bams, "ingest_s": t_in, "finalize_s": t1 - t0 - t_in,
+                    "calls": len(calls), "entries_per_bam": int(E),
+                    "breakdown_one_bam": {"host_plan_s": b1 - b0, "host_fill_pinned_s": b2 - b1,
+                                          "h2d_pinned_plus_gpu_s": g1 - g0,
+                                          "pcie_inclusive_gpu_positions_per_s": L_SARS / (g1 - g0)}}
+        caller.engine.close()
+        del caller
     res["bam_bytes"] = os.path.getsize(bam)
     res["reads"] = n_reads
     res["simulate_s"] = t_sim
     res["host_threads"] = args.e2e_threads
     os.remove(bam)
+    os.remove(fasta)
     os.rmdir(d)
     return res
 

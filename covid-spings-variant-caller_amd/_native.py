@@ -20,7 +20,7 @@ SPG_CODE_DEL = 16
 SPG_CODE_SKIP = 17
 SPG_F_PRESENT, SPG_F_EVALUATED, SPG_F_REPLAYED, SPG_F_EXOTIC, SPG_F_CANDIDATE, SPG_F_PARTIAL = 1, 2, 4, 8, 16, 32
 SPG_P_CALLS_ONLY = 1
-SPG_IN_DEVICE, SPG_IN_BORROW = 1, 2
+SPG_IN_DEVICE, SPG_IN_BORROW, SPG_IN_TRUSTED = 1, 2, 4
 NIBBLE = "=ACMGRSVTWYHKDBN"
 SLOT_CHARS = "ACGTN"
 SLOT_CODES = (1, 2, 4, 8, 15)
@@ -167,6 +167,8 @@ def pileup_lib():
          C.POINTER(i64), C.POINTER(i64))
     _sig(L.spp_batch_arrays, C.c_int, vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp))
     _sig(L.spp_batch_free, C.c_int, vp)
+    _sig(L.spp_pileup_plan, C.c_int, vp, i32, i64, i64, C.POINTER(SppParams), C.POINTER(vp))
+    _sig(L.spp_batch_fill, C.c_int, vp, vp, vp)
     _sig(L.spp_default_sim_params, None, C.POINTER(SimParams))
     _sig(L.spp_simulate_bam, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, i64, C.POINTER(SimParams),
          C.POINTER(i64))

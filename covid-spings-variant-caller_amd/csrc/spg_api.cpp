@@ -743,7 +743,7 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
     if (n_entries >= (1ull << 40)) return fail("spg_accumulate: batch too large");
     const bool dev = flags & SPG_IN_DEVICE;
     const bool borrow = dev && (flags & SPG_IN_BORROW);
-    if (!dev) {
+    if (!dev && !(flags & SPG_IN_TRUSTED)) {
         // validate the host CSR (offsets O(n_cols), codes O(E)); device inputs are trusted
         if (offsets[0] != 0 || offsets[n_cols] != n_entries)
             return fail("spg_accumulate: offsets[0] must be 0 and offsets[n_cols] == n_entries");

@@ -28,6 +28,7 @@
 #include <stdexcept>
 #include <string>
 #include <chrono>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -77,6 +78,40 @@ struct NoInit : std::allocator<T> {
 };
 template <class T> using Vec = std::vector<T, NoInit<T>>;
 
+// Process-wide pool of 2 MiB-aligned blocks (up to SPP_POOL_MB, default 4096 MiB, kept resident)
+std::mutex g_pool_mu;
+std::vector<std::pair<uint8_t *, size_t>> g_pool;
+size_t g_pool_bytes = 0;
+size_t pool_cap() {
+    static const size_t cap = [] { const char *e = getenv("SPP_POOL_MB"); return (size_t)(e ? atoll(e) : 4096) << 20; }();
+    return cap;
+}
+uint8_t *block_pool_get(size_t sz) {
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size(); i++)
+            if (g_pool[i].second == sz) {
+                uint8_t *b = g_pool[i].first;
+                g_pool.erase(g_pool.begin() + (long)i);
+                g_pool_bytes -= sz;
+                return b;
+            }
+    }
+    uint8_t *b = (uint8_t *)aligned_alloc(2u << 20, sz);
+    if (!b) throw std::runtime_error("out of host memory for the reads");
+    madvise(b, sz, MADV_HUGEPAGE);
+    return b;
+}
+void block_pool_put(uint8_t *b, size_t sz) {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    if (g_pool_bytes + sz <= pool_cap()) {
+        g_pool.emplace_back(b, sz);
+        g_pool_bytes += sz;
+    } else {
+        free(b);
+    }
+}
+
 struct Reads {                 // one contig's reads, structure of arrays
     Vec<int64_t> pos, end, mpos, isize;
     Vec<int32_t> mtid;
@@ -91,22 +126,25 @@ struct Reads {                 // one contig's reads, structure of arrays
     int64_t max_span = 0;                       // longest reference span of any read of the contig
     bool decode(int64_t pos, int64_t end) const { return end > dlo && pos < dhi; }
     Vec<char> names;
-    // bases storage: 2 MiB-aligned blocks (transparent huge pages requested), never moved, so the
-    // decoders can fill a window's records in parallel without a serial grow-and-copy
+    // bases storage: 2 MiB-aligned 64 MiB blocks (transparent huge pages requested), never moved, so
+    // the decoders can fill a window's records in parallel without a serial grow-and-copy.  Blocks
+    // come from a process-wide pool and go back to it: the next BAM reuses resident pages (no page
+    // faults, no munmap on the critical path).
     struct Arena {
-        std::vector<uint8_t *> blocks;
+        std::vector<std::pair<uint8_t *, size_t>> blocks;
         uint8_t *cur = nullptr;
         size_t left = 0;
+        Arena() = default;
+        Arena(const Arena &) = delete;
+        Arena &operator=(const Arena &) = delete;
         ~Arena() {
-            for (uint8_t *b : blocks) free(b);
+            for (auto &b : blocks) block_pool_put(b.first, b.second);
         }
         uint8_t *alloc(size_t n) {
             if (n > left) {
                 const size_t sz = std::max<size_t>(n + (2u << 20) - 1, 64u << 20) & ~(size_t)((2u << 20) - 1);
-                cur = (uint8_t *)aligned_alloc(2u << 20, sz);
-                if (!cur) throw std::runtime_error("out of host memory for the reads");
-                madvise(cur, sz, MADV_HUGEPAGE);
-                blocks.push_back(cur);
+                cur = block_pool_get(sz);
+                blocks.emplace_back(cur, sz);
                 left = sz;
             }
             uint8_t *r = cur;
@@ -134,15 +172,24 @@ struct spp_file {
     std::unordered_map<std::string, int32_t> tid_of;
 };
 
+struct spp_plan;                   // the parsed reads between spp_pileup_plan and spp_batch_fill
+void release_plan(spp_plan *p);
+
 struct spp_batch {
     int64_t pos_begin = 0, n_cols = 0;
     uint64_t n_entries = 0;
     int64_t n_used = 0, n_dropped = 0;
     std::vector<uint64_t> off;
     uint8_t *code = nullptr, *qual = nullptr;
+    bool owns = true;              // code / qual allocated here (else the caller's buffers)
+    spp_plan *plan = nullptr;
+    int threads = 1;
     ~spp_batch() {
-        free(code);
-        free(qual);
+        if (owns) {
+            free(code);
+            free(qual);
+        }
+        release_plan(plan);
     }
 };
 
@@ -154,7 +201,8 @@ namespace {
 // ---------------------------------------------------------------------------------------------
 class BgzfReader {
   public:
-    BgzfReader(const std::string &path, int threads) : threads_(std::max(1, threads)) {
+    BgzfReader(const std::string &path, int threads, size_t window = 0) : threads_(std::max(1, threads)) {
+        if (window) window_ = std::max<size_t>(window, 65554);
         // SPP_BGZF_WINDOW (bytes, >= 65554): a smaller read window, for the boundary tests
         if (const char *w = getenv("SPP_BGZF_WINDOW")) window_ = std::max<size_t>(strtoull(w, nullptr, 10), 65554);
         f_ = fopen(path.c_str(), "rb");
@@ -243,7 +291,7 @@ class BgzfReader {
 // copied, so a refill swaps buffers instead of moving the window.
 class BamStream {
   public:
-    BamStream(const std::string &path, int threads) : z_(path, threads) { launch(); }
+    BamStream(const std::string &path, int threads, size_t window = 0) : z_(path, threads, window) { launch(); }
     ~BamStream() {
         if (pending_.joinable()) pending_.join();
     }
@@ -649,8 +697,16 @@ struct EndQueue {
 // pairing.  Returns keep[r].
 std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks &T) {
     const size_t n = R.size();
-    std::vector<uint8_t> keep(n, 0);
     T.col.assign(n, INT64_MAX);
+    // Uncapped, every read spans >= 1 column and no overlap pairing can happen: every read is pushed
+    // (sorted starts keep the pending position <= each read's start < its end) and nothing is tweaked
+    if (p.max_depth <= 0) {
+        bool simple = true;
+        for (size_t r = 0; r < n && simple; r++)
+            simple = R.end[r] > R.pos[r] && !(p.ignore_overlaps && (R.flag[r] & F_PROPER));
+        if (simple) return std::vector<uint8_t>(n, 1);
+    }
+    std::vector<uint8_t> keep(n, 0);
     const int64_t maxcnt = p.max_depth > 0 ? p.max_depth : INT64_MAX;
     // live buffer: reads pushed and not yet freed.  Freed while scanning column c when end <= c.
     EndQueue by_end;
@@ -730,8 +786,34 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
     return keep;
 }
 
-void fill_csr(const Reads &R, const std::vector<uint8_t> &keep, const Tweaks &T, spp_batch *B, int threads,
-              int64_t rlo = INT64_MIN, int64_t rhi = INT64_MAX) {
+}  // namespace
+
+struct spp_plan {
+    Reads R;
+    std::vector<uint8_t> keep;
+    Tweaks T;
+    std::vector<size_t> kept;      // reads with entries in the batch's columns, in BAM order
+    int64_t rlo = INT64_MIN, rhi = INT64_MAX;
+};
+
+// The parsed reads are large (bases, names, CIGARs): released on a helper thread, so the pipeline's
+// next BAM does not wait for the frees (the arena's blocks go back to the pool).
+void release_plan(spp_plan *p) {
+    if (!p) return;
+    try {
+        std::thread([p] { delete p; }).detach();
+    } catch (...) {
+        delete p;
+    }
+}
+
+namespace {
+
+// CSR offsets of the kept reads' columns (the batch's entry count is known after this)
+void plan_csr(spp_plan &P, spp_batch *B) {
+    const Reads &R = P.R;
+    const std::vector<uint8_t> &keep = P.keep;
+    const int64_t rlo = P.rlo, rhi = P.rhi;
     int64_t lo = INT64_MAX, hi = INT64_MIN;
     auto inreg = [&](size_t r) { return keep[r] && R.end[r] > R.pos[r] && R.end[r] > rlo && R.pos[r] < rhi; };
     for (size_t r = 0; r < R.size(); r++)
@@ -752,18 +834,25 @@ void fill_csr(const Reads &R, const std::vector<uint8_t> &keep, const Tweaks &T,
         run += diff[(size_t)c];
         B->off[(size_t)c + 1] = B->off[(size_t)c] + (uint64_t)run;
     }
-    const uint64_t E = B->off[(size_t)C];
-    B->n_entries = E;
-    B->code = (uint8_t *)malloc(E + 16);
-    B->qual = (uint8_t *)malloc(E + 16);
-    if (!B->code || !B->qual) throw std::runtime_error("out of host memory for the pileup");
+    B->n_entries = B->off[(size_t)C];
+    P.kept.clear();
+    for (size_t r = 0; r < R.size(); r++)
+        if (inreg(r)) P.kept.push_back(r);
+}
+
+// base_code / qual of every entry into code / qual (>= n_entries + 16 bytes each)
+void fill_csr(const spp_plan &P, spp_batch *B, uint8_t *code, uint8_t *qual, int threads) {
+    const Reads &R = P.R;
+    const Tweaks &T = P.T;
+    const std::vector<size_t> &kept = P.kept;
+    const int64_t lo = B->pos_begin, C = B->n_cols;
+    const uint64_t E = B->n_entries;
+    B->code = code;
+    B->qual = qual;
     memset(B->code + E, 0xFF, 16);
     memset(B->qual + E, 0, 16);
     // Column-range parallel fill: a thread owns columns [c0, c1) and walks the reads overlapping
     // them in read order, so each column's entries keep htslib's order.
-    std::vector<size_t> kept;
-    for (size_t r = 0; r < R.size(); r++)
-        if (inreg(r)) kept.push_back(r);
     const int nt = std::max(1, std::min(threads, 64));
     auto work = [&](int t) {
         const int64_t c0 = C * t / nt, c1 = C * (t + 1) / nt;
@@ -910,7 +999,9 @@ int spp_open(const char *path, spp_file **out) {
         f->path = path;
         f->bam = is_bgzf(path);
         if (f->bam) {
-            BamStream s(path, 1);
+            // the header only: a small inflate window (the default 16 MiB one inflated ~40 MB of reads
+            // just to read it, 0.2-0.5 s per BAM)
+            BamStream s(path, 1, 256u << 10);
             bam_header(s, f);
         } else {
             for_lines(path, [&](const std::string &line) {
@@ -953,48 +1044,107 @@ int spp_target_id(spp_file *f, const char *name, int32_t *tid) {
     return 0;
 }
 
-static int pileup_impl(spp_file *f, int32_t tid, const spp_params *p, int64_t lo, int64_t hi, spp_batch **out) {
+static int plan_impl(spp_file *f, int32_t tid, const spp_params *p, int64_t lo, int64_t hi, spp_batch **out) {
     if (!f || !p || !out) return fail("spp_pileup: null argument");
     if (tid < 0 || (size_t)tid >= f->targets.size()) return fail("spp_pileup: tid out of range");
     if (lo >= hi) return fail("spp_pileup_region: empty region");
     *out = nullptr;
+    spp_plan *P = nullptr;
     try {
         const bool region = lo != INT64_MIN || hi != INT64_MAX;
         // region: bases of reads within a read span of [lo, hi) (mates that can overlap a region read);
         // the span bound is checked against the longest read and the pass redone if it was too short
         int64_t pad = 16384;
         for (;;) {
-            // SPP_TIMING=1: phase times on stderr (read / depth-cap simulation / CSR fill)
+            // SPP_TIMING=1: phase times on stderr (read / depth-cap simulation / offsets)
             static const bool timing = getenv("SPP_TIMING") != nullptr;
             auto now = [] { return std::chrono::steady_clock::now(); };
             const auto t0 = now();
-            Reads R;
+            P = new spp_plan();
+            Reads &R = P->R;
             if (region) { R.dlo = lo == INT64_MIN ? lo : lo - pad; R.dhi = hi == INT64_MAX ? hi : hi + pad; }
             if (f->bam) read_bam(f, tid, *p, R);
             else read_sam(f, tid, *p, R);
-            if (region && R.max_span > pad) { pad = 2 * R.max_span; continue; }
+            if (region && R.max_span > pad) {
+                pad = 2 * R.max_span;
+                release_plan(P);
+                P = nullptr;
+                continue;
+            }
             const auto t1 = now();
-            Tweaks T;
-            const std::vector<uint8_t> keep = simulate(R, *p, tid, T);   // every read: exact depth cap
+            P->keep = simulate(R, *p, tid, P->T);      // every read: exact depth cap
             const auto t2 = now();
             auto *B = new spp_batch();
             int64_t used = 0;
-            for (uint8_t k : keep) used += k;
+            for (uint8_t k : P->keep) used += k;
             B->n_used = used;
             B->n_dropped = (int64_t)R.size() - used;
-            fill_csr(R, keep, T, B, std::max(1, p->n_threads), lo, hi);
+            B->threads = std::max(1, p->n_threads);
+            P->rlo = lo;
+            P->rhi = hi;
+            plan_csr(*P, B);
+            B->plan = P;
+            P = nullptr;
             if (timing) {
                 const auto t3 = now();
-                auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-                fprintf(stderr, "[spp timing] read %.1f ms, simulate %.1f ms, fill %.1f ms (%zu reads, %d threads)\n",
-                        ms(t0, t1), ms(t1, t2), ms(t2, t3), (size_t)R.size(), p->n_threads);
+                auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+                fprintf(stderr, "[spp timing] read %.1f ms, simulate %.1f ms, offsets %.1f ms (%zu reads, %d threads)\n",
+                        ms(t0, t1), ms(t1, t2), ms(t2, t3), (size_t)B->plan->R.size(), p->n_threads);
             }
             *out = B;
             return 0;
         }
     } catch (const std::exception &e) {
+        release_plan(P);
         return fail(std::string("spp_pileup: ") + e.what());
     }
+}
+
+int spp_batch_fill(spp_batch *b, uint8_t *base_code, uint8_t *qual) {
+    if (!b) return fail("spp_batch_fill: null batch");
+    if (!b->plan) return fail("spp_batch_fill: the batch is already filled");
+    if ((base_code == nullptr) != (qual == nullptr)) return fail("spp_batch_fill: give both buffers or neither");
+    try {
+        static const bool timing = getenv("SPP_TIMING") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
+        const uint64_t E = b->n_entries;
+        if (!base_code) {
+            base_code = (uint8_t *)malloc(E + 16);
+            qual = (uint8_t *)malloc(E + 16);
+            if (!base_code || !qual) {
+                free(base_code);
+                free(qual);
+                return fail("spp_batch_fill: out of host memory for the pileup");
+            }
+            b->owns = true;
+        } else {
+            b->owns = false;
+        }
+        fill_csr(*b->plan, b, base_code, qual, b->threads);
+        release_plan(b->plan);       // helper thread
+        b->plan = nullptr;
+        if (timing)
+            fprintf(stderr, "[spp timing] fill %.1f ms (%s buffers)\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(),
+                    b->owns ? "own" : "caller");
+        return 0;
+    } catch (const std::exception &e) {
+        return fail(std::string("spp_batch_fill: ") + e.what());
+    }
+}
+
+int spp_pileup_plan(spp_file *f, int32_t tid, int64_t lo, int64_t hi, const spp_params *p, spp_batch **out) {
+    return plan_impl(f, tid, p, lo, hi, out);
+}
+
+static int pileup_impl(spp_file *f, int32_t tid, const spp_params *p, int64_t lo, int64_t hi, spp_batch **out) {
+    if (int rc = plan_impl(f, tid, p, lo, hi, out)) return rc;
+    if (int rc = spp_batch_fill(*out, nullptr, nullptr)) {
+        delete *out;
+        *out = nullptr;
+        return rc;
+    }
+    return 0;
 }
 
 int spp_pileup(spp_file *f, int32_t tid, const spp_params *p, spp_batch **out) {

@@ -76,7 +76,8 @@ class PileupEngine:
             self.reference = seq
 
     # -- hot path ---------------------------------------------------------------------------
-    def accumulate(self, pos_begin: int, offsets, codes, quals, borrow: bool = False, n_entries=None):
+    def accumulate(self, pos_begin: int, offsets, codes, quals, borrow: bool = False, n_entries=None,
+                   trusted: bool = False):
         """process_pileup_column over one CSR batch (:74-103).  numpy arrays are host buffers;
         torch tensors on this engine's device are consumed in place (``borrow`` keeps them as
         replay history without a copy — they must stay alive until reset())."""
@@ -88,8 +89,9 @@ class PileupEngine:
                 n_cols = len(o) - 1
                 if len(c) != len(q):
                     raise ValueError("codes and quals differ in length")
-                N.check(self._L.spg_accumulate(self._h, int(pos_begin), n_cols, N.ptr(o), N.ptr(c), N.ptr(q),
-                                               len(c)), "spg_accumulate")
+                # (trusted: the CSR comes from the pileup library, SPG_IN_TRUSTED skips the O(E) scan)
+                N.check(self._L.spg_accumulate_ex(self._h, int(pos_begin), n_cols, N.ptr(o), N.ptr(c), N.ptr(q),
+                                                  len(c), N.SPG_IN_TRUSTED if trusted else 0), "spg_accumulate")
             else:
                 import torch
                 for t in (offsets, codes, quals):

@@ -73,6 +73,32 @@ class FastaFile:
         pass
 
 
+class PinnedIngest:
+    """Pinned host staging for process_bam (spg_host_alloc): two buffer sets used alternately, so the
+    pileup of BAM k+1 is written while BAM k's entries are still being copied to HBM; a set is reused
+    only after the engine's input copies have landed (spg_wait_input).  Pinned pages are DMA'd without
+    a staging copy, take no page faults when reused, and let spg_accumulate return without a host
+    synchronisation."""
+
+    def __init__(self, engine):
+        self.engine = engine
+        self.sets = [None, None]
+        self.slot = 0
+
+    def buffers(self, n_entries: int, n_cols: int):
+        from .engine import pinned_empty
+        s = self.slot
+        self.slot ^= 1
+        need = int(n_entries) + 16
+        cur = self.sets[s]
+        self.engine.wait_input()               # this set's previous copy (and any older) has landed
+        if cur is None or cur[0].nbytes < need or cur[2].size < n_cols + 1:
+            cap = max(need, int(need * 1.125))
+            cur = (pinned_empty(cap), pinned_empty(cap), pinned_empty(int((n_cols + 1) * 1.125) + 1, np.uint64))
+            self.sets[s] = cur
+        return cur
+
+
 class LiveVariantCaller:
     def __init__(self, referenceFasta: str, minBaseQuality: int, minMappingQuality: int, minTotalDepth: int,
                  minAlleleDepth: int, minEvidenceRatio: float, maxVariants: int, device: Optional[int] = None,
@@ -95,6 +121,7 @@ class LiveVariantCaller:
         self.engine = PileupEngine(max(1, n_pos), minBaseQuality, minTotalDepth, minAlleleDepth, minEvidenceRatio,
                                    device=device, calls_only=True)
         self._lock = threading.RLock()
+        self._ingest = PinnedIngest(self.engine)
         self._batch_contig: List[int] = []       # FASTA reference index of each accumulated batch
         self.reset_memory()
 
@@ -169,12 +196,20 @@ class LiveVariantCaller:
         with AlignmentFile(inputBam) as bam:
             if contig not in bam.references:
                 raise ValueError(f"invalid contig `{contig}`")
-            batch = bam.pileup_batch(contig, self.pileup_params)
+            batch = bam.pileup_plan(contig, self.pileup_params)
         with self._lock:
             if batch.n_cols == 0:
+                batch.fill()
+                batch.close()
                 return
+            # the entries go straight into pinned staging (double-buffered): the copy to HBM runs on the
+            # engine's copy stream while the next BAM is read
+            codes, quals, offs = self._ingest.buffers(batch.n_entries, batch.n_cols)
+            batch.fill(codes, quals)
+            offs[:batch.n_cols + 1] = batch.offsets
+            E = batch.n_entries
             self._use_reference(referenceIndex)
-            self.engine.accumulate(batch.pos_begin, batch.offsets, batch.codes, batch.quals)
+            self.engine.accumulate(batch.pos_begin, offs[:batch.n_cols + 1], codes[:E], quals[:E], trusted=True)
             self._batch_contig.append(referenceIndex)
         batch.close()
 

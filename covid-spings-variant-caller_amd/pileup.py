@@ -43,7 +43,7 @@ class PileupBatch:
     """CSR batch owned by the native library: ``offsets`` u64[n_cols+1], ``codes``/``quals`` u8[E]
     (16 padding bytes follow both arrays), columns [pos_begin, pos_begin + n_cols)."""
 
-    def __init__(self, handle):
+    def __init__(self, handle, planned=False):
         L = N.pileup_lib()
         self._h = C.c_void_p(handle)
         pb, nc, ne, nu, nd = C.c_int64(), C.c_int64(), C.c_uint64(), C.c_int64(), C.c_int64()
@@ -51,6 +51,28 @@ class PileupBatch:
                  "spp_batch_info")
         self.pos_begin, self.n_cols, self.n_entries = pb.value, nc.value, ne.value
         self.n_reads_used, self.n_reads_dropped = nu.value, nd.value
+        if not planned:
+            self._arrays()
+
+    def fill(self, codes_buf=None, quals_buf=None):
+        """Second phase of AlignmentFile.pileup_plan: write base codes / qualities into the given uint8
+        arrays (>= n_entries + 16 each, e.g. pinned host memory reused across BAMs) or into the
+        library's own allocation.  Returns self."""
+        L = N.pileup_lib()
+        if (codes_buf is None) != (quals_buf is None):
+            raise ValueError("fill: give both buffers or neither")
+        if codes_buf is not None:
+            need = self.n_entries + 16
+            if codes_buf.nbytes < need or quals_buf.nbytes < need:
+                raise ValueError(f"fill: buffers must hold n_entries + 16 = {need} bytes")
+            N.pcheck(L.spp_batch_fill(self._h, N.ptr(codes_buf), N.ptr(quals_buf)), "spp_batch_fill")
+        else:
+            N.pcheck(L.spp_batch_fill(self._h, None, None), "spp_batch_fill")
+        self._arrays()
+        return self
+
+    def _arrays(self):
+        L = N.pileup_lib()
         po, pc, pq = C.c_void_p(), C.c_void_p(), C.c_void_p()
         N.pcheck(L.spp_batch_arrays(self._h, C.byref(po), C.byref(pc), C.byref(pq)), "spp_batch_arrays")
         E = self.n_entries
@@ -112,6 +134,20 @@ class AlignmentFile:
             hi = (1 << 62) if stop is None else int(stop)
             N.pcheck(L.spp_pileup_region(self._h, tid.value, lo, hi, C.byref(prm), C.byref(b)), "pileup")
         return PileupBatch(b.value)
+
+    def pileup_plan(self, reference: str, params: PileupParams | None = None, start: int | None = None,
+                    stop: int | None = None) -> PileupBatch:
+        """First phase of the two-phase pileup (spp_pileup_plan): reads parsed, depth cap applied, CSR
+        offsets and n_entries known; PileupBatch.fill() writes the entries (into caller buffers)."""
+        L = N.pileup_lib()
+        tid = C.c_int32()
+        N.pcheck(L.spp_target_id(self._h, reference.encode(), C.byref(tid)), "pileup")
+        b = C.c_void_p()
+        prm = (params or PileupParams()).native()
+        lo = -(1 << 63) if start is None else int(start)
+        hi = (1 << 63) - 1 if stop is None else int(stop)
+        N.pcheck(L.spp_pileup_plan(self._h, tid.value, lo, hi, C.byref(prm), C.byref(b)), "pileup")
+        return PileupBatch(b.value, planned=True)
 
     def close(self):
         if self._h:

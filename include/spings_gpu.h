@@ -59,6 +59,8 @@ extern "C" {
 #define SPG_IN_BORROW 0x2     /* with SPG_IN_DEVICE: keep the caller's device buffers as replay
                                  history without copying; they must stay valid until
                                  spg_reset/spg_destroy */
+#define SPG_IN_TRUSTED 0x4    /* host input produced by spp_pileup / spp_batch_fill (already valid CSR):
+                               skip the O(E) host validation scan */
 
 /* spg_params.flags */
 #define SPG_P_CALLS_ONLY 0x1  /* compute what prepare_variants() emits and nothing it cannot see: the

@@ -74,6 +74,15 @@ int spp_batch_info(spp_batch *b, int64_t *pos_begin, int64_t *n_cols, uint64_t *
 int spp_batch_arrays(spp_batch *b, const uint64_t **offsets, const uint8_t **base_code, const uint8_t **qual);
 int spp_batch_free(spp_batch *b);
 
+/* Two-phase pileup for an ingest pipeline: spp_pileup_plan parses the reads, applies the depth cap /
+ * overlap rules and computes the CSR offsets (n_entries known: spp_batch_info); spp_batch_fill then
+ * writes base_code / qual into caller buffers of >= n_entries + 16 bytes each (e.g. pinned memory from
+ * spg_host_alloc, reused across BAMs: no page faults, DMA-able), or into its own allocation when both
+ * are null.  The batch keeps the caller's pointers (spp_batch_arrays) and does not free them.  Region
+ * form: lo/hi as in spp_pileup_region (INT64_MIN / INT64_MAX = whole contig). */
+int spp_pileup_plan(spp_file *f, int32_t tid, int64_t lo, int64_t hi, const spp_params *p, spp_batch **out);
+int spp_batch_fill(spp_batch *b, uint8_t *base_code, uint8_t *qual);
+
 /* Synthetic read simulator (SURVEY.md §8 d "Synthetic inputs"): writes a coordinate-sorted BGZF
  * BAM of single-end reads (flag 0, MAPQ 60) over one contig — starts uniform on [0, L-read_len],
  * CIGAR read_len M (a del_frac share "70M2D..M", an ins_frac share "70M2I..M"), q =

@@ -172,3 +172,16 @@ def test_errors(planted, tmp_path):
     samgen.write_sam(other, [("chrX", 800)], samgen.snv_records("chrX", ref, 5, seed=1))
     with pytest.raises(ValueError):
         c.process_bam(other)
+
+
+def test_pinned_ingest_stream_vs_oracle(planted):
+    """A stream of process_bam calls (the live mode, vc_queue.py:142-144) through the pinned,
+    double-buffered staging: both buffer sets are reused, calls and memory equal the oracle's."""
+    d, ref, fasta, files = planted
+    c = _caller(fasta)
+    seq = [files[0], files[1], files[0], files[1], files[0]]
+    for f in seq:
+        c.process_bam(f)
+    compare_variants(c.prepare_variants(), _oracle(ref, seq).prepare_variants(), RTOL)
+    mem, omem = c.memory, _oracle(ref, seq).memory
+    assert list(mem) == list(omem) and all(mem[p] == omem[p] for p in omem)
