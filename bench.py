@@ -115,8 +115,10 @@ def measure(D, step, eng, K_min, reps, min_ms, every):
     eng.sync()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    flush = getattr(step, "flush", lambda: None)     # outstanding asynchronous gathers
     for k in range(3):
         step(k)
+    flush()
     eng.sync()
     est = D.max((time.perf_counter() - t0) / 3)
     K = max(K_min, int(math.ceil(min_ms * 1e-3 / max(est, 1e-7))))
@@ -132,6 +134,7 @@ def measure(D, step, eng, K_min, reps, min_ms, every):
             eng.set_timing(1 if k % every == 0 else 0)
             step(k)
         enq.append(time.perf_counter() - t0)       # host time to enqueue the K steps
+        flush()                                    # the last steps' gathers complete inside the window
         eng.sync()
         torch.cuda.synchronize()
         D.barrier()
@@ -146,6 +149,7 @@ def finalize_ms(step, eng, n=8):
     eng.set_timing(2)
     for k in range(n):
         step(k)
+    getattr(step, "flush", lambda: None)()
     eng.sync()
     _, f = eng.kernel_times(4096)
     eng.set_timing(0)
@@ -219,24 +223,42 @@ def run_point(args, D, L, depth, max_depth, local, world, rank, contig):
     eng.accumulate(0, d_off, d_c, d_q, borrow=True, n_entries=E)
     eng.finalize()
     n_cand, n_replay = eng.counts()
-    # call-table gather: persistent buffers, sized from this first pass (KBs per step)
+    # call-table gather: persistent double buffers, sized from this first pass (KBs per step).  The
+    # gather of step k runs asynchronously (RCCL's stream) while step k + 1 computes; a buffer is
+    # reused two steps later, after its gather has completed.
     cap = max(64, 4 * n_cand)
     cap = int(D.max(cap))
     rec = 56
-    gather_buf = torch.zeros(cap * rec + 8, dtype=torch.uint8, device=dev)
     gdev = dev if args.backend == "nccl" else torch.device("cpu")
-    send = gather_buf if args.backend == "nccl" else torch.zeros_like(gather_buf, device="cpu")
-    recv = [torch.zeros_like(send) for _ in range(world)] if (world > 1 and rank == 0) else None
+    gbufs = [torch.zeros(cap * rec + 8, dtype=torch.uint8, device=dev) for _ in range(2)]
+    sends = gbufs if args.backend == "nccl" else [torch.zeros_like(b, device="cpu") for b in gbufs]
+    recvs = [[torch.zeros_like(sd) for _ in range(world)] if (world > 1 and rank == 0) else None for sd in sends]
+    pending = [None, None]
 
     def step(k):
         eng.reset()
         eng.accumulate(0, d_off, d_c, d_q, borrow=True, n_entries=E)
         eng.finalize()
         if world > 1:
-            eng.copy_candidates_device(gather_buf, cap=cap)
+            j = k & 1
+            if pending[j] is not None:
+                pending[j].wait()                       # nccl: torch's stream waits on the gather
+                pending[j] = None
+                # the engine's stream (which writes the buffer) waits on torch's stream
+                eng._torch_stream().wait_stream(torch.cuda.current_stream(dev))
+            eng.copy_candidates_device(gbufs[j], cap=cap)
             if args.backend != "nccl":
-                send.copy_(gather_buf)                  # device -> persistent host buffer (gloo)
-            D.dist.gather(send, recv, dst=0)            # RCCL over xGMI for nccl
+                sends[j].copy_(gbufs[j])                # device -> persistent host buffer (gloo)
+            pending[j] = D.dist.gather(sends[j], recvs[j], dst=0, async_op=True)   # RCCL over xGMI
+
+    def flush():
+        for j in range(2):
+            if pending[j] is not None:
+                pending[j].wait()
+                pending[j] = None
+        torch.cuda.synchronize(dev)
+
+    step.flush = flush
 
     for k in range(args.warmup):
         step(k)
@@ -246,8 +268,10 @@ def run_point(args, D, L, depth, max_depth, local, world, rank, contig):
     if world > 1:
         # the gathered table must equal every rank's own table (count and bytes)
         step(0)
+        flush()
         eng.sync()
         torch.cuda.synchronize()
+        send, gather_buf, recv = sends[0], gbufs[0], recvs[0]
         mine = np.frombuffer(send.cpu().numpy().tobytes(), np.uint8) if args.backend != "nccl" else \
             gather_buf.cpu().numpy()
         n_mine = int(mine[:8].view(np.uint64)[0])
