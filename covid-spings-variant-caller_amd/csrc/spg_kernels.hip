@@ -1646,7 +1646,9 @@ __global__ __launch_bounds__(64 * MW) __attribute__((amdgpu_waves_per_eu(3, 8)))
                 fcnt += __popc(f80);
                 fsq = __builtin_amdgcn_udot4(q_, f80 >> 7, fsq, false);
                 if (any_msum) lut_sums(q_, msum ? f80 : 0u, lut, fsl, fse);
-                if (any_rsl) lut_sl(q_, rsl ? f80 : 0u, l1m8, fsl);
+                // FUSED: the REF allele's sum(ln(1-eps)) is needed only where a call is possible, so it
+                // is recomputed for those lanes after the pre-check (no LUT work for every entry)
+                if (!FUSED && any_rsl) lut_sl(q_, rsl ? f80 : 0u, l1m8, fsl);
                 if (ffirst == INF32 && f80) ffirst = (uint32_t)(x0 + 4 * d) + ((uint32_t)__builtin_ctz(f80) >> 3);
                 while (r80) {
                     const int sh = __builtin_ctz(r80) - 7;
@@ -1688,6 +1690,29 @@ __global__ __launch_bounds__(64 * MW) __attribute__((amdgpu_waves_per_eu(3, 8)))
                     P.list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u))] = p;
             }
             write = write && want;
+            if (write && rsl && len) {
+                // the REF allele's sum(ln(1-eps)) for this lane's column (its blocks are still in L2):
+                // every block load at once, then the fast entries' LUT sums
+                double rs = 0.0;
+                for (uint32_t u0 = 0; u0 < nblk; u0 += ONE_BLK) {
+                    u32x4 cw[ONE_BLK], qw[ONE_BLK];
+#pragma unroll
+                    for (int v = 0; v < ONE_BLK; v++) blk(s1, nblk, u0 + v, cw[v], qw[v]);
+#pragma unroll
+                    for (int v = 0; v < ONE_BLK; v++) {
+                        const int32_t x0 = (int32_t)(16u * (u0 + v)) - lead1;
+                        uint32_t vm[4];
+                        valid_masks<4>(x0, 0, (int32_t)len, vm);
+#pragma unroll
+                        for (int d = 0; d < 4; d++) {
+                            uint32_t f80, r80;
+                            swar4(dw<4>(cw[v], d), dw<4>(qw[v], d), vm[d], mrep, P.kpass, P.kok, f80, r80);
+                            lut_sl(dw<4>(qw[v], d), f80, l1m8, rs);
+                        }
+                    }
+                }
+                S.sl[Ms] += rs;
+            }
         }
         if (write) {                                   // this lane's record (FRESH), 16-B stores
             Acc a = Acc{};
