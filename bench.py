@@ -186,6 +186,8 @@ def build_shard(rank, world, L, depth, max_depth, device):
 
 def kernel_name(E, C):
     """The accumulate instantiation the engine picks for this batch (csrc/spg_api.cpp add_batch)."""
+    if E <= 40 * C:      # one shallow batch into a fresh memory (spg_api.cpp flush_run)
+        return "k_acc_one (+ k_acc_seg<1> for columns >= 128 entries)"
     if E < 256 * C:
         return "k_acc_multi (+ k_acc_seg<1> for columns >= 128 entries)"
     nt = 2 * E > (192 << 20)

@@ -405,12 +405,6 @@ static int trace_sync(spg_ctx *c, const char *what) {
     return e == hipSuccess ? 0 : fail(std::string("spg trace: ") + what + ": " + hipGetErrorString(e));
 }
 
-#ifndef SPG_GMAX
-#define SPG_GMAX 64
-#endif
-#ifndef SPG_NB
-#define SPG_NB 8
-#endif
 static constexpr int64_t NB_RING = SPG_NB;   // k_acc_seg's finishing ring (columns per wave when fused)
 
 static int64_t env_i64(const char *name, int64_t dflt) {
@@ -506,19 +500,21 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     const HistBatch &hb = c->hist[(size_t)idx];
     const int64_t n_cols = hb.n_cols;
     const double avg = (double)hb.n_entries / (double)n_cols;
-    // Each wave owns G consecutive columns.  A wave's setup (CSR offsets, then its first chunk) costs
-    // two memory round trips, so a deep wave gets ~16 chunks where that still leaves one grid
-    // generation of <= 4,096 waves (16 per CU) to fill the chip (1,000x: G = 8, 3,738 waves:
-    // 40 -> 36 us); otherwise G targets 16,384 waves (10,000x: G = 2, measured best).
+    // Each wave owns G consecutive columns.  A new wave costs a workgroup dispatch (median 1.4 us from
+    // the previous wave's end in its slot) and its setup (LUT + CSR offsets, then its first chunk: two
+    // memory round trips), so a deep wave gets ~24 chunks where that still leaves one grid generation
+    // of <= 4,096 waves (16 per CU) to fill the chip (1,000x: G = 8, 3,738 waves: 40 -> 36 us);
+    // otherwise G targets 16,384 waves.  10,000x: G = 3 (interleaved A/B on one box: 109.5 us vs
+    // 114.7 us for G = 2, 113.5 us for G = 5).
     static const int64_t target_waves = env_i64("SPG_TARGET_WAVES", 16384);
     int64_t g = std::max<int64_t>(1, (n_cols + target_waves - 1) / target_waves);
     if (deep_batch && !getenv("SPG_TARGET_WAVES")) {
-        const int64_t g_chunks = (int64_t)std::ceil(16384.0 / std::max(avg, 1.0));    // ~16 chunks per wave
+        const int64_t g_chunks = (int64_t)std::ceil(24576.0 / std::max(avg, 1.0));    // ~24 chunks per wave
         const int64_t g_fill = std::max<int64_t>(1, (n_cols + 4095) / 4096);           // one generation
         g = std::max<int64_t>(g, std::min(g_chunks, g_fill));
     }
     // fused: a wave's columns fit its finishing ring (its records stay in LDS for the finalize)
-    const uint32_t G = (uint32_t)std::min<int64_t>(F ? NB_RING : SPG_GMAX, g);
+    const uint32_t G = (uint32_t)std::min<int64_t>(F ? NB_RING : (deep_batch ? SPG_GMAX_DEEP : SPG_GMAX), g);
     KParams P{};
     P.pos_begin = hb.pos_begin;
     P.n_cols = n_cols;
@@ -549,6 +545,7 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     P.dbg = trace_on() ? trace_dbg() : nullptr;
     if (listed) {                 // the long columns k_acc_multi listed, one per wave
         P.G = 1;
+        P.G2 = 1;
         P.deep_list = c->deep_list;
         P.deep_n = c->deep_n;
     }

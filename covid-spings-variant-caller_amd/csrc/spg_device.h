@@ -22,6 +22,23 @@ constexpr uint32_t MISC_EXOTIC = 0x100u;  // acc.misc bit: an allele outside A,C
 // kernel skips them for a column's major allele when it is the REF char; finalize treats that
 // allele's hypothesis product as unknown and replays a position whose calls would depend on it)
 constexpr int MISC_SKIP_SHIFT = 9;
+// acc.misc bits 14..18: slot k's sum(eps) IS complete although its skip bit is set (only its
+// sum(ln(1-eps)) is not: the fused deep kernel's second allele in dual mode keeps QUAL's sum)
+constexpr int MISC_SEONLY_SHIFT = 14;
+
+// k_acc_seg's per-wave LDS: a finishing ring of SPG_NB columns (fused: a wave's whole group) and the
+// descriptors of its group (at most SPG_GMAX_DEEP columns per wave of a deep batch, SPG_GMAX for the
+// W = 1 kernel).  Sized so a 4-wave workgroup stays under 32 KiB: 5 workgroups per CU, so the waves of
+// a fifth start in the slots of finished waves while their workgroups' longest wave still runs.
+#ifndef SPG_NB
+#define SPG_NB 4
+#endif
+#ifndef SPG_GMAX
+#define SPG_GMAX 64
+#endif
+#ifndef SPG_GMAX_DEEP
+#define SPG_GMAX_DEEP 16
+#endif
 
 // Accumulators replacing Site (structs.py:2-6).  The q lists are replaced by sufficient
 // statistics: counts, the integer sum of q (log10 of the eps product up to fp64 rounding), the sum

@@ -123,6 +123,7 @@ __device__ __forceinline__ void merge_state(Acc &a, const MState &c, const KeyT 
     a.n_other += c.n_other;
     if (c.n_other) a.misc |= MISC_EXOTIC;
     a.misc |= (uint32_t)c.skip << MISC_SKIP_SHIFT;
+    a.misc &= ~((uint32_t)c.skip << MISC_SEONLY_SHIFT);
     const uint32_t have = order_mask(a.order);
     uint32_t newmask = 0;
 #pragma unroll
@@ -142,7 +143,7 @@ __device__ __forceinline__ void merge_state(Acc &a, const MState &c, const KeyT 
 
 // A FRESH record needs its sl/se half (bytes 80..159) only when some present slot holds sums
 __device__ __forceinline__ bool record_has_sums(const Acc &a) {
-    const uint32_t skip = (a.misc >> MISC_SKIP_SHIFT) & 0x1Fu;
+    const uint32_t skip = (a.misc >> MISC_SKIP_SHIFT) & ~(a.misc >> MISC_SEONLY_SHIFT) & 0x1Fu;
     bool sums = false;
 #pragma unroll
     for (int k = 0; k < NSLOT; k++) sums |= a.cnt[k] != 0 && !((skip >> k) & 1u);
@@ -519,6 +520,7 @@ __device__ __forceinline__ bool finalize_position(const FParams &F, const Acc *r
     if (!evaluated) { if (table) O.flags[pos] = flags; return false; }
     const int n = (int)(a.order & 7u);
     const uint32_t skip = (a.misc >> MISC_SKIP_SHIFT) & 0x1Fu;
+    const uint32_t skip_se = skip & ~(a.misc >> MISC_SEONLY_SHIFT);   // slots whose Σ eps is incomplete too
     uint32_t slot[NSLOT], cnts[NSLOT];
     LV Pv[NSLOT], Hv[NSLOT];
     double Sv[NSLOT];
@@ -560,6 +562,9 @@ __device__ __forceinline__ bool finalize_position(const FParams &F, const Acc *r
         G[h] = g.s == 0 ? g.v : (g.s == 3 ? NaN : 0.0);
         if (h < n && g.s == 3) unknown = true;
         // a candidate needs S = sum(GL) unless its own GL is exactly 0 (SCORE = 0 for any S)
+        // a candidate whose slot skipped Σ eps as well lacks its QUAL: exact replay (a REF-major skip on a
+        // slot that is not the record's REF: a reference switch between batches)
+        if (h < n && ((skip_se >> slot[h]) & 1u) && is_candidate(F, a, slot_code((int)slot[h]), cnts[h])) band = true;
         if (h < n && g.s != 1 && is_candidate(F, a, slot_code((int)slot[h]), cnts[h])) {
             cand_needs_s = true;
             if (g.s == 3) band = true;        // its own GL depends on terms not accumulated
@@ -599,21 +604,20 @@ __device__ __forceinline__ bool finalize_position(const FParams &F, const Acc *r
 // merge of rare record, fast sums and (not FRESH) the record already in HBM — in LDS, and the wave
 // writes the records with 16-B stores, ten lanes per record.  The serial per-column work of
 // process_pileup_column / process_svn's dict bookkeeping (:77-101) thus runs lane-parallel.
-#ifndef SPG_NB
-#define SPG_NB 8
+#ifndef SPG_FUSE_SL2
+#define SPG_FUSE_SL2 0       // 1: the fused kernel's second allele keeps Σ ln(1-eps) too (A/B builds)
 #endif
 #ifndef SPG_SEG_WPE
 #define SPG_SEG_WPE 4
-#endif
-#ifndef SPG_GMAX
-#define SPG_GMAX 64
 #endif
 constexpr int NB = SPG_NB;   // columns a wave finishes together
 constexpr int KW = 4;        // waves per k_acc_seg workgroup
 
 struct ColSum {              // one finished column's fast-path statistics (written by lane 0)
     uint32_t M, M2, fc, fs, fc2, fs2, ffirst, ffirst2;
-    uint32_t skipped, cj, crefc, fsamp;   // fsamp: first sample of a multi-sample column (0 otherwise)
+    uint32_t skipped, cj, crefc, fsamp;   // skipped: bit 0 the major's, bit 1 the second allele's likelihood
+                                          // sums were not accumulated; fsamp: first sample of a
+                                          // multi-sample column (0 otherwise)
     double fl, fe, fl2, fe2;
 };
 static_assert(sizeof(ColSum) == 80, "ColSum");
@@ -671,7 +675,16 @@ __device__ __forceinline__ void assemble_record(const KParams &P, const Acc *__r
     h0.x += R->depth + fc + fc2;                                      // :87
     h0.z = merge_order(h0.z, newmask, first);
     if (R->n_other) h0.w |= MISC_EXOTIC;
-    if (S->skipped && Ms >= 0) h0.w |= (1u << Ms) << MISC_SKIP_SHIFT;
+    if ((S->skipped & 1u) && Ms >= 0) {
+        h0.w |= (1u << Ms) << MISC_SKIP_SHIFT;
+        h0.w &= ~((1u << Ms) << MISC_SEONLY_SHIFT);           // its Σ eps is incomplete as well
+    }
+    if ((S->skipped & 2u) && s2 >= 0) {                       // Σ ln(1-eps) incomplete, Σ eps complete
+        const uint32_t b = 1u << s2;
+        const bool se_ok = !(h0.w & (b << MISC_SKIP_SHIFT)) || (h0.w & (b << MISC_SEONLY_SHIFT));
+        h0.w |= b << MISC_SKIP_SHIFT;
+        if (se_ok) h0.w |= b << MISC_SEONLY_SHIFT;
+    }
     h1.x += R->n_del + (M2 == SPG_CODE_DEL ? fc2 : 0u);
     h1.y += R->n_skip + (M2 == SPG_CODE_SKIP ? fc2 : 0u);
     h1.z += R->n_other;
@@ -753,8 +766,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     __shared__ uint32_t rqr[KW][QCAP];
     __shared__ Dual2 dual2[KW];
     __shared__ Acc accimg[KW][NB];
-    __shared__ ColDesc coldesc[KW][SPG_GMAX];
+    __shared__ ColDesc coldesc[KW][W == 4 ? SPG_GMAX_DEEP : SPG_GMAX];
     __shared__ Hist hdl;                                // FUSE: this batch's descriptor for the replay
+    const uint64_t we = P.wtime ? __builtin_amdgcn_s_memrealtime() : 0;   // SPG_WAVE_TIMES: wave entry
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * KW + (threadIdx.x >> 6);
+    // deep_list (the long columns of a shallow batch): the waves stride over the listed columns, one
+    // column each; otherwise one group of G consecutive columns per wave
+    const bool listed = W == 1 && P.deep_n != nullptr;  // (W = 4: compile-time off; the loop runs once)
+    // A wave's own group: its CSR offsets and REF chars are loaded before the LUT, so the two round
+    // trips of a starting wave overlap (the LUT's wait covers both)
+    const bool tail0 = !listed && wave >= (int64_t)P.w1;
+    const int64_t g00 = tail0 ? (int64_t)P.w1 * P.G + (wave - P.w1) * P.G2 : wave * P.G;
+    const int ng0 = (int)max((int64_t)0, min((int64_t)(tail0 ? P.G2 : P.G), P.n_cols - g00));
+    uint64_t ob0 = 0, oe0 = 0;
+    uint32_t refc0 = 0, fsv0 = 0;
+    if (!listed && lane < ng0) {
+        ob0 = off[g00 + lane]; oe0 = off[g00 + lane + 1]; refc0 = ref[P.pos_begin + g00 + lane];
+        if (P.fsamp) fsv0 = P.fsamp[g00 + lane];
+    }
     write_hist(P);
     if (FUSE && threadIdx.x == 0) hdl = P.hdesc;
     if constexpr (FUSE) {
@@ -765,19 +795,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         if (q >= 128u) lut[q + 128u] = make_double2(T->fast[q][0], T->fast[q][1]);
     }
     __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * KW + (threadIdx.x >> 6);
-    // deep_list (the long columns of a shallow batch): the waves stride over the listed columns, one
-    // column each; otherwise one group of G consecutive columns per wave
-    const bool listed = W == 1 && P.deep_n != nullptr;  // (W = 4: compile-time off; the loop runs once)
     const int64_t n_items = listed ? (int64_t)*P.deep_n : wave + 1;
     const int64_t istride = listed ? (int64_t)gridDim.x * KW : 1;
     for (int64_t item = wave; item < n_items; item += istride) {
-    const bool tail = !listed && wave >= (int64_t)P.w1;
-    const int64_t g0 = listed ? (int64_t)P.deep_list[item]
-                              : (tail ? (int64_t)P.w1 * P.G + (wave - P.w1) * P.G2 : wave * P.G);
+    const int64_t g0 = listed ? (int64_t)P.deep_list[item] : g00;
     if (g0 >= P.n_cols) continue;
-    const int ng = listed ? 1 : (int)min((int64_t)(tail ? P.G2 : P.G), P.n_cols - g0);
+    const int ng = listed ? 1 : ng0;
     // SPG_TRACE: lane 0 posts (stage, a, b, c) to host-mapped memory, so a fault leaves each wave's
     // last step readable by the host
     auto prog = [&](uint32_t stage, uint32_t a, uint32_t b, uint32_t c) {
@@ -811,6 +834,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     uint32_t mrep2 = 0, M2 = 0;
     bool sem = true;                           // the major is not the REF char (calls-only mode skips REF sums)
     bool skipped = false;                      // this column's major skipped its likelihood sums
+    bool skipped2 = false;                     // ... and its second allele (FUSE dual mode)
     auto drain = [&]() __attribute__((always_inline)) {
         prog(3, qn, nb, 0);
         wave_sync();
@@ -864,7 +888,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     uint64_t ob = 0, oe = 0;
     uint32_t refc = 0;
     uint32_t fsv = 0;                    // multi-sample batches: first sample holding entries of the column
-    if (lane < ng) {
+    if (!listed) {
+        ob = ob0; oe = oe0; refc = refc0; fsv = fsv0;
+    } else if (lane < ng) {
         ob = off[g0 + lane]; oe = off[g0 + lane + 1]; refc = ref[P.pos_begin + g0 + lane];
         if (P.fsamp) fsv = P.fsamp[g0 + lane];
     }
@@ -997,6 +1023,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
             mrep = M * 0x01010101u;
             sem = nibble_char(M) != (uint8_t)crefc;
             skipped = false;
+            skipped2 = false;
             dual = b2 >= 0;
             M2 = dual ? VC[b2] : 0u;
             mrep2 = dual ? M2 * 0x01010101u : 0xFFFFFFFFu;
@@ -1027,9 +1054,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 r80 &= ~g80;
             }
         };
-        auto body = [&](auto dual_tag, auto sl_tag) {
+        auto body = [&](auto dual_tag, auto sl_tag, auto sl2_tag) {
             constexpr bool DUAL = decltype(dual_tag)::value;
             constexpr bool SL = decltype(sl_tag)::value;     // false: counts / sum(q) only (calls-only REF major)
+            constexpr bool SL2 = DUAL && decltype(sl2_tag)::value;   // false: Σ eps only for the second allele
             uint32_t rany = 0;                  // the chunk slice's rare entries: bit 8 b + 7 - d
             uint32_t fcnt2 = 0, fsq2 = 0, lsq = 0;
             double fsl2 = 0.0, fse2 = 0.0;
@@ -1041,7 +1069,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 if constexpr (DUAL) {           // the second allele's entries leave the rare set
                     fcnt2 += __popc(g80);
                     fsq2 = __builtin_amdgcn_udot4(qw, g80 >> 7, fsq2, false);
-                    const uint32_t idx2 = (qw & 0x7F7F7F7Fu) ^ g80 ^ 0x80808080u;
+                }
+                if constexpr (DUAL && !SL2) {   // Σ eps only: the rows' second halves (8-B reads)
+                    const uint32_t idx2 = qw & ((g80 >> 7) * 0xFFu);
+                    fse2 += (lut[idx2 & 0xFFu].y + lut[(idx2 >> 8) & 0xFFu].y) +
+                            (lut[(idx2 >> 16) & 0xFFu].y + lut[idx2 >> 24].y);
+                    asm volatile("" : "+v"(fse2) :: "memory");
+                }
+                if constexpr (SL2) {
+                    const uint32_t idx2 = qw & ((g80 >> 7) * 0xFFu);
                     const double2 u0 = lut[idx2 & 0xFFu], u1 = lut[(idx2 >> 8) & 0xFFu];
                     fsl2 += u0.x + u1.x;
                     fse2 += u0.y + u1.y;
@@ -1056,7 +1092,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 lsq = __builtin_amdgcn_udot4(qw, f80, lsq, false);
                 if constexpr (SL) {
                     // fast entries have q < 128: their row is q; every other byte gets bit 7 -> a zero row
-                    const uint32_t idx = (qw & 0x7F7F7F7Fu) ^ f80 ^ 0x80808080u;
+                    const uint32_t idx = qw & ((f80 >> 7) * 0xFFu);
                     const double2 t0 = lut[idx & 0xFFu], t1 = lut[(idx >> 8) & 0xFFu];
                     const double2 t2 = lut[(idx >> 16) & 0xFFu], t3 = lut[idx >> 24];
                     fsl += (t0.x + t1.x) + (t2.x + t3.x);
@@ -1070,9 +1106,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 // second allele: lane-private LDS accumulators (no registers held across chunks)
                 __hip_atomic_fetch_add(&D2->cnt[lane], fcnt2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 __hip_atomic_fetch_add(&D2->sq[lane], fsq2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(&D2->sl[lane], fsl2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(&D2->se[lane], fse2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
+            if constexpr (SL2) __hip_atomic_fetch_add(&D2->sl[lane], fsl2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if constexpr (DUAL) __hip_atomic_fetch_add(&D2->se[lane], fse2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (!found || (DUAL && !found2)) {   // first fast entry of each fast allele (dict order)
                 uint32_t mine = INF32, mine2 = INF32;
 #pragma unroll
@@ -1098,14 +1134,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         using T_ = std::true_type;
         using F_ = std::false_type;
         if (dual) {
-            if (sem || !P.calls_only) body(T_{}, T_{});
-            else {                             // calls-only, REF major: only the second allele's sums
-                body(T_{}, F_{});
-                skipped = true;
+            // FUSE (calls-only): the second allele skips Σ ln(1-eps) but keeps Σ eps (QUAL).  Its H is
+            // needed only when its own GL is not exactly 0 — in a deep column the other allele's P
+            // underflows to 0 — and then finalize replays the position exactly.
+            if constexpr (FUSE && !SPG_FUSE_SL2) {
+                if (sem || !P.calls_only) body(T_{}, T_{}, F_{});
+                else { body(T_{}, F_{}, F_{}); skipped = true; }
+                skipped2 = true;
+            } else {
+                if (sem || !P.calls_only) body(T_{}, T_{}, T_{});
+                else {                         // calls-only, REF major: only the second allele's sums
+                    body(T_{}, F_{}, T_{});
+                    skipped = true;
+                }
             }
-        } else if (sem || !P.calls_only) body(F_{}, T_{});
+        } else if (sem || !P.calls_only) body(F_{}, T_{}, F_{});
         else {                                 // calls-only, REF major: counts and sum(q) only
-            body(F_{}, F_{});
+            body(F_{}, F_{}, F_{});
             skipped = true;
         }
         if (cs + 1 == cn) {                    // ---- column end ----
@@ -1117,13 +1162,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
             if (dual) {
                 wave_sync();
                 fc2 = dsum_u32(D2->cnt[lane]); fs2 = dsum_u32(D2->sq[lane]);
-                fl2 = dsum_f64(D2->sl[lane]); fe2 = dsum_f64(D2->se[lane]);
+                if (!skipped2) fl2 = dsum_f64(D2->sl[lane]);
+                fe2 = dsum_f64(D2->se[lane]);
             }
             const uint32_t fsc = (uint32_t)__builtin_amdgcn_readlane(fsv, (int)cj);
             if (lane == 0) {
                 ColSum *S = CS + nb;
                 S->M = M; S->M2 = dual ? M2 : 0u; S->fc = fc; S->fs = fs; S->fc2 = fc2; S->fs2 = fs2;
-                S->ffirst = ffirst; S->ffirst2 = ffirst2; S->skipped = skipped ? 1u : 0u; S->cj = cj;
+                S->ffirst = ffirst; S->ffirst2 = ffirst2; S->skipped = (skipped ? 1u : 0u) | (skipped2 ? 2u : 0u); S->cj = cj;
                 S->crefc = crefc; S->fl = fl; S->fe = fe; S->fl2 = fl2; S->fe2 = fe2;
                 S->fsamp = fsc;
             }
@@ -1170,7 +1216,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         const uint64_t wt2 = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
         const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
-        P.wtime[wave] = make_uint4((uint32_t)wt0, (uint32_t)g0, (uint32_t)(wt2 - wt0), (hw & 0xFFFFFu) | (xcc << 24));
+        // {entry, first column, lifetime from entry (bits 0-19) | entry-to-loop ticks (bits 20-31), hw id}
+        const uint64_t pro = min(wt0 - we, (uint64_t)0xFFF), life = min(wt2 - we, (uint64_t)0xFFFFF);
+        P.wtime[wave] = make_uint4((uint32_t)we, (uint32_t)g0, (uint32_t)(life | (pro << 20)), (hw & 0xFFFFFu) | (xcc << 24));
     }
     prog(6, 0, 0, 0);
     }   // items
@@ -1215,10 +1263,11 @@ __device__ __forceinline__ void ms_rare(MState &S, uint32_t code, uint32_t q, ui
 }
 
 // sum over a fast allele's entries of a dword: {ln(1-eps), eps} rows of the LDS LUT (row q for the
-// selected bytes, a zero row for every other byte)
+// selected bytes, whose q is in 4..127; row 0, which is zero, for every other byte: one address, so
+// the lanes' reads of it broadcast instead of spreading over 128 zero rows and their banks)
 __device__ __forceinline__ void lut_sums(uint32_t qw, uint32_t sel80, const double2 *__restrict__ lut, double &sl,
                                          double &se) {
-    const uint32_t idx = (qw & 0x7F7F7F7Fu) ^ sel80 ^ 0x80808080u;
+    const uint32_t idx = qw & ((sel80 >> 7) * 0xFFu);
     const double2 t0 = lut[idx & 0xFFu], t1 = lut[(idx >> 8) & 0xFFu];
     const double2 t2 = lut[(idx >> 16) & 0xFFu], t3 = lut[idx >> 24];
     sl += (t0.x + t1.x) + (t2.x + t3.x);
@@ -1228,7 +1277,7 @@ __device__ __forceinline__ void lut_sums(uint32_t qw, uint32_t sel80, const doub
 // sum of ln(1-eps) only (calls-only REF major of a shallow run: its sum(eps) is never used, the REF
 // allele is never a call): 8-B rows, half the LDS traffic of lut_sums
 __device__ __forceinline__ void lut_sl(uint32_t qw, uint32_t sel80, const double *__restrict__ l1m, double &sl) {
-    const uint32_t idx = (qw & 0x7F7F7F7Fu) ^ sel80 ^ 0x80808080u;
+    const uint32_t idx = qw & ((sel80 >> 7) * 0xFFu);
     sl += (l1m[idx & 0xFFu] + l1m[(idx >> 8) & 0xFFu]) + (l1m[(idx >> 16) & 0xFFu] + l1m[idx >> 24]);
 }
 
@@ -1846,6 +1895,7 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
     const int64_t blocks = P.deep_n ? std::min<int64_t>((P.n_cols + KW - 1) / KW, 2048) : (waves + KW - 1) / KW;
     const bool fresh = P.batch_seq == 1;
     const bool w4 = P.t_deep <= 1;
+    if (P.G > (uint32_t)(w4 ? SPG_GMAX_DEEP : SPG_GMAX) || (!P.deep_n && P.G2 > P.G)) return hipErrorInvalidValue;   // coldesc
     // batches far beyond the 256 MiB Infinity Cache stream with non-temporal loads
     const bool nt = 2 * P.n_entries > (192ull << 20);
     // (W = 1, and a deep batch into a memory that already holds records (the old record is read and

@@ -460,3 +460,40 @@ def test_fused_deep_finalize_replays(depth):
     t = eng.table()
     assert t["flags"][800] & 12 == 12 and t["flags"][801] & 12 == 12   # exotic + replayed
     eng.close()
+
+
+@pytest.mark.parametrize("shift", [0, 3, 8, 13])
+def test_fused_dual_second_allele_eps_only(shift):
+    """FUSE dual mode: a column's frequent second allele (an SNV at AF 0.05-0.5) accumulates counts,
+    sum(q) and sum(eps) but not sum ln(1-eps) (acc.misc skip + "eps complete" bits): a deep call's GL is
+    exactly 0 without it.  Entries at several 16-B alignments (the CSR shifted by `shift` bytes in device
+    memory).  Calls vs the oracle (QUAL within 1e-9), no replays for the deep calls, and a second,
+    unfused finalize from the records in memory gives the same calls bit for bit."""
+    import torch
+    from covid_spings_variant_caller_amd import synth
+    L = 3000
+    ref = synth.reference(L, seed=81)
+    p = dict(DEF, minEvidenceRatio=0.02)
+    lo, off, c, q = synth.pileup(L, 3000, seed=82, ref=ref, snv_every=13, lo=700, hi=1500)
+    E = len(c)
+    orc = COracle(ref, p["minBaseQuality"], p["minTotalDepth"], p["minAlleleDepth"], p["minEvidenceRatio"])
+    orc.accumulate(lo, off, c, q)
+    orc.finalize()
+    dc = torch.full((shift + E + 64,), 0xFF, dtype=torch.uint8, device="cuda")
+    dq = torch.zeros(shift + E + 64, dtype=torch.uint8, device="cuda")
+    dc[shift:shift + E] = torch.from_numpy(c).cuda()
+    dq[shift:shift + E] = torch.from_numpy(q).cuda()
+    do = torch.from_numpy(off.astype(np.int64) + shift).cuda()
+    eng = _engine(ref, p, calls_only=True)
+    eng.accumulate(lo, do, dc, dq, borrow=True, n_entries=E)
+    eng.finalize()
+    fused = eng.variants()
+    exp = orc.variants()
+    assert len(exp) > 40
+    compare_variants(fused, exp, rtol=RTOL)
+    eng.finalize()                                           # unfused: from the records in memory
+    compare_variants(eng.variants(), fused, rtol=0)
+    t = eng.table()
+    deep = [v["start"] for v in fused if v["info"]["DP"] >= 1000]
+    assert len(deep) > 40 and not (t["flags"][deep] & 4).any()   # deep calls: no exact replay
+    eng.close()

@@ -1,8 +1,8 @@
 """Per-wave timeline of the deep accumulate kernel (profiling; SPG_WAVE_TIMES instrumentation).
 
 Runs the bench's 10,000x SARS-CoV-2 batch through the fused accumulate a few times with
-SPG_WAVE_TIMES=<file> (k_acc_seg records per wave: start, lifetime in s_memrealtime ticks of
-10 ns, its first column, and HW_ID / XCC_ID), then reports the launch's span, the wave generations, setup and lifetime
+SPG_WAVE_TIMES=<file> (k_acc_seg records per wave: entry, lifetime from entry and entry-to-loop prologue in
+s_memrealtime ticks of 10 ns, its first column, and HW_ID / XCC_ID), then reports the launch's span, the wave generations, setup and lifetime
 distributions, and how the tail ends.  Usage: python tools/wavetimes.py [depth] [out.json]
 """
 import json
@@ -50,13 +50,14 @@ def analyse(path):
     t0 = w[:, 0].astype(np.int64)
     t0 = (t0 - t0.min()) * 10e-3                     # us
     col = w[:, 1].astype(np.int64)
-    life = w[:, 2] * 10e-3
+    life = (w[:, 2] & 0xFFFFF) * 10e-3              # from the wave's entry
+    pro = (w[:, 2] >> 20) * 10e-3                    # entry -> first chunk loop setup (LUT, CSR offsets)
     end = t0 + life
     xcc = w[:, 3] >> 24
     span = float(end.max())
     q = lambda a: {p: round(float(np.percentile(a, p)), 2) for p in (5, 25, 50, 75, 95, 100)}
     res = {"waves": int(len(w)), "G": g, "span_us": round(span, 2),
-           "start_us": q(t0), "life_us": q(life), "end_us": q(end),
+           "start_us": q(t0), "life_us": q(life), "prologue_us": q(pro), "end_us": q(end),
            "longest_waves": [{"first_column": int(col[i]), "life_us": round(float(life[i]), 2),
                               "start_us": round(float(t0[i]), 2)} for i in np.argsort(-life)[:8]],
            "waves_ending_after_span_minus_5us": int((end > span - 5).sum()),
@@ -64,6 +65,21 @@ def analyse(path):
            "busy_wave_us_over_span": round(float(life.sum()) / span, 1),
            "per_xcc_span_us": {int(x): round(float(end[xcc == x].max() - t0[xcc == x].min()), 2)
                                for x in np.unique(xcc)}}
+    # a workgroup's LDS is held until its longest wave ends: wave-time its finished waves leave idle
+    # (records are indexed by wave id; 4 waves per workgroup)
+    nb4 = len(w) // 4 * 4
+    blk_end = end[:nb4].reshape(-1, 4).max(axis=1)
+    res["workgroup_slack_over_wave_time"] = round(float((blk_end[:, None] - end[:nb4].reshape(-1, 4)).sum())
+                                                  / float(life.sum()), 3)
+    # wave slot turnover: per hardware wave slot (XCC, HW_ID wave/SIMD/CU/SA/SE fields), the gap from
+    # one wave's end to the next wave's entry in that slot (dispatch of the next workgroup)
+    key = (xcc.astype(np.int64) << 20) | (w[:, 3] & 0xFFFF).astype(np.int64)
+    o = np.lexsort((t0, key))
+    same = key[o][1:] == key[o][:-1]
+    gaps = (t0[o][1:] - end[o][:-1])[same]
+    if len(gaps):
+        res["slot_gap_us"] = q(gaps)
+        res["slot_gap_total_over_wave_time"] = round(float(np.clip(gaps, 0, None).sum()) / float(life.sum()), 3)
     hist, edges = np.histogram(t0, bins=20, range=(0, span))
     res["start_histogram"] = hist.tolist()
     conc = [int(((t0 <= t) & (end > t)).sum()) for t in np.linspace(0, span, 23)[1:-1]]
