@@ -99,7 +99,7 @@ def build_pileup(force=False, verbose=False) -> str:
     deps = srcs + [os.path.join(INC, "spings_pileup.h")]
     if force or _stale(out, deps):
         cxx = shutil.which("g++") or "g++"
-        cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{INC}", "-o", out + ".tmp"] + srcs + ["-lz", "-pthread"]
+        cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{INC}", "-o", out + ".tmp"] + srcs + ["-lz", "-ldl", "-pthread"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         _run(cmd)
