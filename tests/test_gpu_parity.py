@@ -497,3 +497,28 @@ def test_fused_dual_second_allele_eps_only(shift):
     deep = [v["start"] for v in fused if v["info"]["DP"] >= 1000]
     assert len(deep) > 40 and not (t["flags"][deep] & 4).any()   # deep calls: no exact replay
     eng.close()
+
+
+def test_fused_then_more_batches_keep_eps_bits_exact():
+    """A fused deep finalize (second alleles keep only sum(eps): acc.misc eps-complete bits), then more
+    batches into the same memory — a deep one (k_acc_seg, non-FRESH record merge) and a shallow one
+    (k_acc_multi) — each followed by a finalize: calls vs the oracle after every step."""
+    from covid_spings_variant_caller_amd import synth
+    L = 3000
+    ref = synth.reference(L, seed=91)
+    p = dict(DEF, minEvidenceRatio=0.02)
+    b1 = synth.pileup(L, 3000, seed=92, ref=ref, snv_every=13, lo=600, hi=1400)
+    b2 = synth.pileup(L, 2000, seed=93, ref=ref, snv_every=17, lo=900, hi=1700)
+    b3 = synth.pileup(L, 40, seed=94, ref=ref, snv_every=11, lo=0, hi=L)
+    orc = COracle(ref, p["minBaseQuality"], p["minTotalDepth"], p["minAlleleDepth"], p["minEvidenceRatio"])
+    eng = _engine(ref, p, calls_only=True)
+    for b in (b1, b2, b3):
+        eng.accumulate(*b)
+        orc.accumulate(*b)
+        eng.finalize()
+        orc.finalize()
+        got, exp = eng.variants(), orc.variants()
+        assert len(exp) > 20
+        compare_variants(got, exp, rtol=RTOL)
+    assert eng.memory_summary() == orc.memory_summary()
+    eng.close()
