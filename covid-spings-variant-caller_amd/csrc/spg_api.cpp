@@ -502,14 +502,16 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     const double avg = (double)hb.n_entries / (double)n_cols;
     // Each wave owns G consecutive columns.  A new wave costs a workgroup dispatch (median 1.4 us from
     // the previous wave's end in its slot) and its setup (LUT + CSR offsets, then its first chunk: two
-    // memory round trips), so a deep wave gets ~24 chunks where that still leaves one grid generation
+    // memory round trips), so a deep wave gets ~22-30 chunks where that still leaves one grid generation
     // of <= 4,096 waves (16 per CU) to fill the chip (1,000x: G = 8, 3,738 waves: 40 -> 36 us);
     // otherwise G targets 16,384 waves.  10,000x: G = 3 (interleaved A/B on one box: 109.5 us vs
     // 114.7 us for G = 2, 113.5 us for G = 5).
     static const int64_t target_waves = env_i64("SPG_TARGET_WAVES", 16384);
     int64_t g = std::max<int64_t>(1, (n_cols + target_waves - 1) / target_waves);
     if (deep_batch && !getenv("SPG_TARGET_WAVES")) {
-        const int64_t g_chunks = (int64_t)std::ceil(24576.0 / std::max(avg, 1.0));    // ~24 chunks per wave
+        // ~22-30 chunks per wave: G = 3 at both 10,000x (10 chunks a column) and the 8000-capped
+        // 7,960x (8 chunks; G = 4 there measured 103.5 vs 95.9 us)
+        const int64_t g_chunks = (int64_t)std::ceil(22528.0 / std::max(avg, 1.0));
         const int64_t g_fill = std::max<int64_t>(1, (n_cols + 4095) / 4096);           // one generation
         g = std::max<int64_t>(g, std::min(g_chunks, g_fill));
     }
