@@ -745,28 +745,51 @@ struct Tweaks {
     std::unordered_map<size_t, std::vector<uint8_t>> orig;      // first mate -> qualities before
 };
 
-// Min-queue of (end, read) for the live buffer.  Reads arrive in start order, so their ends are
-// mostly non-decreasing (equal-length reads): those go to a FIFO, the rest to a heap.  The order
-// among equal ends is immaterial (scan frees every read with end <= col).
+// The live buffer's reads keyed by end, for "free every read with end <= col" (the order among equal
+// ends is immaterial).  A bucket ring over end positions: a live read's end lies within its span of
+// the scan position, so ends in [lo, lo + S) index the ring directly (O(1) push and pop; a binary
+// heap took ~45 % of the reads at 10,000x, whose ends are not monotone); ends beyond the ring (after
+// a coverage gap) wait in an overflow heap.
 struct EndQueue {
     using E = std::pair<int64_t, size_t>;
-    std::deque<E> fifo;
-    std::priority_queue<E, std::vector<E>, std::greater<E>> heap;
-    size_t size() const { return fifo.size() + heap.size(); }
-    bool empty() const { return fifo.empty() && heap.empty(); }
+    std::vector<std::vector<size_t>> ring;
+    size_t mask = 0;
+    int64_t lo = INT64_MIN;             // every end < lo has been popped
+    size_t cnt = 0;                     // reads in the ring
+    std::priority_queue<E, std::vector<E>, std::greater<E>> ov;
+    explicit EndQueue(int64_t max_span) {
+        size_t S = 64;
+        while ((int64_t)S < max_span + 2 && S < ((size_t)1 << 20)) S <<= 1;
+        ring.resize(S);
+        mask = S - 1;
+    }
+    size_t size() const { return cnt + ov.size(); }
     void emplace(int64_t end, size_t r) {
-        if (fifo.empty() || fifo.back().first <= end) fifo.emplace_back(end, r);
-        else heap.emplace(end, r);
+        if (cnt == 0 && end >= lo) lo = end;          // empty ring: start it at this end
+        if (end >= lo && end - lo < (int64_t)ring.size()) {
+            ring[(size_t)end & mask].push_back(r);
+            cnt++;
+        } else {
+            ov.emplace(end, r);
+        }
     }
-    const E &top() const {
-        if (heap.empty()) return fifo.front();
-        if (fifo.empty()) return heap.top();
-        return heap.top().first < fifo.front().first ? heap.top() : fifo.front();
-    }
-    void pop() {
-        if (heap.empty()) fifo.pop_front();
-        else if (fifo.empty() || heap.top().first < fifo.front().first) heap.pop();
-        else fifo.pop_front();
+    template <class Fn> void pop_upto(int64_t col, Fn &&fn) {
+        while (!ov.empty() && ov.top().first <= col) {
+            const size_t r = ov.top().second;
+            ov.pop();
+            fn(r);
+        }
+        if (cnt == 0) {
+            if (col >= lo) lo = col + 1;
+            return;
+        }
+        for (; lo <= col && cnt; lo++) {
+            std::vector<size_t> &b = ring[(size_t)lo & mask];
+            for (size_t r : b) fn(r);
+            cnt -= b.size();
+            b.clear();
+        }
+        if (cnt == 0 && col >= lo) lo = col + 1;
     }
 };
 
@@ -786,7 +809,9 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
     std::vector<uint8_t> keep(n, 0);
     const int64_t maxcnt = p.max_depth > 0 ? p.max_depth : INT64_MAX;
     // live buffer: reads pushed and not yet freed.  Freed while scanning column c when end <= c.
-    EndQueue by_end;
+    int64_t max_span = 0;
+    for (size_t r = 0; r < n; r++) max_span = std::max(max_span, R.end[r] - R.pos[r]);
+    EndQueue by_end(max_span);
     std::vector<uint8_t> freed(n, 0);
     size_t head = 0;                          // oldest pushed read not yet freed (list head)
     std::vector<size_t> pushed;               // kept reads in push order
@@ -803,12 +828,10 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
         if (itr != olap.end()) olap.erase(itr);
     };
     auto scan = [&](int64_t col) {            // free reads with end <= col (bam_plp_next)
-        while (!by_end.empty() && by_end.top().first <= col) {
-            const size_t r = by_end.top().second;
-            by_end.pop();
+        by_end.pop_upto(col, [&](size_t r) {
             freed[r] = 1;
             olap_remove(r);
-        }
+        });
         while (head < pushed.size() && freed[pushed[head]]) head++;
     };
     auto advance = [&]() {                     // bam_plp_next loop while max_pos > pos

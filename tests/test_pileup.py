@@ -229,3 +229,35 @@ def test_region_pileup_equals_whole_contig_slice(tmp_path, fmt, kw):
                 assert len(got[1]) == 1 or int(got[1][-1]) == 0
             else:
                 assert_same(got, exp)
+
+
+@pytest.mark.parametrize("max_depth", [0, 3, 8000])
+def test_long_spans_and_coverage_gaps(tmp_path, max_depth):
+    """The depth-cap simulation's end queue (a bucket ring sized by the longest read span, an overflow
+    heap beyond it): stacked short reads, reads with 5,000-base refskips still live while later
+    clusters start, coverage gaps wider than the ring, and reads past every live end."""
+    import random
+    rng = random.Random(7)
+    recs = []
+
+    def rec(i, pos1, cigar, n):
+        seq = "".join(rng.choice("ACGT") for _ in range(n))
+        qual = "".join(chr(33 + rng.randrange(2, 41)) for _ in range(n))
+        recs.append(dict(qname=f"r{i}", flag=0, rname="c", pos=pos1, mapq=60, cigar=cigar, rnext="*", pnext=0,
+                         tlen=0, seq=seq, qual=qual))
+
+    i = 0
+    for start in [1] * 6 + [3, 5, 5, 9, 20, 40]:                  # a stack (cap stress) and stragglers
+        rec(i, start, "20M", 20); i += 1
+    rec(i, 10, "10M5000N10M", 20); i += 1                          # long span: ring of 8,192
+    rec(i, 12, "5M3D5M", 10); i += 1
+    for start in [3000] * 5 + [3001, 3020, 3040]:                  # while the long read is live
+        rec(i, start, "30M", 30); i += 1
+    for start in [12000] * 4 + [12005, 12010]:                     # ends past lo + 8,192: overflow heap
+        rec(i, start, "25M", 25); i += 1
+    for start in [30000, 30000, 30001, 45000]:                     # gaps after every read has ended
+        rec(i, start, "15M2I13M", 30); i += 1
+    recs.sort(key=lambda r: r["pos"])                             # coordinate order (stable)
+    sam = str(tmp_path / "spans.sam")
+    samgen.write_sam(sam, [("c", 50000)], recs)
+    assert_same(product(sam, "c", max_depth=max_depth), oracle(sam, "c", max_depth=max_depth))
