@@ -604,6 +604,9 @@ __device__ __forceinline__ bool finalize_position(const FParams &F, const Acc *r
 // merge of rare record, fast sums and (not FRESH) the record already in HBM — in LDS, and the wave
 // writes the records with 16-B stores, ten lanes per record.  The serial per-column work of
 // process_pileup_column / process_svn's dict bookkeeping (:77-101) thus runs lane-parallel.
+#ifndef SPG_NT_MIB
+#define SPG_NT_MIB 192       // batches whose entries exceed this stream with non-temporal loads
+#endif
 #ifndef SPG_FUSE_SL2
 #define SPG_FUSE_SL2 0       // 1: the fused kernel's second allele keeps Σ ln(1-eps) too (A/B builds)
 #endif
@@ -1897,7 +1900,7 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
     const bool w4 = P.t_deep <= 1;
     if (P.G > (uint32_t)(w4 ? SPG_GMAX_DEEP : SPG_GMAX) || (!P.deep_n && P.G2 > P.G)) return hipErrorInvalidValue;   // coldesc
     // batches far beyond the 256 MiB Infinity Cache stream with non-temporal loads
-    const bool nt = 2 * P.n_entries > (192ull << 20);
+    const bool nt = 2 * P.n_entries > ((uint64_t)SPG_NT_MIB << 20);
     // (W = 1, and a deep batch into a memory that already holds records (the old record is read and
     // merged): 3 waves per SIMD, so the register allocation needs no scratch)
 #define SPG_SEG(WW, FF, NN) hipLaunchKernelGGL((k_acc_seg<WW, FF, (WW == 1 || !FF) ? 3 : SPG_SEG_WPE, NN, false>), dim3((unsigned)blocks), dim3(64 * KW), 0, st, P, off, code, qual, ref, T, acc)
