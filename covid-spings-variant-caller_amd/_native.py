@@ -86,6 +86,8 @@ def gpu_lib():
     _sig(L.spg_host_alloc, i32, C.c_size_t, C.POINTER(vp))
     _sig(L.spg_host_free, i32, vp)
     _sig(L.spg_wait_input, i32, vp)
+    _sig(L.spg_input_ticket, i32, vp, C.POINTER(u64))
+    _sig(L.spg_wait_ticket, i32, vp, u64)
     _sig(L.spg_finalize, i32, vp)
     _sig(L.spg_sync, i32, vp)
     _sig(L.spg_stream, i32, vp, C.POINTER(vp))

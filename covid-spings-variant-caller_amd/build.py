@@ -21,8 +21,8 @@ LIBDIR = os.path.join(PKG, "_lib")
 INC = os.path.join(ROOT, "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-GPU_SOURCES = ["spg_kernels.hip", "spg_api.cpp"]
-GPU_HEADERS = ["spg_device.h"]
+GPU_SOURCES = ["spg_kernels.hip", "spg_tile.hip", "spg_lite.hip", "spg_api.cpp"]
+GPU_HEADERS = ["spg_device.h", "spg_common.h"]
 PILEUP_SOURCES = ["spp_pileup.cpp"]
 
 
@@ -62,7 +62,7 @@ def build_gpu(force=False, verbose=False) -> str:
 
 
 # kernels on the measured paths: a scratch spill there costs occupancy and time (tests/test_cabi.py)
-HOT_KERNELS = ("k_acc_seg<4", "k_acc_one", "k_acc_multi", "k_finalize")
+HOT_KERNELS = ("k_acc_seg<4", "k_acc_tile", "k_acc_lite", "k_acc_one", "k_acc_multi", "k_finalize")
 
 
 def kernel_resources(remarks: str) -> dict:

@@ -23,6 +23,13 @@ hipError_t launch_multi(const MParams &P, const Hist *H, const uint8_t *ref, con
                         int64_t max_blocks, bool fused, hipStream_t st);
 hipError_t launch_one(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc,
                       int64_t max_blocks, bool fused, hipStream_t st);
+hipError_t launch_lite(const MParams &P, const Hist &hb, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
+                       hipStream_t st);
+int lite_blocks_per_cu();
+hipError_t launch_tile(const MParams &P, const Hist *H, const uint8_t *ref, int64_t ref_len, const Tables *T, Acc *acc,
+                       int lpc, int64_t max_blocks, bool fused, hipStream_t st);
+hipError_t launch_merge(const MParams &P, const uint8_t *ref, Acc *acc, hipStream_t st);
+int tile_blocks_per_cu(int lpc, bool fused, bool one);
 }  // namespace spg
 
 using namespace spg;
@@ -91,12 +98,19 @@ struct Arena {
 
 struct spg_ctx {
     int device = 0;
+    int n_cu = 256;                     // compute units (the tile kernel's resident grid: 5 workgroups per CU)
     int64_t n_pos = 0;
     spg_params p{};
     hipStream_t stream = nullptr;       // kernels
     hipStream_t copy_stream = nullptr;  // host -> device batch copies
     hipEvent_t copy_ev = nullptr;       // after the latest batch copy
     hipEvent_t compute_ev = nullptr;    // reset fence: recycled arena copies wait for the old kernels
+    hipEvent_t hist_ev = nullptr;       // after the latest descriptor upload (pinned mirror -> d_hist)
+    bool hist_up = false;               // an upload was enqueued since the last reset
+    bool hist_fence = false;            // reset since that upload: the mirror's first rewrite waits for it
+    static constexpr int NIN = 8;       // input tickets: an event per host-input batch copy (ring)
+    hipEvent_t in_ev[NIN] = {};
+    uint64_t in_seq = 0;
     bool copy_pending = false;          // the compute stream has not waited on copy_ev yet
     bool arena_fence = false;           // the arena was recycled: the next copy into it waits for the kernels
                                         // enqueued before the reset (recorded lazily: an event record per
@@ -229,13 +243,18 @@ int spg_create(int device, int64_t n_pos, const spg_params *p, spg_ctx **out) {
     int rc = 0;
     auto bail = [&](int r) { spg_destroy(c); return r; };
     if (hipSetDevice(device) != hipSuccess) return bail(fail("spg_create: hipSetDevice failed"));
+    if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->n_cu <= 0)
+        c->n_cu = 256;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail("spg_create: stream"));
     if (hipEventCreateWithFlags(&c->copy_ev, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->compute_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ridx_ev, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&c->ridx_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->hist_ev, hipEventDisableTiming) != hipSuccess)
         return bail(fail("spg_create: event"));
+    for (auto &e : c->in_ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return bail(fail("spg_create: event"));
     if (hipMalloc(&c->acc, sizeof(Acc) * n_pos) != hipSuccess) return bail(fail("spg_create: acc alloc"));
     if (hipMalloc(&c->tables, sizeof(Tables)) != hipSuccess) return bail(fail("spg_create: tables alloc"));
     if (hipMemsetAsync(c->acc, 0, sizeof(Acc) * n_pos, c->stream) != hipSuccess) return bail(fail("memset"));
@@ -276,7 +295,9 @@ int spg_destroy(spg_ctx *c) {
     for (auto &row : c->ev)
         for (auto &e : row)
             if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {c->copy_ev, c->compute_ev, c->ridx_ev})
+    for (hipEvent_t e : {c->copy_ev, c->compute_ev, c->ridx_ev, c->hist_ev})
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->in_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -292,7 +313,10 @@ int spg_reset(spg_ctx *c) {
     // batches still pending belong to the old sample: dropped.  Copies into the recycled arena are
     // ordered after every kernel enqueued so far (add_batch records that fence before its first copy).
     if (!c->arena.slabs.empty()) c->arena_fence = true;
+    // descriptor uploads still queued read the pinned mirror, which the next sample rewrites from index 0
+    if (c->hist_up) c->hist_fence = true;
     clear_history(c);
+    HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));   // a new sample starts error-free
     if (++c->epoch == 0) {     // wrapped: clear the records once and restart at epoch 1
         HIPCHK(hipMemsetAsync(c->acc, 0, sizeof(Acc) * c->n_pos, c->stream));
         c->epoch = 1;
@@ -336,11 +360,14 @@ int spg_set_eps_lut(spg_ctx *c, const double lut[256]) {
 
 static int flush_run(spg_ctx *c, int64_t h1 = -1, bool fused = false);
 static int flush_deep(spg_ctx *c);
+static int materialize(spg_ctx *c);
 
 int spg_set_reference(spg_ctx *c, const char *seq, int64_t len) {
     if (!c || !seq || len < 0) return fail("spg_set_reference: bad argument");
     HIPCHK(hipSetDevice(c->device));
-    // pending batches take their first-visit REF chars from the reference they were accumulated under
+    // pending batches take their first-visit REF chars from the reference they were accumulated under, and
+    // so do the records a fused finalize left unwritten (materialize re-folds them under this reference)
+    if (int rc = materialize(c)) return rc;
     if (int rc = flush_deep(c)) return rc;
     if (int rc = flush_run(c)) return rc;
     if (c->ref) {
@@ -598,8 +625,62 @@ static int flush_deep(spg_ctx *c) {
     return acc_end(c);
 }
 
-// Fold the pending run [pend0, size) into the records: k_acc_multi (+ k_merge_parts when split), and
-// for a single batch the long columns through k_acc_seg<1>.
+// How a run of shallow batches [h0, h1) over positions [u0, u1) is folded.  k_acc_tile (default): LPC lanes
+// per column so that a tile's bytes of one batch fit a 2 KiB DMA slot (TC = 64 / LPC columns per tile), and
+// the batch range split S ways when the tiles alone cannot fill the resident grid (items of equal work:
+// S is the smallest split whose last round keeps >= 90 % of the waves busy).  SPG_SHALLOW=old: the r02
+// kernels (k_acc_one / k_acc_multi, A/B only).
+struct RunPlan {
+    bool tile;
+    int lpc;
+    int64_t n_groups, S, kper, tc;
+};
+static bool shallow_old() {
+    static const bool old = [] { const char *e = getenv("SPG_SHALLOW"); return e && strcmp(e, "old") == 0; }();
+    return old;
+}
+static int64_t tile_blocks(const spg_ctx *c, int lpc, bool fused, bool one) {
+    static const int64_t env = [] { const char *e = getenv("SPG_TILE_BLOCKS"); return e ? atoll(e) : 0ll; }();
+    return env > 0 ? env : (int64_t)c->n_cu * tile_blocks_per_cu(lpc, fused, one);
+}
+static RunPlan plan_run(const spg_ctx *c, int64_t h0, int64_t h1, int64_t u0, int64_t u1, uint64_t run_entries) {
+    const int64_t K = h1 - h0, L = u1 - u0;
+    RunPlan R{!shallow_old(), 1, 0, 1, K, 64};
+    if (!R.tile) {
+        R.n_groups = (L + 63) / 64;
+        static const int64_t target_items = env_i64("SPG_MULTI_ITEMS", 16384);
+        int64_t S = std::min<int64_t>(K, std::max<int64_t>(1, target_items / std::max<int64_t>(1, R.n_groups)));
+        R.kper = (K + S - 1) / S;
+        R.S = (K + R.kper - 1) / R.kper;
+        return R;
+    }
+    // bytes of one batch in a tile: TC x mean column length (whole 16-B blocks around it)
+    static const double fill = [] { const char *e = getenv("SPG_TILE_FILL"); return e ? atof(e) : 1984.0; }();
+    const double mean = (double)run_entries / ((double)K * (double)std::max<int64_t>(1, L));
+    while (R.lpc < 8 && (64.0 / R.lpc) * mean > fill) R.lpc *= 2;
+    R.tc = 64 / R.lpc;
+    R.n_groups = (L + R.tc - 1) / R.tc;
+    // (resident waves: the fused and plain forms have the same LDS and register footprint)
+    const int64_t waves = tile_blocks(c, R.lpc, false, false) * 2;
+    int64_t best = 1;
+    if (K > 1 && R.n_groups < waves) {
+        double best_eff = -1.0;
+        for (int64_t S = 1; S <= std::min<int64_t>(K, 64); S++) {
+            const int64_t kper = (K + S - 1) / S, s_eff = (K + kper - 1) / kper;
+            const double items = (double)(R.n_groups * s_eff);
+            const double rounds = std::ceil(items / (double)waves);
+            const double eff = items / (rounds * (double)waves);
+            if (eff > best_eff + 1e-9) { best_eff = eff; best = S; }
+            if (eff >= 0.9) { best = S; break; }
+        }
+    }
+    R.kper = (K + best - 1) / best;
+    R.S = (K + R.kper - 1) / R.kper;
+    return R;
+}
+
+// Fold the pending run [pend0, size) into the records: k_acc_tile (+ k_merge_parts when split), and for a
+// single batch the long columns through k_acc_seg<1>.
 static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
     if (h1 < 0) h1 = (int64_t)c->hist.size();
     const int64_t h0 = c->pend0;
@@ -617,32 +698,30 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
     if (int rc = acc_begin(c)) return rc;
     // descriptors of the run (pinned mirror -> device table)
     HIPCHK(hipMemcpyAsync(c->d_hist + h0, c->h_hist + h0, sizeof(Hist) * K, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipEventRecord(c->hist_ev, c->stream));
+    c->hist_up = true;
+    uint64_t run_entries = 0;
+    for (int64_t i = h0; i < h1; i++) run_entries += c->hist[(size_t)i].n_entries;
+    const RunPlan R = plan_run(c, h0, h1, u0, u1, run_entries);
     MParams P{};
     P.u0 = u0;
     P.u1 = u1;
     P.h0 = (int32_t)h0;
     P.K = K;
-    P.n_groups = (int32_t)((u1 - u0 + 63) / 64);
-    // split the run over batch ranges when its positions alone cannot fill the chip (16,384 items:
-    // 2,000 per-BAM SARS-CoV-2 batches 4.55 -> 4.24 ms vs 8,192; 32,768 no better)
-    static const int64_t target_items = env_i64("SPG_MULTI_ITEMS", 16384);
-    int64_t S = std::min<int64_t>(K, std::max<int64_t>(1, target_items / std::max<int32_t>(1, P.n_groups)));
-    const int64_t kper = (K + S - 1) / S;
-    S = (K + kper - 1) / kper;
-    P.S = (int32_t)S;
-    P.kper = (int32_t)kper;
+    P.n_groups = (int32_t)R.n_groups;
+    P.S = (int32_t)R.S;
+    P.kper = (int32_t)R.kper;
+    P.pstride = R.n_groups * R.tc;
     fill_swar(c, P.min_bq, P.qlo, P.kpass, P.kok);
     P.seq0 = c->hist[(size_t)h0].seq0;
     P.epoch = c->epoch;
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
     P.t_deep = K == 1 ? 128u : 0u;
     P.fresh = h0 == 0 ? 1u : 0u;
-    uint64_t run_entries = 0;
-    for (int64_t i = h0; i < h1; i++) run_entries += c->hist[(size_t)i].n_entries;
     P.ref_sl = P.calls_only && (double)run_entries < 200.0 * (double)(u1 - u0) ? 1u : 0u;
     P.err = c->kerr;
     if (fused) {
-        if (S != 1 || h0 != 0) return fail("spg: internal: fused run must be one FRESH unsplit run");
+        if (P.S != 1 || h0 != 0) return fail("spg: internal: fused run must be one FRESH unsplit run");
         P.min_td = c->p.min_total_depth;
         P.min_ad = c->p.min_allele_depth;
         P.ratio_lo = c->p.min_evidence_ratio * (1.0 - 1e-9);
@@ -650,8 +729,11 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
         P.n_list = c->nlist;
         HIPCHK(hipMemsetAsync(c->nlist, 0, sizeof(uint32_t), c->stream));
     }
-    if (S > 1) {
-        const size_t need = sizeof(MState) * (size_t)S * (size_t)P.n_groups * 64;
+    // partial states folded by k_merge_parts: a split run, or (k_acc_tile) any run into records that may
+    // already hold this sample's earlier batches
+    const bool use_part = P.S > 1 || (R.tile && !P.fresh);
+    if (use_part) {
+        const size_t need = sizeof(MState) * (size_t)P.S * (size_t)P.pstride;
         if (need > c->part_bytes) {
             if (c->part) { HIPCHK(hipStreamSynchronize(c->stream)); HIPCHK(hipFree(c->part)); }
             c->part = nullptr;
@@ -676,17 +758,31 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
         P.deep_list = c->deep_list;
         P.deep_n = c->deep_n;
     }
-    static const int64_t max_blocks = env_i64("SPG_MULTI_BLOCKS", 6144);
-    // a single shallow batch into a FRESH memory (mean column <= 40 entries: the pipelined blocks cover
-    // almost every column): k_acc_one; otherwise the run kernel
-    static const bool no_one = getenv("SPG_NO_ONE") != nullptr;
-    if (K == 1 && h0 == 0 && !no_one && (double)run_entries <= 40.0 * (double)(u1 - u0))
-        HIPCHK(launch_one(P, c->d_hist, c->ref, c->tables, c->acc, max_blocks, fused, c->stream));
-    else
-        HIPCHK(launch_multi(P, c->d_hist, c->ref, c->tables, c->acc, nt, max_blocks, fused, c->stream));
-    if (int rc = trace_sync(c, "accumulate (k_acc_multi)")) return rc;
+    // a FUSED single shallow batch into a FRESH memory (process_bam + prepare_variants; mean column <= 40
+    // entries): k_acc_lite, counts + the exact fold of the columns that may call
+    static const bool lite_on = env_i64("SPG_LITE", 1) != 0;
+    const bool lite = lite_on && fused && K == 1 && P.fresh && (double)run_entries <= 40.0 * (double)(u1 - u0);
+    if (lite) {
+        static const int64_t lb = env_i64("SPG_LITE_BLOCKS", 0);
+        P.n_groups = (int32_t)((u1 - u0 + 63) / 64);
+        HIPCHK(launch_lite(P, c->h_hist[h0], c->ref, c->tables, c->acc, lb > 0 ? lb : (int64_t)c->n_cu * lite_blocks_per_cu(),
+                           c->stream));
+    } else if (R.tile) {
+        HIPCHK(launch_tile(P, c->d_hist, c->ref, c->ref_len, c->tables, c->acc, R.lpc, tile_blocks(c, R.lpc, fused, K == 1), fused,
+                           c->stream));
+        if (use_part) HIPCHK(launch_merge(P, c->ref, c->acc, c->stream));
+    } else {
+        static const int64_t max_blocks = env_i64("SPG_MULTI_BLOCKS", 6144);
+        // a single shallow batch into a FRESH memory (mean column <= 40 entries): k_acc_one; else k_acc_multi
+        if (K == 1 && h0 == 0 && (double)run_entries <= 40.0 * (double)(u1 - u0))
+            HIPCHK(launch_one(P, c->d_hist, c->ref, c->tables, c->acc, max_blocks, fused, c->stream));
+        else
+            HIPCHK(launch_multi(P, c->d_hist, c->ref, c->tables, c->acc, nt, max_blocks, fused, c->stream));
+    }
+    if (int rc = trace_sync(c, lite ? "accumulate (k_acc_lite)" : R.tile ? "accumulate (k_acc_tile)" : "accumulate (k_acc_multi)"))
+        return rc;
     if (K == 1) {
-        // a single shallow batch: its long columns (>= 128 entries), listed by k_acc_multi, go through the
+        // a single shallow batch: its long columns (>= 128 entries), listed by the run kernel, go through the
         // wave-wide kernel
         if (int rc = launch_seg(c, h0, false, nullptr, nullptr, true)) return rc;
     }
@@ -709,15 +805,13 @@ static int materialize(spg_ctx *c) {
 // split count of a run, as flush_run computes it
 static int64_t run_splits(const spg_ctx *c, int64_t h0, int64_t h1) {
     int64_t u0 = INT64_MAX, u1 = INT64_MIN;
+    uint64_t e = 0;
     for (int64_t i = h0; i < h1; i++) {
         u0 = std::min(u0, c->hist[(size_t)i].pos_begin);
         u1 = std::max(u1, c->hist[(size_t)i].pos_begin + c->hist[(size_t)i].n_cols);
+        e += c->hist[(size_t)i].n_entries;
     }
-    const int64_t K = h1 - h0, groups = (u1 - u0 + 63) / 64;
-    static const int64_t target_items = env_i64("SPG_MULTI_ITEMS", 16384);
-    int64_t S = std::min<int64_t>(K, std::max<int64_t>(1, target_items / std::max<int64_t>(1, groups)));
-    const int64_t kper = (K + S - 1) / S;
-    return (K + kper - 1) / kper;
+    return plan_run(c, h0, h1, u0, u1, e).S;
 }
 
 static bool is_pinned(const void *p) {
@@ -794,6 +888,8 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
             HIPCHK(hipMemcpyAsync(hb.fsamp, first_sample, sizeof(uint32_t) * n_cols, k, cs));
         }
         HIPCHK(hipEventRecord(c->copy_ev, cs));
+        HIPCHK(hipEventRecord(c->in_ev[c->in_seq % spg_ctx::NIN], cs));
+        c->in_seq++;
         c->copy_pending = true;
         // pageable host buffers are the caller's again on return; pinned ones after spg_wait_input
         if (!dev && !(is_pinned(offsets) && (!n_entries || (is_pinned(base_code) && is_pinned(qual)))))
@@ -802,6 +898,11 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
     c->hist.push_back(hb);
     const int64_t idx = (int64_t)c->hist.size() - 1;
     if (int rc = grow_history_table(c)) return rc;
+    if (c->hist_fence) {       // the previous sample's last upload may still read these mirror entries
+        HIPCHK(hipEventSynchronize(c->hist_ev));
+        c->hist_fence = false;
+        c->hist_up = false;
+    }
     c->h_hist[idx] = Hist{pos_begin, n_cols, hb.off, hb.code, hb.qual};
     for (int64_t b = pos_begin >> RIDX_SHIFT; b <= (pos_begin + n_cols - 1) >> RIDX_SHIFT; b++) {
         c->buckets[(size_t)b].push_back((int32_t)idx);
@@ -892,6 +993,22 @@ int spg_history_samples(spg_ctx *c, int64_t i, int64_t *n_samples, uint32_t *fir
             memset(first_sample, 0, sizeof(uint32_t) * h.n_cols);
         }
     }
+    return 0;
+}
+
+int spg_input_ticket(spg_ctx *c, uint64_t *ticket) {
+    if (!c || !ticket) return fail("spg_input_ticket: null argument");
+    *ticket = c->in_seq;
+    return 0;
+}
+
+int spg_wait_ticket(spg_ctx *c, uint64_t ticket) {
+    if (!c) return fail("spg_wait_ticket: null ctx");
+    if (ticket == 0) return 0;
+    if (ticket > c->in_seq) return fail("spg_wait_ticket: ticket from the future");
+    HIPCHK(hipSetDevice(c->device));
+    // the ring slot of copy #ticket; if it has been re-recorded since, the wait covers a later copy too
+    HIPCHK(hipEventSynchronize(c->in_ev[(ticket - 1) % spg_ctx::NIN]));
     return 0;
 }
 
@@ -1060,8 +1177,11 @@ static int settle(spg_ctx *c, Counters &h) {
         if (h.err) return fail("spg: replay found a depth mismatch between history and accumulators");
         uint32_t kerr = 0;
         HIPCHK(hipMemcpy(&kerr, c->kerr, sizeof(kerr), hipMemcpyDeviceToHost));
-        if (kerr) return fail("spg: a shallow batch held >= 2^30 entries in 64 consecutive columns; accumulate it "
-                              "on its own as a deep batch (spg_accumulate on a context without a pending run)");
+        if (kerr) {
+            HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));   // reported once
+            return fail("spg: a shallow batch held >= 2^30 entries in 64 consecutive columns; accumulate it "
+                        "on its own as a deep batch (spg_accumulate on a context without a pending run)");
+        }
         bool again = false;
         if ((int64_t)h.n_cand > c->cand_cap) {
             HIPCHK(hipFree(c->cand));

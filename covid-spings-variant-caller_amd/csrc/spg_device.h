@@ -134,7 +134,8 @@ struct MParams {             // one k_acc_multi launch: history batches [h0, h0 
     uint32_t ref_sl;         // calls-only, shallow run: still sum ln(1-eps) for a REF-char major (at such
                              // depths a call's GL is not 0, its SCORE needs S = sum(GL), which needs the
                              // REF allele's H; skipping it would send every call to the exact replay)
-    MState *part;            // S > 1: partial records [S][n_groups * 64]
+    MState *part;            // S > 1: partial records [S][pstride]
+    int64_t pstride;         // positions per split in `part` (>= u1 - u0)
     uint32_t *err;           // bit 0: a 64-column window of a run's batch held >= 2^30 entries (not run)
     uint32_t *deep_list;     // K == 1: columns with >= t_deep entries, listed for k_acc_seg<1> ...
     uint32_t *deep_n;        // ... and their count

@@ -189,6 +189,18 @@ class PileupEngine:
         with self._lock:
             N.check(self._L.spg_wait_input(self._h), "spg_wait_input")
 
+    def input_ticket(self) -> int:
+        """Ticket of the latest host-input batch copy enqueued (spg_input_ticket)."""
+        t = C.c_uint64()
+        with self._lock:
+            N.check(self._L.spg_input_ticket(self._h, C.byref(t)), "spg_input_ticket")
+        return t.value
+
+    def wait_ticket(self, ticket: int):
+        """Block until host-input copy #ticket has landed, not the ones enqueued after it."""
+        with self._lock:
+            N.check(self._L.spg_wait_ticket(self._h, int(ticket)), "spg_wait_ticket")
+
     def _torch_stream(self):
         if getattr(self, "_ext", None) is None:
             import torch

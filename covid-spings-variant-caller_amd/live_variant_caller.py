@@ -75,28 +75,33 @@ class FastaFile:
 
 class PinnedIngest:
     """Pinned host staging for process_bam (spg_host_alloc): two buffer sets used alternately, so the
-    pileup of BAM k+1 is written while BAM k's entries are still being copied to HBM; a set is reused
-    only after the engine's input copies have landed (spg_wait_input).  Pinned pages are DMA'd without
-    a staging copy, take no page faults when reused, and let spg_accumulate return without a host
-    synchronisation."""
+    pileup of BAM k+1 is written into one set while BAM k's entries are still being copied to HBM from the
+    other.  A set is reused only after ITS copy has landed (spg_wait_ticket on the ticket taken when it was
+    enqueued); the copy of the other set, and kernels, keep running.  Pinned pages are DMA'd without a
+    staging copy, take no page faults when reused, and let spg_accumulate return without a host sync."""
 
     def __init__(self, engine):
         self.engine = engine
         self.sets = [None, None]
+        self.tickets = [0, 0]
         self.slot = 0
 
     def buffers(self, n_entries: int, n_cols: int):
         from .engine import pinned_empty
         s = self.slot
-        self.slot ^= 1
         need = int(n_entries) + 16
         cur = self.sets[s]
-        self.engine.wait_input()               # this set's previous copy (and any older) has landed
+        self.engine.wait_ticket(self.tickets[s])   # this set's previous copy has landed
         if cur is None or cur[0].nbytes < need or cur[2].size < n_cols + 1:
             cap = max(need, int(need * 1.125))
             cur = (pinned_empty(cap), pinned_empty(cap), pinned_empty(int((n_cols + 1) * 1.125) + 1, np.uint64))
             self.sets[s] = cur
         return cur
+
+    def enqueued(self):
+        """The set returned by the last buffers() call has been handed to spg_accumulate."""
+        self.tickets[self.slot] = self.engine.input_ticket()
+        self.slot ^= 1
 
 
 class LiveVariantCaller:
@@ -210,6 +215,7 @@ class LiveVariantCaller:
             E = batch.n_entries
             self._use_reference(referenceIndex)
             self.engine.accumulate(batch.pos_begin, offs[:batch.n_cols + 1], codes[:E], quals[:E], trusted=True)
+            self._ingest.enqueued()
             self._batch_contig.append(referenceIndex)
         batch.close()
 

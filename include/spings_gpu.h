@@ -171,6 +171,11 @@ int spg_host_alloc(size_t bytes, void **out);
 int spg_host_free(void *p);
 /* Block until every input copy enqueued so far has completed (the host buffers are free again). */
 int spg_wait_input(spg_ctx *ctx);
+/* Per-batch input tracking for double-buffered staging: spg_input_ticket returns the number of host-input
+ * batch copies enqueued so far (the ticket of the latest one); spg_wait_ticket(t) blocks until copy #t has
+ * landed (not the copies enqueued after it), so staging set A can be refilled while set B's copy runs. */
+int spg_input_ticket(spg_ctx *ctx, uint64_t *ticket);
+int spg_wait_ticket(spg_ctx *ctx, uint64_t ticket);
 
 /* prepare_variants (:120-231) + genotype_likelihood / to_phred_scale (utils.py:12-24):
  * per-position table and the candidate list, on device.  Returns after enqueue. */
