@@ -52,8 +52,9 @@ def parse():
     ap.add_argument("--no-parity", action="store_true", help="skip the max_depth 8000 nested line")
     ap.add_argument("--many-batches", type=int, default=10000, help="config 4 samples (0 = skip)")
     ap.add_argument("--many-depth", type=float, default=100.0)
-    ap.add_argument("--runs-batches", type=int, default=2000,
-                    help="config 4 as per-BAM batches folded in runs (k_acc_multi); 0 = skip")
+    ap.add_argument("--runs-batches", type=int, default=10000,
+                    help="config 4 as per-BAM CSR batches (the live form) folded in runs (k_acc_tile); 0 = skip")
+    ap.add_argument("--no-chr1", action="store_true", help="skip the nested chr1 30x line (BASELINE config 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-positions", type=int, default=6000)
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end BAM -> calls leg")
@@ -122,6 +123,21 @@ def measure(D, step, eng, K_min, reps, min_ms, every):
     eng.sync()
     est = D.max((time.perf_counter() - t0) / 3)
     K = max(K_min, int(math.ceil(min_ms * 1e-3 / max(est, 1e-7))))
+    # re-estimate K from timed batches of K steps (the 3 steps above carry first-call overheads), so that
+    # every measurement lasts >= min_ms
+    for _ in range(3):
+        torch.cuda.synchronize()
+        D.barrier()
+        t0 = time.perf_counter()
+        for k in range(K):
+            step(k)
+        flush()
+        eng.sync()
+        torch.cuda.synchronize()
+        t = D.max(time.perf_counter() - t0)
+        if t >= min_ms * 1e-3:
+            break
+        K = max(K + 1, int(math.ceil(K * min_ms * 1.1e-3 / max(t, 1e-9))))
     eng.kernel_times(4096)
     times, acc, enq = [], [], []
     for _ in range(reps):
@@ -184,14 +200,16 @@ def build_shard(rank, world, L, depth, max_depth, device):
     return ref, "".join(refs), off, d_off, d_c, d_q, int(base)
 
 
-def kernel_name(E, C):
-    """The accumulate instantiation the engine picks for this batch (csrc/spg_api.cpp add_batch)."""
-    if E <= 40 * C:      # one shallow batch into a fresh memory (spg_api.cpp flush_run)
-        return "k_acc_one (+ k_acc_seg<1> for columns >= 128 entries)"
+def kernel_name(E, C, calls_only=True):
+    """The accumulate kernel the engine picks for one batch of E entries over C columns
+    (csrc/spg_api.cpp add_batch / flush_run) and its PMC summary key."""
+    if E <= 40 * C and calls_only:   # one shallow batch into a fresh memory, fused with the calls-only finalize
+        return "k_acc_lite (+ k_acc_seg<1> for columns >= 128 entries)", "spg::k_acc_lite"
     if E < 256 * C:
-        return "k_acc_multi (+ k_acc_seg<1> for columns >= 128 entries)"
+        return "k_acc_tile (+ k_acc_seg<1> for columns >= 128 entries)", "spg::k_acc_tile"
     nt = 2 * E > (192 << 20)
-    return f"k_acc_seg<4,true,4,{'true' if nt else 'false'}> (spg_accumulate{'; non-temporal loads' if nt else ''})"
+    return (f"k_acc_seg<4,true,4,{'true' if nt else 'false'}> (spg_accumulate{'; non-temporal loads' if nt else ''})",
+            "spg::k_acc_seg<4, true")
 
 
 def pmc_traffic(key, E):
@@ -302,7 +320,9 @@ def run_point(args, D, L, depth, max_depth, local, world, rank, contig):
                 assert np.array_equal(a[:8 + n * rec], b[:8 + n * rec]), f"rank {r}: gathered bytes differ"
     med = float(np.median(times))
     t_acc = float(np.mean(acc)) * 1e-3 if len(acc) else float("nan")
-    algo_bytes = 2 * E + 8 * (C + 1)          # base_code + qual + u64 offsets read by the accumulate kernel
+    # bytes the accumulate + finalize must move: base_code + qual + u64 offsets + REF chars read, the
+    # calls-only candidate records (56 B) written
+    algo_bytes = 2 * E + 8 * (C + 1) + C + 56 * n_cand
     eng.close()
     return {
         "value": world * L * K / med, "ms_per_step": med / K * 1e3, "steps": K, "E": E, "C": C,
@@ -312,6 +332,23 @@ def run_point(args, D, L, depth, max_depth, local, world, rank, contig):
         "finalize_ms": fin, "n_cand": n_cand, "n_replay": n_replay, "gathered": gathered,
         "host_enqueue_ms_per_step": measure.host_enqueue_ms_per_step,
     }
+
+
+def nested_point(args, D, workload, local, world, rank):
+    """Another BASELINE config as a nested line (never `value`): same step and timing as the main point."""
+    L, depth, contig = WORKLOADS[workload]
+    p = run_point(args, D, L, depth, 0, local, world, rank, contig)
+    name, key = kernel_name(p["E"], p["C"], not args.full_table)
+    return {"workload": f"{workload}: {contig} L={L}, {depth:.0f}x, 150-bp reads, uncapped, 1 sample per GPU per "
+                        f"step (coordinate-sharded x{world})",
+            "value": p["value"], "unit": "positions/s", "ms_per_step": p["ms_per_step"], "steps": p["steps"],
+            "measurement_ms": p["measurements_ms"], "entries_per_gpu_step": p["E"], "columns_per_gpu": p["C"],
+            "datagen_s": p["t_gen"], "finalize_ms": p["finalize_ms"], "candidates_per_gpu_step": p["n_cand"],
+            "roofline": {"bound": "hbm", "achieved": p["achieved"] / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                         "frac": p["achieved"] / PEAK_HBM, "algorithmic_bytes": p["algo_bytes"],
+                         "frac_incl_finalize": p["algo_bytes"] / ((p["kernel_ms"] + p["finalize_ms"]) * 1e-3) / PEAK_HBM,
+                         "traffic": pmc_traffic(key, p["E"]), "kernel": name, "kernel_ms": p["kernel_ms"],
+                         "kernel_ms_median": p["kernel_ms_median"], "kernel_samples": p["kernel_samples"]}}
 
 
 def run_config4(args, D, local, world, rank):
@@ -353,10 +390,12 @@ def run_config4(args, D, local, world, rank):
     fin = finalize_ms(step, eng)
     med = float(np.median(times))
     t_acc = float(np.mean(acc)) * 1e-3 if len(acc) else float("nan")
-    # SURVEY §8(d) canonical bytes: 2E + 4 x CSR columns read + 68 x positions output (the BAMs'
-    # per-BAM columns B x C count as read, although the batched layout reads only C + 1 offsets)
+    # bytes the kernel must move for this layout: base_code + qual + u64 offsets + u32 first-sample per column
+    # read, 56-B candidate records written.  (SURVEY §8(d)'s canonical 2E + 4BC + 68C also credits per-BAM
+    # offsets this layout never reads and a full table calls-only mode never writes: reported, not used.)
+    read = 2 * E + 8 * (C + 1) + 4 * C + C
+    moved = read + 56 * n_cand
     canon = 2 * E + 4 * B * C + 68 * C
-    read = 2 * E + 8 * (C + 1) + 4 * C
     eng.close()
     del d
     torch.cuda.empty_cache()
@@ -367,12 +406,11 @@ def run_config4(args, D, local, world, rank):
         "value": B * L * K / med, "unit": "positions/s (BAMs x L per step)",
         "ms_per_step": med / K * 1e3, "steps": K, "measurements": len(times),
         "entries_per_gpu_step": E, "columns_per_gpu": C, "datagen_s": t_gen,
-        "kernel": kernel_name(E, C), "accumulate_ms": t_acc * 1e3, "accumulate_samples": int(len(acc)),
+        "kernel": kernel_name(E, C)[0], "accumulate_ms": t_acc * 1e3, "accumulate_samples": int(len(acc)),
         "finalize_ms": fin,
-        "roofline": {"bound": "hbm", "achieved": canon / t_acc / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                     "frac": canon / t_acc / PEAK_HBM, "algorithmic_bytes": canon, "read_bytes_per_step": read,
-                     "frac_of_bytes_read": read / t_acc / PEAK_HBM,
-                     "traffic": pmc_traffic("spg::k_acc_seg<4, true", E)},
+        "roofline": {"bound": "hbm", "achieved": moved / t_acc / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                     "frac": moved / t_acc / PEAK_HBM, "algorithmic_bytes": moved,
+                     "survey_canonical_bytes": canon, "traffic": pmc_traffic(kernel_name(E, C)[1], E)},
         "candidates_per_gpu_step": n_cand, "replayed_positions_per_gpu_step": n_replay,
     }
     if args.runs_batches > 0:
@@ -405,15 +443,20 @@ def run_config4_runs(args, D, local, world, rank, ref, lo, hi):
     K, times, acc = measure(D, step, eng, 1, max(5, args.reps // 4), args.min_ms, 1)
     med = float(np.median(times))
     t_acc = float(np.mean(acc)) * 1e-3 if len(acc) else float("nan")
-    canon = 2 * E + 4 * B * C + 68 * C
+    # bytes the run must move: each BAM's base_code + qual + u64 offsets, the REF chars, the candidate records
+    moved = 2 * E + 8 * B * (C + 1) + C + 56 * n_cand
+    kname = "k_acc_tile (+ k_merge_parts when split)"
     eng.close()
     del data
     torch.cuda.empty_cache()
-    return {"bams": B, "value": B * L * K / med, "ms_per_step": med / K * 1e3, "measurements": len(times),
-            "entries_per_gpu_step": E, "datagen_s": t_gen, "kernel": "k_acc_multi + k_merge_parts",
-            "accumulate_ms": t_acc * 1e3, "candidates_per_gpu_step": n_cand,
-            "roofline": {"achieved": canon / t_acc / 1e9, "frac": canon / t_acc / PEAK_HBM,
-                         "algorithmic_bytes": canon, "traffic": pmc_traffic("spg::k_acc_multi", E)}}
+    return {"bams": B, "value": B * L * K / med, "unit": "positions/s (BAMs x L per step)",
+            "ms_per_step": med / K * 1e3, "steps": K, "measurements": len(times),
+            "measurement_ms": [round(t * 1e3, 3) for t in times],
+            "entries_per_gpu_step": E, "datagen_s": t_gen, "kernel": kname,
+            "accumulate_ms": t_acc * 1e3, "accumulate_samples": int(len(acc)), "candidates_per_gpu_step": n_cand,
+            "roofline": {"bound": "hbm", "achieved": moved / t_acc / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                         "frac": moved / t_acc / PEAK_HBM, "algorithmic_bytes": moved,
+                         "traffic": pmc_traffic("spg::k_acc_tile", E)}}
 
 
 def cpu_model():
@@ -448,8 +491,11 @@ def cpu_baseline(args):
     _, off2, c2, q2 = synth.pileup(len(ref), depth, seed=2, ref=ref, hi=n_c, max_depth=args.max_depth)
     res = {}
     cores = len(os.sched_getaffinity(0))
-    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or cores
-    for tag, threads in (("c_restatement", 1), ("c_restatement_all_cores", min(cores, omp))):
+    # the multi-threaded leg runs on this process's CPU share: OMP_NUM_THREADS (16 per GPU on the pool's boxes,
+    # whose affinity mask lists the whole machine) or, unset, every CPU in the affinity mask
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    share = min(cores, omp) if omp else cores
+    for tag, threads in (("c_restatement", 1), (f"c_restatement_{share}_threads", share)):
         COracle.set_threads(threads)
         t0 = time.perf_counter()
         co = COracle(ref, 30, 10, 5, 0.10)
@@ -465,7 +511,7 @@ def cpu_baseline(args):
             "sample": f"oracle/reference_port.py (Python/numpy restatement of live_variant_caller.py:74-185) "
                       f"on {n} positions x {depth:.0f}x ({int(off[-1])} entries), {t_py:.2f} s, 1 core; "
                       f"pysam pileup/BAM decode not included (absent)",
-            **res, "cores_available": cores, "cpu_model": cpu_model()}
+            **res, "cores_in_affinity_mask": cores, "omp_num_threads": omp or None, "cpu_model": cpu_model()}
 
 
 def end_to_end(args, device):
@@ -590,8 +636,9 @@ def main():
                    "steps_requested": args.steps, "measurement_ms": main_pt["measurements_ms"],
                    "statistic": "median measurement; max over ranks"},
         "roofline": {"bound": "hbm", "achieved": main_pt["achieved"] / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                     "frac": main_pt["achieved"] / PEAK_HBM, "traffic": pmc_traffic("spg::k_acc_seg<4, true", E),
-                     "kernel": kernel_name(E, C), "kernel_ms": main_pt["kernel_ms"],
+                     "frac": main_pt["achieved"] / PEAK_HBM,
+                     "traffic": pmc_traffic(kernel_name(E, C, not args.full_table)[1], E),
+                     "kernel": kernel_name(E, C, not args.full_table)[0], "kernel_ms": main_pt["kernel_ms"],
                      "kernel_ms_median": main_pt["kernel_ms_median"], "kernel_samples": main_pt["kernel_samples"],
                      "algorithmic_bytes": main_pt["algo_bytes"]},
         "finalize_ms": main_pt["finalize_ms"], "host_enqueue_ms_per_step": main_pt["host_enqueue_ms_per_step"],
@@ -604,9 +651,11 @@ def main():
         res["parity_mode"] = {"max_depth": 8000, "value": p["value"], "ms_per_step": p["ms_per_step"],
                               "steps": p["steps"], "entries_per_gpu_step": p["E"], "kernel_ms": p["kernel_ms"],
                               "roofline_frac": p["achieved"] / PEAK_HBM, "finalize_ms": p["finalize_ms"],
-                              "candidates_per_gpu_step": p["n_cand"], "kernel": kernel_name(p["E"], p["C"])}
+                              "candidates_per_gpu_step": p["n_cand"], "kernel": kernel_name(p["E"], p["C"])[0]}
     if args.many_batches > 0 and args.workload == "sars10k":
         res["config4"] = run_config4(args, D, local, world, rank)
+    if not args.no_chr1 and args.workload == "sars10k":
+        res["chr1_30x"] = nested_point(args, D, "chr1_30x", local, world, rank)
     if rank == 0 and world == 1 and not args.no_e2e and L == L_SARS:
         res["end_to_end"] = end_to_end(args, 0)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -760,7 +760,7 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
     }
     // a FUSED single shallow batch into a FRESH memory (process_bam + prepare_variants; mean column <= 40
     // entries): k_acc_lite, counts + the exact fold of the columns that may call
-    static const bool lite_on = env_i64("SPG_LITE", 1) != 0;
+    static const bool lite_on = [] { const char *e = getenv("SPG_LITE"); return !(e && atoi(e) == 0); }();
     const bool lite = lite_on && fused && K == 1 && P.fresh && (double)run_entries <= 40.0 * (double)(u1 - u0);
     if (lite) {
         static const int64_t lb = env_i64("SPG_LITE_BLOCKS", 0);

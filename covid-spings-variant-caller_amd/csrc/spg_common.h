@@ -278,6 +278,15 @@ __device__ __forceinline__ void lut_sl(uint32_t qw, uint32_t sel80, const double
     sl += (l1m[idx & 0xFFu] + l1m[(idx >> 8) & 0xFFu]) + (l1m[(idx >> 16) & 0xFFu] + l1m[idx >> 24]);
 }
 
+// wave-wide max of a per-lane count (DPP within rows, then the four row maxima)
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) v = max(v, dpp_u32(v, c));
+    const uint32_t a = max((uint32_t)__builtin_amdgcn_readlane(v, 0), (uint32_t)__builtin_amdgcn_readlane(v, 16));
+    const uint32_t b = max((uint32_t)__builtin_amdgcn_readlane(v, 32), (uint32_t)__builtin_amdgcn_readlane(v, 48));
+    return max(a, b);
+}
+
 // MBLK: 16-B blocks per lane per load round (MBLK x 16 entries)
 // prepare_variants' filters on a position's totals (:131, :151-157), a superset of the early exit
 // k_finalize takes in calls-only mode: false = the position can produce no call and needs no replay

@@ -11,27 +11,40 @@
 // written and listed for the sparse finalize.  Records of the other positions are never written (the
 // context re-materializes them if anything reads them later, spg_api.cpp materialize()).
 //
-// Memory: each lane loads its column's bytes directly, four 16-B loads from its dword-aligned first entry
-// (covers columns of <= 61 entries; longer ones finish with further loads), and the loads of the next tile
-// are in flight while a tile is counted: the tile loop is unrolled twice over two register sets, so no
-// register copy of a pending load forces a wait (hipcc waits for a load before copying its destination).
-// Each tile's CSR bounds and REF chars are loaded two tiles ahead.
+// Memory: a tile's bytes [off[c0], off[c0 + 64]) are contiguous in base_code / qual; the wave loads them coalesced
+// (16 B per lane, three 1 KiB chunks per array from the 16-B aligned start) into registers one tile ahead, stores
+// them into its LDS slot when the tile comes up, and each lane reads its column's aligned blocks from there
+// (bytes past the 3 KiB slot — a tile with a column >= 128 entries, or a rare 100x+ stretch — from global
+// memory).  The tile loop is unrolled twice over two register sets, so no register copy of a pending load
+// forces a wait (hipcc waits for a load before copying its destination).  CSR bounds and REF chars are loaded
+// two tiles ahead.
 #include "spg_common.h"
 
 namespace spg {
 
 constexpr int LW = 4;      // waves per workgroup
-constexpr int LB = 4;      // 16-B blocks per lane per tile, prefetched
+constexpr int LCH = 3;     // 1 KiB chunks per array staged per tile
+constexpr int LSLOT = 1024 * LCH;   // bytes per array in a wave's LDS slot
+constexpr int LNBLK = LSLOT / 16;
 
-struct LHead {             // loaded unconditionally (a load under a branch makes hipcc wait for every load
-    uint64_t ob, oe;       // before the next use of any); `ok` selects at the first use
-    uint32_t rc;           // REF char
-    bool ok;               // column in range
+// One tile in flight, loaded unconditionally (a load under a branch makes hipcc wait for every load before the
+// next use of any): its staged chunks (lane l: bytes 1024 k + 16 l from the tile's 16-B aligned start, per
+// array) and the lane's column bounds and REF char.  Two of them alternate (no register copies: hipcc waits
+// for a pending load before copying its destination).
+struct LData {
+    u32x4 c[LCH], q[LCH];
+    uint64_t ob;
+    uint32_t oe;           // low half of the column's end (columns hold < 2^32 entries)
+    uint32_t rc;
+};
+struct LBounds {           // a tile's byte range [off[c0], off[c0 + 64]) (wave-uniform)
+    uint64_t b, e;
 };
 
 __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_acc_lite(
     MParams P, Hist hb, const uint8_t *__restrict__ ref, const Tables *__restrict__ T, Acc *__restrict__ acc) {
     __shared__ double2 lut[256];                       // {ln(1-eps), eps} per q (the exact fold only)
+    __shared__ __attribute__((aligned(16))) uint8_t slots[LW][2][LSLOT];   // per wave: a tile's code, qual
     for (uint32_t q = threadIdx.x; q < 256u; q += 64u * LW) lut[q] = make_double2(T->fast[q][0], T->fast[q][1]);
     __syncthreads();
     const int lane = threadIdx.x & 63;
@@ -39,40 +52,61 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
     const int64_t stride = (int64_t)gridDim.x * LW;
     int64_t tile = (int64_t)__builtin_amdgcn_readfirstlane(blockIdx.x * LW + (threadIdx.x >> 6));   // wave-uniform
 
-    auto head = [&](int64_t t) -> LHead {
-        const int64_t p = P.u0 + t * 64 + lane;
-        const int64_t col = p - hb.pos_begin;
-        const bool ok = t < n_tiles && p < P.u1 && col >= 0 && col < hb.n_cols;
-        const int64_t cc = min(max(col, (int64_t)0), hb.n_cols - 1);
-        const int64_t pc = min(max(p, P.u0), P.u1 - 1);
-        return LHead{__builtin_nontemporal_load(hb.off + cc), __builtin_nontemporal_load(hb.off + cc + 1), (uint32_t)ref[pc], ok};
+    auto bounds = [&](int64_t t) -> LBounds {
+        const int64_t c0 = min(max(P.u0 + t * 64 - hb.pos_begin, (int64_t)0), hb.n_cols);
+        const int64_t c1 = min(c0 + 64, hb.n_cols);
+        return LBounds{hb.off[c0], hb.off[c1]};
     };
-    // a tile's blocks: LB 16-B loads per array from the column's dword-aligned first entry.  Blocks past the
-    // column (and every block of an empty or out-of-range column) reload the first one (in the batch arrays:
-    // they carry 16 bytes of padding), and valid_masks drops them
-    auto issue = [&](const LHead &h, u32x4 (&c)[LB], u32x4 (&q)[LB]) {
-        const uint64_t ob = h.ok ? h.ob : 0, oe = h.ok ? h.oe : 0;
-        const uint64_t a0 = ob & ~(uint64_t)3;
+    auto in_range = [&](int64_t t) {
+        const int64_t p = P.u0 + t * 64 + lane, col = p - hb.pos_begin;
+        return t < n_tiles && p < P.u1 && col >= 0 && col < hb.n_cols;
+    };
+    // LCH coalesced 16-B loads per lane and array; lanes past the tile's bytes (and a tile past the end) reload
+    // the first chunk's line (in the batch arrays: they carry 16 bytes of padding)
+    auto issue = [&](int64_t t, const LBounds &B, LData &D) {
+        const uint64_t base = B.b & ~(uint64_t)15;
+        const uint64_t span = t < n_tiles ? B.e - base : 0;
 #pragma unroll
-        for (int u = 0; u < LB; u++) {
-            const uint64_t a = a0 + 16u * u < oe ? a0 + 16u * u : a0;
-            c[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(hb.code + a));
-            q[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(hb.qual + a));
+        for (int k = 0; k < LCH; k++) {
+            const uint32_t o = 1024u * k + 16u * lane;
+            const uint64_t a = o < span ? base + o : base;
+            D.c[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(hb.code + a));
+            D.q[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(hb.qual + a));
         }
+        const int64_t p = P.u0 + t * 64 + lane;
+        const int64_t cc = min(max(p - hb.pos_begin, (int64_t)0), hb.n_cols - 1);
+        D.ob = hb.off[cc];
+        D.oe = reinterpret_cast<const uint32_t *>(hb.off + cc + 1)[0];
+        D.rc = ref[min(max(p, P.u0), P.u1 - 1)];
     };
 
     // one tile: counts of its columns, then the exact fold of the columns that may call
-    auto process = [&](int64_t t, const LHead &h, const u32x4 (&c)[LB], const u32x4 (&q)[LB]) {
+    uint8_t *const sc = slots[threadIdx.x >> 6][0];
+    uint8_t *const sq = slots[threadIdx.x >> 6][1];
+    auto process = [&](int64_t t, const LData &D) {
+        // stage the tile (this wave's slot; LDS operations of a wave complete in order)
+#pragma unroll
+        for (int k = 0; k < LCH; k++) {
+            *reinterpret_cast<u32x4 *>(sc + 1024 * k + 16 * lane) = D.c[k];
+            *reinterpret_cast<u32x4 *>(sq + 1024 * k + 16 * lane) = D.q[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        // the tile's 16-B aligned start (lane 0's column is always in range)
+        // (readfirstlane returns int: through uint32_t, or the low half's bit 31 would sign-extend)
+        const uint32_t b_hi = __builtin_amdgcn_readfirstlane((uint32_t)(D.ob >> 32));
+        const uint32_t b_lo = __builtin_amdgcn_readfirstlane((uint32_t)D.ob);
+        const uint64_t base = (((uint64_t)b_hi << 32) | b_lo) & ~(uint64_t)15;
         const int64_t p = P.u0 + t * 64 + lane;
-        const bool inr = h.ok;
-        const uint64_t hob = inr ? h.ob : 0, hoe = inr ? h.oe : 0;
-        const uint8_t refc = (uint8_t)h.rc;
+        const bool inr = in_range(t);
+        const uint64_t hob = inr ? D.ob : 0;
+        const uint8_t refc = (uint8_t)D.rc;
         const uint32_t lx = ((uint32_t)refc & 0xDFu) - 65u;
         const uint32_t lc = lx < 16u ? (uint32_t)(0x00F0000004000201ull >> (4u * lx)) & 0xFu
                                      : (lx < 26u ? (0x8000u >> (4u * (lx - 16u))) & 0xFu : 0u);
         const uint32_t M = lc ? lc : 1u, mrep = M * 0x01010101u;   // code_of_ref, branch-free
         const int Ms = M == 15u ? 4 : (int)__builtin_ctz(M);
-        uint32_t len = (uint32_t)(hoe - hob);
+        uint32_t len = inr ? D.oe - (uint32_t)D.ob : 0u;
         bool deep = false;
         if (inr && P.t_deep && len >= P.t_deep) { deep = true; len = 0; }   // k_acc_seg<1> takes it
         const uint64_t dm = __ballot(deep);
@@ -84,11 +118,11 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
                 P.deep_list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u))] =
                     (uint32_t)(p - hb.pos_begin);
         }
-        const int32_t lead = (int32_t)(hob & 3u);
+        const uint32_t brel = inr ? (uint32_t)(hob - base) : 0u;      // the column's first byte in the tile
         uint32_t mcf = 0, drare = 0, n_other = 0, cnt[NSLOT] = {0, 0, 0, 0, 0};
-        auto count = [&](const u32x4 &cw, const u32x4 &qw, int32_t x0) {
+        auto count = [&](const u32x4 &cw, const u32x4 &qw, int32_t x0, int32_t vlen) {
             uint32_t vm[4];
-            valid_masks<4>(x0, 0, (int32_t)len, vm);
+            valid_masks<4>(x0, 0, vlen, vm);
 #pragma unroll
             for (int d = 0; d < 4; d++) {
                 const uint32_t c_ = dw<4>(cw, d), q_ = dw<4>(qw, d);
@@ -108,21 +142,29 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
                 }
             }
         };
-#pragma unroll
-        for (int u = 0; u < LB; u++) count(c[u], q[u], 16 * u - lead);
-        // columns longer than the prefetched window (rare at 30x: > 61 entries)
-        const uint32_t nblk = len ? (uint32_t)(((uint32_t)lead + len + 15u) >> 4) : 0u;
-        if (__ballot(nblk > LB)) {
-            const uint64_t a0 = hob & ~(uint64_t)3;
-            for (uint32_t u = LB;; u++) {
-                const bool more = u < nblk;
+        // the column's aligned blocks j0 .. j1 - 1 of the tile: from the slot, then (past it) from memory
+        const uint32_t j0 = brel >> 4, j1 = len ? (brel + len + 15u) >> 4 : j0;
+        const uint32_t jl = min(j1, (uint32_t)LNBLK);
+        const uint32_t nl = jl > j0 ? jl - j0 : 0u;
+        const uint32_t mx = wave_max_u32(nl);
+        const int32_t vlen = (int32_t)min(len, (uint32_t)LSLOT - min(brel, (uint32_t)LSLOT));   // entries in the slot
+        for (uint32_t u = 0; u < mx; u++) {
+            const uint32_t j = min(j0 + u, (uint32_t)LNBLK - 1u);
+            const u32x4 cw = *reinterpret_cast<const u32x4 *>(sc + 16u * j);
+            const u32x4 qw = *reinterpret_cast<const u32x4 *>(sq + 16u * j);
+            count(cw, qw, (int32_t)(16u * (j0 + u)) - (int32_t)brel, vlen);
+        }
+        if (__ballot(j1 > (uint32_t)LNBLK)) {
+            const uint32_t f0 = max(j0, (uint32_t)LNBLK);
+            for (uint32_t j = f0;; j++) {
+                const bool more = j < j1;
                 if (!__ballot(more)) break;
                 u32x4 cw{0, 0, 0, 0}, qw{0, 0, 0, 0};
                 if (more) {
-                    cw = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(hb.code + a0) + u);
-                    qw = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(hb.qual + a0) + u);
+                    cw = *(reinterpret_cast<const u32x4 *>(hb.code + base) + j);
+                    qw = *(reinterpret_cast<const u32x4 *>(hb.qual + base) + j);
                 }
-                count(cw, qw, (int32_t)(16u * u) - lead);
+                count(cw, qw, (int32_t)(16u * j) - (int32_t)brel, (int32_t)len);
             }
         }
         // prepare_variants' filters on the counts (:131, :151-157); an exotic allele goes to the exact replay
@@ -155,8 +197,9 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
         double fsl[NSLOT], fse[NSLOT];
 #pragma unroll
         for (int k = 0; k < NSLOT; k++) { fc[k] = fsq[k] = 0; ffirst[k] = INF32; fqf[k] = 255; fsl[k] = fse[k] = 0.0; }
-        const uint64_t a0 = hob & ~(uint64_t)3;
-        const uint32_t nb = fold ? nblk : 0u;
+        const uint64_t a0 = hob & ~(uint64_t)3;       // (dword-aligned column window, L2-resident)
+        const int32_t lead = (int32_t)(hob & 3u);
+        const uint32_t nb = fold && len ? (uint32_t)(((uint32_t)lead + len + 15u) >> 4) : 0u;
         for (uint32_t u = 0;; u++) {
             const bool more = u < nb;
             if (!__ballot(more)) break;
@@ -221,24 +264,22 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
         }
     };
 
-    // the pipeline: tile t's blocks are in set A or B (issued one tile ahead), heads two tiles ahead
-    LHead h0 = head(tile), h1 = head(tile + stride);
-    u32x4 cA[LB], qA[LB], cB[LB], qB[LB];
-    issue(h0, cA, qA);
+    // the pipeline: tile t's chunks and heads in set A or B (issued one tile ahead), its byte range two ahead
+    LBounds B0 = bounds(tile), B1 = bounds(tile + stride);
+    LData A, B;
+    issue(tile, B0, A);
+    // (each half loads the range before its chunks: loads complete in order, so the next half's wait for the
+    // range leaves the chunks in flight)
     while (tile < n_tiles) {
-        LHead h2 = head(tile + 2 * stride);
-        issue(h1, cB, qB);
-        process(tile, h0, cA, qA);
+        B0 = bounds(tile + 2 * stride);
+        issue(tile + stride, B1, B);
+        process(tile, A);
         tile += stride;
-        h0 = h1;
-        h1 = h2;
         if (tile >= n_tiles) break;
-        h2 = head(tile + 2 * stride);
-        issue(h1, cA, qA);
-        process(tile, h0, cB, qB);
+        B1 = bounds(tile + 2 * stride);
+        issue(tile + stride, B0, A);
+        process(tile, B);
         tile += stride;
-        h0 = h1;
-        h1 = h2;
     }
 }
 

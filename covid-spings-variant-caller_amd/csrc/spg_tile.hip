@@ -75,14 +75,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_u(const void *p, uint32_t
 }
 
 // wave-wide max (DPP within rows of 16, then the four row results): uniform result
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int c = 0; c < 4; c++) v = max(v, dpp_u32(v, c));
-    const uint32_t a = max((uint32_t)__builtin_amdgcn_readlane(v, 0), (uint32_t)__builtin_amdgcn_readlane(v, 16));
-    const uint32_t b = max((uint32_t)__builtin_amdgcn_readlane(v, 32), (uint32_t)__builtin_amdgcn_readlane(v, 48));
-    return max(a, b);
-}
-
 template <int LPC>
 __device__ __forceinline__ uint32_t grp_add(uint32_t v) {
 #pragma unroll

@@ -25,6 +25,7 @@ from __future__ import annotations
 import logging
 import os
 import threading
+from collections.abc import Mapping
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -104,6 +105,36 @@ class PinnedIngest:
         self.slot ^= 1
 
 
+class MemoryView(Mapping):
+    """``memory`` (live_variant_caller.py:32, dict[int, Site]) over the arrays LiveVariantCaller.memory
+    builds: iteration in insertion order (first visit), a Site built per lookup."""
+
+    def __init__(self, order, depth, first_batch, refs, groups):
+        self._order = order
+        self._sorted = np.sort(order)
+        self._depth, self._fb, self._refs = depth, first_batch, refs
+        self._gpos, self._gcode, self._gs, self._ge, self._q = groups
+
+    def __len__(self):
+        return len(self._order)
+
+    def __iter__(self):
+        return iter(self._order.tolist())
+
+    def __contains__(self, p):
+        i = np.searchsorted(self._sorted, p)
+        return bool(i < len(self._sorted) and self._sorted[i] == p)
+
+    def __getitem__(self, p) -> Site:
+        if not isinstance(p, (int, np.integer)) or p not in self:
+            raise KeyError(p)
+        p = int(p)
+        lo, hi = np.searchsorted(self._gpos, p, "left"), np.searchsorted(self._gpos, p, "right")
+        snvs = {N.NIBBLE[int(self._gcode[g])]: self._q[self._gs[g]:self._ge[g]].tolist() for g in range(lo, hi)}
+        return {"reference": self._refs[int(self._fb[p]) - 1][p], "totalDepth": int(self._depth[p]),
+                "snvs": snvs, "indels": {}}
+
+
 class LiveVariantCaller:
     def __init__(self, referenceFasta: str, minBaseQuality: int, minMappingQuality: int, minTotalDepth: int,
                  minAlleleDepth: int, minEvidenceRatio: float, maxVariants: int, device: Optional[int] = None,
@@ -151,10 +182,11 @@ class LiveVariantCaller:
             self._current_ref = index
 
     @property
-    def memory(self) -> Dict[int, Site]:
-        """Read-only view of the reference's ``memory`` (dict[int, Site], insertion order):
-        reference char and totalDepth from the device table, per-allele quality lists (bq-filtered,
-        BAM order) regrouped from the batch history."""
+    def memory(self) -> Mapping[int, Site]:
+        """Read-only view of the reference's ``memory`` (dict[int, Site], insertion order), as a lazy
+        mapping: reference char and totalDepth from the device table, per-allele quality lists
+        (bq-filtered, BAM order) regrouped from the batch history with array sorts; a position's Site
+        is built when it is read (chr1 memories hold ~2.5e8 positions)."""
         with self._lock:
             self.engine.finalize()
             t = self.engine.table()
@@ -162,11 +194,7 @@ class LiveVariantCaller:
             minbq = self.minBaseQuality
             present = np.nonzero(t["flags"] & N.SPG_F_PRESENT)[0]
             order = present[np.lexsort((present, t["first_batch"][present]))]
-            mem: Dict[int, Site] = {}
             refs = [self.fastaFile.fetch(self.fastaFile.references[i]) for i in self._batch_contig]
-            for p in order.tolist():
-                b = int(t["first_batch"][p]) - 1
-                mem[p] = {"reference": refs[b][p], "totalDepth": int(t["depth"][p]), "snvs": {}, "indels": {}}
             # every accumulated entry in accumulate order, then grouped per (position, allele) with a
             # stable sort: each group is that allele's q list in BAM order (:103), groups of a position
             # in order of their first entry (snvs dict order, :100-101)
@@ -176,6 +204,8 @@ class LiveVariantCaller:
                 pos = np.repeat(np.arange(pb, pb + len(lens), dtype=np.int64), lens)
                 keep = (quals >= minbq) & (codes < 16)
                 pos_l.append(pos[keep]); code_l.append(codes[keep]); q_l.append(quals[keep])
+            e = np.zeros(0, np.int64)
+            groups = (e, e, e, e, np.zeros(0, np.uint8))
             if pos_l:
                 pos = np.concatenate(pos_l)
                 code = np.concatenate(code_l).astype(np.int64)
@@ -187,10 +217,9 @@ class LiveVariantCaller:
                 ends = np.r_[starts[1:], len(key_s)]
                 first = srt[starts]                       # encounter index of each group's first entry
                 gpos, gcode = key_s[starts] // 16, key_s[starts] % 16
-                q_sorted = qs[srt]
-                for gi in np.lexsort((first, gpos)).tolist():
-                    mem[int(gpos[gi])]["snvs"][N.NIBBLE[int(gcode[gi])]] = q_sorted[starts[gi]:ends[gi]].tolist()
-            return mem
+                go = np.lexsort((first, gpos))            # by position, then dict order
+                groups = (gpos[go], gcode[go], starts[go], ends[go], qs[srt])
+            return MemoryView(order, t["depth"], t["first_batch"], refs, groups)
 
     # -- hot path -----------------------------------------------------------------------------
     def process_bam(self, inputBam: str, referenceIndex=0):

@@ -176,3 +176,37 @@ def test_lite_single_batch_shapes(calls_only):
     assert sum(1 for x in v if 10_000 <= x["start"] < 12_000) > 50
     assert sum(1 for x in v if 20_000 <= x["start"] < 20_500) > 10
     eng.close()
+
+
+def test_lite_offsets_past_2_32():
+    """k_acc_lite with every CSR offset above 2^32 (the device batch arrays open with 2^32 bytes no column
+    references; offsets index them as given): the tile bases, the slot-overflow reads of a 120x stretch and the
+    exact fold all address past 4 GiB.  Calls vs the oracle on the same columns."""
+    import torch
+    from covid_spings_variant_caller_amd import synth
+    dev = torch.device("cuda", 0)
+    L = 60_000
+    ref = synth.reference(L, seed=121)
+    b = synth.pileup(L, 30, seed=122, ref=ref, snv_every=89)
+    b = _splice(b, synth.pileup(L, 120, seed=123, ref=ref, snv_every=7, lo=30_000, hi=33_000, max_depth=127))
+    pb, off, c, q = b
+    SH = 1 << 32
+    E = len(c)
+    codes = torch.zeros(SH + E + 16, dtype=torch.uint8, device=dev)
+    quals = torch.zeros(SH + E + 16, dtype=torch.uint8, device=dev)
+    codes[SH:SH + E] = torch.from_numpy(np.ascontiguousarray(c)).to(dev)
+    quals[SH:SH + E] = torch.from_numpy(np.ascontiguousarray(q)).to(dev)
+    d_off = torch.from_numpy(np.asarray(off, np.int64) + SH).to(dev)
+    torch.cuda.synchronize()
+    eng = _engine(ref, DEF, True)
+    eng.accumulate(pb, d_off, codes, quals, borrow=True, n_entries=E)
+    eng.finalize()
+    orc = _oracle(ref, DEF)
+    orc.accumulate(*b)
+    orc.finalize()
+    got = eng.variants()
+    compare_variants(got, orc.variants(), rtol=RTOL)
+    assert sum(1 for v in got if 30_000 <= v["start"] < 33_000) > 100
+    eng.close()
+    del codes, quals
+    torch.cuda.empty_cache()
