@@ -26,6 +26,8 @@ hipError_t launch_one(const MParams &P, const Hist *H, const uint8_t *ref, const
 hipError_t launch_lite(const MParams &P, const Hist &hb, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
                        hipStream_t st);
 int lite_blocks_per_cu();
+hipError_t launch_lite_fold(const MParams &P, const Hist &hb, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
+                            hipStream_t st);
 hipError_t launch_tile(const MParams &P, const Hist *H, const uint8_t *ref, int64_t ref_len, const Tables *T, Acc *acc,
                        int lpc, int64_t max_blocks, bool fused, hipStream_t st);
 hipError_t launch_merge(const MParams &P, const uint8_t *ref, Acc *acc, hipStream_t st);
@@ -767,6 +769,8 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
         P.n_groups = (int32_t)((u1 - u0 + 63) / 64);
         HIPCHK(launch_lite(P, c->h_hist[h0], c->ref, c->tables, c->acc, lb > 0 ? lb : (int64_t)c->n_cu * lite_blocks_per_cu(),
                            c->stream));
+        // the listed positions' exact fold (their records; deep columns are k_acc_seg<1>'s below)
+        HIPCHK(launch_lite_fold(P, c->h_hist[h0], c->ref, c->tables, c->acc, 2 * (int64_t)c->n_cu, c->stream));
     } else if (R.tile) {
         HIPCHK(launch_tile(P, c->d_hist, c->ref, c->ref_len, c->tables, c->acc, R.lpc, tile_blocks(c, R.lpc, fused, K == 1), fused,
                            c->stream));

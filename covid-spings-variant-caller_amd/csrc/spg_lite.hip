@@ -41,7 +41,7 @@ struct LBounds {           // a tile's byte range [off[c0], off[c0 + 64]) (wave-
     uint64_t b, e;
 };
 
-__global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_acc_lite(
+__global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_acc_lite(
     MParams P, Hist hb, const uint8_t *__restrict__ ref, const Tables *__restrict__ T, Acc *__restrict__ acc) {
     __shared__ double2 lut[256];                       // {ln(1-eps), eps} per q (the exact fold only)
     __shared__ __attribute__((aligned(16))) uint8_t slots[LW][2][LSLOT];   // per wave: a tile's code, qual
@@ -105,7 +105,6 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
         const uint32_t lc = lx < 16u ? (uint32_t)(0x00F0000004000201ull >> (4u * lx)) & 0xFu
                                      : (lx < 26u ? (0x8000u >> (4u * (lx - 16u))) & 0xFu : 0u);
         const uint32_t M = lc ? lc : 1u, mrep = M * 0x01010101u;   // code_of_ref, branch-free
-        const int Ms = M == 15u ? 4 : (int)__builtin_ctz(M);
         uint32_t len = inr ? D.oe - (uint32_t)D.ob : 0u;
         bool deep = false;
         if (inr && P.t_deep && len >= P.t_deep) { deep = true; len = 0; }   // k_acc_seg<1> takes it
@@ -119,27 +118,19 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
                     (uint32_t)(p - hb.pos_begin);
         }
         const uint32_t brel = inr ? (uint32_t)(hob - base) : 0u;      // the column's first byte in the tile
-        uint32_t mcf = 0, drare = 0, n_other = 0, cnt[NSLOT] = {0, 0, 0, 0, 0};
+        // counts: the entries that pass the bq filter (totalDepth, :87) and those that are the REF code at a
+        // q of 4..127 (SWAR; every other passing entry — another allele, D/N, a REF entry at q < 4 or >= 128 —
+        // counts as non-REF)
+        uint32_t mcf = 0, dep = 0;
         auto count = [&](const u32x4 &cw, const u32x4 &qw, int32_t x0, int32_t vlen) {
             uint32_t vm[4];
             valid_masks<4>(x0, 0, vlen, vm);
 #pragma unroll
             for (int d = 0; d < 4; d++) {
-                const uint32_t c_ = dw<4>(cw, d), q_ = dw<4>(qw, d);
                 uint32_t f80, r80;
-                swar4(c_, q_, vm[d], mrep, P.kpass, P.kok, f80, r80);
+                swar4(dw<4>(cw, d), dw<4>(qw, d), vm[d], mrep, P.kpass, P.kok, f80, r80);
                 mcf += __popc(f80);
-                while (r80) {                          // every other entry: its slot's count
-                    const int sh = __builtin_ctz(r80) - 7;
-                    r80 &= r80 - 1;
-                    const uint32_t cc = (c_ >> sh) & 0xFFu, qq = (q_ >> sh) & 0xFFu;
-                    if ((int)qq < P.min_bq) continue;
-                    drare++;
-                    const int s = slot_of(cc);
-                    n_other += (s < 0 && cc < 16u) ? 1u : 0u;
-#pragma unroll
-                    for (int k = 0; k < NSLOT; k++) cnt[k] += k == s ? 1u : 0u;
-                }
+                dep += __popc(f80 | r80);
             }
         };
         // the column's aligned blocks j0 .. j1 - 1 of the tile: from the slot, then (past it) from memory
@@ -167,31 +158,65 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
                 count(cw, qw, (int32_t)(16u * j) - (int32_t)brel, (int32_t)len);
             }
         }
-        // prepare_variants' filters on the counts (:131, :151-157); an exotic allele goes to the exact replay
-        const uint32_t depth = mcf + drare;
-        bool mc = n_other != 0;
-        if (!mc && (int64_t)depth >= (int64_t)P.min_td) {
-            const double dlo = (double)depth * P.ratio_lo;
-#pragma unroll
-            for (int k = 0; k < NSLOT; k++) {
-                const uint32_t n = cnt[k] + (k == Ms ? mcf : 0u);
-                mc |= n != 0 && refc != nibble_char(slot_code(k)) && (int64_t)n >= P.min_ad && (double)n >= dlo;
-            }
+        // prepare_variants' filters (:131, :151-157) on what the counts bound: an allele other than the REF char
+        // has at most dep - mcf entries; the REF code's own entries (mcf) are a candidate allele when the stored REF
+        // char is not its upper-case letter (soft-masked 'a' != 'A', :151; a REF outside ACGTN maps to A).  A
+        // position that passes is folded exactly by k_lite_fold and decided by the sparse finalize.
+        bool mc = false;
+        if ((int64_t)dep >= (int64_t)P.min_td) {
+            const double dlo = (double)dep * P.ratio_lo;
+            const uint32_t nonref = dep - mcf;
+            mc = ((int64_t)nonref >= P.min_ad && (double)nonref >= dlo) ||
+                 (refc != nibble_char(M) && (int64_t)mcf >= P.min_ad && (double)mcf >= dlo);
         }
         const bool want = inr && (deep || (len != 0 && mc));
         const uint64_t wm = __ballot(want);
-        if (!wm) return;
-        {
+        if (wm) {
             uint32_t at = 0;                           // one list reservation per wave
             if (lane == 0) at = atomicAdd(P.n_list, (uint32_t)__popcll(wm));
             at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
             if (want) P.list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u))] = p;
         }
-        if (!__ballot(want && !deep)) return;
-        // ---- the exact fold of the columns that may call: process_pileup_column / process_svn (:74-103) in
-        // BAM order — totalDepth, D/N/other, per allele count, sum q, q lower bound, first entry (dict order),
-        // sum ln(1 - eps), sum eps — merged into an empty record (first visit :77-85)
-        const bool fold = want && !deep;
+    };
+
+    // the pipeline: tile t's chunks and heads in set A or B (issued one tile ahead), its byte range two ahead
+    LBounds B0 = bounds(tile), B1 = bounds(tile + stride);
+    LData A, B;
+    issue(tile, B0, A);
+    // (each half loads the range before its chunks: loads complete in order, so the next half's wait for the
+    // range leaves the chunks in flight)
+    while (tile < n_tiles) {
+        B0 = bounds(tile + 2 * stride);
+        issue(tile + stride, B1, B);
+        process(tile, A);
+        tile += stride;
+        if (tile >= n_tiles) break;
+        B1 = bounds(tile + 2 * stride);
+        issue(tile + stride, B0, A);
+        process(tile, B);
+        tile += stride;
+    }
+}
+
+// The exact fold of the positions k_acc_lite listed (the ones whose counts pass the pre-check; columns of
+// >= t_deep entries are left to k_acc_seg<1>): one lane per position, its column read in BAM order from the
+// batch (L2-resident after k_acc_lite) — process_pileup_column / process_svn (:74-103): totalDepth, D/N/other,
+// per allele count, sum q, q lower bound, first entry (dict order), sum ln(1 - eps), sum eps — merged into an
+// empty record (first visit :77-85).
+__global__ __launch_bounds__(256) void k_lite_fold(MParams P, Hist hb, const uint8_t *__restrict__ ref,
+                                                   const Tables *__restrict__ T, Acc *__restrict__ acc) {
+    __shared__ double2 lut[256];
+    for (uint32_t q = threadIdx.x; q < 256u; q += 256u) lut[q] = make_double2(T->fast[q][0], T->fast[q][1]);
+    __syncthreads();
+    const uint32_t n_list = *P.n_list;
+    for (uint32_t i0 = blockIdx.x * 256u + (threadIdx.x & ~63u); i0 < n_list; i0 += gridDim.x * 256u) {
+        const uint32_t i = i0 + (threadIdx.x & 63u);
+        const int64_t p = i < n_list ? P.list[i] : P.u0;
+        const int64_t col = p - hb.pos_begin;
+        const uint64_t hob = hb.off[col];
+        const uint32_t len = (uint32_t)(hb.off[col + 1] - hob);
+        const bool fold = i < n_list && len != 0 && !(P.t_deep && len >= P.t_deep);
+        const uint8_t refc = ref[p];
         uint32_t fd = 0, fdel = 0, fskip = 0, foth = 0;
         uint32_t fc[NSLOT], fsq[NSLOT], ffirst[NSLOT], fqf[NSLOT];
         double fsl[NSLOT], fse[NSLOT];
@@ -229,7 +254,7 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
                     }
             }
         }
-        if (!fold) return;
+        if (!fold) continue;
         uint32_t newmask = 0;
         bool sums = false;
 #pragma unroll
@@ -262,25 +287,13 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
             dst[8] = make_uint4(d2(ose[1]).x, d2(ose[1]).y, d2(ose[2]).x, d2(ose[2]).y);
             dst[9] = make_uint4(d2(ose[3]).x, d2(ose[3]).y, d2(ose[4]).x, d2(ose[4]).y);
         }
-    };
-
-    // the pipeline: tile t's chunks and heads in set A or B (issued one tile ahead), its byte range two ahead
-    LBounds B0 = bounds(tile), B1 = bounds(tile + stride);
-    LData A, B;
-    issue(tile, B0, A);
-    // (each half loads the range before its chunks: loads complete in order, so the next half's wait for the
-    // range leaves the chunks in flight)
-    while (tile < n_tiles) {
-        B0 = bounds(tile + 2 * stride);
-        issue(tile + stride, B1, B);
-        process(tile, A);
-        tile += stride;
-        if (tile >= n_tiles) break;
-        B1 = bounds(tile + 2 * stride);
-        issue(tile + stride, B0, A);
-        process(tile, B);
-        tile += stride;
     }
+}
+
+hipError_t launch_lite_fold(const MParams &P, const Hist &hb, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(k_lite_fold, dim3((unsigned)std::max<int64_t>(1, blocks)), dim3(256), 0, st, P, hb, ref, T, acc);
+    return hipGetLastError();
 }
 
 int lite_blocks_per_cu() {
