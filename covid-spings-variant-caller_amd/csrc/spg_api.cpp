@@ -28,6 +28,12 @@ hipError_t launch_lite(const MParams &P, const Hist &hb, const uint8_t *ref, con
 int lite_blocks_per_cu();
 hipError_t launch_lite_fold(const MParams &P, const Hist &hb, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
                             hipStream_t st);
+hipError_t launch_count_run(const MParams &P, const Hist *H, const uint8_t *ref, uint32_t *cdep, uint32_t *cmcf, int lpc,
+                            int64_t blocks, hipStream_t st);
+int count_run_blocks_per_cu(int lpc);
+hipError_t launch_count_list(const MParams &P, const uint8_t *ref, const uint32_t *cdep, const uint32_t *cmcf, hipStream_t st);
+hipError_t launch_fold_hist(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
+                            hipStream_t st);
 hipError_t launch_tile(const MParams &P, const Hist *H, const uint8_t *ref, int64_t ref_len, const Tables *T, Acc *acc,
                        int lpc, int64_t max_blocks, bool fused, hipStream_t st);
 hipError_t launch_merge(const MParams &P, const uint8_t *ref, Acc *acc, hipStream_t st);
@@ -140,6 +146,12 @@ struct spg_ctx {
                                         // finalize runs it fused (k_acc_seg<..., FUSE>), anything else first
                                         // accumulates it on its own
     int64_t stale_end = 0;
+    // counted mode (calls-only runs of shallow batches): per-position bq-passing / REF-code entry counts of history
+    // [0, count_end), the records stale; see finalize_counted
+    bool counted = false;
+    int64_t count_end = 0;
+    int64_t n_deep_hist = 0;            // deep / multi-sample batches since reset (counted mode needs none)
+    uint32_t *cdep = nullptr, *cmcf = nullptr;
     MState *part = nullptr;             // split-run partial states
     size_t part_bytes = 0;
     // replay index: history batches per 2^RIDX_SHIFT-position bucket
@@ -288,7 +300,7 @@ int spg_destroy(spg_ctx *c) {
     c->arena.release();
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
-                    c->d_fused, c->deep_list, c->deep_n};
+                    c->d_fused, c->deep_list, c->deep_n, c->cdep, c->cmcf};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
@@ -312,6 +324,9 @@ int spg_reset(spg_ctx *c) {
     HIPCHK(hipSetDevice(c->device));
     c->stale = false;
     c->deep_pend = false;
+    c->counted = false;
+    c->count_end = 0;
+    c->n_deep_hist = 0;
     // batches still pending belong to the old sample: dropped.  Copies into the recycled arena are
     // ordered after every kernel enqueued so far (add_batch records that fence before its first copy).
     if (!c->arena.slabs.empty()) c->arena_fence = true;
@@ -799,6 +814,7 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
 static int materialize(spg_ctx *c) {
     if (!c->stale) return 0;
     c->stale = false;
+    c->counted = false;            // the records hold history [0, stale_end) again; pending batches fold into them
     const int64_t keep = c->pend0;
     c->pend0 = 0;
     const int rc = flush_run(c, c->stale_end, false);
@@ -830,7 +846,11 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
                      const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags,
                      bool *pageable_copy, int64_t n_samples = 1, const uint32_t *first_sample = nullptr) {
     if (n_samples < 1 || n_samples > (1 << 30)) return fail("spg_accumulate_samples: n_samples out of range");
-    if (int rc = materialize(c)) return rc;
+    static const double deep_min = [] { const char *e = getenv("SPG_DEEP_MIN"); return e ? atof(e) : 256.0; }();
+    const bool deep_batch = (n_cols > 0 && (double)n_entries / (double)n_cols >= deep_min) || n_samples > 1 || first_sample;
+    // counted mode keeps the records stale while shallow batches arrive (they are counted at the next finalize)
+    if (!(c->counted && !deep_batch))
+        if (int rc = materialize(c)) return rc;
     if (int rc = flush_deep(c)) return rc;
     if (n_cols < 0 || pos_begin < 0 || pos_begin + n_cols > c->n_pos)
         return fail("spg_accumulate: column range outside the context's positions");
@@ -915,9 +935,8 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
     c->ridx_dirty = true;
     c->batch_seq += (uint32_t)n_samples;
     c->finalized = false;
-    static const double deep_min = [] { const char *e = getenv("SPG_DEEP_MIN"); return e ? atof(e) : 256.0; }();
-    const double avg = (double)n_entries / (double)n_cols;
-    if (avg >= deep_min || n_samples > 1 || first_sample) {
+    if (deep_batch) {
+        c->n_deep_hist++;
         // a deep (or multi-sample) batch: the run before it first (accumulate order), then k_acc_seg on
         // its own (a run folds single-sample batches with consecutive batch numbers)
         if (int rc = flush_run(c, idx)) return rc;
@@ -933,8 +952,9 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
         return acc_end(c);
     }
     c->pend_entries += n_entries;
+    // (calls-only: the pending run waits for the finalize, which counts it — see finalize_counted)
     static const int64_t run_max = env_i64("SPG_RUN_MAX", 4096);
-    if ((int64_t)c->hist.size() - c->pend0 >= run_max) return flush_run(c);
+    if (!(c->p.flags & SPG_P_CALLS_ONLY) && (int64_t)c->hist.size() - c->pend0 >= run_max) return flush_run(c);
     return 0;
 }
 
@@ -1086,6 +1106,94 @@ static FParams make_fparams(spg_ctx *c) {
     return F;
 }
 
+// Counted mode (a calls-only finalize of a sample of shallow batches, e.g. one process_bam per BAM): count the
+// batches not counted yet into the per-position totals (k_acc_lite_run), list the positions whose totals can
+// pass prepare_variants' filters (k_count_list), build their records exactly from the whole history
+// (k_fold_hist); the sparse finalize then decides them.  The other records stay stale (materialize() re-folds
+// the history if anything reads them).
+static int finalize_counted(spg_ctx *c) {
+    const int64_t nh = (int64_t)c->hist.size();
+    if (!c->counted) {
+        if (!c->cdep) {
+            HIPCHK(hipMalloc(&c->cdep, sizeof(uint32_t) * c->n_pos));
+            HIPCHK(hipMalloc(&c->cmcf, sizeof(uint32_t) * c->n_pos));
+        }
+        HIPCHK(hipMemsetAsync(c->cdep, 0, sizeof(uint32_t) * c->n_pos, c->stream));
+        HIPCHK(hipMemsetAsync(c->cmcf, 0, sizeof(uint32_t) * c->n_pos, c->stream));
+        c->count_end = 0;
+    }
+    const int64_t h0 = c->count_end;
+    int64_t ua = INT64_MAX, ub = INT64_MIN;            // positions of the whole history (listing)
+    int64_t u0 = INT64_MAX, u1 = INT64_MIN;            // ... and of the batches counted now
+    uint64_t run_entries = 0;
+    for (int64_t i = 0; i < nh; i++) {
+        const HistBatch &b = c->hist[(size_t)i];
+        ua = std::min(ua, b.pos_begin);
+        ub = std::max(ub, b.pos_begin + b.n_cols);
+        if (i >= h0) {
+            u0 = std::min(u0, b.pos_begin);
+            u1 = std::max(u1, b.pos_begin + b.n_cols);
+            run_entries += b.n_entries;
+        }
+    }
+    if (int rc = wait_copies(c)) return rc;
+    if (int rc = acc_begin(c)) return rc;
+    // descriptors of every batch not uploaded yet (pinned mirror -> device table)
+    const int64_t up0 = std::min(h0, c->pend0);
+    if (nh > up0) {
+        HIPCHK(hipMemcpyAsync(c->d_hist + up0, c->h_hist + up0, sizeof(Hist) * (nh - up0), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipEventRecord(c->hist_ev, c->stream));
+        c->hist_up = true;
+    }
+    MParams P{};
+    fill_swar(c, P.min_bq, P.qlo, P.kpass, P.kok);
+    P.epoch = c->epoch;
+    P.calls_only = 1u;
+    P.min_td = c->p.min_total_depth;
+    P.min_ad = c->p.min_allele_depth;
+    P.ratio_lo = c->p.min_evidence_ratio * (1.0 - 1e-9);
+    P.list = c->band;
+    P.n_list = c->nlist;
+    if (nh > h0) {
+        // one wave per (tile, batch split): LPC lanes per column so that a tile's bytes of one batch fit the
+        // 3 KiB slot; splits until the items fill the resident grid twice over
+        const int64_t K = nh - h0, L = u1 - u0;
+        const double mean = (double)run_entries / ((double)K * (double)std::max<int64_t>(1, L));
+        int lpc = 1;
+        while (lpc < 8 && (64.0 / lpc) * mean > 2200.0) lpc *= 2;
+        const int64_t tc = 64 / lpc, n_tiles = (L + tc - 1) / tc;
+        const int64_t blocks = (int64_t)c->n_cu * count_run_blocks_per_cu(lpc);
+        const int64_t want_items = 2 * blocks * 4;
+        const int64_t S = std::min<int64_t>(K, std::max<int64_t>(1, (want_items + n_tiles - 1) / n_tiles));
+        P.u0 = u0;
+        P.u1 = u1;
+        P.h0 = (int32_t)h0;
+        P.K = (int32_t)K;
+        P.kper = (int32_t)((K + S - 1) / S);
+        P.S = (int32_t)((K + P.kper - 1) / P.kper);
+        P.n_groups = (int32_t)n_tiles;
+        HIPCHK(launch_count_run(P, c->d_hist, c->ref, c->cdep, c->cmcf, lpc, blocks, c->stream));
+        if (int rc = trace_sync(c, "accumulate (k_acc_lite_run)")) return rc;
+    }
+    c->count_end = nh;
+    c->counted = true;
+    c->pend0 = nh;
+    c->pend_entries = 0;
+    // list, then the exact records of the listed positions over the whole history
+    HIPCHK(hipMemsetAsync(c->nlist, 0, sizeof(uint32_t), c->stream));
+    P.u0 = ua;
+    P.u1 = ub;
+    HIPCHK(launch_count_list(P, c->ref, c->cdep, c->cmcf, c->stream));
+    P.h0 = 0;
+    P.K = (int32_t)nh;
+    P.seq0 = c->hist[0].seq0;
+    HIPCHK(launch_fold_hist(P, c->d_hist, c->ref, c->tables, c->acc, 4 * (int64_t)c->n_cu, c->stream));
+    if (int rc = trace_sync(c, "accumulate (k_fold_hist)")) return rc;
+    c->stale = true;
+    c->stale_end = nh;
+    return acc_end(c);
+}
+
 static int finalize_impl(spg_ctx *c, bool table);
 
 int spg_finalize(spg_ctx *c) {
@@ -1106,10 +1214,15 @@ static int finalize_impl(spg_ctx *c, bool table) {
     const bool fused_deep = !table && c->deep_pend && nh == 1;
     if (!fused_deep)
         if (int rc = flush_deep(c)) return rc;
-    const bool fused = !fused_deep && !table && !no_fuse && (c->p.flags & SPG_P_CALLS_ONLY) && c->pend0 == 0 &&
+    static const bool no_count = getenv("SPG_NO_COUNT") != nullptr;
+    const bool counted = !fused_deep && !table && !no_fuse && !no_count && (c->p.flags & SPG_P_CALLS_ONLY) && nh >= 2 &&
+                         c->n_deep_hist == 0 && (c->counted || (c->pend0 == 0 && !c->stale));
+    const bool fused = !counted && !fused_deep && !table && !no_fuse && (c->p.flags & SPG_P_CALLS_ONLY) && c->pend0 == 0 &&
                        nh > 0 && run_splits(c, 0, nh) == 1;
     if (fused_deep) {
         c->deep_pend = false;
+    } else if (counted) {
+        if (int rc = finalize_counted(c)) return rc;
     } else if (fused) {
         if (int rc = flush_run(c, -1, true)) return rc;
         c->stale = true;
@@ -1140,7 +1253,7 @@ static int finalize_impl(spg_ctx *c, bool table) {
         if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
     } else {
         if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
-        if (fused) { F.list = c->band; F.n_list = c->nlist; }
+        if (fused || counted) { F.list = c->band; F.n_list = c->nlist; }
         if (int rc = upload_ridx(c, F.ridx)) return rc;
         HIPCHK(launch_finalize(F, c->acc, c->tables, make_out(c), c->d_hist, c->stream));
         if (trace_sync(c, "finalize")) return -1;

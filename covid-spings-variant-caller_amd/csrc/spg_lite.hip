@@ -316,4 +316,320 @@ hipError_t launch_lite(const MParams &P, const Hist &hb, const uint8_t *ref, con
     return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------------------------------------
+// Counted mode: a calls-only sample accumulated as many shallow batches (process_bam once per BAM,
+// vc_queue.py:142-144; BASELINE config 4 in its live form).  prepare_variants' filters need, per position,
+// totalDepth and the counts of its alleles; k_acc_lite_run adds each batch's bq-passing entries and its
+// REF-code entries (q 4..127) into two u32 arrays — additive, so batches fold in any order and across
+// finalizes — and k_count_list lists the positions whose counts can pass the filters.  k_fold_hist then
+// builds those positions' records exactly from the batch history (every batch since reset, in order); the
+// sparse finalize decides them.  Records of the other positions are re-materialized if anything reads them.
+// ---------------------------------------------------------------------------------------------------------
+
+struct RUnit {             // one (tile, batch) unit in flight: the batch's arrays and the tile's byte range
+    const uint64_t *off;
+    const uint8_t *code, *qual;
+    int64_t pos_begin, n_cols;
+    uint64_t b, e;
+};
+struct RData {             // its staged chunks and the lane's column bounds (see LData)
+    u32x4 c[LCH], q[LCH];
+    uint64_t ob;
+    uint32_t oe;
+};
+
+// items = (tile of 64 / LPC columns, batch split); a wave streams its item's batches through the LDS slot,
+// LPC lanes per column taking the column's 16-B blocks round-robin
+template <int LPC>
+__global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_acc_lite_run(
+    MParams P, const Hist *__restrict__ H, const uint8_t *__restrict__ ref, uint32_t *__restrict__ cdep,
+    uint32_t *__restrict__ cmcf) {
+    constexpr int TC = 64 / LPC;
+    __shared__ __attribute__((aligned(16))) uint8_t slots[LW][2][LSLOT];
+    const int lane = threadIdx.x & 63, sub = lane % LPC, cl = lane / LPC;
+    uint8_t *const sc = slots[threadIdx.x >> 6][0];
+    uint8_t *const sq = slots[threadIdx.x >> 6][1];
+    const int64_t n_tiles = P.n_groups, n_items = n_tiles * P.S;
+    const int64_t wstride = (int64_t)gridDim.x * LW;
+    for (int64_t item = (int64_t)__builtin_amdgcn_readfirstlane(blockIdx.x * LW + (threadIdx.x >> 6)); item < n_items;
+         item += wstride) {
+        const int64_t g = item % n_tiles, sp = item / n_tiles;
+        const int32_t k0 = (int32_t)sp * P.kper, k1 = min(P.K, k0 + P.kper);
+        const int64_t t0 = P.u0 + g * TC, t1 = min(t0 + TC, P.u1);
+        const int64_t p = t0 + cl;
+        const bool inr = p < P.u1;
+        const uint8_t refc = ref[min(p, P.u1 - 1)];
+        const uint32_t lx = ((uint32_t)refc & 0xDFu) - 65u;
+        const uint32_t lc = lx < 16u ? (uint32_t)(0x00F0000004000201ull >> (4u * lx)) & 0xFu
+                                     : (lx < 26u ? (0x8000u >> (4u * (lx - 16u))) & 0xFu : 0u);
+        const uint32_t mrep = (lc ? lc : 1u) * 0x01010101u;
+        uint32_t dep = 0, mcf = 0;
+
+        auto unit = [&](int32_t k) -> RUnit {         // batch k's descriptor and the tile's byte range in it
+            const Hist h = H[P.h0 + min(k, P.K - 1)];
+            const int64_t cA = min(max(t0 - h.pos_begin, (int64_t)0), h.n_cols);
+            const int64_t cB = min(max(t1 - h.pos_begin, (int64_t)0), h.n_cols);
+            return RUnit{h.off, h.code, h.qual, h.pos_begin, h.n_cols, h.off[cA], h.off[cB]};
+        };
+        auto issue = [&](int32_t k, const RUnit &U, RData &D) {
+            const uint64_t base = U.b & ~(uint64_t)15;
+            const uint64_t span = k < k1 ? U.e - base : 0;
+#pragma unroll
+            for (int c = 0; c < LCH; c++) {
+                const uint32_t o = 1024u * c + 16u * lane;
+                const uint64_t a = o < span ? base + o : base;
+                D.c[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(U.code + a));
+                D.q[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(U.qual + a));
+            }
+            const int64_t cc = min(max(p - U.pos_begin, (int64_t)0), max(U.n_cols - 1, (int64_t)0));
+            D.ob = U.off[cc];
+            D.oe = reinterpret_cast<const uint32_t *>(U.off + cc + 1)[0];
+        };
+        auto process = [&](int32_t k, const RUnit &U, const RData &D) {
+#pragma unroll
+            for (int c = 0; c < LCH; c++) {
+                *reinterpret_cast<u32x4 *>(sc + 1024 * c + 16 * lane) = D.c[c];
+                *reinterpret_cast<u32x4 *>(sq + 1024 * c + 16 * lane) = D.q[c];
+            }
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+            const uint64_t base = U.b & ~(uint64_t)15;
+            const int64_t col = p - U.pos_begin;
+            const bool inb = inr && col >= 0 && col < U.n_cols && U.e > U.b;
+            const uint32_t len = inb ? D.oe - (uint32_t)D.ob : 0u;
+            const uint32_t brel = inb ? (uint32_t)(D.ob - base) : 0u;
+            auto count = [&](const u32x4 &cw, const u32x4 &qw, int32_t x0, int32_t vlen) {
+                uint32_t vm[4];
+                valid_masks<4>(x0, 0, vlen, vm);
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    uint32_t f80, r80;
+                    swar4(dw<4>(cw, d), dw<4>(qw, d), vm[d], mrep, P.kpass, P.kok, f80, r80);
+                    mcf += __popc(f80);
+                    dep += __popc(f80 | r80);
+                }
+            };
+            // this lane's blocks of the column: j0 + sub, j0 + sub + LPC, ... (slot, then memory past it)
+            const uint32_t j0 = brel >> 4, j1 = len ? (brel + len + 15u) >> 4 : j0;
+            const uint32_t jl = min(j1, (uint32_t)LNBLK);
+            const uint32_t nl = jl > j0 + (uint32_t)sub ? (jl - j0 - (uint32_t)sub + LPC - 1) / LPC : 0u;
+            const uint32_t mx = wave_max_u32(nl);
+            const int32_t vlen = (int32_t)min(len, (uint32_t)LSLOT - min(brel, (uint32_t)LSLOT));
+            for (uint32_t t = 0; t < mx; t++) {
+                const uint32_t jj = j0 + (uint32_t)sub + LPC * t;
+                const uint32_t j = min(jj, (uint32_t)LNBLK - 1u);
+                const u32x4 cw = *reinterpret_cast<const u32x4 *>(sc + 16u * j);
+                const u32x4 qw = *reinterpret_cast<const u32x4 *>(sq + 16u * j);
+                count(cw, qw, (int32_t)(16u * jj) - (int32_t)brel, vlen);
+            }
+            if (__ballot(j1 > (uint32_t)LNBLK)) {
+                const uint32_t b0 = max(j0 + (uint32_t)sub, (uint32_t)LNBLK);
+                const uint32_t f0 = j0 + (uint32_t)sub + ((b0 - (j0 + (uint32_t)sub) + LPC - 1) / LPC) * LPC;
+                for (uint32_t j = f0;; j += LPC) {
+                    const bool more = j < j1;
+                    if (!__ballot(more)) break;
+                    u32x4 cw{0, 0, 0, 0}, qw{0, 0, 0, 0};
+                    if (more) {
+                        cw = *(reinterpret_cast<const u32x4 *>(U.code + base) + j);
+                        qw = *(reinterpret_cast<const u32x4 *>(U.qual + base) + j);
+                    }
+                    count(cw, qw, (int32_t)(16u * j) - (int32_t)brel, (int32_t)len);
+                }
+            }
+        };
+        // the pipeline over the item's batches (as k_acc_lite's over tiles)
+        RUnit B0 = unit(k0), B1 = unit(k0 + 1);
+        RData A, B;
+        issue(k0, B0, A);
+        for (int32_t k = k0; k < k1;) {
+            RUnit N0 = unit(k + 2);
+            issue(k + 1, B1, B);
+            process(k, B0, A);
+            B0 = N0;
+            if (++k >= k1) break;
+            RUnit N1 = unit(k + 2);
+            issue(k + 1, B0, A);
+            process(k, B1, B);
+            B1 = N1;
+            ++k;
+        }
+        // the column's totals (its LPC lanes), added to the position's counts
+#pragma unroll
+        for (int o = 1; o < LPC; o <<= 1) {
+            dep += (uint32_t)__shfl_xor((int)dep, o);
+            mcf += (uint32_t)__shfl_xor((int)mcf, o);
+        }
+        if (inr && sub == 0 && dep) {
+            atomicAdd(cdep + p, dep);
+            atomicAdd(cmcf + p, mcf);
+        }
+    }
+}
+
+// prepare_variants' filters on the counted totals (as k_acc_lite's pre-check): positions listed for the exact
+// fold and the sparse finalize
+__global__ __launch_bounds__(256) void k_count_list(MParams P, const uint8_t *__restrict__ ref,
+                                                    const uint32_t *__restrict__ cdep, const uint32_t *__restrict__ cmcf) {
+    const int64_t p = P.u0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    bool want = false;
+    if (p < P.u1) {
+        const uint32_t dep = cdep[p], mcf = cmcf[p];
+        if (dep && (int64_t)dep >= (int64_t)P.min_td) {
+            const uint8_t refc = ref[p];
+            const uint32_t lx = ((uint32_t)refc & 0xDFu) - 65u;
+            const uint32_t lc = lx < 16u ? (uint32_t)(0x00F0000004000201ull >> (4u * lx)) & 0xFu
+                                         : (lx < 26u ? (0x8000u >> (4u * (lx - 16u))) & 0xFu : 0u);
+            const double dlo = (double)dep * P.ratio_lo;
+            const uint32_t nonref = dep - mcf;
+            want = ((int64_t)nonref >= P.min_ad && (double)nonref >= dlo) ||
+                   (refc != nibble_char(lc ? lc : 1u) && (int64_t)mcf >= P.min_ad && (double)mcf >= dlo);
+        }
+    }
+    const uint64_t wm = __ballot(want);
+    if (!wm) return;
+    uint32_t at = 0;
+    if ((threadIdx.x & 63) == 0) at = atomicAdd(P.n_list, (uint32_t)__popcll(wm));
+    at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
+    if (want) P.list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u))] = p;
+}
+
+// The exact record of each listed position over history batches [h0, h0 + K) (every batch since reset): TPP
+// threads per position (up to a workgroup), thread r folding a contiguous batch range in BAM order (the per-entry rules of
+// process_pileup_column / process_svn, :74-103), then the 256 partial states merged in thread order with
+// first-entry keys (thread, stream index) — k_merge_parts' merge — into a FRESH record (first visit :77-85).
+// (The fp64 sums are added in that thread order: within 1e-16 relative of the sequential fold; positions
+// where the order matters are replayed exactly from the history by the finalize.)
+__global__ __launch_bounds__(256) void k_fold_hist(MParams P, const Hist *__restrict__ H, const uint8_t *__restrict__ ref,
+                                                   const Tables *__restrict__ T, Acc *__restrict__ acc) {
+    __shared__ double2 lut[256];
+    __shared__ MState part[256];
+    lut[threadIdx.x] = make_double2(T->fast[threadIdx.x][0], T->fast[threadIdx.x][1]);
+    __syncthreads();
+    const uint32_t n_list = *P.n_list;
+    // TPP threads per position (a power of two, <= 256, >= K when K is small): G positions per workgroup
+    uint32_t tpp = 1;
+    while (tpp < 256u && tpp < (uint32_t)P.K) tpp <<= 1;
+    const uint32_t G = 256u / tpp, grp = threadIdx.x / tpp, r = threadIdx.x % tpp;
+    const int32_t per = (P.K + (int32_t)tpp - 1) / (int32_t)tpp;
+    const int32_t k0 = min(P.K, (int32_t)r * per), k1 = min(P.K, k0 + per);
+    for (uint32_t lb = blockIdx.x * G; lb < n_list; lb += gridDim.x * G) {
+        const uint32_t li = lb + grp;
+        const bool act = li < n_list;
+        const int64_t p = act ? P.list[li] : P.u0;
+        MState S;
+        ms_init(S);
+        uint32_t sidx = 0;                             // raw entries of this position in this thread's batches
+        for (int32_t k = k0; act && k < k1; k++) {
+            const Hist h = H[P.h0 + k];
+            const int64_t col = p - h.pos_begin;
+            if (col < 0 || col >= h.n_cols) continue;
+            const uint64_t ob = h.off[col];
+            const uint32_t len = (uint32_t)(h.off[col + 1] - ob);
+            if (!len) continue;
+            if (S.fb == INF32) S.fb = (uint32_t)k;
+            const uint64_t a0 = ob & ~(uint64_t)3;
+            const int32_t lead = (int32_t)(ob & 3u);
+            const uint32_t nb = ((uint32_t)lead + len + 15u) >> 4;
+            for (uint32_t u = 0; u < nb; u++) {
+                const u32x4 cw = *(reinterpret_cast<const u32x4 *>(h.code + a0) + u);
+                const u32x4 qw = *(reinterpret_cast<const u32x4 *>(h.qual + a0) + u);
+#pragma unroll
+                for (int b = 0; b < 16; b++) {
+                    const int32_t x = (int32_t)(16u * u) + b - lead;
+                    const uint32_t cc = (dw<4>(cw, b >> 2) >> (8 * (b & 3))) & 0xFFu;
+                    const uint32_t qq = (dw<4>(qw, b >> 2) >> (8 * (b & 3))) & 0xFFu;
+                    if (x < 0 || x >= (int32_t)len || (int)qq < P.min_bq) continue;
+                    S.depth++;
+                    if (cc == SPG_CODE_DEL) { S.n_del++; continue; }
+                    if (cc == SPG_CODE_SKIP) { S.n_skip++; continue; }
+                    const int s = slot_of(cc);
+                    if (s < 0) { S.n_other++; continue; }
+                    const double2 tt = lut[qq];
+#pragma unroll
+                    for (int j = 0; j < NSLOT; j++)
+                        if (j == s) {
+                            S.cnt[j]++; S.sq[j] = sat_add31(S.sq[j], qq); S.qf[j] = (uint8_t)min((uint32_t)S.qf[j], qq);
+                            S.first[j] = min(S.first[j], sidx + (uint32_t)x);
+                            S.sl[j] += tt.x; S.se[j] += qq == 0 ? 1.0 : tt.y;
+                        }
+                }
+            }
+            sidx += len;
+        }
+        part[threadIdx.x] = S;
+        __syncthreads();
+        if (act && r == 0) {                           // the position's partial states, in thread (batch) order
+            MState c;
+            ms_init(c);
+            uint64_t key[NSLOT];
+#pragma unroll
+            for (int j = 0; j < NSLOT; j++) key[j] = ~0ull;
+            for (uint32_t rr = 0; rr < tpp; rr++) {
+                const MState &q = part[grp * tpp + rr];
+                if (q.fb == INF32) continue;
+                if (c.fb == INF32) c.fb = q.fb;
+                c.depth += q.depth; c.n_del += q.n_del; c.n_skip += q.n_skip; c.n_other += q.n_other;
+#pragma unroll
+                for (int j = 0; j < NSLOT; j++) {
+                    const uint32_t n = q.cnt[j];
+                    if (!n) continue;
+                    if (!c.cnt[j]) { key[j] = ((uint64_t)rr << 32) | q.first[j]; c.qf[j] = q.qf[j]; }
+                    else c.qf[j] = (uint8_t)min((uint32_t)c.qf[j], (uint32_t)q.qf[j]);
+                    c.cnt[j] += n;
+                    c.sq[j] = sat_add31(c.sq[j], q.sq[j]);
+                    c.sl[j] += q.sl[j];
+                    c.se[j] += q.se[j];
+                }
+            }
+            if (c.fb != INF32) {
+                Acc a{};
+                a.epoch = P.epoch;
+                merge_state(a, c, key, P.seq0 + c.fb, ref[p]);
+                const uint4 *src = reinterpret_cast<const uint4 *>(&a);
+                uint4 *dst = reinterpret_cast<uint4 *>(acc + p);
+#pragma unroll
+                for (int t = 0; t < 10; t++) dst[t] = src[t];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_count_run(const MParams &P, const Hist *H, const uint8_t *ref, uint32_t *cdep, uint32_t *cmcf, int lpc,
+                            int64_t blocks, hipStream_t st) {
+    if (P.n_groups == 0 || P.K == 0) return hipSuccess;
+    const dim3 grid((unsigned)std::max<int64_t>(1, blocks)), blk(64 * LW);
+    switch (lpc) {
+        case 1: hipLaunchKernelGGL(k_acc_lite_run<1>, grid, blk, 0, st, P, H, ref, cdep, cmcf); break;
+        case 2: hipLaunchKernelGGL(k_acc_lite_run<2>, grid, blk, 0, st, P, H, ref, cdep, cmcf); break;
+        case 4: hipLaunchKernelGGL(k_acc_lite_run<4>, grid, blk, 0, st, P, H, ref, cdep, cmcf); break;
+        default: hipLaunchKernelGGL(k_acc_lite_run<8>, grid, blk, 0, st, P, H, ref, cdep, cmcf); break;
+    }
+    return hipGetLastError();
+}
+int count_run_blocks_per_cu(int lpc) {
+    static int n[4] = {-1, -1, -1, -1};
+    const int i = lpc == 1 ? 0 : lpc == 2 ? 1 : lpc == 4 ? 2 : 3;
+    if (n[i] < 0) {
+        int b = 0;
+        const void *f = i == 0 ? (const void *)k_acc_lite_run<1> : i == 1 ? (const void *)k_acc_lite_run<2>
+                      : i == 2 ? (const void *)k_acc_lite_run<4> : (const void *)k_acc_lite_run<8>;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, 64 * LW, 0) != hipSuccess || b < 1) b = 2;
+        n[i] = b;
+    }
+    return n[i];
+}
+hipError_t launch_count_list(const MParams &P, const uint8_t *ref, const uint32_t *cdep, const uint32_t *cmcf, hipStream_t st) {
+    const int64_t n = P.u1 - P.u0;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_count_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, ref, cdep, cmcf);
+    return hipGetLastError();
+}
+hipError_t launch_fold_hist(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_hist, dim3((unsigned)std::max<int64_t>(1, blocks)), dim3(256), 0, st, P, H, ref, T, acc);
+    return hipGetLastError();
+}
+
 }  // namespace spg

@@ -86,8 +86,9 @@ def test_reset_accumulate_finalize_loop_without_reads():
 
 def test_run_error_is_reported_once_and_cleared_by_reset():
     """A run holding a batch with 2^30 entries in one tile (16 columns: the batch's mean depth puts 4 lanes on
-    a column) fails its settle (the shallow kernel does not fold a tile that size); after reset the context
-    accumulates and finalizes normally again."""
+    a column) fails its settle (the record path's shallow kernel, k_acc_tile, does not fold a tile that size;
+    a full-table context, so the finalize takes that path rather than calls-only counting); after reset the
+    context accumulates and finalizes normally again."""
     import torch
     from covid_spings_variant_caller_amd import synth
     dev = torch.device("cuda", 0)
@@ -103,7 +104,7 @@ def test_run_error_is_reported_once_and_cleared_by_reset():
     small = synth.pileup(n_cols, 0.01, seed=802, ref=ref, lo=1000, hi=3000)
     so, sc, sq = synth.to_device(small[1], small[2], small[3])
     torch.cuda.synchronize()
-    eng = _engine(n_cols, ref)
+    eng = _engine(n_cols, ref, calls_only=False)
     eng.accumulate_batches([(0, off, codes, quals, big), (1000, so, sc, sq, len(small[2]))], device=True, borrow=True)
     eng.finalize()
     with pytest.raises(RuntimeError):

@@ -293,7 +293,8 @@ def test_fused_fresh_run_then_more_batches_and_table():
     L = 400_000
     ref = synth.reference(L, seed=91)
     b1 = synth.pileup(L, 30, seed=92, ref=ref, snv_every=997, lo=0, hi=L)
-    b1 = _plant(b1, 123_456, 5, 35)                 # an IUPAC entry: exotic, replayed
+    for _ in range(8):                              # IUPAC entries (an exotic allele that can be called): replayed
+        b1 = _plant(b1, 123_456, 5, 35)
     b2 = synth.pileup(L, 20, seed=93, ref=ref, snv_every=501, lo=50_000, hi=350_000)
     eng = _engine(ref, True)
     orc = _oracle(ref)
