@@ -45,7 +45,8 @@ def build_gpu(force=False, verbose=False) -> str:
     out = os.path.join(LIBDIR, "libspings_gpu.so")
     deps = [os.path.join(CSRC, f) for f in GPU_SOURCES + GPU_HEADERS] + [os.path.join(INC, "spings_gpu.h")]
     if force or _stale(out, deps):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", f"-I{INC}", "-o", out + ".tmp",
+        # (-z defs: a kernel launcher the C-ABI declares but no source defines fails the build, not the load)
+        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wl,-z,defs", f"-I{INC}", "-o", out + ".tmp",
                "-Rpass-analysis=kernel-resource-usage"]
         cmd += [os.path.join(CSRC, f) for f in GPU_SOURCES]
         if verbose:

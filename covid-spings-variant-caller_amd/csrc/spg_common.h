@@ -278,6 +278,15 @@ __device__ __forceinline__ void lut_sl(uint32_t qw, uint32_t sel80, const double
     sl += (l1m[idx & 0xFFu] + l1m[(idx >> 8) & 0xFFu]) + (l1m[(idx >> 16) & 0xFFu] + l1m[idx >> 24]);
 }
 
+// A pointer read from a descriptor table is address-space generic to hipcc (flat loads: counted in both vmcnt
+// and lgkmcnt, so every wait on them drains both); these assert global memory (global_load).
+template <typename T>
+using gptr = const T __attribute__((address_space(1))) *;
+template <typename T>
+__device__ __forceinline__ gptr<T> gbl(const T *p) {
+    return (gptr<T>)p;
+}
+
 // wave-wide max of a per-lane count (DPP within rows, then the four row maxima)
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll

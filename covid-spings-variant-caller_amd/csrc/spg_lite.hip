@@ -33,15 +33,17 @@ constexpr int LNBLK = LSLOT / 16;
 // for a pending load before copying its destination).
 struct LData {
     u32x4 c[LCH], q[LCH];
-    uint64_t ob;
-    uint32_t oe;           // low half of the column's end (columns hold < 2^32 entries)
-    uint32_t rc;
+    uint64_t base;         // the tile's 16-B aligned start (resolved at issue)
+};
+struct LHead {             // the lane's column bounds and REF char (its own ping-pong pair, one tile ahead); the
+    uint32_t ob, oe;       // bounds' low halves only (a loaded dword nothing reads lets hipcc reuse its register,
+    uint32_t rc;           // which costs a full wait; tile-relative offsets need no more)
 };
 struct LBounds {           // a tile's byte range [off[c0], off[c0 + 64]) (wave-uniform)
     uint64_t b, e;
 };
 
-__global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_acc_lite(
+__global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_acc_lite(
     MParams P, Hist hb, const uint8_t *__restrict__ ref, const Tables *__restrict__ T, Acc *__restrict__ acc) {
     __shared__ double2 lut[256];                       // {ln(1-eps), eps} per q (the exact fold only)
     __shared__ __attribute__((aligned(16))) uint8_t slots[LW][2][LSLOT];   // per wave: a tile's code, qual
@@ -73,18 +75,20 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(5, 8)))
             D.c[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(hb.code + a));
             D.q[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(hb.qual + a));
         }
+        D.base = base;
+    };
+    auto head = [&](int64_t t) -> LHead {
         const int64_t p = P.u0 + t * 64 + lane;
         const int64_t cc = min(max(p - hb.pos_begin, (int64_t)0), hb.n_cols - 1);
-        D.ob = hb.off[cc];
-        D.oe = reinterpret_cast<const uint32_t *>(hb.off + cc + 1)[0];
-        D.rc = ref[min(max(p, P.u0), P.u1 - 1)];
+        return LHead{reinterpret_cast<const uint32_t *>(hb.off + cc)[0], reinterpret_cast<const uint32_t *>(hb.off + cc + 1)[0],
+                     (uint32_t)ref[min(max(p, P.u0), P.u1 - 1)]};
     };
 
     // one tile: counts of its columns, then the exact fold of the columns that may call
     uint8_t *const sc = slots[threadIdx.x >> 6][0];
     uint8_t *const sq = slots[threadIdx.x >> 6][1];
-    auto process = [&](int64_t t, const LData &D) {
-        // stage the tile (this wave's slot; LDS operations of a wave complete in order)
+    // stage a tile into this wave's slot (LDS operations of a wave complete in order)
+    auto stage = [&](const LData &D) {
 #pragma unroll
         for (int k = 0; k < LCH; k++) {
             *reinterpret_cast<u32x4 *>(sc + 1024 * k + 16 * lane) = D.c[k];
@@ -92,20 +96,16 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(5, 8)))
         }
         __builtin_amdgcn_wave_barrier();
         asm volatile("" ::: "memory");
-        // the tile's 16-B aligned start (lane 0's column is always in range)
-        // (readfirstlane returns int: through uint32_t, or the low half's bit 31 would sign-extend)
-        const uint32_t b_hi = __builtin_amdgcn_readfirstlane((uint32_t)(D.ob >> 32));
-        const uint32_t b_lo = __builtin_amdgcn_readfirstlane((uint32_t)D.ob);
-        const uint64_t base = (((uint64_t)b_hi << 32) | b_lo) & ~(uint64_t)15;
+    };
+    auto process = [&](int64_t t, uint64_t base, const LHead &D) {
         const int64_t p = P.u0 + t * 64 + lane;
         const bool inr = in_range(t);
-        const uint64_t hob = inr ? D.ob : 0;
         const uint8_t refc = (uint8_t)D.rc;
         const uint32_t lx = ((uint32_t)refc & 0xDFu) - 65u;
         const uint32_t lc = lx < 16u ? (uint32_t)(0x00F0000004000201ull >> (4u * lx)) & 0xFu
                                      : (lx < 26u ? (0x8000u >> (4u * (lx - 16u))) & 0xFu : 0u);
         const uint32_t M = lc ? lc : 1u, mrep = M * 0x01010101u;   // code_of_ref, branch-free
-        uint32_t len = inr ? D.oe - (uint32_t)D.ob : 0u;
+        uint32_t len = inr ? D.oe - D.ob : 0u;
         bool deep = false;
         if (inr && P.t_deep && len >= P.t_deep) { deep = true; len = 0; }   // k_acc_seg<1> takes it
         const uint64_t dm = __ballot(deep);
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(5, 8)))
                 P.deep_list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u))] =
                     (uint32_t)(p - hb.pos_begin);
         }
-        const uint32_t brel = inr ? (uint32_t)(hob - base) : 0u;      // the column's first byte in the tile
+        const uint32_t brel = inr ? D.ob - (uint32_t)base : 0u;       // the column's first byte in the tile
         // counts: the entries that pass the bq filter (totalDepth, :87) and those that are the REF code at a
         // q of 4..127 (SWAR; every other passing entry — another allele, D/N, a REF entry at q < 4 or >= 128 —
         // counts as non-REF)
@@ -179,21 +179,41 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(5, 8)))
         }
     };
 
-    // the pipeline: tile t's chunks and heads in set A or B (issued one tile ahead), its byte range two ahead
+    // the pipeline: tiles t and t + stride in flight in sets A and B while t is counted, their byte ranges two
+    // tiles further ahead, the lanes' column bounds one tile ahead (sets HA, HB).  A tile's set is staged into
+    // the slot and reloaded with the tile two ahead before the counting starts.  Every pair alternates: no
+    // register copy of a pending load (hipcc would wait for it).
+    // (compiler barriers keep each set's loads together and in this order: hipcc's wait counts follow issue order)
+#define SPG_ORDER asm volatile("" ::: "memory")
     LBounds B0 = bounds(tile), B1 = bounds(tile + stride);
     LData A, B;
     issue(tile, B0, A);
-    // (each half loads the range before its chunks: loads complete in order, so the next half's wait for the
-    // range leaves the chunks in flight)
+    SPG_ORDER;
+    issue(tile + stride, B1, B);
+    SPG_ORDER;
+    B0 = bounds(tile + 2 * stride);
+    B1 = bounds(tile + 3 * stride);
+    LHead HA = head(tile), HB;
+    SPG_ORDER;
     while (tile < n_tiles) {
-        B0 = bounds(tile + 2 * stride);
-        issue(tile + stride, B1, B);
-        process(tile, A);
+        stage(A);
+        uint64_t base = A.base;
+        issue(tile + 2 * stride, B0, A);
+        SPG_ORDER;
+        B0 = bounds(tile + 4 * stride);
+        HB = head(tile + stride);
+        SPG_ORDER;
+        process(tile, base, HA);
         tile += stride;
         if (tile >= n_tiles) break;
-        B1 = bounds(tile + 2 * stride);
-        issue(tile + stride, B0, A);
-        process(tile, B);
+        stage(B);
+        base = B.base;
+        issue(tile + 2 * stride, B1, B);
+        SPG_ORDER;
+        B1 = bounds(tile + 4 * stride);
+        HA = head(tile + stride);
+        SPG_ORDER;
+        process(tile, base, HB);
         tile += stride;
     }
 }
@@ -333,16 +353,24 @@ struct RUnit {             // one (tile, batch) unit in flight: the batch's arra
     int64_t pos_begin, n_cols;
     uint64_t b, e;
 };
-struct RData {             // its staged chunks and the lane's column bounds (see LData)
+struct RMeta {             // a unit's values the counting needs (resolved at issue: no pending loads)
+    uint64_t base;
+    const uint8_t *code, *qual;
+    int64_t pos_begin, n_cols;
+    bool nonempty;
+};
+struct RData {             // its staged chunks
     u32x4 c[LCH], q[LCH];
-    uint64_t ob;
-    uint32_t oe;
+    RMeta m;
+};
+struct RHead {             // the lane's column bounds in the unit's batch (ping-pong, one unit ahead); low
+    uint32_t ob, oe;       // halves only (a loaded dword nothing reads lets hipcc reuse its register: a full wait)
 };
 
 // items = (tile of 64 / LPC columns, batch split); a wave streams its item's batches through the LDS slot,
 // LPC lanes per column taking the column's 16-B blocks round-robin
 template <int LPC>
-__global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_acc_lite_run(
+__global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_acc_lite_run(
     MParams P, const Hist *__restrict__ H, const uint8_t *__restrict__ ref, uint32_t *__restrict__ cdep,
     uint32_t *__restrict__ cmcf) {
     constexpr int TC = 64 / LPC;
@@ -370,7 +398,7 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(4, 8)))
             const Hist h = H[P.h0 + min(k, P.K - 1)];
             const int64_t cA = min(max(t0 - h.pos_begin, (int64_t)0), h.n_cols);
             const int64_t cB = min(max(t1 - h.pos_begin, (int64_t)0), h.n_cols);
-            return RUnit{h.off, h.code, h.qual, h.pos_begin, h.n_cols, h.off[cA], h.off[cB]};
+            return RUnit{h.off, h.code, h.qual, h.pos_begin, h.n_cols, gbl(h.off)[cA], gbl(h.off)[cB]};
         };
         auto issue = [&](int32_t k, const RUnit &U, RData &D) {
             const uint64_t base = U.b & ~(uint64_t)15;
@@ -379,14 +407,18 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(4, 8)))
             for (int c = 0; c < LCH; c++) {
                 const uint32_t o = 1024u * c + 16u * lane;
                 const uint64_t a = o < span ? base + o : base;
-                D.c[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(U.code + a));
-                D.q[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(U.qual + a));
+                D.c[c] = __builtin_nontemporal_load(gbl(reinterpret_cast<const u32x4 *>(U.code + a)));
+                D.q[c] = __builtin_nontemporal_load(gbl(reinterpret_cast<const u32x4 *>(U.qual + a)));
             }
-            const int64_t cc = min(max(p - U.pos_begin, (int64_t)0), max(U.n_cols - 1, (int64_t)0));
-            D.ob = U.off[cc];
-            D.oe = reinterpret_cast<const uint32_t *>(U.off + cc + 1)[0];
+            D.m = RMeta{base, U.code, U.qual, U.pos_begin, U.n_cols, U.e > U.b};
         };
-        auto process = [&](int32_t k, const RUnit &U, const RData &D) {
+        auto head = [&](int32_t k) -> RHead {
+            const Hist h = H[P.h0 + min(k, P.K - 1)];
+            const int64_t cc = min(max(p - h.pos_begin, (int64_t)0), max(h.n_cols - 1, (int64_t)0));
+            return RHead{gbl(reinterpret_cast<const uint32_t *>(h.off + cc))[0],
+                         gbl(reinterpret_cast<const uint32_t *>(h.off + cc + 1))[0]};
+        };
+        auto stage = [&](const RData &D) {
 #pragma unroll
             for (int c = 0; c < LCH; c++) {
                 *reinterpret_cast<u32x4 *>(sc + 1024 * c + 16 * lane) = D.c[c];
@@ -394,11 +426,13 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(4, 8)))
             }
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
-            const uint64_t base = U.b & ~(uint64_t)15;
+        };
+        auto process = [&](const RMeta &U, const RHead &D) {
+            const uint64_t base = U.base;
             const int64_t col = p - U.pos_begin;
-            const bool inb = inr && col >= 0 && col < U.n_cols && U.e > U.b;
-            const uint32_t len = inb ? D.oe - (uint32_t)D.ob : 0u;
-            const uint32_t brel = inb ? (uint32_t)(D.ob - base) : 0u;
+            const bool inb = inr && col >= 0 && col < U.n_cols && U.nonempty;
+            const uint32_t len = inb ? D.oe - D.ob : 0u;
+            const uint32_t brel = inb ? D.ob - (uint32_t)base : 0u;
             auto count = [&](const u32x4 &cw, const u32x4 &qw, int32_t x0, int32_t vlen) {
                 uint32_t vm[4];
                 valid_masks<4>(x0, 0, vlen, vm);
@@ -431,27 +465,43 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(4, 8)))
                     if (!__ballot(more)) break;
                     u32x4 cw{0, 0, 0, 0}, qw{0, 0, 0, 0};
                     if (more) {
-                        cw = *(reinterpret_cast<const u32x4 *>(U.code + base) + j);
-                        qw = *(reinterpret_cast<const u32x4 *>(U.qual + base) + j);
+                        cw = gbl(reinterpret_cast<const u32x4 *>(U.code + base))[j];
+                        qw = gbl(reinterpret_cast<const u32x4 *>(U.qual + base))[j];
                     }
                     count(cw, qw, (int32_t)(16u * j) - (int32_t)brel, (int32_t)len);
                 }
             }
         };
-        // the pipeline over the item's batches (as k_acc_lite's over tiles)
+        // the pipeline over the item's batches (as k_acc_lite's over tiles: two units in flight, their ranges two
+        // further ahead, the lanes' column bounds one ahead; every pair alternates)
         RUnit B0 = unit(k0), B1 = unit(k0 + 1);
         RData A, B;
         issue(k0, B0, A);
+        SPG_ORDER;
+        issue(k0 + 1, B1, B);
+        SPG_ORDER;
+        B0 = unit(k0 + 2);
+        B1 = unit(k0 + 3);
+        RHead HA = head(k0), HB;
+        SPG_ORDER;
         for (int32_t k = k0; k < k1;) {
-            RUnit N0 = unit(k + 2);
-            issue(k + 1, B1, B);
-            process(k, B0, A);
-            B0 = N0;
+            stage(A);
+            const RMeta MA = A.m;
+            issue(k + 2, B0, A);
+            SPG_ORDER;
+            B0 = unit(k + 4);
+            HB = head(k + 1);
+            SPG_ORDER;
+            process(MA, HA);
             if (++k >= k1) break;
-            RUnit N1 = unit(k + 2);
-            issue(k + 1, B0, A);
-            process(k, B1, B);
-            B1 = N1;
+            stage(B);
+            const RMeta MB = B.m;
+            issue(k + 2, B1, B);
+            SPG_ORDER;
+            B1 = unit(k + 4);
+            HA = head(k + 1);
+            SPG_ORDER;
+            process(MB, HB);
             ++k;
         }
         // the column's totals (its LPC lanes), added to the position's counts
@@ -494,105 +544,152 @@ __global__ __launch_bounds__(256) void k_count_list(MParams P, const uint8_t *__
     if (want) P.list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u))] = p;
 }
 
+// wave reductions for the fold's partial states (fixed DPP pattern: deterministic)
+__device__ __forceinline__ uint32_t wmin_u32(uint32_t v) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) v = min(v, dpp_u32(v, c));
+    return min(min((uint32_t)__builtin_amdgcn_readlane(v, 0), (uint32_t)__builtin_amdgcn_readlane(v, 16)),
+               min((uint32_t)__builtin_amdgcn_readlane(v, 32), (uint32_t)__builtin_amdgcn_readlane(v, 48)));
+}
+__device__ __forceinline__ uint64_t wmin_u64(uint64_t v) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const uint64_t o = ((uint64_t)dpp_u32((uint32_t)(v >> 32), c) << 32) | dpp_u32((uint32_t)v, c);
+        v = min(v, o);
+    }
+    uint64_t m = ~0ull;
+#pragma unroll
+    for (int l = 0; l < 64; l += 16) {
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+        m = min(m, ((uint64_t)hi << 32) | lo);
+    }
+    return m;
+}
+
+struct FoldPart {          // one wave's reduced partial state of a position (k_fold_hist)
+    uint32_t depth, n_del, n_skip, n_other, fb;
+    uint32_t cnt[NSLOT], sq[NSLOT], qf[NSLOT];
+    uint64_t key[NSLOT];
+    double sl[NSLOT], se[NSLOT];
+};
+
 // The exact record of each listed position over history batches [h0, h0 + K) (every batch since reset): TPP
-// threads per position (up to a workgroup), thread r folding a contiguous batch range in BAM order (the per-entry rules of
-// process_pileup_column / process_svn, :74-103), then the 256 partial states merged in thread order with
-// first-entry keys (thread, stream index) — k_merge_parts' merge — into a FRESH record (first visit :77-85).
-// (The fp64 sums are added in that thread order: within 1e-16 relative of the sequential fold; positions
-// where the order matters are replayed exactly from the history by the finalize.)
-__global__ __launch_bounds__(256) void k_fold_hist(MParams P, const Hist *__restrict__ H, const uint8_t *__restrict__ ref,
-                                                   const Tables *__restrict__ T, Acc *__restrict__ acc) {
+// threads per position (64 .. 1024, about one batch each), thread r folding a contiguous batch range in BAM
+// order (the per-entry rules of process_pileup_column / process_svn, :74-103).  The partial states reduce
+// with sums and with minima of the first-entry keys (thread r, stream index) — the batch order, as
+// k_merge_parts' (split, index) keys — first per wave, then over the position's waves in order, into a FRESH
+// record (first visit :77-85).  (The fp64 sums are added in that fixed tree order: within 1e-16 relative of
+// the sequential fold; positions where the order matters are replayed exactly from the history by the
+// finalize.)
+__global__ __launch_bounds__(1024) void k_fold_hist(MParams P, const Hist *__restrict__ H, const uint8_t *__restrict__ ref,
+                                                    const Tables *__restrict__ T, Acc *__restrict__ acc) {
     __shared__ double2 lut[256];
-    __shared__ MState part[256];
-    lut[threadIdx.x] = make_double2(T->fast[threadIdx.x][0], T->fast[threadIdx.x][1]);
+    __shared__ FoldPart wp[16];
+    if (threadIdx.x < 256) lut[threadIdx.x] = make_double2(T->fast[threadIdx.x][0], T->fast[threadIdx.x][1]);
     __syncthreads();
     const uint32_t n_list = *P.n_list;
-    // TPP threads per position (a power of two, <= 256, >= K when K is small): G positions per workgroup
-    uint32_t tpp = 1;
-    while (tpp < 256u && tpp < (uint32_t)P.K) tpp <<= 1;
-    const uint32_t G = 256u / tpp, grp = threadIdx.x / tpp, r = threadIdx.x % tpp;
+    uint32_t tpp = 64;
+    while (tpp < 1024u && tpp < (uint32_t)P.K) tpp <<= 1;
+    const uint32_t G = 1024u / tpp, grp = threadIdx.x / tpp, r = threadIdx.x % tpp;
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const int32_t per = (P.K + (int32_t)tpp - 1) / (int32_t)tpp;
     const int32_t k0 = min(P.K, (int32_t)r * per), k1 = min(P.K, k0 + per);
     for (uint32_t lb = blockIdx.x * G; lb < n_list; lb += gridDim.x * G) {
         const uint32_t li = lb + grp;
         const bool act = li < n_list;
         const int64_t p = act ? P.list[li] : P.u0;
-        MState S;
-        ms_init(S);
-        uint32_t sidx = 0;                             // raw entries of this position in this thread's batches
+        uint32_t depth = 0, n_del = 0, n_skip = 0, n_other = 0, fb = INF32, sidx = 0;
+        uint32_t cnt[NSLOT], sq[NSLOT], qf[NSLOT], first[NSLOT];
+        double sl[NSLOT], se[NSLOT];
+#pragma unroll
+        for (int j = 0; j < NSLOT; j++) { cnt[j] = sq[j] = 0; qf[j] = 255; first[j] = INF32; sl[j] = se[j] = 0.0; }
         for (int32_t k = k0; act && k < k1; k++) {
             const Hist h = H[P.h0 + k];
             const int64_t col = p - h.pos_begin;
             if (col < 0 || col >= h.n_cols) continue;
-            const uint64_t ob = h.off[col];
-            const uint32_t len = (uint32_t)(h.off[col + 1] - ob);
+            const uint64_t ob = gbl(h.off)[col];
+            const uint32_t len = (uint32_t)(gbl(h.off)[col + 1] - ob);
             if (!len) continue;
-            if (S.fb == INF32) S.fb = (uint32_t)k;
+            if (fb == INF32) fb = (uint32_t)k;
             const uint64_t a0 = ob & ~(uint64_t)3;
             const int32_t lead = (int32_t)(ob & 3u);
             const uint32_t nb = ((uint32_t)lead + len + 15u) >> 4;
             for (uint32_t u = 0; u < nb; u++) {
-                const u32x4 cw = *(reinterpret_cast<const u32x4 *>(h.code + a0) + u);
-                const u32x4 qw = *(reinterpret_cast<const u32x4 *>(h.qual + a0) + u);
+                const u32x4 cw = gbl(reinterpret_cast<const u32x4 *>(h.code + a0))[u];
+                const u32x4 qw = gbl(reinterpret_cast<const u32x4 *>(h.qual + a0))[u];
 #pragma unroll
                 for (int b = 0; b < 16; b++) {
                     const int32_t x = (int32_t)(16u * u) + b - lead;
                     const uint32_t cc = (dw<4>(cw, b >> 2) >> (8 * (b & 3))) & 0xFFu;
                     const uint32_t qq = (dw<4>(qw, b >> 2) >> (8 * (b & 3))) & 0xFFu;
                     if (x < 0 || x >= (int32_t)len || (int)qq < P.min_bq) continue;
-                    S.depth++;
-                    if (cc == SPG_CODE_DEL) { S.n_del++; continue; }
-                    if (cc == SPG_CODE_SKIP) { S.n_skip++; continue; }
+                    depth++;
+                    if (cc == SPG_CODE_DEL) { n_del++; continue; }
+                    if (cc == SPG_CODE_SKIP) { n_skip++; continue; }
                     const int s = slot_of(cc);
-                    if (s < 0) { S.n_other++; continue; }
+                    if (s < 0) { n_other++; continue; }
                     const double2 tt = lut[qq];
 #pragma unroll
                     for (int j = 0; j < NSLOT; j++)
                         if (j == s) {
-                            S.cnt[j]++; S.sq[j] = sat_add31(S.sq[j], qq); S.qf[j] = (uint8_t)min((uint32_t)S.qf[j], qq);
-                            S.first[j] = min(S.first[j], sidx + (uint32_t)x);
-                            S.sl[j] += tt.x; S.se[j] += qq == 0 ? 1.0 : tt.y;
+                            cnt[j]++; sq[j] += qq; qf[j] = min(qf[j], qq); first[j] = min(first[j], sidx + (uint32_t)x);
+                            sl[j] += tt.x; se[j] += qq == 0 ? 1.0 : tt.y;
                         }
                 }
             }
             sidx += len;
         }
-        part[threadIdx.x] = S;
-        __syncthreads();
-        if (act && r == 0) {                           // the position's partial states, in thread (batch) order
-            MState c;
-            ms_init(c);
-            uint64_t key[NSLOT];
+        // this wave's partial (its threads are consecutive in batch order)
+        FoldPart w;
+        w.depth = dsum_u32(depth); w.n_del = dsum_u32(n_del); w.n_skip = dsum_u32(n_skip); w.n_other = dsum_u32(n_other);
+        w.fb = wmin_u32(fb);
 #pragma unroll
-            for (int j = 0; j < NSLOT; j++) key[j] = ~0ull;
-            for (uint32_t rr = 0; rr < tpp; rr++) {
-                const MState &q = part[grp * tpp + rr];
-                if (q.fb == INF32) continue;
-                if (c.fb == INF32) c.fb = q.fb;
-                c.depth += q.depth; c.n_del += q.n_del; c.n_skip += q.n_skip; c.n_other += q.n_other;
+        for (int j = 0; j < NSLOT; j++) {
+            w.cnt[j] = dsum_u32(cnt[j]);
+            w.sq[j] = dsum_u32(sq[j]);
+            w.qf[j] = wmin_u32(qf[j]);
+            w.key[j] = wmin_u64(cnt[j] ? ((uint64_t)r << 32) | first[j] : ~0ull);
+            w.sl[j] = dsum_f64(sl[j]);
+            w.se[j] = dsum_f64(se[j]);
+        }
+        if (tpp > 64) {
+            if (lane == 0) wp[wave] = w;
+            __syncthreads();
+        }
+        if (act && r == 0) {                           // the position's waves, in order
+            const uint32_t nw = tpp / 64;
+            for (uint32_t v = 1; v < nw; v++) {
+                const FoldPart &o = wp[wave + v];
+                w.depth += o.depth; w.n_del += o.n_del; w.n_skip += o.n_skip; w.n_other += o.n_other;
+                w.fb = min(w.fb, o.fb);
 #pragma unroll
                 for (int j = 0; j < NSLOT; j++) {
-                    const uint32_t n = q.cnt[j];
-                    if (!n) continue;
-                    if (!c.cnt[j]) { key[j] = ((uint64_t)rr << 32) | q.first[j]; c.qf[j] = q.qf[j]; }
-                    else c.qf[j] = (uint8_t)min((uint32_t)c.qf[j], (uint32_t)q.qf[j]);
-                    c.cnt[j] += n;
-                    c.sq[j] = sat_add31(c.sq[j], q.sq[j]);
-                    c.sl[j] += q.sl[j];
-                    c.se[j] += q.se[j];
+                    w.cnt[j] += o.cnt[j]; w.sq[j] += o.sq[j]; w.qf[j] = min(w.qf[j], o.qf[j]);
+                    w.key[j] = min(w.key[j], o.key[j]); w.sl[j] += o.sl[j]; w.se[j] += o.se[j];
                 }
             }
-            if (c.fb != INF32) {
+            if (w.fb != INF32) {
+                MState c;
+                ms_init(c);
+                c.depth = w.depth; c.n_del = w.n_del; c.n_skip = w.n_skip; c.n_other = w.n_other; c.fb = w.fb;
+#pragma unroll
+                for (int j = 0; j < NSLOT; j++) {
+                    c.cnt[j] = w.cnt[j];
+                    c.sq[j] = min(w.sq[j], 0x80000000u);           // (sum q saturating at 2^31)
+                    c.qf[j] = (uint8_t)w.qf[j];
+                    c.sl[j] = w.sl[j];
+                    c.se[j] = w.se[j];
+                }
                 Acc a{};
                 a.epoch = P.epoch;
-                merge_state(a, c, key, P.seq0 + c.fb, ref[p]);
+                merge_state(a, c, w.key, P.seq0 + c.fb, ref[p]);
                 const uint4 *src = reinterpret_cast<const uint4 *>(&a);
                 uint4 *dst = reinterpret_cast<uint4 *>(acc + p);
 #pragma unroll
                 for (int t = 0; t < 10; t++) dst[t] = src[t];
             }
         }
-        __syncthreads();
+        if (tpp > 64) __syncthreads();
     }
 }
 
@@ -628,7 +725,7 @@ hipError_t launch_count_list(const MParams &P, const uint8_t *ref, const uint32_
 }
 hipError_t launch_fold_hist(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
                             hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_hist, dim3((unsigned)std::max<int64_t>(1, blocks)), dim3(256), 0, st, P, H, ref, T, acc);
+    hipLaunchKernelGGL(k_fold_hist, dim3((unsigned)std::max<int64_t>(1, blocks)), dim3(1024), 0, st, P, H, ref, T, acc);
     return hipGetLastError();
 }
 
