@@ -62,6 +62,8 @@ def parse():
                     help="HIP events around the accumulate kernel on every K-th timed step")
     ap.add_argument("--e2e-threads", type=int, default=16)
     ap.add_argument("--e2e-bams", type=int, default=4, help="BAMs per end-to-end stream")
+    ap.add_argument("--e2e-many", type=int, default=64,
+                    help="config 4 end to end: 100x SARS-CoV-2 BAM files through process_bams (0 = skip)")
     ap.add_argument("--full-table", action="store_true", help="also accumulate every table GL term")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
                                                       "gloo only to exercise the path on one GPU)")
@@ -584,6 +586,37 @@ def end_to_end(args, device):
     res["simulate_s"] = t_sim
     res["host_threads"] = args.e2e_threads
     os.remove(bam)
+    if args.e2e_many > 0:
+        # BASELINE config 4 from files: many 100x BAMs through LiveVariantCaller.process_bams (plans on a thread
+        # pool, per-BAM batches accumulated in order, counted at prepare_variants)
+        paths = []
+        t0 = time.perf_counter()
+        for i in range(args.e2e_many):
+            pth = os.path.join(d, f"m{i}.bam")
+            simulate_bam(pth, "NC_045512.2", ref, depth=100.0, seed=1000 + i, n_threads=args.e2e_threads)
+            paths.append(pth)
+        t_sim = time.perf_counter() - t0
+        caller = LiveVariantCaller(fasta, 30, 20, 10, 5, 0.10, 1, device=device, max_depth=8000,
+                                   n_threads=args.e2e_threads)
+        caller.process_bams(paths[:4])                # warm-up
+        caller.reset_memory()
+        caller.engine.sync()
+        t0 = time.perf_counter()
+        caller.process_bams(paths)
+        t_in = time.perf_counter() - t0
+        calls = caller.prepare_variants()
+        caller.engine.sync()
+        t1 = time.perf_counter()
+        res["config4_process_bams"] = {
+            "bams": len(paths), "depth": 100, "positions_per_s": len(paths) * L_SARS / (t1 - t0),
+            "s_per_bam": (t1 - t0) / len(paths), "ingest_s": t_in, "prepare_variants_s": t1 - t0 - t_in,
+            "calls": len(calls), "bam_bytes_each": os.path.getsize(paths[0]), "simulate_s": t_sim,
+            "path": "process_bams: host plans on a thread pool -> pinned staging -> per-BAM batches -> "
+                    "counted mode (k_acc_lite_run + k_count_list + k_fold_hist) + sparse finalize"}
+        caller.engine.close()
+        del caller
+        for pth in paths:
+            os.remove(pth)
     os.remove(fasta)
     os.rmdir(d)
     return res

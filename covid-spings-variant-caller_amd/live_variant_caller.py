@@ -231,13 +231,49 @@ class LiveVariantCaller:
             if contig not in bam.references:
                 raise ValueError(f"invalid contig `{contig}`")
             batch = bam.pileup_plan(contig, self.pileup_params)
+        # the entries go straight into pinned staging (double-buffered): the copy to HBM runs on the engine's
+        # copy stream while the next BAM is read
+        self._accumulate_plan(batch, referenceIndex)
+
+    def process_bams(self, inputBams, referenceIndex=0, workers: Optional[int] = None):
+        """vc_queue.py:142-144's loop of process_bam (:54-72) over many BAMs, as one call: the BAMs'
+        pileups are planned on a thread pool (the C++ emulator, outside the GIL; each plan applies its own
+        BAM's depth cap) a few BAMs ahead, and accumulated in the given order — first visits, dict order and
+        history exactly as len(inputBams) process_bam calls.  A calls-only engine counts the whole run at the
+        next prepare_variants (counted mode: k_acc_lite_run + the exact fold of the positions that can call)."""
+        from concurrent.futures import ThreadPoolExecutor
+        paths = list(inputBams)
+        for f in paths:
+            if not os.path.exists(f):
+                raise FileNotFoundError(f"[Errno 2] could not open alignment file `{f}`: No such file or directory")
+        import dataclasses
+        contig = self.fastaFile.references[referenceIndex]
+        workers = workers or max(1, min(8, (os.cpu_count() or 2) // 2))
+        # the host threads split between the concurrent plans
+        params = dataclasses.replace(self.pileup_params, n_threads=max(1, self.pileup_params.n_threads // workers))
+
+        def plan(path):
+            with AlignmentFile(path) as bam:
+                if contig not in bam.references:
+                    raise ValueError(f"invalid contig `{contig}`")
+                return bam.pileup_plan(contig, params)
+
+        window = 2 * workers                  # plans in flight (each holds its BAM's decoded reads)
+        with ThreadPoolExecutor(workers) as ex:
+            pending = [ex.submit(plan, p) for p in paths[:window]]
+            for i in range(len(paths)):
+                batch = pending[i].result()
+                if i + window < len(paths):
+                    pending.append(ex.submit(plan, paths[i + window]))
+                pending[i] = None
+                self._accumulate_plan(batch, referenceIndex)
+
+    def _accumulate_plan(self, batch, referenceIndex):
         with self._lock:
             if batch.n_cols == 0:
                 batch.fill()
                 batch.close()
                 return
-            # the entries go straight into pinned staging (double-buffered): the copy to HBM runs on the
-            # engine's copy stream while the next BAM is read
             codes, quals, offs = self._ingest.buffers(batch.n_entries, batch.n_cols)
             batch.fill(codes, quals)
             offs[:batch.n_cols + 1] = batch.offsets

@@ -185,3 +185,42 @@ def test_pinned_ingest_stream_vs_oracle(planted):
     compare_variants(c.prepare_variants(), _oracle(ref, seq).prepare_variants(), RTOL)
     mem, omem = c.memory, _oracle(ref, seq).memory
     assert list(mem) == list(omem) and all(mem[p] == omem[p] for p in omem)
+
+
+def test_process_bams_equals_sequential_process_bam(tmp_path):
+    """process_bams (the many-BAM ingest: plans on a thread pool, accumulated in order, counted at
+    prepare_variants) == one process_bam per BAM == the oracle, on 7 BAMs whose depth caps bind and whose
+    first visits differ (BAM 3 covers a region no earlier BAM does), then more BAMs after a prepare_variants."""
+    L = 900
+    ref = _ref(L, 31)
+    fasta = str(tmp_path / "ref.fa")
+    samgen.write_fasta(fasta, [("chrS", ref)])
+    snvs = {120: ("T" if ref[120] != "T" else "A", 0.4), 480: ("G" if ref[480] != "G" else "C", 0.25),
+            700: ("C" if ref[700] != "C" else "G", 0.8)}
+    files = []
+    for k in range(9):
+        recs = samgen.snv_records("chrS", ref, 300 + 60 * k, snvs=snvs, seed=300 + k)
+        if k == 3:
+            recs = [r for r in recs if r["pos"] > 500]       # a BAM that starts later: later first visits
+        p = str(tmp_path / f"m{k}.bam")
+        samgen.write_bam(p, [("chrS", L)], recs)
+        samgen.write_sam(str(tmp_path / f"m{k}.sam"), [("chrS", L)], recs)
+        files.append(p)
+    a = _caller(fasta, max_depth=250)
+    b = _caller(fasta, max_depth=250)
+    a.process_bams(files[:7], workers=3)
+    for f in files[:7]:
+        b.process_bam(f)
+    va, vb = a.prepare_variants(), b.prepare_variants()
+    o = _oracle(ref, files[:7], max_depth=250)
+    compare_variants(va, o.prepare_variants(), RTOL)
+    compare_variants(va, vb, 0.0)
+    assert len(va) >= 2
+    a.process_bams(files[7:])
+    for f in files[7:]:
+        b.process_bam(f)
+    va, vb = a.prepare_variants(), b.prepare_variants()
+    compare_variants(va, vb, 0.0)
+    compare_variants(va, _oracle(ref, files, max_depth=250).prepare_variants(), RTOL)
+    mem, omem = a.memory, _oracle(ref, files, max_depth=250).memory
+    assert list(mem) == list(omem) and all(mem[p] == omem[p] for p in omem)
