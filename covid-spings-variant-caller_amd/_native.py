@@ -86,6 +86,8 @@ def gpu_lib():
     _sig(L.spg_host_alloc, i32, C.c_size_t, C.POINTER(vp))
     _sig(L.spg_host_free, i32, vp)
     _sig(L.spg_wait_input, i32, vp)
+    _sig(L.spg_set_history_cap, i32, vp, i64)
+    _sig(L.spg_history_resident, i32, vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64))
     _sig(L.spg_input_ticket, i32, vp, C.POINTER(u64))
     _sig(L.spg_wait_ticket, i32, vp, u64)
     _sig(L.spg_finalize, i32, vp)

@@ -71,37 +71,61 @@ struct HistBatch {
     uint32_t seq0;         // batch_seq of its (first) sample
     int64_t n_samples;     // > 1: a multi-sample column-major batch (spg_accumulate_samples)
     uint32_t *fsamp;       // multi-sample: first sample holding entries, per column (device)
+    int slab = -1;         // owned: the arena slab holding it
+    size_t bytes = 0;      // owned: its bytes there (offsets + both padded arrays)
+    uint8_t *dev0 = nullptr;   // owned: start of its arena block
+    void *host = nullptr;      // spilled to pinned host memory (the descriptors point there, mapped)
 };
 
 // Device arena for the owned batch copies (the replay history): slabs allocated once and bump-
 // allocated per batch, recycled at spg_reset (no hipMalloc / hipFree per batch).  Copies into a
 // recycled slab are ordered after the kernels that read its old content (reset_fence below).
 struct Arena {
-    struct Slab { uint8_t *base; size_t cap, used; };
-    std::vector<Slab> slabs;
+    struct Slab { uint8_t *base; size_t cap, used; int64_t live; };
+    std::vector<Slab> slabs;               // a released slab stays as a tombstone (base null): indices are stable
     size_t cur = 0;
-    hipError_t alloc(size_t n, uint8_t **out) {
+    size_t max_slab = (size_t)8 << 30;     // smaller under a history cap (spilling frees whole slabs)
+    hipError_t alloc(size_t n, uint8_t **out, int *slab) {
         n = (n + 255) & ~size_t(255);
         while (cur < slabs.size()) {
             Slab &s = slabs[cur];
-            if (s.cap - s.used >= n) { *out = s.base + s.used; s.used += n; return hipSuccess; }
+            if (s.base && s.cap - s.used >= n) {
+                *out = s.base + s.used; s.used += n; s.live++; *slab = (int)cur;
+                return hipSuccess;
+            }
             cur++;
         }
-        // geometric slabs: 256 MiB, 512 MiB, 1 GiB, ... 8 GiB
-        size_t cap = (size_t)256 << 20;
-        for (size_t i = 0; i < slabs.size() && cap < ((size_t)8 << 30); i++) cap <<= 1;
-        cap = std::max(cap, n);
-        Slab s{nullptr, cap, 0};
+        // geometric slabs: 256 MiB, 512 MiB, 1 GiB, ... max_slab
+        size_t cap = std::min((size_t)256 << 20, max_slab);
+        for (size_t i = 0; i < slabs.size() && cap < max_slab; i++) cap <<= 1;
+        cap = std::max(std::min(cap, max_slab), n);
+        Slab s{nullptr, cap, 0, 0};
         hipError_t e = hipMalloc(&s.base, cap);
         if (e != hipSuccess) return e;
         slabs.push_back(s);
         cur = slabs.size() - 1;
         slabs[cur].used = n;
+        slabs[cur].live = 1;
         *out = s.base;
+        *slab = (int)cur;
         return hipSuccess;
     }
-    void recycle() { for (auto &s : slabs) s.used = 0; cur = 0; }
-    void release() { for (auto &s : slabs) (void)hipFree(s.base); slabs.clear(); cur = 0; }
+    void recycle() {
+        for (auto &s : slabs) { s.used = 0; s.live = 0; }
+        cur = 0;
+    }
+    void release() {
+        for (auto &s : slabs)
+            if (s.base) (void)hipFree(s.base);
+        slabs.clear();
+        cur = 0;
+    }
+    size_t bytes() const {
+        size_t n = 0;
+        for (auto &s : slabs)
+            if (s.base) n += s.cap;
+        return n;
+    }
 };
 
 struct spg_ctx {
@@ -152,6 +176,10 @@ struct spg_ctx {
     int64_t count_end = 0;
     int64_t n_deep_hist = 0;            // deep / multi-sample batches since reset (counted mode needs none)
     uint32_t *cdep = nullptr, *cmcf = nullptr;
+    // bounded history: owned batches past `hist_cap` bytes of HBM are spilled, oldest folded first
+    int64_t hist_cap = 0;               // 0 = no cap
+    int64_t hist_dev_bytes = 0;         // owned history bytes resident in HBM
+    int64_t n_spilled = 0;
     MState *part = nullptr;             // split-run partial states
     size_t part_bytes = 0;
     // replay index: history batches per 2^RIDX_SHIFT-position bucket
@@ -259,6 +287,11 @@ int spg_create(int device, int64_t n_pos, const spg_params *p, spg_ctx **out) {
     if (hipSetDevice(device) != hipSuccess) return bail(fail("spg_create: hipSetDevice failed"));
     if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->n_cu <= 0)
         c->n_cu = 256;
+    if (const char *e = getenv("SPG_HIST_CAP")) {          // bytes of owned history kept in HBM (0 = no cap)
+        c->hist_cap = atoll(e);
+        if (c->hist_cap > 0)
+            c->arena.max_slab = std::max<size_t>((size_t)16 << 20, std::min<size_t>((size_t)8 << 30, (size_t)c->hist_cap / 4));
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail("spg_create: stream"));
@@ -281,8 +314,11 @@ int spg_create(int device, int64_t n_pos, const spg_params *p, spg_ctx **out) {
     return 0;
 }
 
+static void free_spilled(spg_ctx *c);
 static void clear_history(spg_ctx *c) {
+    free_spilled(c);
     c->hist.clear();
+    c->hist_dev_bytes = 0;
     c->arena.recycle();
     c->pend0 = 0;
     c->pend_entries = 0;
@@ -297,6 +333,7 @@ int spg_destroy(spg_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    free_spilled(c);
     c->arena.release();
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
@@ -842,6 +879,86 @@ static bool is_pinned(const void *p) {
 
 // One batch: validation, its history copy (arena) or borrowed device buffers, descriptors, bucket
 // index; a deep batch is accumulated right away, a shallow one joins the pending run.
+// ---- bounded history ------------------------------------------------------------------
+// Owned batches live in the device arena so that the exact replay, the counted mode's exact fold and a
+// re-materialization can read them.  Past the cap, the oldest batches whose entries are already folded (into
+// the records, or into the counted totals) move to pinned host memory: their descriptors then point at the
+// mapped host copy, so those rare readers stream the few columns they need over PCIe, and a slab whose
+// batches have all moved is freed.
+static int count_pending(spg_ctx *c);
+
+static int spill_batch(spg_ctx *c, int64_t i) {
+    HistBatch &b = c->hist[(size_t)i];
+    void *h = nullptr;
+    HIPCHK(hipHostMalloc(&h, b.bytes, hipHostMallocMapped));
+    void *hd = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&hd, h, 0));
+    // after every kernel enqueued so far (some may read the batch), before any later one
+    if (int rc = wait_copies(c)) return rc;
+    HIPCHK(hipMemcpyAsync(h, b.dev0, b.bytes, hipMemcpyDeviceToHost, c->stream));
+    uint8_t *d = (uint8_t *)hd;
+    b.code = d + (b.code - b.dev0);
+    b.qual = d + (b.qual - b.dev0);
+    b.off = reinterpret_cast<uint64_t *>(d + ((uint8_t *)b.off - b.dev0));
+    b.host = h;
+    // the pinned descriptor mirror: an upload still queued may read it (it would pick up the new pointers
+    // before the copy above ran)
+    if (c->hist_up) HIPCHK(hipEventSynchronize(c->hist_ev));
+    c->h_hist[i] = Hist{b.pos_begin, b.n_cols, b.off, b.code, b.qual};
+    HIPCHK(hipMemcpyAsync(c->d_hist + i, c->h_hist + i, sizeof(Hist), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipEventRecord(c->hist_ev, c->stream));
+    c->hist_up = true;
+    c->hist_dev_bytes -= (int64_t)b.bytes;
+    c->n_spilled++;
+    Arena::Slab &sl = c->arena.slabs[(size_t)b.slab];
+    if (--sl.live == 0 && (size_t)b.slab != c->arena.cur) {
+        HIPCHK(hipStreamSynchronize(c->stream));      // the copies out of it have run
+        HIPCHK(hipFree(sl.base));
+        sl.base = nullptr;
+        sl.cap = sl.used = 0;
+    }
+    b.dev0 = nullptr;
+    return 0;
+}
+
+static int enforce_history_cap(spg_ctx *c) {
+    if (c->hist_cap <= 0 || c->hist_dev_bytes <= c->hist_cap) return 0;
+    // batches [0, folded) are in the records / the counted totals
+    int64_t folded = c->counted ? c->count_end : c->pend0;
+    const int64_t nh = (int64_t)c->hist.size();
+    int64_t movable = 0;
+    for (int64_t i = 0; i < folded; i++)
+        if (c->hist[(size_t)i].dev0 && c->hist[(size_t)i].n_samples == 1) movable += (int64_t)c->hist[(size_t)i].bytes;
+    if (c->hist_dev_bytes - movable > c->hist_cap && nh > folded) {
+        // fold the pending batches first (all but the newest: it stays pending for the next finalize)
+        const bool can_count = (c->p.flags & SPG_P_CALLS_ONLY) && c->n_deep_hist == 0 && !c->deep_pend &&
+                               (c->counted || (c->pend0 == 0 && !c->stale));
+        if (can_count) {
+            if (int rc = count_pending(c)) return rc;
+            folded = c->count_end;
+        } else {
+            if (int rc = materialize(c)) return rc;
+            if (int rc = flush_run(c)) return rc;
+            folded = c->pend0;
+        }
+    }
+    for (int64_t i = 0; i < folded && c->hist_dev_bytes > c->hist_cap; i++) {
+        const HistBatch &b = c->hist[(size_t)i];
+        if (!b.dev0 || b.n_samples != 1) continue;
+        if (int rc = spill_batch(c, i)) return rc;
+    }
+    return 0;
+}
+
+static void free_spilled(spg_ctx *c) {
+    bool any = false;
+    for (auto &b : c->hist) any |= b.host != nullptr;
+    if (!any) return;
+    (void)hipStreamSynchronize(c->stream);             // kernels reading the mapped copies are done
+    for (auto &b : c->hist)
+        if (b.host) { (void)hipHostFree(b.host); b.host = nullptr; }
+}
+
 static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
                      const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags,
                      bool *pageable_copy, int64_t n_samples = 1, const uint32_t *first_sample = nullptr) {
@@ -892,7 +1009,10 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
             HIPCHK(hipStreamWaitEvent(c->copy_stream, c->compute_ev, 0));
             c->arena_fence = false;
         }
-        HIPCHK(c->arena.alloc(sizeof(uint64_t) * (n_cols + 1) + 2 * pad, &m));
+        hb.bytes = sizeof(uint64_t) * (n_cols + 1) + 2 * pad;
+        HIPCHK(c->arena.alloc(hb.bytes, &m, &hb.slab));
+        hb.dev0 = m;
+        c->hist_dev_bytes += (int64_t)hb.bytes;
         hb.code = m;
         hb.qual = m + pad;
         hb.off = reinterpret_cast<uint64_t *>(m + 2 * pad);
@@ -907,7 +1027,8 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
         HIPCHK(hipMemsetAsync(hb.qual + n_entries, 0, pad - n_entries, cs));
         if (first_sample) {
             uint8_t *fs = nullptr;
-            HIPCHK(c->arena.alloc(sizeof(uint32_t) * n_cols, &fs));
+            int fslab = -1;
+            HIPCHK(c->arena.alloc(sizeof(uint32_t) * n_cols, &fs, &fslab));
             hb.fsamp = reinterpret_cast<uint32_t *>(fs);
             HIPCHK(hipMemcpyAsync(hb.fsamp, first_sample, sizeof(uint32_t) * n_cols, k, cs));
         }
@@ -954,8 +1075,9 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
     c->pend_entries += n_entries;
     // (calls-only: the pending run waits for the finalize, which counts it — see finalize_counted)
     static const int64_t run_max = env_i64("SPG_RUN_MAX", 4096);
-    if (!(c->p.flags & SPG_P_CALLS_ONLY) && (int64_t)c->hist.size() - c->pend0 >= run_max) return flush_run(c);
-    return 0;
+    if (!(c->p.flags & SPG_P_CALLS_ONLY) && (int64_t)c->hist.size() - c->pend0 >= run_max)
+        if (int rc = flush_run(c)) return rc;
+    return enforce_history_cap(c);
 }
 
 static int accumulate_many(spg_ctx *c, const spg_batch *b, int64_t n, uint32_t flags) {
@@ -1111,7 +1233,7 @@ static FParams make_fparams(spg_ctx *c) {
 // pass prepare_variants' filters (k_count_list), build their records exactly from the whole history
 // (k_fold_hist); the sparse finalize then decides them.  The other records stay stale (materialize() re-folds
 // the history if anything reads them).
-static int finalize_counted(spg_ctx *c) {
+static int count_pending(spg_ctx *c) {
     const int64_t nh = (int64_t)c->hist.size();
     if (!c->counted) {
         if (!c->cdep) {
@@ -1123,40 +1245,29 @@ static int finalize_counted(spg_ctx *c) {
         c->count_end = 0;
     }
     const int64_t h0 = c->count_end;
-    int64_t ua = INT64_MAX, ub = INT64_MIN;            // positions of the whole history (listing)
-    int64_t u0 = INT64_MAX, u1 = INT64_MIN;            // ... and of the batches counted now
+    int64_t u0 = INT64_MAX, u1 = INT64_MIN;            // positions of the batches counted now
     uint64_t run_entries = 0;
-    for (int64_t i = 0; i < nh; i++) {
+    for (int64_t i = h0; i < nh; i++) {
         const HistBatch &b = c->hist[(size_t)i];
-        ua = std::min(ua, b.pos_begin);
-        ub = std::max(ub, b.pos_begin + b.n_cols);
-        if (i >= h0) {
-            u0 = std::min(u0, b.pos_begin);
-            u1 = std::max(u1, b.pos_begin + b.n_cols);
-            run_entries += b.n_entries;
-        }
+        u0 = std::min(u0, b.pos_begin);
+        u1 = std::max(u1, b.pos_begin + b.n_cols);
+        run_entries += b.n_entries;
     }
     if (int rc = wait_copies(c)) return rc;
     if (int rc = acc_begin(c)) return rc;
     // descriptors of every batch not uploaded yet (pinned mirror -> device table)
     const int64_t up0 = std::min(h0, c->pend0);
     if (nh > up0) {
+        if (c->hist_fence) { HIPCHK(hipEventSynchronize(c->hist_ev)); c->hist_fence = false; }
         HIPCHK(hipMemcpyAsync(c->d_hist + up0, c->h_hist + up0, sizeof(Hist) * (nh - up0), hipMemcpyHostToDevice, c->stream));
         HIPCHK(hipEventRecord(c->hist_ev, c->stream));
         c->hist_up = true;
     }
-    MParams P{};
-    fill_swar(c, P.min_bq, P.qlo, P.kpass, P.kok);
-    P.epoch = c->epoch;
-    P.calls_only = 1u;
-    P.min_td = c->p.min_total_depth;
-    P.min_ad = c->p.min_allele_depth;
-    P.ratio_lo = c->p.min_evidence_ratio * (1.0 - 1e-9);
-    P.list = c->band;
-    P.n_list = c->nlist;
     if (nh > h0) {
         // one wave per (tile, batch split): LPC lanes per column so that a tile's bytes of one batch fit the
         // 3 KiB slot; splits until the items fill the resident grid twice over
+        MParams P{};
+        fill_swar(c, P.min_bq, P.qlo, P.kpass, P.kok);
         const int64_t K = nh - h0, L = u1 - u0;
         const double mean = (double)run_entries / ((double)K * (double)std::max<int64_t>(1, L));
         int lpc = 1;
@@ -1179,6 +1290,35 @@ static int finalize_counted(spg_ctx *c) {
     c->counted = true;
     c->pend0 = nh;
     c->pend_entries = 0;
+    c->stale = true;                   // records of history [0, nh) are not written
+    c->stale_end = nh;
+    return acc_end(c);
+}
+
+// Counted mode (a calls-only finalize of a sample of shallow batches, e.g. one process_bam per BAM): count the
+// batches not counted yet into the per-position totals (k_acc_lite_run), list the positions whose totals can
+// pass prepare_variants' filters (k_count_list), build their records exactly from the whole history
+// (k_fold_hist); the sparse finalize then decides them.  The other records stay stale (materialize() re-folds
+// the history if anything reads them).
+static int finalize_counted(spg_ctx *c) {
+    if (int rc = count_pending(c)) return rc;
+    const int64_t nh = (int64_t)c->hist.size();
+    int64_t ua = INT64_MAX, ub = INT64_MIN;            // positions of the whole history (listing)
+    for (int64_t i = 0; i < nh; i++) {
+        const HistBatch &b = c->hist[(size_t)i];
+        ua = std::min(ua, b.pos_begin);
+        ub = std::max(ub, b.pos_begin + b.n_cols);
+    }
+    if (int rc = acc_begin(c)) return rc;
+    MParams P{};
+    fill_swar(c, P.min_bq, P.qlo, P.kpass, P.kok);
+    P.epoch = c->epoch;
+    P.calls_only = 1u;
+    P.min_td = c->p.min_total_depth;
+    P.min_ad = c->p.min_allele_depth;
+    P.ratio_lo = c->p.min_evidence_ratio * (1.0 - 1e-9);
+    P.list = c->band;
+    P.n_list = c->nlist;
     // list, then the exact records of the listed positions over the whole history
     HIPCHK(hipMemsetAsync(c->nlist, 0, sizeof(uint32_t), c->stream));
     P.u0 = ua;
@@ -1189,8 +1329,6 @@ static int finalize_counted(spg_ctx *c) {
     P.seq0 = c->hist[0].seq0;
     HIPCHK(launch_fold_hist(P, c->d_hist, c->ref, c->tables, c->acc, 4 * (int64_t)c->n_cu, c->stream));
     if (int rc = trace_sync(c, "accumulate (k_fold_hist)")) return rc;
-    c->stale = true;
-    c->stale_end = nh;
     return acc_end(c);
 }
 
@@ -1461,15 +1599,38 @@ int spg_history_info(spg_ctx *c, int64_t i, int64_t *pos_begin, int64_t *n_cols,
     return 0;
 }
 
+int spg_set_history_cap(spg_ctx *c, int64_t bytes) {
+    if (!c || bytes < 0) return fail("spg_set_history_cap: bad argument");
+    HIPCHK(hipSetDevice(c->device));
+    c->hist_cap = bytes;
+    // spilling frees whole slabs: keep them a fraction of the cap
+    c->arena.max_slab = bytes ? std::max<size_t>((size_t)16 << 20, std::min<size_t>((size_t)8 << 30, (size_t)bytes / 4))
+                              : (size_t)8 << 30;
+    return enforce_history_cap(c);
+}
+
+int spg_history_resident(spg_ctx *c, int64_t *device_bytes, int64_t *n_spilled, int64_t *arena_bytes) {
+    if (!c) return fail("spg_history_resident: null ctx");
+    if (device_bytes) *device_bytes = c->hist_dev_bytes;
+    if (n_spilled) {
+        int64_t n = 0;
+        for (auto &b : c->hist) n += b.host != nullptr;
+        *n_spilled = n;
+    }
+    if (arena_bytes) *arena_bytes = (int64_t)c->arena.bytes();
+    return 0;
+}
+
 int spg_history_copy(spg_ctx *c, int64_t i, uint64_t *offsets, uint8_t *base_code, uint8_t *qual) {
     if (!c) return fail("spg_history_copy: null ctx");
     if (i < 0 || i >= (int64_t)c->hist.size()) return fail("spg_history_copy: batch index out of range");
     HIPCHK(hipSetDevice(c->device));
     if (int rc = wait_copies(c)) return rc;
     const HistBatch &h = c->hist[(size_t)i];
-    if (offsets) HIPCHK(hipMemcpyAsync(offsets, h.off, sizeof(uint64_t) * (h.n_cols + 1), hipMemcpyDeviceToHost, c->stream));
-    if (base_code && h.n_entries) HIPCHK(hipMemcpyAsync(base_code, h.code, h.n_entries, hipMemcpyDeviceToHost, c->stream));
-    if (qual && h.n_entries) HIPCHK(hipMemcpyAsync(qual, h.qual, h.n_entries, hipMemcpyDeviceToHost, c->stream));
+    // (hipMemcpyDefault: a spilled batch is in pinned host memory)
+    if (offsets) HIPCHK(hipMemcpyAsync(offsets, h.off, sizeof(uint64_t) * (h.n_cols + 1), hipMemcpyDefault, c->stream));
+    if (base_code && h.n_entries) HIPCHK(hipMemcpyAsync(base_code, h.code, h.n_entries, hipMemcpyDefault, c->stream));
+    if (qual && h.n_entries) HIPCHK(hipMemcpyAsync(qual, h.qual, h.n_entries, hipMemcpyDefault, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }

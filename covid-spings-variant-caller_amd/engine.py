@@ -189,6 +189,19 @@ class PileupEngine:
         with self._lock:
             N.check(self._L.spg_wait_input(self._h), "spg_wait_input")
 
+    def set_history_cap(self, nbytes: int):
+        """Bound the HBM the engine's own batch copies (the replay history) may hold: past it, the oldest
+        folded batches move to pinned host memory (spg_set_history_cap; 0 = no cap)."""
+        with self._lock:
+            N.check(self._L.spg_set_history_cap(self._h, int(nbytes)), "spg_set_history_cap")
+
+    def history_resident(self):
+        """(owned history bytes in HBM, batches spilled to host, arena bytes allocated)."""
+        a, b, d = C.c_int64(), C.c_int64(), C.c_int64()
+        with self._lock:
+            N.check(self._L.spg_history_resident(self._h, C.byref(a), C.byref(b), C.byref(d)), "spg_history_resident")
+        return a.value, b.value, d.value
+
     def input_ticket(self) -> int:
         """Ticket of the latest host-input batch copy enqueued (spg_input_ticket)."""
         t = C.c_uint64()

@@ -292,13 +292,18 @@ class LiveVariantCaller:
 
     # -- checkpoint ---------------------------------------------------------------------------
     def create_checkpoint(self, filename):
-        """:40-45 — the accumulated batches (exact engine state), numpy .npz."""
+        """:40-45 — the accumulated batches (exact engine state), numpy .npz.  Like the reference's pickled
+        `memory`, which holds only the base qualities that passed the filter (:96-103), each batch keeps only
+        its entries with q >= minBaseQuality — plus, for a column whose every entry fails it, its first entry,
+        so that the position's first visit (:77-85) survives the round trip."""
         log.info("Creating checkpoint %s", filename)
         with self._lock:
             hist = self.engine.history()
             arrays = {"contig": np.array(self._batch_contig, np.int64),
-                      "names": np.array(self.fastaFile.references)}
+                      "names": np.array(self.fastaFile.references),
+                      "min_base_quality": np.int64(self.minBaseQuality)}
             for i, (pb, off, codes, quals) in enumerate(hist):
+                off, codes, quals = _bq_compact(off, codes, quals, self.minBaseQuality)
                 arrays[f"b{i}_pos"] = np.int64(pb)
                 arrays[f"b{i}_off"] = off
                 arrays[f"b{i}_codes"] = codes
@@ -350,6 +355,25 @@ INFO_META = [
                            "defined precisely as the GL field)"),
     ("SCORE", "1", "Float", "Custom scoring function"),
 ]
+
+
+def _bq_compact(off, codes, quals, min_bq: int):
+    """A CSR batch without the entries the base-quality filter drops (:96-103 never sees them); a column whose
+    every entry is dropped keeps its first one (its q < min_bq: the engine filters it again), which records the
+    position's first visit (:77-85)."""
+    off = np.asarray(off, np.uint64)
+    if min_bq <= 0 or len(codes) == 0:
+        return off, codes, quals
+    lens = np.diff(off.astype(np.int64))
+    col = np.repeat(np.arange(len(lens), dtype=np.int64), lens)
+    keep = quals >= min_bq
+    kept = np.bincount(col[keep], minlength=len(lens))
+    marker = (lens > 0) & (kept == 0)
+    keep[off[:-1][marker].astype(np.int64)] = True
+    new_lens = np.bincount(col[keep], minlength=len(lens))
+    new_off = np.zeros(len(off), np.uint64)
+    np.cumsum(new_lens, out=new_off[1:])
+    return new_off, np.ascontiguousarray(codes[keep]), np.ascontiguousarray(quals[keep])
 
 
 def _hval(v: str) -> str:

@@ -207,6 +207,16 @@ int spg_device_results(spg_ctx *ctx, void **candidates, void **n_candidates);
  * order a consumer on another stream (e.g. an RCCL gather) after it through spg_stream. */
 int spg_copy_candidates_device(spg_ctx *ctx, void *dst, int64_t cap);
 
+/* Bound the HBM held by the context's own copies of accumulated batches (the replay history; borrowed
+ * batches are the caller's).  Past `bytes`, the oldest batches already folded into the records (or, calls-only,
+ * into the counted totals) move to pinned host memory; the rare readers (exact replay, the exact fold of the
+ * positions that may call, re-materialization) read them there over PCIe.  0 = no cap (default; env
+ * SPG_HIST_CAP sets it at spg_create).  Replaces nothing in the reference: its `memory` grows in host RAM
+ * (live_variant_caller.py:100-103); this keeps the engine from being the first thing to run out. */
+int spg_set_history_cap(spg_ctx *ctx, int64_t bytes);
+/* Owned history bytes resident in HBM, batches spilled to host, arena bytes allocated (any may be NULL). */
+int spg_history_resident(spg_ctx *ctx, int64_t *device_bytes, int64_t *n_spilled, int64_t *arena_bytes);
+
 /* The accumulated batches (replay history) since the last spg_reset, in accumulate order: the
  * exact state behind LiveVariantCaller.memory, used for create_checkpoint (:40-45) and the
  * memory view.  spg_history_copy copies batch i to host buffers (offsets n_cols+1, base_code /

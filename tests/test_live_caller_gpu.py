@@ -120,7 +120,9 @@ def test_checkpoint_roundtrip(planted):
     b.load_checkpoint(ck)
     b.process_bam(files[1])                      # resume: live mode (vc_queue.py:134-144)
     a.process_bam(files[1])
-    compare_variants(b.prepare_variants(), a.prepare_variants(), 0.0)
+    # (a's records were materialized for its checkpoint and take the next BAM through the record path; b counts
+    # both at prepare_variants: fp64 sums added in different orders, equal within the oracle tolerance)
+    compare_variants(b.prepare_variants(), a.prepare_variants(), RTOL)
     # and against the oracle chain that never checkpointed: calls and the memory view after resume
     o = _oracle(ref, files)
     compare_variants(b.prepare_variants(), o.prepare_variants(), RTOL)
