@@ -86,6 +86,17 @@ def gpu_lib():
     _sig(L.spg_host_alloc, i32, C.c_size_t, C.POINTER(vp))
     _sig(L.spg_host_free, i32, vp)
     _sig(L.spg_wait_input, i32, vp)
+    _sig(L.spg_multi_create, i32, C.POINTER(C.c_int), i32, i64, C.POINTER(SpgParams), C.POINTER(vp))
+    _sig(L.spg_multi_destroy, i32, vp)
+    _sig(L.spg_multi_last_error, C.c_char_p)
+    _sig(L.spg_multi_set_eps_lut, i32, vp, vp)
+    _sig(L.spg_multi_set_reference, i32, vp, C.c_char_p, i64)
+    _sig(L.spg_multi_reset, i32, vp)
+    _sig(L.spg_multi_accumulate, i32, vp, i64, i64, vp, vp, vp, u64, C.c_uint32)
+    _sig(L.spg_multi_finalize, i32, vp)
+    _sig(L.spg_multi_get_candidates, i32, vp, vp, i64, C.POINTER(i64))
+    _sig(L.spg_multi_partition, i32, vp, C.POINTER(i64))
+    _sig(L.spg_multi_context, i32, vp, i32, C.POINTER(vp))
     _sig(L.spg_set_history_cap, i32, vp, i64)
     _sig(L.spg_history_resident, i32, vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64))
     _sig(L.spg_input_ticket, i32, vp, C.POINTER(u64))

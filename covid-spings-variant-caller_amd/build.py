@@ -21,7 +21,7 @@ LIBDIR = os.path.join(PKG, "_lib")
 INC = os.path.join(ROOT, "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-GPU_SOURCES = ["spg_kernels.hip", "spg_tile.hip", "spg_lite.hip", "spg_api.cpp"]
+GPU_SOURCES = ["spg_kernels.hip", "spg_tile.hip", "spg_lite.hip", "spg_api.cpp", "spg_multi.cpp"]
 GPU_HEADERS = ["spg_device.h", "spg_common.h"]
 PILEUP_SOURCES = ["spp_pileup.cpp"]
 
@@ -48,7 +48,7 @@ def build_gpu(force=False, verbose=False) -> str:
         # (-z defs: a kernel launcher the C-ABI declares but no source defines fails the build, not the load)
         cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wl,-z,defs", f"-I{INC}", "-o", out + ".tmp",
                "-Rpass-analysis=kernel-resource-usage"]
-        cmd += [os.path.join(CSRC, f) for f in GPU_SOURCES]
+        cmd += [os.path.join(CSRC, f) for f in GPU_SOURCES] + ["-lrccl"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = _run(cmd)

@@ -245,6 +245,30 @@ size_t spg_sizeof_candidate(void);
 size_t spg_sizeof_detail(void);
 size_t spg_sizeof_acc(void);
 
+/* ---- one process, N devices (SURVEY §8 b/e; shard.py's ShardedEngine without torch) ----------------------
+ * Each device's context owns a contiguous coordinate range, cut on the first batch of a sample (equal entries)
+ * and kept until reset; host batches are sliced at the cuts (a device with an empty slice gets an empty batch, so
+ * batch numbers and first visits stay global); the compact call tables come back to devices[0] with ONE RCCL
+ * ncclGather over xGMI and are merged in memory order (first_batch, pos, allele rank).  Replaces the
+ * reference's single-process loop (live_variant_caller.py:54-185) for multi-GPU hosts. */
+typedef struct spg_multi spg_multi;
+int spg_multi_create(const int *devices, int n, int64_t n_pos, const spg_params *params, spg_multi **out);
+int spg_multi_destroy(spg_multi *m);
+const char *spg_multi_last_error(void);
+int spg_multi_set_eps_lut(spg_multi *m, const double lut[256]);
+int spg_multi_set_reference(spg_multi *m, const char *seq, int64_t len);
+int spg_multi_reset(spg_multi *m);
+/* Host CSR batch, as spg_accumulate (SPG_IN_TRUSTED allowed; no device / borrowed input). */
+int spg_multi_accumulate(spg_multi *m, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
+                         const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags);
+int spg_multi_finalize(spg_multi *m);
+/* The merged call table (needs n_out <= cap; *n_out is set either way). */
+int spg_multi_get_candidates(spg_multi *m, spg_candidate *out, int64_t cap, int64_t *n_out);
+/* cuts[0..n]: device i owns positions [cuts[i], cuts[i+1]) (after the sample's first batch). */
+int spg_multi_partition(spg_multi *m, int64_t *cuts);
+/* The context of device index i (spg_* calls on it: table, details, timing). */
+int spg_multi_context(spg_multi *m, int i, spg_ctx **ctx);
+
 #ifdef __cplusplus
 }
 #endif

@@ -86,3 +86,10 @@ def test_hot_kernels_do_not_spill_to_scratch():
     assert all(v.get("scratch", 0) == 0 for v in hot.values()), {k: v for k, v in hot.items() if v.get("scratch")}
     deep = [v for k, v in hot.items() if k.startswith("spg::k_acc_seg<4, true, 4")]
     assert deep and all(v["waves_per_simd"] >= 4 for v in deep), deep
+
+
+def test_python_modules_import():
+    """Every package module imports on a CPU host (no GPU calls at import)."""
+    import importlib
+    for m in ("engine", "live_variant_caller", "multi", "shard", "pileup", "synth"):
+        importlib.import_module(f"covid_spings_variant_caller_amd.{m}")
