@@ -1270,9 +1270,13 @@ static int count_pending(spg_ctx *c) {
         fill_swar(c, P.min_bq, P.qlo, P.kpass, P.kok);
         const int64_t K = nh - h0, L = u1 - u0;
         const double mean = (double)run_entries / ((double)K * (double)std::max<int64_t>(1, L));
+        // (LPC 2 stages 4 KiB per array: up to ~3,500 B of a batch per 32-column tile)
+        static const int64_t force_lpc = env_i64("SPG_RUN_LPC", 0);
         int lpc = 1;
-        while (lpc < 8 && (64.0 / lpc) * mean > 2200.0) lpc *= 2;
-        const int64_t tc = 64 / lpc, n_tiles = (L + tc - 1) / tc;
+        while (lpc < 8 && (64.0 / lpc) * mean > (lpc == 2 ? 3500.0 : 2200.0)) lpc *= 2;
+        if (force_lpc == 1 || force_lpc == 2 || force_lpc == 4 || force_lpc == 8) lpc = (int)force_lpc;
+        if (force_lpc == 7) lpc = 0;                   // (A/B: one lane per column, 7 KiB slots)
+        const int64_t tc = lpc ? 64 / lpc : 64, n_tiles = (L + tc - 1) / tc;
         const int64_t blocks = (int64_t)c->n_cu * count_run_blocks_per_cu(lpc);
         const int64_t want_items = 2 * blocks * 4;
         const int64_t S = std::min<int64_t>(K, std::max<int64_t>(1, (want_items + n_tiles - 1) / n_tiles));

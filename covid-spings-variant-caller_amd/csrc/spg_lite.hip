@@ -359,8 +359,9 @@ struct RMeta {             // a unit's values the counting needs (resolved at is
     int64_t pos_begin, n_cols;
     bool nonempty;
 };
+template <int NCH>
 struct RData {             // its staged chunks
-    u32x4 c[LCH], q[LCH];
+    u32x4 c[NCH], q[NCH];
     RMeta m;
 };
 struct RHead {             // the lane's column bounds in the unit's batch (ping-pong, one unit ahead); low
@@ -369,12 +370,13 @@ struct RHead {             // the lane's column bounds in the unit's batch (ping
 
 // items = (tile of 64 / LPC columns, batch split); a wave streams its item's batches through the LDS slot,
 // LPC lanes per column taking the column's 16-B blocks round-robin
-template <int LPC>
+template <int LPC, int NCH>
 __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_acc_lite_run(
     MParams P, const Hist *__restrict__ H, const uint8_t *__restrict__ ref, uint32_t *__restrict__ cdep,
     uint32_t *__restrict__ cmcf) {
     constexpr int TC = 64 / LPC;
-    __shared__ __attribute__((aligned(16))) uint8_t slots[LW][2][LSLOT];
+    constexpr int RSLOT = 1024 * NCH, RNBLK = RSLOT / 16;   // NCH 1 KiB chunks per array per unit
+    __shared__ __attribute__((aligned(16))) uint8_t slots[LW][2][RSLOT];
     const int lane = threadIdx.x & 63, sub = lane % LPC, cl = lane / LPC;
     uint8_t *const sc = slots[threadIdx.x >> 6][0];
     uint8_t *const sq = slots[threadIdx.x >> 6][1];
@@ -400,11 +402,11 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
             const int64_t cB = min(max(t1 - h.pos_begin, (int64_t)0), h.n_cols);
             return RUnit{h.off, h.code, h.qual, h.pos_begin, h.n_cols, gbl(h.off)[cA], gbl(h.off)[cB]};
         };
-        auto issue = [&](int32_t k, const RUnit &U, RData &D) {
+        auto issue = [&](int32_t k, const RUnit &U, RData<NCH> &D) {
             const uint64_t base = U.b & ~(uint64_t)15;
             const uint64_t span = k < k1 ? U.e - base : 0;
 #pragma unroll
-            for (int c = 0; c < LCH; c++) {
+            for (int c = 0; c < NCH; c++) {
                 const uint32_t o = 1024u * c + 16u * lane;
                 const uint64_t a = o < span ? base + o : base;
                 D.c[c] = __builtin_nontemporal_load(gbl(reinterpret_cast<const u32x4 *>(U.code + a)));
@@ -418,9 +420,9 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
             return RHead{gbl(reinterpret_cast<const uint32_t *>(h.off + cc))[0],
                          gbl(reinterpret_cast<const uint32_t *>(h.off + cc + 1))[0]};
         };
-        auto stage = [&](const RData &D) {
+        auto stage = [&](const RData<NCH> &D) {
 #pragma unroll
-            for (int c = 0; c < LCH; c++) {
+            for (int c = 0; c < NCH; c++) {
                 *reinterpret_cast<u32x4 *>(sc + 1024 * c + 16 * lane) = D.c[c];
                 *reinterpret_cast<u32x4 *>(sq + 1024 * c + 16 * lane) = D.q[c];
             }
@@ -446,19 +448,19 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
             };
             // this lane's blocks of the column: j0 + sub, j0 + sub + LPC, ... (slot, then memory past it)
             const uint32_t j0 = brel >> 4, j1 = len ? (brel + len + 15u) >> 4 : j0;
-            const uint32_t jl = min(j1, (uint32_t)LNBLK);
+            const uint32_t jl = min(j1, (uint32_t)RNBLK);
             const uint32_t nl = jl > j0 + (uint32_t)sub ? (jl - j0 - (uint32_t)sub + LPC - 1) / LPC : 0u;
             const uint32_t mx = wave_max_u32(nl);
-            const int32_t vlen = (int32_t)min(len, (uint32_t)LSLOT - min(brel, (uint32_t)LSLOT));
+            const int32_t vlen = (int32_t)min(len, (uint32_t)RSLOT - min(brel, (uint32_t)RSLOT));
             for (uint32_t t = 0; t < mx; t++) {
                 const uint32_t jj = j0 + (uint32_t)sub + LPC * t;
-                const uint32_t j = min(jj, (uint32_t)LNBLK - 1u);
+                const uint32_t j = min(jj, (uint32_t)RNBLK - 1u);
                 const u32x4 cw = *reinterpret_cast<const u32x4 *>(sc + 16u * j);
                 const u32x4 qw = *reinterpret_cast<const u32x4 *>(sq + 16u * j);
                 count(cw, qw, (int32_t)(16u * jj) - (int32_t)brel, vlen);
             }
-            if (__ballot(j1 > (uint32_t)LNBLK)) {
-                const uint32_t b0 = max(j0 + (uint32_t)sub, (uint32_t)LNBLK);
+            if (__ballot(j1 > (uint32_t)RNBLK)) {
+                const uint32_t b0 = max(j0 + (uint32_t)sub, (uint32_t)RNBLK);
                 const uint32_t f0 = j0 + (uint32_t)sub + ((b0 - (j0 + (uint32_t)sub) + LPC - 1) / LPC) * LPC;
                 for (uint32_t j = f0;; j += LPC) {
                     const bool more = j < j1;
@@ -475,7 +477,7 @@ __global__ __launch_bounds__(64 * LW) __attribute__((amdgpu_waves_per_eu(3, 8)))
         // the pipeline over the item's batches (as k_acc_lite's over tiles: two units in flight, their ranges two
         // further ahead, the lanes' column bounds one ahead; every pair alternates)
         RUnit B0 = unit(k0), B1 = unit(k0 + 1);
-        RData A, B;
+        RData<NCH> A, B;
         issue(k0, B0, A);
         SPG_ORDER;
         issue(k0 + 1, B1, B);
@@ -693,26 +695,30 @@ __global__ __launch_bounds__(1024) void k_fold_hist(MParams P, const Hist *__res
     }
 }
 
+// units of about `fill` bytes per array: LPC lanes per column (64 / LPC columns per tile); 4 KiB slots for
+// LPC 2 (32 columns of a 100x run), 3 KiB otherwise
+#define SPG_RUN_KERNEL(L) (L == 1 ? (const void *)k_acc_lite_run<1, 3> : L == 2 ? (const void *)k_acc_lite_run<2, 4> \
+                         : L == 4 ? (const void *)k_acc_lite_run<4, 3> : L == 8 ? (const void *)k_acc_lite_run<8, 3> \
+                         : (const void *)k_acc_lite_run<1, 7>)
 hipError_t launch_count_run(const MParams &P, const Hist *H, const uint8_t *ref, uint32_t *cdep, uint32_t *cmcf, int lpc,
                             int64_t blocks, hipStream_t st) {
     if (P.n_groups == 0 || P.K == 0) return hipSuccess;
     const dim3 grid((unsigned)std::max<int64_t>(1, blocks)), blk(64 * LW);
     switch (lpc) {
-        case 1: hipLaunchKernelGGL(k_acc_lite_run<1>, grid, blk, 0, st, P, H, ref, cdep, cmcf); break;
-        case 2: hipLaunchKernelGGL(k_acc_lite_run<2>, grid, blk, 0, st, P, H, ref, cdep, cmcf); break;
-        case 4: hipLaunchKernelGGL(k_acc_lite_run<4>, grid, blk, 0, st, P, H, ref, cdep, cmcf); break;
-        default: hipLaunchKernelGGL(k_acc_lite_run<8>, grid, blk, 0, st, P, H, ref, cdep, cmcf); break;
+        case 1: hipLaunchKernelGGL((k_acc_lite_run<1, 3>), grid, blk, 0, st, P, H, ref, cdep, cmcf); break;
+        case 2: hipLaunchKernelGGL((k_acc_lite_run<2, 4>), grid, blk, 0, st, P, H, ref, cdep, cmcf); break;
+        case 4: hipLaunchKernelGGL((k_acc_lite_run<4, 3>), grid, blk, 0, st, P, H, ref, cdep, cmcf); break;
+        case 8: hipLaunchKernelGGL((k_acc_lite_run<8, 3>), grid, blk, 0, st, P, H, ref, cdep, cmcf); break;
+        default: hipLaunchKernelGGL((k_acc_lite_run<1, 7>), grid, blk, 0, st, P, H, ref, cdep, cmcf); break;   // "lpc" 0
     }
     return hipGetLastError();
 }
 int count_run_blocks_per_cu(int lpc) {
-    static int n[4] = {-1, -1, -1, -1};
-    const int i = lpc == 1 ? 0 : lpc == 2 ? 1 : lpc == 4 ? 2 : 3;
+    static int n[5] = {-1, -1, -1, -1, -1};
+    const int i = lpc == 1 ? 0 : lpc == 2 ? 1 : lpc == 4 ? 2 : lpc == 8 ? 3 : 4;
     if (n[i] < 0) {
         int b = 0;
-        const void *f = i == 0 ? (const void *)k_acc_lite_run<1> : i == 1 ? (const void *)k_acc_lite_run<2>
-                      : i == 2 ? (const void *)k_acc_lite_run<4> : (const void *)k_acc_lite_run<8>;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, f, 64 * LW, 0) != hipSuccess || b < 1) b = 2;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, SPG_RUN_KERNEL(lpc), 64 * LW, 0) != hipSuccess || b < 1) b = 2;
         n[i] = b;
     }
     return n[i];
