@@ -33,7 +33,8 @@ hipError_t launch_count_run(const MParams &P, const Hist *H, const uint8_t *ref,
 int count_run_blocks_per_cu(int lpc);
 hipError_t launch_count_list(const MParams &P, const uint8_t *ref, const uint32_t *cdep, const uint32_t *cmcf, hipStream_t st);
 hipError_t launch_fold_hist(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
-                            hipStream_t st);
+                            void *part, uint32_t *arrived, int bpp, int cap, hipStream_t st);
+size_t fold_part_bytes();
 hipError_t launch_tile(const MParams &P, const Hist *H, const uint8_t *ref, int64_t ref_len, const Tables *T, Acc *acc,
                        int lpc, int64_t max_blocks, bool fused, hipStream_t st);
 hipError_t launch_merge(const MParams &P, const uint8_t *ref, Acc *acc, hipStream_t st);
@@ -176,6 +177,8 @@ struct spg_ctx {
     int64_t count_end = 0;
     int64_t n_deep_hist = 0;            // deep / multi-sample batches since reset (counted mode needs none)
     uint32_t *cdep = nullptr, *cmcf = nullptr;
+    void *fold_part = nullptr;          // k_fold_hist's multi-workgroup partials [FOLD_CAP][FOLD_BPP]
+    uint32_t *fold_arrived = nullptr;   // ... and arrival counts (zero between launches)
     // bounded history: owned batches past `hist_cap` bytes of HBM are spilled, oldest folded first
     int64_t hist_cap = 0;               // 0 = no cap
     int64_t hist_dev_bytes = 0;         // owned history bytes resident in HBM
@@ -337,7 +340,7 @@ int spg_destroy(spg_ctx *c) {
     c->arena.release();
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
-                    c->d_fused, c->deep_list, c->deep_n, c->cdep, c->cmcf};
+                    c->d_fused, c->deep_list, c->deep_n, c->cdep, c->cmcf, c->fold_part, c->fold_arrived};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
@@ -1331,7 +1334,17 @@ static int finalize_counted(spg_ctx *c) {
     P.h0 = 0;
     P.K = (int32_t)nh;
     P.seq0 = c->hist[0].seq0;
-    HIPCHK(launch_fold_hist(P, c->d_hist, c->ref, c->tables, c->acc, 4 * (int64_t)c->n_cu, c->stream));
+    // thousands of batches: up to 8 workgroups per listed position (the first FOLD_CAP of them), so a few dozen
+    // positions still spread over the chip
+    constexpr int FOLD_BPP = 8, FOLD_CAP = 4096;
+    const int bpp = (int)std::min<int64_t>(FOLD_BPP, nh / 1024);
+    if (bpp > 1 && !c->fold_part) {
+        HIPCHK(hipMalloc(&c->fold_part, fold_part_bytes() * FOLD_BPP * FOLD_CAP));
+        HIPCHK(hipMalloc(&c->fold_arrived, sizeof(uint32_t) * FOLD_CAP));
+        HIPCHK(hipMemsetAsync(c->fold_arrived, 0, sizeof(uint32_t) * FOLD_CAP, c->stream));
+    }
+    HIPCHK(launch_fold_hist(P, c->d_hist, c->ref, c->tables, c->acc, 4 * (int64_t)c->n_cu, bpp > 1 ? c->fold_part : nullptr,
+                            c->fold_arrived, bpp, FOLD_CAP, c->stream));
     if (int rc = trace_sync(c, "accumulate (k_fold_hist)")) return rc;
     return acc_end(c);
 }

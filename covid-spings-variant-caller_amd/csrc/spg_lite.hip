@@ -583,63 +583,112 @@ struct FoldPart {          // one wave's reduced partial state of a position (k_
 // record (first visit :77-85).  (The fp64 sums are added in that fixed tree order: within 1e-16 relative of
 // the sequential fold; positions where the order matters are replayed exactly from the history by the
 // finalize.)
+struct FoldAux {            // several workgroups per position (long histories): their partials and arrival counts
+    FoldPart *part;        // [cap][bpp]
+    uint32_t *arrived;     // [cap], zero between launches (the last arrival resets it)
+    int32_t bpp, cap;      // parts per position (1 = one workgroup), positions that may take them
+};
+
 __global__ __launch_bounds__(1024) void k_fold_hist(MParams P, const Hist *__restrict__ H, const uint8_t *__restrict__ ref,
-                                                    const Tables *__restrict__ T, Acc *__restrict__ acc) {
+                                                    const Tables *__restrict__ T, Acc *__restrict__ acc, FoldAux X) {
     __shared__ double2 lut[256];
     __shared__ FoldPart wp[16];
     if (threadIdx.x < 256) lut[threadIdx.x] = make_double2(T->fast[threadIdx.x][0], T->fast[threadIdx.x][1]);
     __syncthreads();
     const uint32_t n_list = *P.n_list;
+    // X.bpp > 1 (a history of thousands of batches): each of the first X.cap listed positions is folded by
+    // X.bpp workgroups over consecutive batch ranges (the work of one position otherwise occupies one CU); the
+    // last to arrive merges their partials in range order.  Items: (position, part) for those, then one item
+    // per remaining position.
+    const int32_t bpp = X.bpp;
+    const uint32_t n_multi = bpp > 1 ? min(n_list, (uint32_t)X.cap) : 0u;
+    const uint32_t n_items_blk = n_multi * (uint32_t)bpp + (n_list - n_multi);
     uint32_t tpp = 64;
     while (tpp < 1024u && tpp < (uint32_t)P.K) tpp <<= 1;
+    if (bpp > 1) tpp = 1024;
     const uint32_t G = 1024u / tpp, grp = threadIdx.x / tpp, r = threadIdx.x % tpp;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const int32_t per = (P.K + (int32_t)tpp - 1) / (int32_t)tpp;
-    const int32_t k0 = min(P.K, (int32_t)r * per), k1 = min(P.K, k0 + per);
-    for (uint32_t lb = blockIdx.x * G; lb < n_list; lb += gridDim.x * G) {
-        const uint32_t li = lb + grp;
+    const uint32_t n_iter = bpp > 1 ? n_items_blk : n_list;
+    for (uint32_t lb = blockIdx.x * G; lb < n_iter; lb += gridDim.x * G) {
+        uint32_t li, part = 0, nparts = 1;
+        if (bpp > 1) {
+            if (lb < n_multi * (uint32_t)bpp) { li = lb / (uint32_t)bpp; part = lb % (uint32_t)bpp; nparts = (uint32_t)bpp; }
+            else li = n_multi + (lb - n_multi * (uint32_t)bpp);
+        } else {
+            li = lb + grp;
+        }
         const bool act = li < n_list;
         const int64_t p = act ? P.list[li] : P.u0;
+        // this item's batch range, then this thread's share of it
+        const int32_t kp = (P.K + (int32_t)nparts - 1) / (int32_t)nparts;
+        const int32_t kb0 = min(P.K, (int32_t)part * kp), kb1 = min(P.K, kb0 + kp);
+        const int32_t per = (kb1 - kb0 + (int32_t)tpp - 1) / (int32_t)tpp;
+        const int32_t k0 = min(kb1, kb0 + (int32_t)r * per), k1 = min(kb1, k0 + per);
         uint32_t depth = 0, n_del = 0, n_skip = 0, n_other = 0, fb = INF32, sidx = 0;
         uint32_t cnt[NSLOT], sq[NSLOT], qf[NSLOT], first[NSLOT];
         double sl[NSLOT], se[NSLOT];
 #pragma unroll
         for (int j = 0; j < NSLOT; j++) { cnt[j] = sq[j] = 0; qf[j] = 255; first[j] = INF32; sl[j] = se[j] = 0.0; }
-        for (int32_t k = k0; act && k < k1; k++) {
-            const Hist h = H[P.h0 + k];
+        // batch k's column for this position (descriptor, then bounds: two dependent loads), fetched one batch
+        // ahead so that those loads are in flight while the current batch folds
+        struct FCol {
+            const uint8_t *code, *qual;
+            uint64_t ob;
+            uint32_t len;
+        };
+        auto fetch = [&](int32_t k) -> FCol {
+            const Hist h = H[P.h0 + min(k, P.K - 1)];
             const int64_t col = p - h.pos_begin;
-            if (col < 0 || col >= h.n_cols) continue;
-            const uint64_t ob = gbl(h.off)[col];
-            const uint32_t len = (uint32_t)(gbl(h.off)[col + 1] - ob);
-            if (!len) continue;
-            if (fb == INF32) fb = (uint32_t)k;
-            const uint64_t a0 = ob & ~(uint64_t)3;
-            const int32_t lead = (int32_t)(ob & 3u);
-            const uint32_t nb = ((uint32_t)lead + len + 15u) >> 4;
-            for (uint32_t u = 0; u < nb; u++) {
-                const u32x4 cw = gbl(reinterpret_cast<const u32x4 *>(h.code + a0))[u];
-                const u32x4 qw = gbl(reinterpret_cast<const u32x4 *>(h.qual + a0))[u];
+            const bool in = act && k < k1 && col >= 0 && col < h.n_cols;
+            const int64_t cc = in ? col : 0;
+            const uint64_t ob = gbl(h.off)[cc], oe = gbl(h.off)[cc + 1];
+            return FCol{h.code, h.qual, ob, in ? (uint32_t)(oe - ob) : 0u};
+        };
+        FCol cur = fetch(k0);
+        for (int32_t k = k0; act && k < k1; k++) {
+            const FCol nxt = fetch(k + 1);
+            const uint32_t len = cur.len;
+            if (len) {
+                if (fb == INF32) fb = (uint32_t)k;
+                const uint64_t a0 = cur.ob & ~(uint64_t)3;
+                const int32_t lead = (int32_t)(cur.ob & 3u);
+                const uint32_t nb = ((uint32_t)lead + len + 15u) >> 4;
+                for (uint32_t u0 = 0; u0 < nb; u0 += 2) {
+                    u32x4 cw[2], qw[2];
 #pragma unroll
-                for (int b = 0; b < 16; b++) {
-                    const int32_t x = (int32_t)(16u * u) + b - lead;
-                    const uint32_t cc = (dw<4>(cw, b >> 2) >> (8 * (b & 3))) & 0xFFu;
-                    const uint32_t qq = (dw<4>(qw, b >> 2) >> (8 * (b & 3))) & 0xFFu;
-                    if (x < 0 || x >= (int32_t)len || (int)qq < P.min_bq) continue;
-                    depth++;
-                    if (cc == SPG_CODE_DEL) { n_del++; continue; }
-                    if (cc == SPG_CODE_SKIP) { n_skip++; continue; }
-                    const int s = slot_of(cc);
-                    if (s < 0) { n_other++; continue; }
-                    const double2 tt = lut[qq];
+                    for (int i = 0; i < 2; i++) {         // two blocks in flight together (clamped: no branch)
+                        const uint32_t u = min(u0 + (uint32_t)i, nb - 1u);
+                        cw[i] = gbl(reinterpret_cast<const u32x4 *>(cur.code + a0))[u];
+                        qw[i] = gbl(reinterpret_cast<const u32x4 *>(cur.qual + a0))[u];
+                    }
 #pragma unroll
-                    for (int j = 0; j < NSLOT; j++)
-                        if (j == s) {
-                            cnt[j]++; sq[j] += qq; qf[j] = min(qf[j], qq); first[j] = min(first[j], sidx + (uint32_t)x);
-                            sl[j] += tt.x; se[j] += qq == 0 ? 1.0 : tt.y;
+                    for (int i = 0; i < 2; i++) {
+                        const uint32_t u = u0 + (uint32_t)i;
+                        if (u >= nb) break;
+#pragma unroll
+                        for (int b = 0; b < 16; b++) {
+                            const int32_t x = (int32_t)(16u * u) + b - lead;
+                            const uint32_t cc = (dw<4>(cw[i], b >> 2) >> (8 * (b & 3))) & 0xFFu;
+                            const uint32_t qq = (dw<4>(qw[i], b >> 2) >> (8 * (b & 3))) & 0xFFu;
+                            if (x < 0 || x >= (int32_t)len || (int)qq < P.min_bq) continue;
+                            depth++;
+                            if (cc == SPG_CODE_DEL) { n_del++; continue; }
+                            if (cc == SPG_CODE_SKIP) { n_skip++; continue; }
+                            const int s = slot_of(cc);
+                            if (s < 0) { n_other++; continue; }
+                            const double2 tt = lut[qq];
+#pragma unroll
+                            for (int j = 0; j < NSLOT; j++)
+                                if (j == s) {
+                                    cnt[j]++; sq[j] += qq; qf[j] = min(qf[j], qq); first[j] = min(first[j], sidx + (uint32_t)x);
+                                    sl[j] += tt.x; se[j] += qq == 0 ? 1.0 : tt.y;
+                                }
                         }
+                    }
                 }
+                sidx += len;
             }
-            sidx += len;
+            cur = nxt;
         }
         // this wave's partial (its threads are consecutive in batch order)
         FoldPart w;
@@ -650,7 +699,7 @@ __global__ __launch_bounds__(1024) void k_fold_hist(MParams P, const Hist *__res
             w.cnt[j] = dsum_u32(cnt[j]);
             w.sq[j] = dsum_u32(sq[j]);
             w.qf[j] = wmin_u32(qf[j]);
-            w.key[j] = wmin_u64(cnt[j] ? ((uint64_t)r << 32) | first[j] : ~0ull);
+            w.key[j] = wmin_u64(cnt[j] ? ((uint64_t)(part * tpp + r) << 32) | first[j] : ~0ull);
             w.sl[j] = dsum_f64(sl[j]);
             w.se[j] = dsum_f64(se[j]);
         }
@@ -670,7 +719,36 @@ __global__ __launch_bounds__(1024) void k_fold_hist(MParams P, const Hist *__res
                     w.key[j] = min(w.key[j], o.key[j]); w.sl[j] += o.sl[j]; w.se[j] += o.se[j];
                 }
             }
-            if (w.fb != INF32) {
+            bool write = true;
+            if (nparts > 1) {
+                // publish this part; the last part to arrive merges them all, in range order
+                X.part[(size_t)li * (size_t)bpp + part] = w;
+                __threadfence();
+                const uint32_t old = atomicAdd(X.arrived + li, 1u);
+                write = old == (uint32_t)bpp - 1u;
+                if (write) {
+                    __threadfence();
+                    const volatile FoldPart *pp = X.part + (size_t)li * (size_t)bpp;
+                    FoldPart m;
+                    m.depth = m.n_del = m.n_skip = m.n_other = 0;
+                    m.fb = INF32;
+#pragma unroll
+                    for (int j = 0; j < NSLOT; j++) { m.cnt[j] = m.sq[j] = 0; m.qf[j] = 255; m.key[j] = ~0ull; m.sl[j] = m.se[j] = 0.0; }
+                    for (int32_t v = 0; v < bpp; v++) {
+                        const volatile FoldPart &o = pp[v];
+                        m.depth += o.depth; m.n_del += o.n_del; m.n_skip += o.n_skip; m.n_other += o.n_other;
+                        m.fb = min(m.fb, (uint32_t)o.fb);
+#pragma unroll
+                        for (int j = 0; j < NSLOT; j++) {
+                            m.cnt[j] += o.cnt[j]; m.sq[j] += o.sq[j]; m.qf[j] = min(m.qf[j], (uint32_t)o.qf[j]);
+                            m.key[j] = min(m.key[j], (uint64_t)o.key[j]); m.sl[j] += o.sl[j]; m.se[j] += o.se[j];
+                        }
+                    }
+                    w = m;
+                    X.arrived[li] = 0;                 // ready for the next launch
+                }
+            }
+            if (write && w.fb != INF32) {
                 MState c;
                 ms_init(c);
                 c.depth = w.depth; c.n_del = w.n_del; c.n_skip = w.n_skip; c.n_other = w.n_other; c.fb = w.fb;
@@ -730,9 +808,11 @@ hipError_t launch_count_list(const MParams &P, const uint8_t *ref, const uint32_
     return hipGetLastError();
 }
 hipError_t launch_fold_hist(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
-                            hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_hist, dim3((unsigned)std::max<int64_t>(1, blocks)), dim3(1024), 0, st, P, H, ref, T, acc);
+                            void *part, uint32_t *arrived, int bpp, int cap, hipStream_t st) {
+    const FoldAux X{(FoldPart *)part, arrived, part ? bpp : 1, cap};
+    hipLaunchKernelGGL(k_fold_hist, dim3((unsigned)std::max<int64_t>(1, blocks)), dim3(1024), 0, st, P, H, ref, T, acc, X);
     return hipGetLastError();
 }
+size_t fold_part_bytes() { return sizeof(FoldPart); }
 
 }  // namespace spg

@@ -374,3 +374,22 @@ def test_chr1_30x_full_size_count_conservation():
     eng.close()
     del d
     torch.cuda.empty_cache()
+
+
+def test_2500_batches_counted_fold_across_workgroups():
+    """A calls-only finalize over 2,500 batches: counted mode's exact fold splits each listed position's history
+    over several workgroups (merged in batch order by the last to arrive) — calls, dict order and first visits
+    vs the oracle, then the table (re-materialized) vs the oracle's memory."""
+    L = 900
+    ref, batches = _many(L, 2500, 20, 12000, span=600, band_pos=450, iupac_pos=460, cap=18)
+    eng = _engine(ref, True)
+    orc = _oracle(ref)
+    eng.accumulate_batches(batches)
+    for b in batches:
+        orc.accumulate(*b)
+    eng.finalize()
+    orc.finalize()
+    compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
+    assert len(eng.variants()) > 10
+    assert eng.memory_summary() == orc.memory_summary()
+    eng.close()
