@@ -518,10 +518,12 @@ def cpu_baseline(args):
 
 
 def end_to_end(args, device):
-    """BAM -> calls through the drop-in (LiveVariantCaller.process_bam, live_variant_caller.py:54-72):
-    host pileup (libspings_pileup: BGZF inflate, htslib-rule pileup, CSR offsets) -> entries written
-    into pinned, double-buffered staging -> async H2D on the engine's copy stream -> accumulate; the
-    next BAM's pileup overlaps the previous BAM's copy and kernels.  A stream of --e2e-bams synthetic
+    """BAM -> calls through the drop-in (LiveVariantCaller.process_bam, live_variant_caller.py:54-72).
+    Product path (device pileup): host BGZF inflate straight into pinned memory + record scan +
+    htslib depth cap / overlap tweak + CSR offsets (spp_pileup_plan_records) -> async H2D of the inflated BAM
+    on the engine's copy stream -> k_pileup_fill decodes the records and walks the CIGARs -> accumulate; the
+    next BAM's host work overlaps the previous BAM's copy and kernels.  Beside it, r02's host-fill path
+    (the host writes every entry into pinned staging).  A stream of --e2e-bams synthetic
     10,000x BAMs (written by the C++ read simulator) into one memory, then prepare_variants.  Reported
     beside `value` (never as it): it includes the host front end and PCIe."""
     import tempfile
@@ -542,10 +544,12 @@ def end_to_end(args, device):
     t_sim = time.perf_counter() - t0
     res = {}
     n_bams = max(1, args.e2e_bams)
-    for cap, tag in ((8000, "parity_mode_max_depth_8000"), (0, "uncapped")):
+    def stream(cap, device_pileup):
+        os.environ["SPG_DEVICE_PILEUP"] = "1" if device_pileup else "0"
         caller = LiveVariantCaller(fasta, 30, 20, 10, 5, 0.10, 1, device=device, max_depth=cap,
                                    n_threads=args.e2e_threads)
-        caller.process_bam(bam)                    # warm-up: pinned staging, library state
+        for _ in range(3):                         # warm-up: pinned staging / record buffers, library state
+            caller.process_bam(bam)
         caller.reset_memory()
         caller.engine.sync()
         t0 = time.perf_counter()
@@ -555,7 +559,12 @@ def end_to_end(args, device):
         calls = caller.prepare_variants()
         caller.engine.sync()
         t1 = time.perf_counter()
-        # breakdown of one more BAM: host pileup phases, then the GPU leg alone
+        return caller, calls, t0, t_in, t1
+
+    for cap, tag in ((8000, "parity_mode_max_depth_8000"), (0, "uncapped")):
+        # the host-fill path first (r02's product path: the host writes every entry into pinned staging)
+        caller, calls_h, t0, t_in, t1 = stream(cap, False)
+        host_leg = {"positions_per_s_per_bam": n_bams * L_SARS / (t1 - t0), "s_per_bam": (t1 - t0) / n_bams}
         p = caller.pileup_params
         b0 = time.perf_counter()
         with AlignmentFile(bam) as f:
@@ -564,24 +573,41 @@ def end_to_end(args, device):
         codes, quals = pinned_empty(b.n_entries + 16), pinned_empty(b.n_entries + 16)
         b.fill(codes, quals)
         b2 = time.perf_counter()
+        host_leg.update(host_plan_s=b1 - b0, host_fill_pinned_s=b2 - b1)
+        b.close()
+        caller.engine.close()
+        del caller
+        # the product path: device-side pileup (spg_accumulate_records)
+        caller, calls, t0, t_in, t1 = stream(cap, True)
+        assert [v["start"] for v in calls] == [v["start"] for v in calls_h], "device / host pileup calls differ"
+        p = caller.pileup_params
+        b0 = time.perf_counter()
+        with AlignmentFile(bam) as f:
+            b = f.pileup_records("NC_045512.2", p)
+        b1 = time.perf_counter()
         eng = caller.engine
         eng.reset()
         eng.sync()
         g0 = time.perf_counter()
-        eng.accumulate(b.pos_begin, b.offsets, codes[:b.n_entries], quals[:b.n_entries], trusted=True)
+        eng.accumulate_bam_records(b)
         eng.finalize()
         eng.sync()
         g1 = time.perf_counter()
         E = b.n_entries
+        data_mb = b.records().data_bytes / 1e6
         b.close()
         res[tag] = {"bams": n_bams, "positions_per_s_per_bam": n_bams * L_SARS / (t1 - t0),
                     "s_per_bam": (t1 - t0) / n_bams, "ingest_s": t_in, "finalize_s": t1 - t0 - t_in,
                     "calls": len(calls), "entries_per_bam": int(E),
-                    "breakdown_one_bam": {"host_plan_s": b1 - b0, "host_fill_pinned_s": b2 - b1,
-                                          "h2d_pinned_plus_gpu_s": g1 - g0,
-                                          "pcie_inclusive_gpu_positions_per_s": L_SARS / (g1 - g0)}}
+                    "path": "device pileup: host inflate + record scan + depth cap (spp_pileup_plan_records) -> "
+                            "pinned inflated BAM -> H2D -> k_pileup_fill (decode + CIGAR walk) -> accumulate",
+                    "breakdown_one_bam": {"host_plan_records_s": b1 - b0, "inflated_mb": data_mb,
+                                          "h2d_records_plus_gpu_s": g1 - g0,
+                                          "pcie_inclusive_gpu_positions_per_s": L_SARS / (g1 - g0)},
+                    "host_fill_path": host_leg}
         caller.engine.close()
         del caller
+    os.environ.pop("SPG_DEVICE_PILEUP", None)
     res["bam_bytes"] = os.path.getsize(bam)
     res["reads"] = n_reads
     res["simulate_s"] = t_sim

@@ -38,6 +38,18 @@ CANDIDATE_DTYPE = np.dtype([("pos", "<i8"), ("dp", "<i4"), ("ad", "<i4"), ("pl",
 # spg_batch (include/spings_gpu.h): one CSR batch of spg_accumulate_batches
 BATCH_DTYPE = np.dtype([("pos_begin", "<i8"), ("n_cols", "<i8"), ("offsets", "<u8"), ("base_code", "<u8"),
                         ("qual", "<u8"), ("n_entries", "<u8")])
+
+
+class SpgRecords(C.Structure):
+    """spg_records (include/spings_gpu.h): a records plan's raw BAM bytes + per-read index."""
+    _fields_ = [("pos_begin", C.c_int64), ("n_cols", C.c_int64), ("n_entries", C.c_uint64),
+                ("offsets", C.c_void_p), ("data", C.c_void_p), ("data_bytes", C.c_uint64), ("n_reads", C.c_int64),
+                ("rec", C.c_void_p), ("rpos", C.c_void_p), ("rend", C.c_void_p), ("tweak", C.c_void_p),
+                ("n_tweaks", C.c_int64), ("tweak_col", C.c_void_p), ("tweak_qual", C.c_void_p),
+                ("orig_qual", C.c_void_p), ("orig_bytes", C.c_uint64), ("max_span", C.c_int64),
+                ("reserved", C.c_int64 * 4)]
+
+
 DETAIL_DTYPE = np.dtype([("pos", "<i8"), ("depth", "<u4"), ("n_alleles", "u1"), ("pad", "u1", 3),
                          ("code", "u1", 16), ("count", "<u4", 16), ("gl", "<f8", 16)])
 
@@ -83,6 +95,7 @@ def gpu_lib():
     _sig(L.spg_accumulate_batches, i32, vp, vp, i64, C.c_uint32)
     _sig(L.spg_accumulate_samples, i32, vp, i64, i64, i64, vp, vp, vp, vp, u64, C.c_uint32)
     _sig(L.spg_history_samples, i32, vp, i64, C.POINTER(i64), vp)
+    _sig(L.spg_accumulate_records, i32, vp, C.POINTER(SpgRecords), C.c_uint32)
     _sig(L.spg_host_alloc, i32, C.c_size_t, C.POINTER(vp))
     _sig(L.spg_host_free, i32, vp)
     _sig(L.spg_wait_input, i32, vp)
@@ -184,12 +197,30 @@ def pileup_lib():
     _sig(L.spp_batch_free, C.c_int, vp)
     _sig(L.spp_pileup_plan, C.c_int, vp, i32, i64, i64, C.POINTER(SppParams), C.POINTER(vp))
     _sig(L.spp_batch_fill, C.c_int, vp, vp, vp)
+    _sig(L.spp_pileup_plan_records, C.c_int, vp, i32, i64, i64, C.POINTER(SppParams), C.POINTER(vp))
+    _sig(L.spp_batch_records, C.c_int, vp, C.POINTER(SpgRecords))
+    _sig(L.spp_set_host_allocator, C.c_int, vp, vp)
     _sig(L.spp_default_sim_params, None, C.POINTER(SimParams))
     _sig(L.spp_simulate_bam, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, i64, C.POINTER(SimParams),
          C.POINTER(i64))
     _sig(L.spp_synth_batch, C.c_int, C.c_char_p, i64, i64, i64, C.POINTER(SimParams), i64, C.POINTER(vp))
     _pileup = L
     return L
+
+
+_pinned_records = False
+
+
+def use_pinned_records():
+    """Route the records plans' host buffers through spg_host_alloc / spg_host_free (pinned: the copy of the
+    inflated BAM to HBM is then a DMA without a staging copy).  Idempotent."""
+    global _pinned_records
+    if _pinned_records:
+        return
+    G, P = gpu_lib(), pileup_lib()
+    pcheck(P.spp_set_host_allocator(C.cast(G.spg_host_alloc, C.c_void_p), C.cast(G.spg_host_free, C.c_void_p)),
+           "spp_set_host_allocator")
+    _pinned_records = True
 
 
 def pcheck(rc: int, what: str = ""):

@@ -21,7 +21,7 @@ LIBDIR = os.path.join(PKG, "_lib")
 INC = os.path.join(ROOT, "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-GPU_SOURCES = ["spg_kernels.hip", "spg_tile.hip", "spg_lite.hip", "spg_api.cpp", "spg_multi.cpp"]
+GPU_SOURCES = ["spg_kernels.hip", "spg_tile.hip", "spg_lite.hip", "spg_fill.hip", "spg_api.cpp", "spg_multi.cpp"]
 GPU_HEADERS = ["spg_device.h", "spg_common.h"]
 PILEUP_SOURCES = ["spp_pileup.cpp"]
 
@@ -97,7 +97,7 @@ def build_pileup(force=False, verbose=False) -> str:
     srcs = [os.path.join(CSRC, f) for f in PILEUP_SOURCES]
     if not all(os.path.exists(s) for s in srcs):
         return ""
-    deps = srcs + [os.path.join(INC, "spings_pileup.h")]
+    deps = srcs + [os.path.join(INC, "spings_pileup.h"), os.path.join(INC, "spings_gpu.h")]
     if force or _stale(out, deps):
         cxx = shutil.which("g++") or "g++"
         cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{INC}", "-o", out + ".tmp"] + srcs + ["-lz", "-ldl", "-pthread"]

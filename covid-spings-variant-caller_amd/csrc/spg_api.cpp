@@ -39,6 +39,7 @@ hipError_t launch_tile(const MParams &P, const Hist *H, const uint8_t *ref, int6
                        int lpc, int64_t max_blocks, bool fused, hipStream_t st);
 hipError_t launch_merge(const MParams &P, const uint8_t *ref, Acc *acc, hipStream_t st);
 int tile_blocks_per_cu(int lpc, bool fused, bool one);
+hipError_t launch_pileup_fill(const FillArgs &A, hipStream_t st);
 }  // namespace spg
 
 using namespace spg;
@@ -183,6 +184,9 @@ struct spg_ctx {
     int64_t hist_cap = 0;               // 0 = no cap
     int64_t hist_dev_bytes = 0;         // owned history bytes resident in HBM
     int64_t n_spilled = 0;
+    // spg_accumulate_records: HBM staging of the last records batch (inflated BAM + per-read index), grow-only
+    uint8_t *rs = nullptr;
+    size_t rs_cap = 0;
     MState *part = nullptr;             // split-run partial states
     size_t part_bytes = 0;
     // replay index: history batches per 2^RIDX_SHIFT-position bucket
@@ -340,7 +344,7 @@ int spg_destroy(spg_ctx *c) {
     c->arena.release();
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
-                    c->d_fused, c->deep_list, c->deep_n, c->cdep, c->cmcf, c->fold_part, c->fold_arrived};
+                    c->d_fused, c->deep_list, c->deep_n, c->cdep, c->cmcf, c->fold_part, c->fold_arrived, c->rs};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
@@ -962,9 +966,65 @@ static void free_spilled(spg_ctx *c) {
         if (b.host) { (void)hipHostFree(b.host); b.host = nullptr; }
 }
 
+// Records batch (spg_accumulate_records): the inflated BAM and its per-read index to HBM, then the device-side
+// pileup writes the batch's entries (all on the copy stream, so the batch is ready where a copied one would be).
+static int upload_records(spg_ctx *c, const spg_records *R, const HistBatch &hb, hipStream_t cs) {
+    const uint64_t n = (uint64_t)R->n_reads, nt = (uint64_t)R->n_tweaks;
+    const int64_t n_tiles = (R->n_cols + 63) / 64;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_data = 0, o_rec = al(R->data_bytes + 64), o_pos = al(o_rec + 8 * n), o_end = al(o_pos + 4 * n),
+                 o_tw = al(o_end + 4 * n), o_tcol = al(o_tw + 4 * n), o_tq = al(o_tcol + 8 * nt),
+                 o_orig = al(o_tq + 8 * nt), o_tf = al(o_orig + R->orig_bytes), need = al(o_tf + 4 * (n_tiles + 1));
+    if (need > c->rs_cap) {
+        if (c->rs) HIPCHK(hipFree(c->rs));      // (synchronous: the previous fill has run)
+        c->rs = nullptr;
+        c->rs_cap = need + need / 8;
+        HIPCHK(hipMalloc(&c->rs, c->rs_cap));
+    }
+    uint8_t *m = c->rs;
+    const hipMemcpyKind k = hipMemcpyHostToDevice;
+    if (R->data_bytes) HIPCHK(hipMemcpyAsync(m + o_data, R->data, R->data_bytes, k, cs));
+    HIPCHK(hipMemsetAsync(m + o_data + R->data_bytes, 0, 64, cs));
+    if (n) {
+        HIPCHK(hipMemcpyAsync(m + o_rec, R->rec, 8 * n, k, cs));
+        HIPCHK(hipMemcpyAsync(m + o_pos, R->rpos, 4 * n, k, cs));
+        HIPCHK(hipMemcpyAsync(m + o_end, R->rend, 4 * n, k, cs));
+        HIPCHK(hipMemcpyAsync(m + o_tw, R->tweak, 4 * n, k, cs));
+    }
+    if (nt) {
+        HIPCHK(hipMemcpyAsync(m + o_tcol, R->tweak_col, 8 * nt, k, cs));
+        HIPCHK(hipMemcpyAsync(m + o_tq, R->tweak_qual, 8 * nt, k, cs));
+    }
+    if (R->orig_bytes) HIPCHK(hipMemcpyAsync(m + o_orig, R->orig_qual, R->orig_bytes, k, cs));
+    FillArgs A{};
+    A.data = m + o_data;
+    A.data_bytes = R->data_bytes;
+    A.rec = reinterpret_cast<const uint64_t *>(m + o_rec);
+    A.rpos = reinterpret_cast<const int32_t *>(m + o_pos);
+    A.rend = reinterpret_cast<const int32_t *>(m + o_end);
+    A.tweak = reinterpret_cast<const int32_t *>(m + o_tw);
+    A.tw_col = reinterpret_cast<const int64_t *>(m + o_tcol);
+    A.tw_q = reinterpret_cast<const uint64_t *>(m + o_tq);
+    A.orig = m + o_orig;
+    A.orig_bytes = R->orig_bytes;
+    A.tile_first = reinterpret_cast<uint32_t *>(m + o_tf);
+    A.off = hb.off;
+    A.code = hb.code;
+    A.qual = hb.qual;
+    A.pos_begin = R->pos_begin;
+    A.n_cols = (int32_t)R->n_cols;
+    A.n_tiles = (int32_t)n_tiles;
+    A.n_reads = (uint32_t)n;
+    A.back = (int32_t)((R->max_span + 63) / 64);
+    A.err = c->kerr;
+    HIPCHK(launch_pileup_fill(A, cs));
+    return 0;
+}
+
 static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
                      const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags,
-                     bool *pageable_copy, int64_t n_samples = 1, const uint32_t *first_sample = nullptr) {
+                     bool *pageable_copy, int64_t n_samples = 1, const uint32_t *first_sample = nullptr,
+                     const spg_records *recs = nullptr) {
     if (n_samples < 1 || n_samples > (1 << 30)) return fail("spg_accumulate_samples: n_samples out of range");
     static const double deep_min = [] { const char *e = getenv("SPG_DEEP_MIN"); return e ? atof(e) : 256.0; }();
     const bool deep_batch = (n_cols > 0 && (double)n_entries / (double)n_cols >= deep_min) || n_samples > 1 || first_sample;
@@ -977,11 +1037,11 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
     if (pos_begin + n_cols > c->ref_len)
         return fail("spg_accumulate: column range beyond the reference sequence (IndexError in the reference)");
     if (n_cols == 0) return 0;
-    if (!offsets || (n_entries && (!base_code || !qual))) return fail("spg_accumulate: null buffer");
+    if (!offsets || (n_entries && !recs && (!base_code || !qual))) return fail("spg_accumulate: null buffer");
     if (n_entries >= (1ull << 40)) return fail("spg_accumulate: batch too large");
-    const bool dev = flags & SPG_IN_DEVICE;
+    const bool dev = !recs && (flags & SPG_IN_DEVICE);
     const bool borrow = dev && (flags & SPG_IN_BORROW);
-    if (!dev && !(flags & SPG_IN_TRUSTED)) {
+    if (!dev && !recs && !(flags & SPG_IN_TRUSTED)) {
         // validate the host CSR (offsets O(n_cols), codes O(E)); device inputs are trusted
         if (offsets[0] != 0 || offsets[n_cols] != n_entries)
             return fail("spg_accumulate: offsets[0] must be 0 and offsets[n_cols] == n_entries");
@@ -1022,7 +1082,9 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
         const hipMemcpyKind k = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
         hipStream_t cs = c->copy_stream;
         HIPCHK(hipMemcpyAsync(hb.off, offsets, sizeof(uint64_t) * (n_cols + 1), k, cs));
-        if (n_entries) {
+        if (recs) {
+            if (int rc = upload_records(c, recs, hb, cs)) return rc;
+        } else if (n_entries) {
             HIPCHK(hipMemcpyAsync(hb.code, base_code, n_entries, k, cs));
             HIPCHK(hipMemcpyAsync(hb.qual, qual, n_entries, k, cs));
         }
@@ -1040,8 +1102,12 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
         c->in_seq++;
         c->copy_pending = true;
         // pageable host buffers are the caller's again on return; pinned ones after spg_wait_input
-        if (!dev && !(is_pinned(offsets) && (!n_entries || (is_pinned(base_code) && is_pinned(qual)))))
+        if (recs) {
+            if (!(is_pinned(offsets) && (!recs->data_bytes || is_pinned(recs->data)) && (!recs->n_reads || is_pinned(recs->rec))))
+                *pageable_copy = true;
+        } else if (!dev && !(is_pinned(offsets) && (!n_entries || (is_pinned(base_code) && is_pinned(qual))))) {
             *pageable_copy = true;
+        }
     }
     c->hist.push_back(hb);
     const int64_t idx = (int64_t)c->hist.size() - 1;
@@ -1123,6 +1189,28 @@ int spg_accumulate_samples(spg_ctx *c, int64_t pos_begin, int64_t n_cols, int64_
     bool pageable = false;
     int rc = add_batch(c, pos_begin, n_cols, offsets, base_code, qual, n_entries, flags, &pageable, n_samples,
                        first_sample);
+    if (pageable) HIPCHK(hipStreamSynchronize(c->copy_stream));
+    return rc;
+}
+
+int spg_accumulate_records(spg_ctx *c, const spg_records *r, uint32_t flags) {
+    if (!c || !r) return fail("spg_accumulate_records: null argument");
+    if (!c->lut_set) return fail("spg_accumulate: spg_set_eps_lut not called");
+    if (!c->ref) return fail("spg_accumulate: spg_set_reference not called");
+    if (r->n_cols < 0 || r->n_cols > ((int64_t)1 << 31) - 128) return fail("spg_accumulate_records: n_cols out of range");
+    if (r->n_reads < 0 || r->n_reads >= ((int64_t)1 << 31)) return fail("spg_accumulate_records: n_reads out of range");
+    if (r->n_tweaks < 0 || r->n_tweaks > r->n_reads || r->max_span < 0)
+        return fail("spg_accumulate_records: bad tweak count / span");
+    if (r->n_cols > 0 && (!r->offsets || (r->n_reads && (!r->data || !r->rec || !r->rpos || !r->rend || !r->tweak)) ||
+                          (r->n_tweaks && (!r->tweak_col || !r->tweak_qual || (r->orig_bytes && !r->orig_qual)))))
+        return fail("spg_accumulate_records: null buffer");
+    if (r->n_cols > 0 && (r->offsets[0] != 0 || r->offsets[r->n_cols] != r->n_entries))
+        return fail("spg_accumulate_records: offsets[0] must be 0 and offsets[n_cols] == n_entries");
+    (void)flags;
+    HIPCHK(hipSetDevice(c->device));
+    bool pageable = false;
+    int rc = add_batch(c, r->pos_begin, r->n_cols, r->offsets, nullptr, nullptr, r->n_entries, SPG_IN_TRUSTED, &pageable,
+                       1, nullptr, r);
     if (pageable) HIPCHK(hipStreamSynchronize(c->copy_stream));
     return rc;
 }
@@ -1449,6 +1537,10 @@ static int settle(spg_ctx *c, Counters &h) {
         if (h.err) return fail("spg: replay found a depth mismatch between history and accumulators");
         uint32_t kerr = 0;
         HIPCHK(hipMemcpy(&kerr, c->kerr, sizeof(kerr), hipMemcpyDeviceToHost));
+        if (kerr & 2) {
+            HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));   // reported once
+            return fail("spg: spg_accumulate_records: the records disagree with the batch's offsets (inconsistent plan)");
+        }
         if (kerr) {
             HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));   // reported once
             return fail("spg: a shallow batch held >= 2^30 entries in 64 consecutive columns; accumulate it "

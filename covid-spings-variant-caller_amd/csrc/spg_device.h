@@ -201,4 +201,24 @@ __host__ __device__ __forceinline__ uint8_t nibble_char(uint32_t c) {
     return (uint8_t)(t >> (8u * (c & 7u)));
 }
 
+// spg_accumulate_records: the device-side pileup (spg_fill.hip)
+struct FillArgs {
+    const uint8_t *data;           // the inflated BAM (64 readable pad bytes past data_bytes)
+    uint64_t data_bytes;
+    const uint64_t *rec;           // per read: offset of its refID field in data
+    const int32_t *rpos, *rend, *tweak;
+    const int64_t *tw_col;
+    const uint64_t *tw_q;
+    const uint8_t *orig;
+    uint64_t orig_bytes;
+    uint32_t *tile_first;          // [n_tiles + 1]: first read starting at or after the tile (0 for tile 0)
+    const uint64_t *off;           // CSR offsets [n_cols + 1]
+    uint8_t *code, *qual;
+    int64_t pos_begin;
+    int32_t n_cols, n_tiles;
+    uint32_t n_reads;
+    int32_t back;                  // tiles to look back: ceil(max_span / 64)
+    uint32_t *err;                 // |= 2: the records disagree with the offsets (inconsistent plan)
+};
+
 }  // namespace spg

@@ -11,6 +11,11 @@
 // Semantics restated from the published htslib sam.c / pysam libcalignmentfile.pyx (absent here:
 // parity unpinned; oracle/pileup_port.py is the independent restatement the tests compare with).
 #include "spings_pileup.h"
+#include "spings_gpu.h"      // spg_records (the device-decode plan's view)
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <dlfcn.h>
 #include <sys/mman.h>
@@ -160,13 +165,38 @@ struct Reads {                 // one contig's reads, structure of arrays
             return r;
         }
     } arena;
+    // records plans (spp_pileup_plan_records): bases stay packed in the inflated BAM bytes `raw`; rec[r] is the
+    // offset of read r's refID field there and bases[r] only marks reads inside the decode window
+    uint8_t *raw = nullptr;
+    Vec<uint64_t> rec;
+    size_t qual_off(size_t r) const {
+        return rec[r] + 32 + raw[rec[r] + 8] + 4 * (size_t)n_cig[r] + (l_seq[r] + 1) / 2;
+    }
+    // CIGAR op i / read name of read r (records plans: read in place, nothing copied)
+    uint32_t cig(size_t r, uint32_t i) const {
+        if (!raw) return cigar[cig_off[r] + i];
+        uint32_t v;
+        memcpy(&v, raw + rec[r] + 32 + raw[rec[r] + 8] + 4 * (size_t)i, 4);
+        return v;
+    }
+    std::string name(size_t r) const {
+        if (!raw) return std::string(names.data() + name_off[r]);
+        const uint8_t ln = raw[rec[r] + 8];
+        return std::string((const char *)raw + rec[r] + 32, ln ? ln - 1u : 0u);
+    }
     uint8_t *seq(size_t r) const { return bases[r]; }
-    uint8_t *qual(size_t r) const { return bases[r] + l_seq[r]; }
+    uint8_t *qual(size_t r) const { return raw ? raw + qual_off(r) : bases[r] + l_seq[r]; }
+    uint8_t base(size_t r, uint32_t i) const {
+        if (!raw) return bases[r][i];
+        const uint8_t b = raw[rec[r] + 32 + raw[rec[r] + 8] + 4 * (size_t)n_cig[r] + i / 2];
+        return (i & 1) ? (b & 15) : (b >> 4);
+    }
     size_t size() const { return pos.size(); }
     void clear() {                      // empty, keeping every array's capacity (and its resident pages)
         pos.clear(); end.clear(); mpos.clear(); isize.clear(); mtid.clear(); flag.clear(); mapq.clear();
         cig_off.clear(); name_off.clear(); n_cig.clear(); l_seq.clear(); cigar.clear(); bases.clear();
-        names.clear();
+        names.clear(); rec.clear();
+        raw = nullptr;
         dlo = INT64_MIN; dhi = INT64_MAX; max_span = 0;
         arena.clear();
     }
@@ -596,6 +626,296 @@ void read_bam(const spp_file *f, int32_t tid, const spp_params &p, Reads &R) {
     if (s.avail()) throw std::runtime_error("truncated BAM record");
 }
 
+// ---------------------------------------------------------------------------------------------
+// Records plans (spp_pileup_plan_records): the whole BAM inflated into one host buffer that goes to HBM
+// as is; the GPU decodes bases / qualities and walks the CIGARs (spg_accumulate_records).
+// ---------------------------------------------------------------------------------------------
+spp_alloc_fn g_alloc = nullptr;
+spp_free_fn g_free = nullptr;
+
+struct HostBuf {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    spp_free_fn fr = nullptr;      // allocator hook's release (null: free())
+    void release() {
+        if (!p) return;
+        if (fr) fr(p);
+        else free(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+// Recycled buffers (pinned allocations cost ~0.2 s per GB; a 10,000x SARS-CoV-2 BAM inflates to ~0.6 GB)
+std::mutex &g_buf_mu = *new std::mutex;
+std::vector<HostBuf> &g_bufs = *new std::vector<HostBuf>;
+
+HostBuf buf_get(size_t need, bool pinned = true) {
+    const spp_free_fn want = pinned ? g_free : nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_buf_mu);
+        size_t best = SIZE_MAX;
+        for (size_t i = 0; i < g_bufs.size(); i++)
+            if (g_bufs[i].cap >= need && g_bufs[i].fr == want && (best == SIZE_MAX || g_bufs[i].cap < g_bufs[best].cap))
+                best = i;
+        if (best != SIZE_MAX) {
+            HostBuf b = g_bufs[best];
+            g_bufs.erase(g_bufs.begin() + (long)best);
+            return b;
+        }
+    }
+    HostBuf b;
+    b.cap = ((need + need / 16) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    if (g_alloc && pinned) {
+        void *q = nullptr;
+        if (g_alloc(b.cap, &q) != 0 || !q) throw std::runtime_error("host allocator failed");
+        b.p = (uint8_t *)q;
+        b.fr = g_free;
+    } else {
+        b.p = (uint8_t *)aligned_alloc(4096, b.cap);
+        if (!b.p) throw std::runtime_error("out of host memory for the BAM records");
+    }
+    return b;
+}
+
+void buf_put(HostBuf &b) {
+    if (!b.p) return;
+    std::lock_guard<std::mutex> lk(g_buf_mu);
+    size_t held = 0;
+    for (auto &x : g_bufs) held += x.cap;
+    if ((b.fr == g_free || !b.fr) && g_bufs.size() < 12 && held + b.cap <= ((size_t)6 << 30)) g_bufs.push_back(b);
+    else b.release();
+    b = HostBuf{};
+}
+
+// Parallel chunked loop: fn(t, i0, i1) on nt threads over [0, n)
+template <class Fn> void par_chunks(size_t n, int nt, Fn &&fn) {
+    nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, (n + 16383) / 16384));
+    std::vector<std::thread> pool;
+    std::exception_ptr err;
+    std::mutex emu;
+    auto run = [&](int t) {
+        try {
+            fn(t, n * (size_t)t / (size_t)nt, n * (size_t)(t + 1) / (size_t)nt);
+        } catch (...) {
+            std::lock_guard<std::mutex> lk(emu);
+            if (!err) err = std::current_exception();
+        }
+    };
+    for (int t = 1; t < nt; t++) pool.emplace_back(run, t);
+    run(0);
+    for (auto &t : pool) t.join();
+    if (err) std::rethrow_exception(err);
+}
+
+// The BAM mapped, its BGZF members located, inflated in parallel straight into `out` (the helpers take
+// members in file order; this thread scans the records as the inflated prefix grows, inflating members
+// itself while it waits), then the kept records' fixed fields parsed in parallel.  Bases and qualities
+// stay packed in `out`.
+size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &R, HostBuf &out) {
+    const int nt = std::max(1, std::min(p.n_threads, 64));
+    const auto tm0 = std::chrono::steady_clock::now();
+    const int fd = open(f->path.c_str(), O_RDONLY);
+    if (fd < 0) throw std::runtime_error("cannot open " + f->path);
+    struct stat st;
+    if (fstat(fd, &st) != 0) { close(fd); throw std::runtime_error("cannot stat " + f->path); }
+    const size_t fsz = (size_t)st.st_size;
+    if (fsz == 0) { close(fd); throw std::runtime_error("not a BAM file"); }
+    void *mp = mmap(nullptr, fsz, PROT_READ, MAP_PRIVATE, fd, 0);
+    close(fd);
+    if (mp == MAP_FAILED) throw std::runtime_error("cannot map " + f->path);
+    // (unmapped on a helper thread: tearing down the mapped pages took 5-12 ms per 0.2 GB; parallel preads into a
+    // buffer instead of the mapping were slower still, 4 GB/s)
+    struct Unmap {
+        void *m; size_t n;
+        ~Unmap() {
+            try { std::thread([m = m, n = n] { munmap(m, n); }).detach(); } catch (...) { munmap(m, n); }
+        }
+    } unmap{mp, fsz};
+    const uint8_t *m = (const uint8_t *)mp;
+    struct Blk { size_t off, clen, ulen; };
+    std::vector<Blk> blks;
+    // Members located in parallel: each thread finds the first member header in its byte range (a BGZF header
+    // whose BSIZE chain reaches the next header), walks the chain to the next thread's start, and the chains
+    // must meet exactly; otherwise (a false header inside compressed data, a damaged file) the serial walk
+    // below locates them and reports the error.
+    auto member = [&](size_t q, Blk *bk) -> size_t {      // member size at q, 0 if no valid header there
+        if (q + 18 > fsz) return 0;
+        const uint8_t *h = m + q;
+        if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) return 0;
+        const size_t xlen = h[10] | (h[11] << 8);
+        size_t bsize = 0;
+        for (size_t x = 12; x + 4 <= 12 + xlen && q + x + 4 <= fsz;) {
+            const size_t slen = h[x + 2] | (h[x + 3] << 8);
+            if (h[x] == 66 && h[x + 1] == 67 && slen == 2 && q + x + 6 <= fsz) bsize = (h[x + 4] | (h[x + 5] << 8)) + 1;
+            x += 4 + slen;
+        }
+        if (!bsize || q + bsize > fsz || bsize < xlen + 20) return 0;
+        if (bk) *bk = {q + 12 + xlen, bsize - xlen - 20, (size_t)h[bsize - 4] | ((size_t)h[bsize - 3] << 8) |
+                                                             ((size_t)h[bsize - 2] << 16) | ((size_t)h[bsize - 1] << 24)};
+        return bsize;
+    };
+    {
+        const int np = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, fsz >> 22));
+        std::vector<size_t> start((size_t)np + 1, fsz);
+        std::vector<std::vector<Blk>> part((size_t)np);
+        std::atomic<bool> ok{np > 1};
+        if (np > 1) {
+            par_chunks((size_t)np, np, [&](int, size_t t0, size_t t1) {
+                for (size_t t = t0; t < t1; t++) {
+                    if (t == 0) { start[0] = 0; continue; }
+                    for (size_t q = fsz * t / (size_t)np, e = fsz * (t + 1) / (size_t)np; q < e; q++) {
+                        const size_t bs = member(q, nullptr);
+                        if (bs && (q + bs == fsz || member(q + bs, nullptr))) { start[t] = q; break; }
+                    }
+                }
+            });
+            for (int t = np - 1; t >= 1; t--) start[(size_t)t] = std::min(start[(size_t)t], start[(size_t)t + 1]);
+            par_chunks((size_t)np, np, [&](int, size_t t0, size_t t1) {
+                for (size_t t = t0; t < t1; t++) {
+                    size_t q = start[t];
+                    Blk bk;
+                    while (q < start[t + 1]) {
+                        const size_t bs = member(q, &bk);
+                        if (!bs) { ok = false; break; }
+                        part[t].push_back(bk);
+                        q += bs;
+                    }
+                    if (q != start[t + 1]) ok = false;
+                }
+            });
+        }
+        if (ok)
+            for (auto &v : part) blks.insert(blks.end(), v.begin(), v.end());
+    }
+    for (size_t q = blks.empty() ? 0 : fsz; q < fsz;) {
+        if (q + 18 > fsz) throw std::runtime_error("truncated BGZF file");
+        const uint8_t *h = m + q;
+        if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) throw std::runtime_error("not a BGZF block");
+        const size_t xlen = h[10] | (h[11] << 8);
+        size_t bsize = 0;
+        for (size_t x = 12; x + 4 <= 12 + xlen && q + x + 4 <= fsz;) {
+            const size_t slen = h[x + 2] | (h[x + 3] << 8);
+            if (h[x] == 66 && h[x + 1] == 67 && slen == 2 && q + x + 6 <= fsz) bsize = (h[x + 4] | (h[x + 5] << 8)) + 1;
+            x += 4 + slen;
+        }
+        if (!bsize) throw std::runtime_error("BGZF block without BSIZE");
+        if (q + bsize > fsz || bsize < xlen + 20) throw std::runtime_error("truncated BGZF file");
+        const size_t ulen = (size_t)h[bsize - 4] | ((size_t)h[bsize - 3] << 8) | ((size_t)h[bsize - 2] << 16) |
+                            ((size_t)h[bsize - 1] << 24);
+        blks.push_back({q + 12 + xlen, bsize - xlen - 20, ulen});
+        q += bsize;
+    }
+    const size_t nb = blks.size();
+    std::vector<size_t> uoff(nb + 1, 0);
+    for (size_t i = 0; i < nb; i++) uoff[i + 1] = uoff[i] + blks[i].ulen;
+    const size_t total = uoff[nb];
+    const auto tm1 = std::chrono::steady_clock::now();
+    out = buf_get(total + 64);
+    const auto tm2 = std::chrono::steady_clock::now();
+    uint8_t *buf = out.p;
+    memset(buf + total, 0, 64);
+    std::unique_ptr<std::atomic<uint8_t>[]> done(new std::atomic<uint8_t>[nb ? nb : 1]);
+    for (size_t i = 0; i < nb; i++) done[i].store(0, std::memory_order_relaxed);
+    std::atomic<size_t> next{0};
+    std::atomic<bool> bad{false};
+    auto inflate_one = [&](Inflater &inf, size_t i) {
+        if (blks[i].ulen && !inf.run(m + blks[i].off, blks[i].clen, buf + uoff[i], blks[i].ulen)) bad = true;
+        done[i].store(1, std::memory_order_release);
+    };
+    std::vector<std::thread> pool;
+    struct Join { std::vector<std::thread> &v; std::atomic<size_t> &nx; size_t n;
+                  ~Join() { nx = n; for (auto &t : v) if (t.joinable()) t.join(); } } join{pool, next, nb};
+    for (int t = 1; t < nt; t++)
+        pool.emplace_back([&] {
+            Inflater inf;
+            for (size_t i; (i = next++) < nb;) inflate_one(inf, i);
+        });
+    Inflater minf;
+    size_t ready = 0, nready = 0;
+    auto avail_to = [&](size_t end) -> bool {   // bytes [0, end) inflated (false: past the end of the BAM)
+        while (ready < end) {
+            if (bad) throw std::runtime_error("BGZF inflate failed");
+            if (nready < nb && done[nready].load(std::memory_order_acquire)) { ready = uoff[++nready]; continue; }
+            if (nready == nb) return false;
+            const size_t i = next++;
+            if (i < nb) inflate_one(minf, i);
+            else std::this_thread::yield();
+        }
+        return true;
+    };
+    if (!avail_to(12) || memcmp(buf, "BAM\1", 4) != 0) throw std::runtime_error("not a BAM file");
+    size_t cur = 8 + (size_t)(uint32_t)rd32(buf + 4);
+    if (!avail_to(cur + 4)) throw std::runtime_error("truncated BAM header");
+    const int32_t n_ref = rd32(buf + cur);
+    cur += 4;
+    for (int32_t i = 0; i < n_ref; i++) {
+        if (!avail_to(cur + 4)) throw std::runtime_error("truncated BAM header");
+        const size_t l_name = (size_t)(uint32_t)rd32(buf + cur);
+        if (!avail_to(cur + 8 + l_name)) throw std::runtime_error("truncated BAM header");
+        cur += 8 + l_name;
+    }
+    int64_t last_pos = -1;
+    static const bool timing = getenv("SPP_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (avail_to(cur + 4)) {
+        const uint32_t bs = rdu32(buf + cur);
+        if (bs < 32 || !avail_to(cur + 4 + (size_t)bs)) throw std::runtime_error("truncated BAM record");
+        const uint8_t *b = buf + cur + 4;
+        if (rd32(b) == tid) {
+            const int64_t pos = rd32(b + 4);
+            if (pos < last_pos) throw std::runtime_error("BAM is not coordinate-sorted");
+            last_pos = pos;
+            if (stepper_keeps(p, rdu16(b + 14), b[9])) R.rec.push_back(cur + 4);
+        }
+        cur += 4 + (size_t)bs;
+    }
+    if (cur != total) throw std::runtime_error("truncated BAM record");
+    const auto t1 = std::chrono::steady_clock::now();
+    R.raw = buf;
+    // fixed fields of the kept records, in parallel (names and CIGARs stay in place: Reads::name / Reads::cig)
+    const size_t k = R.rec.size();
+    R.pos.resize(k); R.end.resize(k); R.flag.resize(k); R.mapq.resize(k); R.mtid.resize(k); R.mpos.resize(k);
+    R.isize.resize(k); R.n_cig.resize(k); R.bases.resize(k); R.l_seq.resize(k);
+    const int nw = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, (k + 16383) / 16384));
+    std::vector<int64_t> spans((size_t)nw, 0);
+    par_chunks(k, nw, [&](int t, size_t i0, size_t i1) {
+        int64_t span = 0;
+        for (size_t i = i0; i < i1; i++) {
+            const uint8_t *b = buf + R.rec[i];
+            const uint32_t bs = rdu32(b - 4), n_cig = rdu16(b + 12), l_name = b[8];
+            const int32_t l_seq = rd32(b + 16);
+            if (l_seq < 0 || 32ull + l_name + 4ull * n_cig + ((uint64_t)l_seq + 1) / 2 + (uint64_t)l_seq > bs)
+                throw std::runtime_error("corrupt BAM record (field lengths exceed block_size)");
+            R.n_cig[i] = n_cig;
+            R.l_seq[i] = (uint32_t)l_seq;
+            R.pos[i] = rd32(b + 4);
+            R.mapq[i] = b[9];
+            R.flag[i] = rdu16(b + 14);
+            R.mtid[i] = rd32(b + 20);
+            R.mpos[i] = rd32(b + 24);
+            R.isize[i] = rd32(b + 28);
+            const uint8_t *cg = b + 32 + l_name;
+            int64_t rl = 0;
+            for (uint32_t j = 0; j < n_cig; j++) {
+                const uint32_t c = rdu32(cg + 4 * (size_t)j);
+                if (consumes_ref(c & 0xF)) rl += c >> 4;
+            }
+            R.end[i] = R.pos[i] + rl;
+            span = std::max(span, rl);
+            R.bases[i] = R.decode(R.pos[i], R.end[i]) ? const_cast<uint8_t *>(b) : nullptr;
+        }
+        spans[(size_t)t] = span;
+    });
+    for (int64_t v : spans) R.max_span = std::max(R.max_span, v);
+    if (timing)
+        fprintf(stderr, "[spp timing] read_bam_raw: %zu members, map+members %.1f ms, buffer %.1f ms, inflate+scan %.1f ms, "
+                "fields %.1f ms\n", nb, std::chrono::duration<double, std::milli>(tm1 - tm0).count(),
+                std::chrono::duration<double, std::milli>(tm2 - tm1).count(),
+                std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
+    return total;
+}
+
 void sam_header_line(spp_file *f, const std::string &line) {
     if (line.compare(0, 3, "@SQ") != 0) return;
     Target t;
@@ -701,9 +1021,8 @@ void tweak_overlap(Reads &R, size_t a, size_t b) {
     auto aligned = [&](size_t r, std::vector<std::pair<int64_t, uint32_t>> &out) {
         int64_t x = R.pos[r];
         uint32_t y = 0;
-        const uint32_t *c = R.cigar.data() + R.cig_off[r];
         for (uint32_t i = 0; i < R.n_cig[r]; i++) {
-            const uint32_t op = c[i] & 0xF, l = c[i] >> 4;
+            const uint32_t c = R.cig(r, i), op = c & 0xF, l = c >> 4;
             if (op == C_M || op == C_EQ || op == C_X)
                 for (uint32_t k = 0; k < l; k++) out.emplace_back(x + k, y + k);
             if (consumes_ref(op)) x += l;
@@ -720,7 +1039,7 @@ void tweak_overlap(Reads &R, size_t a, size_t b) {
         const uint32_t ia = pa[i].second, ib = pb[j].second;
         if (ia >= R.l_seq[a] || ib >= R.l_seq[b]) return;
         uint8_t &qa = R.qual(a)[ia], &qb = R.qual(b)[ib];
-        if (R.seq(a)[ia] == R.seq(b)[ib]) {
+        if (R.base(a, ia) == R.base(b, ib)) {
             const int q = qa + qb;
             qa = (uint8_t)(q > 200 ? 200 : q);
             qb = 0;
@@ -821,7 +1140,7 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
     int64_t it_pos = 0, max_pos = -1;
     bool started = tid == 0;
     std::unordered_map<std::string, size_t> olap;
-    auto name = [&](size_t r) { return std::string(R.names.data() + R.name_off[r]); };
+    auto name = [&](size_t r) { return R.name(r); };
     auto olap_remove = [&](size_t r) {
         if (!p.ignore_overlaps || olap.empty()) return;
         auto itr = olap.find(name(r));
@@ -894,9 +1213,18 @@ struct spp_plan {
     Tweaks T;
     std::vector<size_t> kept;      // reads with entries in the batch's columns, in BAM order
     int64_t rlo = INT64_MIN, rhi = INT64_MAX;
+    // records plan: the inflated BAM (R.raw) and the per-read index + CSR offsets handed to the GPU
+    bool raw = false;
+    HostBuf data, idx;
+    size_t data_len = 0;           // inflated bytes in `data`
+    spg_records view{};
     void clear() {
         R.clear(); keep.clear(); T.col.clear(); T.orig.clear(); kept.clear();
         rlo = INT64_MIN; rhi = INT64_MAX;
+        buf_put(data);
+        buf_put(idx);
+        raw = false;
+        view = spg_records{};
     }
 };
 
@@ -936,35 +1264,62 @@ void release_plan(spp_plan *p) {
 
 namespace {
 
-// CSR offsets of the kept reads' columns (the batch's entry count is known after this)
-void plan_csr(spp_plan &P, spp_batch *B) {
+// CSR offsets of the kept reads' columns (the batch's entry count is known after this).  Parallel over read
+// chunks: the column range by reduction, the coverage difference array per thread when it is small (else one
+// shared array, serially), the kept list by chunk counts.
+void plan_csr(spp_plan &P, spp_batch *B, int threads) {
     const Reads &R = P.R;
     const std::vector<uint8_t> &keep = P.keep;
     const int64_t rlo = P.rlo, rhi = P.rhi;
-    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    const size_t n = R.size();
     auto inreg = [&](size_t r) { return keep[r] && R.end[r] > R.pos[r] && R.end[r] > rlo && R.pos[r] < rhi; };
-    for (size_t r = 0; r < R.size(); r++)
-        if (inreg(r)) { lo = std::min(lo, std::max(R.pos[r], rlo)); hi = std::max(hi, std::min(R.end[r], rhi)); }
+    const int nw = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, threads), (n + 65535) / 65536));
+    std::vector<int64_t> tlo((size_t)nw, INT64_MAX), thi((size_t)nw, INT64_MIN);
+    std::vector<size_t> tcnt((size_t)nw + 1, 0);
+    par_chunks(n, nw, [&](int t, size_t i0, size_t i1) {
+        int64_t a = INT64_MAX, z = INT64_MIN;
+        size_t k = 0;
+        for (size_t r = i0; r < i1; r++)
+            if (inreg(r)) { a = std::min(a, std::max(R.pos[r], rlo)); z = std::max(z, std::min(R.end[r], rhi)); k++; }
+        tlo[(size_t)t] = a;
+        thi[(size_t)t] = z;
+        tcnt[(size_t)t + 1] = k;
+    });
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (int t = 0; t < nw; t++) { lo = std::min(lo, tlo[(size_t)t]); hi = std::max(hi, thi[(size_t)t]); }
+    for (int t = 0; t < nw; t++) tcnt[(size_t)t + 1] += tcnt[(size_t)t];
     if (lo == INT64_MAX) { lo = 0; hi = 0; }
     const int64_t C = hi - lo;
     B->pos_begin = lo;
     B->n_cols = C;
-    std::vector<int64_t> diff((size_t)C + 1, 0);
-    for (size_t r = 0; r < R.size(); r++)
-        if (inreg(r)) {
-            diff[(size_t)(std::max(R.pos[r], lo) - lo)]++;
-            diff[(size_t)(std::min(R.end[r], hi) - lo)]--;
-        }
+    const bool per_thread = nw > 1 && (uint64_t)(C + 1) * (uint64_t)nw <= ((uint64_t)1 << 24);
+    std::vector<std::vector<int64_t>> tdiff(per_thread ? (size_t)nw : 1);
+    P.kept.resize(tcnt[(size_t)nw]);
+    auto scatter = [&](int t, size_t i0, size_t i1, std::vector<int64_t> &diff) {
+        size_t k = tcnt[(size_t)t];
+        for (size_t r = i0; r < i1; r++)
+            if (inreg(r)) {
+                diff[(size_t)(std::max(R.pos[r], lo) - lo)]++;
+                diff[(size_t)(std::min(R.end[r], hi) - lo)]--;
+                P.kept[k++] = r;
+            }
+    };
+    if (per_thread) {
+        par_chunks(n, nw, [&](int t, size_t i0, size_t i1) {
+            tdiff[(size_t)t].assign((size_t)C + 1, 0);
+            scatter(t, i0, i1, tdiff[(size_t)t]);
+        });
+    } else {
+        tdiff[0].assign((size_t)C + 1, 0);
+        for (int t = 0; t < nw; t++) scatter(t, n * (size_t)t / (size_t)nw, n * (size_t)(t + 1) / (size_t)nw, tdiff[0]);
+    }
     B->off.assign((size_t)C + 1, 0);
     int64_t run = 0;
     for (int64_t c = 0; c < C; c++) {
-        run += diff[(size_t)c];
+        for (auto &d : tdiff) run += d[(size_t)c];
         B->off[(size_t)c + 1] = B->off[(size_t)c] + (uint64_t)run;
     }
     B->n_entries = B->off[(size_t)C];
-    P.kept.clear();
-    for (size_t r = 0; r < R.size(); r++)
-        if (inreg(r)) P.kept.push_back(r);
 }
 
 // base_code / qual of every entry into code / qual (>= n_entries + 16 bytes each)
@@ -1027,6 +1382,85 @@ void fill_csr(const spp_plan &P, spp_batch *B, uint8_t *code, uint8_t *qual, int
     for (int t = 1; t < nt; t++) pool.emplace_back(work, t);
     work(0);
     for (auto &t : pool) t.join();
+}
+
+// The records plan's GPU view: per kept read its record offset, span and tweak index; the tweaked reads'
+// original qualities; the CSR offsets — one host buffer (pinned under the allocator hook).
+void plan_records(spp_plan &P, spp_batch *B, int threads) {
+    const Reads &R = P.R;
+    const std::vector<size_t> &kept = P.kept;
+    const size_t n = kept.size();
+    if (n >= ((size_t)1 << 31)) throw std::runtime_error("more than 2^31 reads in one batch");
+    std::vector<int32_t> tw;            // per kept read: tweak index (only when some read was tweaked)
+    std::vector<size_t> tw_read;
+    uint64_t orig_bytes = 0;
+    if (!P.T.orig.empty()) {
+        tw.assign(n, -1);
+        for (size_t i = 0; i < n; i++) {
+            const size_t r = kept[i];
+            if (P.T.col[r] != INT64_MAX) {
+                tw[i] = (int32_t)tw_read.size();
+                tw_read.push_back(r);
+                orig_bytes += R.l_seq[r];
+            }
+        }
+    }
+    const size_t nt = tw_read.size(), C = (size_t)B->n_cols;
+    auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
+    const size_t o_off = 0, o_rec = al(o_off + 8 * (C + 1)), o_pos = al(o_rec + 8 * n), o_end = al(o_pos + 4 * n),
+                 o_tw = al(o_end + 4 * n), o_tcol = al(o_tw + 4 * n), o_tq = al(o_tcol + 8 * nt),
+                 o_orig = al(o_tq + 8 * nt), bytes = al(o_orig + orig_bytes) + 64;
+    P.idx = buf_get(bytes);
+    uint8_t *m = P.idx.p;
+    uint64_t *off = (uint64_t *)(m + o_off), *rec = (uint64_t *)(m + o_rec), *tq = (uint64_t *)(m + o_tq);
+    int32_t *rpos = (int32_t *)(m + o_pos), *rend = (int32_t *)(m + o_end), *twi = (int32_t *)(m + o_tw);
+    int64_t *tcol = (int64_t *)(m + o_tcol);
+    uint8_t *orig = m + o_orig;
+    memcpy(off, B->off.data(), 8 * (C + 1));
+    const int nw = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, threads), (n + 65535) / 65536));
+    std::vector<int64_t> spans((size_t)nw, 0);
+    par_chunks(n, nw, [&](int t, size_t i0, size_t i1) {
+        int64_t sp = 0;
+        for (size_t i = i0; i < i1; i++) {
+            const size_t r = kept[i];
+            rec[i] = R.rec[r];
+            rpos[i] = (int32_t)R.pos[r];
+            rend[i] = (int32_t)R.end[r];
+            twi[i] = tw.empty() ? -1 : tw[i];
+            sp = std::max(sp, R.end[r] - R.pos[r]);
+        }
+        spans[(size_t)t] = sp;
+    });
+    int64_t span = 0;
+    for (int64_t v : spans) span = std::max(span, v);
+    uint64_t oq = 0;
+    for (size_t j = 0; j < nt; j++) {
+        const size_t r = tw_read[j];
+        tcol[j] = P.T.col[r];
+        tq[j] = oq;
+        const std::vector<uint8_t> &o = P.T.orig.at(r);
+        memcpy(orig + oq, o.data(), o.size());
+        oq += o.size();
+    }
+    spg_records &v = P.view;
+    v = spg_records{};
+    v.pos_begin = B->pos_begin;
+    v.n_cols = B->n_cols;
+    v.n_entries = B->n_entries;
+    v.offsets = off;
+    v.data = P.data.p;
+    v.data_bytes = P.data_len;
+    v.n_reads = (int64_t)n;
+    v.rec = rec;
+    v.rpos = rpos;
+    v.rend = rend;
+    v.tweak = twi;
+    v.n_tweaks = (int64_t)nt;
+    v.tweak_col = tcol;
+    v.tweak_qual = tq;
+    v.orig_qual = orig;
+    v.orig_bytes = orig_bytes;
+    v.max_span = span;
 }
 
 
@@ -1171,8 +1605,10 @@ int spp_target_id(spp_file *f, const char *name, int32_t *tid) {
     return 0;
 }
 
-static int plan_impl(spp_file *f, int32_t tid, const spp_params *p, int64_t lo, int64_t hi, spp_batch **out) {
+static int plan_impl(spp_file *f, int32_t tid, const spp_params *p, int64_t lo, int64_t hi, spp_batch **out,
+                     bool raw = false) {
     if (!f || !p || !out) return fail("spp_pileup: null argument");
+    if (raw && !f->bam) return fail("spp_pileup_plan_records: the device-decode plan needs a BAM (this is SAM text)");
     if (tid < 0 || (size_t)tid >= f->targets.size()) return fail("spp_pileup: tid out of range");
     if (lo >= hi) return fail("spp_pileup_region: empty region");
     *out = nullptr;
@@ -1190,8 +1626,14 @@ static int plan_impl(spp_file *f, int32_t tid, const spp_params *p, int64_t lo, 
             P = plan_get();
             Reads &R = P->R;
             if (region) { R.dlo = lo == INT64_MIN ? lo : lo - pad; R.dhi = hi == INT64_MAX ? hi : hi + pad; }
-            if (f->bam) read_bam(f, tid, *p, R);
-            else read_sam(f, tid, *p, R);
+            if (raw) {
+                P->raw = true;
+                P->data_len = read_bam_raw(f, tid, *p, R, P->data);
+            } else if (f->bam) {
+                read_bam(f, tid, *p, R);
+            } else {
+                read_sam(f, tid, *p, R);
+            }
             if (region && R.max_span > pad) {
                 pad = 2 * R.max_span;
                 release_plan(P);
@@ -1209,14 +1651,17 @@ static int plan_impl(spp_file *f, int32_t tid, const spp_params *p, int64_t lo, 
             B->threads = std::max(1, p->n_threads);
             P->rlo = lo;
             P->rhi = hi;
-            plan_csr(*P, B);
+            plan_csr(*P, B, B->threads);
+            const auto t3 = now();
+            if (raw) plan_records(*P, B, B->threads);
             B->plan = P;
             P = nullptr;
             if (timing) {
-                const auto t3 = now();
+                const auto t4 = now();
                 auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
-                fprintf(stderr, "[spp timing] read %.1f ms, simulate %.1f ms, offsets %.1f ms (%zu reads, %d threads)\n",
-                        ms(t0, t1), ms(t1, t2), ms(t2, t3), (size_t)B->plan->R.size(), p->n_threads);
+                fprintf(stderr, "[spp timing] read %.1f ms, simulate %.1f ms, offsets %.1f ms, records index %.1f ms "
+                        "(%zu reads, %d threads)\n", ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4),
+                        (size_t)B->plan->R.size(), p->n_threads);
             }
             *out = B;
             return 0;
@@ -1230,6 +1675,7 @@ static int plan_impl(spp_file *f, int32_t tid, const spp_params *p, int64_t lo, 
 int spp_batch_fill(spp_batch *b, uint8_t *base_code, uint8_t *qual) {
     if (!b) return fail("spp_batch_fill: null batch");
     if (!b->plan) return fail("spp_batch_fill: the batch is already filled");
+    if (b->plan->raw) return fail("spp_batch_fill: a records plan is filled on the GPU (spg_accumulate_records)");
     if ((base_code == nullptr) != (qual == nullptr)) return fail("spp_batch_fill: give both buffers or neither");
     try {
         static const bool timing = getenv("SPP_TIMING") != nullptr;
@@ -1262,6 +1708,27 @@ int spp_batch_fill(spp_batch *b, uint8_t *base_code, uint8_t *qual) {
 
 int spp_pileup_plan(spp_file *f, int32_t tid, int64_t lo, int64_t hi, const spp_params *p, spp_batch **out) {
     return plan_impl(f, tid, p, lo, hi, out);
+}
+
+int spp_pileup_plan_records(spp_file *f, int32_t tid, int64_t lo, int64_t hi, const spp_params *p, spp_batch **out) {
+    return plan_impl(f, tid, p, lo, hi, out, true);
+}
+
+int spp_batch_records(spp_batch *b, spg_records *out) {
+    if (!b || !out) return fail("spp_batch_records: null argument");
+    if (!b->plan || !b->plan->raw) return fail("spp_batch_records: not a records plan (spp_pileup_plan_records)");
+    *out = b->plan->view;
+    return 0;
+}
+
+int spp_set_host_allocator(spp_alloc_fn alloc, spp_free_fn release) {
+    if ((alloc == nullptr) != (release == nullptr)) return fail("spp_set_host_allocator: give both or neither");
+    std::lock_guard<std::mutex> lk(g_buf_mu);
+    for (auto &b : g_bufs) b.release();     // pooled buffers of the previous allocator
+    g_bufs.clear();
+    g_alloc = alloc;
+    g_free = release;
+    return 0;
 }
 
 static int pileup_impl(spp_file *f, int32_t tid, const spp_params *p, int64_t lo, int64_t hi, spp_batch **out) {

@@ -184,6 +184,15 @@ class PileupEngine:
                 flags = N.SPG_IN_DEVICE | (N.SPG_IN_BORROW if borrow else 0)
             N.check(self._L.spg_accumulate_batches(self._h, N.ptr(rec), len(rec), flags), "spg_accumulate_batches")
 
+    def accumulate_bam_records(self, batch):
+        """process_bam's accumulate step from a records plan (pileup.AlignmentFile.pileup_records): the inflated
+        BAM and per-read index go to HBM and the device-side pileup writes the batch (spg_accumulate_records).
+        Pinned plan buffers are copied asynchronously: keep ``batch`` open until wait_ticket(input_ticket())
+        taken after this call returns."""
+        r = batch.records()
+        with self._lock:
+            N.check(self._L.spg_accumulate_records(self._h, C.byref(r), 0), "spg_accumulate_records")
+
     def wait_input(self):
         """Block until every input copy enqueued so far has landed (pinned host buffers are free)."""
         with self._lock:

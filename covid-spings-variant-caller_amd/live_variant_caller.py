@@ -22,6 +22,7 @@ libspings_gpu.so or a GPU the constructor raises.
 """
 from __future__ import annotations
 
+import collections
 import logging
 import os
 import threading
@@ -159,19 +160,35 @@ class LiveVariantCaller:
         self._lock = threading.RLock()
         self._ingest = PinnedIngest(self.engine)
         self._batch_contig: List[int] = []       # FASTA reference index of each accumulated batch
+        # device-side pileup: a BAM's records go to HBM and the GPU decodes bases / qualities and
+        # walks the CIGARs (spg_accumulate_records); the host keeps the read filter, depth cap and overlap
+        # tweak.  SPG_DEVICE_PILEUP=0 selects the host fill (SAM input always uses it).
+        self.device_pileup = os.environ.get("SPG_DEVICE_PILEUP", "1") != "0"
+        if self.device_pileup:
+            N.use_pinned_records()
+        self._inflight = collections.deque()     # (input ticket, records plan) whose copy may still be running
         self.reset_memory()
 
     def __del__(self):
         try:
+            self._drain()
             self.fastaFile.close()
             self.engine.close()
         except Exception:
             pass
 
     # -- memory -------------------------------------------------------------------------------
+    def _drain(self, keep: int = 0):
+        """Close the records plans whose inputs have landed in HBM (all but the newest ``keep``)."""
+        while len(self._inflight) > keep:
+            t, b = self._inflight.popleft()
+            self.engine.wait_ticket(t)
+            b.close()
+
     def reset_memory(self):
         """:37-38"""
         with self._lock:
+            self._drain()
             self.engine.reset()
             self._batch_contig = []
             self._current_ref = None
@@ -230,7 +247,10 @@ class LiveVariantCaller:
         with AlignmentFile(inputBam) as bam:
             if contig not in bam.references:
                 raise ValueError(f"invalid contig `{contig}`")
-            batch = bam.pileup_plan(contig, self.pileup_params)
+            if self.device_pileup and _is_bgzf(inputBam):
+                batch = bam.pileup_records(contig, self.pileup_params)
+            else:
+                batch = bam.pileup_plan(contig, self.pileup_params)
         # the entries go straight into pinned staging (double-buffered): the copy to HBM runs on the engine's
         # copy stream while the next BAM is read
         self._accumulate_plan(batch, referenceIndex)
@@ -256,6 +276,8 @@ class LiveVariantCaller:
             with AlignmentFile(path) as bam:
                 if contig not in bam.references:
                     raise ValueError(f"invalid contig `{contig}`")
+                if self.device_pileup and _is_bgzf(path):
+                    return bam.pileup_records(contig, params)
                 return bam.pileup_plan(contig, params)
 
         window = 2 * workers                  # plans in flight (each holds its BAM's decoded reads)
@@ -270,6 +292,17 @@ class LiveVariantCaller:
 
     def _accumulate_plan(self, batch, referenceIndex):
         with self._lock:
+            if batch.is_records:
+                if batch.n_cols == 0:
+                    batch.close()
+                    return
+                self._use_reference(referenceIndex)
+                self.engine.accumulate_bam_records(batch)
+                # the plan's pinned buffers are copied on the engine's copy stream: keep them until that copy lands
+                self._inflight.append((self.engine.input_ticket(), batch))
+                self._drain(keep=2)
+                self._batch_contig.append(referenceIndex)
+                return
             if batch.n_cols == 0:
                 batch.fill()
                 batch.close()
@@ -287,6 +320,7 @@ class LiveVariantCaller:
     def prepare_variants(self) -> List[Variant]:
         """:120-231"""
         with self._lock:
+            self._drain()
             self.engine.finalize()
             return self.engine.variants()
 
@@ -355,6 +389,11 @@ INFO_META = [
                            "defined precisely as the GL field)"),
     ("SCORE", "1", "Float", "Custom scoring function"),
 ]
+
+
+def _is_bgzf(path: str) -> bool:
+    with open(path, "rb") as f:
+        return f.read(2) == b"\x1f\x8b"
 
 
 def _bq_compact(off, codes, quals, min_bq: int):

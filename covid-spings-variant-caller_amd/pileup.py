@@ -43,8 +43,9 @@ class PileupBatch:
     """CSR batch owned by the native library: ``offsets`` u64[n_cols+1], ``codes``/``quals`` u8[E]
     (16 padding bytes follow both arrays), columns [pos_begin, pos_begin + n_cols)."""
 
-    def __init__(self, handle, planned=False):
+    def __init__(self, handle, planned=False, records=False):
         L = N.pileup_lib()
+        self.is_records = bool(records)
         self._h = C.c_void_p(handle)
         pb, nc, ne, nu, nd = C.c_int64(), C.c_int64(), C.c_uint64(), C.c_int64(), C.c_int64()
         N.pcheck(L.spp_batch_info(self._h, C.byref(pb), C.byref(nc), C.byref(ne), C.byref(nu), C.byref(nd)),
@@ -70,6 +71,14 @@ class PileupBatch:
             N.pcheck(L.spp_batch_fill(self._h, None, None), "spp_batch_fill")
         self._arrays()
         return self
+
+    def records(self) -> N.SpgRecords:
+        """The records plan's spg_records view (valid until close())."""
+        if not self.is_records:
+            raise ValueError("records(): not a records plan (AlignmentFile.pileup_records)")
+        r = N.SpgRecords()
+        N.pcheck(N.pileup_lib().spp_batch_records(self._h, C.byref(r)), "spp_batch_records")
+        return r
 
     def _arrays(self):
         L = N.pileup_lib()
@@ -148,6 +157,21 @@ class AlignmentFile:
         hi = (1 << 63) - 1 if stop is None else int(stop)
         N.pcheck(L.spp_pileup_plan(self._h, tid.value, lo, hi, C.byref(prm), C.byref(b)), "pileup")
         return PileupBatch(b.value, planned=True)
+
+    def pileup_records(self, reference: str, params: PileupParams | None = None, start: int | None = None,
+                       stop: int | None = None) -> PileupBatch:
+        """Device-decode form of pileup_plan (spp_pileup_plan_records, BAM only): reads parsed, depth cap /
+        overlap tweak applied, CSR offsets known; the entries are written on the GPU from the raw records
+        (PileupEngine.accumulate_bam_records -> spg_accumulate_records)."""
+        L = N.pileup_lib()
+        tid = C.c_int32()
+        N.pcheck(L.spp_target_id(self._h, reference.encode(), C.byref(tid)), "pileup")
+        b = C.c_void_p()
+        prm = (params or PileupParams()).native()
+        lo = -(1 << 63) if start is None else int(start)
+        hi = (1 << 63) - 1 if stop is None else int(stop)
+        N.pcheck(L.spp_pileup_plan_records(self._h, tid.value, lo, hi, C.byref(prm), C.byref(b)), "pileup")
+        return PileupBatch(b.value, planned=True, records=True)
 
     def close(self):
         if self._h:

@@ -163,6 +163,35 @@ int spg_accumulate_samples(spg_ctx *ctx, int64_t pos_begin, int64_t n_cols, int6
                            const uint64_t *offsets, const uint32_t *first_sample, const uint8_t *base_code,
                            const uint8_t *qual, uint64_t n_entries, uint32_t flags);
 
+/* Device-side pileup (replaces the host CIGAR walk of process_bam, live_variant_caller.py:54-72
+ * driving pysam's pileup): one BAM contig's inflated records plus the host's per-read decisions
+ * (spp_pileup_plan_records: stepper filter, htslib depth cap, mate-overlap tweak, CSR offsets).  The
+ * engine copies the record bytes to HBM and a kernel decodes the packed bases / qualities, walks each
+ * read's CIGAR and writes the batch's base_code / qual in htslib column order (reads in BAM order per
+ * column; D = 16 / N = 17 with the next query base's quality, 0 past the read end) — bit-identical to
+ * spp_batch_fill of the same plan.  The batch is then accumulated like spg_accumulate_ex's. */
+typedef struct spg_records {
+    int64_t pos_begin, n_cols;     /* the batch's columns */
+    uint64_t n_entries;
+    const uint64_t *offsets;       /* n_cols + 1 */
+    const uint8_t *data;           /* inflated BAM bytes holding the records (64 readable bytes of padding past
+                                      data_bytes) */
+    uint64_t data_bytes;
+    int64_t n_reads;               /* the reads with entries in the columns, in BAM order (< 2^31) */
+    const uint64_t *rec;           /* per read: offset in data of its record's refID field */
+    const int32_t *rpos, *rend;    /* per read: first reference position, one past its CIGAR's last */
+    const int32_t *tweak;          /* per read: index into tweak_col / tweak_qual, or -1 */
+    int64_t n_tweaks;
+    const int64_t *tweak_col;      /* the read's D/N entries in columns < tweak_col read orig_qual (the
+                                      qualities before htslib's mate-overlap tweak; data holds the tweaked ones) */
+    const uint64_t *tweak_qual;    /* offset of the read's original qualities in orig_qual */
+    const uint8_t *orig_qual;
+    uint64_t orig_bytes;
+    int64_t max_span;              /* max(rend - rpos) */
+    int64_t reserved[4];
+} spg_records;
+int spg_accumulate_records(spg_ctx *ctx, const spg_records *r, uint32_t flags);
+
 /* Pinned (page-locked) host staging buffers for the CSR inputs (north_star: "SoA pinned buffers").
  * Inputs in pinned memory are copied asynchronously on the context's copy stream: spg_accumulate
  * returns after enqueue and the caller must not modify them until spg_wait_input (or spg_sync)

@@ -24,6 +24,7 @@
 #ifndef SPINGS_PILEUP_H
 #define SPINGS_PILEUP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -82,6 +83,21 @@ int spp_batch_free(spp_batch *b);
  * form: lo/hi as in spp_pileup_region (INT64_MIN / INT64_MAX = whole contig). */
 int spp_pileup_plan(spp_file *f, int32_t tid, int64_t lo, int64_t hi, const spp_params *p, spp_batch **out);
 int spp_batch_fill(spp_batch *b, uint8_t *base_code, uint8_t *qual);
+
+/* Device-decode form of spp_pileup_plan (BAM only): the BGZF members are inflated in parallel
+ * straight into one buffer, the records' fixed fields are parsed on the host (what the stepper filter, the
+ * depth cap and the overlap pairing decide on), and the packed bases / qualities are NOT decoded: the batch
+ * exposes the raw record bytes and per-read index as an spg_records (include/spings_gpu.h) for
+ * spg_accumulate_records, whose kernel writes the CSR entries.  The record buffer comes from the host
+ * allocator below when one is set (spg_host_alloc: pinned, so the copy to HBM is a DMA), else malloc; it is
+ * reused across plans.  spp_batch_fill is not available on such a batch. */
+struct spg_records;
+int spp_pileup_plan_records(spp_file *f, int32_t tid, int64_t lo, int64_t hi, const spp_params *p, spp_batch **out);
+int spp_batch_records(spp_batch *b, struct spg_records *out);
+/* Allocator for the record buffers (e.g. spg_host_alloc / spg_host_free); NULLs restore malloc/free. */
+typedef int (*spp_alloc_fn)(size_t bytes, void **out);
+typedef int (*spp_free_fn)(void *p);
+int spp_set_host_allocator(spp_alloc_fn alloc, spp_free_fn release);
 
 /* Synthetic read simulator (SURVEY.md §8 d "Synthetic inputs"): writes a coordinate-sorted BGZF
  * BAM of single-end reads (flag 0, MAPQ 60) over one contig — starts uniform on [0, L-read_len],

@@ -1,0 +1,178 @@
+"""Device-side pileup: spg_accumulate_records' kernel (csrc/spg_fill.hip)
+decodes the BAM records and walks their CIGARs on the GPU.  The batch it writes must be bit-identical to
+spp_batch_fill's host CSR of the same BAM (tests/test_pileup*.py pin that one against oracle/pileup_port.py
+and the hand-derived fixtures) — on every fixture those tests use: config 1's testfile.sam, the hand-derived
+cases, random reads with every CIGAR op / '*' SEQ+QUAL / stacks / overlapping pairs under each stepper and
+depth cap, regions, and the simulator's BAMs up to 10,000x.  Then process_bam through it vs the host fill."""
+import os
+
+import numpy as np
+import pytest
+
+import spings  # noqa: F401
+from covid_spings_variant_caller_amd import _native as N
+from covid_spings_variant_caller_amd.engine import PileupEngine
+from covid_spings_variant_caller_amd.pileup import AlignmentFile, PileupParams
+import samgen
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def host_fill(path, contig, start=None, stop=None, **kw):
+    with AlignmentFile(path) as f:
+        b = f.pileup_plan(contig, PileupParams(n_threads=kw.pop("n_threads", 4), **kw), start, stop)
+        b.fill()
+        out = (b.pos_begin, b.offsets.copy(), b.codes.copy(), b.quals.copy())
+        b.close()
+    return out
+
+
+def device_fill(path, contig, start=None, stop=None, pinned=False, **kw):
+    if pinned:
+        N.use_pinned_records()
+    with AlignmentFile(path) as f:
+        L = f.get_reference_length(contig)
+        b = f.pileup_records(contig, PileupParams(n_threads=kw.pop("n_threads", 4), **kw), start, stop)
+    eng = PileupEngine(L + 1, reference="A" * (L + 1))
+    try:
+        if b.n_cols == 0:
+            return None
+        eng.accumulate_bam_records(b)
+        eng.sync()
+        hist = eng.history()
+        assert len(hist) == 1
+        eng.finalize()
+        eng.counts()                      # settles: raises if the kernel flagged an inconsistent plan
+        return hist[0]
+    finally:
+        b.close()
+        eng.close()
+
+
+def assert_same(a, b):
+    assert a[0] == b[0]
+    np.testing.assert_array_equal(a[1], b[1])
+    np.testing.assert_array_equal(a[2], b[2])
+    np.testing.assert_array_equal(a[3], b[3])
+
+
+def sam_to_bam(sam, bam):
+    targets, recs = [], []
+    for line in open(sam):
+        if line.startswith("@SQ"):
+            f = dict(x.split(":", 1) for x in line.rstrip("\n").split("\t")[1:])
+            targets.append((f["SN"], int(f["LN"])))
+        elif line.strip() and not line.startswith("@"):
+            v = line.rstrip("\n").split("\t")
+            recs.append(dict(qname=v[0], flag=int(v[1]), rname=v[2], pos=int(v[3]), mapq=int(v[4]), cigar=v[5],
+                             rnext=v[6], pnext=int(v[7]), tlen=int(v[8]), seq=v[9], qual=v[10]))
+    samgen.write_bam(bam, targets, recs, block=3000)
+    return targets
+
+
+def test_testfile_config1(tmp_path):
+    """Config 1's input (test/testdata/testfile.sam as BAM): 4 reads, 421 columns, 1,642 entries."""
+    bam = str(tmp_path / "t.bam")
+    sam_to_bam(os.path.join(GOLD, "testfile.sam"), bam)
+    got = device_fill(bam, "NC_045512.2")
+    assert got[0] == 10 and len(got[1]) == 422 and int(got[1][-1]) == 1642
+    assert_same(got, host_fill(bam, "NC_045512.2"))
+    z = np.load(os.path.join(GOLD, "testfile_pileup.npz"))
+    np.testing.assert_array_equal(got[2], z["codes"])
+    np.testing.assert_array_equal(got[3], z["quals"])
+
+
+def _hand_cases():
+    import test_pileup_handderived as H
+    q = [30] * 10
+    yield [H.rec(f"a{i}", 1, "10M", "A" * 10, q) for i in range(5)] + \
+          [H.rec(f"b{i}", 3, "10M", "C" * 10, q) for i in range(2)], dict(max_depth=3)
+    yield [H.rec(f"a{i}", 5, "4M", "G" * 4, [30] * 4) for i in range(9)], dict(max_depth=0)
+    yield [H.rec("d1", 1, "3M2D2M", "ACGTA", [10, 11, 12, 13, 14]), H.rec("d2", 1, "5M2D", "TTTTT", [20, 21, 22, 23, 24]),
+           H.rec("n1", 1, "2M3N1M", "GGC", [30, 31, 32])], dict()
+    yield H._pair("A" * 10, [30] * 10, "A" * 10, [25] * 10), dict()
+    yield H._pair("A" * 10, [150] * 10, "A" * 10, [90] * 10), dict()
+    yield H._pair("A" * 10, [30] * 10, "C" * 10, [20] * 10), dict()
+    yield H._pair("G" * 10, [21] * 10, "T" * 10, [33] * 10), dict()
+    yield H._pair("G" * 10, [25] * 10, "T" * 10, [25] * 10), dict()
+    yield H._pair("A" * 10, [30] * 10, "A" * 10, [25] * 10), dict(ignore_overlaps=False)
+
+
+@pytest.mark.parametrize("case", range(9))
+def test_hand_derived_fixtures(tmp_path, case):
+    recs, kw = list(_hand_cases())[case]
+    bam = str(tmp_path / "h.bam")
+    samgen.write_bam(bam, [("c", 60)], recs)
+    assert_same(device_fill(bam, "c", **kw), host_fill(bam, "c", **kw))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("kw", [dict(), dict(max_depth=4), dict(max_depth=0), dict(ignore_overlaps=False, max_depth=3),
+                                dict(stepper="samtools", min_mapping_quality=20, max_depth=6), dict(stepper="nofilter")])
+def test_random_reads(tmp_path, seed, kw):
+    contigs = [("chrA", 700), ("chrB", 700)]
+    bam = str(tmp_path / "r.bam")
+    samgen.write_bam(bam, contigs, samgen.random_records(seed, contigs, n_reads=400), block=5000)
+    for c, _ in contigs:
+        assert_same(device_fill(bam, c, **kw), host_fill(bam, c, **kw))
+
+
+@pytest.mark.parametrize("region", [(100, 300), (0, 50), (550, 700), (250, 251)])
+def test_regions(tmp_path, region):
+    contigs = [("chrA", 700)]
+    bam = str(tmp_path / "r.bam")
+    samgen.write_bam(bam, contigs, samgen.random_records(7, contigs, n_reads=500), block=9000)
+    assert_same(device_fill(bam, "chrA", *region), host_fill(bam, "chrA", *region))
+
+
+def test_long_spans_and_gaps(tmp_path):
+    """Reads with 5 kb N skips (the tile look-back spans ~80 tiles) around a coverage gap."""
+    recs = []
+    for i in range(60):
+        s = 1 + 37 * i if i < 30 else 9000 + 11 * i
+        cig = "20M5000N30M" if i % 3 == 0 else "50M"
+        recs.append(dict(qname=f"r{i}", flag=0, rname="c", pos=s, mapq=60, cigar=cig, rnext="*", pnext=0, tlen=0,
+                         seq="ACGTN" * 10, qual="".join(chr(33 + (7 * i + j) % 42) for j in range(50))))
+    recs.sort(key=lambda r: r["pos"])
+    bam = str(tmp_path / "g.bam")
+    samgen.write_bam(bam, [("c", 20000)], recs)
+    assert_same(device_fill(bam, "c", max_depth=0), host_fill(bam, "c", max_depth=0))
+
+
+@pytest.mark.parametrize("depth,max_depth", [(200, 8000), (10000, 8000), (10000, 0)])
+def test_simulated_bams(tmp_path, depth, max_depth):
+    """The simulator's reads (150M, 1 % 2D / 2I) over 3 kb, up to 10,000x — through the pinned path."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.pileup import simulate_bam
+    bam = str(tmp_path / "s.bam")
+    simulate_bam(bam, "NC_045512.2", synth.reference(3000, seed=1), depth=depth, seed=5, n_threads=8)
+    assert_same(device_fill(bam, "NC_045512.2", pinned=True, max_depth=max_depth),
+                host_fill(bam, "NC_045512.2", max_depth=max_depth))
+
+
+def test_process_bam_device_pileup_matches_host(tmp_path, monkeypatch):
+    """LiveVariantCaller.process_bam (live_variant_caller.py:54-72) over 3 BAMs with the device pileup vs
+    the host fill (SPG_DEVICE_PILEUP=0): identical prepare_variants() and memory."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.live_variant_caller import LiveVariantCaller
+    from covid_spings_variant_caller_amd.pileup import simulate_bam
+    ref = synth.reference(4000, seed=3)
+    fa = str(tmp_path / "r.fa")
+    samgen.write_fasta(fa, [("NC_045512.2", ref)])
+    bams = []
+    for k in range(3):
+        p = str(tmp_path / f"b{k}.bam")
+        simulate_bam(p, "NC_045512.2", ref, depth=300, seed=10 + k, n_threads=4, snv_every=97)
+        bams.append(p)
+    out = []
+    for dev in ("1", "0"):
+        monkeypatch.setenv("SPG_DEVICE_PILEUP", dev)
+        vc = LiveVariantCaller(fa, 20, 0, 10, 5, 0.1, 0)
+        assert vc.device_pileup == (dev == "1")
+        for p in bams:
+            vc.process_bam(p)
+        out.append((vc.prepare_variants(), {k: (v["reference"], v["totalDepth"]) for k, v in vc.memory.items()}))
+        del vc
+    assert out[0][0] == out[1][0] and len(out[0][0]) > 0
+    assert out[0][1] == out[1][1]
