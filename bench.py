@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--many-batches", type=int, default=10000, help="config 4 samples (0 = skip)")
     ap.add_argument("--many-depth", type=float, default=100.0)
     ap.add_argument("--runs-batches", type=int, default=10000,
-                    help="config 4 as per-BAM CSR batches (the live form) folded in runs (k_acc_tile); 0 = skip")
+                    help="config 4 as per-BAM CSR batches (the live form, counted mode); 0 = skip")
     ap.add_argument("--no-chr1", action="store_true", help="skip the nested chr1 30x line (BASELINE config 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-positions", type=int, default=6000)
@@ -229,6 +229,13 @@ def pmc_traffic(key, E):
             if k.startswith(key) and v.get("entries") == E:
                 return v.get("hbm_bytes_per_launch")
     return None
+
+
+def pmc_traffic_sum(keys, E):
+    """Sum of pmc_traffic over the kernels of one step (each from the newest summary measured on this
+    workload); None when any of them was not measured."""
+    vals = [pmc_traffic(k, E) for k in keys]
+    return None if any(v is None for v in vals) else float(sum(vals))
 
 
 def run_point(args, D, L, depth, max_depth, local, world, rank, contig):
@@ -422,7 +429,8 @@ def run_config4(args, D, local, world, rank):
 
 
 def run_config4_runs(args, D, local, world, rank, ref, lo, hi):
-    """Config 4 as per-BAM CSR batches (batch-major), folded in runs by k_acc_multi."""
+    """Config 4 as per-BAM CSR batches (batch-major, what one process_bam per BAM produces), counted at the
+    finalize (counted mode: k_acc_lite_run + k_count_list + k_fold_hist + the sparse k_finalize)."""
     import torch
     from covid_spings_variant_caller_amd.engine import PileupEngine
     from covid_spings_variant_caller_amd.synth_device import many_bams
@@ -448,7 +456,7 @@ def run_config4_runs(args, D, local, world, rank, ref, lo, hi):
     t_acc = float(np.mean(acc)) * 1e-3 if len(acc) else float("nan")
     # bytes the run must move: each BAM's base_code + qual + u64 offsets, the REF chars, the candidate records
     moved = 2 * E + 8 * B * (C + 1) + C + 56 * n_cand
-    kname = "k_acc_tile (+ k_merge_parts when split)"
+    kname = "counted mode: k_acc_lite_run + k_count_list + k_fold_hist + sparse k_finalize"
     eng.close()
     del data
     torch.cuda.empty_cache()
@@ -459,7 +467,8 @@ def run_config4_runs(args, D, local, world, rank, ref, lo, hi):
             "accumulate_ms": t_acc * 1e3, "accumulate_samples": int(len(acc)), "candidates_per_gpu_step": n_cand,
             "roofline": {"bound": "hbm", "achieved": moved / t_acc / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                          "frac": moved / t_acc / PEAK_HBM, "algorithmic_bytes": moved,
-                         "traffic": pmc_traffic("spg::k_acc_tile", E)}}
+                         "traffic": pmc_traffic_sum(("spg::k_acc_lite_run", "spg::k_count_list", "spg::k_fold_hist",
+                                                     "spg::k_finalize"), E)}}
 
 
 def cpu_model():

@@ -163,6 +163,7 @@ struct spg_ctx {
     int64_t pend0 = 0;                  // history batches [pend0, size) are not accumulated yet (a run)
     uint64_t pend_entries = 0;
     uint32_t *kerr = nullptr;           // k_acc_multi error word (a batch too deep for a run)
+    bool kerr_dirty = false;            // a kernel that may set kerr was enqueued since it was last cleared
     uint32_t *nlist = nullptr;          // fused run: positions listed for the sparse finalize (in `band`)
     uint32_t *deep_list = nullptr;      // single shallow batch: its long columns (for k_acc_seg<1>) ...
     int64_t deep_cap = 0;
@@ -377,7 +378,12 @@ int spg_reset(spg_ctx *c) {
     // descriptor uploads still queued read the pinned mirror, which the next sample rewrites from index 0
     if (c->hist_up) c->hist_fence = true;
     clear_history(c);
-    HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));   // a new sample starts error-free
+    // a new sample starts error-free (only the run and records kernels write the word, and settle clears what it
+    // reports: no per-step memset launch for the deep path)
+    if (c->kerr_dirty) {
+        HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));
+        c->kerr_dirty = false;
+    }
     if (++c->epoch == 0) {     // wrapped: clear the records once and restart at epoch 1
         HIPCHK(hipMemsetAsync(c->acc, 0, sizeof(Acc) * c->n_pos, c->stream));
         c->epoch = 1;
@@ -781,6 +787,7 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
     P.fresh = h0 == 0 ? 1u : 0u;
     P.ref_sl = P.calls_only && (double)run_entries < 200.0 * (double)(u1 - u0) ? 1u : 0u;
     P.err = c->kerr;
+    c->kerr_dirty = true;
     if (fused) {
         if (P.S != 1 || h0 != 0) return fail("spg: internal: fused run must be one FRESH unsplit run");
         P.min_td = c->p.min_total_depth;
@@ -1017,6 +1024,7 @@ static int upload_records(spg_ctx *c, const spg_records *R, const HistBatch &hb,
     A.n_reads = (uint32_t)n;
     A.back = (int32_t)((R->max_span + 63) / 64);
     A.err = c->kerr;
+    c->kerr_dirty = true;
     HIPCHK(launch_pileup_fill(A, cs));
     return 0;
 }
@@ -1537,6 +1545,7 @@ static int settle(spg_ctx *c, Counters &h) {
         if (h.err) return fail("spg: replay found a depth mismatch between history and accumulators");
         uint32_t kerr = 0;
         HIPCHK(hipMemcpy(&kerr, c->kerr, sizeof(kerr), hipMemcpyDeviceToHost));
+        c->kerr_dirty = false;         // the stream is idle: zero, or cleared below (reported once)
         if (kerr & 2) {
             HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));   // reported once
             return fail("spg: spg_accumulate_records: the records disagree with the batch's offsets (inconsistent plan)");

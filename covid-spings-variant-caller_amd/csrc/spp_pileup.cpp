@@ -732,6 +732,8 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
         }
     } unmap{mp, fsz};
     const uint8_t *m = (const uint8_t *)mp;
+    const auto tmm = std::chrono::steady_clock::now();
+    auto tms = tmm;
     struct Blk { size_t off, clen, ulen; };
     std::vector<Blk> blks;
     // Members located in parallel: each thread finds the first member header in its byte range (a BGZF header
@@ -769,6 +771,7 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
                     }
                 }
             });
+            tms = std::chrono::steady_clock::now();
             for (int t = np - 1; t >= 1; t--) start[(size_t)t] = std::min(start[(size_t)t], start[(size_t)t + 1]);
             par_chunks((size_t)np, np, [&](int, size_t t0, size_t t1) {
                 for (size_t t = t0; t < t1; t++) {
@@ -908,8 +911,10 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
     });
     for (int64_t v : spans) R.max_span = std::max(R.max_span, v);
     if (timing)
-        fprintf(stderr, "[spp timing] read_bam_raw: %zu members, map+members %.1f ms, buffer %.1f ms, inflate+scan %.1f ms, "
-                "fields %.1f ms\n", nb, std::chrono::duration<double, std::milli>(tm1 - tm0).count(),
+        fprintf(stderr, "[spp timing] read_bam_raw: %zu members, map %.1f ms + search %.1f ms + members %.1f ms, buffer %.1f ms, inflate+scan %.1f ms, "
+                "fields %.1f ms\n", nb, std::chrono::duration<double, std::milli>(tmm - tm0).count(),
+                std::chrono::duration<double, std::milli>(tms - tmm).count(),
+                std::chrono::duration<double, std::milli>(tm1 - tms).count(),
                 std::chrono::duration<double, std::milli>(tm2 - tm1).count(),
                 std::chrono::duration<double, std::milli>(t1 - t0).count(),
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
