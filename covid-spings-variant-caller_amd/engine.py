@@ -269,13 +269,21 @@ class PileupEngine:
             N.check(self._L.spg_kernel_times(self._h, N.ptr(a), N.ptr(f), int(cap), C.byref(n)), "spg_kernel_times")
         return a[:n.value].astype(np.float64), f[:n.value].astype(np.float64)
 
-    def history(self):
-        """The accumulated batches since reset(), as host copies: [(pos_begin, offsets, codes, quals)]."""
+    def history_count(self) -> int:
+        """Batches accumulated since reset() (spg_history_count)."""
+        n = C.c_int64()
+        with self._lock:
+            N.check(self._L.spg_history_count(self._h, C.byref(n)), "spg_history_count")
+        return n.value
+
+    def history(self, start: int = 0):
+        """The accumulated batches since reset() from batch `start` on, as host copies:
+        [(pos_begin, offsets, codes, quals)]."""
         out = []
         with self._lock:
             n = C.c_int64()
             N.check(self._L.spg_history_count(self._h, C.byref(n)), "spg_history_count")
-            for i in range(n.value):
+            for i in range(max(0, int(start)), n.value):
                 pb, nc, ne = C.c_int64(), C.c_int64(), C.c_uint64()
                 N.check(self._L.spg_history_info(self._h, i, C.byref(pb), C.byref(nc), C.byref(ne)),
                         "spg_history_info")

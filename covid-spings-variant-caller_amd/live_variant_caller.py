@@ -23,6 +23,7 @@ libspings_gpu.so or a GPU the constructor raises.
 from __future__ import annotations
 
 import collections
+import uuid
 import logging
 import os
 import threading
@@ -192,6 +193,7 @@ class LiveVariantCaller:
             self.engine.reset()
             self._batch_contig = []
             self._current_ref = None
+            self._ck_token = uuid.uuid4().hex     # identity of this memory for incremental checkpoints
 
     def _use_reference(self, index: int):
         if self._current_ref != index:
@@ -326,41 +328,95 @@ class LiveVariantCaller:
 
     # -- checkpoint ---------------------------------------------------------------------------
     def create_checkpoint(self, filename):
-        """:40-45 — the accumulated batches (exact engine state), numpy .npz.  Like the reference's pickled
-        `memory`, which holds only the base qualities that passed the filter (:96-103), each batch keeps only
-        its entries with q >= minBaseQuality — plus, for a column whose every entry fails it, its first entry,
-        so that the position's first visit (:77-85) survives the round trip."""
+        """:40-45 — the accumulated batches (exact engine state) as numpy .npz files.  Like the reference's
+        pickled `memory`, which holds only the base qualities that passed the filter (:96-103), each batch keeps
+        only its entries with q >= minBaseQuality — plus, for a column whose every entry fails it, its first
+        entry, so that the position's first visit (:77-85) survives the round trip.
+
+        Incremental: `filename` is a small manifest (FASTA names, contig of every batch, the shard files); the
+        batches live in shards beside it (`<filename>.<token>.<first batch>.npz`).  vc_queue.py:142-144 writes a
+        checkpoint after every BAM: when `filename` already holds this memory's earlier checkpoint (same
+        memory token — a reset or a load starts a new one), only the batches accumulated since are written,
+        so a call costs O(new entries), not O(everything accumulated).  The manifest is replaced atomically
+        after its shards are on disk; shards no manifest lists any more are removed."""
         log.info("Creating checkpoint %s", filename)
         with self._lock:
-            hist = self.engine.history()
-            arrays = {"contig": np.array(self._batch_contig, np.int64),
-                      "names": np.array(self.fastaFile.references),
-                      "min_base_quality": np.int64(self.minBaseQuality)}
-            for i, (pb, off, codes, quals) in enumerate(hist):
-                off, codes, quals = _bq_compact(off, codes, quals, self.minBaseQuality)
-                arrays[f"b{i}_pos"] = np.int64(pb)
-                arrays[f"b{i}_off"] = off
-                arrays[f"b{i}_codes"] = codes
-                arrays[f"b{i}_quals"] = quals
-            with open(filename, "wb") as f:
-                np.savez(f, **arrays)
+            n = self.engine.history_count()
+            names = list(self.fastaFile.references)
+            old = _read_manifest(filename)
+            keep = []
+            if (old is not None and old["token"] == self._ck_token and old["names"] == names
+                    and old["min_base_quality"] == self.minBaseQuality and old["n"] <= n
+                    and old["contig"] == self._batch_contig[:old["n"]]):
+                keep = old["shards"]
+            first = sum(k for _, _, k in keep)
+            shards = list(keep)
+            base = os.path.basename(filename)
+            if first < n:
+                arrays = {}
+                for i, (pb, off, codes, quals) in enumerate(self.engine.history(start=first)):
+                    off, codes, quals = _bq_compact(off, codes, quals, self.minBaseQuality)
+                    arrays[f"b{i}_pos"] = np.int64(pb)
+                    arrays[f"b{i}_off"] = off
+                    arrays[f"b{i}_codes"] = codes
+                    arrays[f"b{i}_quals"] = quals
+                shard = f"{base}.{self._ck_token[:12]}.{first}.npz"
+                with open(os.path.join(os.path.dirname(os.path.abspath(filename)), shard), "wb") as f:
+                    np.savez(f, **arrays)
+                shards.append((shard, first, n - first))
+            tmp = filename + ".tmp"
+            with open(tmp, "wb") as f:
+                np.savez(f, format=np.int64(2), token=np.array(self._ck_token),
+                         contig=np.array(self._batch_contig, np.int64), names=np.array(names),
+                         min_base_quality=np.int64(self.minBaseQuality),
+                         shard_files=np.array([s for s, _, _ in shards] or [""]),
+                         shard_ranges=np.array([[a, k] for _, a, k in shards], np.int64).reshape(-1, 2))
+            os.replace(tmp, filename)
+            if old is not None:
+                live = {s for s, _, _ in shards}
+                for s, _, _ in old["shards"]:
+                    if s not in live:
+                        try:
+                            os.remove(os.path.join(os.path.dirname(os.path.abspath(filename)), s))
+                        except OSError:
+                            pass
 
     def load_checkpoint(self, filename):
-        """:47-52 — replaces memory with the checkpoint's (replays its batches)."""
+        """:47-52 — replaces memory with the checkpoint's (replays its batches).  Reads the incremental
+        manifest format and the single-file format of earlier versions."""
         log.info("Loading checkpoint %s", filename)
-        with np.load(filename, allow_pickle=False) as z:
-            contig = z["contig"].tolist()
-            names = z["names"].tolist()
-            if names != self.fastaFile.references:
+        man = _read_manifest(filename)
+        if man is not None:
+            if man["names"] != self.fastaFile.references:
                 raise ValueError("checkpoint was made with a different reference FASTA")
-            batches = [(int(z[f"b{i}_pos"]), z[f"b{i}_off"], z[f"b{i}_codes"], z[f"b{i}_quals"])
-                       for i in range(len(contig))]
+            d = os.path.dirname(os.path.abspath(filename))
+            contig, batches = man["contig"], []
+            for s, a, k in man["shards"]:
+                with np.load(os.path.join(d, s), allow_pickle=False) as z:
+                    batches += [(int(z[f"b{i}_pos"]), z[f"b{i}_off"], z[f"b{i}_codes"], z[f"b{i}_quals"])
+                                for i in range(k)]
+            token = man["token"]
+        else:
+            with np.load(filename, allow_pickle=False) as z:
+                contig = z["contig"].tolist()
+                names = z["names"].tolist()
+                if names != self.fastaFile.references:
+                    raise ValueError("checkpoint was made with a different reference FASTA")
+                batches = [(int(z[f"b{i}_pos"]), z[f"b{i}_off"], z[f"b{i}_codes"], z[f"b{i}_quals"])
+                           for i in range(len(contig))]
+            token = None
+        if len(batches) != len(contig):
+            raise ValueError(f"checkpoint {filename}: {len(batches)} batches for {len(contig)} contig entries")
         with self._lock:
             self.reset_memory()
             for ci, (pb, off, codes, quals) in zip(contig, batches):
                 self._use_reference(ci)
                 self.engine.accumulate(pb, off, codes, quals)
                 self._batch_contig.append(ci)
+            if token is not None:
+                # the memory now holds exactly the manifest's batches: later checkpoints to the same file
+                # append to its shards
+                self._ck_token = token
 
     # -- output ------------------------------------------------------------------------------
     def write_vcf(self, outputVfc: str):
@@ -389,6 +445,24 @@ INFO_META = [
                            "defined precisely as the GL field)"),
     ("SCORE", "1", "Float", "Custom scoring function"),
 ]
+
+
+def _read_manifest(filename):
+    """The incremental checkpoint manifest at `filename` (create_checkpoint), or None when the file is absent,
+    unreadable or in the single-file format."""
+    try:
+        with np.load(filename, allow_pickle=False) as z:
+            if "format" not in z.files or int(z["format"]) != 2:
+                return None
+            files = [str(x) for x in z["shard_files"].tolist()]
+            rng = z["shard_ranges"].reshape(-1, 2).tolist()
+            shards = [(f, int(a), int(k)) for f, (a, k) in zip(files, rng)]
+            contig = z["contig"].tolist()
+            return {"token": str(z["token"]), "names": [str(x) for x in z["names"].tolist()],
+                    "contig": contig, "n": len(contig), "min_base_quality": int(z["min_base_quality"]),
+                    "shards": shards}
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def _is_bgzf(path: str) -> bool:

@@ -131,6 +131,50 @@ def test_checkpoint_roundtrip(planted):
     assert all(mem[p] == o.memory[p] for p in o.memory)
 
 
+def test_checkpoint_incremental_per_bam(planted):
+    """vc_queue.py:142-144's loop — process_bam then create_checkpoint(same file) per BAM: each checkpoint
+    writes only the batches accumulated since the previous one (earlier shards untouched), a reset starts a
+    fresh set (the old shards removed), a loaded checkpoint keeps appending to its own shards, and the
+    resumed memory matches the oracle."""
+    d, ref, fasta, files = planted
+    ck = str(d / "inc.npz")
+    seq = [files[0], files[1], files[0]]
+    a = _caller(fasta)
+    listed = []
+    for f in seq:
+        a.process_bam(f)
+        a.create_checkpoint(ck)
+        shards = sorted(x for x in os.listdir(d) if x.startswith("inc.npz.") and x.endswith(".npz"))
+        listed.append(shards)
+    assert [len(x) for x in listed] == [1, 2, 3]
+    assert listed[1][:1] == listed[0] and set(listed[1]) < set(listed[2])
+    first = os.path.join(d, listed[0][0])
+    m0 = os.stat(first).st_mtime_ns
+    a.create_checkpoint(ck)                      # nothing new: only the manifest is rewritten
+    assert os.stat(first).st_mtime_ns == m0
+    assert sorted(x for x in os.listdir(d) if x.startswith("inc.npz.") and x.endswith(".npz")) == listed[2]
+    b = _caller(fasta)
+    b.load_checkpoint(ck)
+    o = _oracle(ref, seq)
+    compare_variants(b.prepare_variants(), o.prepare_variants(), RTOL)
+    mem = b.memory
+    assert list(mem) == list(o.memory) and all(mem[p] == o.memory[p] for p in o.memory)
+    b.process_bam(files[1])                      # the loaded memory appends to the same shards
+    b.create_checkpoint(ck)
+    now = sorted(x for x in os.listdir(d) if x.startswith("inc.npz.") and x.endswith(".npz"))
+    assert len(now) == 4 and set(listed[2]) < set(now)
+    c = _caller(fasta)
+    c.load_checkpoint(ck)
+    compare_variants(c.prepare_variants(), _oracle(ref, seq + [files[1]]).prepare_variants(), RTOL)
+    a.reset_memory()                             # a new memory: a fresh shard set, the old shards removed
+    a.process_bam(files[1])
+    a.create_checkpoint(ck)
+    now = sorted(x for x in os.listdir(d) if x.startswith("inc.npz.") and x.endswith(".npz"))
+    assert len(now) == 1 and now[0] not in listed[2]
+    c.load_checkpoint(ck)
+    compare_variants(c.prepare_variants(), _oracle(ref, files[1:]).prepare_variants(), RTOL)
+
+
 def test_checkpoint_resume_into_fresh_process_state(planted):
     """A checkpoint taken before any BAM, and one loaded into a caller that already holds data
     (load_checkpoint replaces memory, live_variant_caller.py:48-52), both match the oracle."""
