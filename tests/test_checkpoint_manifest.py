@@ -1,0 +1,37 @@
+"""Incremental checkpoint manifest (live_variant_caller._read_manifest; create_checkpoint writes it): recognised
+only for the manifest layout, None for absent, foreign, single-file-layout or pickled files (CPU; the GPU round
+trips are in tests/test_live_caller_gpu.py)."""
+import pickle
+
+import numpy as np
+
+import spings  # noqa: F401
+from covid_spings_variant_caller_amd.live_variant_caller import _read_manifest
+
+
+def test_manifest_roundtrip(tmp_path):
+    f = str(tmp_path / "ck.npz")
+    with open(f, "wb") as fh:
+        np.savez(fh, format=np.int64(2), token=np.array("abc123"), contig=np.array([0, 0, 1], np.int64),
+                 names=np.array(["chrA", "chrB"]), min_base_quality=np.int64(30),
+                 shard_files=np.array(["ck.npz.abc.0.npz", "ck.npz.abc.2.npz"]),
+                 shard_ranges=np.array([[0, 2], [2, 1]], np.int64))
+    m = _read_manifest(f)
+    assert m == {"token": "abc123", "names": ["chrA", "chrB"], "contig": [0, 0, 1], "n": 3,
+                 "min_base_quality": 30, "shards": [("ck.npz.abc.0.npz", 0, 2), ("ck.npz.abc.2.npz", 2, 1)]}
+
+
+def test_not_a_manifest(tmp_path):
+    assert _read_manifest(str(tmp_path / "absent.npz")) is None
+    old = str(tmp_path / "v1.npz")
+    with open(old, "wb") as fh:
+        np.savez(fh, contig=np.array([0], np.int64), names=np.array(["chrA"]), min_base_quality=np.int64(30),
+                 b0_pos=np.int64(0), b0_off=np.zeros(2, np.uint64), b0_codes=np.zeros(0, np.uint8),
+                 b0_quals=np.zeros(0, np.uint8))
+    assert _read_manifest(old) is None
+    txt = tmp_path / "t.npz"
+    txt.write_text("not numpy")
+    assert _read_manifest(str(txt)) is None
+    pk = tmp_path / "p.npz"
+    pk.write_bytes(pickle.dumps({"memory": {}}))      # the reference's pickle: never unpickled
+    assert _read_manifest(str(pk)) is None

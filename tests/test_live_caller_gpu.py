@@ -175,6 +175,30 @@ def test_checkpoint_incremental_per_bam(planted):
     compare_variants(c.prepare_variants(), _oracle(ref, files[1:]).prepare_variants(), RTOL)
 
 
+def test_checkpoint_single_file_format_still_loads(planted):
+    """A checkpoint in the earlier single-file layout (every batch inside the named .npz) loads as before."""
+    d, ref, fasta, files = planted
+    from covid_spings_variant_caller_amd.live_variant_caller import _bq_compact
+    a = _caller(fasta)
+    for f in files:
+        a.process_bam(f)
+    arrays = {"contig": np.array(a._batch_contig, np.int64), "names": np.array(a.fastaFile.references),
+              "min_base_quality": np.int64(a.minBaseQuality)}
+    for i, (pb, off, codes, quals) in enumerate(a.engine.history()):
+        off, codes, quals = _bq_compact(off, codes, quals, a.minBaseQuality)
+        arrays.update({f"b{i}_pos": np.int64(pb), f"b{i}_off": off, f"b{i}_codes": codes, f"b{i}_quals": quals})
+    ck = str(d / "v1.npz")
+    with open(ck, "wb") as fh:
+        np.savez(fh, **arrays)
+    b = _caller(fasta)
+    b.load_checkpoint(ck)
+    compare_variants(b.prepare_variants(), _oracle(ref, files).prepare_variants(), RTOL)
+    b.create_checkpoint(ck)                      # rewritten in the manifest layout, loads the same
+    c = _caller(fasta)
+    c.load_checkpoint(ck)
+    compare_variants(c.prepare_variants(), _oracle(ref, files).prepare_variants(), RTOL)
+
+
 def test_checkpoint_resume_into_fresh_process_state(planted):
     """A checkpoint taken before any BAM, and one loaded into a caller that already holds data
     (load_checkpoint replaces memory, live_variant_caller.py:48-52), both match the oracle."""
