@@ -337,7 +337,8 @@ class LiveVariantCaller:
         batches live in shards beside it (`<filename>.<token>.<first batch>.npz`).  vc_queue.py:142-144 writes a
         checkpoint after every BAM: when `filename` already holds this memory's earlier checkpoint (same
         memory token — a reset or a load starts a new one), only the batches accumulated since are written,
-        so a call costs O(new entries), not O(everything accumulated).  The manifest is replaced atomically
+        so a call costs O(new entries), not O(everything accumulated).  A loaded checkpoint is a new memory (its first
+checkpoint writes every batch once): two callers that load one file never append to each other's shards.  The manifest is replaced atomically
         after its shards are on disk; shards no manifest lists any more are removed."""
         log.info("Creating checkpoint %s", filename)
         with self._lock:
@@ -395,7 +396,6 @@ class LiveVariantCaller:
                 with np.load(os.path.join(d, s), allow_pickle=False) as z:
                     batches += [(int(z[f"b{i}_pos"]), z[f"b{i}_off"], z[f"b{i}_codes"], z[f"b{i}_quals"])
                                 for i in range(k)]
-            token = man["token"]
         else:
             with np.load(filename, allow_pickle=False) as z:
                 contig = z["contig"].tolist()
@@ -404,7 +404,6 @@ class LiveVariantCaller:
                     raise ValueError("checkpoint was made with a different reference FASTA")
                 batches = [(int(z[f"b{i}_pos"]), z[f"b{i}_off"], z[f"b{i}_codes"], z[f"b{i}_quals"])
                            for i in range(len(contig))]
-            token = None
         if len(batches) != len(contig):
             raise ValueError(f"checkpoint {filename}: {len(batches)} batches for {len(contig)} contig entries")
         with self._lock:
@@ -413,10 +412,6 @@ class LiveVariantCaller:
                 self._use_reference(ci)
                 self.engine.accumulate(pb, off, codes, quals)
                 self._batch_contig.append(ci)
-            if token is not None:
-                # the memory now holds exactly the manifest's batches: later checkpoints to the same file
-                # append to its shards
-                self._ck_token = token
 
     # -- output ------------------------------------------------------------------------------
     def write_vcf(self, outputVfc: str):

@@ -133,9 +133,8 @@ def test_checkpoint_roundtrip(planted):
 
 def test_checkpoint_incremental_per_bam(planted):
     """vc_queue.py:142-144's loop — process_bam then create_checkpoint(same file) per BAM: each checkpoint
-    writes only the batches accumulated since the previous one (earlier shards untouched), a reset starts a
-    fresh set (the old shards removed), a loaded checkpoint keeps appending to its own shards, and the
-    resumed memory matches the oracle."""
+    writes only the batches accumulated since the previous one (earlier shards untouched), a reset or a load
+    starts a fresh set (the old shards removed), and the resumed memory matches the oracle."""
     d, ref, fasta, files = planted
     ck = str(d / "inc.npz")
     seq = [files[0], files[1], files[0]]
@@ -159,18 +158,22 @@ def test_checkpoint_incremental_per_bam(planted):
     compare_variants(b.prepare_variants(), o.prepare_variants(), RTOL)
     mem = b.memory
     assert list(mem) == list(o.memory) and all(mem[p] == o.memory[p] for p in o.memory)
-    b.process_bam(files[1])                      # the loaded memory appends to the same shards
-    b.create_checkpoint(ck)
+    b.process_bam(files[1])                      # a loaded memory is a new one: its first checkpoint writes all
+    b.create_checkpoint(ck)                      # its batches once, then appends
     now = sorted(x for x in os.listdir(d) if x.startswith("inc.npz.") and x.endswith(".npz"))
-    assert len(now) == 4 and set(listed[2]) < set(now)
+    assert len(now) == 1 and now[0] not in listed[2]
+    b.process_bam(files[0])
+    b.create_checkpoint(ck)
+    now2 = sorted(x for x in os.listdir(d) if x.startswith("inc.npz.") and x.endswith(".npz"))
+    assert len(now2) == 2 and set(now) < set(now2)
     c = _caller(fasta)
     c.load_checkpoint(ck)
-    compare_variants(c.prepare_variants(), _oracle(ref, seq + [files[1]]).prepare_variants(), RTOL)
+    compare_variants(c.prepare_variants(), _oracle(ref, seq + [files[1], files[0]]).prepare_variants(), RTOL)
     a.reset_memory()                             # a new memory: a fresh shard set, the old shards removed
     a.process_bam(files[1])
     a.create_checkpoint(ck)
     now = sorted(x for x in os.listdir(d) if x.startswith("inc.npz.") and x.endswith(".npz"))
-    assert len(now) == 1 and now[0] not in listed[2]
+    assert len(now) == 1 and now[0] not in now2
     c.load_checkpoint(ck)
     compare_variants(c.prepare_variants(), _oracle(ref, files[1:]).prepare_variants(), RTOL)
 
