@@ -732,6 +732,16 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
         }
     } unmap{mp, fsz};
     const uint8_t *m = (const uint8_t *)mp;
+    // The mapped file's pages faulted in by all threads at once, one touch per page: the member walk below
+    // (a dependent chain per thread) and the inflate then run on mapped pages
+    static const bool pretouch = [] { const char *e = getenv("SPP_PRETOUCH"); return !e || atoi(e) != 0; }();
+    if (pretouch) {
+        par_chunks((fsz + 4095) >> 12, nt, [&](int, size_t i0, size_t i1) {
+            uint32_t acc = 0;
+            for (size_t i = i0; i < i1; i++) acc += ((const volatile uint8_t *)m)[i << 12];
+            (void)acc;
+        });
+    }
     const auto tmm = std::chrono::steady_clock::now();
     auto tms = tmm;
     struct Blk { size_t off, clen, ulen; };
