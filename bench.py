@@ -6,11 +6,16 @@ call tables to rank 0 (RCCL over xGMI).  Headline workload (BASELINE metric poin
 SARS-CoV-2 (L = 29,903), 10,000x depth, 150-bp reads, uncapped.  Weak scaling: with N GPUs a step
 processes N samples; rank r owns the r-th coordinate range of every sample.
 
-Also on the same line (nested, never `value`):
+Also on the same line (nested, never `value`), one per BASELINE config:
 * ``parity_mode``: the metric point with pysam's max_depth 8,000 (E = 2.36e8);
-* ``config4``: BASELINE config 4 — 10,000 BAM-sized 100x SARS-CoV-2 samples accumulated into one
-  memory per step (live_variant_caller.py:54-103 once per BAM) and finalized; coordinate-sharded over
+* ``sars1k`` (config 2): SARS-CoV-2 at 1,000x, 64 samples stacked per GPU step (one sample is ~10 us of
+  HBM traffic: SURVEY §8 d batches >= 64 samples per measurement);
+* ``sars100k`` (config 3): 100,000x uncapped (the deep-column stress) and, nested, at max_depth 8,000;
+* ``config4`` (config 4): 10,000 BAM-sized 100x samples as the per-BAM batches the drop-in produces, accumulated
+  into one memory and finalized per step (the headline ``value``), the per-BAM finalize loop of
+  vc_queue.py:142-144 (``per_bam_finalize``), and the column-major layout as an aside; coordinate-sharded over
   the N ranks (each rank: its range of every BAM);
+* ``chr1_30x`` (config 5);
 * ``end_to_end`` (host BAM -> calls) and ``cpu_baseline`` (the oracle restatements on host cores).
 
 Timing: W untimed warm-up steps; then 20 measurements, each of K steps (K = max(--steps, enough
@@ -53,18 +58,25 @@ def parse():
     ap.add_argument("--many-batches", type=int, default=10000, help="config 4 samples (0 = skip)")
     ap.add_argument("--many-depth", type=float, default=100.0)
     ap.add_argument("--runs-batches", type=int, default=10000,
-                    help="config 4 as per-BAM CSR batches (the live form, counted mode); 0 = skip")
+                    help="config 4 as per-BAM CSR batches (the product path, counted mode; the headline); 0 = skip")
+    ap.add_argument("--per-bam-bams", type=int, default=10000,
+                    help="config 4's per-BAM finalize loop (vc_queue.py:142-144) over the first N BAMs; 0 = skip")
     ap.add_argument("--no-chr1", action="store_true", help="skip the nested chr1 30x line (BASELINE config 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-positions", type=int, default=6000)
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end BAM -> calls leg")
     ap.add_argument("--time-every", type=int, default=8,
                     help="HIP events around the accumulate kernel on every K-th timed step")
-    ap.add_argument("--e2e-threads", type=int, default=16)
+    ap.add_argument("--e2e-threads", type=int, default=0,
+                    help="host threads of the end-to-end plan (0 = the per-GPU share of an 8-GPU node: "
+                         "len(sched_getaffinity) // 8, at least 16)")
     ap.add_argument("--e2e-bams", type=int, default=4, help="BAMs per end-to-end stream")
     ap.add_argument("--e2e-many", type=int, default=64,
                     help="config 4 end to end: 100x SARS-CoV-2 BAM files through process_bams (0 = skip)")
     ap.add_argument("--full-table", action="store_true", help="also accumulate every table GL term")
+    ap.add_argument("--legs", default="parity,sars1k,sars100k,config4,chr1,e2e,cpu",
+                    help="nested legs of the default sars10k line (comma list; 'none' = the main point only)")
+    ap.add_argument("--sars1k-samples", type=int, default=64, help="stacked samples per GPU step at 1,000x")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
                                                       "gloo only to exercise the path on one GPU)")
     return ap.parse_args()
@@ -175,32 +187,42 @@ def finalize_ms(step, eng, n=8):
     return float(np.mean(f[f > 0])) if (f > 0).any() else 0.0
 
 
-def build_shard(rank, world, L, depth, max_depth, device):
-    """This rank's coordinate range of each of `world` samples, generated natively
-    (libspings_pileup spp_synth_batch: SURVEY §8 d read model) and concatenated in HBM."""
+def build_shard(rank, world, L, depth, max_depth, device, samples=1, distinct=None):
+    """This rank's coordinate range of each of `world` x `samples` samples, generated natively
+    (libspings_pileup spp_synth_batch: SURVEY §8 d read model) and concatenated in HBM.  The samples are
+    STACKED: sample s owns positions [s C, (s + 1) C) of the engine's coordinate space, so one context holds
+    `samples` independent memories and one launch processes them all (SURVEY §8 d: batches of >= 64 samples
+    for the 1,000x config, whose single sample is ~10 us of HBM traffic).  Only `distinct` samples are
+    generated (seeds 2, 3, ...); the others repeat them (the kernel reads every copy)."""
     import torch
     from covid_spings_variant_caller_amd import synth
     from covid_spings_variant_caller_amd.pileup import synth_batch
     ref = synth.reference(L, seed=1)
     shard = (L + world - 1) // world
     lo, hi = rank * shard, min(L, (rank + 1) * shard)
-    offs, dc, dq, refs = [np.zeros(1, np.uint64)], [], [], []
-    base = 0
+    n = world * samples
+    distinct = n if distinct is None else max(1, min(n, distinct))
     threads = min(16, len(os.sched_getaffinity(0)))
-    for s in range(world):
+    gen = []
+    for s in range(distinct):
         b = synth_batch(ref, depth, lo=lo, hi=hi, seed=2 + s, n_threads=threads, max_depth=max_depth)
-        offs.append(b.offsets[1:] + np.uint64(base))
-        base += b.n_entries
-        dc.append(torch.from_numpy(b.codes).to(device))
-        dq.append(torch.from_numpy(b.quals).to(device))
-        refs.append(ref[lo:hi])
+        gen.append((b.offsets.copy(), torch.from_numpy(b.codes).to(device), torch.from_numpy(b.quals).to(device)))
         b.close()
+    offs, dc, dq = [np.zeros(1, np.uint64)], [], []
+    base = 0
+    for s in range(n):
+        o, c, q = gen[s % distinct]
+        offs.append(o[1:] + np.uint64(base))
+        base += int(o[-1])
+        dc.append(c)
+        dq.append(q)
     pad = torch.zeros(16, dtype=torch.uint8, device=device)
     d_c = torch.cat(dc + [pad + 0xFF])
     d_q = torch.cat(dq + [pad])
+    del gen, dc, dq
     off = np.concatenate(offs)
     d_off = torch.from_numpy(off.view(np.int64).copy()).to(device)
-    return ref, "".join(refs), off, d_off, d_c, d_q, int(base)
+    return ref, ref[lo:hi] * n, off, d_off, d_c, d_q, int(base)
 
 
 def kernel_name(E, C, calls_only=True):
@@ -238,13 +260,14 @@ def pmc_traffic_sum(keys, E):
     return None if any(v is None for v in vals) else float(sum(vals))
 
 
-def run_point(args, D, L, depth, max_depth, local, world, rank, contig):
-    """The metric point (one sample per GPU per step, coordinate-sharded): returns the result dict."""
+def run_point(args, D, L, depth, max_depth, local, world, rank, contig, samples=1, distinct=None):
+    """The metric point (`samples` stacked samples per GPU per step, each coordinate-sharded): returns the
+    result dict."""
     import torch
     from covid_spings_variant_caller_amd.engine import PileupEngine
     dev = torch.device("cuda", local)
     t_gen = time.perf_counter()
-    ref, vref, off, d_off, d_c, d_q, E = build_shard(rank, world, L, depth, max_depth, dev)
+    ref, vref, off, d_off, d_c, d_q, E = build_shard(rank, world, L, depth, max_depth, dev, samples, distinct)
     C = len(off) - 1
     t_gen = time.perf_counter() - t_gen
     # calls-only engine (SPG_P_CALLS_ONLY): the call table prepare_variants() returns, exactly
@@ -334,8 +357,11 @@ def run_point(args, D, L, depth, max_depth, local, world, rank, contig):
     # calls-only candidate records (56 B) written
     algo_bytes = 2 * E + 8 * (C + 1) + C + 56 * n_cand
     eng.close()
+    del d_off, d_c, d_q
+    torch.cuda.empty_cache()
     return {
-        "value": world * L * K / med, "ms_per_step": med / K * 1e3, "steps": K, "E": E, "C": C,
+        "value": world * samples * L * K / med, "ms_per_step": med / K * 1e3, "steps": K, "reps": len(times),
+        "E": E, "C": C,
         "measurements_ms": [round(t * 1e3, 3) for t in times], "t_gen": t_gen,
         "kernel_ms": t_acc * 1e3, "kernel_ms_median": float(np.median(acc)) if len(acc) else None,
         "kernel_samples": int(len(acc)), "algo_bytes": algo_bytes, "achieved": algo_bytes / t_acc,
@@ -344,42 +370,60 @@ def run_point(args, D, L, depth, max_depth, local, world, rank, contig):
     }
 
 
-def nested_point(args, D, workload, local, world, rank):
-    """Another BASELINE config as a nested line (never `value`): same step and timing as the main point."""
+def nested_point(args, D, workload, local, world, rank, max_depth=0, samples=1, distinct=None, step_frac=False):
+    """Another BASELINE config as a nested line (never `value`): same step and timing as the main point.
+    `step_frac`: the roofline fraction is taken over the whole step's kernels (accumulate + finalize launches),
+    for paths where the finalize is a launch of its own (chr1: k_acc_lite + k_lite_fold + sparse k_finalize)."""
     L, depth, contig = WORKLOADS[workload]
-    p = run_point(args, D, L, depth, 0, local, world, rank, contig)
+    p = run_point(args, D, L, depth, max_depth, local, world, rank, contig, samples, distinct)
     name, key = kernel_name(p["E"], p["C"], not args.full_table)
-    return {"workload": f"{workload}: {contig} L={L}, {depth:.0f}x, 150-bp reads, uncapped, 1 sample per GPU per "
-                        f"step (coordinate-sharded x{world})",
-            "value": p["value"], "unit": "positions/s", "ms_per_step": p["ms_per_step"], "steps": p["steps"],
-            "measurement_ms": p["measurements_ms"], "entries_per_gpu_step": p["E"], "columns_per_gpu": p["C"],
+    frac_k = p["achieved"] / PEAK_HBM
+    frac_s = p["algo_bytes"] / ((p["kernel_ms"] + p["finalize_ms"]) * 1e-3) / PEAK_HBM
+    stack = (f"{samples} samples stacked per GPU per step (sample s = positions [s C, (s+1) C) of one context; "
+             f"{distinct or samples * world} distinct, repeated)" if samples > 1 else "1 sample per GPU per step")
+    return {"workload": f"{workload}: {contig} L={L}, {depth:.0f}x, 150-bp reads, "
+                        f"{'uncapped' if not max_depth else f'max_depth {max_depth}'}, {stack} (coordinate-sharded x{world})",
+            "value": p["value"], "unit": "positions/s", "ms_per_step": p["ms_per_step"], "steps": p["steps"] * p["reps"],
+            "steps_per_measurement": p["steps"], "measurement_ms": p["measurements_ms"], "samples_per_gpu_step": samples,
+            "entries_per_gpu_step": p["E"], "columns_per_gpu": p["C"],
             "datagen_s": p["t_gen"], "finalize_ms": p["finalize_ms"], "candidates_per_gpu_step": p["n_cand"],
-            "roofline": {"bound": "hbm", "achieved": p["achieved"] / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                         "frac": p["achieved"] / PEAK_HBM, "algorithmic_bytes": p["algo_bytes"],
-                         "frac_incl_finalize": p["algo_bytes"] / ((p["kernel_ms"] + p["finalize_ms"]) * 1e-3) / PEAK_HBM,
+            "replayed_positions_per_gpu_step": p["n_replay"],
+            "roofline": {"bound": "hbm", "achieved": (frac_s if step_frac else frac_k) * PEAK_HBM / 1e9,
+                         "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": frac_s if step_frac else frac_k,
+                         "frac_basis": "accumulate + finalize kernels" if step_frac else "accumulate kernel",
+                         "algorithmic_bytes": p["algo_bytes"], "frac_kernel_only": frac_k, "frac_incl_finalize": frac_s,
                          "traffic": pmc_traffic(key, p["E"]), "kernel": name, "kernel_ms": p["kernel_ms"],
                          "kernel_ms_median": p["kernel_ms_median"], "kernel_samples": p["kernel_samples"]}}
 
 
 def run_config4(args, D, local, world, rank):
-    """BASELINE config 4: args.many_batches BAM-sized samples (args.many_depth x, per-BAM cap 8,000)
-    accumulated into one memory per step, then finalized; this rank's coordinate range of every BAM.
+    """BASELINE config 4: args.runs_batches BAM-sized samples (args.many_depth x, per-BAM cap 8,000) accumulated
+    into one memory; this rank's coordinate range of every BAM.
 
-    Main figure: the batched layout a multi-BAM pileup emits (column-major: each position's entries of
-    every BAM concatenated, spg_accumulate_samples) - one deep column per position, k_acc_seg.
-    ``live_runs``: the same kind of samples as per-BAM CSR batches (what process_bam produces one BAM
-    at a time), folded in runs by k_acc_multi (args.runs_batches BAMs, spg_accumulate_batches)."""
-    import torch
+    Headline (``value``): the product path — the per-BAM CSR batches one process_bam per BAM produces
+    (live_variant_caller.py:54-72; LiveVariantCaller.process_bams), accumulated and finalized once per step
+    (counted mode).  ``per_bam_finalize``: vc_queue.py:142-144's loop — process_bam then write_vcf's
+    prepare_variants after EVERY BAM, the call table read back each time.  ``column_major_aside``: the same
+    BAMs as one column-major multi-BAM batch (spg_accumulate_samples), a layout no product path produces
+    (reported for comparison only)."""
     from covid_spings_variant_caller_amd import synth
-    from covid_spings_variant_caller_amd.engine import PileupEngine
-    from covid_spings_variant_caller_amd.synth_device import many_bams, many_bams_columns
-    dev = torch.device("cuda", local)
     L = L_SARS
     ref = synth.reference(L, seed=1)
     shard = (L + world - 1) // world
     lo, hi = rank * shard, min(L, (rank + 1) * shard)
-    C = hi - lo
-    B = args.many_batches
+    res = run_config4_runs(args, D, local, world, rank, ref, lo, hi)
+    if args.many_batches > 0:
+        res["column_major_aside"] = run_config4_columns(args, D, local, world, rank, ref, lo, hi)
+    return res
+
+
+def run_config4_columns(args, D, local, world, rank, ref, lo, hi):
+    """Config 4's BAMs as one column-major multi-sample batch (k_acc_seg over deep columns)."""
+    import torch
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.synth_device import many_bams_columns
+    dev = torch.device("cuda", local)
+    L, C, B = L_SARS, hi - lo, args.many_batches
     t0 = time.perf_counter()
     d = many_bams_columns(ref, B, args.many_depth, seed=1000, lo=lo, hi=hi, max_depth=8000, device=dev)
     torch.cuda.synchronize()
@@ -401,36 +445,28 @@ def run_config4(args, D, local, world, rank):
     med = float(np.median(times))
     t_acc = float(np.mean(acc)) * 1e-3 if len(acc) else float("nan")
     # bytes the kernel must move for this layout: base_code + qual + u64 offsets + u32 first-sample per column
-    # read, 56-B candidate records written.  (SURVEY §8(d)'s canonical 2E + 4BC + 68C also credits per-BAM
-    # offsets this layout never reads and a full table calls-only mode never writes: reported, not used.)
-    read = 2 * E + 8 * (C + 1) + 4 * C + C
-    moved = read + 56 * n_cand
-    canon = 2 * E + 4 * B * C + 68 * C
+    # read, 56-B candidate records written
+    moved = 2 * E + 8 * (C + 1) + 4 * C + C + 56 * n_cand
     eng.close()
     del d
     torch.cuda.empty_cache()
-    res = {
-        "workload": f"{B} synthetic SARS-CoV-2 BAMs x {args.many_depth:.0f}x (per-BAM cap 8000, generated in HBM) "
-                    f"as one column-major multi-BAM batch (spg_accumulate_samples), accumulated into one memory + "
-                    f"finalize per step; coordinate-sharded x{world}",
+    return {
+        "workload": f"{B} synthetic SARS-CoV-2 BAMs x {args.many_depth:.0f}x as ONE column-major multi-BAM batch "
+                    f"(spg_accumulate_samples; not a layout the drop-in produces), accumulated + finalized per step",
         "value": B * L * K / med, "unit": "positions/s (BAMs x L per step)",
-        "ms_per_step": med / K * 1e3, "steps": K, "measurements": len(times),
+        "ms_per_step": med / K * 1e3, "steps": K * len(times), "steps_per_measurement": K,
         "entries_per_gpu_step": E, "columns_per_gpu": C, "datagen_s": t_gen,
         "kernel": kernel_name(E, C)[0], "accumulate_ms": t_acc * 1e3, "accumulate_samples": int(len(acc)),
-        "finalize_ms": fin,
+        "finalize_ms": fin, "candidates_per_gpu_step": n_cand, "replayed_positions_per_gpu_step": n_replay,
         "roofline": {"bound": "hbm", "achieved": moved / t_acc / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                      "frac": moved / t_acc / PEAK_HBM, "algorithmic_bytes": moved,
-                     "survey_canonical_bytes": canon, "traffic": pmc_traffic(kernel_name(E, C)[1], E)},
-        "candidates_per_gpu_step": n_cand, "replayed_positions_per_gpu_step": n_replay,
-    }
-    if args.runs_batches > 0:
-        res["live_runs"] = run_config4_runs(args, D, local, world, rank, ref, lo, hi)
-    return res
+                     "traffic": pmc_traffic(kernel_name(E, C)[1], E)}}
 
 
 def run_config4_runs(args, D, local, world, rank, ref, lo, hi):
     """Config 4 as per-BAM CSR batches (batch-major, what one process_bam per BAM produces), counted at the
-    finalize (counted mode: k_acc_lite_run + k_count_list + k_fold_hist + the sparse k_finalize)."""
+    finalize (counted mode: k_acc_lite_run + k_count_list + k_fold_hist + the sparse k_finalize); then the
+    per-BAM finalize loop over the same batches."""
     import torch
     from covid_spings_variant_caller_amd.engine import PileupEngine
     from covid_spings_variant_caller_amd.synth_device import many_bams
@@ -451,24 +487,79 @@ def run_config4_runs(args, D, local, world, rank, ref, lo, hi):
 
     step(0)
     n_cand = eng.counts()[0]
+    final_calls = eng.candidates()
     K, times, acc = measure(D, step, eng, 1, max(5, args.reps // 4), args.min_ms, 1)
     med = float(np.median(times))
     t_acc = float(np.mean(acc)) * 1e-3 if len(acc) else float("nan")
     # bytes the run must move: each BAM's base_code + qual + u64 offsets, the REF chars, the candidate records
     moved = 2 * E + 8 * B * (C + 1) + C + 56 * n_cand
     kname = "counted mode: k_acc_lite_run + k_count_list + k_fold_hist + sparse k_finalize"
+    res = {"workload": f"{B} synthetic SARS-CoV-2 BAMs x {args.many_depth:.0f}x (per-BAM cap 8000, generated in HBM) "
+                       f"as per-BAM CSR batches (what LiveVariantCaller.process_bams accumulates), accumulated into one "
+                       f"memory + prepare_variants per step; coordinate-sharded x{world}",
+           "bams": B, "value": B * L * K / med, "unit": "positions/s (BAMs x L per step)",
+           "ms_per_step": med / K * 1e3, "steps": K * len(times), "steps_per_measurement": K,
+           "measurement_ms": [round(t * 1e3, 3) for t in times],
+           "entries_per_gpu_step": E, "columns_per_gpu": C, "datagen_s": t_gen, "kernel": kname,
+           "accumulate_ms": t_acc * 1e3, "accumulate_samples": int(len(acc)), "candidates_per_gpu_step": n_cand,
+           "roofline": {"bound": "hbm", "achieved": moved / t_acc / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                        "frac": moved / t_acc / PEAK_HBM, "algorithmic_bytes": moved,
+                        "traffic": pmc_traffic_sum(("spg::k_acc_lite_run", "spg::k_count_list", "spg::k_fold_hist",
+                                                    "spg::k_finalize"), E)}}
+    if args.per_bam_bams > 0:
+        res["per_bam_finalize"] = per_bam_loop(args, D, eng, data, recs, min(B, args.per_bam_bams), C, final_calls)
     eng.close()
     del data
     torch.cuda.empty_cache()
-    return {"bams": B, "value": B * L * K / med, "unit": "positions/s (BAMs x L per step)",
-            "ms_per_step": med / K * 1e3, "steps": K, "measurements": len(times),
-            "measurement_ms": [round(t * 1e3, 3) for t in times],
-            "entries_per_gpu_step": E, "datagen_s": t_gen, "kernel": kname,
-            "accumulate_ms": t_acc * 1e3, "accumulate_samples": int(len(acc)), "candidates_per_gpu_step": n_cand,
-            "roofline": {"bound": "hbm", "achieved": moved / t_acc / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                         "frac": moved / t_acc / PEAK_HBM, "algorithmic_bytes": moved,
-                         "traffic": pmc_traffic_sum(("spg::k_acc_lite_run", "spg::k_count_list", "spg::k_fold_hist",
-                                                     "spg::k_finalize"), E)}}
+    return res
+
+
+def per_bam_loop(args, D, eng, data, recs, nb, C, final_calls):
+    """vc_queue.py:142-144 without the file I/O: per BAM, accumulate its batch (process_bam's accumulate step), then
+    prepare_variants (finalize + the call table read back to the host, as write_vcf needs it).  Every finalize
+    after the first counts only the new BAM and re-folds only the positions that can call (incremental counted
+    mode); the first is the fused single-batch finalize."""
+    import torch
+    eng.reset()
+    eng.sync()
+    eng.kernel_times(4096)
+    eng.set_timing(2)
+    lat, gpu = np.zeros(nb), np.zeros(nb)
+    n_calls = np.zeros(nb, np.int64)
+    D.barrier()
+    t0 = time.perf_counter()
+    done = 0
+    for i in range(nb):
+        t = time.perf_counter()
+        eng.accumulate_records(recs[i:i + 1])
+        eng.finalize()
+        calls = eng.candidates()                    # device -> host (synchronises the step)
+        lat[i] = time.perf_counter() - t
+        n_calls[i] = len(calls)
+        if (i + 1) % 128 == 0 or i == nb - 1:       # the timing ring holds 256 finalizes
+            a, f = eng.kernel_times(4096)
+            gpu[done:done + len(a)] = (a + f) * 1e-3
+            done += len(a)
+    total = D.max(time.perf_counter() - t0)
+    eng.set_timing(0)
+    same = nb != len(data) or (len(calls) == len(final_calls) and np.array_equal(calls, final_calls))
+    E_b = data.n_entries[:nb].astype(np.float64)
+    # bytes per BAM the finalize path must move: the new BAM's base_code + qual + offsets (counted), the per-position
+    # totals and REF chars the listing reads (2 x u32 + 1 B), the calls written
+    moved = 2 * E_b + 8 * (C + 1) + 9 * C + 56 * n_calls
+    g = gpu[:done]
+    return {"bams": nb, "total_s": total, "ms_per_bam": total / nb * 1e3,
+            "latency_ms_p50": float(np.median(lat)) * 1e3, "latency_ms_p99": float(np.percentile(lat, 99)) * 1e3,
+            "latency_ms_first_100": float(np.mean(lat[:100])) * 1e3, "latency_ms_last_100": float(np.mean(lat[-100:])) * 1e3,
+            "gpu_ms_per_bam": float(np.mean(g)) * 1e3, "gpu_ms_last_100": float(np.mean(g[-100:])) * 1e3,
+            "bams_per_s": nb / total, "calls_last": int(n_calls[-1]), "final_table_equals_one_shot": bool(same),
+            "path": "per BAM: spg_accumulate_batches (1 borrowed batch) + spg_finalize (BAM 1: fused k_acc_tile; then "
+                    "counted mode: k_acc_lite_run over the new BAM, k_count_list, incremental k_fold_hist, sparse "
+                    "k_finalize) + spg_get_candidates",
+            "roofline": {"bound": "hbm (launch-bound at 6 MB per BAM)", "achieved": float(np.mean(moved[:done]) / np.mean(g) / 1e9),
+                         "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                         "frac": float(np.mean(moved[:done]) / np.mean(g) / PEAK_HBM),
+                         "algorithmic_bytes_per_bam": float(np.mean(moved))}}
 
 
 def cpu_model():
@@ -660,6 +751,14 @@ def end_to_end(args, device):
 
 def main():
     args = parse()
+    legs = set() if args.legs == "none" else set(args.legs.split(","))
+    if args.no_parity: legs.discard("parity")
+    if args.no_chr1: legs.discard("chr1")
+    if args.no_e2e: legs.discard("e2e")
+    if args.no_cpu_baseline: legs.discard("cpu")
+    if args.many_batches <= 0 and args.runs_batches <= 0: legs.discard("config4")
+    if not args.e2e_threads:
+        args.e2e_threads = max(16, len(os.sched_getaffinity(0)) // 8)
     import torch
     import spings  # noqa: F401
 
@@ -692,7 +791,7 @@ def main():
         "metric": ("pileup positions/s at 10,000x depth (SARS-CoV-2, synthetic)" if args.workload == "sars10k"
                    and depth == 10000 and L == L_SARS else f"pileup positions/s at {depth:,.0f}x depth ({contig} "
                    f"L={L:,}, synthetic)"),
-        "value": main_pt["value"], "unit": "positions/s", "n_gpus": world, "steps": main_pt["steps"],
+        "value": main_pt["value"], "unit": "positions/s", "n_gpus": world, "steps": main_pt["steps"] * main_pt["reps"],
         "warmup": args.warmup, "ms_per_step": main_pt["ms_per_step"], "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8/f64", "data": "synthetic",
         "config": {"workload": f"{args.workload}: {contig} L={L}, {depth:.0f}x, 150-bp reads, "
@@ -702,8 +801,10 @@ def main():
                    "parallelism": f"coord-shard x{world}",
                    "engine_mode": "full_table" if args.full_table else "calls_only"},
         "timing": {"measurements": len(main_pt["measurements_ms"]), "steps_per_measurement": main_pt["steps"],
+                   "steps_timed_total": main_pt["steps"] * main_pt["reps"],
                    "steps_requested": args.steps, "measurement_ms": main_pt["measurements_ms"],
-                   "statistic": "median measurement; max over ranks"},
+                   "statistic": "median measurement (each >= --min-ms of back-to-back steps); max over ranks; "
+                                "`steps` = every timed step of the 20 measurements"},
         "roofline": {"bound": "hbm", "achieved": main_pt["achieved"] / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                      "frac": main_pt["achieved"] / PEAK_HBM,
                      "traffic": pmc_traffic(kernel_name(E, C, not args.full_table)[1], E),
@@ -715,19 +816,22 @@ def main():
         "replayed_positions_per_gpu_step": main_pt["n_replay"], "datagen_s": main_pt["t_gen"],
         "calls_gathered_per_step": main_pt["gathered"] if main_pt["gathered"] is not None else main_pt["n_cand"],
     }
-    if not args.no_parity and not args.max_depth and args.workload == "sars10k":
-        p = run_point(args, D, L, depth, 8000, local, world, rank, contig)
-        res["parity_mode"] = {"max_depth": 8000, "value": p["value"], "ms_per_step": p["ms_per_step"],
-                              "steps": p["steps"], "entries_per_gpu_step": p["E"], "kernel_ms": p["kernel_ms"],
-                              "roofline_frac": p["achieved"] / PEAK_HBM, "finalize_ms": p["finalize_ms"],
-                              "candidates_per_gpu_step": p["n_cand"], "kernel": kernel_name(p["E"], p["C"])[0]}
-    if args.many_batches > 0 and args.workload == "sars10k":
+    nested = args.workload == "sars10k" and not args.length and not args.depth
+    if "parity" in legs and not args.max_depth and nested:
+        res["parity_mode"] = nested_point(args, D, "sars10k", local, world, rank, max_depth=8000)
+    if "sars1k" in legs and nested:           # BASELINE config 2
+        res["sars1k"] = nested_point(args, D, "sars1k", local, world, rank, samples=args.sars1k_samples,
+                                     distinct=min(16, args.sars1k_samples * world))
+    if "sars100k" in legs and nested:         # BASELINE config 3, uncapped (the LDS stress) and pysam's cap
+        res["sars100k"] = nested_point(args, D, "sars100k", local, world, rank)
+        res["sars100k"]["parity_mode"] = nested_point(args, D, "sars100k", local, world, rank, max_depth=8000)
+    if "config4" in legs and nested:          # BASELINE config 4
         res["config4"] = run_config4(args, D, local, world, rank)
-    if not args.no_chr1 and args.workload == "sars10k":
-        res["chr1_30x"] = nested_point(args, D, "chr1_30x", local, world, rank)
-    if rank == 0 and world == 1 and not args.no_e2e and L == L_SARS:
+    if "chr1" in legs and nested:             # BASELINE config 5
+        res["chr1_30x"] = nested_point(args, D, "chr1_30x", local, world, rank, step_frac=True)
+    if rank == 0 and world == 1 and "e2e" in legs and L == L_SARS:
         res["end_to_end"] = end_to_end(args, 0)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and "cpu" in legs:
         res["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
         print(json.dumps(res), flush=True)

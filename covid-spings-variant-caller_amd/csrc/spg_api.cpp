@@ -19,10 +19,6 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
                              const uint8_t *ref, const Tables *T, Acc *acc, hipStream_t st);
 hipError_t launch_finalize(const FParams &F, const Acc *acc, const Tables *T, const Out &O, const Hist *H,
                            hipStream_t st);
-hipError_t launch_multi(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, bool nt,
-                        int64_t max_blocks, bool fused, hipStream_t st);
-hipError_t launch_one(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc,
-                      int64_t max_blocks, bool fused, hipStream_t st);
 hipError_t launch_lite(const MParams &P, const Hist &hb, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
                        hipStream_t st);
 int lite_blocks_per_cu();
@@ -162,8 +158,11 @@ struct spg_ctx {
     int64_t h_hist_cap = 0;
     int64_t pend0 = 0;                  // history batches [pend0, size) are not accumulated yet (a run)
     uint64_t pend_entries = 0;
-    uint32_t *kerr = nullptr;           // k_acc_multi error word (a batch too deep for a run)
+    uint32_t *kerr = nullptr;           // run kernels' error word (bit 0: a batch too deep for a run), compute stream
     bool kerr_dirty = false;            // a kernel that may set kerr was enqueued since it was last cleared
+    uint32_t *ferr = nullptr;           // k_pileup_fill's error word (bit 2: the records disagree with the offsets):
+                                        // written, read and cleared on the copy stream, where the fills run
+    bool ferr_dirty = false;
     uint32_t *nlist = nullptr;          // fused run: positions listed for the sparse finalize (in `band`)
     uint32_t *deep_list = nullptr;      // single shallow batch: its long columns (for k_acc_seg<1>) ...
     int64_t deep_cap = 0;
@@ -179,6 +178,8 @@ struct spg_ctx {
     int64_t count_end = 0;
     int64_t n_deep_hist = 0;            // deep / multi-sample batches since reset (counted mode needs none)
     uint32_t *cdep = nullptr, *cmcf = nullptr;
+    uint64_t *fwm = nullptr;            // k_fold_hist's per-position fold watermarks ((generation << 32) | batches)
+    uint32_t count_gen = 0;             // generation of the current counted run (bumped whenever counted mode starts)
     void *fold_part = nullptr;          // k_fold_hist's multi-workgroup partials [FOLD_CAP][FOLD_BPP]
     uint32_t *fold_arrived = nullptr;   // ... and arrival counts (zero between launches)
     // bounded history: owned batches past `hist_cap` bytes of HBM are spilled, oldest folded first
@@ -227,6 +228,7 @@ struct spg_ctx {
     bool table_valid = false;           // the SoA table matches the last finalize
     int timing = default_timing();
     int acc_timing = 0;                 // level the open / last accumulate interval was recorded at
+    int64_t path[8] = {};               // spg_path_counters
 };
 
 
@@ -276,9 +278,12 @@ static int alloc_outputs(spg_ctx *c) {
     memset(c->h_fused, 0, 2 * sizeof(FusedArgs));
     HIPCHK(hipMemsetAsync(c->ctr, 0, 2 * sizeof(Counters), c->stream));
     HIPCHK(hipMalloc(&c->kerr, sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&c->ferr, sizeof(uint32_t)));
     HIPCHK(hipMalloc(&c->nlist, sizeof(uint32_t)));
     HIPCHK(hipMalloc(&c->deep_n, sizeof(uint32_t)));
     HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));
+    HIPCHK(hipMemsetAsync(c->ferr, 0, sizeof(uint32_t), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));        // (ferr is then used on the copy stream)
     return 0;
 }
 
@@ -345,7 +350,8 @@ int spg_destroy(spg_ctx *c) {
     c->arena.release();
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
-                    c->d_fused, c->deep_list, c->deep_n, c->cdep, c->cmcf, c->fold_part, c->fold_arrived, c->rs};
+                    c->d_fused, c->deep_list, c->deep_n, c->cdep, c->cmcf, c->fwm, c->fold_part, c->fold_arrived, c->rs,
+                    c->ferr};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
@@ -383,6 +389,11 @@ int spg_reset(spg_ctx *c) {
     if (c->kerr_dirty) {
         HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));
         c->kerr_dirty = false;
+    }
+    // (on the copy stream: ordered after the dropped sample's records fills, before the next sample's)
+    if (c->ferr_dirty) {
+        HIPCHK(hipMemsetAsync(c->ferr, 0, sizeof(uint32_t), c->copy_stream));
+        c->ferr_dirty = false;
     }
     if (++c->epoch == 0) {     // wrapped: clear the records once and restart at epoch 1
         HIPCHK(hipMemsetAsync(c->acc, 0, sizeof(Acc) * c->n_pos, c->stream));
@@ -639,7 +650,7 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
     P.n_entries = hb.n_entries;
     P.dbg = trace_on() ? trace_dbg() : nullptr;
-    if (listed) {                 // the long columns k_acc_multi listed, one per wave
+    if (listed) {                 // the long columns the run kernel listed, one per wave
         P.G = 1;
         P.G2 = 1;
         P.deep_list = c->deep_list;
@@ -692,35 +703,21 @@ static int flush_deep(spg_ctx *c) {
     return acc_end(c);
 }
 
-// How a run of shallow batches [h0, h1) over positions [u0, u1) is folded.  k_acc_tile (default): LPC lanes
-// per column so that a tile's bytes of one batch fit a 2 KiB DMA slot (TC = 64 / LPC columns per tile), and
-// the batch range split S ways when the tiles alone cannot fill the resident grid (items of equal work:
-// S is the smallest split whose last round keeps >= 90 % of the waves busy).  SPG_SHALLOW=old: the r02
-// kernels (k_acc_one / k_acc_multi, A/B only).
+// How a run of shallow batches [h0, h1) over positions [u0, u1) is folded by k_acc_tile: LPC lanes per
+// column so that a tile's bytes of one batch fit a 2 KiB DMA slot (TC = 64 / LPC columns per tile), and the
+// batch range split S ways when the tiles alone cannot fill the resident grid (items of equal work: S is the
+// smallest split whose last round keeps >= 90 % of the waves busy).
 struct RunPlan {
-    bool tile;
     int lpc;
     int64_t n_groups, S, kper, tc;
 };
-static bool shallow_old() {
-    static const bool old = [] { const char *e = getenv("SPG_SHALLOW"); return e && strcmp(e, "old") == 0; }();
-    return old;
-}
 static int64_t tile_blocks(const spg_ctx *c, int lpc, bool fused, bool one) {
     static const int64_t env = [] { const char *e = getenv("SPG_TILE_BLOCKS"); return e ? atoll(e) : 0ll; }();
     return env > 0 ? env : (int64_t)c->n_cu * tile_blocks_per_cu(lpc, fused, one);
 }
 static RunPlan plan_run(const spg_ctx *c, int64_t h0, int64_t h1, int64_t u0, int64_t u1, uint64_t run_entries) {
     const int64_t K = h1 - h0, L = u1 - u0;
-    RunPlan R{!shallow_old(), 1, 0, 1, K, 64};
-    if (!R.tile) {
-        R.n_groups = (L + 63) / 64;
-        static const int64_t target_items = env_i64("SPG_MULTI_ITEMS", 16384);
-        int64_t S = std::min<int64_t>(K, std::max<int64_t>(1, target_items / std::max<int64_t>(1, R.n_groups)));
-        R.kper = (K + S - 1) / S;
-        R.S = (K + R.kper - 1) / R.kper;
-        return R;
-    }
+    RunPlan R{1, 0, 1, K, 64};
     // bytes of one batch in a tile: TC x mean column length (whole 16-B blocks around it)
     static const double fill = [] { const char *e = getenv("SPG_TILE_FILL"); return e ? atof(e) : 1984.0; }();
     const double mean = (double)run_entries / ((double)K * (double)std::max<int64_t>(1, L));
@@ -758,7 +755,6 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
         u0 = std::min(u0, c->hist[(size_t)i].pos_begin);
         u1 = std::max(u1, c->hist[(size_t)i].pos_begin + c->hist[(size_t)i].n_cols);
     }
-    const bool nt = 2 * c->pend_entries > (192ull << 20);
     c->pend0 = h1;
     c->pend_entries = 0;
     if (int rc = wait_copies(c)) return rc;
@@ -799,7 +795,7 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
     }
     // partial states folded by k_merge_parts: a split run, or (k_acc_tile) any run into records that may
     // already hold this sample's earlier batches
-    const bool use_part = P.S > 1 || (R.tile && !P.fresh);
+    const bool use_part = P.S > 1 || !P.fresh;
     if (use_part) {
         const size_t need = sizeof(MState) * (size_t)P.S * (size_t)P.pstride;
         if (need > c->part_bytes) {
@@ -828,8 +824,7 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
     }
     // a FUSED single shallow batch into a FRESH memory (process_bam + prepare_variants; mean column <= 40
     // entries): k_acc_lite, counts + the exact fold of the columns that may call
-    static const bool lite_on = [] { const char *e = getenv("SPG_LITE"); return !(e && atoi(e) == 0); }();
-    const bool lite = lite_on && fused && K == 1 && P.fresh && (double)run_entries <= 40.0 * (double)(u1 - u0);
+    const bool lite = fused && K == 1 && P.fresh && (double)run_entries <= 40.0 * (double)(u1 - u0);
     if (lite) {
         static const int64_t lb = env_i64("SPG_LITE_BLOCKS", 0);
         P.n_groups = (int32_t)((u1 - u0 + 63) / 64);
@@ -837,20 +832,13 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
                            c->stream));
         // the listed positions' exact fold (their records; deep columns are k_acc_seg<1>'s below)
         HIPCHK(launch_lite_fold(P, c->h_hist[h0], c->ref, c->tables, c->acc, 2 * (int64_t)c->n_cu, c->stream));
-    } else if (R.tile) {
+    } else {
+        if (!fused) c->path[0]++;
         HIPCHK(launch_tile(P, c->d_hist, c->ref, c->ref_len, c->tables, c->acc, R.lpc, tile_blocks(c, R.lpc, fused, K == 1), fused,
                            c->stream));
         if (use_part) HIPCHK(launch_merge(P, c->ref, c->acc, c->stream));
-    } else {
-        static const int64_t max_blocks = env_i64("SPG_MULTI_BLOCKS", 6144);
-        // a single shallow batch into a FRESH memory (mean column <= 40 entries): k_acc_one; else k_acc_multi
-        if (K == 1 && h0 == 0 && (double)run_entries <= 40.0 * (double)(u1 - u0))
-            HIPCHK(launch_one(P, c->d_hist, c->ref, c->tables, c->acc, max_blocks, fused, c->stream));
-        else
-            HIPCHK(launch_multi(P, c->d_hist, c->ref, c->tables, c->acc, nt, max_blocks, fused, c->stream));
     }
-    if (int rc = trace_sync(c, lite ? "accumulate (k_acc_lite)" : R.tile ? "accumulate (k_acc_tile)" : "accumulate (k_acc_multi)"))
-        return rc;
+    if (int rc = trace_sync(c, lite ? "accumulate (k_acc_lite)" : "accumulate (k_acc_tile)")) return rc;
     if (K == 1) {
         // a single shallow batch: its long columns (>= 128 entries), listed by the run kernel, go through the
         // wave-wide kernel
@@ -866,6 +854,7 @@ static int materialize(spg_ctx *c) {
     if (!c->stale) return 0;
     c->stale = false;
     c->counted = false;            // the records hold history [0, stale_end) again; pending batches fold into them
+    c->path[1]++;
     const int64_t keep = c->pend0;
     c->pend0 = 0;
     const int rc = flush_run(c, c->stale_end, false);
@@ -883,6 +872,15 @@ static int64_t run_splits(const spg_ctx *c, int64_t h0, int64_t h1) {
         e += c->hist[(size_t)i].n_entries;
     }
     return plan_run(c, h0, h1, u0, u1, e).S;
+}
+
+// Counted mode (count_pending) may take a calls-only sample of shallow single-sample batches whose records are
+// not needed as they stand: none written yet (pend0 == 0), or stale (a fused finalize or counted mode left them
+// unwritten; counting reads the history, not the records).  vc_queue.py:142-144 finalizes after every BAM: the
+// first BAM's finalize is fused (k_acc_lite / k_acc_tile FUSED), every later one counts.
+static bool countable(const spg_ctx *c) {
+    return (c->p.flags & SPG_P_CALLS_ONLY) && c->n_deep_hist == 0 && !c->deep_pend &&
+           (c->counted || c->stale || c->pend0 == 0);
 }
 
 static bool is_pinned(const void *p) {
@@ -945,9 +943,7 @@ static int enforce_history_cap(spg_ctx *c) {
         if (c->hist[(size_t)i].dev0 && c->hist[(size_t)i].n_samples == 1) movable += (int64_t)c->hist[(size_t)i].bytes;
     if (c->hist_dev_bytes - movable > c->hist_cap && nh > folded) {
         // fold the pending batches first (all but the newest: it stays pending for the next finalize)
-        const bool can_count = (c->p.flags & SPG_P_CALLS_ONLY) && c->n_deep_hist == 0 && !c->deep_pend &&
-                               (c->counted || (c->pend0 == 0 && !c->stale));
-        if (can_count) {
+        if (countable(c)) {
             if (int rc = count_pending(c)) return rc;
             folded = c->count_end;
         } else {
@@ -1023,8 +1019,8 @@ static int upload_records(spg_ctx *c, const spg_records *R, const HistBatch &hb,
     A.n_tiles = (int32_t)n_tiles;
     A.n_reads = (uint32_t)n;
     A.back = (int32_t)((R->max_span + 63) / 64);
-    A.err = c->kerr;
-    c->kerr_dirty = true;
+    A.err = c->ferr;
+    c->ferr_dirty = true;
     HIPCHK(launch_pileup_fill(A, cs));
     return 0;
 }
@@ -1036,8 +1032,8 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
     if (n_samples < 1 || n_samples > (1 << 30)) return fail("spg_accumulate_samples: n_samples out of range");
     static const double deep_min = [] { const char *e = getenv("SPG_DEEP_MIN"); return e ? atof(e) : 256.0; }();
     const bool deep_batch = (n_cols > 0 && (double)n_entries / (double)n_cols >= deep_min) || n_samples > 1 || first_sample;
-    // counted mode keeps the records stale while shallow batches arrive (they are counted at the next finalize)
-    if (!(c->counted && !deep_batch))
+    // a shallow batch into a countable sample leaves the records stale (it is counted at the next finalize)
+    if (deep_batch || n_samples > 1 || !countable(c))
         if (int rc = materialize(c)) return rc;
     if (int rc = flush_deep(c)) return rc;
     if (n_cols < 0 || pos_begin < 0 || pos_begin + n_cols > c->n_pos)
@@ -1139,15 +1135,15 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
         // its own (a run folds single-sample batches with consecutive batch numbers)
         if (int rc = flush_run(c, idx)) return rc;
         c->pend0 = idx + 1;
-        static const bool no_fuse = getenv("SPG_NO_FUSE") != nullptr;
-        if (idx == 0 && (c->p.flags & SPG_P_CALLS_ONLY) && !no_fuse) {
+        if (idx == 0 && (c->p.flags & SPG_P_CALLS_ONLY)) {
             c->deep_pend = true;               // the sample's first batch: launched by spg_finalize
             return 0;
         }
         if (int rc = wait_copies(c)) return rc;
         if (int rc = acc_begin(c)) return rc;
         if (int rc = launch_seg(c, idx, true)) return rc;
-        return acc_end(c);
+        if (int rc = acc_end(c)) return rc;
+        return enforce_history_cap(c);         // every batch is folded now: any of them may move
     }
     c->pend_entries += n_entries;
     // (calls-only: the pending run waits for the finalize, which counts it — see finalize_counted)
@@ -1214,6 +1210,24 @@ int spg_accumulate_records(spg_ctx *c, const spg_records *r, uint32_t flags) {
         return fail("spg_accumulate_records: null buffer");
     if (r->n_cols > 0 && (r->offsets[0] != 0 || r->offsets[r->n_cols] != r->n_entries))
         return fail("spg_accumulate_records: offsets[0] must be 0 and offsets[n_cols] == n_entries");
+    // the fill writes column c's entries at [offsets[c], offsets[c + 1]) and reads each read's fixed fields at
+    // rec[i] + 0..35: both bounded here (O(n_cols + n_reads) branch-free scans)
+    if (r->n_cols > 0) {
+        uint64_t desc = 0;
+        for (int64_t i = 0; i < r->n_cols; i++) desc |= (uint64_t)(r->offsets[i + 1] < r->offsets[i]);
+        if (desc) return fail("spg_accumulate_records: offsets not monotone");
+    }
+    if (r->n_reads > 0) {
+        uint64_t hi = 0;
+        int32_t thi = -1;
+        for (int64_t i = 0; i < r->n_reads; i++) {
+            hi = std::max(hi, r->rec[i]);
+            thi = std::max(thi, r->tweak[i]);
+        }
+        if (r->data_bytes < 36 || hi > r->data_bytes - 36)
+            return fail("spg_accumulate_records: a record offset points past the records buffer");
+        if (thi >= (int32_t)r->n_tweaks) return fail("spg_accumulate_records: tweak index >= n_tweaks");
+    }
     (void)flags;
     HIPCHK(hipSetDevice(c->device));
     bool pageable = false;
@@ -1338,6 +1352,13 @@ static int count_pending(spg_ctx *c) {
         if (!c->cdep) {
             HIPCHK(hipMalloc(&c->cdep, sizeof(uint32_t) * c->n_pos));
             HIPCHK(hipMalloc(&c->cmcf, sizeof(uint32_t) * c->n_pos));
+            HIPCHK(hipMalloc(&c->fwm, sizeof(uint64_t) * c->n_pos));
+            HIPCHK(hipMemsetAsync(c->fwm, 0, sizeof(uint64_t) * c->n_pos, c->stream));
+        }
+        // a new counted run: records folded before it (by other paths) carry no watermark of this generation
+        if (++c->count_gen == 0) {
+            HIPCHK(hipMemsetAsync(c->fwm, 0, sizeof(uint64_t) * c->n_pos, c->stream));
+            c->count_gen = 1;
         }
         HIPCHK(hipMemsetAsync(c->cdep, 0, sizeof(uint32_t) * c->n_pos, c->stream));
         HIPCHK(hipMemsetAsync(c->cmcf, 0, sizeof(uint32_t) * c->n_pos, c->stream));
@@ -1387,6 +1408,7 @@ static int count_pending(spg_ctx *c) {
         P.S = (int32_t)((K + P.kper - 1) / P.kper);
         P.n_groups = (int32_t)n_tiles;
         HIPCHK(launch_count_run(P, c->d_hist, c->ref, c->cdep, c->cmcf, lpc, blocks, c->stream));
+        c->path[7] += K;
         if (int rc = trace_sync(c, "accumulate (k_acc_lite_run)")) return rc;
     }
     c->count_end = nh;
@@ -1422,7 +1444,10 @@ static int finalize_counted(spg_ctx *c) {
     P.ratio_lo = c->p.min_evidence_ratio * (1.0 - 1e-9);
     P.list = c->band;
     P.n_list = c->nlist;
-    // list, then the exact records of the listed positions over the whole history
+    P.wm = c->fwm;
+    P.wm_gen = c->count_gen;
+    // list, then the exact records of the listed positions over the whole history (incremental: a listed
+    // position's record from an earlier counted finalize takes only the batches since)
     HIPCHK(hipMemsetAsync(c->nlist, 0, sizeof(uint32_t), c->stream));
     P.u0 = ua;
     P.u1 = ub;
@@ -1460,21 +1485,21 @@ static int finalize_impl(spg_ctx *c, bool table) {
     // pre-filter in one pass, finalize only the listed positions.  Otherwise: records complete, every
     // position.
     const int64_t nh = (int64_t)c->hist.size();
-    static const bool no_fuse = getenv("SPG_NO_FUSE") != nullptr;
     // one deep batch pending: accumulate + finalize in one launch
     const bool fused_deep = !table && c->deep_pend && nh == 1;
     if (!fused_deep)
         if (int rc = flush_deep(c)) return rc;
-    static const bool no_count = getenv("SPG_NO_COUNT") != nullptr;
-    const bool counted = !fused_deep && !table && !no_fuse && !no_count && (c->p.flags & SPG_P_CALLS_ONLY) && nh >= 2 &&
-                         c->n_deep_hist == 0 && (c->counted || (c->pend0 == 0 && !c->stale));
-    const bool fused = !counted && !fused_deep && !table && !no_fuse && (c->p.flags & SPG_P_CALLS_ONLY) && c->pend0 == 0 &&
+    const bool counted = !fused_deep && !table && nh >= 2 && countable(c);
+    const bool fused = !counted && !fused_deep && !table && (c->p.flags & SPG_P_CALLS_ONLY) && c->pend0 == 0 &&
                        nh > 0 && run_splits(c, 0, nh) == 1;
     if (fused_deep) {
         c->deep_pend = false;
+        c->path[5]++;
     } else if (counted) {
         if (int rc = finalize_counted(c)) return rc;
+        c->path[4]++;
     } else if (fused) {
+        c->path[6]++;
         if (int rc = flush_run(c, -1, true)) return rc;
         c->stale = true;
         c->stale_end = nh;
@@ -1505,6 +1530,7 @@ static int finalize_impl(spg_ctx *c, bool table) {
     } else {
         if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
         if (fused || counted) { F.list = c->band; F.n_list = c->nlist; }
+        c->path[(fused || counted) ? 3 : 2]++;
         if (int rc = upload_ridx(c, F.ridx)) return rc;
         HIPCHK(launch_finalize(F, c->acc, c->tables, make_out(c), c->d_hist, c->stream));
         if (trace_sync(c, "finalize")) return -1;
@@ -1543,13 +1569,21 @@ static int settle(spg_ctx *c, Counters &h) {
         HIPCHK(hipMemcpyAsync(&h, c->ctr + c->cslot, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (h.err) return fail("spg: replay found a depth mismatch between history and accumulators");
-        uint32_t kerr = 0;
-        HIPCHK(hipMemcpy(&kerr, c->kerr, sizeof(kerr), hipMemcpyDeviceToHost));
-        c->kerr_dirty = false;         // the stream is idle: zero, or cleared below (reported once)
-        if (kerr & 2) {
-            HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));   // reported once
-            return fail("spg: spg_accumulate_records: the records disagree with the batch's offsets (inconsistent plan)");
+        if (c->ferr_dirty) {
+            // every records fill enqueued so far has run (the ones this finalize read, and any enqueued since)
+            uint32_t ferr = 0;
+            HIPCHK(hipMemcpyAsync(&ferr, c->ferr, sizeof(ferr), hipMemcpyDeviceToHost, c->copy_stream));
+            HIPCHK(hipStreamSynchronize(c->copy_stream));
+            c->ferr_dirty = false;
+            if (ferr) {
+                HIPCHK(hipMemsetAsync(c->ferr, 0, sizeof(uint32_t), c->copy_stream));   // reported once
+                return fail("spg: spg_accumulate_records: the records disagree with the batch's offsets (inconsistent plan)");
+            }
         }
+        uint32_t kerr = 0;
+        HIPCHK(hipMemcpyAsync(&kerr, c->kerr, sizeof(kerr), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->kerr_dirty = false;         // the stream is idle: zero, or cleared below (reported once)
         if (kerr) {
             HIPCHK(hipMemsetAsync(c->kerr, 0, sizeof(uint32_t), c->stream));   // reported once
             return fail("spg: a shallow batch held >= 2^30 entries in 64 consecutive columns; accumulate it "
@@ -1698,6 +1732,12 @@ int spg_kernel_times(spg_ctx *c, float *acc_ms, float *fin_ms, int64_t cap, int6
     }
     c->ring_r += n;
     *n_out = n;
+    return 0;
+}
+
+int spg_path_counters(spg_ctx *c, int64_t *out, int64_t n) {
+    if (!c || (!out && n > 0)) return fail("spg_path_counters: bad argument");
+    for (int64_t i = 0; i < std::min<int64_t>(n, 8); i++) out[i] = c->path[i];
     return 0;
 }
 

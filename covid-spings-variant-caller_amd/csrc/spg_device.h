@@ -97,12 +97,12 @@ struct KParams {
     const uint32_t *fsamp; // multi-sample batch: per column, the first sample holding entries (else null)
     uint32_t *dbg;         // SPG_TRACE: range violations recorded here instead of faulting (else null)
     uint4 *prog;           // SPG_TRACE: per-wave progress records in host-mapped memory (else null)
-    const uint32_t *deep_list;   // W = 1: the long columns k_acc_multi listed (batch-relative) ...
+    const uint32_t *deep_list;   // W = 1: the long columns the run kernel listed (batch-relative) ...
     const uint32_t *deep_n;      // ... and their count (null: one group of G columns per wave)
     uint4 *wtime;          // SPG_WAVE_TIMES: per wave {start, first column, lifetime} (s_memrealtime, 100 MHz), hw id
 };
 
-// Per-position state of one lane of k_acc_multi over a run of batches (lane-private, in LDS), and
+// Per-position state of a run of batches folded by one lane group (k_acc_tile), and
 // the partial record one batch split hands to k_merge_parts (same 176-B layout in HBM).
 struct __align__(16) MState {
     uint32_t depth, n_del, n_skip, n_other;
@@ -119,7 +119,7 @@ struct __align__(16) MState {
 };
 static_assert(sizeof(MState) == 176, "MState layout");
 
-struct MParams {             // one k_acc_multi launch: history batches [h0, h0 + K) over positions [u0, u1)
+struct MParams {             // one run-kernel launch: history batches [h0, h0 + K) over positions [u0, u1)
     int64_t u0, u1;
     int32_t h0, K;
     int32_t S, kper;         // batch splits (partial records merged by k_merge_parts when S > 1)
@@ -146,6 +146,12 @@ struct MParams {             // one k_acc_multi launch: history batches [h0, h0 
     double ratio_lo;         // min_evidence_ratio * (1 - 1e-9): the conservative AD/DP pre-check
     int64_t *list;           // positions whose record was written (the sparse finalize's input)
     uint32_t *n_list;
+    // counted mode's exact fold (k_fold_hist), incremental: wm[p] = (wm_gen << 32) | n says position p's record
+    // already holds history batches [0, n) (written by an earlier counted finalize of this sample; any other
+    // generation: fold from batch 0)
+    uint64_t *wm;
+    uint32_t wm_gen;
+    uint32_t pad_wm;
 };
 
 // Replay index: history batches overlapping each 2^RIDX_SHIFT-position bucket, in accumulate order.

@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void k_pileup_fill(FillArgs A) {
         uint32_t ncig = 0, ls = 0, y = 0, ci = 0, op = 0, len = 0;
         int32_t tcol = INT32_MIN;                // D/N entries in columns < tcol read orig (none: no tweak)
         if (act) {
-            const uint64_t ro = A.rec[r];
+            const uint64_t ro = min(A.rec[r], A.data_bytes);    // (the host checked rec + 36 <= data_bytes)
             const uint32_t l_name = ld32u(A.data, ro + 8) & 0xFF;
             ncig = ld32u(A.data, ro + 12) & 0xFFFF;
             ls = ld32u(A.data, ro + 16);

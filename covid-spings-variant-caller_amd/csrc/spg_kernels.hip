@@ -8,9 +8,8 @@
 //                  fast path (v_bcnt counts, v_dot4_u32_u8 quality sums, LDS {ln(1-eps), eps} table);
 //                  the rare entries (other alleles, D/N, q < 4, q >= 128, IUPAC) are queued as lane
 //                  slices and decoded exactly into a per-wave LDS record at column end.
-//   k_acc_multi    shallow batches, one lane per position, a run of K batches (BAMs) per launch: the
-//                  record of a position is read and written once per run (k_merge_parts folds split
-//                  runs).
+//   k_merge_parts  folds the partial states of a split run of shallow batches (k_acc_tile, spg_tile.hip)
+//                  into the records in batch order.
 //   k_finalize     prepare_variants (:120-185) + genotype_likelihood / to_phred_scale
 //                  (utils.py:12-24): per-position GL in fp64 with the reference's underflow decisions,
 //                  candidate filters, GL/PL/SCORE/QUAL.  A position whose result depends on the order
@@ -996,507 +995,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     }   // items
 }
 
-// ------------------------------------------------------------------------------------------
-// k_acc_multi: shallow batches.  One lane per reference position, one wave per 64 consecutive
-// positions, and a RUN of K batches per launch: for every batch in accumulate order the wave reads
-// the 64 columns' CSR offsets (one coalesced 520-B load) and then each lane streams its column's
-// entries in 16-B blocks (the wave's blocks of one batch cover one contiguous ~64-column range, so
-// consecutive block loads of neighbouring lanes share cache lines).  Per lane: SWAR counts / sum(q)
-// against the REF allele, a second SWAR allele promoted once a non-REF base is frequent (an SNV),
-// and every other entry decoded exactly into the lane's LDS state.  The Acc record is read and
-// written ONCE per run instead of once per batch: the reference's per-BAM appends
-// (process_pileup_column / process_svn, live_variant_caller.py:74-103, repeated by process_bam for
-// every BAM, :54-72) become one pass.  When the run's positions are too few to fill the chip (a
-// 29.9-kb genome), the run is split into S batch ranges whose partial states k_merge_parts folds in
-// order.
-// ------------------------------------------------------------------------------------------
-constexpr int MW = 4;          // waves per k_acc_multi workgroup
-
-
-template <bool NT, int MBLK, bool FUSED>
-__global__ __launch_bounds__(64 * MW) __attribute__((amdgpu_waves_per_eu(FUSED ? 2 : 3, 8))) void k_acc_multi(MParams P, const Hist *__restrict__ H,
-                                                       const uint8_t *__restrict__ ref,
-                                                       const Tables *__restrict__ T, Acc *__restrict__ acc) {
-    // rows 0..127 {ln(1-eps), eps} for q < 128; rows 128..255 zero (the index of non-selected bytes)
-    __shared__ double2 lut[256];
-    __shared__ double l1m8[256];                       // ln(1-eps) rows of the same layout (P.ref_sl)
-    __shared__ MState st[MW][64];
-    for (uint32_t q = threadIdx.x; q < 256u; q += 64u * MW) {
-        lut[q] = q < 128u ? make_double2(T->fast[q][0], T->fast[q][1]) : make_double2(0.0, 0.0);
-        l1m8[q] = q < 128u ? T->fast[q][0] : 0.0;
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    MState *ST = st[threadIdx.x >> 6];
-    MState &S = ST[lane];
-    const int64_t n_items = (int64_t)P.n_groups * P.S;
-    // grid-stride over (position group, batch split) items: the LUT is loaded once per workgroup
-    // an item's REF chars and first-batch CSR bounds (per lane), issued one item ahead: while a wave
-    // streams item i, the loads that start item i + 1 are in flight
-    const int64_t istride = (int64_t)gridDim.x * MW;
-#define SPG_ITEM_HEAD(IT)                                                                              \
-    do {                                                                                               \
-        const int64_t it_ = (IT);                                                                      \
-        rc_next = (uint8_t)'A';                                                                        \
-        ob_next = oe_next = 0;                                                                         \
-        if (it_ < n_items) {                                                                           \
-            const int32_t g_ = (int32_t)(it_ % P.n_groups), k_ = (int32_t)(it_ / P.n_groups) * P.kper;  \
-            const int64_t p_ = P.u0 + (int64_t)g_ * 64 + lane;                                          \
-            if (p_ < P.u1) {                                                                           \
-                rc_next = ref[p_];                                                                     \
-                if (k_ < P.K) {                                                                        \
-                    const Hist hn = H[P.h0 + k_];                                                      \
-                    const int64_t cn = p_ - hn.pos_begin;                                              \
-                    if (cn >= 0 && cn < hn.n_cols) {                                                   \
-                        ob_next = __builtin_nontemporal_load(hn.off + cn);                             \
-                        oe_next = __builtin_nontemporal_load(hn.off + cn + 1);                         \
-                    }                                                                                  \
-                }                                                                                      \
-            }                                                                                          \
-        }                                                                                              \
-    } while (0)
-    int64_t item = (int64_t)blockIdx.x * MW + (threadIdx.x >> 6);
-    uint8_t rc_next;
-    uint64_t ob_next, oe_next;
-    SPG_ITEM_HEAD(item);
-    for (; item < n_items; item += istride) {
-        const int32_t g = (int32_t)(item % P.n_groups), s = (int32_t)(item / P.n_groups);
-        const int64_t p0 = P.u0 + (int64_t)g * 64;
-        const int64_t p = p0 + lane;
-        const bool inr = p < P.u1;
-        ms_init(S);
-        const uint8_t refc = rc_next;
-        uint64_t obn = ob_next, oen = oe_next;
-        SPG_ITEM_HEAD(item + istride);
-        const uint32_t M = code_of_ref(refc), mrep = M * 0x01010101u;
-        const int Ms = slot_of(M);
-        // calls-only: no likelihood sums for a REF-char major (never a candidate) — except its
-        // sum(ln(1-eps)) in shallow runs (P.ref_sl)
-        const bool msum = !P.calls_only || nibble_char(M) != refc;
-        const bool any_msum = __ballot(msum && inr) != 0;
-        const bool rsl = !msum && P.ref_sl;
-        const bool any_rsl = __ballot(rsl && inr) != 0;
-        int s2 = -1;                                   // slot of the promoted second allele
-        // no second allele: code 0x7F matches nothing (the SWAR compare needs code ^ M < 0x80)
-        uint32_t mrep2 = 0x7F7F7F7Fu;
-        uint32_t fcnt = 0, fsq = 0, ffirst = INF32;
-        double fsl = 0.0, fse = 0.0;
-        uint32_t gcnt = 0, gsq = 0, gfirst = INF32;
-        double gsl = 0.0, gse = 0.0;
-        bool deep = false;
-        uint32_t sidx = 0;                             // raw entries of this position in earlier batches
-        const int32_t k0 = s * P.kper, k1 = min(P.K, k0 + P.kper);
-        // later batches' CSR bounds are loaded one batch ahead as well
-        for (int32_t k = k0; k < k1; k++) {
-            const Hist h = H[P.h0 + k];
-            const uint64_t ob = obn, oe = oen;
-            if (k + 1 < k1) {
-                const Hist hn = H[P.h0 + k + 1];
-                const int64_t cn = p - hn.pos_begin;
-                obn = oen = 0;
-                if (inr && cn >= 0 && cn < hn.n_cols) {
-                    obn = __builtin_nontemporal_load(hn.off + cn);
-                    oen = __builtin_nontemporal_load(hn.off + cn + 1);
-                }
-            }
-            const int64_t col = p - h.pos_begin;
-            const bool cov = inr && col >= 0 && col < h.n_cols;
-            if (__ballot(cov) == 0) continue;
-            uint32_t len = (uint32_t)(oe - ob);
-            if (P.t_deep && len >= P.t_deep) { deep = true; len = 0; }   // k_acc_seg takes this column
-            if (P.deep_list) {                         // list the long columns for k_acc_seg<1>
-                const uint64_t dm = __ballot(cov && deep);
-                if (dm) {
-                    uint32_t at = 0;
-                    if (lane == 0) at = atomicAdd(P.deep_n, (uint32_t)__popcll(dm));
-                    at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
-                    if (cov && deep)
-                        P.deep_list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32),
-                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u))] = (uint32_t)col;
-                }
-            }
-            if (len && S.fb == INF32) S.fb = (uint32_t)k;
-            const uint64_t a0 = ob & ~(uint64_t)15;
-            const int32_t lead = (int32_t)(ob - a0);
-            const uint32_t nblk = len ? (uint32_t)(((uint64_t)lead + len + 15) >> 4) : 0u;
-            uint32_t mx = nblk;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-            mx = __builtin_amdgcn_readfirstlane(mx);
-            // one buffer descriptor per array over the wave's byte range of this batch (the 64 columns
-            // are consecutive, so their segments are): lanes past their column read zeros, no branch
-            const uint64_t covm = __ballot(nblk != 0);
-            if (covm == 0) { sidx += len; continue; }
-            const int lf = (int)__builtin_ctzll(covm), ll = 63 - (int)__builtin_clzll(covm);
-            const uint64_t a1 = a0 + 16ull * nblk;
-            const uint64_t wb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)a0, lf) |
-                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(a0 >> 32), lf) << 32);
-            const uint64_t we = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)a1, ll) |
-                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(a1 >> 32), ll) << 32);
-            if (we - wb >= (1ull << 30)) {            // > 2^30 entries in 64 columns: not a shallow batch
-                if (lane == 0) atomicOr(P.err, 1u);
-                sidx += len;
-                continue;
-            }
-            const __amdgpu_buffer_rsrc_t rc = column_rsrc(h.code + wb, (uint32_t)(we - wb));
-            const __amdgpu_buffer_rsrc_t rq = column_rsrc(h.qual + wb, (uint32_t)(we - wb));
-            const uint32_t vo = (uint32_t)(a0 - wb);
-            const bool dual = __ballot(s2 >= 0) != 0;
-            for (uint32_t j = 0; j < mx; j += MBLK) {
-                u32x4 cw[MBLK], qw[MBLK];
-#pragma unroll
-                for (int u = 0; u < MBLK; u++) {
-                    const uint32_t o = (j + u < nblk) ? vo + 16u * (j + u) : 0x80000000u;   // OOB -> 0
-                    cw[u] = __builtin_amdgcn_raw_buffer_load_b128(rc, (int)o, 0, 0);
-                    qw[u] = __builtin_amdgcn_raw_buffer_load_b128(rq, (int)o, 0, 0);
-                }
-#pragma unroll
-                for (int u = 0; u < MBLK; u++) {
-                    if (j + u >= mx) break;
-                    const int32_t x0 = (int32_t)(16u * (j + u)) - lead;   // segment index of the block's byte 0
-                    uint32_t vm[4];
-                    valid_masks<4>(x0, 0, (int32_t)len, vm);
-#pragma unroll
-                    for (int d = 0; d < 4; d++) {
-                        const uint32_t c_ = dw<4>(cw[u], d), q_ = dw<4>(qw[u], d);
-                        uint32_t f80, r80, g80 = 0;
-                        swar4(c_, q_, vm[d], mrep, P.kpass, P.kok, f80, r80);
-                        if (dual) {
-                            uint32_t r2;
-                            swar4(c_, q_, vm[d], mrep2, P.kpass, P.kok, g80, r2);
-                            r80 &= ~g80;
-                            gcnt += __popc(g80);
-                            gsq = __builtin_amdgcn_udot4(q_, g80 >> 7, gsq, false);
-                            lut_sums(q_, g80, lut, gsl, gse);
-                            if (gfirst == INF32 && g80)
-                                gfirst = sidx + (uint32_t)(x0 + 4 * d) + ((uint32_t)__builtin_ctz(g80) >> 3);
-                        }
-                        fcnt += __popc(f80);
-                        fsq = __builtin_amdgcn_udot4(q_, f80 >> 7, fsq, false);
-                        if (any_msum) lut_sums(q_, msum ? f80 : 0u, lut, fsl, fse);
-                        if (any_rsl) lut_sl(q_, rsl ? f80 : 0u, l1m8, fsl);
-                        if (ffirst == INF32 && f80)
-                            ffirst = sidx + (uint32_t)(x0 + 4 * d) + ((uint32_t)__builtin_ctz(f80) >> 3);
-                        while (r80) {
-                            const int sh = __builtin_ctz(r80) - 7;
-                            r80 &= r80 - 1;
-                            const uint32_t c = (c_ >> sh) & 0xFFu, q = (q_ >> sh) & 0xFFu;
-                            if ((int)q >= P.min_bq)
-                                ms_rare(S, c, q, sidx + (uint32_t)(x0 + 4 * d + (sh >> 3)), lut, T);
-                        }
-                    }
-                }
-            }
-            sidx += len;
-            if (fsq) { S.sq[Ms] = sat_add31(S.sq[Ms], fsq); fsq = 0; }
-            if (gsq) { S.sq[s2] = sat_add31(S.sq[s2], gsq); gsq = 0; }
-            if (s2 < 0) {                              // promote a frequent non-REF base (SNV) to SWAR
-                uint32_t best = 3;
-#pragma unroll
-                for (int k2 = 0; k2 < 4; k2++)
-                    if (k2 != Ms && S.cnt[k2] > best) { best = S.cnt[k2]; s2 = k2; }
-                if (s2 >= 0) mrep2 = slot_code(s2) * 0x01010101u;
-            }
-        }
-        if (fcnt) {
-            S.depth += fcnt;
-            S.cnt[Ms] += fcnt;
-            S.qf[Ms] = (uint8_t)min((uint32_t)S.qf[Ms], (uint32_t)P.qlo);
-            S.first[Ms] = min(S.first[Ms], ffirst);
-            if (msum) { S.sl[Ms] += fsl; S.se[Ms] += fse; }
-            else if (P.ref_sl) S.sl[Ms] += fsl;        // sum(eps) of the REF allele: never read (no call)
-            else S.skip |= (uint8_t)(1u << Ms);
-        }
-        if (gcnt) {
-            S.depth += gcnt;
-            S.cnt[s2] += gcnt;
-            S.qf[s2] = (uint8_t)min((uint32_t)S.qf[s2], (uint32_t)P.qlo);
-            S.first[s2] = min(S.first[s2], gfirst);
-            S.sl[s2] += gsl;
-            S.se[s2] += gse;
-        }
-        if (P.S > 1) {
-            // partial state of this split -> k_merge_parts (11 x 16 B per lane, coalesced)
-            wave_sync();
-            const uint4 *src = reinterpret_cast<const uint4 *>(ST);
-            uint4 *dst = reinterpret_cast<uint4 *>(P.part + (int64_t)s * P.pstride + (int64_t)g * 64);
-            for (int t = lane; t < 64 * 11; t += 64) dst[t] = src[t];
-            wave_sync();
-            continue;
-        }
-        // one run: assemble the record in the lane's own LDS slot, then store the wave's records
-        // with 16-B pieces (ten lanes per record)
-        uint32_t fl = 0;
-        if constexpr (FUSED) {
-            // most positions cannot produce a call: no record, no listing (the context re-materializes
-            // the records from the history if anything needs them later); deep columns: k_acc_seg writes
-            // their records, listed here
-            const bool want = inr && (deep || (S.fb != INF32 && may_call(S, refc, P)));
-            const uint64_t wm = __ballot(want);
-            if (!wm) continue;
-            uint32_t at = 0;                               // one list slot reservation per wave
-            if (lane == 0) at = atomicAdd(P.n_list, (uint32_t)__popcll(wm));
-            at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
-            if (want)
-                P.list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u))] = p;
-            if (!want) S.fb = INF32;
-        }
-        if (inr && !deep && S.fb != INF32) {
-            const MState c = S;
-            Acc a;
-            if (!P.fresh) a = acc[p];
-            if (P.fresh || a.epoch != P.epoch) { a = Acc{}; a.epoch = P.epoch; }
-            merge_state(a, c, c.first, P.seq0 + c.fb, refc);
-            fl = 1u | ((!P.fresh || record_has_sums(a)) ? 2u : 0u);
-            *reinterpret_cast<Acc *>(&S) = a;
-        }
-        reinterpret_cast<uint32_t *>(&S)[40] = fl;     // byte 160: past the 160-B image
-        wave_sync();
-        for (int t = lane; t < 640; t += 64) {
-            const int r = t / 10, piece = t - 10 * r;
-            const uint32_t f = reinterpret_cast<const uint32_t *>(ST + r)[40];
-            if ((f & 1u) && (piece < 5 || (f & 2u)))
-                reinterpret_cast<uint4 *>(acc + p0 + r)[piece] = reinterpret_cast<const uint4 *>(ST + r)[piece];
-        }
-        wave_sync();
-    }
-#undef SPG_ITEM_HEAD
-}
-
-// ------------------------------------------------------------------------------------------
-// k_acc_one: a single shallow batch into a FRESH memory (the first BAM of a sample: process_bam's
-// columns, live_variant_caller.py:54-103, once).  One lane per position, one wave per 64-column tile,
-// like k_acc_multi, but with a two-tile software pipeline: a tile's CSR bounds are loaded two tiles
-// ahead and its first ONE_BLK 16-B blocks one tile ahead, so a wave keeps the next tile's data in
-// flight while it classifies the current one (k_acc_multi, built for runs of many batches, exposes one
-// memory latency per tile).  Longer columns take extra blocks synchronously; columns with >= t_deep
-// entries are listed for k_acc_seg<1>.  FUSED: records only for positions that may produce a call.
-// ------------------------------------------------------------------------------------------
-#ifndef SPG_ONE_BLK
-#define SPG_ONE_BLK 4
-#endif
-constexpr int ONE_BLK = SPG_ONE_BLK;
-
-template <bool FUSED>
-__global__ __launch_bounds__(64 * MW) __attribute__((amdgpu_waves_per_eu(3, 8))) void k_acc_one(MParams P, const Hist *__restrict__ H,
-                                                       const uint8_t *__restrict__ ref,
-                                                       const Tables *__restrict__ T, Acc *__restrict__ acc) {
-    __shared__ double2 lut[256];                       // {ln(1-eps), eps}, rows 128..255 zero
-    __shared__ double l1m8[256];                       // ln(1-eps), rows 128..255 zero
-    __shared__ MState st[MW][64];
-    for (uint32_t q = threadIdx.x; q < 256u; q += 64u * MW) {
-        lut[q] = q < 128u ? make_double2(T->fast[q][0], T->fast[q][1]) : make_double2(0.0, 0.0);
-        l1m8[q] = q < 128u ? T->fast[q][0] : 0.0;
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    MState &S = st[threadIdx.x >> 6][lane];
-    const Hist h = H[P.h0];
-    const int64_t n_tiles = P.n_groups;
-    const int64_t stride = (int64_t)gridDim.x * MW;
-    int64_t tile = (int64_t)blockIdx.x * MW + (threadIdx.x >> 6);
-
-    // a tile's head: this lane's REF char and column bounds
-    struct Head { uint64_t ob, oe; uint32_t rc; };
-    auto head = [&](int64_t t) -> Head {
-        Head hd{0, 0, (uint32_t)'A'};
-        if (t < n_tiles) {
-            const int64_t p = P.u0 + t * 64 + lane;
-            const int64_t col = p - h.pos_begin;
-            if (p < P.u1 && col >= 0 && col < h.n_cols) {
-                hd.rc = ref[p];
-                hd.ob = __builtin_nontemporal_load(h.off + col);
-                hd.oe = __builtin_nontemporal_load(h.off + col + 1);
-            }
-        }
-        return hd;
-    };
-    // a tile's data: one buffer descriptor per array over the wave's byte range (the 64 columns are
-    // consecutive), ONE_BLK 16-B blocks per lane (lanes past their column read zeros)
-    struct Seg { __amdgpu_buffer_rsrc_t rc, rq; uint32_t vo; };
-    auto seg = [&](const Head &hd, uint32_t &len, int32_t &lead, uint32_t &nblk) -> Seg {
-        len = (uint32_t)(hd.oe - hd.ob);
-        const uint64_t a0 = hd.ob & ~(uint64_t)15;
-        lead = (int32_t)(hd.ob - a0);
-        nblk = len ? (uint32_t)(((uint64_t)lead + len + 15) >> 4) : 0u;
-        const uint64_t covm = __ballot(nblk != 0);
-        Seg sg{column_rsrc(h.code, 0), column_rsrc(h.qual, 0), 0u};
-        if (covm == 0) return sg;
-        const int lf = (int)__builtin_ctzll(covm), ll = 63 - (int)__builtin_clzll(covm);
-        const uint64_t a1 = a0 + 16ull * nblk;
-        const uint64_t wb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)a0, lf) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(a0 >> 32), lf) << 32);
-        const uint64_t we = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)a1, ll) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(a1 >> 32), ll) << 32);
-        if (we - wb >= (1ull << 30)) {                // > 2^30 entries in 64 columns: not a shallow batch
-            if (lane == 0) atomicOr(P.err, 1u);
-            nblk = 0;
-            len = 0;
-            return sg;
-        }
-        sg.rc = column_rsrc(h.code + wb, (uint32_t)(we - wb));
-        sg.rq = column_rsrc(h.qual + wb, (uint32_t)(we - wb));
-        sg.vo = (uint32_t)(a0 - wb);
-        return sg;
-    };
-    auto blk = [&](const Seg &sg, uint32_t nblk, uint32_t u, u32x4 &cw, u32x4 &qw) {
-        const uint32_t o = u < nblk ? sg.vo + 16u * u : 0x80000000u;   // out of range -> zeros
-        cw = __builtin_amdgcn_raw_buffer_load_b128(sg.rc, (int)o, 0, 0);
-        qw = __builtin_amdgcn_raw_buffer_load_b128(sg.rq, (int)o, 0, 0);
-    };
-
-    Head h1 = head(tile), h2 = head(tile + stride);
-    uint32_t len1, nblk1;
-    int32_t lead1;
-    Seg s1 = seg(h1, len1, lead1, nblk1);
-    u32x4 c1[ONE_BLK], q1[ONE_BLK];
-#pragma unroll
-    for (int u = 0; u < ONE_BLK; u++) blk(s1, nblk1, u, c1[u], q1[u]);
-    for (; tile < n_tiles; tile += stride) {
-        // the pipeline: the tile after next's bounds, the next tile's blocks
-        const Head h3 = head(tile + 2 * stride);
-        uint32_t len2, nblk2;
-        int32_t lead2;
-        const Seg s2 = seg(h2, len2, lead2, nblk2);
-        u32x4 c2[ONE_BLK], q2[ONE_BLK];
-#pragma unroll
-        for (int u = 0; u < ONE_BLK; u++) blk(s2, nblk2, u, c2[u], q2[u]);
-
-        // ---- this tile ----
-        const int64_t p = P.u0 + tile * 64 + lane;
-        const bool inr = p < P.u1;
-        ms_init(S);
-        const uint32_t refc = h1.rc;
-        const uint32_t M = code_of_ref((uint8_t)refc), mrep = M * 0x01010101u;
-        const int Ms = slot_of(M);
-        // calls-only: no likelihood sums for a REF-char major (never a call), except its sum(ln(1-eps))
-        // in shallow runs (P.ref_sl)
-        const bool msum = !P.calls_only || nibble_char(M) != (uint8_t)refc;
-        const bool any_msum = __ballot(msum && inr) != 0;
-        const bool rsl = !msum && P.ref_sl;
-        const bool any_rsl = __ballot(rsl && inr) != 0;
-        uint32_t len = len1;
-        bool deep = false;
-        if (P.t_deep && len >= P.t_deep) { deep = true; len = 0; }   // k_acc_seg<1> takes this column
-        const uint64_t dm = __ballot(deep);
-        if (dm) {
-            uint32_t at = 0;
-            if (lane == 0) at = atomicAdd(P.deep_n, (uint32_t)__popcll(dm));
-            at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
-            if (deep)
-                P.deep_list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u))] =
-                    (uint32_t)(p - h.pos_begin);
-        }
-        if (len) S.fb = 0;
-        const uint32_t nblk = len ? nblk1 : 0u;
-        uint32_t mx = nblk;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-        mx = __builtin_amdgcn_readfirstlane(mx);
-        uint32_t fcnt = 0, fsq = 0, ffirst = INF32;
-        double fsl = 0.0, fse = 0.0;
-        auto classify = [&](const u32x4 &cw, const u32x4 &qw, uint32_t u) {
-            const int32_t x0 = (int32_t)(16u * u) - lead1;    // column index of the block's byte 0
-            uint32_t vm[4];
-            valid_masks<4>(x0, 0, (int32_t)len, vm);
-#pragma unroll
-            for (int d = 0; d < 4; d++) {
-                const uint32_t c_ = dw<4>(cw, d), q_ = dw<4>(qw, d);
-                uint32_t f80, r80;
-                swar4(c_, q_, vm[d], mrep, P.kpass, P.kok, f80, r80);
-                fcnt += __popc(f80);
-                fsq = __builtin_amdgcn_udot4(q_, f80 >> 7, fsq, false);
-                if (any_msum) lut_sums(q_, msum ? f80 : 0u, lut, fsl, fse);
-                // FUSED: the REF allele's sum(ln(1-eps)) is needed only where a call is possible, so it
-                // is recomputed for those lanes after the pre-check (no LUT work for every entry)
-                if (!FUSED && any_rsl) lut_sl(q_, rsl ? f80 : 0u, l1m8, fsl);
-                if (ffirst == INF32 && f80) ffirst = (uint32_t)(x0 + 4 * d) + ((uint32_t)__builtin_ctz(f80) >> 3);
-                while (r80) {
-                    const int sh = __builtin_ctz(r80) - 7;
-                    r80 &= r80 - 1;
-                    const uint32_t c = (c_ >> sh) & 0xFFu, q = (q_ >> sh) & 0xFFu;
-                    if ((int)q >= P.min_bq) ms_rare(S, c, q, (uint32_t)(x0 + 4 * d + (sh >> 3)), lut, T);
-                }
-            }
-        };
-#pragma unroll
-        for (int u = 0; u < ONE_BLK; u++)
-            if ((uint32_t)u < mx) classify(c1[u], q1[u], (uint32_t)u);
-        for (uint32_t u = ONE_BLK; u < mx; u++) {      // a longer column: its further blocks, unpipelined
-            u32x4 cw, qw;
-            blk(s1, nblk, u, cw, qw);
-            classify(cw, qw, u);
-        }
-        if (fcnt) {
-            S.depth += fcnt;
-            S.cnt[Ms] += fcnt;
-            S.qf[Ms] = (uint8_t)min((uint32_t)S.qf[Ms], (uint32_t)P.qlo);
-            S.first[Ms] = min(S.first[Ms], ffirst);
-            S.sq[Ms] = sat_add31(S.sq[Ms], fsq);
-            if (msum) { S.sl[Ms] += fsl; S.se[Ms] += fse; }
-            else if (P.ref_sl) S.sl[Ms] += fsl;        // sum(eps) of the REF allele: never read (no call)
-            else S.skip |= (uint8_t)(1u << Ms);
-        }
-        bool write = inr && !deep && S.fb != INF32;
-        if constexpr (FUSED) {
-            // most positions cannot produce a call: no record, no listing (the context re-materializes the
-            // records from the history if anything needs them later); deep columns are listed here
-            const bool want = inr && (deep || (S.fb != INF32 && may_call(S, (uint8_t)refc, P)));
-            const uint64_t wm = __ballot(want);
-            if (wm) {
-                uint32_t at = 0;                       // one list slot reservation per wave
-                if (lane == 0) at = atomicAdd(P.n_list, (uint32_t)__popcll(wm));
-                at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
-                if (want)
-                    P.list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u))] = p;
-            }
-            write = write && want;
-            if (write && rsl && len) {
-                // the REF allele's sum(ln(1-eps)) for this lane's column (its blocks are still in L2):
-                // every block load at once, then the fast entries' LUT sums
-                double rs = 0.0;
-                for (uint32_t u0 = 0; u0 < nblk; u0 += ONE_BLK) {
-                    u32x4 cw[ONE_BLK], qw[ONE_BLK];
-#pragma unroll
-                    for (int v = 0; v < ONE_BLK; v++) blk(s1, nblk, u0 + v, cw[v], qw[v]);
-#pragma unroll
-                    for (int v = 0; v < ONE_BLK; v++) {
-                        const int32_t x0 = (int32_t)(16u * (u0 + v)) - lead1;
-                        uint32_t vm[4];
-                        valid_masks<4>(x0, 0, (int32_t)len, vm);
-#pragma unroll
-                        for (int d = 0; d < 4; d++) {
-                            uint32_t f80, r80;
-                            swar4(dw<4>(cw[v], d), dw<4>(qw[v], d), vm[d], mrep, P.kpass, P.kok, f80, r80);
-                            lut_sl(dw<4>(qw[v], d), f80, l1m8, rs);
-                        }
-                    }
-                }
-                S.sl[Ms] += rs;
-            }
-        }
-        if (write) {                                   // this lane's record (FRESH), 16-B stores
-            Acc a = Acc{};
-            a.epoch = P.epoch;
-            merge_state(a, S, S.first, P.seq0, (uint8_t)refc);
-            const bool sums = record_has_sums(a);
-            uint4 *dst = reinterpret_cast<uint4 *>(acc + p);
-            const uint4 *src = reinterpret_cast<const uint4 *>(&a);
-#pragma unroll
-            for (int t = 0; t < 10; t++)
-                if (t < 5 || sums) dst[t] = src[t];
-        }
-        h1 = h2;
-        h2 = h3;
-        s1 = s2;
-        len1 = len2;
-        lead1 = lead2;
-        nblk1 = nblk2;
-#pragma unroll
-        for (int u = 0; u < ONE_BLK; u++) { c1[u] = c2[u]; q1[u] = q2[u]; }
-    }
-}
-
 // Fold the S partial states of a split run in batch order (first-entry keys (split, stream index)) and
 // merge them into the records.  One thread per position.
 __global__ __launch_bounds__(256) void k_merge_parts(MParams P, const uint8_t *__restrict__ ref,
@@ -1597,7 +1095,7 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
 // launchers (called from spg_api.cpp)
 // ------------------------------------------------------------------------------------------
 // k_acc_seg over one batch: every column of a deep batch (W = 4), or the long columns (>= t_deep) of a
-// shallow one (W = 1; k_acc_multi takes the rest)
+// shallow one (W = 1; k_acc_tile / k_acc_lite take the rest)
 hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_t *code, const uint8_t *qual,
                              const uint8_t *ref, const Tables *T, Acc *acc, hipStream_t st) {
     if (P.n_cols == 0) return hipSuccess;
@@ -1628,38 +1126,9 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
     return hipGetLastError();
 }
 
-hipError_t launch_merge(const MParams &P, const uint8_t *ref, Acc *acc, hipStream_t st);
-
-// k_acc_multi over a run of shallow batches (+ k_merge_parts when the run is split)
-hipError_t launch_multi(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, bool nt,
-                        int64_t max_blocks, bool fused, hipStream_t st) {
-    const int64_t items = (int64_t)P.n_groups * P.S;
-    if (items == 0) return hipSuccess;
-    const int64_t blocks = std::min<int64_t>((items + MW - 1) / MW, max_blocks);
-    // Default-policy loads: a lane's 16-B blocks of one column are strided ~depth bytes from its
-    // neighbours', so one cache line serves several consecutive load instructions of the wave and must
-    // stay in L2 until they have all read it (non-temporal loads re-fetched such lines: 1.7x HBM bytes)
-    (void)nt;
-    // (8 blocks per round measured slower: 5.2 vs 4.5 ms per 2,000 BAMs, its registers cost occupancy)
-    if (fused) hipLaunchKernelGGL((k_acc_multi<false, 4, true>), dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
-    else hipLaunchKernelGGL((k_acc_multi<false, 4, false>), dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
-    if (P.S > 1) return launch_merge(P, ref, acc, st);
-    return hipGetLastError();
-}
-
 hipError_t launch_merge(const MParams &P, const uint8_t *ref, Acc *acc, hipStream_t st) {
     const int64_t mb = (P.u1 - P.u0 + 255) / 256;
     hipLaunchKernelGGL(k_merge_parts, dim3((unsigned)mb), dim3(256), 0, st, P, ref, acc);
-    return hipGetLastError();
-}
-
-// k_acc_one over a single shallow batch into a FRESH memory
-hipError_t launch_one(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc,
-                      int64_t max_blocks, bool fused, hipStream_t st) {
-    if (P.n_groups == 0) return hipSuccess;
-    const int64_t blocks = std::min<int64_t>(((int64_t)P.n_groups + MW - 1) / MW, max_blocks);
-    if (fused) hipLaunchKernelGGL(k_acc_one<true>, dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
-    else hipLaunchKernelGGL(k_acc_one<false>, dim3((unsigned)blocks), dim3(64 * MW), 0, st, P, H, ref, T, acc);
     return hipGetLastError();
 }
 

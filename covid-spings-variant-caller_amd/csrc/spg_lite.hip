@@ -619,9 +619,17 @@ __global__ __launch_bounds__(1024) void k_fold_hist(MParams P, const Hist *__res
         }
         const bool act = li < n_list;
         const int64_t p = act ? P.list[li] : P.u0;
+        // incremental (vc_queue.py:142-144 finalizes after every BAM): a record an earlier counted finalize of this
+        // sample folded holds batches [0, kbase) already; only the batches since are folded and merged into it
+        int32_t kbase = 0;
+        if (act && P.wm) {
+            const uint64_t w = P.wm[p];
+            if ((uint32_t)(w >> 32) == P.wm_gen && acc[p].epoch == P.epoch) kbase = min((int32_t)(uint32_t)w, P.K);
+        }
+        kbase = __builtin_amdgcn_readfirstlane(kbase);     // (one item per wave: tpp >= 64)
         // this item's batch range, then this thread's share of it
-        const int32_t kp = (P.K + (int32_t)nparts - 1) / (int32_t)nparts;
-        const int32_t kb0 = min(P.K, (int32_t)part * kp), kb1 = min(P.K, kb0 + kp);
+        const int32_t kp = (P.K - kbase + (int32_t)nparts - 1) / (int32_t)nparts;
+        const int32_t kb0 = min(P.K, kbase + (int32_t)part * kp), kb1 = min(P.K, kb0 + kp);
         const int32_t per = (kb1 - kb0 + (int32_t)tpp - 1) / (int32_t)tpp;
         const int32_t k0 = min(kb1, kb0 + (int32_t)r * per), k1 = min(kb1, k0 + per);
         uint32_t depth = 0, n_del = 0, n_skip = 0, n_other = 0, fb = INF32, sidx = 0;
@@ -748,6 +756,7 @@ __global__ __launch_bounds__(1024) void k_fold_hist(MParams P, const Hist *__res
                     X.arrived[li] = 0;                 // ready for the next launch
                 }
             }
+            if (write && P.wm && (kbase > 0 || w.fb != INF32)) P.wm[p] = ((uint64_t)P.wm_gen << 32) | (uint32_t)P.K;
             if (write && w.fb != INF32) {
                 MState c;
                 ms_init(c);
@@ -761,7 +770,8 @@ __global__ __launch_bounds__(1024) void k_fold_hist(MParams P, const Hist *__res
                     c.se[j] = w.se[j];
                 }
                 Acc a{};
-                a.epoch = P.epoch;
+                if (kbase > 0) a = acc[p];          // (the slots it holds come first in dict order, :100-101)
+                else a.epoch = P.epoch;
                 merge_state(a, c, w.key, P.seq0 + c.fb, ref[p]);
                 const uint4 *src = reinterpret_cast<const uint4 *>(&a);
                 uint4 *dst = reinterpret_cast<uint4 *>(acc + p);

@@ -211,6 +211,16 @@ class PileupEngine:
             N.check(self._L.spg_history_resident(self._h, C.byref(a), C.byref(b), C.byref(d)), "spg_history_resident")
         return a.value, b.value, d.value
 
+    PATHS = ("record_runs", "materializations", "full_finalizes", "sparse_finalizes", "counted_finalizes",
+             "fused_deep_finalizes", "fused_shallow_finalizes", "batches_counted")
+
+    def path_counters(self) -> Dict[str, int]:
+        """Which engine paths ran since creation (spg_path_counters)."""
+        a = (C.c_int64 * 8)()
+        with self._lock:
+            N.check(self._L.spg_path_counters(self._h, a, 8), "spg_path_counters")
+        return dict(zip(self.PATHS, list(a)))
+
     def input_ticket(self) -> int:
         """Ticket of the latest host-input batch copy enqueued (spg_input_ticket)."""
         t = C.c_uint64()
