@@ -179,6 +179,7 @@ struct spg_ctx {
     int64_t n_deep_hist = 0;            // deep / multi-sample batches since reset (counted mode needs none)
     uint32_t *cdep = nullptr, *cmcf = nullptr;
     uint64_t *fwm = nullptr;            // k_fold_hist's per-position fold watermarks ((generation << 32) | batches)
+    RSlot *rcache = nullptr;            // replay cache (allocated once a history is long enough for replays to matter)
     uint32_t count_gen = 0;             // generation of the current counted run (bumped whenever counted mode starts)
     void *fold_part = nullptr;          // k_fold_hist's multi-workgroup partials [FOLD_CAP][FOLD_BPP]
     uint32_t *fold_arrived = nullptr;   // ... and arrival counts (zero between launches)
@@ -351,7 +352,7 @@ int spg_destroy(spg_ctx *c) {
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
                     c->d_fused, c->deep_list, c->deep_n, c->cdep, c->cmcf, c->fwm, c->fold_part, c->fold_arrived, c->rs,
-                    c->ferr};
+                    c->ferr, c->rcache};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
@@ -581,10 +582,33 @@ static void fill_swar(const spg_ctx *c, int32_t &min_bq, int32_t &qlo, uint32_t 
 // k_acc_seg over one batch (every column of a deep batch; the long columns of a shallow one).  F/O:
 // fused with the calls-only finalize (FRESH deep batch, the sample's only one).
 static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F = nullptr, const Out *O = nullptr,
-                      bool listed = false) {
+                      bool listed = false, bool *list_mode = nullptr) {
+    if (list_mode) *list_mode = false;
+    const HistBatch &hb0 = c->hist[(size_t)idx];
+    static const int64_t target_waves = env_i64("SPG_TARGET_WAVES", 16384);
+    // Each wave owns G consecutive columns.  A new wave costs a workgroup dispatch (median 1.4 us from
+    // the previous wave's end in its slot) and its setup (LUT + CSR offsets, then its first chunk: two
+    // memory round trips), so a deep wave gets ~22-30 chunks where that still leaves one grid generation
+    // of <= 4,096 waves (16 per CU) to fill the chip; otherwise G targets 16,384 waves.  10,000x: G = 3
+    // (interleaved A/B on one box: 109.5 us vs 114.7 us for G = 2, 113.5 us for G = 5).
+    int64_t g = std::max<int64_t>(1, (hb0.n_cols + target_waves - 1) / target_waves);
+    if (deep_batch && !getenv("SPG_TARGET_WAVES")) {
+        // ~22-30 chunks per wave: G = 3 at both 10,000x (10 chunks a column) and the 8000-capped
+        // 7,960x (8 chunks; G = 4 there measured 103.5 vs 95.9 us); 1,000x: G = 16 (list mode below)
+        const double avg0 = (double)hb0.n_entries / (double)std::max<int64_t>(1, hb0.n_cols);
+        const int64_t g_chunks = (int64_t)std::ceil(22528.0 / std::max(avg0, 1.0));
+        const int64_t g_fill = std::max<int64_t>(1, (hb0.n_cols + 4095) / 4096);           // one generation
+        g = std::max<int64_t>(g, std::min(g_chunks, g_fill));
+    }
+    // fused (records kept in the wave's finishing ring for the finalize) only when a wave's columns fit the ring;
+    // a wider group finishes its ring NB columns at a time, lists the positions that may call, and the caller
+    // runs the sparse k_finalize over them (list mode: mid-depth batches such as 1,000x, G = 16)
+    if (F && g > NB_RING && deep_batch && !listed) {
+        if (list_mode) *list_mode = true;
+        F = nullptr;
+        O = nullptr;
+    }
     if (F) {
-        // finalize parameters in device memory (the kernel reads them after its loop); epoch and Counters
-        // slot travel in KParams, everything else changes only when the result buffers grow
         // finalize parameters in device memory (the kernel reads them after its loop), one copy per
         // Counters slot; they change only when the result buffers grow
         FusedArgs fa[2];
@@ -604,22 +628,6 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     }
     const HistBatch &hb = c->hist[(size_t)idx];
     const int64_t n_cols = hb.n_cols;
-    const double avg = (double)hb.n_entries / (double)n_cols;
-    // Each wave owns G consecutive columns.  A new wave costs a workgroup dispatch (median 1.4 us from
-    // the previous wave's end in its slot) and its setup (LUT + CSR offsets, then its first chunk: two
-    // memory round trips), so a deep wave gets ~22-30 chunks where that still leaves one grid generation
-    // of <= 4,096 waves (16 per CU) to fill the chip (1,000x: G = 8, 3,738 waves: 40 -> 36 us);
-    // otherwise G targets 16,384 waves.  10,000x: G = 3 (interleaved A/B on one box: 109.5 us vs
-    // 114.7 us for G = 2, 113.5 us for G = 5).
-    static const int64_t target_waves = env_i64("SPG_TARGET_WAVES", 16384);
-    int64_t g = std::max<int64_t>(1, (n_cols + target_waves - 1) / target_waves);
-    if (deep_batch && !getenv("SPG_TARGET_WAVES")) {
-        // ~22-30 chunks per wave: G = 3 at both 10,000x (10 chunks a column) and the 8000-capped
-        // 7,960x (8 chunks; G = 4 there measured 103.5 vs 95.9 us)
-        const int64_t g_chunks = (int64_t)std::ceil(22528.0 / std::max(avg, 1.0));
-        const int64_t g_fill = std::max<int64_t>(1, (n_cols + 4095) / 4096);           // one generation
-        g = std::max<int64_t>(g, std::min(g_chunks, g_fill));
-    }
     // fused: a wave's columns fit its finishing ring (its records stay in LDS for the finalize)
     const uint32_t G = (uint32_t)std::min<int64_t>(F ? NB_RING : (deep_batch ? SPG_GMAX_DEEP : SPG_GMAX), g);
     KParams P{};
@@ -650,6 +658,14 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
     P.n_entries = hb.n_entries;
     P.dbg = trace_on() ? trace_dbg() : nullptr;
+    if (list_mode && *list_mode) {
+        HIPCHK(hipMemsetAsync(c->nlist, 0, sizeof(uint32_t), c->stream));
+        P.list = c->band;
+        P.n_list = c->nlist;
+        P.min_td = c->p.min_total_depth;
+        P.min_ad = c->p.min_allele_depth;
+        P.ratio_lo = c->p.min_evidence_ratio * (1.0 - 1e-9);
+    }
     if (listed) {                 // the long columns the run kernel listed, one per wave
         P.G = 1;
         P.G2 = 1;
@@ -1472,6 +1488,19 @@ static int finalize_counted(spg_ctx *c) {
 
 static int finalize_impl(spg_ctx *c, bool table);
 
+// The replay cache for a finalize: a history of >= 16 batches (a live memory) keeps each replayed position's exact
+// fold state, so its next replay folds only the batches added since (RSlot, spg_device.h)
+static int replay_cache(spg_ctx *c, RCache &rc) {
+    rc = RCache{nullptr, 0, 0};
+    if ((int64_t)c->hist.size() < 16) return 0;
+    if (!c->rcache) {
+        HIPCHK(hipMalloc(&c->rcache, sizeof(RSlot) * RCACHE_SLOTS));
+        HIPCHK(hipMemsetAsync(c->rcache, 0, sizeof(RSlot) * RCACHE_SLOTS, c->stream));
+    }
+    rc = RCache{c->rcache, (uint32_t)RCACHE_SLOTS - 1, 0};
+    return 0;
+}
+
 int spg_finalize(spg_ctx *c) {
     if (!c) return fail("spg_finalize: null ctx");
     // calls-only contexts write the per-position table lazily (spg_get_table)
@@ -1520,18 +1549,30 @@ static int finalize_impl(spg_ctx *c, bool table) {
     FParams F = make_fparams(c);
     F.table = table ? 1u : 0u;
     if (fused_deep) {
-        // the accumulate interval holds the fused kernel; the finalize interval is empty
+        // the accumulate interval holds the fused kernel; the finalize interval is empty (list mode: the sparse
+        // k_finalize over the positions the accumulate listed)
         const Out O = make_out(c);
         if (int rc = wait_copies(c)) return rc;
         if (int rc = acc_begin(c)) return rc;
-        if (int rc = launch_seg(c, 0, true, &F, &O)) return rc;
+        bool list_mode = false;
+        if (int rc = launch_seg(c, 0, true, &F, &O, false, &list_mode)) return rc;
         if (int rc = acc_end(c)) return rc;
         if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
+        if (list_mode) {
+            F.list = c->band;
+            F.n_list = c->nlist;
+            c->path[3]++;
+            if (int rc = upload_ridx(c, F.ridx)) return rc;
+            if (int rc = replay_cache(c, F.rc)) return rc;
+            HIPCHK(launch_finalize(F, c->acc, c->tables, make_out(c), c->d_hist, c->stream));
+            if (trace_sync(c, "finalize (sparse, listed by k_acc_seg)")) return -1;
+        }
     } else {
         if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
         if (fused || counted) { F.list = c->band; F.n_list = c->nlist; }
         c->path[(fused || counted) ? 3 : 2]++;
         if (int rc = upload_ridx(c, F.ridx)) return rc;
+        if (int rc = replay_cache(c, F.rc)) return rc;
         HIPCHK(launch_finalize(F, c->acc, c->tables, make_out(c), c->d_hist, c->stream));
         if (trace_sync(c, "finalize")) return -1;
     }

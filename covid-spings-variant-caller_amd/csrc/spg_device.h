@@ -100,6 +100,12 @@ struct KParams {
     const uint32_t *deep_list;   // W = 1: the long columns the run kernel listed (batch-relative) ...
     const uint32_t *deep_n;      // ... and their count (null: one group of G columns per wave)
     uint4 *wtime;          // SPG_WAVE_TIMES: per wave {start, first column, lifetime} (s_memrealtime, 100 MHz), hw id
+    // calls-only listing (a FRESH deep batch, the sample's only one, whose waves own more columns than the finishing
+    // ring holds — mid-depth columns, e.g. 1,000x): each finished ring's records pass the division-free pre-check
+    // of prepare_variants' filters (:131, :151-157) and the positions that may call are listed here for the
+    // sparse k_finalize (null: no listing)
+    int64_t *list;
+    uint32_t *n_list;
 };
 
 // Per-position state of a run of batches folded by one lane group (k_acc_tile), and
@@ -162,6 +168,28 @@ struct RIndex {
     int64_t n_buckets;       // 0: no index, scan every batch
 };
 
+// Replay cache: the exact sequential fold state of a replayed position after history batches [0, upto), so the
+// next finalize's replay of it (the live loop finalizes after every BAM, vc_queue.py:142-144) folds only the
+// batches since.  Open addressing, one slot per position per epoch, claimed by atomicCAS on `key`
+// ((epoch << 32) | (pos + 1)); slots of older epochs are reclaimed.  H folds are kept only for the codes whose
+// N_h = prod over the other alleles' P was non-zero at the last replay ("alive"): P products only shrink as
+// entries arrive, so a code whose N_h reached exactly 0 never needs its H again (H * 0 == 0).
+struct RSlot {
+    uint64_t key;
+    uint32_t upto, alive;   // history batches folded (0: no state yet); codes whose H fold is tracked
+    uint32_t depth, pad;
+    uint64_t ord;           // raw entries of the position folded so far (stream index of the next one)
+    uint32_t cnt[16];
+    uint64_t first[16];
+    double P[16], H[16], se[16];
+};
+constexpr int RCACHE_SLOTS = 8192;
+constexpr int RCACHE_PROBE = 16;
+struct RCache {
+    RSlot *slot;            // null: no cache (every replay folds the whole history)
+    uint32_t mask, pad;
+};
+
 struct Counters {           // per finalize; two slots, the kernel zeroes the other one
     uint32_t n_cand, n_band, n_detail, err;   // n_band: positions queued for the exact replay
 };
@@ -178,6 +206,7 @@ struct FParams {
     RIndex ridx;
     const int64_t *list;   // sparse finalize: only these positions (*n_list of them); null = every position
     const uint32_t *n_list;
+    RCache rc;             // replay cache (null slot: none)
 };
 
 struct Out {                // SoA result table

@@ -97,17 +97,24 @@ struct ReplayWs {
     uint32_t needH, n;
 };
 
+// Walk the position's entries in history batches [from, n_hist) in accumulate order; `ord` = raw entries of the
+// position in the batches before (advanced past the ones walked).
 template <typename Fn>
 __device__ __forceinline__ void replay_walk(const FParams &F, const Hist *__restrict__ H, int64_t pos, int lane,
-                                            Fn &&fn) {
+                                            uint32_t from, uint64_t &ord, Fn &&fn) {
     const bool indexed = F.ridx.n_buckets > 0;
-    uint32_t i0 = 0, i1 = (uint32_t)F.n_hist;
+    uint32_t i0 = from, i1 = (uint32_t)F.n_hist;
     if (indexed) {
         const int64_t bk = pos >> RIDX_SHIFT;
-        i0 = F.ridx.off[bk];
-        i1 = F.ridx.off[bk + 1];
+        uint32_t lo = F.ridx.off[bk], hi = F.ridx.off[bk + 1];
+        i1 = hi;
+        while (lo < hi) {                              // a bucket's items ascend: the first batch >= from
+            const uint32_t m = (lo + hi) >> 1;
+            if ((uint32_t)F.ridx.items[m] < from) lo = m + 1;
+            else hi = m;
+        }
+        i0 = lo;
     }
-    uint64_t ord = 0;                                  // raw entries of this position in earlier batches
     for (uint32_t i = i0; i < i1; i++) {
         const int32_t b = indexed ? F.ridx.items[i] : (int32_t)i;
         const Hist h = H[b];
@@ -124,6 +131,35 @@ __device__ __forceinline__ void replay_walk(const FParams &F, const Hist *__rest
     }
 }
 
+// The position's replay-cache slot (lane 0; -1: none free).  `upto` = batches its stored state covers (0: none).
+__device__ __forceinline__ int32_t rcache_claim(const RCache &R, int64_t pos, uint32_t epoch, uint32_t &upto) {
+    const uint64_t key = ((uint64_t)epoch << 32) | (uint64_t)(uint32_t)(pos + 1);
+    const uint32_t h = (uint32_t)(((uint64_t)pos * 0x9E3779B97F4A7C15ull) >> 40) & R.mask;
+    for (int i = 0; i < RCACHE_PROBE; i++) {
+        const uint32_t si = (h + (uint32_t)i) & R.mask;
+        unsigned long long *kp = reinterpret_cast<unsigned long long *>(&R.slot[si].key);
+        const unsigned long long k = __hip_atomic_load(kp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == key) { upto = R.slot[si].upto; return (int32_t)si; }
+        if (k == 0 || (uint32_t)(k >> 32) != epoch) {            // empty, or a slot of an older sample
+            const unsigned long long old = atomicCAS(kp, k, (unsigned long long)key);
+            if (old == k) { R.slot[si].upto = 0; upto = 0; return (int32_t)si; }
+            if (old == key) { upto = R.slot[si].upto; return (int32_t)si; }
+        }
+    }
+    return -1;
+}
+
+// Exact sequential recomputation of one position over the batch history (rare: subnormal band, IUPAC
+// alleles, calls-only terms that were not accumulated).  np.prod is a strict left fold (utils.py:17,19)
+// and N a dict-order fold (:18-22): sequential per allele, but the 16 allele codes' folds are
+// independent.  The wave walks the position's entries 64 at a time (coalesced byte loads, one entry per
+// lane) over the batches the replay index lists for the position; lane c owns code c's fold and takes
+// the chunk's code-c factors in order through readlane, so no fold step waits on a memory load.
+// Cold (no cached state): pass 1 folds counts, first appearance (dict order), sum(eps) and the P folds
+// (stopped at 0: P only shrinks); pass 2 the H folds, only for alleles whose GL is not already exactly 0
+// through N == 0 (H is finite, so H * 0 == 0), each stopped at 0.  Warm (F.rc holds the position's state after
+// batches [0, upto)): one pass over batches [upto, n_hist) continues every fold from that state — P for every
+// code, H for the codes still alive (N != 0 last time) and for codes first seen since; the state is stored back.
 // rec: the position's record (HBM, or the fused accumulate's LDS image); eps(q): from_phred_scale(q)
 template <typename EpsFn>
 __device__ __forceinline__ void replay_wave(const FParams &F, const Hist *__restrict__ H, const Acc *rec,
@@ -131,56 +167,94 @@ __device__ __forceinline__ void replay_wave(const FParams &F, const Hist *__rest
     const int lane = threadIdx.x & 63;
     const Acc a = *rec;
     uint32_t cnt = 0, depth = 0;
-    uint64_t first = ~0ull;
+    uint64_t first = ~0ull, ord = 0;
     double P = 1.0, Hh = 1.0, se = 0.0;
-    replay_walk(F, H, pos, lane, [&](uint32_t c, uint32_t q, bool valid, uint64_t base) {
-        const bool pass = valid && (int)q >= F.min_bq;
-        depth += (uint32_t)__popcll(__ballot(pass));
-        const bool isc = pass && c < 16u;
-        const double e = isc ? eps_s(q) : 0.0;
-        uint64_t todo = __ballot(isc);
-        while (todo) {
-            const int j0 = (int)__builtin_ctzll(todo);
-            const uint32_t cc = __builtin_amdgcn_readlane(c, j0);
-            const bool mine = isc && c == cc;
-            const uint64_t bm = __ballot(mine);
-            todo &= ~bm;
-            const double es = dsum_f64(mine ? e : 0.0);
-            double pc = rl_f64(P, (int)cc);
-            for (uint64_t m = bm; m && pc != 0.0; m &= m - 1) pc = pc * rl_f64(e, (int)__builtin_ctzll(m));
-            if (lane == (int)cc) {
-                if (cnt == 0) first = base + (uint64_t)j0;
-                cnt += (uint32_t)__popcll(bm);
-                se += es;
-                P = pc;
+    RSlot *rs = nullptr;
+    uint32_t from = 0, track = 0;
+    if (F.rc.slot) {
+        int32_t si = -1;
+        uint32_t up = 0;
+        if (lane == 0) si = rcache_claim(F.rc, pos, F.epoch, up);
+        si = __builtin_amdgcn_readfirstlane(si);
+        up = __builtin_amdgcn_readfirstlane(up);
+        if (si >= 0) {
+            rs = F.rc.slot + si;
+            if (up > 0 && up <= (uint32_t)F.n_hist) {
+                from = up;
+                depth = rs->depth;
+                ord = rs->ord;
+                const uint32_t alive = rs->alive;
+                if (lane < 16) { cnt = rs->cnt[lane]; first = rs->first[lane]; P = rs->P[lane]; se = rs->se[lane]; }
+                // H folds continue for the alive codes and start for codes not seen yet
+                const bool tr = lane < 16 && (cnt == 0 || ((alive >> lane) & 1u));
+                if (tr && cnt) Hh = rs->H[lane];
+                track = (uint32_t)__ballot(tr) & 0xFFFFu;
             }
         }
-    });
-    if (lane < 16) { w->cnt[lane] = cnt; w->first[lane] = first; w->P[lane] = P; w->se[lane] = se; }
-    wave_sync();
-    if (lane == 0) {
-        int n = 0;                                     // dict order: codes by first appearance
-        for (int c = 0; c < 16; c++) {
-            if (!w->cnt[c]) continue;
-            int at = n++;
-            while (at > 0 && w->first[w->ord[at - 1]] > w->first[c]) { w->ord[at] = w->ord[at - 1]; at--; }
-            w->ord[at] = (uint32_t)c;
-        }
-        uint32_t need = 0;
-        for (int h = 0; h < n; h++) {                  // N_h = ((1.0 * P_a1) * P_a2) ... over a != h
-            double non = 1.0;
-            for (int j = 0; j < n; j++)
-                if (j != h) non = non * w->P[w->ord[j]];
-            w->non[h] = non;
-            if (non != 0.0) need |= 1u << w->ord[h];
-        }
-        w->n = (uint32_t)n;
-        w->needH = need;
     }
-    wave_sync();
+    for (int attempt = 0; attempt < 2; attempt++) {
+        const bool warm = from > 0;
+        replay_walk(F, H, pos, lane, from, ord, [&](uint32_t c, uint32_t q, bool valid, uint64_t base) {
+            const bool pass = valid && (int)q >= F.min_bq;
+            depth += (uint32_t)__popcll(__ballot(pass));
+            const bool isc = pass && c < 16u;
+            const double e = isc ? eps_s(q) : 0.0;
+            const double om = (warm && isc) ? 1.0 - e : 0.0;
+            uint64_t todo = __ballot(isc);
+            while (todo) {
+                const int j0 = (int)__builtin_ctzll(todo);
+                const uint32_t cc = __builtin_amdgcn_readlane(c, j0);
+                const bool mine = isc && c == cc;
+                const uint64_t bm = __ballot(mine);
+                todo &= ~bm;
+                const double es = dsum_f64(mine ? e : 0.0);
+                double pc = rl_f64(P, (int)cc);
+                for (uint64_t m = bm; m && pc != 0.0; m &= m - 1) pc = pc * rl_f64(e, (int)__builtin_ctzll(m));
+                double hc = 1.0;
+                if (warm && ((track >> cc) & 1u)) {
+                    hc = rl_f64(Hh, (int)cc);
+                    for (uint64_t m = bm; m && hc != 0.0; m &= m - 1) hc = hc * rl_f64(om, (int)__builtin_ctzll(m));
+                }
+                if (lane == (int)cc) {
+                    if (cnt == 0) first = base + (uint64_t)j0;
+                    cnt += (uint32_t)__popcll(bm);
+                    se += es;
+                    P = pc;
+                    if (warm && ((track >> cc) & 1u)) Hh = hc;
+                }
+            }
+        });
+        if (lane < 16) { w->cnt[lane] = cnt; w->first[lane] = first; w->P[lane] = P; w->se[lane] = se; }
+        wave_sync();
+        if (lane == 0) {
+            int n = 0;                                     // dict order: codes by first appearance
+            for (int c = 0; c < 16; c++) {
+                if (!w->cnt[c]) continue;
+                int at = n++;
+                while (at > 0 && w->first[w->ord[at - 1]] > w->first[c]) { w->ord[at] = w->ord[at - 1]; at--; }
+                w->ord[at] = (uint32_t)c;
+            }
+            uint32_t need = 0;
+            for (int h = 0; h < n; h++) {                  // N_h = ((1.0 * P_a1) * P_a2) ... over a != h
+                double non = 1.0;
+                for (int j = 0; j < n; j++)
+                    if (j != h) non = non * w->P[w->ord[j]];
+                w->non[h] = non;
+                if (non != 0.0) need |= 1u << w->ord[h];
+            }
+            w->n = (uint32_t)n;
+            w->needH = need;
+        }
+        wave_sync();
+        // a code needing H whose fold was not tracked cannot occur (N only shrinks); if it did, fold from scratch
+        if (!warm || (w->needH & ~track) == 0) break;
+        from = 0; ord = 0; depth = 0; cnt = 0; first = ~0ull; P = 1.0; Hh = 1.0; se = 0.0; track = 0;
+        wave_sync();
+    }
     const uint32_t needH = w->needH;
-    if (needH) {
-        replay_walk(F, H, pos, lane, [&](uint32_t c, uint32_t q, bool valid, uint64_t) {
+    if (from == 0 && needH) {
+        uint64_t ord2 = 0;
+        replay_walk(F, H, pos, lane, 0u, ord2, [&](uint32_t c, uint32_t q, bool valid, uint64_t) {
             const bool isc = valid && (int)q >= F.min_bq && c < 16u && ((needH >> c) & 1u);
             const double om = isc ? 1.0 - eps_s(q) : 0.0;
             uint64_t todo = __ballot(isc);
@@ -195,6 +269,12 @@ __device__ __forceinline__ void replay_wave(const FParams &F, const Hist *__rest
         });
     }
     if (lane < 16) w->Hh[lane] = Hh;
+    if (rs) {                                          // the state after every batch, for the next replay
+        if (lane < 16) {
+            rs->cnt[lane] = cnt; rs->first[lane] = first; rs->P[lane] = P; rs->se[lane] = se; rs->H[lane] = Hh;
+        }
+        if (lane == 0) { rs->depth = depth; rs->ord = ord; rs->alive = needH; rs->upto = (uint32_t)F.n_hist; }
+    }
     wave_sync();
     if (lane == 0) {
         const int n = (int)w->n;
@@ -392,6 +472,23 @@ struct ColSum {              // one finished column's fast-path statistics (writ
     double fl, fe, fl2, fe2;
 };
 static_assert(sizeof(ColSum) == 80, "ColSum");
+
+// prepare_variants' filters (:131, :151-157) on a finished record's LDS image, division-free and conservative
+// (P.ratio_lo = ratio (1 - 1e-9)): false = the position cannot produce a call and needs no replay
+__device__ __forceinline__ bool may_call_img(const KParams &P, const Acc *r) {
+    const uint32_t depth = r->depth, misc = r->misc;
+    if (misc & MISC_EXOTIC) return true;               // exotic allele: exact replay
+    if ((int64_t)depth < (int64_t)P.min_td) return false;
+    const double dlo = (double)depth * P.ratio_lo;
+    const uint8_t refc = (uint8_t)(misc & 0xFFu);
+    bool maybe = false;
+#pragma unroll
+    for (int k = 0; k < NSLOT; k++) {
+        const uint32_t n = r->cnt[k];
+        maybe |= n != 0 && refc != nibble_char(slot_code(k)) && (int64_t)n >= P.min_ad && (double)n >= dlo;
+    }
+    return maybe;
+}
 
 // Lane-per-column record assembly (lane j of the finisher; R / S in LDS, out = the LDS image).
 template <bool FRESH>
@@ -650,6 +747,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
                 continue;
             }
             reinterpret_cast<uint4 *>(base + CS[r].cj)[piece] = reinterpret_cast<const uint4 *>(img + r)[piece];
+        }
+        if (!FUSE && P.list) {                  // calls-only listing: the ring's records that may call
+            const bool maybe = (uint32_t)lane < nb && may_call_img(P, img + lane);
+            const uint64_t bm = __ballot(maybe);
+            if (bm) {
+                uint32_t at = 0;
+                if (lane == 0) at = atomicAdd(P.n_list, (uint32_t)__popcll(bm));
+                at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
+                if (maybe)
+                    P.list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u))] =
+                        P.pos_begin + g0 + (int64_t)CS[lane].cj;
+            }
         }
         nb = 0;
         wave_sync();
@@ -963,22 +1072,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         // Division-free pre-check from the images (LDS) and the kernel's scalar parameters: most positions
         // cannot produce a call.  Only a wave holding a possible call reads the finalize parameters (vector
         // loads from memory, whose wait would also wait for the record stores just issued).
-        bool maybe = false;
-        if ((uint32_t)lane < nfin) {
-            const Acc *r = img + lane;
-            const uint32_t depth = r->depth, misc = r->misc;
-            if (misc & MISC_EXOTIC) {
-                maybe = true;                              // exotic allele: exact replay
-            } else if ((int64_t)depth >= (int64_t)P.min_td) {
-                const double dlo = (double)depth * P.ratio_lo;
-                const uint8_t refc = (uint8_t)(misc & 0xFFu);
-#pragma unroll
-                for (int k = 0; k < NSLOT; k++) {
-                    const uint32_t n = r->cnt[k];
-                    maybe |= n != 0 && refc != nibble_char(slot_code(k)) && (int64_t)n >= P.min_ad && (double)n >= dlo;
-                }
-            }
-        }
+        const bool maybe = (uint32_t)lane < nfin && may_call_img(P, img + lane);
         if (__ballot(maybe))
             fused_tail(P.fused->F, P.fused->O, T, P.pos_begin + g0, maybe ? nfin : 0u, CS, img,
                        reinterpret_cast<ReplayWs *>(Q), &hdl, lut);

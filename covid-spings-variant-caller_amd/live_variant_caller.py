@@ -390,6 +390,11 @@ checkpoint writes every batch once): two callers that load one file never append
         if man is not None:
             if man["names"] != self.fastaFile.references:
                 raise ValueError("checkpoint was made with a different reference FASTA")
+            # shards keep only the entries that passed the writer's minBaseQuality (plus first-visit markers):
+            # another threshold would silently change depths and calls
+            if man["min_base_quality"] != self.minBaseQuality:
+                raise ValueError(f"checkpoint was made with minBaseQuality {man['min_base_quality']}, "
+                                 f"this caller uses {self.minBaseQuality}")
             d = os.path.dirname(os.path.abspath(filename))
             contig, batches = man["contig"], []
             for s, a, k in man["shards"]:

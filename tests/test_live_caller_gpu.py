@@ -131,6 +131,23 @@ def test_checkpoint_roundtrip(planted):
     assert all(mem[p] == o.memory[p] for p in o.memory)
 
 
+def test_checkpoint_rejects_other_min_base_quality(planted):
+    """a checkpoint's shards hold only the entries that passed the writer's minBaseQuality (plus
+    first-visit markers); a caller with another threshold must refuse it rather than silently change calls."""
+    from covid_spings_variant_caller_amd.live_variant_caller import LiveVariantCaller
+    d, ref, fasta, files = planted
+    a = _caller(fasta)
+    a.process_bam(files[0])
+    ck = str(d / "ck_bq.npz")
+    a.create_checkpoint(ck)
+    b = LiveVariantCaller(fasta, 20, 20, 10, 5, 0.10, 1)
+    with pytest.raises(ValueError, match="minBaseQuality"):
+        b.load_checkpoint(ck)
+    c = _caller(fasta)
+    c.load_checkpoint(ck)                         # same threshold: loads
+    compare_variants(c.prepare_variants(), a.prepare_variants(), RTOL)
+
+
 def test_checkpoint_incremental_per_bam(planted):
     """vc_queue.py:142-144's loop — process_bam then create_checkpoint(same file) per BAM: each checkpoint
     writes only the batches accumulated since the previous one (earlier shards untouched), a reset or a load

@@ -55,7 +55,7 @@ def test_finalize_after_every_bam_300_vs_oracle():
 
 
 def test_every_bam_finalize_with_planted_calls_appearing_late():
-    """Calls whose positions are listed only late in the loop (a planted allele that reaches AD >= 5 after 150 BAMs,
+    """Calls whose positions are listed only late in the loop (a planted allele from BAM 140 on passes AD/DP >= 0.10 at ~BAM 160,
     at positions listed earlier and at positions never listed before): the incremental fold must merge into the
     records of earlier folds and fold never-listed positions from batch 0 — dict order, first visits, AD/DP
     against the oracle at every step."""
@@ -65,8 +65,8 @@ def test_every_bam_finalize_with_planted_calls_appearing_late():
     for i in range(140, 200):
         for p in late:
             code = 8 if ref[p] != "T" else 1
-            batches[i] = _plant(batches[i], p, code, 37)
-            batches[i] = _plant(batches[i], p, code, 36)
+            for k in range(8):
+                batches[i] = _plant(batches[i], p, code, 36 + (k & 1))
     eng = _engine(ref)
     orc = COracle(ref, 30, 10, 5, 0.10)
     for i, b in enumerate(batches):
@@ -167,3 +167,61 @@ def test_records_input_validation():
     with pytest.raises(RuntimeError, match="past the records buffer"):
         N.check(eng._L.spg_accumulate_records(eng._h, C.byref(r), 0), "spg_accumulate_records")
     eng.close()
+
+
+def _deep_calls_only_vs_oracle(ref, b):
+    eng = _engine(ref)
+    orc = COracle(ref, 30, 10, 5, 0.10)
+    eng.accumulate(*b)
+    orc.accumulate(*b)
+    eng.finalize()
+    orc.finalize()
+    compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
+    return eng, orc
+
+
+def test_mid_depth_single_batch_list_mode_vs_oracle():
+    """A calls-only sample whose only batch is mid-depth (1,000x over the whole SARS-CoV-2 genome: G = 16 columns
+    per wave, wider than the fused kernel's finishing ring): k_acc_seg lists the positions that may call at each
+    ring finish and the sparse k_finalize decides them (spg_api.cpp launch_seg list mode) — calls vs the oracle,
+    with planted SNVs every 97th position, an IUPAC allele and a subnormal-band position."""
+    from covid_spings_variant_caller_amd import synth
+    L = 29903
+    ref = synth.reference(L, seed=38000)
+    b = synth.pileup(L, 1000, seed=38001, ref=ref, snv_every=97)
+    b = _plant(b, 5000, 5, 35)                               # 'R': exotic, exact replay
+    for k in range(98):                                      # 98 x Q31 of a non-REF base at a 0-AF position
+        b = _plant(b, 7001, 2 if ref[7001] != "C" else 4, 31)
+    eng, orc = _deep_calls_only_vs_oracle(ref, b)
+    pc = eng.path_counters()
+    assert pc["fused_deep_finalizes"] == 1 and pc["sparse_finalizes"] == 1 and pc["full_finalizes"] == 0, pc
+    assert len(orc.variants()) > 200
+    assert eng.memory_summary() == orc.memory_summary()
+    eng.close()
+
+
+def test_stacked_samples_one_context_equals_separate_engines():
+    """The bench's stacked layout (bench.py build_shard): S samples of one coordinate range side by side in one
+    context (sample s = positions [s C, (s+1) C)) give, per sample, exactly the calls of a context of its own."""
+    from covid_spings_variant_caller_amd import synth
+    L, S = 3000, 8
+    ref = synth.reference(L, seed=39000)
+    samples = [synth.pileup(L, 1000, seed=39001 + s, ref=ref, snv_every=31) for s in range(S)]
+    offs, cs, qs, base = [np.zeros(1, np.uint64)], [], [], 0
+    for _, o, c, q in samples:
+        offs.append(o[1:] + np.uint64(base))
+        base += int(o[-1])
+        cs.append(c)
+        qs.append(q)
+    big = _engine(ref * S)
+    big.accumulate(0, np.concatenate(offs), np.concatenate(cs), np.concatenate(qs))
+    big.finalize()
+    got = big.variants()
+    for s, b in enumerate(samples):
+        one = _engine(ref)
+        one.accumulate(*b)
+        one.finalize()
+        mine = [dict(v, start=v["start"] - s * L, stop=v["stop"] - s * L) for v in got if s * L <= v["start"] < (s + 1) * L]
+        compare_variants(mine, one.variants(), rtol=RTOL)
+        one.close()
+    big.close()
