@@ -47,7 +47,7 @@ class SpgRecords(C.Structure):
                 ("rec", C.c_void_p), ("rpos", C.c_void_p), ("rend", C.c_void_p), ("tweak", C.c_void_p),
                 ("n_tweaks", C.c_int64), ("tweak_col", C.c_void_p), ("tweak_qual", C.c_void_p),
                 ("orig_qual", C.c_void_p), ("orig_bytes", C.c_uint64), ("max_span", C.c_int64),
-                ("reserved", C.c_int64 * 4)]
+                ("pos_origin", C.c_int64), ("reserved", C.c_int64 * 3)]
 
 
 DETAIL_DTYPE = np.dtype([("pos", "<i8"), ("depth", "<u4"), ("n_alleles", "u1"), ("pad", "u1", 3),
@@ -110,6 +110,11 @@ def gpu_lib():
     _sig(L.spg_multi_get_candidates, i32, vp, vp, i64, C.POINTER(i64))
     _sig(L.spg_multi_partition, i32, vp, C.POINTER(i64))
     _sig(L.spg_multi_context, i32, vp, i32, C.POINTER(vp))
+    _sig(L.spg_multi_accumulate_records, i32, vp, C.POINTER(SpgRecords), C.c_uint32)
+    _sig(L.spg_multi_wait_input, i32, vp)
+    _sig(L.spg_multi_set_rebalance, i32, vp, C.c_double, i64)
+    _sig(L.spg_multi_replans, i32, vp, C.POINTER(i64))
+    _sig(L.spg_multi_plan_cuts, i32, vp, i64, i64, i64, i32, C.POINTER(i64))
     _sig(L.spg_set_history_cap, i32, vp, i64)
     _sig(L.spg_history_resident, i32, vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64))
     _sig(L.spg_path_counters, i32, vp, C.POINTER(i64), i64)

@@ -1030,7 +1030,7 @@ static int upload_records(spg_ctx *c, const spg_records *R, const HistBatch &hb,
     A.off = hb.off;
     A.code = hb.code;
     A.qual = hb.qual;
-    A.pos_begin = R->pos_begin;
+    A.pos_begin = R->pos_begin + R->pos_origin;     // (the fill compares reference positions)
     A.n_cols = (int32_t)R->n_cols;
     A.n_tiles = (int32_t)n_tiles;
     A.n_reads = (uint32_t)n;
@@ -1219,8 +1219,8 @@ int spg_accumulate_records(spg_ctx *c, const spg_records *r, uint32_t flags) {
     if (!c->ref) return fail("spg_accumulate: spg_set_reference not called");
     if (r->n_cols < 0 || r->n_cols > ((int64_t)1 << 31) - 128) return fail("spg_accumulate_records: n_cols out of range");
     if (r->n_reads < 0 || r->n_reads >= ((int64_t)1 << 31)) return fail("spg_accumulate_records: n_reads out of range");
-    if (r->n_tweaks < 0 || r->n_tweaks > r->n_reads || r->max_span < 0)
-        return fail("spg_accumulate_records: bad tweak count / span");
+    if (r->n_tweaks < 0 || r->n_tweaks > r->n_reads || r->max_span < 0 || r->pos_origin < 0)
+        return fail("spg_accumulate_records: bad tweak count / span / origin");
     if (r->n_cols > 0 && (!r->offsets || (r->n_reads && (!r->data || !r->rec || !r->rpos || !r->rend || !r->tweak)) ||
                           (r->n_tweaks && (!r->tweak_col || !r->tweak_qual || (r->orig_bytes && !r->orig_qual)))))
         return fail("spg_accumulate_records: null buffer");

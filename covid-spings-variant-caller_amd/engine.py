@@ -345,8 +345,12 @@ class PileupEngine:
     # -- reference-shaped views -----------------------------------------------------------------
     def variants(self) -> List[dict]:
         """The list prepare_variants() returns (live_variant_caller.py:170-185)."""
+        return self._variants_of(self.candidates())
+
+    @staticmethod
+    def _variants_of(cands) -> List[dict]:
         out = []
-        for r in self.candidates():
+        for r in cands:
             gl = 0 if r["gl_zero"] else float(r["gl"])
             out.append({
                 "start": int(r["pos"]), "stop": int(r["pos"]) + 1,

@@ -141,7 +141,11 @@ class LiveVariantCaller:
     def __init__(self, referenceFasta: str, minBaseQuality: int, minMappingQuality: int, minTotalDepth: int,
                  minAlleleDepth: int, minEvidenceRatio: float, maxVariants: int, device: Optional[int] = None,
                  max_depth: int = 8000, stepper: str = "all", ignore_overlaps: bool = True,
-                 n_threads: Optional[int] = None):
+                 n_threads: Optional[int] = None, devices: Optional[List[int]] = None):
+        """The reference's 7 arguments (:22-32), then the engine's: ``device`` (default LOCAL_RANK or 0), or
+        ``devices`` — several GPUs of this host, each owning a coordinate range of the contig (multi.MultiEngine,
+        spg_multi_*: BAM records and host batches sliced at equal-entry cuts, one RCCL gather of the call tables);
+        pileup()'s ``max_depth`` / stepper / ``ignore_overlaps``; host threads of the BAM plan."""
         self.minBaseQuality = minBaseQuality
         self.minMappingQuality = minMappingQuality
         self.minTotalDepth = minTotalDepth
@@ -156,8 +160,13 @@ class LiveVariantCaller:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         n_pos = max(self.fastaFile.lengths) if self.fastaFile.lengths else 1
         # calls-only engine: prepare_variants() is the class's only statistical output
-        self.engine = PileupEngine(max(1, n_pos), minBaseQuality, minTotalDepth, minAlleleDepth, minEvidenceRatio,
-                                   device=device, calls_only=True)
+        if devices is not None and len(devices) > 0:
+            from .multi import MultiEngine
+            self.engine = MultiEngine(list(devices), max(len(devices), n_pos), minBaseQuality, minTotalDepth,
+                                      minAlleleDepth, minEvidenceRatio, calls_only=True)
+        else:
+            self.engine = PileupEngine(max(1, n_pos), minBaseQuality, minTotalDepth, minAlleleDepth, minEvidenceRatio,
+                                       device=device, calls_only=True)
         self._lock = threading.RLock()
         self._ingest = PinnedIngest(self.engine)
         self._batch_contig: List[int] = []       # FASTA reference index of each accumulated batch

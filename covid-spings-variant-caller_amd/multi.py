@@ -1,14 +1,31 @@
 """MultiEngine — the C-ABI's one-process multi-device context (include/spings_gpu.h spg_multi_*): each device
-owns a coordinate range, host batches are sliced at the cuts, and the call tables come back with one RCCL
-gather.  The torch-free counterpart of shard.ShardedEngine (one process per GPU over torch.distributed)."""
+owns a coordinate range (its own context over that range only), host batches and BAM records plans are sliced at
+the cuts (the device pileup runs on every device), cuts follow the entries and are re-planned when the load drifts,
+and the call tables come back with one RCCL gather.  The torch-free counterpart of shard.ShardedEngine (one
+process per GPU over torch.distributed), and the engine behind LiveVariantCaller(..., devices=[...]): it offers
+the PileupEngine methods the caller uses (accumulate, accumulate_bam_records, finalize, variants, table, history)
+with positions in reference coordinates."""
 from __future__ import annotations
 
 import ctypes as C
+import threading
+from typing import Dict, List
 
 import numpy as np
 
 from . import _native as N
-from .engine import eps_lut
+from .engine import PileupEngine, eps_lut
+
+
+def plan_cuts(weights, bucket: int, n_pos: int, n: int) -> np.ndarray:
+    """spg_multi_plan_cuts: equal-entry cuts over a bucket histogram (host only)."""
+    w = np.ascontiguousarray(weights, dtype=np.uint64)
+    cuts = np.zeros(n + 1, np.int64)
+    rc = N.gpu_lib().spg_multi_plan_cuts(N.ptr(w) if len(w) else None, len(w), int(bucket), int(n_pos), int(n),
+                                         cuts.ctypes.data_as(C.POINTER(C.c_int64)))
+    if rc != 0:
+        raise RuntimeError(f"spg_multi_plan_cuts: {N.gpu_lib().spg_multi_last_error().decode()}")
+    return cuts
 
 
 class MultiEngine:
@@ -16,8 +33,10 @@ class MultiEngine:
                  min_allele_depth: int = 5, min_evidence_ratio: float = 0.10, reference: str | None = None,
                  calls_only: bool = True):
         self._L = N.gpu_lib()
+        self._lock = threading.RLock()
         self.devices = [int(d) for d in devices]
         self.n_pos = int(n_pos)
+        self.calls_only = bool(calls_only)
         self.params = N.SpgParams(int(min_base_quality), int(min_total_depth), int(min_allele_depth),
                                   N.SPG_P_CALLS_ONLY if calls_only else 0, float(min_evidence_ratio))
         devs = (C.c_int * len(self.devices))(*self.devices)
@@ -27,17 +46,20 @@ class MultiEngine:
         self._h = h
         self._lut = eps_lut()
         self._check(self._L.spg_multi_set_eps_lut(self._h, N.ptr(self._lut)), "spg_multi_set_eps_lut")
+        self._seq = 0
+        self.reference = None
         if reference is not None:
             self.set_reference(reference)
 
     def _check(self, rc, what):
         if rc != 0:
-            raise RuntimeError(f"{what}: {self._L.spg_multi_last_error().decode()}")
+            raise N.NativeError(f"{what}: {self._L.spg_multi_last_error().decode()}")
 
     def close(self):
-        if getattr(self, "_h", None):
-            self._L.spg_multi_destroy(self._h)
-            self._h = None
+        with self._lock:
+            if getattr(self, "_h", None):
+                self._L.spg_multi_destroy(self._h)
+                self._h = None
 
     def __del__(self):
         try:
@@ -45,37 +67,162 @@ class MultiEngine:
         except Exception:
             pass
 
+    # -- lifecycle / input ---------------------------------------------------------------------
     def set_reference(self, seq: str):
-        b = seq.encode("latin-1")
-        self._check(self._L.spg_multi_set_reference(self._h, b, len(b)), "spg_multi_set_reference")
+        with self._lock:
+            b = seq.encode("latin-1") if isinstance(seq, str) else bytes(seq)
+            self._check(self._L.spg_multi_set_reference(self._h, b, len(b)), "spg_multi_set_reference")
+            self.reference = seq
 
     def reset(self):
-        self._check(self._L.spg_multi_reset(self._h), "spg_multi_reset")
+        with self._lock:
+            self._check(self._L.spg_multi_reset(self._h), "spg_multi_reset")
 
-    def accumulate(self, pos_begin: int, offsets, codes, quals):
-        o = np.ascontiguousarray(offsets, dtype=np.uint64)
-        c = np.ascontiguousarray(codes, dtype=np.uint8)
-        q = np.ascontiguousarray(quals, dtype=np.uint8)
-        self._check(self._L.spg_multi_accumulate(self._h, int(pos_begin), len(o) - 1, N.ptr(o), N.ptr(c), N.ptr(q),
-                                                 len(c), 0), "spg_multi_accumulate")
+    def set_rebalance(self, ratio: float, max_batches: int):
+        with self._lock:
+            self._check(self._L.spg_multi_set_rebalance(self._h, float(ratio), int(max_batches)), "spg_multi_set_rebalance")
+
+    def replans(self) -> int:
+        n = C.c_int64()
+        with self._lock:
+            self._check(self._L.spg_multi_replans(self._h, C.byref(n)), "spg_multi_replans")
+        return n.value
+
+    def accumulate(self, pos_begin: int, offsets, codes, quals, trusted: bool = False, **_):
+        with self._lock:
+            o = np.ascontiguousarray(offsets, dtype=np.uint64)
+            c = np.ascontiguousarray(codes, dtype=np.uint8)
+            q = np.ascontiguousarray(quals, dtype=np.uint8)
+            self._check(self._L.spg_multi_accumulate(self._h, int(pos_begin), len(o) - 1, N.ptr(o), N.ptr(c), N.ptr(q),
+                                                     len(c), N.SPG_IN_TRUSTED if trusted else 0), "spg_multi_accumulate")
+            self._seq += 1
+
+    def accumulate_bam_records(self, batch):
+        """A records plan (pileup.AlignmentFile.pileup_records) sharded over the devices: each decodes the reads that
+        reach its range (spg_multi_accumulate_records).  Keep ``batch`` open until wait_ticket(input_ticket())."""
+        r = batch.records()
+        with self._lock:
+            self._check(self._L.spg_multi_accumulate_records(self._h, C.byref(r), 0), "spg_multi_accumulate_records")
+            self._seq += 1
+
+    def input_ticket(self) -> int:
+        return self._seq
+
+    def wait_ticket(self, ticket: int):
+        """Every input copy enqueued so far has landed (a ticket waits for all of them: coarser than PileupEngine's)."""
+        if ticket:
+            self.wait_input()
+
+    def wait_input(self):
+        with self._lock:
+            self._check(self._L.spg_multi_wait_input(self._h), "spg_multi_wait_input")
 
     def finalize(self):
-        self._check(self._L.spg_multi_finalize(self._h), "spg_multi_finalize")
+        with self._lock:
+            self._check(self._L.spg_multi_finalize(self._h), "spg_multi_finalize")
 
+    def sync(self):
+        with self._lock:
+            for ctx in self._contexts():
+                N.check(self._L.spg_sync(ctx), "spg_sync")
+
+    # -- results ---------------------------------------------------------------------------------
     def partition(self) -> np.ndarray:
         cuts = np.zeros(len(self.devices) + 1, np.int64)
-        self._check(self._L.spg_multi_partition(self._h, cuts.ctypes.data_as(C.POINTER(C.c_int64))), "spg_multi_partition")
+        with self._lock:
+            self._check(self._L.spg_multi_partition(self._h, cuts.ctypes.data_as(C.POINTER(C.c_int64))),
+                        "spg_multi_partition")
         return cuts
 
     def candidates(self) -> np.ndarray:
-        """The merged call table in memory order (first_batch, pos, allele rank)."""
+        """The merged call table in memory order (first_batch, pos, allele rank), reference positions."""
         n = C.c_int64()
         cap = 1024
-        while True:
-            arr = np.zeros(cap, N.CANDIDATE_DTYPE)
-            rc = self._L.spg_multi_get_candidates(self._h, N.ptr(arr), cap, C.byref(n))
-            if rc == 0:
-                return arr[:n.value]
-            if n.value <= cap:
-                self._check(rc, "spg_multi_get_candidates")
-            cap = int(n.value)
+        with self._lock:
+            while True:
+                arr = np.zeros(cap, N.CANDIDATE_DTYPE)
+                rc = self._L.spg_multi_get_candidates(self._h, N.ptr(arr), cap, C.byref(n))
+                if rc == 0:
+                    return arr[:n.value]
+                if n.value <= cap:
+                    self._check(rc, "spg_multi_get_candidates")
+                cap = int(n.value)
+
+    def variants(self) -> List[dict]:
+        """The list prepare_variants() returns (live_variant_caller.py:170-185)."""
+        return PileupEngine._variants_of(self.candidates())
+
+    def _contexts(self):
+        out = []
+        for i in range(len(self.devices)):
+            h = C.c_void_p()
+            if self._L.spg_multi_context(self._h, i, C.byref(h)) != 0:
+                return []
+            out.append(h)
+        return out
+
+    def _cuts_of_contexts(self):
+        """The ranges the device contexts cover (the last planned sample's cuts)."""
+        try:
+            return self.partition()
+        except N.NativeError:
+            return None
+
+    def table(self) -> Dict[str, np.ndarray]:
+        """Every device's per-position table, concatenated in reference coordinates (spg_get_table per device)."""
+        n = self.n_pos
+        out = dict(depth=np.zeros(n, np.uint32), counts=np.zeros((n, N.SPG_NCOUNT), np.uint32),
+                   gl=np.zeros((n, N.SPG_NSLOT), np.float64), flags=np.zeros(n, np.uint8),
+                   order=np.zeros(n, np.uint32), first_batch=np.zeros(n, np.uint32))
+        with self._lock:
+            ctxs, cuts = self._contexts(), self._cuts_of_contexts()
+            if not ctxs or cuts is None:
+                return out
+            for d, ctx in enumerate(ctxs):
+                lo, hi = int(cuts[d]), int(cuts[d + 1])
+                N.check(self._L.spg_get_table(ctx, 0, hi - lo, *[N.ptr(out[k][lo:hi]) for k in
+                                                                  ("depth", "counts", "gl", "flags", "order",
+                                                                   "first_batch")]), "spg_get_table")
+        return out
+
+    def history_count(self) -> int:
+        with self._lock:
+            ctxs = self._contexts()
+            if not ctxs:
+                return 0
+            n = C.c_int64()
+            N.check(self._L.spg_history_count(ctxs[0], C.byref(n)), "spg_history_count")
+            return n.value
+
+    def history(self, start: int = 0):
+        """The accumulated batches, reassembled from the devices' slices in reference coordinates:
+        [(pos_begin, offsets, codes, quals)] (a batch's extent spans the slices that hold entries)."""
+        out = []
+        with self._lock:
+            ctxs, cuts = self._contexts(), self._cuts_of_contexts()
+            if not ctxs or cuts is None:
+                return out
+            for i in range(max(0, int(start)), self.history_count()):
+                parts = []
+                for d, ctx in enumerate(ctxs):
+                    pb, nc, ne = C.c_int64(), C.c_int64(), C.c_uint64()
+                    N.check(self._L.spg_history_info(ctx, i, C.byref(pb), C.byref(nc), C.byref(ne)), "spg_history_info")
+                    if ne.value == 0:
+                        continue
+                    off = np.zeros(nc.value + 1, np.uint64)
+                    codes = np.zeros(ne.value, np.uint8)
+                    quals = np.zeros(ne.value, np.uint8)
+                    N.check(self._L.spg_history_copy(ctx, i, N.ptr(off), N.ptr(codes), N.ptr(quals)), "spg_history_copy")
+                    parts.append((int(cuts[d]) + pb.value, off, codes, quals))
+                if not parts:
+                    out.append((0, np.zeros(1, np.uint64), np.zeros(0, np.uint8), np.zeros(0, np.uint8)))
+                    continue
+                p0 = parts[0][0]
+                p1 = parts[-1][0] + len(parts[-1][1]) - 1
+                lens = np.zeros(p1 - p0, np.int64)
+                for pb, off, _, _ in parts:
+                    lens[pb - p0:pb - p0 + len(off) - 1] = np.diff(off.astype(np.int64))
+                offs = np.zeros(p1 - p0 + 1, np.uint64)
+                np.cumsum(lens, out=offs[1:])
+                out.append((p0, offs, np.concatenate([p[2] for p in parts]), np.concatenate([p[3] for p in parts])))
+        return out

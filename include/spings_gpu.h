@@ -188,7 +188,10 @@ typedef struct spg_records {
     const uint8_t *orig_qual;
     uint64_t orig_bytes;
     int64_t max_span;              /* max(rend - rpos) */
-    int64_t reserved[4];
+    int64_t pos_origin;            /* rpos / rend / tweak_col are reference positions; the context's position of
+                                      reference position x is x - pos_origin (0 for a context over the whole contig;
+                                      spg_multi passes each device's cut) */
+    int64_t reserved[3];
 } spg_records;
 int spg_accumulate_records(spg_ctx *ctx, const spg_records *r, uint32_t flags);
 
@@ -285,27 +288,45 @@ size_t spg_sizeof_detail(void);
 size_t spg_sizeof_acc(void);
 
 /* ---- one process, N devices (SURVEY §8 b/e; shard.py's ShardedEngine without torch) ----------------------
- * Each device's context owns a contiguous coordinate range, cut on the first batch of a sample (equal entries)
- * and kept until reset; host batches are sliced at the cuts (a device with an empty slice gets an empty batch, so
- * batch numbers and first visits stay global); the compact call tables come back to devices[0] with ONE RCCL
- * ncclGather over xGMI and are merged in memory order (first_batch, pos, allele rank).  Replaces the
+ * Each device's context owns a contiguous coordinate range [cuts[d], cuts[d+1]) in its own coordinate space
+ * (records, counted totals and reference slice for that range only).  Cuts give every device equal entries over a
+ * per-bucket entry histogram: a sample is planned at its first batch (from the previous sample's histogram when
+ * there is one, else from that batch) and re-planned — its history re-sliced and re-accumulated — when one device's
+ * cumulative load exceeds `ratio` x the mean while the sample holds at most `max_batches` batches
+ * (spg_multi_set_rebalance; default 1.5, 256).  Every device takes every batch (an empty slice becomes one empty
+ * column), so batch numbers and first visits stay global; the compact call tables come back to devices[0] with ONE
+ * RCCL ncclGather over xGMI (a device listed twice — one GPU standing in for several — uses device copies instead)
+ * and are merged in memory order (first_batch, pos, allele rank), positions in reference coordinates.  Sliced
+ * offsets and record indices are staged in per-device pinned rings, so the devices' copies overlap.  Replaces the
  * reference's single-process loop (live_variant_caller.py:54-185) for multi-GPU hosts. */
 typedef struct spg_multi spg_multi;
 int spg_multi_create(const int *devices, int n, int64_t n_pos, const spg_params *params, spg_multi **out);
 int spg_multi_destroy(spg_multi *m);
 const char *spg_multi_last_error(void);
 int spg_multi_set_eps_lut(spg_multi *m, const double lut[256]);
+/* A contig shorter than n_pos is padded with 'N' internally; batches past its end are refused. */
 int spg_multi_set_reference(spg_multi *m, const char *seq, int64_t len);
 int spg_multi_reset(spg_multi *m);
-/* Host CSR batch, as spg_accumulate (SPG_IN_TRUSTED allowed; no device / borrowed input). */
+/* Host CSR batch, as spg_accumulate (SPG_IN_TRUSTED allowed; no device / borrowed input).  Pinned inputs are copied
+ * asynchronously: keep them until spg_multi_wait_input. */
 int spg_multi_accumulate(spg_multi *m, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
                          const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags);
+/* A BAM records plan (spg_accumulate_records, pos_origin 0), sharded: each device decodes the reads that reach its
+ * range on the GPU.  The plan's buffers are read asynchronously: keep them until spg_multi_wait_input. */
+int spg_multi_accumulate_records(spg_multi *m, const spg_records *r, uint32_t flags);
+int spg_multi_wait_input(spg_multi *m);
 int spg_multi_finalize(spg_multi *m);
 /* The merged call table (needs n_out <= cap; *n_out is set either way). */
 int spg_multi_get_candidates(spg_multi *m, spg_candidate *out, int64_t cap, int64_t *n_out);
 /* cuts[0..n]: device i owns positions [cuts[i], cuts[i+1]) (after the sample's first batch). */
 int spg_multi_partition(spg_multi *m, int64_t *cuts);
-/* The context of device index i (spg_* calls on it: table, details, timing). */
+int spg_multi_set_rebalance(spg_multi *m, double ratio, int64_t max_batches);
+/* Re-plans (history re-sliced) since creation. */
+int spg_multi_replans(spg_multi *m, int64_t *n);
+/* Equal-entry cuts over a bucket histogram (w[b] = entries in positions [b bucket, (b+1) bucket)): cuts[0] = 0,
+ * cuts[n] = n_pos, every range non-empty.  Host only (no GPU). */
+int spg_multi_plan_cuts(const uint64_t *w, int64_t n_buckets, int64_t bucket, int64_t n_pos, int n, int64_t *cuts);
+/* The context of device index i, in its own coordinates (position x of the contig is x - cuts[i] there). */
 int spg_multi_context(spg_multi *m, int i, spg_ctx **ctx);
 
 #ifdef __cplusplus

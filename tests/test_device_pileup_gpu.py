@@ -1,9 +1,11 @@
 """Device-side pileup: spg_accumulate_records' kernel (csrc/spg_fill.hip)
-decodes the BAM records and walks their CIGARs on the GPU.  The batch it writes must be bit-identical to
-spp_batch_fill's host CSR of the same BAM (tests/test_pileup*.py pin that one against oracle/pileup_port.py
-and the hand-derived fixtures) — on every fixture those tests use: config 1's testfile.sam, the hand-derived
-cases, random reads with every CIGAR op / '*' SEQ+QUAL / stacks / overlapping pairs under each stepper and
-depth cap, regions, and the simulator's BAMs up to 10,000x.  Then process_bam through it vs the host fill."""
+decodes the BAM records and walks their CIGARs on the GPU.  Its batch is checked against values the product
+did not compute: the hand-derived columns of tests/test_pileup_handderived.py (worked out from the htslib /
+pysam rules), oracle/pileup_port.py's column-by-column restatement on the same reads (random reads with every
+CIGAR op / '*' SEQ+QUAL / stacks / overlapping pairs under each stepper and depth cap), and config 1's
+restatement-generated fixture — and, on every fixture, against spp_batch_fill's host CSR (regions, long
+skips, the simulator's BAMs up to 10,000x).  Then process_bam through it vs the host fill.  (Parity with
+pysam itself stays unpinned: pysam/htslib is absent here and on the GPU box.)"""
 import os
 
 import numpy as np
@@ -83,39 +85,89 @@ def test_testfile_config1(tmp_path):
     np.testing.assert_array_equal(got[3], z["quals"])
 
 
+def _port(recs, contig, targets, tmp_path, **kw):
+    """oracle/pileup_port.py (the column-by-column restatement, a construction independent of the product's
+    emulator) on the same reads written as SAM text."""
+    from oracle import pileup_port as pp
+    sam = str(tmp_path / "port.sam")
+    samgen.write_sam(sam, targets, recs)
+    return pp.to_csr(pp.pileup_columns(sam, contig, **kw))
+
+
 def _hand_cases():
+    """(records, pileup kwargs, hand-derived columns from pos_begin, pos_begin): the fixtures of
+    tests/test_pileup_handderived.py, whose expected columns were worked out by hand from the htslib / pysam
+    rules (oracle/README.md)."""
     import test_pileup_handderived as H
+    A, C, G, T, DEL, SKIP = H.A, H.C, H.G, H.T, H.DEL, H.SKIP
     q = [30] * 10
-    yield [H.rec(f"a{i}", 1, "10M", "A" * 10, q) for i in range(5)] + \
-          [H.rec(f"b{i}", 3, "10M", "C" * 10, q) for i in range(2)], dict(max_depth=3)
-    yield [H.rec(f"a{i}", 5, "4M", "G" * 4, [30] * 4) for i in range(9)], dict(max_depth=0)
-    yield [H.rec("d1", 1, "3M2D2M", "ACGTA", [10, 11, 12, 13, 14]), H.rec("d2", 1, "5M2D", "TTTTT", [20, 21, 22, 23, 24]),
-           H.rec("n1", 1, "2M3N1M", "GGC", [30, 31, 32])], dict()
-    yield H._pair("A" * 10, [30] * 10, "A" * 10, [25] * 10), dict()
-    yield H._pair("A" * 10, [150] * 10, "A" * 10, [90] * 10), dict()
-    yield H._pair("A" * 10, [30] * 10, "C" * 10, [20] * 10), dict()
-    yield H._pair("G" * 10, [21] * 10, "T" * 10, [33] * 10), dict()
-    yield H._pair("G" * 10, [25] * 10, "T" * 10, [25] * 10), dict()
-    yield H._pair("A" * 10, [30] * 10, "A" * 10, [25] * 10), dict(ignore_overlaps=False)
+    yield ([H.rec(f"a{i}", 1, "10M", "A" * 10, q) for i in range(5)] + [H.rec(f"b{i}", 3, "10M", "C" * 10, q) for i in range(2)],
+           dict(max_depth=3), [[(A, 30)] * 3] * 2 + [[(A, 30)] * 3 + [(C, 30)]] * 8 + [[(C, 30)]] * 2, 0)
+    yield [H.rec(f"a{i}", 5, "4M", "G" * 4, [30] * 4) for i in range(9)], dict(max_depth=0), [[(G, 30)] * 9] * 4, 4
+    yield ([H.rec("d1", 1, "3M2D2M", "ACGTA", [10, 11, 12, 13, 14]), H.rec("d2", 1, "5M2D", "TTTTT", [20, 21, 22, 23, 24]),
+            H.rec("n1", 1, "2M3N1M", "GGC", [30, 31, 32])], dict(),
+           [[(A, 10), (T, 20), (G, 30)], [(C, 11), (T, 21), (G, 31)], [(G, 12), (T, 22), (SKIP, 32)],
+            [(DEL, 13), (T, 23), (SKIP, 32)], [(DEL, 13), (T, 24), (SKIP, 32)], [(T, 13), (DEL, 0), (C, 32)],
+            [(A, 14), (DEL, 0)]], 0)
+    yield (H._pair("A" * 10, [30] * 10, "A" * 10, [25] * 10), dict(),
+           [[(A, 30)]] * 5 + [[(A, 55), (A, 0)]] * 5 + [[(A, 25)]] * 5, 0)
+    yield (H._pair("A" * 10, [150] * 10, "A" * 10, [90] * 10), dict(),
+           [[(A, 150)]] * 5 + [[(A, 200), (A, 0)]] * 5 + [[(A, 90)]] * 5, 0)
+    yield (H._pair("A" * 10, [30] * 10, "C" * 10, [20] * 10), dict(),
+           [[(A, 30)]] * 5 + [[(A, 24), (C, 0)]] * 5 + [[(C, 20)]] * 5, 0)
+    yield (H._pair("G" * 10, [21] * 10, "T" * 10, [33] * 10), dict(),
+           [[(G, 21)]] * 5 + [[(G, 0), (T, 26)]] * 5 + [[(T, 33)]] * 5, 0)
+    yield (H._pair("G" * 10, [25] * 10, "T" * 10, [25] * 10), dict(),
+           [[(G, 25)]] * 5 + [[(G, 20), (T, 0)]] * 5 + [[(T, 25)]] * 5, 0)
+    yield (H._pair("A" * 10, [30] * 10, "A" * 10, [25] * 10), dict(ignore_overlaps=False),
+           [[(A, 30)]] * 5 + [[(A, 30), (A, 25)]] * 5 + [[(A, 25)]] * 5, 0)
+    improper = H._pair("A" * 10, [30] * 10, "A" * 10, [25] * 10)
+    improper[0]["flag"], improper[1]["flag"] = 97, 145
+    yield improper, dict(), [[(A, 30)]] * 5 + [[(A, 30), (A, 25)]] * 5 + [[(A, 25)]] * 5, 0
+    q4 = [30] * 4
+    flt = [H.rec("ok", 1, "4M", "AAAA", q4), dict(H.rec("sec", 1, "4M", "CCCC", q4), flag=0x100),
+           dict(H.rec("qc", 1, "4M", "GGGG", q4), flag=0x200), dict(H.rec("dup", 1, "4M", "TTTT", q4), flag=0x400),
+           dict(H.rec("mq0", 1, "4M", "CCCC", q4), mapq=0)]
+    yield flt, dict(min_mapping_quality=20), [[(A, 30), (C, 30)]] * 4, 0
+    yield flt, dict(stepper="samtools", min_mapping_quality=20), [[(A, 30)]] * 4, 0
 
 
-@pytest.mark.parametrize("case", range(9))
+N_HAND = 12
+
+
+@pytest.mark.parametrize("case", range(N_HAND))
 def test_hand_derived_fixtures(tmp_path, case):
-    recs, kw = list(_hand_cases())[case]
+    """The GPU fill against the hand-derived columns directly (not only against the host fill), and against
+    oracle/pileup_port.py where SAM text can carry the qualities (<= 93)."""
+    import test_pileup_handderived as H
+    recs, kw, cols, pb = list(_hand_cases())[case]
     bam = str(tmp_path / "h.bam")
     samgen.write_bam(bam, [("c", 60)], recs)
-    assert_same(device_fill(bam, "c", **kw), host_fill(bam, "c", **kw))
+    got = device_fill(bam, "c", **kw)
+    H.expect(got, pb, cols)
+    if all(ord(ch) - 33 <= 93 for r in recs for ch in r["qual"]):
+        assert_same(got, _port(recs, "c", [("c", 60)], tmp_path, **kw))
+    assert_same(got, host_fill(bam, "c", **kw))
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
 @pytest.mark.parametrize("kw", [dict(), dict(max_depth=4), dict(max_depth=0), dict(ignore_overlaps=False, max_depth=3),
                                 dict(stepper="samtools", min_mapping_quality=20, max_depth=6), dict(stepper="nofilter")])
 def test_random_reads(tmp_path, seed, kw):
+    """Random reads with every CIGAR op, '*' SEQ/QUAL, stacks and overlapping pairs: the GPU fill against
+    oracle/pileup_port.py, and against the host fill."""
     contigs = [("chrA", 700), ("chrB", 700)]
+    recs = samgen.random_records(seed, contigs, n_reads=400)
     bam = str(tmp_path / "r.bam")
-    samgen.write_bam(bam, contigs, samgen.random_records(seed, contigs, n_reads=400), block=5000)
+    samgen.write_bam(bam, contigs, recs, block=5000)
     for c, _ in contigs:
-        assert_same(device_fill(bam, c, **kw), host_fill(bam, c, **kw))
+        got = device_fill(bam, c, **kw)
+        port = _port(recs, c, contigs, tmp_path, **kw)
+        if got is None:
+            assert int(port[1][-1]) == 0
+            continue
+        assert_same(got, port)
+        assert_same(got, host_fill(bam, c, **kw))
 
 
 @pytest.mark.parametrize("region", [(100, 300), (0, 50), (550, 700), (250, 251)])

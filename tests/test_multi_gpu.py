@@ -1,7 +1,9 @@
-"""spg_multi_* (csrc/spg_multi.cpp): the one-process multi-device context of the C-ABI — coordinate cuts on the
-first batch, host batches sliced at them, one RCCL ncclGather of the call tables.  On the one-GPU box it runs
-with n = 1 (the cuts, the slicing, the gather and the merge order all exercised); the merged table must equal a
-single context's and the oracle's.  (Multi-device runs: unmeasured on hardware until the driver's 8-GPU node.)"""
+"""spg_multi_* (csrc/spg_multi.cpp): the one-process multi-device context of the C-ABI — equal-entry coordinate cuts,
+per-device contexts over their own ranges, host batches and BAM records plans sliced at the cuts, re-plans when the
+load drifts, one RCCL ncclGather of the call tables.  On the one-GPU box it runs with n = 1 and with device 0 listed
+several times (every slicing, empty-slice, re-plan and merge path; the gather by device copies instead of RCCL);
+the merged table must equal a single context's and the oracle's.  (Distinct devices — RCCL — are unmeasured on
+hardware until the driver's 8-GPU node runs.)"""
 import numpy as np
 import pytest
 
@@ -46,3 +48,131 @@ def test_multi_n1_equals_single_context_and_oracle():
     assert m.candidates().tobytes() == s.candidates().tobytes()
     m.close()
     s.close()
+
+
+def _variants_equal(a, b):
+    from oracle_util import compare_variants
+    compare_variants(a, b, rtol=1e-9)
+
+
+def test_multi_three_contexts_on_one_gpu_slices_and_merge():
+    """n = 3 contexts on device 0 (listed three times: no RCCL, tables gathered by device copies): batches sliced at
+    the cuts, empty slices as one-column batches (a batch inside one device's range), per-device coordinate spaces,
+    and the merged table in memory order — vs one context and the oracle, after several samples."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.multi import MultiEngine
+    L = 12_000
+    ref = synth.reference(L, seed=41)
+    batches = [synth.pileup(L, 60, seed=42 + i, ref=ref, snv_every=53, lo=(i * 900) % 4000, hi=L - (i * 500) % 3000)
+               for i in range(5)]
+    batches.append(synth.pileup(L, 80, seed=60, ref=ref, snv_every=53, lo=200, hi=900))      # one device only
+    m = MultiEngine([0, 0, 0], L, reference=ref)
+    m.set_rebalance(1e9, 0)                       # fixed cuts here (re-plans: the next test)
+    s = PileupEngine(L, 30, 10, 5, 0.10, device=0, reference=ref, calls_only=True)
+    for rnd in range(2):
+        m.reset()
+        s.reset()
+        orc = COracle(ref, 30, 10, 5, 0.10)
+        for b in batches[rnd:]:
+            m.accumulate(*b)
+            s.accumulate(*b)
+            orc.accumulate(*b)
+        cuts = m.partition()
+        assert len(cuts) == 4 and cuts[0] == 0 and cuts[-1] == L and np.all(np.diff(cuts) > 0)
+        m.finalize()
+        s.finalize()
+        orc.finalize()
+        got = m.candidates()
+        assert len(got) > 20
+        assert got.tobytes() == s.candidates().tobytes()
+        _variants_equal(m.variants(), orc.variants())
+        # the table and the history, reassembled in reference coordinates
+        t, ts = m.table(), s.table()
+        np.testing.assert_array_equal(t["depth"], ts["depth"])
+        np.testing.assert_array_equal(t["first_batch"], ts["first_batch"])
+        hm, hs = m.history(), s.history()
+        assert len(hm) == len(hs)
+        for (pa, oa, ca, qa), (pb, ob, cb, qb) in zip(hm, hs):
+            assert int(oa[-1]) == int(ob[-1])
+            np.testing.assert_array_equal(ca, cb)
+            np.testing.assert_array_equal(qa, qb)
+    m.close()
+    s.close()
+
+
+def test_multi_amplicon_first_batch_replans():
+    """An amplicon-shaped first batch (three short windows) plans every cut inside the windows; later full-coverage
+    batches overload the last device, the sample is re-planned (history re-sliced at the new cuts) and the calls
+    stay those of one context; the next sample is planned from this sample's histogram."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.multi import MultiEngine
+    L = 12_000
+    ref = synth.reference(L, seed=43)
+    amp = [synth.pileup(L, 300, seed=44 + k, ref=ref, snv_every=29, lo=lo, hi=lo + 300) for k, lo in
+           enumerate((500, 5000, 9000))]
+    full = [synth.pileup(L, 50, seed=50 + i, ref=ref, snv_every=37) for i in range(4)]
+    m = MultiEngine([0, 0, 0, 0], L, reference=ref)
+    s = PileupEngine(L, 30, 10, 5, 0.10, device=0, reference=ref, calls_only=True)
+    orc = COracle(ref, 30, 10, 5, 0.10)
+    for b in amp + full:
+        m.accumulate(*b)
+        s.accumulate(*b)
+        orc.accumulate(*b)
+        if len(amp) and b is amp[0]:
+            first_cuts = m.partition()
+    assert first_cuts[-2] < 9300
+    assert m.replans() >= 1
+    cuts = m.partition()
+    assert cuts[-2] < L - 2000 and cuts[1] > 1000                    # balanced again
+    m.finalize()
+    s.finalize()
+    orc.finalize()
+    assert m.candidates().tobytes() == s.candidates().tobytes()
+    _variants_equal(m.variants(), orc.variants())
+    m.reset()                                                        # planned from the previous histogram,
+    m.accumulate(*amp[0])                                            # not from this amplicon batch
+    assert m.partition()[-2] > 2000
+    m.close()
+    s.close()
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_multi_records_path_vs_oracle(tmp_path, devices):
+    """The device pileup sharded (spg_multi_accumulate_records): LiveVariantCaller(devices=...) over simulated BAMs —
+    each context decodes the reads that reach its range — vs the oracle on the host pileup of the same BAMs, and vs
+    the single-device caller; then the memory view and a checkpoint round trip."""
+    import samgen
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.live_variant_caller import LiveVariantCaller
+    from covid_spings_variant_caller_amd.pileup import AlignmentFile, PileupParams, simulate_bam
+    L = 6000
+    ref = synth.reference(L, seed=45)
+    fasta = str(tmp_path / "ref.fa")
+    samgen.write_fasta(fasta, [("NC_045512.2", ref)])
+    bams = []
+    for i in range(3):
+        p = str(tmp_path / f"b{i}.bam")
+        simulate_bam(p, "NC_045512.2", ref, depth=150.0 + 50 * i, seed=70 + i, n_threads=4)
+        bams.append(p)
+    mc = LiveVariantCaller(fasta, 30, 20, 10, 5, 0.10, 1, devices=devices)
+    sc = LiveVariantCaller(fasta, 30, 20, 10, 5, 0.10, 1, device=0)
+    orc = COracle(ref, 30, 10, 5, 0.10)
+    for p in bams:
+        mc.process_bam(p)
+        sc.process_bam(p)
+        with AlignmentFile(p) as f:
+            b = f.pileup_batch("NC_045512.2", PileupParams(n_threads=4))
+            orc.accumulate(b.pos_begin, b.offsets.copy(), b.codes.copy(), b.quals.copy())
+        orc.finalize()
+        _variants_equal(mc.prepare_variants(), orc.variants())       # after every BAM (vc_queue.py:142-144)
+    _variants_equal(mc.prepare_variants(), sc.prepare_variants())
+    mm, ms = mc.memory, sc.memory
+    assert list(mm) == list(ms)
+    assert all(mm[p] == ms[p] for p in list(ms)[::97])
+    ck = str(tmp_path / "ck.npz")
+    mc.create_checkpoint(ck)
+    mc2 = LiveVariantCaller(fasta, 30, 20, 10, 5, 0.10, 1, devices=devices)
+    mc2.load_checkpoint(ck)
+    _variants_equal(mc2.prepare_variants(), orc.variants())
