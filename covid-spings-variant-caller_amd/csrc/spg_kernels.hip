@@ -637,6 +637,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     __shared__ ColDesc coldesc[KW][W == 4 ? SPG_GMAX_DEEP : SPG_GMAX];
     __shared__ Hist hdl;                                // FUSE: this batch's descriptor for the replay
     const uint64_t we = P.wtime ? __builtin_amdgcn_s_memrealtime() : 0;   // SPG_WAVE_TIMES: wave entry
+    // the batch's history descriptor, first (consumed at once: kept live, hipcc would park it in scratch)
+    write_hist(P);
+    if (FUSE && threadIdx.x == 0) hdl = P.hdesc;
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * KW + (threadIdx.x >> 6);
     // deep_list (the long columns of a shallow batch): the waves stride over the listed columns, one
@@ -644,17 +647,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     const bool listed = W == 1 && P.deep_n != nullptr;  // (W = 4: compile-time off; the loop runs once)
     // A wave's own group: its CSR offsets and REF chars are loaded before the LUT, so the two round
     // trips of a starting wave overlap (the LUT's wait covers both)
-    const bool tail0 = !listed && wave >= (int64_t)P.w1;
-    const int64_t g00 = tail0 ? (int64_t)P.w1 * P.G + (wave - P.w1) * P.G2 : wave * P.G;
-    const int ng0 = (int)max((int64_t)0, min((int64_t)(tail0 ? P.G2 : P.G), P.n_cols - g00));
+    int64_t g00;
+    int ng0;
+    if (P.dyn && blockIdx.x >= P.dyn_b0) {             // (workgroup-uniform) a dynamic-tail workgroup: claim a unit
+        __shared__ int32_t dyn_unit;
+        if (threadIdx.x < 64) {
+            const uint32_t xcd = blockIdx.x & 7u;
+            int32_t u = -1;
+            for (int attempt = 0; attempt < 16 && u < 0; attempt++) {
+                // units left per pool (lane p: one coherent read of pool p's counter)
+                uint32_t rem = 0;
+                if (lane < 8) {
+                    const uint32_t np = P.dyn_units > (uint32_t)lane ? (P.dyn_units - (uint32_t)lane + 7u) / 8u : 0u;
+                    const uint32_t c = __hip_atomic_load(P.dyn + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    rem = c < np ? np - c : 0u;
+                }
+                // this XCD's pool while it has units, else the fullest
+                uint32_t pick = 8u, most = 0u;
+                const uint32_t own = (uint32_t)__builtin_amdgcn_readlane((int)rem, (int)xcd);
+                if (own) pick = xcd;
+                else {
+#pragma unroll
+                    for (int pp = 0; pp < 8; pp++) {
+                        const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rem, pp);
+                        if (r > most) { most = r; pick = (uint32_t)pp; }
+                    }
+                }
+                if (pick == 8u) break;                 // every pool empty: nothing left for this workgroup
+                uint32_t k = 0;
+                if (lane == 0) k = atomicAdd(P.dyn + pick, 1u);
+                k = (uint32_t)__builtin_amdgcn_readfirstlane(k);
+                const uint32_t np = (P.dyn_units - pick + 7u) / 8u;
+                if (k < np) u = (int32_t)(k * 8u + pick);
+            }
+            if (lane == 0) dyn_unit = u;
+        }
+        __syncthreads();
+        const int32_t u = dyn_unit;
+        if (u < 0) return;                             // (the whole workgroup)
+        g00 = P.dyn_col0 + ((int64_t)u * KW + (threadIdx.x >> 6)) * (int64_t)P.G2;
+        ng0 = (int)max((int64_t)0, min((int64_t)P.G2, P.n_cols - g00));
+    } else {
+        const bool tail0 = !listed && wave >= (int64_t)P.w1;
+        g00 = tail0 ? (int64_t)P.w1 * P.G + (wave - P.w1) * P.G2 : wave * P.G;
+        ng0 = (int)max((int64_t)0, min((int64_t)(tail0 ? P.G2 : P.G), P.n_cols - g00));
+    }
     uint64_t ob0 = 0, oe0 = 0;
     uint32_t refc0 = 0, fsv0 = 0;
     if (!listed && lane < ng0) {
         ob0 = off[g00 + lane]; oe0 = off[g00 + lane + 1]; refc0 = ref[P.pos_begin + g00 + lane];
         if (P.fsamp) fsv0 = P.fsamp[g00 + lane];
     }
-    write_hist(P);
-    if (FUSE && threadIdx.x == 0) hdl = P.hdesc;
     if constexpr (FUSE) {
         if (blockIdx.x == 0 && threadIdx.x == 0) P.fused->O.ctr[P.fused->F.cslot ^ 1u] = Counters{0, 0, 0, 0};   // next call's slot
     }
@@ -1196,7 +1239,8 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
     const int64_t waves = P.w1 >= (P.n_cols + P.G - 1) / P.G ? (P.n_cols + P.G - 1) / P.G
                                                              : P.w1 + (P.n_cols - (int64_t)P.w1 * P.G + P.G2 - 1) / P.G2;
     // listed long columns: a fixed grid strides over the list (its length is on the device)
-    const int64_t blocks = P.deep_n ? std::min<int64_t>((P.n_cols + KW - 1) / KW, 2048) : (waves + KW - 1) / KW;
+    const int64_t blocks = P.deep_n ? std::min<int64_t>((P.n_cols + KW - 1) / KW, 2048)
+                                    : P.dyn ? (int64_t)P.dyn_b0 + (int64_t)P.dyn_nb : (waves + KW - 1) / KW;
     const bool fresh = P.batch_seq == 1;
     const bool w4 = P.t_deep <= 1;
     if (P.G > (uint32_t)(w4 ? SPG_GMAX_DEEP : SPG_GMAX) || (!P.deep_n && P.G2 > P.G)) return hipErrorInvalidValue;   // coldesc

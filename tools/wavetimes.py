@@ -47,6 +47,8 @@ def analyse(path):
         at += 16 * int(n)
         launches.append((int(g), w))
     g, w = launches[-1]
+    n_all = len(w)
+    w = w[w[:, 2] != 0]                              # (dynamic-tail waves that found no unit exit unrecorded)
     t0 = w[:, 0].astype(np.int64)
     t0 = (t0 - t0.min()) * 10e-3                     # us
     col = w[:, 1].astype(np.int64)
@@ -56,7 +58,7 @@ def analyse(path):
     xcc = w[:, 3] >> 24
     span = float(end.max())
     q = lambda a: {p: round(float(np.percentile(a, p)), 2) for p in (5, 25, 50, 75, 95, 100)}
-    res = {"waves": int(len(w)), "G": g, "span_us": round(span, 2),
+    res = {"waves": int(len(w)), "waves_launched": int(n_all), "G": g, "span_us": round(span, 2),
            "start_us": q(t0), "life_us": q(life), "prologue_us": q(pro), "end_us": q(end),
            "longest_waves": [{"first_column": int(col[i]), "life_us": round(float(life[i]), 2),
                               "start_us": round(float(t0[i]), 2)} for i in np.argsort(-life)[:8]],
