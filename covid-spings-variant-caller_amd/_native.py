@@ -118,6 +118,7 @@ def gpu_lib():
     _sig(L.spg_set_history_cap, i32, vp, i64)
     _sig(L.spg_history_resident, i32, vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64))
     _sig(L.spg_path_counters, i32, vp, C.POINTER(i64), i64)
+    _sig(L.spg_position_entries, i32, vp, i64, vp, vp, i64, C.POINTER(i64))
     _sig(L.spg_input_ticket, i32, vp, C.POINTER(u64))
     _sig(L.spg_wait_ticket, i32, vp, u64)
     _sig(L.spg_finalize, i32, vp)

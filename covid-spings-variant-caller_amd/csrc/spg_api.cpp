@@ -36,6 +36,9 @@ hipError_t launch_tile(const MParams &P, const Hist *H, const uint8_t *ref, int6
 hipError_t launch_merge(const MParams &P, const uint8_t *ref, Acc *acc, hipStream_t st);
 int tile_blocks_per_cu(int lpc, bool fused, bool one);
 hipError_t launch_pileup_fill(const FillArgs &A, hipStream_t st);
+hipError_t launch_pos_bounds(const Hist *H, const int32_t *items, int32_t n, int64_t pos, uint64_t *rng, hipStream_t st);
+hipError_t launch_pos_copy(const Hist *H, const int32_t *items, int32_t n, const uint64_t *rng, const uint64_t *dst,
+                           uint8_t *oc, uint8_t *oq, hipStream_t st);
 }  // namespace spg
 
 using namespace spg;
@@ -181,6 +184,8 @@ struct spg_ctx {
     uint64_t *fwm = nullptr;            // k_fold_hist's per-position fold watermarks ((generation << 32) | batches)
     RSlot *rcache = nullptr;            // replay cache (allocated once a history is long enough for replays to matter)
     uint32_t *dyn_ctr = nullptr;        // k_acc_seg's dynamic-tail pool counters: 64 launch slots x 8 pools (ring)
+    uint8_t *pe_buf = nullptr;          // spg_position_entries' device scratch (grow-only)
+    size_t pe_cap = 0;
     uint64_t dyn_seq = 0;
     uint32_t count_gen = 0;             // generation of the current counted run (bumped whenever counted mode starts)
     void *fold_part = nullptr;          // k_fold_hist's multi-workgroup partials [FOLD_CAP][FOLD_BPP]
@@ -354,7 +359,7 @@ int spg_destroy(spg_ctx *c) {
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
                     c->d_fused, c->deep_list, c->deep_n, c->cdep, c->cmcf, c->fwm, c->fold_part, c->fold_arrived, c->rs,
-                    c->ferr, c->rcache, c->dyn_ctr};
+                    c->ferr, c->rcache, c->dyn_ctr, c->pe_buf};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
@@ -1812,6 +1817,54 @@ int spg_kernel_times(spg_ctx *c, float *acc_ms, float *fin_ms, int64_t cap, int6
 int spg_path_counters(spg_ctx *c, int64_t *out, int64_t n) {
     if (!c || (!out && n > 0)) return fail("spg_path_counters: bad argument");
     for (int64_t i = 0; i < std::min<int64_t>(n, 8); i++) out[i] = c->path[i];
+    return 0;
+}
+
+int spg_position_entries(spg_ctx *c, int64_t pos, uint8_t *codes, uint8_t *quals, int64_t cap, int64_t *n_out) {
+    if (!c || !n_out || cap < 0 || (cap > 0 && (!codes || !quals))) return fail("spg_position_entries: bad argument");
+    if (pos < 0 || pos >= c->n_pos) return fail("spg_position_entries: position outside the context");
+    HIPCHK(hipSetDevice(c->device));
+    *n_out = 0;
+    const std::vector<int32_t> &items = c->buckets[(size_t)(pos >> RIDX_SHIFT)];
+    const int32_t n = (int32_t)items.size();
+    if (n == 0) return 0;
+    if (int rc = wait_copies(c)) return rc;
+    // every descriptor on the device (a pending batch's may not be yet)
+    const int64_t nh = (int64_t)c->hist.size();
+    if (c->hist_fence) { HIPCHK(hipEventSynchronize(c->hist_ev)); c->hist_fence = false; }
+    HIPCHK(hipMemcpyAsync(c->d_hist, c->h_hist, sizeof(Hist) * nh, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipEventRecord(c->hist_ev, c->stream));
+    c->hist_up = true;
+    const size_t need = sizeof(int32_t) * n + 3 * sizeof(uint64_t) * n + 64;
+    if (need > c->pe_cap) {
+        if (c->pe_buf) { HIPCHK(hipStreamSynchronize(c->stream)); HIPCHK(hipFree(c->pe_buf)); }
+        c->pe_buf = nullptr;
+        c->pe_cap = 0;
+        HIPCHK(hipMalloc(&c->pe_buf, need * 2));
+        c->pe_cap = need * 2;
+    }
+    uint64_t *d_rng = reinterpret_cast<uint64_t *>(c->pe_buf);
+    uint64_t *d_dst = d_rng + 2 * n;
+    int32_t *d_items = reinterpret_cast<int32_t *>(d_dst + n);
+    HIPCHK(hipMemcpyAsync(d_items, items.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_pos_bounds(c->d_hist, d_items, n, pos, d_rng, c->stream));
+    std::vector<uint64_t> rng(2 * (size_t)n), dst((size_t)n);
+    HIPCHK(hipMemcpyAsync(rng.data(), d_rng, sizeof(uint64_t) * 2 * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    uint64_t tot = 0;
+    for (int32_t i = 0; i < n; i++) { dst[(size_t)i] = tot; tot += rng[2 * (size_t)i + 1] - rng[2 * (size_t)i]; }
+    *n_out = (int64_t)tot;
+    if ((int64_t)tot > cap) return cap == 0 ? 0 : fail("spg_position_entries: output capacity too small");
+    if (tot == 0) return 0;
+    uint8_t *oc = nullptr;
+    HIPCHK(hipMalloc(&oc, 2 * tot));
+    HIPCHK(hipMemcpyAsync(d_dst, dst.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice, c->stream));
+    hipError_t e = launch_pos_copy(c->d_hist, d_items, n, d_rng, d_dst, oc, oc + tot, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(codes, oc, tot, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(quals, oc + tot, tot, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(oc);
+    if (e != hipSuccess) return fail(std::string("spg_position_entries: ") + hipGetErrorString(e));
     return 0;
 }
 

@@ -169,6 +169,43 @@ __global__ __launch_bounds__(256) void k_pileup_fill(FillArgs A) {
     if (__ballot(bad) && lane == 0) atomicOr(A.err, 2u);
 }
 
+// One position's entries across the history (LiveVariantCaller.memory, per position): the batches that may cover it
+// (the host's bucket list), their column bounds, then the entries packed in accumulate order.
+__global__ __launch_bounds__(256) void k_pos_bounds(const Hist *__restrict__ H, const int32_t *__restrict__ items, int32_t n,
+                                                    int64_t pos, uint64_t *__restrict__ rng) {
+    const int32_t i = (int32_t)(blockIdx.x * 256 + threadIdx.x);
+    if (i >= n) return;
+    const Hist h = H[items[i]];
+    const int64_t col = pos - h.pos_begin;
+    uint64_t lo = 0, hi = 0;
+    if (col >= 0 && col < h.n_cols) { lo = g(h.off)[col]; hi = g(h.off)[col + 1]; }
+    rng[2 * i] = lo;
+    rng[2 * i + 1] = hi;
+}
+__global__ __launch_bounds__(256) void k_pos_copy(const Hist *__restrict__ H, const int32_t *__restrict__ items, int32_t n,
+                                                  const uint64_t *__restrict__ rng, const uint64_t *__restrict__ dst,
+                                                  uint8_t *__restrict__ oc, uint8_t *__restrict__ oq) {
+    const int32_t i = (int32_t)(blockIdx.x * 4 + (threadIdx.x >> 6));      // one wave per batch
+    if (i >= n) return;
+    const Hist h = H[items[i]];
+    const uint64_t lo = rng[2 * i], hi = rng[2 * i + 1], d = dst[i];
+    for (uint64_t e = lo + (threadIdx.x & 63u); e < hi; e += 64) {
+        oc[d + (e - lo)] = g(h.code)[e];
+        oq[d + (e - lo)] = g(h.qual)[e];
+    }
+}
+hipError_t launch_pos_bounds(const Hist *H, const int32_t *items, int32_t n, int64_t pos, uint64_t *rng, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    k_pos_bounds<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(H, items, n, pos, rng);
+    return hipGetLastError();
+}
+hipError_t launch_pos_copy(const Hist *H, const int32_t *items, int32_t n, const uint64_t *rng, const uint64_t *dst,
+                           uint8_t *oc, uint8_t *oq, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    k_pos_copy<<<(unsigned)((n + 3) / 4), 256, 0, st>>>(H, items, n, rng, dst, oc, oq);
+    return hipGetLastError();
+}
+
 hipError_t launch_pileup_fill(const FillArgs &A, hipStream_t st) {
     if (A.n_tiles <= 0) return hipSuccess;
     k_tile_first<<<(unsigned)((A.n_reads + 1 + 255) / 256), 256, 0, st>>>(A);

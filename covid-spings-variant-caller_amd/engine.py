@@ -279,6 +279,18 @@ class PileupEngine:
             N.check(self._L.spg_kernel_times(self._h, N.ptr(a), N.ptr(f), int(cap), C.byref(n)), "spg_kernel_times")
         return a[:n.value].astype(np.float64), f[:n.value].astype(np.float64)
 
+    def position_entries(self, pos: int):
+        """(codes, quals) of every entry at ``pos`` over the history, in accumulate order (spg_position_entries)."""
+        n = C.c_int64()
+        with self._lock:
+            N.check(self._L.spg_position_entries(self._h, int(pos), None, None, 0, C.byref(n)), "spg_position_entries")
+            codes = np.zeros(n.value, np.uint8)
+            quals = np.zeros(n.value, np.uint8)
+            if n.value:
+                N.check(self._L.spg_position_entries(self._h, int(pos), N.ptr(codes), N.ptr(quals), n.value, C.byref(n)),
+                        "spg_position_entries")
+        return codes, quals
+
     def history_count(self) -> int:
         """Batches accumulated since reset() (spg_history_count)."""
         n = C.c_int64()

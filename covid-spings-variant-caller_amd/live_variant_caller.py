@@ -108,14 +108,15 @@ class PinnedIngest:
 
 
 class MemoryView(Mapping):
-    """``memory`` (live_variant_caller.py:32, dict[int, Site]) over the arrays LiveVariantCaller.memory
-    builds: iteration in insertion order (first visit), a Site built per lookup."""
+    """``memory`` (live_variant_caller.py:32, dict[int, Site]) as a lazy mapping: iteration in insertion order (first
+    visit) from the device table; a position's Site is built when it is read, from that position's entries over the
+    history (spg_position_entries: one device gather per lookup) — O(the position's entries), never O(all entries)."""
 
-    def __init__(self, order, depth, first_batch, refs, groups):
+    def __init__(self, order, depth, first_batch, refs, entries, min_bq):
         self._order = order
         self._sorted = np.sort(order)
         self._depth, self._fb, self._refs = depth, first_batch, refs
-        self._gpos, self._gcode, self._gs, self._ge, self._q = groups
+        self._entries, self._min_bq = entries, min_bq
 
     def __len__(self):
         return len(self._order)
@@ -131,8 +132,11 @@ class MemoryView(Mapping):
         if not isinstance(p, (int, np.integer)) or p not in self:
             raise KeyError(p)
         p = int(p)
-        lo, hi = np.searchsorted(self._gpos, p, "left"), np.searchsorted(self._gpos, p, "right")
-        snvs = {N.NIBBLE[int(self._gcode[g])]: self._q[self._gs[g]:self._ge[g]].tolist() for g in range(lo, hi)}
+        codes, quals = self._entries(p)
+        keep = (quals >= self._min_bq) & (codes < 16)           # pileups' bq filter (:75, :89); D/N: depth only
+        c, q = codes[keep], quals[keep]
+        u, first = np.unique(c, return_index=True)
+        snvs = {N.NIBBLE[int(k)]: q[c == k].tolist() for k in u[np.argsort(first)]}   # dict order = first seen
         return {"reference": self._refs[int(self._fb[p]) - 1][p], "totalDepth": int(self._depth[p]),
                 "snvs": snvs, "indels": {}}
 
@@ -212,42 +216,17 @@ class LiveVariantCaller:
     @property
     def memory(self) -> Mapping[int, Site]:
         """Read-only view of the reference's ``memory`` (dict[int, Site], insertion order), as a lazy
-        mapping: reference char and totalDepth from the device table, per-allele quality lists
-        (bq-filtered, BAM order) regrouped from the batch history with array sorts; a position's Site
-        is built when it is read (chr1 memories hold ~2.5e8 positions)."""
+        mapping: reference char and totalDepth from the device table, a position's per-allele quality lists
+        (bq-filtered, BAM order, dict order of first appearance) gathered from the batch history on the device when
+        the position is read (chr1 memories hold ~2.5e8 positions and ~7.5e9 entries)."""
         with self._lock:
             self.engine.finalize()
             t = self.engine.table()
-            hist = self.engine.history()
-            minbq = self.minBaseQuality
             present = np.nonzero(t["flags"] & N.SPG_F_PRESENT)[0]
             order = present[np.lexsort((present, t["first_batch"][present]))]
             refs = [self.fastaFile.fetch(self.fastaFile.references[i]) for i in self._batch_contig]
-            # every accumulated entry in accumulate order, then grouped per (position, allele) with a
-            # stable sort: each group is that allele's q list in BAM order (:103), groups of a position
-            # in order of their first entry (snvs dict order, :100-101)
-            pos_l, code_l, q_l = [], [], []
-            for pb, off, codes, quals in hist:
-                lens = np.diff(off.astype(np.int64))
-                pos = np.repeat(np.arange(pb, pb + len(lens), dtype=np.int64), lens)
-                keep = (quals >= minbq) & (codes < 16)
-                pos_l.append(pos[keep]); code_l.append(codes[keep]); q_l.append(quals[keep])
-            e = np.zeros(0, np.int64)
-            groups = (e, e, e, e, np.zeros(0, np.uint8))
-            if pos_l:
-                pos = np.concatenate(pos_l)
-                code = np.concatenate(code_l).astype(np.int64)
-                qs = np.concatenate(q_l)
-                key = pos * 16 + code
-                srt = np.argsort(key, kind="stable")
-                key_s = key[srt]
-                starts = np.flatnonzero(np.r_[True, key_s[1:] != key_s[:-1]])
-                ends = np.r_[starts[1:], len(key_s)]
-                first = srt[starts]                       # encounter index of each group's first entry
-                gpos, gcode = key_s[starts] // 16, key_s[starts] % 16
-                go = np.lexsort((first, gpos))            # by position, then dict order
-                groups = (gpos[go], gcode[go], starts[go], ends[go], qs[srt])
-            return MemoryView(order, t["depth"], t["first_batch"], refs, groups)
+            return MemoryView(order, t["depth"], t["first_batch"], refs, self.engine.position_entries,
+                              self.minBaseQuality)
 
     # -- hot path -----------------------------------------------------------------------------
     def process_bam(self, inputBam: str, referenceIndex=0):

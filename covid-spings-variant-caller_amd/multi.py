@@ -185,6 +185,22 @@ class MultiEngine:
                                                                    "first_batch")]), "spg_get_table")
         return out
 
+    def position_entries(self, pos: int):
+        """(codes, quals) of every entry at reference position ``pos``, from the device whose range holds it."""
+        with self._lock:
+            ctxs, cuts = self._contexts(), self._cuts_of_contexts()
+            if not ctxs or cuts is None:
+                return np.zeros(0, np.uint8), np.zeros(0, np.uint8)
+            d = int(np.searchsorted(cuts[1:-1], pos, side="right"))
+            local = int(pos) - int(cuts[d])
+            n = C.c_int64()
+            N.check(self._L.spg_position_entries(ctxs[d], local, None, None, 0, C.byref(n)), "spg_position_entries")
+            codes, quals = np.zeros(n.value, np.uint8), np.zeros(n.value, np.uint8)
+            if n.value:
+                N.check(self._L.spg_position_entries(ctxs[d], local, N.ptr(codes), N.ptr(quals), n.value, C.byref(n)),
+                        "spg_position_entries")
+        return codes, quals
+
     def history_count(self) -> int:
         with self._lock:
             ctxs = self._contexts()

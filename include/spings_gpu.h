@@ -256,6 +256,10 @@ int spg_history_resident(spg_ctx *ctx, int64_t *device_bytes, int64_t *n_spilled
 int spg_history_count(spg_ctx *ctx, int64_t *n_batches);
 int spg_history_info(spg_ctx *ctx, int64_t i, int64_t *pos_begin, int64_t *n_cols, uint64_t *n_entries);
 int spg_history_copy(spg_ctx *ctx, int64_t i, uint64_t *offsets, uint8_t *base_code, uint8_t *qual);
+/* One position's entries over the whole history, in accumulate order (the q list behind memory[pos], before the
+ * base-quality filter): *n_out = their number; codes / quals get them when n_out <= cap (cap 0: count only).
+ * Synchronises.  LiveVariantCaller.memory builds a Site from this per lookup instead of expanding every entry. */
+int spg_position_entries(spg_ctx *ctx, int64_t pos, uint8_t *codes, uint8_t *quals, int64_t cap, int64_t *n_out);
 /* Samples of history batch i (1 unless it came from spg_accumulate_samples) and, if first_sample is
  * not NULL, its per-column first samples (n_cols; zeros for a single-sample batch). */
 int spg_history_samples(spg_ctx *ctx, int64_t i, int64_t *n_samples, uint32_t *first_sample);
