@@ -63,7 +63,7 @@ struct spg_multi {
     std::vector<MBatch> batches;           // this sample's batches (extent), for re-plans
     std::vector<std::vector<Stage>> stage; // [device][NSTAGE]
     int stage_i = 0;
-    double rebalance_ratio = 1.5;          // max device load / mean that triggers a re-plan
+    double rebalance_ratio = 1.25;         // max device load / mean that triggers a re-plan
     int64_t rebalance_max_batches = 256;   // ... while the sample holds at most this many batches
     int64_t n_replans = 0;
     std::vector<void *> send;              // per device: [u64 count][cap x spg_candidate]

@@ -297,7 +297,7 @@ size_t spg_sizeof_acc(void);
  * per-bucket entry histogram: a sample is planned at its first batch (from the previous sample's histogram when
  * there is one, else from that batch) and re-planned — its history re-sliced and re-accumulated — when one device's
  * cumulative load exceeds `ratio` x the mean while the sample holds at most `max_batches` batches
- * (spg_multi_set_rebalance; default 1.5, 256).  Every device takes every batch (an empty slice becomes one empty
+ * (spg_multi_set_rebalance; default 1.25, 256).  Every device takes every batch (an empty slice becomes one empty
  * column), so batch numbers and first visits stay global; the compact call tables come back to devices[0] with ONE
  * RCCL ncclGather over xGMI (a device listed twice — one GPU standing in for several — uses device copies instead)
  * and are merged in memory order (first_batch, pos, allele rank), positions in reference coordinates.  Sliced
