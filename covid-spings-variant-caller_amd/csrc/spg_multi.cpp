@@ -336,7 +336,11 @@ static int replan(spg_multi *m, const std::vector<int64_t> &cuts) {
 // After a batch: re-plan when one device's cumulative load drifted past rebalance_ratio x the mean (an amplicon-
 // shaped or partial first batch), while the history is short enough to re-slice.
 static int maybe_rebalance(spg_multi *m) {
-    if (m->n < 2 || (int64_t)m->batches.size() > m->rebalance_max_batches || m->rebalance_max_batches == 0) return 0;
+    // (not on a sample's first batch: its cuts may come from the previous sample's histogram, which one batch of an
+    // amplicon-shaped BAM should not overturn)
+    if (m->n < 2 || m->batches.size() < 2 || (int64_t)m->batches.size() > m->rebalance_max_batches ||
+        m->rebalance_max_batches == 0)
+        return 0;
     std::vector<long double> load((size_t)m->n, 0);
     long double tot = 0;
     for (size_t b = 0; b < m->w_cur.size(); b++) {

