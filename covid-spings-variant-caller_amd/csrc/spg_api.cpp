@@ -664,12 +664,13 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     // XCD-balanced dynamic tail (KParams.dyn): the last SPG_DYN_FRAC of a deep batch's columns go to workgroups that
     // claim KW x G2 columns at a time from per-XCD pools, launched SPG_DYN_OVER x over-provisioned so that a faster
     // XCD takes more of them (r03 timeline: the XCDs ended 98.4-110.2 us into a 110 us launch)
-    static const double dyn_frac = [] { const char *e = getenv("SPG_DYN_FRAC"); return e ? atof(e) : 0.25; }();
-    static const double dyn_over = [] { const char *e = getenv("SPG_DYN_OVER"); return e ? atof(e) : 2.0; }();
+    static const double dyn_frac = [] { const char *e = getenv("SPG_DYN_FRAC"); return e ? atof(e) : 0.15; }();
+    static const double dyn_over = [] { const char *e = getenv("SPG_DYN_OVER"); return e ? atof(e) : 1.5; }();
+    static const int64_t dyn_half = [] { const char *e = getenv("SPG_DYN_HALF"); return e ? atoll(e) : 0ll; }();
     int64_t n_launch_waves = 0;
     if (deep_batch && !listed && dyn_frac > 0.0 && n_cols >= 512) {
         constexpr int64_t KWv = 4;                     // waves per k_acc_seg workgroup
-        const int64_t G2 = std::max<int64_t>(1, (int64_t)G / 2);
+        const int64_t G2 = dyn_half ? std::max<int64_t>(1, (int64_t)G / 2) : (int64_t)G;
         const int64_t w_static = (int64_t)((1.0 - std::min(dyn_frac, 1.0)) * (double)n_cols) / G / KWv * KWv;
         const int64_t col0 = w_static * G, unit = KWv * G2;
         const int64_t units = (n_cols - col0 + unit - 1) / unit;

@@ -651,36 +651,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     int ng0;
     if (P.dyn && blockIdx.x >= P.dyn_b0) {             // (workgroup-uniform) a dynamic-tail workgroup: claim a unit
         __shared__ int32_t dyn_unit;
-        if (threadIdx.x < 64) {
-            const uint32_t xcd = blockIdx.x & 7u;
-            int32_t u = -1;
-            for (int attempt = 0; attempt < 16 && u < 0; attempt++) {
-                // units left per pool (lane p: one coherent read of pool p's counter)
-                uint32_t rem = 0;
-                if (lane < 8) {
-                    const uint32_t np = P.dyn_units > (uint32_t)lane ? (P.dyn_units - (uint32_t)lane + 7u) / 8u : 0u;
-                    const uint32_t c = __hip_atomic_load(P.dyn + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    rem = c < np ? np - c : 0u;
-                }
-                // this XCD's pool while it has units, else the fullest
-                uint32_t pick = 8u, most = 0u;
-                const uint32_t own = (uint32_t)__builtin_amdgcn_readlane((int)rem, (int)xcd);
-                if (own) pick = xcd;
-                else {
-#pragma unroll
-                    for (int pp = 0; pp < 8; pp++) {
-                        const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)rem, pp);
-                        if (r > most) { most = r; pick = (uint32_t)pp; }
-                    }
-                }
-                if (pick == 8u) break;                 // every pool empty: nothing left for this workgroup
-                uint32_t k = 0;
-                if (lane == 0) k = atomicAdd(P.dyn + pick, 1u);
-                k = (uint32_t)__builtin_amdgcn_readfirstlane(k);
-                const uint32_t np = (P.dyn_units - pick + 7u) / 8u;
-                if (k < np) u = (int32_t)(k * 8u + pick);
-            }
-            if (lane == 0) dyn_unit = u;
+        if (threadIdx.x == 0) {
+            // one claim per workgroup from the launch's counter (units in column order); the over-provisioned ones
+            // find it past the end and exit
+            const uint32_t k = atomicAdd(P.dyn, 1u);
+            dyn_unit = k < P.dyn_units ? (int32_t)k : -1;
         }
         __syncthreads();
         const int32_t u = dyn_unit;
