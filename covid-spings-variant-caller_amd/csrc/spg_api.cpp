@@ -183,10 +183,8 @@ struct spg_ctx {
     uint32_t *cdep = nullptr, *cmcf = nullptr;
     uint64_t *fwm = nullptr;            // k_fold_hist's per-position fold watermarks ((generation << 32) | batches)
     RSlot *rcache = nullptr;            // replay cache (allocated once a history is long enough for replays to matter)
-    uint32_t *dyn_ctr = nullptr;        // k_acc_seg's dynamic-tail pool counters: 64 launch slots x 8 pools (ring)
     uint8_t *pe_buf = nullptr;          // spg_position_entries' device scratch (grow-only)
     size_t pe_cap = 0;
-    uint64_t dyn_seq = 0;
     uint32_t count_gen = 0;             // generation of the current counted run (bumped whenever counted mode starts)
     void *fold_part = nullptr;          // k_fold_hist's multi-workgroup partials [FOLD_CAP][FOLD_BPP]
     uint32_t *fold_arrived = nullptr;   // ... and arrival counts (zero between launches)
@@ -359,7 +357,7 @@ int spg_destroy(spg_ctx *c) {
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
                     c->d_fused, c->deep_list, c->deep_n, c->cdep, c->cmcf, c->fwm, c->fold_part, c->fold_arrived, c->rs,
-                    c->ferr, c->rcache, c->dyn_ctr, c->pe_buf};
+                    c->ferr, c->rcache, c->pe_buf};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_hist) (void)hipHostFree(c->h_hist);
@@ -610,7 +608,8 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     // fused (records kept in the wave's finishing ring for the finalize) only when a wave's columns fit the ring;
     // a wider group finishes its ring NB columns at a time, lists the positions that may call, and the caller
     // runs the sparse k_finalize over them (list mode: mid-depth batches such as 1,000x, G = 16)
-    if (F && g > NB_RING && deep_batch && !listed) {
+    static const bool list_on = [] { const char *e = getenv("SPG_LIST"); return !(e && atoi(e) == 0); }();   // (A/B)
+    if (F && g > NB_RING && deep_batch && !listed && list_on) {
         if (list_mode) *list_mode = true;
         F = nullptr;
         O = nullptr;
@@ -661,37 +660,7 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
             P.G2 = (uint32_t)G2;
         }
     }
-    // XCD-balanced dynamic tail (KParams.dyn): the last SPG_DYN_FRAC of a deep batch's columns go to workgroups that
-    // claim KW x G2 columns at a time from per-XCD pools, launched SPG_DYN_OVER x over-provisioned so that a faster
-    // XCD takes more of them (r03 timeline: the XCDs ended 98.4-110.2 us into a 110 us launch)
-    static const double dyn_frac = [] { const char *e = getenv("SPG_DYN_FRAC"); return e ? atof(e) : 0.15; }();
-    static const double dyn_over = [] { const char *e = getenv("SPG_DYN_OVER"); return e ? atof(e) : 1.5; }();
-    static const int64_t dyn_half = [] { const char *e = getenv("SPG_DYN_HALF"); return e ? atoll(e) : 0ll; }();
     int64_t n_launch_waves = 0;
-    if (deep_batch && !listed && dyn_frac > 0.0 && n_cols >= 512) {
-        constexpr int64_t KWv = 4;                     // waves per k_acc_seg workgroup
-        const int64_t G2 = dyn_half ? std::max<int64_t>(1, (int64_t)G / 2) : (int64_t)G;
-        const int64_t w_static = (int64_t)((1.0 - std::min(dyn_frac, 1.0)) * (double)n_cols) / G / KWv * KWv;
-        const int64_t col0 = w_static * G, unit = KWv * G2;
-        const int64_t units = (n_cols - col0 + unit - 1) / unit;
-        if (units > 0) {
-            if (!c->dyn_ctr) {
-                HIPCHK(hipMalloc(&c->dyn_ctr, sizeof(uint32_t) * 64 * 8));
-                HIPCHK(hipMemsetAsync(c->dyn_ctr, 0, sizeof(uint32_t) * 64 * 8, c->stream));
-            }
-            const uint64_t slot = c->dyn_seq++ % 64;
-            if (slot % 32 == 0)          // zero the other half of the ring (its launches are all enqueued before)
-                HIPCHK(hipMemsetAsync(c->dyn_ctr + (slot == 0 ? 32 : 0) * 8, 0, sizeof(uint32_t) * 32 * 8, c->stream));
-            P.w1 = (uint32_t)w_static;
-            P.G2 = (uint32_t)G2;
-            P.dyn = c->dyn_ctr + slot * 8;
-            P.dyn_b0 = (uint32_t)(w_static / KWv);
-            P.dyn_units = (uint32_t)units;
-            P.dyn_nb = (uint32_t)std::max<int64_t>(units, (int64_t)std::ceil((double)units * std::max(1.0, dyn_over)));
-            P.dyn_col0 = col0;
-            n_launch_waves = ((int64_t)P.dyn_b0 + (int64_t)P.dyn_nb) * KWv;
-        }
-    }
     P.t_deep = deep_batch ? 1u : 128u;
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
     P.n_entries = hb.n_entries;
@@ -716,8 +685,7 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     static const char *wt_file = getenv("SPG_WAVE_TIMES");
     static uint4 *wt_buf = nullptr;
     static int64_t wt_cap = 0;
-    const int64_t n_waves = P.dyn ? n_launch_waves
-                          : P.w1 >= (n_cols + G - 1) / G ? (n_cols + G - 1) / G
+    const int64_t n_waves = P.w1 >= (n_cols + G - 1) / G ? (n_cols + G - 1) / G
                                                         : P.w1 + (n_cols - (int64_t)P.w1 * G + P.G2 - 1) / P.G2;
     if (wt_file && deep_batch) {
         if (n_waves > wt_cap) {

@@ -106,15 +106,6 @@ struct KParams {
     // sparse k_finalize (null: no listing)
     int64_t *list;
     uint32_t *n_list;
-    // XCD-balanced dynamic tail (deep batches): workgroups >= dyn_b0 claim units of KW x G2 consecutive columns from
-    // [dyn_col0, n_cols) through 8 pool counters (this launch's slot, zeroed; pool p holds units u = 8 k + p, a
-    // workgroup tries the pool of its XCD (blockIdx mod 8) first) and exit once every pool is empty.  Workgroups are
-    // dealt to the XCDs round-robin, so each XCD gets the same number of dynamic workgroups, but those of a faster
-    // XCD start sooner and claim more units: the launch no longer waits for its slowest XCD.  (null: no dynamic tail)
-    uint32_t *dyn;
-    uint32_t dyn_b0, dyn_units;   // first dynamic workgroup (the static ones before it own G columns per wave); units
-    uint32_t dyn_nb, pad_dyn;     // dynamic workgroups launched (>= units: the spare ones exit when the pools are empty)
-    int64_t dyn_col0;
 };
 
 // Per-position state of a run of batches folded by one lane group (k_acc_tile), and

@@ -647,26 +647,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     const bool listed = W == 1 && P.deep_n != nullptr;  // (W = 4: compile-time off; the loop runs once)
     // A wave's own group: its CSR offsets and REF chars are loaded before the LUT, so the two round
     // trips of a starting wave overlap (the LUT's wait covers both)
-    int64_t g00;
-    int ng0;
-    if (P.dyn && blockIdx.x >= P.dyn_b0) {             // (workgroup-uniform) a dynamic-tail workgroup: claim a unit
-        __shared__ int32_t dyn_unit;
-        if (threadIdx.x == 0) {
-            // one claim per workgroup from the launch's counter (units in column order); the over-provisioned ones
-            // find it past the end and exit
-            const uint32_t k = atomicAdd(P.dyn, 1u);
-            dyn_unit = k < P.dyn_units ? (int32_t)k : -1;
-        }
-        __syncthreads();
-        const int32_t u = dyn_unit;
-        if (u < 0) return;                             // (the whole workgroup)
-        g00 = P.dyn_col0 + ((int64_t)u * KW + (threadIdx.x >> 6)) * (int64_t)P.G2;
-        ng0 = (int)max((int64_t)0, min((int64_t)P.G2, P.n_cols - g00));
-    } else {
-        const bool tail0 = !listed && wave >= (int64_t)P.w1;
-        g00 = tail0 ? (int64_t)P.w1 * P.G + (wave - P.w1) * P.G2 : wave * P.G;
-        ng0 = (int)max((int64_t)0, min((int64_t)(tail0 ? P.G2 : P.G), P.n_cols - g00));
-    }
+    const bool tail0 = !listed && wave >= (int64_t)P.w1;
+    const int64_t g00 = tail0 ? (int64_t)P.w1 * P.G + (wave - P.w1) * P.G2 : wave * P.G;
+    const int ng0 = (int)max((int64_t)0, min((int64_t)(tail0 ? P.G2 : P.G), P.n_cols - g00));
     uint64_t ob0 = 0, oe0 = 0;
     uint32_t refc0 = 0, fsv0 = 0;
     if (!listed && lane < ng0) {
@@ -1215,7 +1198,7 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
                                                              : P.w1 + (P.n_cols - (int64_t)P.w1 * P.G + P.G2 - 1) / P.G2;
     // listed long columns: a fixed grid strides over the list (its length is on the device)
     const int64_t blocks = P.deep_n ? std::min<int64_t>((P.n_cols + KW - 1) / KW, 2048)
-                                    : P.dyn ? (int64_t)P.dyn_b0 + (int64_t)P.dyn_nb : (waves + KW - 1) / KW;
+                                    : (waves + KW - 1) / KW;
     const bool fresh = P.batch_seq == 1;
     const bool w4 = P.t_deep <= 1;
     if (P.G > (uint32_t)(w4 ? SPG_GMAX_DEEP : SPG_GMAX) || (!P.deep_n && P.G2 > P.G)) return hipErrorInvalidValue;   // coldesc
