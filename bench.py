@@ -74,8 +74,9 @@ def parse():
     ap.add_argument("--e2e-many", type=int, default=64,
                     help="config 4 end to end: 100x SARS-CoV-2 BAM files through process_bams (0 = skip)")
     ap.add_argument("--full-table", action="store_true", help="also accumulate every table GL term")
-    ap.add_argument("--legs", default="parity,sars1k,sars100k,config4,chr1,e2e,cpu",
+    ap.add_argument("--legs", default="parity,sars1k,sars100k,sars100k_capped,config4,chr1,e2e,cpu",
                     help="nested legs of the default sars10k line (comma list; 'none' = the main point only)")
+    ap.add_argument("--no-main", action="store_true", help="profiling: skip the main point (nested legs only)")
     ap.add_argument("--sars1k-samples", type=int, default=64, help="stacked samples per GPU step at 1,000x")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
                                                       "gloo only to exercise the path on one GPU)")
@@ -785,7 +786,14 @@ def main():
     L = args.length or L
     depth = args.depth or depth
     args.eff_L, args.eff_depth = L, depth
-    main_pt = run_point(args, D, L, depth, args.max_depth, local, world, rank, contig)
+    if args.no_main:                            # (profiling: one nested leg on its own)
+        args.steps, args.reps, args.warmup = max(1, args.steps), max(1, args.reps), max(0, args.warmup)
+        main_pt = {"E": 0, "C": 0, "value": None, "steps": 0, "reps": 0, "ms_per_step": None, "achieved": 0.0,
+                   "kernel_ms": None, "kernel_ms_median": None, "kernel_samples": 0, "algo_bytes": 0,
+                   "measurements_ms": [], "finalize_ms": None, "host_enqueue_ms_per_step": None, "n_cand": 0,
+                   "n_replay": 0, "t_gen": 0.0, "gathered": None}
+    else:
+        main_pt = run_point(args, D, L, depth, args.max_depth, local, world, rank, contig)
     E, C = main_pt["E"], main_pt["C"]
     res = {
         "metric": ("pileup positions/s at 10,000x depth (SARS-CoV-2, synthetic)" if args.workload == "sars10k"
@@ -822,9 +830,10 @@ def main():
     if "sars1k" in legs and nested:           # BASELINE config 2
         res["sars1k"] = nested_point(args, D, "sars1k", local, world, rank, samples=args.sars1k_samples,
                                      distinct=min(16, args.sars1k_samples * world))
-    if "sars100k" in legs and nested:         # BASELINE config 3, uncapped (the LDS stress) and pysam's cap
+    if "sars100k" in legs and nested:         # BASELINE config 3, uncapped (the deep-column stress) and pysam's cap
         res["sars100k"] = nested_point(args, D, "sars100k", local, world, rank)
-        res["sars100k"]["parity_mode"] = nested_point(args, D, "sars100k", local, world, rank, max_depth=8000)
+    if "sars100k_capped" in legs and nested:
+        res.setdefault("sars100k", {})["parity_mode"] = nested_point(args, D, "sars100k", local, world, rank, max_depth=8000)
     if "config4" in legs and nested:          # BASELINE config 4
         res["config4"] = run_config4(args, D, local, world, rank)
     if "chr1" in legs and nested:             # BASELINE config 5

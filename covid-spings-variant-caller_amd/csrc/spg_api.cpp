@@ -32,9 +32,9 @@ hipError_t launch_fold_hist(const MParams &P, const Hist *H, const uint8_t *ref,
                             void *part, uint32_t *arrived, int bpp, int cap, hipStream_t st);
 size_t fold_part_bytes();
 hipError_t launch_tile(const MParams &P, const Hist *H, const uint8_t *ref, int64_t ref_len, const Tables *T, Acc *acc,
-                       int lpc, int64_t max_blocks, bool fused, hipStream_t st);
+                       int lpc, int64_t max_blocks, hipStream_t st);
 hipError_t launch_merge(const MParams &P, const uint8_t *ref, Acc *acc, hipStream_t st);
-int tile_blocks_per_cu(int lpc, bool fused, bool one);
+int tile_blocks_per_cu(int lpc, bool one);
 hipError_t launch_pileup_fill(const FillArgs &A, hipStream_t st);
 hipError_t launch_pos_bounds(const Hist *H, const int32_t *items, int32_t n, int64_t pos, uint64_t *rng, hipStream_t st);
 hipError_t launch_pos_copy(const Hist *H, const int32_t *items, int32_t n, const uint64_t *rng, const uint64_t *dst,
@@ -734,9 +734,9 @@ struct RunPlan {
     int lpc;
     int64_t n_groups, S, kper, tc;
 };
-static int64_t tile_blocks(const spg_ctx *c, int lpc, bool fused, bool one) {
+static int64_t tile_blocks(const spg_ctx *c, int lpc, bool one) {
     static const int64_t env = [] { const char *e = getenv("SPG_TILE_BLOCKS"); return e ? atoll(e) : 0ll; }();
-    return env > 0 ? env : (int64_t)c->n_cu * tile_blocks_per_cu(lpc, fused, one);
+    return env > 0 ? env : (int64_t)c->n_cu * tile_blocks_per_cu(lpc, one);
 }
 static RunPlan plan_run(const spg_ctx *c, int64_t h0, int64_t h1, int64_t u0, int64_t u1, uint64_t run_entries) {
     const int64_t K = h1 - h0, L = u1 - u0;
@@ -747,8 +747,7 @@ static RunPlan plan_run(const spg_ctx *c, int64_t h0, int64_t h1, int64_t u0, in
     while (R.lpc < 8 && (64.0 / R.lpc) * mean > fill) R.lpc *= 2;
     R.tc = 64 / R.lpc;
     R.n_groups = (L + R.tc - 1) / R.tc;
-    // (resident waves: the fused and plain forms have the same LDS and register footprint)
-    const int64_t waves = tile_blocks(c, R.lpc, false, false) * 2;
+    const int64_t waves = tile_blocks(c, R.lpc, false) * 2;
     int64_t best = 1;
     if (K > 1 && R.n_groups < waves) {
         double best_eff = -1.0;
@@ -808,7 +807,8 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
     P.err = c->kerr;
     c->kerr_dirty = true;
     if (fused) {
-        if (P.S != 1 || h0 != 0) return fail("spg: internal: fused run must be one FRESH unsplit run");
+        if (K != 1 || h0 != 0 || (double)run_entries > 40.0 * (double)(u1 - u0))
+            return fail("spg: internal: a fused run is one FRESH shallow batch (k_acc_lite)");
         P.min_td = c->p.min_total_depth;
         P.min_ad = c->p.min_allele_depth;
         P.ratio_lo = c->p.min_evidence_ratio * (1.0 - 1e-9);
@@ -847,7 +847,7 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
     }
     // a FUSED single shallow batch into a FRESH memory (process_bam + prepare_variants; mean column <= 40
     // entries): k_acc_lite, counts + the exact fold of the columns that may call
-    const bool lite = fused && K == 1 && P.fresh && (double)run_entries <= 40.0 * (double)(u1 - u0);
+    const bool lite = fused;
     if (lite) {
         static const int64_t lb = env_i64("SPG_LITE_BLOCKS", 0);
         P.n_groups = (int32_t)((u1 - u0 + 63) / 64);
@@ -856,9 +856,8 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
         // the listed positions' exact fold (their records; deep columns are k_acc_seg<1>'s below)
         HIPCHK(launch_lite_fold(P, c->h_hist[h0], c->ref, c->tables, c->acc, 2 * (int64_t)c->n_cu, c->stream));
     } else {
-        if (!fused) c->path[0]++;
-        HIPCHK(launch_tile(P, c->d_hist, c->ref, c->ref_len, c->tables, c->acc, R.lpc, tile_blocks(c, R.lpc, fused, K == 1), fused,
-                           c->stream));
+        c->path[0]++;
+        HIPCHK(launch_tile(P, c->d_hist, c->ref, c->ref_len, c->tables, c->acc, R.lpc, tile_blocks(c, R.lpc, K == 1), c->stream));
         if (use_part) HIPCHK(launch_merge(P, c->ref, c->acc, c->stream));
     }
     if (int rc = trace_sync(c, lite ? "accumulate (k_acc_lite)" : "accumulate (k_acc_tile)")) return rc;
@@ -885,22 +884,10 @@ static int materialize(spg_ctx *c) {
     return rc;
 }
 
-// split count of a run, as flush_run computes it
-static int64_t run_splits(const spg_ctx *c, int64_t h0, int64_t h1) {
-    int64_t u0 = INT64_MAX, u1 = INT64_MIN;
-    uint64_t e = 0;
-    for (int64_t i = h0; i < h1; i++) {
-        u0 = std::min(u0, c->hist[(size_t)i].pos_begin);
-        u1 = std::max(u1, c->hist[(size_t)i].pos_begin + c->hist[(size_t)i].n_cols);
-        e += c->hist[(size_t)i].n_entries;
-    }
-    return plan_run(c, h0, h1, u0, u1, e).S;
-}
-
 // Counted mode (count_pending) may take a calls-only sample of shallow single-sample batches whose records are
 // not needed as they stand: none written yet (pend0 == 0), or stale (a fused finalize or counted mode left them
-// unwritten; counting reads the history, not the records).  vc_queue.py:142-144 finalizes after every BAM: the
-// first BAM's finalize is fused (k_acc_lite / k_acc_tile FUSED), every later one counts.
+// unwritten; counting reads the history, not the records).  vc_queue.py:142-144 finalizes after every BAM: each
+// finalize counts (a lone chr1-like batch of <= 40 entries per column takes k_acc_lite instead).
 static bool countable(const spg_ctx *c) {
     return (c->p.flags & SPG_P_CALLS_ONLY) && c->n_deep_hist == 0 && !c->deep_pend &&
            (c->counted || c->stale || c->pend0 == 0);
@@ -1525,9 +1512,12 @@ static int finalize_impl(spg_ctx *c, bool table) {
     const bool fused_deep = !table && c->deep_pend && nh == 1;
     if (!fused_deep)
         if (int rc = flush_deep(c)) return rc;
-    const bool counted = !fused_deep && !table && nh >= 2 && countable(c);
-    const bool fused = !counted && !fused_deep && !table && (c->p.flags & SPG_P_CALLS_ONLY) && c->pend0 == 0 &&
-                       nh > 0 && run_splits(c, 0, nh) == 1;
+    // a calls-only sample of shallow batches is counted — except a lone batch of <= 40 entries per column (chr1 30x:
+    // one process_bam then prepare_variants), which k_acc_lite counts and folds in one pass
+    const bool lone_lite = nh == 1 && c->pend0 == 0 &&
+                           (double)c->hist[0].n_entries <= 40.0 * (double)std::max<int64_t>(1, c->hist[0].n_cols);
+    const bool counted = !fused_deep && !table && nh >= 1 && !lone_lite && countable(c);
+    const bool fused = !counted && !fused_deep && !table && (c->p.flags & SPG_P_CALLS_ONLY) && lone_lite;
     if (fused_deep) {
         c->deep_pend = false;
         c->path[5]++;

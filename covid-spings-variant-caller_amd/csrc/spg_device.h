@@ -145,9 +145,9 @@ struct MParams {             // one run-kernel launch: history batches [h0, h0 +
     uint32_t *err;           // bit 0: a 64-column window of a run's batch held >= 2^30 entries (not run)
     uint32_t *deep_list;     // K == 1: columns with >= t_deep entries, listed for k_acc_seg<1> ...
     uint32_t *deep_n;        // ... and their count
-    // FUSED (a FRESH run folded at spg_finalize, calls-only): a record is written only for positions that
-    // can produce a call (prepare_variants' filters :131, :151-157) or need the exact replay; they are
-    // listed for the sparse finalize
+    // fused (k_acc_lite: a lone FRESH shallow batch folded at spg_finalize, calls-only) and counted mode
+    // (k_count_list): a record is written only for positions that can produce a call (prepare_variants' filters
+    // :131, :151-157) or need the exact replay; they are listed for the sparse finalize
     int32_t min_td, min_ad;
     double ratio_lo;         // min_evidence_ratio * (1 - 1e-9): the conservative AD/DP pre-check
     int64_t *list;           // positions whose record was written (the sparse finalize's input)

@@ -110,7 +110,7 @@ struct TLane { uint32_t b, e, rc; };          // column bytes [b, e) relative to
                                               // 0x100 column in range | 0x200 deep (listed for k_acc_seg<1>)
 struct TSeg { uint64_t wb; uint32_t nb; };    // unit's byte range base and length
 
-template <int LPC, bool FUSED, bool ONE>
+template <int LPC, bool ONE>
 #ifndef SPG_TILE_WPE
 #define SPG_TILE_WPE 2       // waves per SIMD the register allocation must allow (2: 256 VGPRs, no spills)
 #endif
@@ -139,10 +139,6 @@ __global__ __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(SPG_TIL
         if constexpr (ONE) { (void)k; return hone; }
         else return H[P.h0 + k];
     };
-    // LITE (the fused form of one shallow BAM, LPC = 1: chr1 30x): the loop only counts — totalDepth and the
-    // entries per allele, what prepare_variants' filters (:131, :151-157) read; a column that may call is then
-    // folded again exactly from the slot (its blocks are still there), every statistic included
-    constexpr bool LITE = FUSED && ONE && LPC == 1;
 
     auto next_unit = [&](TUnit u) -> TUnit {
         if (u.s >= P.S) return u;
@@ -299,13 +295,7 @@ __global__ __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(SPG_TIL
         const int64_t g = U0.g;
         const int32_t k0 = U0.s * P.kper, k1 = min(P.K, k0 + P.kper);
         if (U0.k == k0) {
-            if constexpr (LITE) {                        // the counts are all the loop keeps
-                drare = n_del = n_skip = n_other = 0; fb = INF32; sidx = 0; mcf = 0;
-#pragma unroll
-                for (int kk = 0; kk < NSLOT; kk++) cc[kk] = 0;
-            } else {
-                reset_state();
-            }
+            reset_state();
         }
         const int64_t p = P.u0 + g * TC + cl;
         const bool inr = (L0.rc & 0x100u) != 0;
@@ -320,8 +310,8 @@ __global__ __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(SPG_TIL
         const bool msum = !P.calls_only || nibble_char(M) != refc;
         const bool any_msum = __ballot(msum && inr) != 0;
         const bool rsl = !msum && P.ref_sl;
-        // REF sums in a shallow calls-only run: accumulated in the loop (LITE: in the exact re-fold)
-        const bool any_rsl = !LITE && __ballot(rsl && inr) != 0;
+        // REF sums in a shallow calls-only run: accumulated in the loop
+        const bool any_rsl = __ballot(rsl && inr) != 0;
         const bool deep = (L0.rc & 0x200u) != 0;
         const uint32_t len = L0.e - L0.b;
         if (P.deep_list) {                               // long columns of a single batch: k_acc_seg<1>
@@ -343,7 +333,7 @@ __global__ __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(SPG_TIL
         uint32_t lsq = 0, lgsq = 0;
         const uint32_t cbase = dslot0 + (uint32_t)sp * (2 * TCAP);
         // the REF allele's LUT sums: non-REF major (msum) or a shallow calls-only run's REF (rsl)
-        bool msl_on = msum || (!LITE && rsl);
+        const bool msl_on = msum || rsl;
         // One 16-B block of the lane's column: SWAR classes of its four dwords (REF allele; the second allele
         // when DUAL), counts / sum(q) / LUT sums; the first-entry and exact paths run only for lanes that need
         // them (divergent branches taken once per block, not per dword).  SUMS / DUAL: wave-uniform, hoisted.
@@ -457,53 +447,7 @@ __global__ __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(SPG_TIL
         };
         using T_ = std::true_type;
         using F_ = std::false_type;
-        // LITE: counts only (REF fast entries by popcount; every other entry into its slot's count)
-        auto lite = [&](const u32x4 &cw, const u32x4 &qw, int32_t x0, int32_t vlen) {
-            uint32_t vm[4];
-            valid_masks<4>(x0, 0, vlen, vm);
-#pragma unroll
-            for (int d = 0; d < 4; d++) {
-                const uint32_t c_ = dw<4>(cw, d), q_ = dw<4>(qw, d);
-                uint32_t f80, r80;
-                swar4(c_, q_, vm[d], mrep, P.kpass, P.kok, f80, r80);
-                mcf += __popc(f80);
-                while (r80) {
-                    const int sh = __builtin_ctz(r80) - 7;
-                    r80 &= r80 - 1;
-                    const uint32_t c = (c_ >> sh) & 0xFFu, q = (q_ >> sh) & 0xFFu;
-                    if ((int)q < P.min_bq) continue;
-                    drare++;
-                    const int s = slot_of(c);
-                    n_del += c == SPG_CODE_DEL ? 1u : 0u;
-                    n_skip += c == SPG_CODE_SKIP ? 1u : 0u;
-                    n_other += (s < 0 && c < 16u) ? 1u : 0u;
-#pragma unroll
-                    for (int kk = 0; kk < NSLOT; kk++) cc[kk] += kk == s ? 1u : 0u;
-                }
-            }
-        };
-        if constexpr (LITE) {
-            for (uint32_t t = 0; t < mx; t++) {
-                const uint32_t blk = j0 + (uint32_t)sub + LPC * t;
-                u32x4 cw, qw;
-                slot_blk(cbase + 16u * min(blk, TNBLK - 1u), cw, qw);
-                lite(cw, qw, (int32_t)(16u * blk) - (int32_t)L0.b, vlen_l);
-            }
-            if (any_ovf) {
-                const Hist hb = hist(U0.k);
-                const __amdgpu_buffer_rsrc_t oc = rsrc_u(hb.code + G0.wb, (G0.nb + 15u) & ~15u);
-                const __amdgpu_buffer_rsrc_t oq = rsrc_u(hb.qual + G0.wb, (G0.nb + 15u) & ~15u);
-                const uint32_t f0 = max(j0, TNBLK);
-                const uint32_t no = ovf && j1 > f0 ? j1 - f0 : 0u;
-                const uint32_t mo = wave_max_u32(no);
-                for (uint32_t t = 0; t < mo; t++) {
-                    const uint32_t o = t < no ? 16u * (f0 + t) : 0x80000000u;
-                    const u32x4 cw = __builtin_amdgcn_raw_buffer_load_b128(oc, (int)o, 0, 0);
-                    const u32x4 qw = __builtin_amdgcn_raw_buffer_load_b128(oq, (int)o, 0, 0);
-                    lite(cw, qw, (int32_t)(16u * (f0 + t)) - (int32_t)L0.b, (int32_t)len);
-                }
-            }
-        } else {
+        {
             const bool any_sums = any_msum || any_rsl;
             if (any_gon) { if (any_sums) run(T_{}, T_{}); else run(F_{}, T_{}); }
             else { if (any_sums) run(T_{}, F_{}); else run(F_{}, F_{}); }
@@ -512,46 +456,10 @@ __global__ __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(SPG_TIL
         gsq = sat_add31(gsq, lgsq);
         sidx += len;
 
-        bool item_end = U0.k + 1 == k1;
-        if constexpr (LITE) {
-            if (item_end) {
-                // prepare_variants' filters on the counts (:131, :151-157; an exotic allele: exact replay)
-                const uint32_t dl = mcf + drare;
-                bool mc = n_other != 0;
-                if (!mc && (int64_t)dl >= (int64_t)P.min_td) {
-                    const double dlo = (double)dl * P.ratio_lo;
-#pragma unroll
-                    for (int kk = 0; kk < NSLOT; kk++) {
-                        const uint32_t n = cc[kk] + (kk == Ms ? mcf : 0u);
-                        mc |= n != 0 && refc != nibble_char(slot_code(kk)) && (int64_t)n >= P.min_ad && (double)n >= dlo;
-                    }
-                }
-                const bool want = inr && (deep || (fb != INF32 && mc));
-                item_end = __ballot(want) != 0;
-                if (item_end) {
-                    // the exact fold of this wave's columns (K = 1: the unit is the item), REF sums included
-                    reset_state();
-                    if (len) fb = (uint32_t)U0.k;
-                    msl_on = msum || rsl;
-                    lsq = lgsq = 0;
-                    if (__ballot(want && msl_on)) run(T_{}, F_{}); else run(F_{}, F_{});
-                    msq = sat_add31(msq, lsq);
-                }
-            }
-        }
+        const bool item_end = U0.k + 1 == k1;
         const uint32_t depth = grp_add<LPC>(mcf + gcf + drare);
         const uint32_t mcf_c = grp_add<LPC>(mcf);
         const uint32_t no_ = grp_add<LPC>(n_other);
-        if (FUSED && !LITE && item_end) {
-            // most columns of a fused run cannot call (prepare_variants' filters :131, :151-157, on a bound: every
-            // entry that is not a fast REF entry in one allele) and write nothing: when no lane of the wave can,
-            // the item end is skipped entirely
-            const uint32_t cand_max = depth - (msum ? 0u : mcf_c);
-            const bool could = inr && (deep || (fb != INF32 && (no_ != 0 ||
-                               ((int64_t)depth >= (int64_t)P.min_td && (int64_t)cand_max >= (int64_t)P.min_ad &&
-                                (double)cand_max >= (double)depth * P.ratio_lo))));
-            item_end = __ballot(could) != 0;
-        }
         if (item_end) {
             // ================= item end: fold the allele states into per-slot arrays =================
             const uint32_t nd = grp_add<LPC>(n_del), ns = grp_add<LPC>(n_skip);
@@ -612,26 +520,6 @@ __global__ __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(SPG_TIL
                 // composed straight from the per-slot arrays.  (every lane of a column holds the column's totals:
                 // they agree on want / write)
                 bool write = inr && !deep && fbi != INF32;
-                if constexpr (FUSED) {
-                    bool mc = no_ != 0;                  // prepare_variants' filters (may_call, :131, :151-157)
-                    if (!mc && (int64_t)depth >= (int64_t)P.min_td) {
-                        const double dlo = (double)depth * P.ratio_lo;
-#pragma unroll
-                        for (int kk = 0; kk < NSLOT; kk++)
-                            mc |= cc[kk] != 0 && refc != nibble_char(slot_code(kk)) && (int64_t)cc[kk] >= P.min_ad &&
-                                  (double)cc[kk] >= dlo;
-                    }
-                    const bool want = inr && (deep || (fbi != INF32 && mc));
-                    const uint64_t wm = __ballot(want && sub == 0);
-                    if (wm) {
-                        uint32_t at = 0;
-                        if (lane == 0) at = atomicAdd(P.n_list, (uint32_t)__popcll(wm));
-                        at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
-                        if (want && sub == 0)
-                            P.list[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u))] = p;
-                    }
-                    write = write && want;
-                }
                 if (write && sub == 0) {
                     // merge_state into an empty record of this epoch: first visit (:77-85), totalDepth (:87), the
                     // slots present with their sums, dict order by first entry (:100-101); absent slots stay 0
@@ -677,9 +565,8 @@ __global__ __launch_bounds__(64 * TW) __attribute__((amdgpu_waves_per_eu(SPG_TIL
 
 // Resident workgroups per CU of a k_acc_tile instantiation (the occupancy API; the grid never exceeds what is
 // resident, or the waves of a second generation would start after the first has streamed its units)
-static const void *tile_fn(int lpc, bool fused, bool one) {
-#define SPG_TF(L) (fused ? (one ? (const void *)k_acc_tile<L, true, true> : (const void *)k_acc_tile<L, true, false>) \
-                         : (one ? (const void *)k_acc_tile<L, false, true> : (const void *)k_acc_tile<L, false, false>))
+static const void *tile_fn(int lpc, bool one) {
+#define SPG_TF(L) (one ? (const void *)k_acc_tile<L, true> : (const void *)k_acc_tile<L, false>)
     switch (lpc) {
         case 1: return SPG_TF(1);
         case 2: return SPG_TF(2);
@@ -690,18 +577,18 @@ static const void *tile_fn(int lpc, bool fused, bool one) {
 #undef SPG_TF
 }
 
-int tile_blocks_per_cu(int lpc, bool fused, bool one) {
-    static int cache[2][2][9] = {};
-    int &c = cache[fused ? 1 : 0][one ? 1 : 0][lpc];
+int tile_blocks_per_cu(int lpc, bool one) {
+    static int cache[2][9] = {};
+    int &c = cache[one ? 1 : 0][lpc];
     if (c) return c;
     int n = 0;
-    const void *f = tile_fn(lpc, fused, one);
+    const void *f = tile_fn(lpc, one);
     if (!f || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 64 * TW, 0) != hipSuccess || n <= 0) n = 4;
     return c = n;
 }
 
 hipError_t launch_tile(const MParams &P, const Hist *H, const uint8_t *ref, int64_t ref_len, const Tables *T, Acc *acc,
-                       int lpc, int64_t max_blocks, bool fused, hipStream_t st) {
+                       int lpc, int64_t max_blocks, hipStream_t st) {
     const int64_t items = (int64_t)P.n_groups * P.S;
     if (items == 0) return hipSuccess;
     if (items >= (1ll << 31)) return hipErrorInvalidValue;     // the kernel's item cursor is 32-bit
@@ -709,10 +596,8 @@ hipError_t launch_tile(const MParams &P, const Hist *H, const uint8_t *ref, int6
 #define SPG_TILE(L)                                                                                                  \
     do {                                                                                                             \
         const dim3 g_((unsigned)blocks), b_(64 * TW);                                                                \
-        if (fused && one) hipLaunchKernelGGL((k_acc_tile<L, true, true>), g_, b_, 0, st, P, H, ref, ref_len, T, acc);     \
-        else if (fused) hipLaunchKernelGGL((k_acc_tile<L, true, false>), g_, b_, 0, st, P, H, ref, ref_len, T, acc);      \
-        else if (one) hipLaunchKernelGGL((k_acc_tile<L, false, true>), g_, b_, 0, st, P, H, ref, ref_len, T, acc);        \
-        else hipLaunchKernelGGL((k_acc_tile<L, false, false>), g_, b_, 0, st, P, H, ref, ref_len, T, acc);                \
+        if (one) hipLaunchKernelGGL((k_acc_tile<L, true>), g_, b_, 0, st, P, H, ref, ref_len, T, acc);               \
+        else hipLaunchKernelGGL((k_acc_tile<L, false>), g_, b_, 0, st, P, H, ref, ref_len, T, acc);                  \
     } while (0)
     const bool one = P.K == 1;
     switch (lpc) {

@@ -280,7 +280,7 @@ int spg_kernel_times(spg_ctx *ctx, float *accumulate_ms, float *finalize_ms, int
  *   out[1] re-materializations (records a fused / counted finalize left stale, re-folded from batch 0)
  *   out[2] full-range finalizes (k_finalize over every position)      out[3] sparse finalizes (listed positions)
  *   out[4] counted finalizes (k_acc_lite_run + k_count_list + k_fold_hist)
- *   out[5] fused deep finalizes (k_acc_seg FUSE)                         out[6] fused shallow finalizes
+ *   out[5] fused deep finalizes (k_acc_seg FUSE, or list mode)           out[6] fused shallow finalizes (k_acc_lite)
  *   out[7] batches counted by k_acc_lite_run
  * Writes min(n, 8) values. */
 int spg_path_counters(spg_ctx *ctx, int64_t *out, int64_t n);

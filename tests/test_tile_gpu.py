@@ -4,8 +4,8 @@ k_acc_tile folds one shallow batch (process_bam's columns, live_variant_caller.p
 them (many BAMs into one `memory`, vc_queue.py:142-144): LDS-DMA tile staging, LPC lanes per column
 (1, 2, 4, 8 by the batch's mean depth), the tile bytes past the 2 KiB slot read from memory, runs split
 over batch ranges.  Each case here drives one of those shapes and compares memory (counts, dict order,
-first visits) and the call table with the oracle; calls-only single batches take the fused form (records
-only for positions that may call, then the sparse finalize).
+first visits) and the call table with the oracle; calls-only contexts decide their calls without it (k_acc_lite for a
+lone batch of <= 40 entries per column, else counted mode) and re-materialize every record through it for the table.
 """
 import numpy as np
 import pytest
