@@ -869,8 +869,89 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
     }
     int64_t last_pos = -1;
     static const bool timing = getenv("SPP_TIMING") != nullptr;
+    static const bool par_scan = [] { const char *e = getenv("SPP_PAR_SCAN"); return !e || atoi(e) != 0; }();
     const auto t0 = std::chrono::steady_clock::now();
-    while (avail_to(cur + 4)) {
+    // Record boundaries in parallel: the inflated stream (once every member is in) split into nt ranges; each range's
+    // first record is found by a validated chain — a block_size hop whose fixed fields are plausible (refIDs in range,
+    // lengths inside block_size, a NUL-terminated name) eight records in a row — the ranges are scanned at once, and
+    // the chains must meet exactly (each range's scan ends on the next range's start).  Otherwise (a false start
+    // inside a record, a damaged file) the serial scan below walks the stream from the header, as before.
+    bool scanned = false;
+    const size_t body = cur;
+    if (par_scan && nt > 1 && nb > 0 && total > body + ((size_t)nt << 20) && avail_to(total)) {
+        auto rec_len = [&](size_t x) -> size_t {        // plausible record at x: 4 + block_size, else 0
+            if (x + 40 > total) return 0;
+            const uint32_t bs = rdu32(buf + x);
+            if (bs < 32 || bs > (1u << 26) || x + 4 + (size_t)bs > total) return 0;
+            const uint8_t *b = buf + x + 4;
+            const int32_t ref = rd32(b), mref = rd32(b + 20), pos = rd32(b + 4);
+            if (ref < -1 || ref >= n_ref || mref < -1 || mref >= n_ref || pos < -1) return 0;
+            const uint32_t l_name = b[8], n_cig = rdu16(b + 12);
+            const int32_t l_seq = rd32(b + 16);
+            if (l_name < 1 || l_seq < 0 || 32ull + l_name + 4ull * n_cig + ((uint64_t)l_seq + 1) / 2 + (uint64_t)l_seq > bs)
+                return 0;
+            if (b[32 + l_name - 1] != 0) return 0;
+            return 4 + (size_t)bs;
+        };
+        const int np = nt;
+        std::vector<size_t> start((size_t)np + 1, total);
+        start[0] = body;
+        par_chunks((size_t)np, np, [&](int, size_t t0_, size_t t1_) {
+            for (size_t t = std::max<size_t>(t0_, 1); t < t1_; t++) {
+                const size_t b0 = body + (total - body) * t / (size_t)np, lim = std::min(total, b0 + ((size_t)1 << 20));
+                for (size_t x = b0; x < lim; x++) {
+                    size_t y = x;
+                    int k = 0;
+                    for (; k < 8 && y < total; k++) {
+                        const size_t len = rec_len(y);
+                        if (!len) break;
+                        y += len;
+                    }
+                    if (k == 8 || y == total) { start[t] = x; break; }
+                }
+            }
+        });
+        for (int t = np - 1; t >= 1; t--) start[(size_t)t] = std::min(start[(size_t)t], start[(size_t)t + 1]);
+        std::vector<Vec<uint64_t>> part((size_t)np);
+        std::vector<int64_t> first_pos((size_t)np, INT64_MAX), last_p((size_t)np, -1);
+        std::atomic<bool> ok{true}, unsorted{false};
+        par_chunks((size_t)np, np, [&](int, size_t t0_, size_t t1_) {
+            for (size_t t = t0_; t < t1_; t++) {
+                size_t q = start[t];
+                int64_t lp = -1;
+                while (q < start[t + 1]) {
+                    const uint32_t bs = rdu32(buf + q);
+                    if (bs < 32 || q + 4 + (size_t)bs > total) { ok = false; break; }
+                    const uint8_t *b = buf + q + 4;
+                    if (rd32(b) == tid) {
+                        const int64_t pos = rd32(b + 4);
+                        if (pos < lp) unsorted = true;
+                        if (first_pos[t] == INT64_MAX) first_pos[t] = pos;
+                        lp = pos;
+                        if (stepper_keeps(p, rdu16(b + 14), b[9])) part[t].push_back(q + 4);
+                    }
+                    q += 4 + (size_t)bs;
+                }
+                last_p[t] = lp;
+                if (q != start[t + 1]) ok = false;
+            }
+        });
+        if (ok) {
+            for (int t = 0; t < np; t++) {
+                if (first_pos[(size_t)t] != INT64_MAX && first_pos[(size_t)t] < last_pos) unsorted = true;
+                if (last_p[(size_t)t] >= 0) last_pos = last_p[(size_t)t];
+            }
+            if (unsorted) throw std::runtime_error("BAM is not coordinate-sorted");
+            size_t nrec = 0;
+            for (auto &v : part) nrec += v.size();
+            R.rec.resize(nrec);
+            size_t at = 0;
+            for (auto &v : part) { if (!v.empty()) memcpy(R.rec.data() + at, v.data(), v.size() * sizeof(uint64_t)); at += v.size(); }
+            cur = total;
+            scanned = true;
+        }
+    }
+    while (!scanned && avail_to(cur + 4)) {
         const uint32_t bs = rdu32(buf + cur);
         if (bs < 32 || !avail_to(cur + 4 + (size_t)bs)) throw std::runtime_error("truncated BAM record");
         const uint8_t *b = buf + cur + 4;

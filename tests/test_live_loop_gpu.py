@@ -42,7 +42,8 @@ def test_finalize_after_every_bam_300_vs_oracle():
         compare_variants(got, want, rtol=RTOL)
         n_band_seen += eng.counts()[1] > 0
     pc = eng.path_counters()
-    assert pc["counted_finalizes"] == 300 and pc["fused_shallow_finalizes"] == 0, pc
+    # (BAM 1, a lone batch of <= 40 entries per column, may take k_acc_lite; every later finalize counts)
+    assert pc["counted_finalizes"] + pc["fused_shallow_finalizes"] == 300 and pc["counted_finalizes"] >= 299, pc
     assert pc["record_runs"] == 0, pc                                # no k_acc_tile fold of the records
     assert pc["materializations"] == 0 and pc["full_finalizes"] == 0, pc
     assert pc["batches_counted"] == 300, pc                          # every BAM counted once

@@ -191,3 +191,45 @@ def test_records_fill_refused(tmp_path):
         with pytest.raises(RuntimeError, match="filled on the GPU"):
             b.fill()
         b.close()
+
+
+_SCAN_CHILD = r"""
+import sys, hashlib, numpy as np
+sys.path.insert(0, sys.argv[1])
+import spings
+from covid_spings_variant_caller_amd.pileup import AlignmentFile, PileupParams
+from test_records_plan import _arr
+with AlignmentFile(sys.argv[2]) as f:
+    b = f.pileup_records(sys.argv[3], PileupParams(n_threads=8, max_depth=int(sys.argv[4])))
+r = b.records()
+h = hashlib.sha256()
+for a in (_arr(r.offsets, r.n_cols + 1, np.uint64), _arr(r.rec, r.n_reads, np.uint64), _arr(r.rpos, r.n_reads, np.int32),
+          _arr(r.rend, r.n_reads, np.int32), _arr(r.tweak, r.n_reads, np.int32)):
+    h.update(a.tobytes())
+print(r.pos_begin, r.n_cols, r.n_entries, r.n_reads, h.hexdigest())
+"""
+
+
+@pytest.mark.parametrize("max_depth", [8000, 0])
+def test_parallel_record_scan_equals_serial(tmp_path, max_depth):
+    """The records plan's record boundaries found in parallel (validated chains per range that must meet exactly,
+    csrc/spp_pileup.cpp read_bam_raw) give the plan the serial block_size walk gives (SPP_PAR_SCAN=0): a BAM of
+    ~80 MB inflated (2,000x over 30 kb, 150-bp reads with D/I), 8 threads."""
+    import os
+    import subprocess
+    import sys
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.pileup import simulate_bam
+    bam = str(tmp_path / "p.bam")
+    simulate_bam(bam, "NC_045512.2", synth.reference(29903, seed=1), depth=2000, seed=9, n_threads=8)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = {}
+    for par in ("1", "0"):
+        env = dict(os.environ, SPP_PAR_SCAN=par, PYTHONPATH=here)
+        r = subprocess.run([sys.executable, "-c", _SCAN_CHILD, root, bam, "NC_045512.2", str(max_depth)], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        out[par] = r.stdout.strip().splitlines()[-1]
+    assert out["1"] == out["0"]
+    assert int(out["1"].split()[3]) > 300_000
