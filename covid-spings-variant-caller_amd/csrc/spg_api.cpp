@@ -27,6 +27,9 @@ hipError_t launch_lite_fold(const MParams &P, const Hist &hb, const uint8_t *ref
 hipError_t launch_count_run(const MParams &P, const Hist *H, const uint8_t *ref, uint32_t *cdep, uint32_t *cmcf, int lpc,
                             int64_t blocks, hipStream_t st);
 int count_run_blocks_per_cu(int lpc);
+hipError_t launch_count_cols(const MParams &P, const Hist &hb, const uint8_t *ref, uint32_t *dlist, int lpc, int64_t blocks,
+                             hipStream_t st);
+int count_cols_blocks_per_cu(int lpc);
 hipError_t launch_count_list(const MParams &P, const uint8_t *ref, const uint32_t *cdep, const uint32_t *cmcf, hipStream_t st);
 hipError_t launch_fold_hist(const MParams &P, const Hist *H, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
                             void *part, uint32_t *arrived, int bpp, int cap, hipStream_t st);
@@ -171,6 +174,7 @@ struct spg_ctx {
     int64_t deep_cap = 0;
     uint32_t *deep_n = nullptr;         // ... and their count
     bool stale = false;                 // records of history [0, stale_end) not written (fused run)
+    bool stale_deep = false;            // ... the stale history is the sample's lone deep batch (k_count_cols)
     bool deep_pend = false;             // history batch 0 is a deep batch not accumulated yet: a calls-only
                                         // finalize runs it fused (k_acc_seg<..., FUSE>), anything else first
                                         // accumulates it on its own
@@ -234,7 +238,7 @@ struct spg_ctx {
     bool table_valid = false;           // the SoA table matches the last finalize
     int timing = default_timing();
     int acc_timing = 0;                 // level the open / last accumulate interval was recorded at
-    int64_t path[8] = {};               // spg_path_counters
+    int64_t path[9] = {};               // spg_path_counters
 };
 
 
@@ -380,6 +384,7 @@ int spg_reset(spg_ctx *c) {
     if (!c) return fail("spg_reset: null ctx");
     HIPCHK(hipSetDevice(c->device));
     c->stale = false;
+    c->stale_deep = false;
     c->deep_pend = false;
     c->counted = false;
     c->count_end = 0;
@@ -587,7 +592,7 @@ static void fill_swar(const spg_ctx *c, int32_t &min_bq, int32_t &qlo, uint32_t 
 // k_acc_seg over one batch (every column of a deep batch; the long columns of a shallow one).  F/O:
 // fused with the calls-only finalize (FRESH deep batch, the sample's only one).
 static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F = nullptr, const Out *O = nullptr,
-                      bool listed = false, bool *list_mode = nullptr) {
+                      bool listed = false, bool *list_mode = nullptr, uint32_t t_listed = 128u) {
     if (list_mode) *list_mode = false;
     const HistBatch &hb0 = c->hist[(size_t)idx];
     static const int64_t target_waves = env_i64("SPG_TARGET_WAVES", 16384);
@@ -673,7 +678,8 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
         P.min_ad = c->p.min_allele_depth;
         P.ratio_lo = c->p.min_evidence_ratio * (1.0 - 1e-9);
     }
-    if (listed) {                 // the long columns the run kernel listed, one per wave
+    if (listed) {                 // the long columns the run kernel listed (k_count_cols: every listed column), one per wave
+        P.t_deep = t_listed;
         P.G = 1;
         P.G2 = 1;
         P.deep_list = c->deep_list;
@@ -877,6 +883,18 @@ static int materialize(spg_ctx *c) {
     c->stale = false;
     c->counted = false;            // the records hold history [0, stale_end) again; pending batches fold into them
     c->path[1]++;
+    if (c->stale_deep) {           // the lone deep batch k_count_cols counted: every column through k_acc_seg
+        c->stale_deep = false;
+        if (int rc = wait_copies(c)) return rc;
+        if (int rc = acc_begin(c)) return rc;
+        if (int rc = launch_seg(c, 0, true)) return rc;
+        // the listed columns' records again through k_acc_seg<1> (deep_list / deep_n still hold count_cols' list:
+        // nothing lists between it and this materialize), so every later finalize reads the very records (fp64
+        // sums in the same order) the sparse finalize after the count read: calls stay bit-identical across
+        // finalizes, as the reference's prepare_variants over an unchanged memory
+        if (int rc = launch_seg(c, 0, false, nullptr, nullptr, true, nullptr, 1u)) return rc;
+        return acc_end(c);
+    }
     const int64_t keep = c->pend0;
     c->pend0 = 0;
     const int rc = flush_run(c, c->stale_end, false);
@@ -1482,6 +1500,62 @@ static int finalize_counted(spg_ctx *c) {
 
 static int finalize_impl(spg_ctx *c, bool table);
 
+// k_count_cols' lanes per column for the sample's lone deep batch (0: the fused k_acc_seg takes it).  Mid-depth
+// single-sample batches (mean column < 4,096 entries, e.g. 1,000x) are counted: the fused kernel's waves would own
+// more columns than its finishing ring holds, and its per-column work dominates at one or two chunks a column.
+// SPG_COUNT_COLS=0 disables, =1 takes every lone deep batch (A/B; 10,000x: 127 us vs the fused kernel's 111 us).
+// LPC: two or three 16-B blocks per lane (SPG_COUNT_LPC forces one: tests).
+static int mid_count_lpc(const spg_ctx *c) {
+    static const int mode = [] { const char *e = getenv("SPG_COUNT_COLS"); return e ? atoi(e) : -1; }();
+    if (mode == 0 || c->hist.empty()) return 0;
+    const HistBatch &b = c->hist[0];
+    if (b.n_samples != 1 || b.fsamp || b.n_cols == 0) return 0;
+    const double mean = (double)b.n_entries / (double)b.n_cols;
+    if (mode != 1 && mean >= 4096.0) return 0;
+    const int64_t force = env_i64("SPG_COUNT_LPC", 0);          // (read per call: tests switch it)
+    if (force == 4 || force == 8 || force == 16 || force == 32 || force == 64) return (int)force;
+    int lpc = 4;                        // (1,000x: LPC 32, two rounds: 0.683 ms vs 0.714 ms for LPC 16, r04l)
+    while (lpc < 64 && mean / 16.0 / lpc > 2.5) lpc *= 2;
+    return lpc;
+}
+
+// The lone deep batch of a calls-only sample at its finalize, counted (mid_count_lpc): k_count_cols lists the positions
+// whose counts pass prepare_variants' filters (band: positions; deep_list: columns; deep_n: their number), then
+// k_acc_seg<1> builds exactly those records (FRESH).  The batch's records are left stale.
+static int count_cols(spg_ctx *c) {
+    const HistBatch &hb = c->hist[0];
+    const int lpc = mid_count_lpc(c);
+    if (hb.n_cols > c->deep_cap) {
+        if (c->deep_list) { HIPCHK(hipStreamSynchronize(c->stream)); HIPCHK(hipFree(c->deep_list)); }
+        c->deep_list = nullptr;
+        c->deep_cap = 0;
+        HIPCHK(hipMalloc(&c->deep_list, sizeof(uint32_t) * hb.n_cols));
+        c->deep_cap = hb.n_cols;
+    }
+    if (int rc = wait_copies(c)) return rc;
+    if (int rc = acc_begin(c)) return rc;
+    HIPCHK(hipMemsetAsync(c->deep_n, 0, sizeof(uint32_t), c->stream));
+    MParams P{};
+    fill_swar(c, P.min_bq, P.qlo, P.kpass, P.kok);
+    P.epoch = c->epoch;
+    P.calls_only = 1u;
+    P.min_td = c->p.min_total_depth;
+    P.min_ad = c->p.min_allele_depth;
+    P.ratio_lo = c->p.min_evidence_ratio * (1.0 - 1e-9);
+    P.list = c->band;
+    P.n_list = c->deep_n;
+    const int64_t blocks = (int64_t)c->n_cu * count_cols_blocks_per_cu(lpc);
+    HIPCHK(launch_count_cols(P, c->h_hist[0], c->ref, c->deep_list, lpc, blocks, c->stream));
+    if (int rc = trace_sync(c, "accumulate (k_count_cols)")) return rc;
+    // the listed columns' records (every listed column, whatever its length: t_deep 1)
+    if (int rc = launch_seg(c, 0, false, nullptr, nullptr, true, nullptr, 1u)) return rc;
+    if (int rc = acc_end(c)) return rc;
+    c->stale = true;
+    c->stale_deep = true;
+    c->stale_end = 1;
+    return 0;
+}
+
 // The replay cache for a finalize: a history of >= 16 batches (a live memory) keeps each replayed position's exact
 // fold state, so its next replay folds only the batches added since (RSlot, spg_device.h)
 static int replay_cache(spg_ctx *c, RCache &rc) {
@@ -1545,7 +1619,21 @@ static int finalize_impl(spg_ctx *c, bool table) {
     const int ft = c->timing;
     FParams F = make_fparams(c);
     F.table = table ? 1u : 0u;
-    if (fused_deep) {
+    if (fused_deep && mid_count_lpc(c) > 0) {
+        // a lone mid-depth batch (1,000x): k_count_cols counts every column and lists the positions that may
+        // call, k_acc_seg<1> folds exactly the listed columns' records, the sparse k_finalize decides them; the
+        // other records stay stale (materialize() accumulates the batch through k_acc_seg if anything reads them)
+        if (int rc = count_cols(c)) return rc;
+        if (ft >= 2) HIPCHK(hipEventRecord(ev[2], c->stream));
+        F.list = c->band;
+        F.n_list = c->deep_n;
+        c->path[3]++;
+        c->path[8]++;
+        if (int rc = upload_ridx(c, F.ridx)) return rc;
+        if (int rc = replay_cache(c, F.rc)) return rc;
+        HIPCHK(launch_finalize(F, c->acc, c->tables, make_out(c), c->d_hist, c->stream));
+        if (trace_sync(c, "finalize (sparse, listed by k_count_cols)")) return -1;
+    } else if (fused_deep) {
         // the accumulate interval holds the fused kernel; the finalize interval is empty (list mode: the sparse
         // k_finalize over the positions the accumulate listed)
         const Out O = make_out(c);
@@ -1775,7 +1863,7 @@ int spg_kernel_times(spg_ctx *c, float *acc_ms, float *fin_ms, int64_t cap, int6
 
 int spg_path_counters(spg_ctx *c, int64_t *out, int64_t n) {
     if (!c || (!out && n > 0)) return fail("spg_path_counters: bad argument");
-    for (int64_t i = 0; i < std::min<int64_t>(n, 8); i++) out[i] = c->path[i];
+    for (int64_t i = 0; i < std::min<int64_t>(n, 9); i++) out[i] = c->path[i];
     return 0;
 }
 

@@ -1200,7 +1200,7 @@ hipError_t launch_accumulate(const KParams &P, const uint64_t *off, const uint8_
     const int64_t blocks = P.deep_n ? std::min<int64_t>((P.n_cols + KW - 1) / KW, 2048)
                                     : (waves + KW - 1) / KW;
     const bool fresh = P.batch_seq == 1;
-    const bool w4 = P.t_deep <= 1;
+    const bool w4 = P.t_deep <= 1 && !P.deep_n;      // (listed columns: W = 1, whatever t_deep)
     if (P.G > (uint32_t)(w4 ? SPG_GMAX_DEEP : SPG_GMAX) || (!P.deep_n && P.G2 > P.G)) return hipErrorInvalidValue;   // coldesc
     // batches far beyond the 256 MiB Infinity Cache stream with non-temporal loads
     const bool nt = 2 * P.n_entries > ((uint64_t)SPG_NT_MIB << 20);

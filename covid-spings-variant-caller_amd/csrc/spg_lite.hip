@@ -310,6 +310,137 @@ __global__ __launch_bounds__(256) void k_lite_fold(MParams P, Hist hb, const uin
     }
 }
 
+// ---------------------------------------------------------------------------------------------------------
+// k_count_cols: the counting pass of a calls-only sample whose only batch is mid-depth (mean column >= 256
+// entries, e.g. 1,000x SARS-CoV-2, BASELINE config 2), finalized once (process_bam then prepare_variants,
+// live_variant_caller.py:54-185).  As k_acc_lite, but for long columns: a wave owns a tile of 64 / LPC consecutive
+// columns and LPC lanes share each column, taking its 16-B blocks round-robin — a column's LPC lanes read LPC x 16
+// contiguous bytes per round and the tile's columns are adjacent, so a wave's loads are a coalesced stream of the
+// tile's bytes with no LDS staging.  U rounds are loaded at once (2U 16-B loads per lane in flight); the kernel
+// needs few registers, so many waves per SIMD keep HBM busy while others count.  Per column the bq-passing
+// entries and the REF-code entries at q 4..127 (SWAR), reduced over its lanes; the positions whose totals pass
+// prepare_variants' filters (:131, :151-157) are listed — the absolute position for the sparse finalize and the
+// batch column for k_acc_seg<1>'s exact fold (the same list index).  No record is written here.
+// ---------------------------------------------------------------------------------------------------------
+template <int LPC, int U>
+__global__ __launch_bounds__(256) void k_count_cols(MParams P, Hist hb, const uint8_t *__restrict__ ref,
+                                                    uint32_t *__restrict__ dlist) {
+    constexpr int TC = 64 / LPC;
+    const int lane = threadIdx.x & 63, sub = lane % LPC, cl = lane / LPC;
+    const int64_t n_tiles = (hb.n_cols + TC - 1) / TC;
+    const int64_t wstride = (int64_t)gridDim.x * 4;
+    const u32x4 *const gc = reinterpret_cast<const u32x4 *>(hb.code);
+    const u32x4 *const gq = reinterpret_cast<const u32x4 *>(hb.qual);
+    // a tile's column header (CSR bounds, REF char), loaded one tile ahead: the data loads of a tile then wait for
+    // one round trip, not two
+    struct Hdr {
+        uint64_t ob, oe;
+        uint32_t rc;
+    };
+    auto header = [&](int64_t t) -> Hdr {
+        const int64_t cc = min(t * TC + cl, hb.n_cols - 1);
+        return Hdr{hb.off[cc], hb.off[cc + 1], (uint32_t)ref[hb.pos_begin + cc]};
+    };
+    int64_t tile = (int64_t)__builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    Hdr nx = header(min(tile, n_tiles - 1));
+    for (; tile < n_tiles; tile += wstride) {
+        const Hdr h = nx;
+        nx = header(min(tile + wstride, n_tiles - 1));
+        asm volatile("" ::: "memory");                  // (issued before this tile's data loads)
+        const int64_t col = tile * TC + cl;
+        const bool inr = col < hb.n_cols;
+        const uint64_t ob = h.ob, oe = h.oe;
+        const uint8_t refc = (uint8_t)h.rc;
+        const uint32_t mrep = code_of_ref(refc) * 0x01010101u;
+        const uint32_t len = inr ? (uint32_t)(oe - ob) : 0u;
+        const uint64_t j0 = ob >> 4;                        // the column's first 16-B block (the arrays are padded)
+        const uint32_t nblk = len ? (uint32_t)(((oe + 15) >> 4) - j0) : 0u;
+        const uint32_t mine = nblk > (uint32_t)sub ? (nblk - (uint32_t)sub + LPC - 1) / LPC : 0u;   // this lane's blocks
+        const uint32_t rounds = wave_max_u32(mine);
+        const int32_t lead = (int32_t)(ob & 15u);
+        uint32_t dep = 0, mcf = 0;
+        for (uint32_t t0 = 0; t0 < rounds; t0 += U) {
+            u32x4 cw[U], qw[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {                   // (blocks past the lane's share reload its first one)
+                const uint32_t t = t0 + (uint32_t)u;
+                const uint64_t j = j0 + (t < mine ? (uint64_t)sub + (uint64_t)LPC * t : 0u);
+                cw[u] = __builtin_nontemporal_load(gc + j);
+                qw[u] = __builtin_nontemporal_load(gq + j);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t t = t0 + (uint32_t)u;
+                if (t >= mine) break;
+                const int32_t x0 = (int32_t)(16u * ((uint32_t)sub + (uint32_t)LPC * t)) - lead;   // entry of the block's byte 0
+                uint32_t vm[4];
+                valid_masks<4>(x0, 0, (int32_t)len, vm);
+#pragma unroll
+                for (int d = 0; d < 4; d++) {
+                    uint32_t f80, r80;
+                    swar4(dw<4>(cw[u], d), dw<4>(qw[u], d), vm[d], mrep, P.kpass, P.kok, f80, r80);
+                    mcf += __popc(f80);
+                    dep += __popc(f80 | r80);
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 1; o < LPC; o <<= 1) {
+            dep += (uint32_t)__shfl_xor((int)dep, o);
+            mcf += (uint32_t)__shfl_xor((int)mcf, o);
+        }
+        // prepare_variants' filters on what the counts bound (as k_acc_lite: non-REF alleles <= dep - mcf; the REF
+        // code's own entries are a candidate when the stored REF char is not its upper-case letter, :151)
+        bool mc = false;
+        if (len && (int64_t)dep >= (int64_t)P.min_td) {
+            const double dlo = (double)dep * P.ratio_lo;
+            const uint32_t nonref = dep - mcf;
+            mc = ((int64_t)nonref >= P.min_ad && (double)nonref >= dlo) ||
+                 (refc != nibble_char(mrep & 0xFFu) && (int64_t)mcf >= P.min_ad && (double)mcf >= dlo);
+        }
+        const bool want = inr && sub == 0 && mc;
+        const uint64_t wm = __ballot(want);
+        if (wm) {
+            uint32_t at = 0;
+            if (lane == 0) at = atomicAdd(P.n_list, (uint32_t)__popcll(wm));
+            at = (uint32_t)__builtin_amdgcn_readfirstlane(at);
+            if (want) {
+                const uint32_t k = at + __builtin_amdgcn_mbcnt_hi((uint32_t)(wm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wm, 0u));
+                P.list[k] = hb.pos_begin + col;
+                dlist[k] = (uint32_t)col;
+            }
+        }
+    }
+}
+
+#define SPG_COUNT_COLS(L) (L == 4 ? (const void *)k_count_cols<4, 4> : L == 8 ? (const void *)k_count_cols<8, 4> \
+                           : L == 16 ? (const void *)k_count_cols<16, 4> : L == 32 ? (const void *)k_count_cols<32, 4> \
+                           : (const void *)k_count_cols<64, 4>)
+int count_cols_blocks_per_cu(int lpc) {
+    static int n[5] = {-1, -1, -1, -1, -1};
+    const int i = lpc == 4 ? 0 : lpc == 8 ? 1 : lpc == 16 ? 2 : lpc == 32 ? 3 : 4;
+    if (n[i] < 0) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, SPG_COUNT_COLS(lpc), 256, 0) != hipSuccess || b < 1) b = 2;
+        n[i] = b;
+    }
+    return n[i];
+}
+hipError_t launch_count_cols(const MParams &P, const Hist &hb, const uint8_t *ref, uint32_t *dlist, int lpc, int64_t blocks,
+                             hipStream_t st) {
+    if (hb.n_cols == 0) return hipSuccess;
+    const dim3 grid((unsigned)std::max<int64_t>(1, blocks)), blk(256);
+    switch (lpc) {
+        case 4: hipLaunchKernelGGL((k_count_cols<4, 4>), grid, blk, 0, st, P, hb, ref, dlist); break;
+        case 8: hipLaunchKernelGGL((k_count_cols<8, 4>), grid, blk, 0, st, P, hb, ref, dlist); break;
+        case 16: hipLaunchKernelGGL((k_count_cols<16, 4>), grid, blk, 0, st, P, hb, ref, dlist); break;
+        case 32: hipLaunchKernelGGL((k_count_cols<32, 4>), grid, blk, 0, st, P, hb, ref, dlist); break;
+        case 64: hipLaunchKernelGGL((k_count_cols<64, 4>), grid, blk, 0, st, P, hb, ref, dlist); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_lite_fold(const MParams &P, const Hist &hb, const uint8_t *ref, const Tables *T, Acc *acc, int64_t blocks,
                             hipStream_t st) {
     hipLaunchKernelGGL(k_lite_fold, dim3((unsigned)std::max<int64_t>(1, blocks)), dim3(256), 0, st, P, hb, ref, T, acc);

@@ -212,13 +212,13 @@ class PileupEngine:
         return a.value, b.value, d.value
 
     PATHS = ("record_runs", "materializations", "full_finalizes", "sparse_finalizes", "counted_finalizes",
-             "fused_deep_finalizes", "fused_shallow_finalizes", "batches_counted")
+             "fused_deep_finalizes", "fused_shallow_finalizes", "batches_counted", "mid_counted_finalizes")
 
     def path_counters(self) -> Dict[str, int]:
         """Which engine paths ran since creation (spg_path_counters)."""
-        a = (C.c_int64 * 8)()
+        a = (C.c_int64 * len(self.PATHS))()
         with self._lock:
-            N.check(self._L.spg_path_counters(self._h, a, 8), "spg_path_counters")
+            N.check(self._L.spg_path_counters(self._h, a, len(self.PATHS)), "spg_path_counters")
         return dict(zip(self.PATHS, list(a)))
 
     def input_ticket(self) -> int:

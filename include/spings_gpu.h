@@ -282,7 +282,8 @@ int spg_kernel_times(spg_ctx *ctx, float *accumulate_ms, float *finalize_ms, int
  *   out[4] counted finalizes (k_acc_lite_run + k_count_list + k_fold_hist)
  *   out[5] fused deep finalizes (k_acc_seg FUSE, or list mode)           out[6] fused shallow finalizes (k_acc_lite)
  *   out[7] batches counted by k_acc_lite_run
- * Writes min(n, 8) values. */
+ *   out[8] lone mid-depth batches counted by k_count_cols (+ k_acc_seg<1> over the listed columns)
+ * Writes min(n, 9) values. */
 int spg_path_counters(spg_ctx *ctx, int64_t *out, int64_t n);
 
 /* Introspection for tests. */

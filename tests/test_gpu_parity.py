@@ -522,3 +522,71 @@ def test_fused_then_more_batches_keep_eps_bits_exact():
         compare_variants(got, exp, rtol=RTOL)
     assert eng.memory_summary() == orc.memory_summary()
     eng.close()
+
+
+@pytest.mark.parametrize("lpc", [0, 4, 16, 64])
+def test_mid_depth_lone_batch_counted(lpc, monkeypatch):
+    """A calls-only sample whose only batch is mid-depth (1,000x: BASELINE config 2): spg_finalize counts every
+    column (k_count_cols, lpc lanes per column: 0 = the default choice), folds exactly only the listed columns
+    (k_acc_seg<1>) and runs the sparse finalize.
+    Planted: short columns that may call (< 128 entries), an IUPAC call, a lone exotic entry, a P product in the
+    subnormal band, q in {0..3, >= 128}.  Calls vs the oracle; a second finalize (the records materialized through
+    k_acc_seg) returns the same calls bit for bit; then a second batch folds into the same memory."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    L = 5000
+    ref = synth.reference(L, seed=171)
+    p = dict(DEF, minEvidenceRatio=0.02)
+    lo, off, c, q = synth.pileup(L, 1000, seed=172, ref=ref, snv_every=41, lo=300, hi=2300)
+    rng = np.random.default_rng(173)
+    q = q.copy()
+    m = rng.random(len(q)) < 0.01
+    q[m] = rng.choice(np.array([0, 1, 2, 3, 4, 127, 128, 200, 255], np.uint8), size=m.sum())
+    b = (lo, off, c, q)
+    b = _plant_many(b, 900, 5, 35, 200)                      # 'R' x 20 %: an IUPAC call
+    b = _plant_many(b, 901, 3, 33, 1)                        # one 'M': exotic, replayed, no call
+    alt = 2 if ref[1000] != "C" else 4
+    b = _plant_many(b, 1000, alt, 31, 100)                   # sum q = 3100: P in the subnormal band
+    # the last columns of the window: short (tens of entries), some with an SNV that calls
+    pb, off, c, q = b
+    offs = off.astype(np.int64)
+    keep = np.ones(len(c), bool)
+    for col in range(2300 - 300 - 12, 2300 - 300):
+        s, e = offs[col], offs[col + 1]
+        keep[s + 40 + col % 7:e] = False
+    starts = offs[:-1]
+    newoff = np.concatenate([[0], np.cumsum(np.add.reduceat(keep.astype(np.int64), starts) * (np.diff(offs) > 0))])
+    c, q = c[keep].copy(), q[keep].copy()
+    for col in range(2300 - 300 - 12, 2300 - 300, 3):
+        s = newoff[col]
+        alt = 1 if ref[pb + col] != "A" else 8
+        c[s:s + 12] = alt
+        q[s:s + 12] = 37
+    b = (pb, newoff.astype(np.uint64), c, q)
+    if lpc:
+        monkeypatch.setenv("SPG_COUNT_LPC", str(lpc))
+    eng = PileupEngine(L, p["minBaseQuality"], p["minTotalDepth"], p["minAlleleDepth"], p["minEvidenceRatio"],
+                       device=0, reference=ref, calls_only=True)
+    orc = COracle(ref, p["minBaseQuality"], p["minTotalDepth"], p["minAlleleDepth"], p["minEvidenceRatio"])
+    eng.accumulate(*b)
+    orc.accumulate(*b)
+    eng.finalize()
+    orc.finalize()
+    got = eng.variants()
+    exp = orc.variants()
+    assert len(exp) > 40
+    assert any(v["alleles"][1] == "R" for v in exp)
+    assert any(v["info"]["DP"] < 128 for v in exp)
+    compare_variants(got, exp, rtol=RTOL)
+    pc = eng.path_counters()
+    assert pc["mid_counted_finalizes"] == 1 and pc["fused_deep_finalizes"] == 1, pc
+    eng.finalize()                                           # records materialized: the same calls, bit for bit
+    compare_variants(eng.variants(), got, rtol=0)
+    assert eng.memory_summary() == orc.memory_summary()
+    b2 = synth.pileup(L, 300, seed=174, ref=ref, snv_every=17, lo=1500, hi=3500)
+    eng.accumulate(*b2)
+    orc.accumulate(*b2)
+    eng.finalize()
+    orc.finalize()
+    compare_variants(eng.variants(), orc.variants(), rtol=RTOL)
+    eng.close()
