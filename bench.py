@@ -519,7 +519,7 @@ def per_bam_loop(args, D, eng, data, recs, nb, C, final_calls):
     """vc_queue.py:142-144 without the file I/O: per BAM, accumulate its batch (process_bam's accumulate step), then
     prepare_variants (finalize + the call table read back to the host, as write_vcf needs it).  Every finalize
     after the first counts only the new BAM and re-folds only the positions that can call (incremental counted
-    mode); the first is the fused single-batch finalize."""
+    mode, from the first BAM on: no record-path run and no full-range finalize, `engine_paths` counts them)."""
     import torch
     eng.reset()
     eng.sync()
@@ -527,6 +527,7 @@ def per_bam_loop(args, D, eng, data, recs, nb, C, final_calls):
     eng.set_timing(2)
     lat, gpu = np.zeros(nb), np.zeros(nb)
     n_calls = np.zeros(nb, np.int64)
+    pc0 = eng.path_counters()
     D.barrier()
     t0 = time.perf_counter()
     done = 0
@@ -543,6 +544,8 @@ def per_bam_loop(args, D, eng, data, recs, nb, C, final_calls):
             done += len(a)
     total = D.max(time.perf_counter() - t0)
     eng.set_timing(0)
+    pc1 = eng.path_counters()
+    paths = {k: pc1[k] - pc0[k] for k in pc1}
     # the last BAM's table against the one-shot counted table of the same BAMs: integer fields exact, GL / QUAL within
     # 1e-9 relative (the incremental folds add the fp64 sums in another grouping)
     same = None
@@ -561,9 +564,10 @@ def per_bam_loop(args, D, eng, data, recs, nb, C, final_calls):
             "latency_ms_first_100": float(np.mean(lat[:100])) * 1e3, "latency_ms_last_100": float(np.mean(lat[-100:])) * 1e3,
             "gpu_ms_per_bam": float(np.mean(g)) * 1e3, "gpu_ms_last_100": float(np.mean(g[-100:])) * 1e3,
             "bams_per_s": nb / total, "calls_last": int(n_calls[-1]), "final_table_equals_one_shot": same,
-            "path": "per BAM: spg_accumulate_batches (1 borrowed batch) + spg_finalize (BAM 1: fused k_acc_tile; then "
-                    "counted mode: k_acc_lite_run over the new BAM, k_count_list, incremental k_fold_hist, sparse "
-                    "k_finalize) + spg_get_candidates",
+            "path": "per BAM: spg_accumulate_batches (1 borrowed batch) + spg_finalize (counted mode from BAM 1: "
+                    "k_acc_lite_run over the new BAM, k_count_list, incremental k_fold_hist, sparse k_finalize) + "
+                    "spg_get_candidates",
+            "engine_paths": paths,
             "roofline": {"bound": "hbm (launch-bound at 6 MB per BAM)", "achieved": float(np.mean(moved[:done]) / np.mean(g) / 1e9),
                          "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                          "frac": float(np.mean(moved[:done]) / np.mean(g) / PEAK_HBM),

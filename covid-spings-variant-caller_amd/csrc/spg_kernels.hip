@@ -98,8 +98,15 @@ struct ReplayWs {
 };
 
 // Walk the position's entries in history batches [from, n_hist) in accumulate order; `ord` = raw entries of the
-// position in the batches before (advanced past the ones walked).
-template <typename Fn>
+// position in the batches before (advanced past the ones walked).  64 batches at a time: lane j resolves batch j's
+// descriptor and the position's column bounds in it (two round trips for 64 batches, not per batch), a wave prefix
+// sum lays their entries end to end, and the wave streams that sequence 64 entries per step — lane e finds its
+// entry's batch by a binary search over the lanes' prefix (ds_bpermute, no LDS) — one step's loads in flight while
+// the previous step folds.  (A live memory's position spans thousands of per-BAM batches: the per-batch walk was
+// three dependent round trips each, ~15 ms for a cold replay after 2,700 BAMs.)
+// (GROUPED false: batch by batch — the fused deep kernel's replays, whose history is the sample's one batch, and
+// whose registers the grouped form would raise into scratch)
+template <bool GROUPED, typename Fn>
 __device__ __forceinline__ void replay_walk(const FParams &F, const Hist *__restrict__ H, int64_t pos, int lane,
                                             uint32_t from, uint64_t &ord, Fn &&fn) {
     const bool indexed = F.ridx.n_buckets > 0;
@@ -115,19 +122,70 @@ __device__ __forceinline__ void replay_walk(const FParams &F, const Hist *__rest
         }
         i0 = lo;
     }
-    for (uint32_t i = i0; i < i1; i++) {
-        const int32_t b = indexed ? F.ridx.items[i] : (int32_t)i;
-        const Hist h = H[b];
-        const int64_t col = pos - h.pos_begin;
-        if (col < 0 || col >= h.n_cols) continue;
-        const uint64_t lo = h.off[col], hi = h.off[col + 1];
-        for (uint64_t e0 = lo; e0 < hi; e0 += 64) {
-            const uint64_t e = e0 + (uint64_t)lane;
-            const bool valid = e < hi;
-            const uint32_t c = valid ? h.code[e] : 0xFFu, q = valid ? h.qual[e] : 0u;
-            fn(c, q, valid, ord + (e0 - lo));
+    if constexpr (!GROUPED) {
+        for (uint32_t i = i0; i < i1; i++) {
+            const int32_t b = indexed ? F.ridx.items[i] : (int32_t)i;
+            const Hist h = H[b];
+            const int64_t col = pos - h.pos_begin;
+            if (col < 0 || col >= h.n_cols) continue;
+            const uint64_t lo = h.off[col], hi = h.off[col + 1];
+            for (uint64_t e0 = lo; e0 < hi; e0 += 64) {
+                const uint64_t e = e0 + (uint64_t)lane;
+                const bool valid = e < hi;
+                const uint32_t c = valid ? h.code[e] : 0xFFu, q = valid ? h.qual[e] : 0u;
+                fn(c, q, valid, ord + (e0 - lo));
+            }
+            ord += hi - lo;
         }
-        ord += hi - lo;
+        return;
+    }
+    for (uint32_t g0 = i0; g0 < i1; g0 += 64) {
+        // lane j: batch g0 + j's column of this position (empty when the batch does not cover it)
+        uint32_t len = 0;
+        uint64_t cp = 0, qp = 0;
+        if (g0 + (uint32_t)lane < i1) {
+            const int32_t b = indexed ? F.ridx.items[g0 + lane] : (int32_t)(g0 + lane);
+            const Hist h = H[b];
+            const int64_t col = pos - h.pos_begin;
+            if (col >= 0 && col < h.n_cols) {
+                const uint64_t lo = h.off[col], hi = h.off[col + 1];
+                len = (uint32_t)(hi - lo);
+                cp = (uint64_t)(h.code + lo);
+                qp = (uint64_t)(h.qual + lo);
+            }
+        }
+        uint32_t pre = len;                            // inclusive prefix of the lengths, then exclusive
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)pre, o);
+            if (lane >= o) pre += t;
+        }
+        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane(pre, 63);
+        pre -= len;
+        if (T == 0) continue;
+        // entry t0 + lane of the group's sequence: its batch = the last lane whose prefix is <= it
+        auto fetch = [&](uint32_t t0, uint32_t &c, uint32_t &q) {
+            const uint32_t gi = t0 + (uint32_t)lane;
+            int k = 0;
+#pragma unroll
+            for (int st = 32; st >= 1; st >>= 1)
+                if ((uint32_t)__shfl((int)pre, k + st) <= gi) k += st;
+            const uint32_t e = gi - (uint32_t)__shfl((int)pre, k);
+            const uint64_t ck = (uint64_t)(uint32_t)__shfl((int)(uint32_t)cp, k) | ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(cp >> 32), k) << 32);
+            const uint64_t qk = (uint64_t)(uint32_t)__shfl((int)(uint32_t)qp, k) | ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(qp >> 32), k) << 32);
+            c = 0xFFu; q = 0u;
+            if (gi < T) { c = reinterpret_cast<const uint8_t *>(ck)[e]; q = reinterpret_cast<const uint8_t *>(qk)[e]; }
+        };
+        uint32_t cA, qA, cB, qB;
+        fetch(0u, cA, qA);
+        for (uint32_t t0 = 0; t0 < T; t0 += 128) {
+            fetch(t0 + 64u, cB, qB);
+            fn(cA, qA, t0 + (uint32_t)lane < T, ord + t0);
+            if (t0 + 64u >= T) break;
+            fetch(t0 + 128u, cA, qA);
+            fn(cB, qB, t0 + 64u + (uint32_t)lane < T, ord + t0 + 64u);
+        }
+        ord += T;
     }
 }
 
@@ -161,7 +219,7 @@ __device__ __forceinline__ int32_t rcache_claim(const RCache &R, int64_t pos, ui
 // batches [0, upto)): one pass over batches [upto, n_hist) continues every fold from that state — P for every
 // code, H for the codes still alive (N != 0 last time) and for codes first seen since; the state is stored back.
 // rec: the position's record (HBM, or the fused accumulate's LDS image); eps(q): from_phred_scale(q)
-template <typename EpsFn>
+template <bool GROUPED, typename EpsFn>
 __device__ __forceinline__ void replay_wave(const FParams &F, const Hist *__restrict__ H, const Acc *rec,
                                          const Out &O, int64_t pos, ReplayWs *w, EpsFn &&eps_s) {
     const int lane = threadIdx.x & 63;
@@ -194,7 +252,7 @@ __device__ __forceinline__ void replay_wave(const FParams &F, const Hist *__rest
     }
     for (int attempt = 0; attempt < 2; attempt++) {
         const bool warm = from > 0;
-        replay_walk(F, H, pos, lane, from, ord, [&](uint32_t c, uint32_t q, bool valid, uint64_t base) {
+        replay_walk<GROUPED>(F, H, pos, lane, from, ord, [&](uint32_t c, uint32_t q, bool valid, uint64_t base) {
             const bool pass = valid && (int)q >= F.min_bq;
             depth += (uint32_t)__popcll(__ballot(pass));
             const bool isc = pass && c < 16u;
@@ -254,7 +312,7 @@ __device__ __forceinline__ void replay_wave(const FParams &F, const Hist *__rest
     const uint32_t needH = w->needH;
     if (from == 0 && needH) {
         uint64_t ord2 = 0;
-        replay_walk(F, H, pos, lane, 0u, ord2, [&](uint32_t c, uint32_t q, bool valid, uint64_t) {
+        replay_walk<GROUPED>(F, H, pos, lane, 0u, ord2, [&](uint32_t c, uint32_t q, bool valid, uint64_t) {
             const bool isc = valid && (int)q >= F.min_bq && c < 16u && ((needH >> c) & 1u);
             const double om = isc ? 1.0 - eps_s(q) : 0.0;
             uint64_t todo = __ballot(isc);
@@ -603,7 +661,7 @@ __device__ __forceinline__ void fused_tail(const FParams &F, const Out &O, const
         const int j = (int)__builtin_ctzll(rb);
         rb &= rb - 1;
         const int64_t pj = pos0 + (int64_t)(uint32_t)__builtin_amdgcn_readlane(cjl, j);
-        replay_wave(F, hdl, img + j, O, pj, ws, [&](uint32_t q) {
+        replay_wave<false>(F, hdl, img + j, O, pj, ws, [&](uint32_t q) {
             return q == 0u ? 1.0 : lut[q < 128u ? q : q + 128u].y;     // from_phred_scale (eps(Q0) = 1)
         });
     }
@@ -1166,7 +1224,7 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
                 rb &= rb - 1;
                 const int64_t pj = (int64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)pos, j) |
                                    ((int64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)((uint64_t)pos >> 32), j) << 32);
-                replay_wave(F, H, acc + pj, O, pj, &ws, [&](uint32_t q) { return eps_s[q]; });
+                replay_wave<true>(F, H, acc + pj, O, pj, &ws, [&](uint32_t q) { return eps_s[q]; });
             }
         }
         return;
@@ -1182,7 +1240,7 @@ __global__ __launch_bounds__(64) void k_finalize(FParams F, const Acc *__restric
         const int j = (int)__builtin_ctzll(rb);
         rb &= rb - 1;
         const int64_t pj = (int64_t)blockIdx.x * 64 + j;
-        replay_wave(F, H, acc + pj, O, pj, &ws, [&](uint32_t q) { return eps_s[q]; });
+        replay_wave<true>(F, H, acc + pj, O, pj, &ws, [&](uint32_t q) { return eps_s[q]; });
     }
 }
 
