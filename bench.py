@@ -233,6 +233,12 @@ def kernel_name(E, C, calls_only=True):
         return "k_acc_lite (+ k_acc_seg<1> for columns >= 128 entries)", "spg::k_acc_lite"
     if E < 256 * C:
         return "k_acc_tile (+ k_acc_seg<1> for columns >= 128 entries)", "spg::k_acc_tile"
+    if E < 4096 * C and calls_only:   # a lone mid-depth batch (1,000x): counted, the listed columns folded exactly
+        lpc = 4
+        while lpc < 64 and E / C / 16.0 / lpc > 2.5:
+            lpc *= 2
+        return (f"k_count_cols<{lpc},4> + k_acc_seg<1> over the listed columns (+ sparse k_finalize)",
+                f"spg::k_count_cols<{lpc}, 4>")
     nt = 2 * E > (192 << 20)
     return (f"k_acc_seg<4,true,4,{'true' if nt else 'false'}> (spg_accumulate{'; non-temporal loads' if nt else ''})",
             "spg::k_acc_seg<4, true")

@@ -1506,7 +1506,8 @@ static int finalize_impl(spg_ctx *c, bool table);
 // SPG_COUNT_COLS=0 disables, =1 takes every lone deep batch (A/B; 10,000x: 127 us vs the fused kernel's 111 us).
 // LPC: two or three 16-B blocks per lane (SPG_COUNT_LPC forces one: tests).
 static int mid_count_lpc(const spg_ctx *c) {
-    static const int mode = [] { const char *e = getenv("SPG_COUNT_COLS"); return e ? atoi(e) : -1; }();
+    const char *me = getenv("SPG_COUNT_COLS");        // (read per call: tests compare both paths)
+    const int mode = me ? atoi(me) : -1;
     if (mode == 0 || c->hist.empty()) return 0;
     const HistBatch &b = c->hist[0];
     if (b.n_samples != 1 || b.fsamp || b.n_cols == 0) return 0;

@@ -524,7 +524,7 @@ def test_fused_then_more_batches_keep_eps_bits_exact():
     eng.close()
 
 
-@pytest.mark.parametrize("lpc", [0, 4, 16, 64])
+@pytest.mark.parametrize("lpc", [0, 4, 16, 64, "list"])
 def test_mid_depth_lone_batch_counted(lpc, monkeypatch):
     """A calls-only sample whose only batch is mid-depth (1,000x: BASELINE config 2): spg_finalize counts every
     column (k_count_cols, lpc lanes per column: 0 = the default choice), folds exactly only the listed columns
@@ -563,7 +563,9 @@ def test_mid_depth_lone_batch_counted(lpc, monkeypatch):
         c[s:s + 12] = alt
         q[s:s + 12] = 37
     b = (pb, newoff.astype(np.uint64), c, q)
-    if lpc:
+    if lpc == "list":                                        # the fused kernel's list mode (multi-sample batches)
+        monkeypatch.setenv("SPG_COUNT_COLS", "0")
+    elif lpc:
         monkeypatch.setenv("SPG_COUNT_LPC", str(lpc))
     eng = PileupEngine(L, p["minBaseQuality"], p["minTotalDepth"], p["minAlleleDepth"], p["minEvidenceRatio"],
                        device=0, reference=ref, calls_only=True)
@@ -579,7 +581,7 @@ def test_mid_depth_lone_batch_counted(lpc, monkeypatch):
     assert any(v["info"]["DP"] < 128 for v in exp)
     compare_variants(got, exp, rtol=RTOL)
     pc = eng.path_counters()
-    assert pc["mid_counted_finalizes"] == 1 and pc["fused_deep_finalizes"] == 1, pc
+    assert pc["mid_counted_finalizes"] == (0 if lpc == "list" else 1) and pc["fused_deep_finalizes"] == 1, pc
     eng.finalize()                                           # records materialized: the same calls, bit for bit
     compare_variants(eng.variants(), got, rtol=0)
     assert eng.memory_summary() == orc.memory_summary()
