@@ -68,8 +68,8 @@ def parse():
     ap.add_argument("--time-every", type=int, default=8,
                     help="HIP events around the accumulate kernel on every K-th timed step")
     ap.add_argument("--e2e-threads", type=int, default=0,
-                    help="host threads of the end-to-end plan (0 = the per-GPU share of an 8-GPU node: "
-                         "len(sched_getaffinity) // 8, at least 16)")
+                    help="host threads of the end-to-end plan (0 = the per-GPU share of an 8-GPU node, "
+                         "len(sched_getaffinity) // 8, capped by the process's cgroup CPU quota)")
     ap.add_argument("--e2e-bams", type=int, default=4, help="BAMs per end-to-end stream")
     ap.add_argument("--e2e-many", type=int, default=64,
                     help="config 4 end to end: 100x SARS-CoV-2 BAM files through process_bams (0 = skip)")
@@ -776,7 +776,8 @@ def main():
     if args.no_cpu_baseline: legs.discard("cpu")
     if args.many_batches <= 0 and args.runs_batches <= 0: legs.discard("config4")
     if not args.e2e_threads:
-        args.e2e_threads = max(16, len(os.sched_getaffinity(0)) // 8)
+        from covid_spings_variant_caller_amd.pileup import cpu_share
+        args.e2e_threads = max(1, min(len(os.sched_getaffinity(0)) // 8, cpu_share()))
     import torch
     import spings  # noqa: F401
 

@@ -34,7 +34,7 @@ import numpy as np
 
 from . import _native as N
 from .engine import PileupEngine
-from .pileup import AlignmentFile, PileupParams
+from .pileup import AlignmentFile, PileupParams, cpu_share
 from .structs import Site, Variant
 
 log = logging.getLogger("covid_spings_variant_caller_amd")
@@ -159,7 +159,7 @@ class LiveVariantCaller:
         self.fastaFile = FastaFile(referenceFasta)
         self.pileup_params = PileupParams(stepper=stepper, min_mapping_quality=minMappingQuality, max_depth=max_depth,
                                           ignore_overlaps=ignore_overlaps,
-                                          n_threads=n_threads or min(16, len(os.sched_getaffinity(0))))
+                                          n_threads=n_threads or min(16, cpu_share()))
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
         n_pos = max(self.fastaFile.lengths) if self.fastaFile.lengths else 1
