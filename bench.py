@@ -775,11 +775,11 @@ def main():
     if args.no_e2e: legs.discard("e2e")
     if args.no_cpu_baseline: legs.discard("cpu")
     if args.many_batches <= 0 and args.runs_batches <= 0: legs.discard("config4")
+    import torch
+    import spings  # noqa: F401
     if not args.e2e_threads:
         from covid_spings_variant_caller_amd.pileup import cpu_share
         args.e2e_threads = max(1, min(len(os.sched_getaffinity(0)) // 8, cpu_share()))
-    import torch
-    import spings  # noqa: F401
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -233,6 +233,17 @@ __device__ __forceinline__ typename Vec<W>::T bload(__amdgpu_buffer_rsrc_t r, ui
     else return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, NT ? 2 : 0);
 }
 
+// The same with the wave-uniform part of the offset in soffset (an SGPR; the range check covers voffset + soffset,
+// tools/bufcheck.hip): a streaming loop's loads then take a loop-invariant VGPR offset, so no address register is
+// written while loads are in flight (hipcc otherwise drains every load at the loop header: an address VGPR it
+// allocated over a pending load's destination)
+template <int W, bool NT>
+__device__ __forceinline__ typename Vec<W>::T bload_s(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    const int so = (int)__builtin_amdgcn_readfirstlane(soff);
+    if constexpr (W == 4) return __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, so, NT ? 2 : 0);
+    else return __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, so, NT ? 2 : 0);
+}
+
 __device__ __forceinline__ void write_hist(const KParams &P) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *P.hslot = P.hdesc;
 }

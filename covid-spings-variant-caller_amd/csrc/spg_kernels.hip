@@ -619,10 +619,6 @@ __device__ __forceinline__ void assemble_record(const KParams &P, const Acc *__r
     reinterpret_cast<uint4 *>(out)[1] = h1;
 }
 
-struct ColDesc {             // one column of a wave's segment (LDS, 16 B)
-    uint32_t a, pre, e;     // 4W-aligned first chunk, first chunk index, end rel. to a (chunks = ceil(e / STEP))
-    uint32_t bic;           // start rel. to a (bits 0-3) | column within the group (4-9) | REF char (10-17)
-};
 
 struct RareItem {            // one lane's chunk slice (up to 16 entries) holding rare entries
     uint32_t c[4], q[4];    // (its column-relative offset is kept beside, in rqo)
@@ -631,6 +627,11 @@ struct RareItem {            // one lane's chunk slice (up to 16 entries) holdin
 struct Dual2 {              // per-lane partial sums of a wave's second fast allele
     double sl[64], se[64];
     uint32_t cnt[64], sq[64];
+};
+
+struct ColDesc {             // one column of a wave's segment (LDS, 16 B; the non-fused instantiations)
+    uint32_t a, pre, e;     // 4W-aligned first chunk, first chunk index, end rel. to a (chunks = ceil(e / STEP))
+    uint32_t bic;           // start rel. to a (bits 0-3) | column within the group (4-9) | REF char (10-17)
 };
 
 // Segment streaming: wave w owns G consecutive columns and walks them as ONE stream of 64 x 4W-entry
@@ -692,7 +693,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     __shared__ uint32_t rqr[KW][QCAP];
     __shared__ Dual2 dual2[KW];
     __shared__ Acc accimg[KW][NB];
-    __shared__ ColDesc coldesc[KW][W == 4 ? SPG_GMAX_DEEP : SPG_GMAX];
+    __shared__ ColDesc coldesc[KW][FUSE ? 1 : (W == 4 ? SPG_GMAX_DEEP : SPG_GMAX)];
     __shared__ Hist hdl;                                // FUSE: this batch's descriptor for the replay
     const uint64_t we = P.wtime ? __builtin_amdgcn_s_memrealtime() : 0;   // SPG_WAVE_TIMES: wave entry
     // the batch's history descriptor, first (consumed at once: kept live, hipcc would park it in scratch)
@@ -861,41 +862,60 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     const uint32_t total = __builtin_amdgcn_readlane(pre, 63);   // SGPR: loop bounds stay scalar
     pre -= nch;
     if (total == 0) continue;
-    // Column descriptors of the columns with chunks, compacted into LDS; the loop walks them with
-    // two scalar cursors (consumption and prefetch), so no per-lane descriptor stays in a VGPR.
-    {
-        const uint64_t nz = __ballot(nch > 0);
+    // Column descriptors of the columns with chunks stay in their lanes (lane j: the group's column j); the loop walks
+    // them with two scalar cursors (consumption and prefetch) over the ballot of lanes with chunks, reading a column's
+    // fields with v_readlane into SGPRs: no VGPR is written when a cursor moves.  (They were compacted into LDS, and
+    // the LDS read's address register — allocated over a pending chunk load's destination — made hipcc drain every
+    // load in flight each time the prefetch cursor entered a column.)
+    // (The non-fused instantiations keep the descriptors compacted in LDS as before: three more VGPRs put their
+    // 127-VGPR allocation into scratch.)
+    constexpr bool REGDESC = FUSE;
+    const uint64_t nz = __ballot(nch > 0);
+    if constexpr (!REGDESC) {
         if (nch > 0) {
             const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(nz >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nz, 0u));
             CD[k] = ColDesc{a_rel, pre, e_rel - a_rel, (b_rel - a_rel) | ((uint32_t)lane << 4) | (refc << 10)};
         }
         wave_sync();
     }
+    // (three VGPRs: the start, the end, and the first chunk's index packed with the start's offset in its 16-B block and
+    // the REF char — a group's chunks stay below 2^20, i.e. 10^9 entries per wave)
+    const uint32_t d_a = a_rel, d_e = e_rel - a_rel, d_x = pre | ((b_rel - a_rel) << 20) | (refc << 24);
     const uint32_t lo = (uint32_t)lane * ALIGN;
-    auto cd = [&](uint32_t k, int f) -> uint32_t {      // uniform LDS read of descriptor field f
-        return __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t *>(CD + k)[f]);
+    auto nxt = [&](int l) -> int {                      // the next lane with chunks after l (-1: the first); exists
+        if constexpr (!REGDESC) return l + 1;           // whenever a caller asks (LDS: the compacted index)
+        return (int)__builtin_ctzll(l >= 63 ? 0ull : (nz & (~0ull << (l + 1))));
+    };
+    auto cd = [&](int l, int f) -> uint32_t {           // field f of lane l's descriptor (uniform): start, first chunk,
+        if constexpr (!REGDESC) return __builtin_amdgcn_readfirstlane(reinterpret_cast<const uint32_t *>(CD + l)[f]);
+        if (f == 0) return __builtin_amdgcn_readlane(d_a, l);                       // end, start in block | column | REF
+        if (f == 2) return __builtin_amdgcn_readlane(d_e, l);
+        const uint32_t x = __builtin_amdgcn_readlane(d_x, l);
+        return f == 1 ? (x & 0xFFFFFu) : (((x >> 20) & 15u) | ((uint32_t)l << 4) | ((x >> 24) << 10));
     };
     // prefetch cursor: column of the chunk being loaded (chunk indices only grow, by one per call)
-    uint32_t pk = 0, p_a = cd(0, 0), p_pre = cd(0, 1), p_end = p_pre + (cd(0, 2) + STEP - 1) / STEP;
+    int pk = nxt(-1);
+    uint32_t p_a = cd(pk, 0), p_pre = cd(pk, 1), p_end = p_pre + (cd(pk, 2) + STEP - 1) / STEP;
     auto chunk_off = [&](uint32_t i) -> uint32_t {   // chunks past the end reload the last one (ignored)
         if (i >= p_end && i < total) {
-            pk++;
+            pk = nxt(pk);
             p_a = cd(pk, 0);
             p_pre = cd(pk, 1);
             p_end = p_pre + (cd(pk, 2) + STEP - 1) / STEP;
         }
         const uint32_t ii = i < p_end ? i : p_end - 1;
-        return p_a + (ii - p_pre) * STEP + lo;
+        return p_a + (ii - p_pre) * STEP;               // (wave-uniform: the lane's part, lo, is the voffset)
     };
 
     // register ring of three chunks: two loads stay in flight while one chunk is processed
     V c0, q0, c1, q1, c2, q2;
-#define SPG_LD(C, Q, I) do { const uint32_t o_ = chunk_off(I); C = bload<W, NT>(rc, o_); Q = bload<W, NT>(rq, o_); } while (0)
+#define SPG_LD(C, Q, I) do { const uint32_t o_ = chunk_off(I); C = bload_s<W, NT>(rc, lo, o_); Q = bload_s<W, NT>(rq, lo, o_); } while (0)
     SPG_LD(c0, q0, 0u);
     SPG_LD(c1, q1, 1u);
 
     // per-column state (consumption cursor)
-    uint32_t ck = 0xFFFFFFFFu, cj = 0, crefc = 0;
+    int ck = -1;
+    uint32_t cj = 0, crefc = 0;
     uint32_t cs = 0, cpre = 0, cn = 0;
     uint32_t fcnt = 0, fsq = 0, ffirst = INF32;
     double fsl = 0.0, fse = 0.0;
@@ -933,7 +953,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     // and registers costing more occupancy than the instructions they save.
     auto process = [&](const V &cc, const V &qq, uint32_t i) {
         if (i == cpre + cn) {                  // next column with chunks
-            ck++;
+            ck = nxt(ck);
             cpre = cd(ck, 1);
             const uint32_t e = cd(ck, 2), bic = cd(ck, 3);
             cn = (e + STEP - 1) / STEP;
@@ -944,7 +964,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         }
         cs = i - cpre;
         if (cs == 0) {                         // ---- column begin ----
-            prog(2, ck, i, cn);
+            prog(2, (uint32_t)ck, i, cn);
             rare_init(RR + nb, lane);
             const uint32_t v0 = dw<W>(cc, 0) & 0xFFu;
             const int vote = ((int32_t)lo >= bl && (int32_t)lo < el) ? (int)v0 : -1;
