@@ -698,6 +698,17 @@ def end_to_end(args, device):
         # the product path: device-side pileup (spg_accumulate_records)
         caller, calls, t0, t_in, t1 = stream(cap, True)
         assert [v["start"] for v in calls] == [v["start"] for v in calls_h], "device / host pileup calls differ"
+        # the same BAMs through process_bams (the drop-in's many-BAM call: plans of two BAMs overlap on the host)
+        caller.reset_memory()
+        caller.engine.sync()
+        m0 = time.perf_counter()
+        caller.process_bams([bam] * (2 * n_bams))
+        calls_m = caller.prepare_variants()
+        caller.engine.sync()
+        m1 = time.perf_counter()
+        assert [v["start"] for v in calls_m] == [v["start"] for v in calls_h], "process_bams calls differ"
+        many_leg = {"bams": 2 * n_bams, "positions_per_s_per_bam": 2 * n_bams * L_SARS / (m1 - m0),
+                    "s_per_bam": (m1 - m0) / (2 * n_bams)}
         p = caller.pileup_params
         b0 = time.perf_counter()
         with AlignmentFile(bam) as f:
@@ -722,7 +733,7 @@ def end_to_end(args, device):
                     "breakdown_one_bam": {"host_plan_records_s": b1 - b0, "inflated_mb": data_mb,
                                           "h2d_records_plus_gpu_s": g1 - g0,
                                           "pcie_inclusive_gpu_positions_per_s": L_SARS / (g1 - g0)},
-                    "host_fill_path": host_leg}
+                    "host_fill_path": host_leg, "process_bams": many_leg}
         caller.engine.close()
         del caller
     os.environ.pop("SPG_DEVICE_PILEUP", None)

@@ -33,6 +33,7 @@
 #include <cmath>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <chrono>
 #include <mutex>
 #include <thread>
@@ -179,10 +180,11 @@ struct Reads {                 // one contig's reads, structure of arrays
         memcpy(&v, raw + rec[r] + 32 + raw[rec[r] + 8] + 4 * (size_t)i, 4);
         return v;
     }
-    std::string name(size_t r) const {
-        if (!raw) return std::string(names.data() + name_off[r]);
+    std::string name(size_t r) const { return std::string(name_view(r)); }
+    std::string_view name_view(size_t r) const {        // (valid while the reads are: no copy)
+        if (!raw) return std::string_view(names.data() + name_off[r]);
         const uint8_t ln = raw[rec[r] + 8];
-        return std::string((const char *)raw + rec[r] + 32, ln ? ln - 1u : 0u);
+        return std::string_view((const char *)raw + rec[r] + 32, ln ? ln - 1u : 0u);
     }
     uint8_t *seq(size_t r) const { return bases[r]; }
     uint8_t *qual(size_t r) const { return raw ? raw + qual_off(r) : bases[r] + l_seq[r]; }
@@ -1237,8 +1239,11 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
     // to that read's position.
     int64_t it_pos = 0, max_pos = -1;
     bool started = tid == 0;
-    std::unordered_map<std::string, size_t> olap;
-    auto name = [&](size_t r) { return R.name(r); };
+    // (keyed by views of the names in place: no string built per read — the std::string keys cost about half of
+    // this sweep at 10,000x)
+    std::unordered_map<std::string_view, size_t> olap;
+    if (p.ignore_overlaps) olap.reserve(1u << 16);
+    auto name = [&](size_t r) { return R.name_view(r); };
     auto olap_remove = [&](size_t r) {
         if (!p.ignore_overlaps || olap.empty()) return;
         auto itr = olap.find(name(r));
@@ -1276,7 +1281,7 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
                                   !(R.mtid[r] >= 0 && R.mtid[r] != tid) &&
                                   !(std::llabs(R.isize[r]) >= 2 * (int64_t)R.l_seq[r] && R.mpos[r] >= R.end[r]);
                 if (cand) {
-                    const std::string nm = name(r);
+                    const std::string_view nm = name(r);
                     auto itr = olap.find(nm);
                     if (itr == olap.end()) {
                         if (R.mpos[r] >= R.pos[r] || ((fl & F_PAIRED) && R.mpos[r] == -1)) olap.emplace(nm, r);

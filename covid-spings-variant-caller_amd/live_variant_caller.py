@@ -258,8 +258,9 @@ class LiveVariantCaller:
                 raise FileNotFoundError(f"[Errno 2] could not open alignment file `{f}`: No such file or directory")
         import dataclasses
         contig = self.fastaFile.references[referenceIndex]
-        workers = workers or max(1, min(8, (os.cpu_count() or 2) // 2))
-        # the host threads split between the concurrent plans
+        # concurrent plans: one per 8 CPUs this process may use (the GPU box's 16-CPU quota: two), so one plan's serial
+        # phases (record scan, depth-cap sweep) overlap the other's inflate; the host threads split between them
+        workers = workers or max(1, min(4, cpu_share() // 8))
         params = dataclasses.replace(self.pileup_params, n_threads=max(1, self.pileup_params.n_threads // workers))
 
         def plan(path):
@@ -270,7 +271,7 @@ class LiveVariantCaller:
                     return bam.pileup_records(contig, params)
                 return bam.pileup_plan(contig, params)
 
-        window = 2 * workers                  # plans in flight (each holds its BAM's decoded reads)
+        window = workers + 1                  # plans in flight (each holds its BAM's inflated records, ~0.5 GB at 10,000x)
         with ThreadPoolExecutor(workers) as ex:
             pending = [ex.submit(plan, p) for p in paths[:window]]
             for i in range(len(paths)):
