@@ -58,7 +58,8 @@ extern "C" {
 #define SPG_IN_DEVICE 0x1     /* offsets/base_code/qual are device pointers on the ctx device */
 #define SPG_IN_BORROW 0x2     /* with SPG_IN_DEVICE: keep the caller's device buffers as replay
                                  history without copying; they must stay valid until
-                                 spg_reset/spg_destroy */
+                                 spg_reset/spg_destroy, and base_code / qual must be readable for
+                                 16 bytes past the last entry (the kernels load 16-B blocks) */
 #define SPG_IN_TRUSTED 0x4    /* host input produced by spp_pileup / spp_batch_fill (already valid CSR):
                                skip the O(E) host validation scan */
 
