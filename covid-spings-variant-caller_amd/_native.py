@@ -118,6 +118,8 @@ def gpu_lib():
     _sig(L.spg_set_history_cap, i32, vp, i64)
     _sig(L.spg_history_resident, i32, vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64))
     _sig(L.spg_path_counters, i32, vp, C.POINTER(i64), i64)
+    _sig(L.spg_bgzf_inflate, i32, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp, C.POINTER(C.c_float))
+    _sig(L.spg_bgzf_last_error, C.c_char_p)
     _sig(L.spg_position_entries, i32, vp, i64, vp, vp, i64, C.POINTER(i64))
     _sig(L.spg_input_ticket, i32, vp, C.POINTER(u64))
     _sig(L.spg_wait_ticket, i32, vp, u64)
@@ -207,6 +209,7 @@ def pileup_lib():
     _sig(L.spp_pileup_plan_records, C.c_int, vp, i32, i64, i64, C.POINTER(SppParams), C.POINTER(vp))
     _sig(L.spp_batch_records, C.c_int, vp, C.POINTER(SpgRecords))
     _sig(L.spp_set_host_allocator, C.c_int, vp, vp)
+    _sig(L.spp_set_inflater, C.c_int, vp, C.c_int)
     _sig(L.spp_default_sim_params, None, C.POINTER(SimParams))
     _sig(L.spp_simulate_bam, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, i64, C.POINTER(SimParams),
          C.POINTER(i64))
@@ -228,6 +231,22 @@ def use_pinned_records():
     pcheck(P.spp_set_host_allocator(C.cast(G.spg_host_alloc, C.c_void_p), C.cast(G.spg_host_free, C.c_void_p)),
            "spp_set_host_allocator")
     _pinned_records = True
+
+
+_gpu_inflate_dev = None
+
+
+def use_gpu_inflate(device: int = 0, on: bool = True):
+    """Records plans inflate the BAM's BGZF members on `device` (spg_bgzf_inflate, csrc/spg_inflate.hip) instead of
+    on the host; members the GPU reports bad are inflated on the host.  on=False restores the host inflate."""
+    global _gpu_inflate_dev
+    G, P = gpu_lib(), pileup_lib()
+    if on:
+        pcheck(P.spp_set_inflater(C.cast(G.spg_bgzf_inflate, C.c_void_p), int(device)), "spp_set_inflater")
+        _gpu_inflate_dev = int(device)
+    else:
+        pcheck(P.spp_set_inflater(None, 0), "spp_set_inflater")
+        _gpu_inflate_dev = None
 
 
 def pcheck(rc: int, what: str = ""):

@@ -952,6 +952,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     // handling): specialised bodies for full / all-q<128 chunks measured slower, their extra code
     // and registers costing more occupancy than the instructions they save.
     auto process = [&](const V &cc, const V &qq, uint32_t i) {
+        if (i >= total) return;                // (the last round's chunks past the end)
         if (i == cpre + cn) {                  // next column with chunks
             ck = nxt(ck);
             cpre = cd(ck, 1);
@@ -1138,9 +1139,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         }
     };
 
+    // rounds of three chunks with no exit in between (hipcc's wait counts stay exact across the back edge: with an
+    // exit after each chunk the first of the three waited for one chunk more than it needs); a chunk index past the
+    // end is a no-op (process), its load a clamped reload
     for (uint32_t i = 0; i < total; i += 3) {
-        SPG_LD(c2, q2, i + 2); process(c0, q0, i); if (i + 1 >= total) break;
-        SPG_LD(c0, q0, i + 3); process(c1, q1, i + 1); if (i + 2 >= total) break;
+        SPG_LD(c2, q2, i + 2); process(c0, q0, i);
+        SPG_LD(c0, q0, i + 3); process(c1, q1, i + 1);
         SPG_LD(c1, q1, i + 4); process(c2, q2, i + 2);
     }
 #undef SPG_LD

@@ -634,6 +634,8 @@ void read_bam(const spp_file *f, int32_t tid, const spp_params &p, Reads &R) {
 // ---------------------------------------------------------------------------------------------
 spp_alloc_fn g_alloc = nullptr;
 spp_free_fn g_free = nullptr;
+std::atomic<spp_inflate_fn> g_inflate{nullptr};  // GPU inflater of the records plans (spp_set_inflater)
+std::atomic<int> g_inflate_dev{0};
 
 struct HostBuf {
     uint8_t *p = nullptr;
@@ -837,10 +839,38 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
         if (blks[i].ulen && !inf.run(m + blks[i].off, blks[i].clen, buf + uoff[i], blks[i].ulen)) bad = true;
         done[i].store(1, std::memory_order_release);
     };
+    // GPU inflate (spp_set_inflater): the mapped file's bytes copied into pinned staging in parallel, every member
+    // inflated on the device (one call: upload, kernel, download into `buf`); members it reports bad — and all of them
+    // if the call fails — are inflated here below.  The host's threads are then free for the record scan.
+    bool gpu_inflated = false;
+    if (const spp_inflate_fn gfn = g_inflate.load(); gfn && nb > 0) {
+        struct GM { uint64_t coff; uint32_t clen, ulen; uint64_t uoff; };
+        std::vector<GM> gm(nb);
+        for (size_t i = 0; i < nb; i++) gm[i] = {blks[i].off, (uint32_t)blks[i].clen, (uint32_t)blks[i].ulen, uoff[i]};
+        HostBuf cb = buf_get(fsz + 64);
+        par_chunks(fsz, nt, [&](int, size_t a, size_t b) { memcpy(cb.p + a, m + a, b - a); });
+        std::vector<uint32_t> gst(nb, 1);
+        const bool ok_call = gfn(g_inflate_dev.load(), cb.p, fsz, gm.data(), (int64_t)nb, buf, total, gst.data(), nullptr) == 0;
+        buf_put(cb);
+        if (ok_call) {
+            gpu_inflated = true;
+            for (size_t i = 0; i < nb; i++)
+                if (gst[i] == 0) done[i].store(1, std::memory_order_relaxed);
+        }
+    }
     std::vector<std::thread> pool;
     struct Join { std::vector<std::thread> &v; std::atomic<size_t> &nx; size_t n;
                   ~Join() { nx = n; for (auto &t : v) if (t.joinable()) t.join(); } } join{pool, next, nb};
-    for (int t = 1; t < nt; t++)
+    // (after a GPU inflate the helpers only redo the members it reported bad)
+    if (gpu_inflated) {
+        std::vector<size_t> redo;
+        for (size_t i = 0; i < nb; i++)
+            if (!done[i].load(std::memory_order_relaxed)) redo.push_back(i);
+        Inflater rinf;
+        for (size_t i : redo) inflate_one(rinf, i);
+        next = nb;
+    }
+    for (int t = 1; t < nt && !gpu_inflated; t++)
         pool.emplace_back([&] {
             Inflater inf;
             for (size_t i; (i = next++) < nb;) inflate_one(inf, i);
@@ -882,7 +912,7 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
     // inside a record, a damaged file) the serial scan below walks the stream from the header, as before.
     bool scanned = false;
     const size_t body = cur;
-    if (par_scan && nt > 1 && nb > 0 && total > body + ((size_t)nt << 20) && avail_to(total)) {
+    if ((par_scan || gpu_inflated) && nt > 1 && nb > 0 && total > body + ((size_t)nt << 20) && avail_to(total)) {
         auto rec_len = [&](size_t x) -> size_t {        // plausible record at x: 4 + block_size, else 0
             if (x + 40 > total) return 0;
             const uint32_t bs = rdu32(buf + x);
@@ -1821,6 +1851,12 @@ int spp_batch_records(spp_batch *b, spg_records *out) {
     if (!b || !out) return fail("spp_batch_records: null argument");
     if (!b->plan || !b->plan->raw) return fail("spp_batch_records: not a records plan (spp_pileup_plan_records)");
     *out = b->plan->view;
+    return 0;
+}
+
+int spp_set_inflater(spp_inflate_fn fn, int device) {
+    g_inflate_dev = device;
+    g_inflate = fn;
     return 0;
 }
 

@@ -180,6 +180,10 @@ class LiveVariantCaller:
         self.device_pileup = os.environ.get("SPG_DEVICE_PILEUP", "1") != "0"
         if self.device_pileup:
             N.use_pinned_records()
+            # BGZF members inflated on the GPU (spg_bgzf_inflate) when SPG_GPU_INFLATE=1: the host's threads then only
+            # scan the records and take the read decisions
+            if os.environ.get("SPG_GPU_INFLATE", "0") == "1":
+                N.use_gpu_inflate(device if device is not None else 0)
         self._inflight = collections.deque()     # (input ticket, records plan) whose copy may still be running
         self.reset_memory()
 

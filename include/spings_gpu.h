@@ -287,6 +287,20 @@ int spg_kernel_times(spg_ctx *ctx, float *accumulate_ms, float *finalize_ms, int
  * Writes min(n, 9) values. */
 int spg_path_counters(spg_ctx *ctx, int64_t *out, int64_t n);
 
+/* BGZF members inflated on the GPU (the records plan's BAM read).  comp: the file's bytes (each
+ * member's raw-DEFLATE payload at coff, clen bytes, followed by its 8-byte CRC32/ISIZE trailer); out: the inflated
+ * stream (member m at uoff, exactly ulen <= 65536 bytes).  status[m] = 0 when member m inflated to ulen bytes
+ * (else the caller inflates it on the host).  kernel_ms: the inflate kernel's time (may be null).  Synchronous. */
+typedef struct spg_bgzf_member {
+    uint64_t coff;
+    uint32_t clen;
+    uint32_t ulen;
+    uint64_t uoff;
+} spg_bgzf_member;
+int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const spg_bgzf_member *members, int64_t n,
+                     uint8_t *out, size_t out_bytes, uint32_t *status, float *kernel_ms);
+const char *spg_bgzf_last_error(void);
+
 /* Introspection for tests. */
 int spg_device_count(int *n);
 size_t spg_sizeof_candidate(void);

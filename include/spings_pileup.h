@@ -98,6 +98,12 @@ int spp_batch_records(spp_batch *b, struct spg_records *out);
 typedef int (*spp_alloc_fn)(size_t bytes, void **out);
 typedef int (*spp_free_fn)(void *p);
 int spp_set_host_allocator(spp_alloc_fn alloc, spp_free_fn release);
+/* BGZF inflater for the records plans (e.g. spg_bgzf_inflate on `device`): called once per BAM with the mapped
+ * file, its members ({u64 coff, u32 clen, u32 ulen, u64 uoff}, layout of spg_bgzf_member) and the record buffer;
+ * members whose status is not 0 are inflated on the host.  NULL restores the host inflate. */
+typedef int (*spp_inflate_fn)(int device, const uint8_t *comp, size_t comp_bytes, const void *members, int64_t n,
+                              uint8_t *out, size_t out_bytes, uint32_t *status, float *kernel_ms);
+int spp_set_inflater(spp_inflate_fn fn, int device);
 
 /* Synthetic read simulator (SURVEY.md §8 d "Synthetic inputs"): writes a coordinate-sorted BGZF
  * BAM of single-end reads (flag 0, MAPQ 60) over one contig — starts uniform on [0, L-read_len],
