@@ -33,7 +33,7 @@ struct IBits {
     const uint8_t *p, *lim;                        // lim: the last dword load that stays inside payload + trailer
     uint64_t buf;
     int n;
-    __device__ __forceinline__ void fill() {
+    __host__ __device__ __forceinline__ void fill() {
         if (n <= 32) {
             uint32_t w = 0;                        // (past the member: zeros, and the overrun check fails it)
             if (p <= lim) __builtin_memcpy(&w, p, 4);
@@ -42,9 +42,9 @@ struct IBits {
             n += 32;
         }
     }
-    __device__ __forceinline__ uint32_t peek(int k) const { return (uint32_t)(buf & ((1ull << k) - 1)); }
-    __device__ __forceinline__ void drop(int k) { buf >>= k; n -= k; }
-    __device__ __forceinline__ uint32_t get(int k) {   // k <= 24 after fill()
+    __host__ __device__ __forceinline__ uint32_t peek(int k) const { return (uint32_t)(buf & ((1ull << k) - 1)); }
+    __host__ __device__ __forceinline__ void drop(int k) { buf >>= k; n -= k; }
+    __host__ __device__ __forceinline__ uint32_t get(int k) {   // k <= 24 after fill()
         fill();
         const uint32_t v = peek(k);
         drop(k);
@@ -54,7 +54,7 @@ struct IBits {
 
 // canonical Huffman tables from code lengths (RFC 1951 3.2.2); false: over-subscribed or an incomplete code
 // with more than one symbol (a single-symbol distance code is allowed incomplete)
-__device__ bool build(HTab &T, const uint8_t *len, int n, int pb) {
+__host__ __device__ bool build(HTab &T, const uint8_t *len, int n, int pb) {
     for (int i = 0; i < 16; i++) T.count[i] = 0;
     for (int s = 0; s < n; s++) T.count[len[s]]++;
     if (T.count[0] == n) {                             // no codes: every lookup fails (only a distance code may)
@@ -80,7 +80,7 @@ __device__ bool build(HTab &T, const uint8_t *len, int n, int pb) {
     for (int l = 1; l <= 15; l++) {
         for (int c = 0; c < T.count[l]; c++, k++) {
             if (l <= pb) {
-                const uint32_t rev = __builtin_bitreverse32(code) >> (32 - l);
+                const uint32_t rev = __builtin_bitreverse32(code) >> (32 - l);   // (clang builtin: host and device)
                 const uint16_t e = (uint16_t)(T.sym[k] | (l << 9));
                 for (uint32_t x = rev; x < (1u << pb); x += 1u << l) T.prim[x] = e;
             }
@@ -92,7 +92,7 @@ __device__ bool build(HTab &T, const uint8_t *len, int n, int pb) {
 }
 
 // one symbol; -1 on an invalid code
-__device__ __forceinline__ int decode(IBits &B, const HTab &T, int pb) {
+__host__ __device__ __forceinline__ int decode(IBits &B, const HTab &T, int pb) {
     B.fill();
     const uint16_t e = T.prim[B.peek(pb)];
     if (e >> 9) {
@@ -114,17 +114,23 @@ __device__ __forceinline__ int decode(IBits &B, const HTab &T, int pb) {
     return -1;
 }
 
-__constant__ uint16_t LBASE[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115,
-                                   131, 163, 195, 227, 258};
-__constant__ uint8_t LEXT[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t DBASE[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769, 1025, 1537,
-                                   2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t DEXT[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
-__constant__ uint8_t CLORD[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+struct InfTabs {                           // RFC 1951 3.2.5 / 3.2.7
+    uint16_t lbase[29];
+    uint8_t lext[29];
+    uint16_t dbase[30];
+    uint8_t dext[30];
+    uint8_t clord[19];
+};
+#define SPG_INF_TABS {{3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258}, \
+                      {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0},                      \
+                      {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, \
+                       6145, 8193, 12289, 16385, 24577},                                                                           \
+                      {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13},          \
+                      {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15}}
+__constant__ InfTabs d_tabs = SPG_INF_TABS;
+static const InfTabs h_tabs = SPG_INF_TABS;
 
-// the fixed Huffman tables (RFC 1951 3.2.6), once
-__global__ void k_inflate_fixed(IScratch *fx) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__host__ __device__ void fixed_tables(IScratch *fx) {
     uint8_t len[288];
     for (int s = 0; s < 288; s++) len[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
     build(fx->lit, len, 288, IB_LIT);
@@ -132,15 +138,14 @@ __global__ void k_inflate_fixed(IScratch *fx) {
     build(fx->dist, len, 30, IB_DIST);
 }
 
-// status: 0 ok; 1 bad block type; 2 bad stored length; 3 bad code lengths; 4 bad table; 5 bad symbol;
-// 6 distance too far back; 7 output overrun; 8 input overrun; 9 wrong size
-__global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
-                                                int64_t n, uint8_t *__restrict__ out, IScratch *__restrict__ scr,
-                                                const IScratch *__restrict__ fx, uint32_t *__restrict__ status) {
-    const int64_t m = (int64_t)blockIdx.x * 64 + threadIdx.x;
-    if (m >= n) return;
-    const spg_bgzf_member M = mem[m];
-    IScratch &S = scr[m];
+// the fixed Huffman tables (RFC 1951 3.2.6), once
+__global__ void k_inflate_fixed(IScratch *fx) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) fixed_tables(fx);
+}
+
+// one member: status (see k_inflate)
+__host__ __device__ uint32_t inflate_member(const uint8_t *comp, const spg_bgzf_member &M, uint8_t *out, IScratch &S,
+                                            const IScratch *fx, const InfTabs &TB) {
     uint8_t *o = out + M.uoff;
     const uint32_t ulen = M.ulen;
     const uint8_t *const cend = comp + M.coff + M.clen;
@@ -175,7 +180,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp
             const int hlit = (int)B.get(5) + 257, hdist = (int)B.get(5) + 1, hclen = (int)B.get(4) + 4;
             uint8_t cl[19];
             for (int i = 0; i < 19; i++) cl[i] = 0;
-            for (int i = 0; i < hclen; i++) cl[CLORD[i]] = (uint8_t)B.get(3);
+            for (int i = 0; i < hclen; i++) cl[TB.clord[i]] = (uint8_t)B.get(3);
             if (!build(S.cl, cl, 19, IB_CL)) { st = 3; break; }
             int k = 0;
             while (k < hlit + hdist) {
@@ -215,10 +220,10 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp
             }
             if (s == 256) break;
             if (s > 285) { st = 5; break; }
-            const uint32_t len = LBASE[s - 257] + B.get(LEXT[s - 257]);
+            const uint32_t len = TB.lbase[s - 257] + B.get(TB.lext[s - 257]);
             const int ds = decode(B, *D, IB_DIST);
             if (ds < 0 || ds > 29) { st = 5; break; }
-            const uint32_t dist = DBASE[ds] + B.get(DEXT[ds]);
+            const uint32_t dist = TB.dbase[ds] + B.get(TB.dext[ds]);
             if (dist > w) { st = 6; break; }
             if (w + len > ulen) { st = 7; break; }
             uint8_t *dst = o + w;
@@ -248,7 +253,17 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp
         if (B.p - (B.n >> 3) > cend) { st = 8; break; }
     } while (!bfinal);
     if (!st && w != ulen) st = 9;
-    status[m] = st;
+    return st;
+}
+
+// status: 0 ok; 1 bad block type; 2 bad stored length; 3 bad code lengths; 4 bad table; 5 bad symbol;
+// 6 distance too far back; 7 output overrun; 8 input overrun; 9 wrong size
+__global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
+                                                int64_t n, uint8_t *__restrict__ out, IScratch *__restrict__ scr,
+                                                const IScratch *__restrict__ fx, uint32_t *__restrict__ status) {
+    const int64_t m = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (m >= n) return;
+    status[m] = inflate_member(comp, mem[m], out, scr[m], fx, d_tabs);
 }
 
 }  // namespace spg
@@ -290,6 +305,21 @@ template <class T> int grow(T *&p, size_t &cap, size_t need) {
 
 extern "C" {
 const char *spg_bgzf_last_error(void) { return g_inf_err.c_str(); }
+
+// The device decoder compiled for the host, member by member (CPU tests of its logic; the product inflates on the GPU)
+int spg_bgzf_inflate_check(const uint8_t *comp, size_t comp_bytes, const spg_bgzf_member *members, int64_t n,
+                           uint8_t *out, size_t out_bytes, uint32_t *status) {
+    if (n < 0 || (n && (!comp || !members || !out || !status))) return ifail("spg_bgzf_inflate_check: bad argument");
+    for (int64_t i = 0; i < n; i++) {
+        const spg_bgzf_member &m = members[i];
+        if (m.coff + m.clen + 8 > comp_bytes || m.uoff + m.ulen > out_bytes || m.ulen > 65536)
+            return ifail("spg_bgzf_inflate_check: member " + std::to_string(i) + " outside the buffers");
+    }
+    std::vector<spg::IScratch> s(2);
+    spg::fixed_tables(&s[1]);
+    for (int64_t i = 0; i < n; i++) status[i] = spg::inflate_member(comp, members[i], out, s[0], &s[1], spg::h_tabs);
+    return 0;
+}
 
 int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const spg_bgzf_member *members, int64_t n,
                      uint8_t *out, size_t out_bytes, uint32_t *status, float *kernel_ms) {

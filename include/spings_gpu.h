@@ -300,6 +300,10 @@ typedef struct spg_bgzf_member {
 int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const spg_bgzf_member *members, int64_t n,
                      uint8_t *out, size_t out_bytes, uint32_t *status, float *kernel_ms);
 const char *spg_bgzf_last_error(void);
+/* The same decoder compiled for the host (CPU tests of its logic only; comp needs 8 readable bytes past each
+ * member's payload, as in a BGZF file). */
+int spg_bgzf_inflate_check(const uint8_t *comp, size_t comp_bytes, const spg_bgzf_member *members, int64_t n,
+                           uint8_t *out, size_t out_bytes, uint32_t *status);
 
 /* Introspection for tests. */
 int spg_device_count(int *n);
