@@ -118,9 +118,10 @@ def gpu_lib():
     _sig(L.spg_set_history_cap, i32, vp, i64)
     _sig(L.spg_history_resident, i32, vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64))
     _sig(L.spg_path_counters, i32, vp, C.POINTER(i64), i64)
-    _sig(L.spg_bgzf_inflate, i32, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp, C.POINTER(C.c_float))
-    _sig(L.spg_bgzf_last_error, C.c_char_p)
-    _sig(L.spg_bgzf_inflate_check, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp)
+    if hasattr(L, "spg_bgzf_inflate"):              # (older A/B builds loaded through SPG_GPU_LIB lack it)
+        _sig(L.spg_bgzf_inflate, i32, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp, C.POINTER(C.c_float))
+        _sig(L.spg_bgzf_last_error, C.c_char_p)
+        _sig(L.spg_bgzf_inflate_check, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp)
     _sig(L.spg_position_entries, i32, vp, i64, vp, vp, i64, C.POINTER(i64))
     _sig(L.spg_input_ticket, i32, vp, C.POINTER(u64))
     _sig(L.spg_wait_ticket, i32, vp, u64)
