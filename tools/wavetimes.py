@@ -46,6 +46,13 @@ def analyse(path):
         w = np.frombuffer(raw[at:at + 16 * n], np.uint32).reshape(n, 4)
         at += 16 * int(n)
         launches.append((int(g), w))
+    per_launch = []                                  # per-XCC spans of every launch (is the slow XCD always the same?)
+    for _, wl in launches:
+        wl = wl[wl[:, 2] != 0]
+        s0 = wl[:, 0].astype(np.int64)
+        e0 = (s0 - s0.min()) * 10e-3 + (wl[:, 2] & 0xFFFFF) * 10e-3
+        x0 = wl[:, 3] >> 24
+        per_launch.append({int(x): round(float(e0[x0 == x].max()), 2) for x in np.unique(x0)})
     g, w = launches[-1]
     n_all = len(w)
     w = w[w[:, 2] != 0]                              # (dynamic-tail waves that found no unit exit unrecorded)
@@ -86,6 +93,7 @@ def analyse(path):
     res["start_histogram"] = hist.tolist()
     conc = [int(((t0 <= t) & (end > t)).sum()) for t in np.linspace(0, span, 23)[1:-1]]
     res["resident_waves_over_time"] = conc
+    res["per_xcc_end_us_every_launch"] = per_launch
     return res
 
 
