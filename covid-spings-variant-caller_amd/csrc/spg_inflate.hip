@@ -2,14 +2,12 @@
 // live_variant_caller.py:54-72, whose host BGZF inflate bounds the end-to-end stream at the GPU box's 16-CPU share).
 //
 // A BGZF file is a sequence of independent raw-DEFLATE members (RFC 1951) of at most 64 KiB of output each: one
-// thread per member decodes its blocks (stored, fixed Huffman, dynamic Huffman) into the member's output range.
-// Huffman decoding: a 10-bit primary table per code (entry = symbol | length << 9; codes longer than 10 bits, rare,
-// take the canonical bit-serial walk over the code's length counts and sorted symbols), built per block in the
-// thread's slice of a scratch buffer; the fixed-Huffman tables are built once into their own slice.  The bit buffer
-// is refilled 32 bits at a time (unaligned dword loads; every member is followed by its 8-byte CRC32/ISIZE trailer
-// and the uploaded file by 64 bytes of padding, so the refill may read past the payload).  A member's status word
-// is 0 when it inflated to exactly its ISIZE bytes; anything else (a corrupt stream) is reported and the caller
-// inflates that member on the host.
+// lane per member decodes its blocks (stored, fixed Huffman, dynamic Huffman) into the member's output range.  All
+// per-member state lives in registers and the lane's LDS slice: the Huffman tables (10-bit primary table for the
+// literal/length code, 8-bit for distances, a canonical walk for the rare longer codes), the code lengths; length and
+// distance bases are computed, not looked up.  The compressed stream is read as aligned 16-byte chunks one ahead of
+// use.  A member's status word is 0 when it inflated to exactly its ISIZE bytes; anything else (a corrupt stream) is
+// reported and the caller inflates that member on the host.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -17,96 +15,139 @@
 
 namespace spg {
 
-constexpr int IB_LIT = 10;                 // primary table bits, literal/length code
-constexpr int IB_DIST = 8;                 // primary table bits, distance code
-constexpr int IB_CL = 7;                   // the code-length code (max 7 bits: always primary)
-struct HTab {                              // one Huffman code's decode tables (in the thread's scratch slice)
-    uint16_t prim[1 << IB_LIT];            // (the distance / code-length codes use the first 2^8 / 2^7 entries)
-    uint16_t count[16];                    // codes per length
-    uint16_t sym[288];                     // symbols sorted by (length, value)
-};
-struct IScratch {
-    HTab lit, dist, cl;
-};
+// Per-member decode tables: one slice of SLICE bytes (LDS on the device: mpw slices per block; a host array in the
+// check).  u16 entries of a primary table are symbol | code length << 9 (0: a longer code or no code); the counts and
+// length-sorted symbols serve the canonical walk for codes longer than the primary table.  The code-length code's
+// tables borrow the literal table's primary area and the distance code's count / symbol areas (it is done with
+// before those codes are built); its 19 code lengths are read into the lengths area.
+constexpr int IB_LIT = 10, IB_DIST = 8, IB_CL = 7;      // primary table bits
+constexpr int SL_LITP = 0, SL_DISTP = 2048, SL_LCNT = 2560, SL_DCNT = 2592, SL_LSYM = 2624, SL_DSYM = 3200,
+              SL_LENS = 3264, SLICE = 3584;
+static_assert(SL_LENS + 320 == SLICE && SL_DSYM + 64 == SL_LENS && SL_LSYM + 576 == SL_DSYM, "slice layout");
 
+// The bit stream: a 64-bit buffer refilled 32 bits at a time from a 128-bit reservoir r, which is refilled from the
+// next 16-byte aligned chunk q, loaded one chunk ahead (its address never depends on the bits consumed, so its
+// latency can hide behind the symbols of the chunk before).  Past the member's trailer the last chunk is read again
+// (the overrun check then fails the member); the buffers are padded so an aligned chunk never leaves them.
 struct IBits {
-    const uint8_t *p, *lim;                        // lim: the last dword load that stays inside payload + trailer
-    uint64_t buf;
-    int n;
-    __host__ __device__ __forceinline__ void fill() {
-        if (n <= 32) {
-            uint32_t w = 0;                        // (past the member: zeros, and the overrun check fails it)
-            if (p <= lim) __builtin_memcpy(&w, p, 4);
-            buf |= (uint64_t)w << n;
-            p += 4;
-            n += 32;
+    const uint8_t *qa;          // the chunk held in q (r's chunk ends here)
+    const uint8_t *end;         // member payload + its 8-byte trailer
+    uint64_t buf, r0, r1, q0, q1;
+    int n, rn;                  // bits in buf; bits in r (a multiple of 8)
+    __host__ __device__ __forceinline__ void chunk(const uint8_t *a, uint64_t &x0, uint64_t &x1) const {
+        // past the trailer the last chunk is read again (garbage the overrun check fails; never outside the buffer):
+        // an unconditional load, so no branch merge forces a wait for it before its use one chunk later
+        const uint8_t *lastc = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(end - 1) & ~(uintptr_t)15);
+        a = a < end ? a : lastc;
+#if defined(__HIP_DEVICE_COMPILE__)
+        // a global (not flat) load: a flat load also counts on the LDS wait counter
+        typedef __attribute__((address_space(1))) const uint64_t gu64;
+        gu64 *c = (gu64 *)a;
+#else
+        const uint64_t *c = reinterpret_cast<const uint64_t *>(a);
+#endif
+        x0 = c[0];
+        x1 = c[1];
+    }
+    // start at byte address s (any alignment)
+    __host__ __device__ __forceinline__ void start(const uint8_t *s) {
+        const uint8_t *a = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(s) & ~(uintptr_t)15);
+        const int skip = (int)(s - a) * 8;
+        chunk(a, r0, r1);
+        if (skip >= 64) {
+            r0 = r1 >> (skip - 64);
+            r1 = 0;
+        } else if (skip) {
+            r0 = (r0 >> skip) | (r1 << (64 - skip));
+            r1 >>= skip;
         }
+        rn = 128 - skip;
+        qa = a + 16;
+        chunk(qa, q0, q1);
+        buf = 0;
+        n = 0;
+    }
+    __host__ __device__ __forceinline__ void fill() {
+        if (n > 32) return;
+        uint32_t v;
+        if (rn >= 32) {
+            v = (uint32_t)r0;
+            r0 = (r0 >> 32) | (r1 << 32);
+            r1 >>= 32;
+            rn -= 32;
+        } else {                                 // rn in {0, 8, 16, 24}: r's last bits, then q's first
+            const int k = 32 - rn;               // 8..32 bits from q
+            v = (uint32_t)((rn ? (r0 & ((1ull << rn) - 1)) : 0) | (q0 << rn));
+            r0 = (q0 >> k) | (q1 << (64 - k));
+            r1 = q1 >> k;
+            rn = 128 - k;
+            qa += 16;
+            chunk(qa, q0, q1);
+        }
+        buf |= (uint64_t)v << n;
+        n += 32;
     }
     __host__ __device__ __forceinline__ uint32_t peek(int k) const { return (uint32_t)(buf & ((1ull << k) - 1)); }
     __host__ __device__ __forceinline__ void drop(int k) { buf >>= k; n -= k; }
-    __host__ __device__ __forceinline__ uint32_t get(int k) {   // k <= 24 after fill()
+    __host__ __device__ __forceinline__ uint32_t get(int k) {   // k <= 24
         fill();
         const uint32_t v = peek(k);
         drop(k);
         return v;
     }
+    // the byte address of the next unread whole byte (after a drop to a byte boundary)
+    __host__ __device__ __forceinline__ const uint8_t *byte_pos() const { return qa - (rn >> 3) - (n >> 3); }
 };
 
-// canonical Huffman tables from code lengths (RFC 1951 3.2.2); false: over-subscribed or an incomplete code
-// with more than one symbol (a single-symbol distance code is allowed incomplete)
-__host__ __device__ bool build(HTab &T, const uint8_t *len, int n, int pb) {
-    for (int i = 0; i < 16; i++) T.count[i] = 0;
-    for (int s = 0; s < n; s++) T.count[len[s]]++;
-    if (T.count[0] == n) {                             // no codes: every lookup fails (only a distance code may)
-        for (int i = 0; i < (1 << pb); i++) T.prim[i] = 0;
-        return true;
-    }
+// canonical Huffman tables from code lengths (RFC 1951 3.2.2); false: over-subscribed, or an incomplete code with
+// more than one symbol (a single-code distance alphabet may be incomplete)
+__host__ __device__ __forceinline__ bool build(uint16_t *prim, uint16_t *count, uint16_t *sym, const uint8_t *len, int n,
+                                               int pb) {
+    for (int i = 0; i < 16; i++) count[i] = 0;
+    for (int s = 0; s < n; s++) count[len[s]]++;
+    uint64_t *p8 = reinterpret_cast<uint64_t *>(prim);
+    for (int i = 0; i < (1 << pb) / 4; i++) p8[i] = 0;
+    if (count[0] == n) return true;                      // no codes: every lookup fails (only a distance code may)
     int left = 1;
     for (int l = 1; l < 16; l++) {
-        left <<= 1;
-        left -= T.count[l];
+        left = (left << 1) - count[l];
         if (left < 0) return false;
     }
+    if (left > 0 && n - count[0] > 1) return false;
     uint16_t offs[16];
     offs[1] = 0;
-    for (int l = 1; l < 15; l++) offs[l + 1] = offs[l] + T.count[l];
+    for (int l = 1; l < 15; l++) offs[l + 1] = (uint16_t)(offs[l] + count[l]);
     for (int s = 0; s < n; s++)
-        if (len[s]) T.sym[offs[len[s]]++] = (uint16_t)s;
-    if (left > 0 && n - T.count[0] > 1) return false;   // incomplete with more than one code
-    for (int i = 0; i < (1 << pb); i++) T.prim[i] = 0;
-    // primary table: each code of length <= pb fills 2^(pb - len) entries at its bit-reversed code
+        if (len[s]) sym[offs[len[s]]++] = (uint16_t)s;
+    // each code of length <= pb fills 2^(pb - len) entries at its bit-reversed code
     uint32_t code = 0;
     int k = 0;
-    for (int l = 1; l <= 15; l++) {
-        for (int c = 0; c < T.count[l]; c++, k++) {
-            if (l <= pb) {
-                const uint32_t rev = __builtin_bitreverse32(code) >> (32 - l);   // (clang builtin: host and device)
-                const uint16_t e = (uint16_t)(T.sym[k] | (l << 9));
-                for (uint32_t x = rev; x < (1u << pb); x += 1u << l) T.prim[x] = e;
-            }
-            code++;
+    for (int l = 1; l <= pb; l++) {
+        for (int c = 0; c < count[l]; c++, k++, code++) {
+            const uint32_t rev = __builtin_bitreverse32(code) >> (32 - l);
+            const uint16_t e = (uint16_t)(sym[k] | (l << 9));
+            for (uint32_t x = rev; x < (1u << pb); x += 1u << l) prim[x] = e;
         }
         code <<= 1;
     }
     return true;
 }
 
-// one symbol; -1 on an invalid code
-__host__ __device__ __forceinline__ int decode(IBits &B, const HTab &T, int pb) {
-    B.fill();
-    const uint16_t e = T.prim[B.peek(pb)];
+// one symbol; -1 on an invalid code.  Needs >= 15 bits in the buffer (the caller's fill()).
+__host__ __device__ __forceinline__ int decode(IBits &B, const uint16_t *prim, const uint16_t *count, const uint16_t *sym,
+                                               int pb) {
+    const uint16_t e = prim[B.peek(pb)];
     if (e >> 9) {
         B.drop(e >> 9);
         return e & 0x1FF;
     }
-    // longer than the primary table (or invalid): canonical walk, one bit at a time (the first bit read is the
-    // code's most significant)
+    // longer than the primary table (or invalid): the canonical walk, one bit at a time (first bit read = MSB)
     int code = 0, first = 0, index = 0;
     for (int l = 1; l <= 15; l++) {
         code |= (int)B.peek(1);
         B.drop(1);
-        const int c = T.count[l];
-        if (code - first < c) return T.sym[index + (code - first)];
+        const int c = count[l];
+        if (code - first < c) return sym[index + (code - first)];
         index += c;
         first = (first + c) << 1;
         code <<= 1;
@@ -114,80 +155,81 @@ __host__ __device__ __forceinline__ int decode(IBits &B, const HTab &T, int pb) 
     return -1;
 }
 
-struct InfTabs {                           // RFC 1951 3.2.5 / 3.2.7
-    uint16_t lbase[29];
-    uint8_t lext[29];
-    uint16_t dbase[30];
-    uint8_t dext[30];
-    uint8_t clord[19];
-};
-#define SPG_INF_TABS {{3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27, 31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258}, \
-                      {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0},                      \
-                      {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129, 193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, \
-                       6145, 8193, 12289, 16385, 24577},                                                                           \
-                      {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13},          \
-                      {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15}}
-__constant__ InfTabs d_tabs = SPG_INF_TABS;
-static const InfTabs h_tabs = SPG_INF_TABS;
-
-__host__ __device__ void fixed_tables(IScratch *fx) {
-    uint8_t len[288];
-    for (int s = 0; s < 288; s++) len[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-    build(fx->lit, len, 288, IB_LIT);
-    for (int s = 0; s < 30; s++) len[s] = 5;
-    build(fx->dist, len, 30, IB_DIST);
+// length / distance bases and extra bits (RFC 1951 3.2.5), computed: c = length code - 257, d = distance code
+__host__ __device__ __forceinline__ uint32_t len_ext(int c) { return c < 8 || c == 28 ? 0u : (uint32_t)(c >> 2) - 1u; }
+__host__ __device__ __forceinline__ uint32_t len_base(int c) {
+    return c < 8 ? (uint32_t)c + 3u : c == 28 ? 258u : ((4u | (uint32_t)(c & 3)) << len_ext(c)) + 3u;
+}
+__host__ __device__ __forceinline__ uint32_t dist_ext(int d) { return d < 4 ? 0u : (uint32_t)(d >> 1) - 1u; }
+__host__ __device__ __forceinline__ uint32_t dist_base(int d) {
+    return d < 4 ? (uint32_t)d + 1u : ((2u | (uint32_t)(d & 1)) << dist_ext(d)) + 1u;
 }
 
-// the fixed Huffman tables (RFC 1951 3.2.6), once
-__global__ void k_inflate_fixed(IScratch *fx) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) fixed_tables(fx);
-}
-
-// one member: status (see k_inflate)
-__host__ __device__ uint32_t inflate_member(const uint8_t *comp, const spg_bgzf_member &M, uint8_t *out, IScratch &S,
-                                            const IScratch *fx, const InfTabs &TB) {
+// one member into out + M.uoff; status (see k_inflate).  slice: SLICE bytes, 8-byte aligned.
+__host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp, const spg_bgzf_member &M, uint8_t *out,
+                                                            uint8_t *slice) {
+    uint16_t *const litp = reinterpret_cast<uint16_t *>(slice + SL_LITP);
+    uint16_t *const distp = reinterpret_cast<uint16_t *>(slice + SL_DISTP);
+    uint16_t *const lcnt = reinterpret_cast<uint16_t *>(slice + SL_LCNT);
+    uint16_t *const dcnt = reinterpret_cast<uint16_t *>(slice + SL_DCNT);
+    uint16_t *const lsym = reinterpret_cast<uint16_t *>(slice + SL_LSYM);
+    uint16_t *const dsym = reinterpret_cast<uint16_t *>(slice + SL_DSYM);
+    uint8_t *const lens = slice + SL_LENS;
     uint8_t *o = out + M.uoff;
     const uint32_t ulen = M.ulen;
     const uint8_t *const cend = comp + M.coff + M.clen;
-    IBits B{comp + M.coff, cend + 4, 0, 0};
-    uint32_t w = 0;                                 // bytes written
+    IBits B;
+    B.end = cend + 8;
+    B.start(comp + M.coff);
+    uint32_t w = 0;                                      // bytes written
     uint32_t st = 0;
-    uint8_t lens[288 + 32];
     int bfinal = 0;
+    bool fixed_built = false;
     do {
         bfinal = (int)B.get(1);
         const uint32_t type = B.get(2);
-        if (type == 0) {                            // stored: to a byte boundary, LEN, NLEN, LEN bytes
+        if (type == 0) {                                 // stored: to a byte boundary, LEN, NLEN, LEN bytes
             B.drop(B.n & 7);
             const uint32_t ln = B.get(16), nl = B.get(16);
             if ((ln ^ 0xFFFFu) != nl) { st = 2; break; }
-            // the whole bytes still in the bit buffer come first
-            const uint8_t *src = B.p - (B.n >> 3);
-            B.buf = 0;
-            B.n = 0;
+            const uint8_t *src = B.byte_pos();
             if (w + ln > ulen) { st = 7; break; }
             if (src + ln > cend) { st = 8; break; }
+#if defined(__HIP_DEVICE_COMPILE__)
+            typedef __attribute__((address_space(1))) const uint8_t gu8;
+            for (uint32_t i = 0; i < ln; i++) o[w + i] = ((gu8 *)src)[i];
+#else
             for (uint32_t i = 0; i < ln; i++) o[w + i] = src[i];
+#endif
             w += ln;
-            B.p = src + ln;
+            B.start(src + ln);
             continue;
         }
-        const HTab *L, *D;
-        if (type == 1) {
-            L = &fx->lit;
-            D = &fx->dist;
+        if (type == 1) {                                 // the fixed codes (RFC 1951 3.2.6), built once per member
+            if (!fixed_built) {
+                for (int s = 0; s < 288; s++) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+                build(litp, lcnt, lsym, lens, 288, IB_LIT);
+                for (int s = 0; s < 32; s++) lens[s] = 5;   // (30 and 31 complete the code; decoding them fails)
+                build(distp, dcnt, dsym, lens, 32, IB_DIST);
+                fixed_built = true;
+            }
         } else if (type == 2) {
+            fixed_built = false;
             const int hlit = (int)B.get(5) + 257, hdist = (int)B.get(5) + 1, hclen = (int)B.get(4) + 4;
-            uint8_t cl[19];
+            uint8_t *const cl = lens;                    // 19 code-length code lengths, in RFC order
             for (int i = 0; i < 19; i++) cl[i] = 0;
-            for (int i = 0; i < hclen; i++) cl[TB.clord[i]] = (uint8_t)B.get(3);
-            if (!build(S.cl, cl, 19, IB_CL)) { st = 3; break; }
+            for (int i = 0; i < hclen; i++) {
+                const int ord = i < 3 ? 16 + i : i == 3 ? 0 : (i & 1) ? 7 - (i - 5) / 2 : 8 + (i - 4) / 2;   // RFC 1951 3.2.7
+                cl[ord] = (uint8_t)B.get(3);
+            }
+            if (!build(litp, dcnt, dsym, cl, 19, IB_CL)) { st = 3; break; }
             int k = 0;
             while (k < hlit + hdist) {
-                const int s = decode(B, S.cl, IB_CL);
+                B.fill();
+                const int s = decode(B, litp, dcnt, dsym, IB_CL);
                 if (s < 0) { st = 3; break; }
                 if (s < 16) { lens[k++] = (uint8_t)s; continue; }
-                int rep = 0;
+                int rep;
                 uint8_t v = 0;
                 if (s == 16) {
                     if (k == 0) { st = 3; break; }
@@ -202,33 +244,57 @@ __host__ __device__ uint32_t inflate_member(const uint8_t *comp, const spg_bgzf_
                 while (rep--) lens[k++] = v;
             }
             if (st) break;
-            if (lens[256] == 0) { st = 3; break; }          // no end-of-block code
-            if (!build(S.lit, lens, hlit, IB_LIT) || !build(S.dist, lens + hlit, hdist, IB_DIST)) { st = 4; break; }
-            L = &S.lit;
-            D = &S.dist;
+            if (lens[256] == 0) { st = 3; break; }       // no end-of-block code
+            if (!build(distp, dcnt, dsym, lens + hlit, hdist, IB_DIST) || !build(litp, lcnt, lsym, lens, hlit, IB_LIT)) {
+                st = 4;
+                break;
+            }
         } else {
             st = 1;
             break;
         }
-        while (true) {                              // the block's codes
-            const int s = decode(B, *L, IB_LIT);
-            if (s < 0) { st = 5; break; }
+        while (true) {                                   // the block's codes
+            B.fill();
+            const int s = decode(B, litp, lcnt, lsym, IB_LIT);
             if (s < 256) {
+                if (s < 0) { st = 5; break; }
                 if (w >= ulen) { st = 7; break; }
                 o[w++] = (uint8_t)s;
                 continue;
             }
             if (s == 256) break;
             if (s > 285) { st = 5; break; }
-            const uint32_t len = TB.lbase[s - 257] + B.get(TB.lext[s - 257]);
-            const int ds = decode(B, *D, IB_DIST);
+            B.fill();                                    // <= 5 extra bits, then <= 15 of the distance code
+            const uint32_t len = len_base(s - 257) + B.peek((int)len_ext(s - 257));
+            B.drop((int)len_ext(s - 257));
+            const int ds = decode(B, distp, dcnt, dsym, IB_DIST);
             if (ds < 0 || ds > 29) { st = 5; break; }
-            const uint32_t dist = TB.dbase[ds] + B.get(TB.dext[ds]);
+            const uint32_t dist = dist_base(ds) + B.get((int)dist_ext(ds));
             if (dist > w) { st = 6; break; }
             if (w + len > ulen) { st = 7; break; }
             uint8_t *dst = o + w;
             const uint8_t *from = dst - dist;
-            if (dist >= 4) {                        // four bytes at a time: each source dword was written before
+            if (dist >= 16 && w + len + 15 <= ulen) {
+                // 16-byte chunks, up to four loads in flight before their stores (a round's sources all precede its
+                // first store: round = min(64, dist rounded down to 16)); the last chunk may write up to 15 bytes past
+                // the match, inside the member, which later symbols overwrite
+                const uint32_t R = dist >= 64 ? 64u : dist & ~15u;
+                for (uint32_t i = 0; i < len; i += R) {
+                    uint64_t v[8];
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; k++)
+                        if (16 * k < R && i + 16 * k < len) {
+                            __builtin_memcpy(&v[2 * k], from + i + 16 * k, 8);
+                            __builtin_memcpy(&v[2 * k + 1], from + i + 16 * k + 8, 8);
+                        }
+#pragma unroll
+                    for (uint32_t k = 0; k < 4; k++)
+                        if (16 * k < R && i + 16 * k < len) {
+                            __builtin_memcpy(dst + i + 16 * k, &v[2 * k], 8);
+                            __builtin_memcpy(dst + i + 16 * k + 8, &v[2 * k + 1], 8);
+                        }
+                }
+            } else if (dist >= 4) {                             // four bytes at a time: each source dword was written before
                 uint32_t i = 0;
                 for (; i + 4 <= len; i += 4) {
                     uint32_t v;
@@ -236,7 +302,7 @@ __host__ __device__ uint32_t inflate_member(const uint8_t *comp, const spg_bgzf_
                     __builtin_memcpy(dst + i, &v, 4);
                 }
                 for (; i < len; i++) dst[i] = from[i];
-            } else {                                // a 1-3 byte pattern repeated (runs of one quality value)
+            } else {                                     // a 1-3 byte pattern repeated (runs of one quality value)
                 uint32_t pat = 0;
                 for (uint32_t j = 0; j < 4; j++) pat |= (uint32_t)from[j % dist] << (8 * j);
                 if (dist == 3) {
@@ -250,23 +316,22 @@ __host__ __device__ uint32_t inflate_member(const uint8_t *comp, const spg_bgzf_
             w += len;
         }
         if (st) break;
-        if (B.p - (B.n >> 3) > cend) { st = 8; break; }
+        if (B.byte_pos() > cend) { st = 8; break; }
     } while (!bfinal);
     if (!st && w != ulen) st = 9;
     return st;
 }
 
 // status: 0 ok; 1 bad block type; 2 bad stored length; 3 bad code lengths; 4 bad table; 5 bad symbol;
-// 6 distance too far back; 7 output overrun; 8 input overrun; 9 wrong size
-// mpw members per wave (lanes >= mpw idle): fewer members in lockstep diverge less, and the members spread over more
-// SIMDs (8,357 members of a 10,000x BAM are 131 full waves)
+// 6 distance too far back; 7 output overrun; 8 input overrun; 9 wrong size.
+// mpw members per block, one per lane (lanes >= mpw idle), each with its SLICE of the block's LDS
 __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
-                                                int64_t n, uint8_t *__restrict__ out, IScratch *__restrict__ scr,
-                                                const IScratch *__restrict__ fx, uint32_t *__restrict__ status, int mpw) {
+                                                int64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ status, int mpw) {
+    extern __shared__ __align__(16) uint8_t inf_lds[];
     if ((int)threadIdx.x >= mpw) return;
     const int64_t m = (int64_t)blockIdx.x * mpw + threadIdx.x;
     if (m >= n) return;
-    status[m] = inflate_member(comp, mem[m], out, scr[m], fx, d_tabs);
+    status[m] = inflate_member(comp, mem[m], out, inf_lds + (size_t)threadIdx.x * SLICE);
 }
 
 }  // namespace spg
@@ -275,6 +340,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp
 // C-ABI (include/spings_gpu.h): upload, inflate, download; per-device scratch kept between calls (grow-only)
 // ---------------------------------------------------------------------------------------------------------------
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -283,13 +349,10 @@ namespace {
 struct InflateDev {
     hipStream_t st = nullptr;
     uint8_t *comp = nullptr, *out = nullptr;
-    size_t comp_cap = 0, out_cap = 0;
+    size_t comp_cap = 0, out_cap = 0, mem_bytes = 0, status_bytes = 0;
     spg_bgzf_member *mem = nullptr;
-    spg::IScratch *scr = nullptr, *fx = nullptr;
     uint32_t *status = nullptr;
-    int64_t mem_cap = 0;
     hipEvent_t ev[2] = {nullptr, nullptr};
-    float ms = 0.f;
 };
 std::mutex g_inf_mu;
 std::vector<InflateDev> g_inf;
@@ -319,9 +382,13 @@ int spg_bgzf_inflate_check(const uint8_t *comp, size_t comp_bytes, const spg_bgz
         if (m.coff + m.clen + 8 > comp_bytes || m.uoff + m.ulen > out_bytes || m.ulen > 65536)
             return ifail("spg_bgzf_inflate_check: member " + std::to_string(i) + " outside the buffers");
     }
-    std::vector<spg::IScratch> s(2);
-    spg::fixed_tables(&s[1]);
-    for (int64_t i = 0; i < n; i++) status[i] = spg::inflate_member(comp, members[i], out, s[0], &s[1], spg::h_tabs);
+    // the decoder reads whole aligned 16-byte chunks: a padded copy, aligned like the device buffer
+    std::vector<uint64_t> padded((comp_bytes + 64) / 8 + 1, 0);
+    std::memcpy(padded.data(), comp, comp_bytes);
+    std::vector<uint64_t> slice(spg::SLICE / 8);
+    for (int64_t i = 0; i < n; i++)
+        status[i] = spg::inflate_member(reinterpret_cast<const uint8_t *>(padded.data()), members[i], out,
+                                        reinterpret_cast<uint8_t *>(slice.data()));
     return 0;
 }
 
@@ -339,9 +406,6 @@ int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const s
         ICHK(hipStreamCreateWithFlags(&D.st, hipStreamNonBlocking));
         ICHK(hipEventCreate(&D.ev[0]));
         ICHK(hipEventCreate(&D.ev[1]));
-        ICHK(hipMalloc(&D.fx, sizeof(spg::IScratch)));
-        hipLaunchKernelGGL(spg::k_inflate_fixed, dim3(1), dim3(64), 0, D.st, D.fx);
-        ICHK(hipGetLastError());
     }
     for (int64_t i = 0; i < n; i++) {
         const spg_bgzf_member &m = members[i];
@@ -349,26 +413,18 @@ int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const s
             return ifail("spg_bgzf_inflate: member " + std::to_string(i) + " outside the buffers");
     }
     if (n == 0) return 0;
-    size_t mcap = (size_t)D.mem_cap * sizeof(spg_bgzf_member);
     if (grow(D.comp, D.comp_cap, comp_bytes + 64) || grow(D.out, D.out_cap, out_bytes + 64) ||
-        grow(D.mem, mcap, (size_t)n * sizeof(spg_bgzf_member)))
+        grow(D.mem, D.mem_bytes, (size_t)n * sizeof(spg_bgzf_member)) ||
+        grow(D.status, D.status_bytes, (size_t)n * sizeof(uint32_t)))
         return ifail("spg_bgzf_inflate: out of device memory");
-    if ((int64_t)(mcap / sizeof(spg_bgzf_member)) > D.mem_cap) {
-        if (D.scr) (void)hipFree(D.scr);
-        if (D.status) (void)hipFree(D.status);
-        D.scr = nullptr;
-        D.status = nullptr;
-        D.mem_cap = (int64_t)(mcap / sizeof(spg_bgzf_member));
-        ICHK(hipMalloc(&D.scr, sizeof(spg::IScratch) * (size_t)D.mem_cap));
-        ICHK(hipMalloc(&D.status, sizeof(uint32_t) * (size_t)D.mem_cap));
-    }
     ICHK(hipMemcpyAsync(D.comp, comp, comp_bytes, hipMemcpyHostToDevice, D.st));
     ICHK(hipMemsetAsync(D.comp + comp_bytes, 0, 64, D.st));
     ICHK(hipMemcpyAsync(D.mem, members, (size_t)n * sizeof(spg_bgzf_member), hipMemcpyHostToDevice, D.st));
     ICHK(hipEventRecord(D.ev[0], D.st));
-    static const int mpw = [] { const char *e = getenv("SPG_INFLATE_MPW"); const int v = e ? atoi(e) : 16; return v >= 1 && v <= 64 ? v : 16; }();
-    hipLaunchKernelGGL(spg::k_inflate, dim3((unsigned)((n + mpw - 1) / mpw)), dim3(64), 0, D.st, D.comp, D.mem, n, D.out, D.scr,
-                       D.fx, D.status, mpw);
+    // members per block (one per lane, SLICE bytes of LDS each): few per wave diverge less and spread over more SIMDs
+    static const int mpw = [] { const char *e = getenv("SPG_INFLATE_MPW"); const int v = e ? atoi(e) : 8; return v >= 1 && v <= 16 ? v : 8; }();
+    hipLaunchKernelGGL(spg::k_inflate, dim3((unsigned)((n + mpw - 1) / mpw)), dim3(64), (size_t)mpw * spg::SLICE, D.st, D.comp,
+                       D.mem, n, D.out, D.status, mpw);
     ICHK(hipGetLastError());
     ICHK(hipEventRecord(D.ev[1], D.st));
     ICHK(hipMemcpyAsync(out, D.out, out_bytes, hipMemcpyDeviceToHost, D.st));
