@@ -303,8 +303,9 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
                 }
                 for (; i < len; i++) dst[i] = from[i];
             } else {                                     // a 1-3 byte pattern repeated (runs of one quality value)
-                uint32_t pat = 0;
-                for (uint32_t j = 0; j < 4; j++) pat |= (uint32_t)from[j % dist] << (8 * j);
+                const uint32_t b0 = from[0], b1 = dist == 1 ? b0 : from[1], b2 = dist == 3 ? from[2] : b0,
+                               b3 = dist == 2 ? b1 : b0;
+                const uint32_t pat = b0 | b1 << 8 | b2 << 16 | b3 << 24;
                 if (dist == 3) {
                     for (uint32_t i = 0; i < len; i++) dst[i] = from[i % 3];
                 } else {
@@ -422,7 +423,7 @@ int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const s
     ICHK(hipMemcpyAsync(D.mem, members, (size_t)n * sizeof(spg_bgzf_member), hipMemcpyHostToDevice, D.st));
     ICHK(hipEventRecord(D.ev[0], D.st));
     // members per block (one per lane, SLICE bytes of LDS each): few per wave diverge less and spread over more SIMDs
-    static const int mpw = [] { const char *e = getenv("SPG_INFLATE_MPW"); const int v = e ? atoi(e) : 8; return v >= 1 && v <= 16 ? v : 8; }();
+    static const int mpw = [] { const char *e = getenv("SPG_INFLATE_MPW"); const int v = e ? atoi(e) : 4; return v >= 1 && v <= 16 ? v : 4; }();
     hipLaunchKernelGGL(spg::k_inflate, dim3((unsigned)((n + mpw - 1) / mpw)), dim3(64), (size_t)mpw * spg::SLICE, D.st, D.comp,
                        D.mem, n, D.out, D.status, mpw);
     ICHK(hipGetLastError());

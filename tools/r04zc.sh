@@ -1,7 +1,7 @@
-# r04zb: LDS-table GPU inflater: tests, kernel time at 4/8/16 members per block, then the deep kernel's per-XCD ends
+# r04zc: LDS-table GPU inflater: tests, kernel time at 4/8/16 members per block, then the deep kernel's per-XCD ends
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-OUT=gpurun_out/${1:-r04zb}; mkdir -p $OUT
+OUT=gpurun_out/${1:-r04zc}; mkdir -p $OUT
 timeout -k 10 300 python3 -u -m pytest tests/test_inflate_gpu.py -x -v --timeout 120 --timeout-method thread > $OUT/tests.txt 2>&1 || { echo "tests failed"; tail -30 $OUT/tests.txt; exit 1; }
 tail -3 $OUT/tests.txt
 for m in 4 2 8; do
