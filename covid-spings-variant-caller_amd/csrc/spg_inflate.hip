@@ -325,8 +325,10 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
 
 // status: 0 ok; 1 bad block type; 2 bad stored length; 3 bad code lengths; 4 bad table; 5 bad symbol;
 // 6 distance too far back; 7 output overrun; 8 input overrun; 9 wrong size.
-// mpw members per block, one per lane (lanes >= mpw idle), each with its SLICE of the block's LDS
-__global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
+// mpw members per block, one per lane (lanes >= mpw idle), each with its SLICE of the block's LDS.  Latency-bound
+// (a member's symbols are a dependent chain): 96 VGPRs for 5 waves per SIMD, 3 members per block (r04ze: 19.3 ms on
+// the 10,000x BAM vs 20.0 at 4 waves, 23.4 at 4 members per block)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_inflate(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
                                                 int64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ status, int mpw) {
     extern __shared__ __align__(16) uint8_t inf_lds[];
     if ((int)threadIdx.x >= mpw) return;
@@ -423,7 +425,7 @@ int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const s
     ICHK(hipMemcpyAsync(D.mem, members, (size_t)n * sizeof(spg_bgzf_member), hipMemcpyHostToDevice, D.st));
     ICHK(hipEventRecord(D.ev[0], D.st));
     // members per block (one per lane, SLICE bytes of LDS each): few per wave diverge less and spread over more SIMDs
-    static const int mpw = [] { const char *e = getenv("SPG_INFLATE_MPW"); const int v = e ? atoi(e) : 4; return v >= 1 && v <= 16 ? v : 4; }();
+    static const int mpw = [] { const char *e = getenv("SPG_INFLATE_MPW"); const int v = e ? atoi(e) : 3; return v >= 1 && v <= 16 ? v : 3; }();
     hipLaunchKernelGGL(spg::k_inflate, dim3((unsigned)((n + mpw - 1) / mpw)), dim3(64), (size_t)mpw * spg::SLICE, D.st, D.comp,
                        D.mem, n, D.out, D.status, mpw);
     ICHK(hipGetLastError());
