@@ -842,8 +842,12 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
     // GPU inflate (spp_set_inflater): the mapped file's bytes copied into pinned staging in parallel, every member
     // inflated on the device (one call: upload, kernel, download into `buf`); members it reports bad — and all of them
     // if the call fails — are inflated here below.  The host's threads are then free for the record scan.
+    // Only BAMs of many members: a member is a dependent chain of ~17k symbols on the GPU (~19 ms however few there
+    // are), the host's threads inflate ~80 members per ms (r04zf); SPP_GPU_INFLATE_MIN overrides the 4096 floor.
+    const char *gme = getenv("SPP_GPU_INFLATE_MIN");
+    const size_t gpu_min = gme ? (size_t)atoll(gme) : (size_t)4096;
     bool gpu_inflated = false;
-    if (const spp_inflate_fn gfn = g_inflate.load(); gfn && nb > 0) {
+    if (const spp_inflate_fn gfn = g_inflate.load(); gfn && nb > 0 && nb >= gpu_min) {
         struct GM { uint64_t coff; uint32_t clen, ulen; uint64_t uoff; };
         std::vector<GM> gm(nb);
         for (size_t i = 0; i < nb; i++) gm[i] = {blks[i].off, (uint32_t)blks[i].clen, (uint32_t)blks[i].ulen, uoff[i]};

@@ -100,7 +100,8 @@ typedef int (*spp_free_fn)(void *p);
 int spp_set_host_allocator(spp_alloc_fn alloc, spp_free_fn release);
 /* BGZF inflater for the records plans (e.g. spg_bgzf_inflate on `device`): called once per BAM with the mapped
  * file, its members ({u64 coff, u32 clen, u32 ulen, u64 uoff}, layout of spg_bgzf_member) and the record buffer;
- * members whose status is not 0 are inflated on the host.  NULL restores the host inflate. */
+ * members whose status is not 0 are inflated on the host.  NULL restores the host inflate.  Used for BAMs of at least
+ * 4096 members (SPP_GPU_INFLATE_MIN): fewer inflate faster on the host's threads. */
 typedef int (*spp_inflate_fn)(int device, const uint8_t *comp, size_t comp_bytes, const void *members, int64_t n,
                               uint8_t *out, size_t out_bytes, uint32_t *status, float *kernel_ms);
 int spp_set_inflater(spp_inflate_fn fn, int device);
