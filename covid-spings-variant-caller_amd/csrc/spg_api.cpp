@@ -668,6 +668,7 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     int64_t n_launch_waves = 0;
     P.t_deep = deep_batch ? 1u : 128u;
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
+    if (const char *e = getenv("SPG_WAVE_ROT")) P.rot = (uint32_t)atoi(e);
     P.n_entries = hb.n_entries;
     P.dbg = trace_on() ? trace_dbg() : nullptr;
     if (list_mode && *list_mode) {

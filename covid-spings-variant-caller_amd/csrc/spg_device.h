@@ -87,6 +87,7 @@ struct KParams {
                            // shorter, so the launch's tail is (w1 = all waves: no split)
     uint32_t t_deep;       // columns with >= t_deep raw entries are processed wave-wide
     uint32_t calls_only;   // SPG_P_CALLS_ONLY
+    uint32_t rot;          // SPG_WAVE_ROT (profiling): block b takes block (b + rot) % grid's work (XCD placement)
     uint64_t n_entries;    // entries of the batch (launch shape only)
     Hist hdesc;            // this batch's history descriptor ...
     Hist *hslot;           // ... written here by the first thread of the launch

@@ -700,7 +700,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     write_hist(P);
     if (FUSE && threadIdx.x == 0) hdl = P.hdesc;
     const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * KW + (threadIdx.x >> 6);
+    const uint32_t bid = P.rot ? (blockIdx.x + P.rot) % gridDim.x : blockIdx.x;
+    const int64_t wave = (int64_t)bid * KW + (threadIdx.x >> 6);
     // deep_list (the long columns of a shallow batch): the waves stride over the listed columns, one
     // column each; otherwise one group of G consecutive columns per wave
     const bool listed = W == 1 && P.deep_n != nullptr;  // (W = 4: compile-time off; the loop runs once)

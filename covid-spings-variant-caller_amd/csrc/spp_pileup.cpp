@@ -851,16 +851,29 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
         struct GM { uint64_t coff; uint32_t clen, ulen; uint64_t uoff; };
         std::vector<GM> gm(nb);
         for (size_t i = 0; i < nb; i++) gm[i] = {blks[i].off, (uint32_t)blks[i].clen, (uint32_t)blks[i].ulen, uoff[i]};
+        auto gms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+        const auto g0 = std::chrono::steady_clock::now();
         HostBuf cb = buf_get(fsz + 64);
+        const auto g1 = std::chrono::steady_clock::now();
         par_chunks(fsz, nt, [&](int, size_t a, size_t b) { memcpy(cb.p + a, m + a, b - a); });
+        const auto g2 = std::chrono::steady_clock::now();
         std::vector<uint32_t> gst(nb, 1);
-        const bool ok_call = gfn(g_inflate_dev.load(), cb.p, fsz, gm.data(), (int64_t)nb, buf, total, gst.data(), nullptr) == 0;
+        float kms = 0.f;
+        const bool ok_call = gfn(g_inflate_dev.load(), cb.p, fsz, gm.data(), (int64_t)nb, buf, total, gst.data(), &kms) == 0;
+        const auto g3 = std::chrono::steady_clock::now();
         buf_put(cb);
+        size_t nbad = nb;
         if (ok_call) {
             gpu_inflated = true;
-            for (size_t i = 0; i < nb; i++)
+            nbad = 0;
+            for (size_t i = 0; i < nb; i++) {
                 if (gst[i] == 0) done[i].store(1, std::memory_order_relaxed);
+                else nbad++;
+            }
         }
+        if (getenv("SPP_TIMING"))
+            fprintf(stderr, "[spp timing] gpu inflate: staging buffer %.1f ms, copy %.1f ms, call %.1f ms (kernel %.1f ms), "
+                    "%zu of %zu members left to the host\n", gms(g0, g1), gms(g1, g2), gms(g2, g3), kms, nbad, nb);
     }
     std::vector<std::thread> pool;
     struct Join { std::vector<std::thread> &v; std::atomic<size_t> &nx; size_t n;
