@@ -12,7 +12,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIBDIR = os.path.join(PKG, "_lib")
 GPU_LIB = os.environ.get("SPG_GPU_LIB") or os.path.join(LIBDIR, "libspings_gpu.so")   # override: A/B builds
-PILEUP_LIB = os.path.join(LIBDIR, "libspings_pileup.so")
+PILEUP_LIB = os.environ.get("SPP_PILEUP_LIB") or os.path.join(LIBDIR, "libspings_pileup.so")   # override: A/B builds
 
 SPG_NSLOT = 5
 SPG_NCOUNT = 8

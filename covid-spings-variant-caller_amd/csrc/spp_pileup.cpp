@@ -711,6 +711,15 @@ template <class Fn> void par_chunks(size_t n, int nt, Fn &&fn) {
     if (err) std::rethrow_exception(err);
 }
 
+// n tasks on up to nt threads (no minimum work per thread, unlike par_chunks: a task here is a whole range)
+template <class Fn> void par_tasks(size_t n, int nt, Fn &&fn) {
+    nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, n));
+    std::atomic<size_t> next{0};
+    par_chunks((size_t)nt * 16384, nt, [&](int, size_t, size_t) {
+        for (size_t i; (i = next++) < n;) fn(i);
+    });
+}
+
 // The BAM mapped, its BGZF members located, inflated in parallel straight into `out` (the helpers take
 // members in file order; this thread scans the records as the inflated prefix grows, inflating members
 // itself while it waits), then the kept records' fixed fields parsed in parallel.  Bases and qualities
@@ -776,9 +785,9 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
         std::vector<std::vector<Blk>> part((size_t)np);
         std::atomic<bool> ok{np > 1};
         if (np > 1) {
-            par_chunks((size_t)np, np, [&](int, size_t t0, size_t t1) {
-                for (size_t t = t0; t < t1; t++) {
-                    if (t == 0) { start[0] = 0; continue; }
+            par_tasks((size_t)np, np, [&](size_t t) {
+                {
+                    if (t == 0) { start[0] = 0; return; }
                     for (size_t q = fsz * t / (size_t)np, e = fsz * (t + 1) / (size_t)np; q < e; q++) {
                         const size_t bs = member(q, nullptr);
                         if (bs && (q + bs == fsz || member(q + bs, nullptr))) { start[t] = q; break; }
@@ -787,8 +796,8 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
             });
             tms = std::chrono::steady_clock::now();
             for (int t = np - 1; t >= 1; t--) start[(size_t)t] = std::min(start[(size_t)t], start[(size_t)t + 1]);
-            par_chunks((size_t)np, np, [&](int, size_t t0, size_t t1) {
-                for (size_t t = t0; t < t1; t++) {
+            par_tasks((size_t)np, np, [&](size_t t) {
+                {
                     size_t q = start[t];
                     Blk bk;
                     while (q < start[t + 1]) {
@@ -929,6 +938,7 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
     // inside a record, a damaged file) the serial scan below walks the stream from the header, as before.
     bool scanned = false;
     const size_t body = cur;
+    auto tps = t0;                               // (SPP_TIMING) start of the parallel record scan
     if ((par_scan || gpu_inflated) && nt > 1 && nb > 0 && total > body + ((size_t)nt << 20) && avail_to(total)) {
         auto rec_len = [&](size_t x) -> size_t {        // plausible record at x: 4 + block_size, else 0
             if (x + 40 > total) return 0;
@@ -944,11 +954,17 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
             if (b[32 + l_name - 1] != 0) return 0;
             return 4 + (size_t)bs;
         };
-        const int np = nt;
+        // np ranges, CH of them per thread: a thread steps its CH chains in turn, so CH record-header loads (each the
+        // next hop of a dependent walk over bytes no CPU cache holds yet) are in flight at once instead of one
+        tps = std::chrono::steady_clock::now();
+        static const int CH = [] { const char *e = getenv("SPP_SCAN_CHAINS"); const int v = e ? atoi(e) : 8; return v >= 1 && v <= 32 ? v : 8; }();
+        const int np = total > body + ((size_t)nt * (size_t)CH << 20) ? nt * CH : nt;
+        const int ch = np / nt;
         std::vector<size_t> start((size_t)np + 1, total);
         start[0] = body;
-        par_chunks((size_t)np, np, [&](int, size_t t0_, size_t t1_) {
-            for (size_t t = std::max<size_t>(t0_, 1); t < t1_; t++) {
+        par_tasks((size_t)np - 1, nt, [&](size_t t1) {
+            {
+                const size_t t = t1 + 1;
                 const size_t b0 = body + (total - body) * t / (size_t)np, lim = std::min(total, b0 + ((size_t)1 << 20));
                 for (size_t x = b0; x < lim; x++) {
                     size_t y = x;
@@ -966,25 +982,32 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
         std::vector<Vec<uint64_t>> part((size_t)np);
         std::vector<int64_t> first_pos((size_t)np, INT64_MAX), last_p((size_t)np, -1);
         std::atomic<bool> ok{true}, unsorted{false};
-        par_chunks((size_t)np, np, [&](int, size_t t0_, size_t t1_) {
-            for (size_t t = t0_; t < t1_; t++) {
-                size_t q = start[t];
-                int64_t lp = -1;
-                while (q < start[t + 1]) {
-                    const uint32_t bs = rdu32(buf + q);
-                    if (bs < 32 || q + 4 + (size_t)bs > total) { ok = false; break; }
-                    const uint8_t *b = buf + q + 4;
-                    if (rd32(b) == tid) {
-                        const int64_t pos = rd32(b + 4);
-                        if (pos < lp) unsorted = true;
-                        if (first_pos[t] == INT64_MAX) first_pos[t] = pos;
-                        lp = pos;
-                        if (stepper_keeps(p, rdu16(b + 14), b[9])) part[t].push_back(q + 4);
+        par_tasks((size_t)nt, nt, [&](size_t w) {
+            {
+                const size_t r0 = w * (size_t)ch;
+                size_t q[32];
+                int64_t lp[32];
+                int live = 0;
+                for (int j = 0; j < ch; j++) { q[j] = start[r0 + (size_t)j]; lp[j] = -1; live += q[j] < start[r0 + (size_t)j + 1]; }
+                while (live > 0) {
+                    for (int j = 0; j < ch; j++) {
+                        const size_t t = r0 + (size_t)j, qq = q[j];
+                        if (qq >= start[t + 1]) continue;
+                        const uint32_t bs = rdu32(buf + qq);
+                        if (bs < 32 || qq + 4 + (size_t)bs > total) { ok = false; q[j] = start[t + 1] + 1; live--; continue; }
+                        const uint8_t *b = buf + qq + 4;
+                        if (rd32(b) == tid) {
+                            const int64_t pos = rd32(b + 4);
+                            if (pos < lp[j]) unsorted = true;
+                            if (first_pos[t] == INT64_MAX) first_pos[t] = pos;
+                            lp[j] = pos;
+                            if (stepper_keeps(p, rdu16(b + 14), b[9])) part[t].push_back(qq + 4);
+                        }
+                        q[j] = qq + 4 + (size_t)bs;
+                        if (q[j] >= start[t + 1]) { live--; if (q[j] != start[t + 1]) ok = false; }
                     }
-                    q += 4 + (size_t)bs;
                 }
-                last_p[t] = lp;
-                if (q != start[t + 1]) ok = false;
+                for (int j = 0; j < ch; j++) last_p[r0 + (size_t)j] = lp[j];
             }
         });
         if (ok) {
@@ -1053,12 +1076,13 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
     });
     for (int64_t v : spans) R.max_span = std::max(R.max_span, v);
     if (timing)
-        fprintf(stderr, "[spp timing] read_bam_raw: %zu members, map %.1f ms + search %.1f ms + members %.1f ms, buffer %.1f ms, inflate+scan %.1f ms, "
-                "fields %.1f ms\n", nb, std::chrono::duration<double, std::milli>(tmm - tm0).count(),
+        fprintf(stderr, "[spp timing] read_bam_raw: %zu members, map %.1f ms + search %.1f ms + members %.1f ms, buffer %.1f ms, inflate+scan %.1f ms "
+                "(parallel scan %.1f ms), fields %.1f ms\n", nb, std::chrono::duration<double, std::milli>(tmm - tm0).count(),
                 std::chrono::duration<double, std::milli>(tms - tmm).count(),
                 std::chrono::duration<double, std::milli>(tm1 - tms).count(),
                 std::chrono::duration<double, std::milli>(tm2 - tm1).count(),
                 std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                scanned ? std::chrono::duration<double, std::milli>(t1 - tps).count() : 0.0,
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count());
     return total;
 }

@@ -213,8 +213,8 @@ print(r.pos_begin, r.n_cols, r.n_entries, r.n_reads, h.hexdigest())
 @pytest.mark.parametrize("max_depth", [8000, 0])
 def test_parallel_record_scan_equals_serial(tmp_path, max_depth):
     """The records plan's record boundaries found in parallel (validated chains per range that must meet exactly,
-    csrc/spp_pileup.cpp read_bam_raw) give the plan the serial block_size walk gives (SPP_PAR_SCAN=0): a BAM of
-    ~80 MB inflated (2,000x over 30 kb, 150-bp reads with D/I), 8 threads."""
+    csrc/spp_pileup.cpp read_bam_raw; each thread steps several ranges' chains in turn) give the plan the serial
+    block_size walk gives (SPP_PAR_SCAN=0): a BAM of ~80 MB inflated (2,000x over 30 kb, 150-bp reads with D/I), 8 threads."""
     import os
     import subprocess
     import sys
@@ -225,11 +225,12 @@ def test_parallel_record_scan_equals_serial(tmp_path, max_depth):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     here = os.path.dirname(os.path.abspath(__file__))
     out = {}
-    for par in ("1", "0"):
-        env = dict(os.environ, SPP_PAR_SCAN=par, PYTHONPATH=here)
+    # ("1:c": the parallel scan with c chains stepped in turn per thread — 8 by default, so 64 ranges here)
+    for par in ("1", "1:3", "0"):
+        env = dict(os.environ, SPP_PAR_SCAN=par[0], SPP_SCAN_CHAINS=par[2:] or "8", PYTHONPATH=here)
         r = subprocess.run([sys.executable, "-c", _SCAN_CHILD, root, bam, "NC_045512.2", str(max_depth)], env=env,
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr
         out[par] = r.stdout.strip().splitlines()[-1]
-    assert out["1"] == out["0"]
+    assert out["1"] == out["0"] == out["1:3"]
     assert int(out["1"].split()[3]) > 300_000
