@@ -731,8 +731,9 @@ def end_to_end(args, device):
         res[tag] = {"bams": n_bams, "positions_per_s_per_bam": n_bams * L_SARS / (t1 - t0),
                     "s_per_bam": (t1 - t0) / n_bams, "ingest_s": t_in, "finalize_s": t1 - t0 - t_in,
                     "calls": len(calls), "entries_per_bam": int(E),
-                    "path": "device pileup: host inflate + record scan + depth cap (spp_pileup_plan_records) -> "
-                            "pinned inflated BAM -> H2D -> k_pileup_fill (decode + CIGAR walk) -> accumulate",
+                    "path": "device pileup: BGZF inflate (" + ("GPU, k_inflate" if caller._gpu_inflate else "host") +
+                            ") + record scan + depth cap (spp_pileup_plan_records) -> pinned inflated BAM -> H2D -> "
+                            "k_pileup_fill (decode + CIGAR walk) -> accumulate",
                     "breakdown_one_bam": {"host_plan_records_s": b1 - b0, "inflated_mb": data_mb,
                                           "h2d_records_plus_gpu_s": g1 - g0,
                                           "pcie_inclusive_gpu_positions_per_s": L_SARS / (g1 - g0)},

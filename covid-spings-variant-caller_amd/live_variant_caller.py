@@ -178,18 +178,17 @@ class LiveVariantCaller:
         # walks the CIGARs (spg_accumulate_records); the host keeps the read filter, depth cap and overlap
         # tweak.  SPG_DEVICE_PILEUP=0 selects the host fill (SAM input always uses it).
         self.device_pileup = os.environ.get("SPG_DEVICE_PILEUP", "1") != "0"
-        self._gpu_inflate, self.last_gpu_inflate = "", False
+        self._gpu_inflate, self.last_gpu_inflate = False, False
         if self.device_pileup:
             N.use_pinned_records()
-            # BGZF members inflated on the GPU (spg_bgzf_inflate; BAMs of >= 4096 members): the host's threads then
-            # only scan the records and take the read decisions.  process_bams turns it on for its run (two plans at
-            # once: one's inflate on the GPU overlaps the other's scan — 5.3e5 vs 4.0e5 positions/s per 10,000x BAM,
-            # profiles/r04zf); a lone process_bam keeps the host inflate (3.7e5 vs 3.3e5: its PCIe round trip of the
-            # inflated bytes is not hidden).  SPG_GPU_INFLATE=1 / 0 forces it on / off everywhere.
-            self._gpu_inflate = os.environ.get("SPG_GPU_INFLATE", "")
+            # BGZF members inflated on the GPU (spg_bgzf_inflate; BAMs of >= 4096 members, SPP_GPU_INFLATE_MIN): the
+            # host's threads then only scan the records (in parallel) and take the read decisions.  Faster for a lone
+            # process_bam (3.8e5 vs 3.5e5 positions/s per 10,000x BAM) and for process_bams (two plans at once: one's
+            # inflate on the GPU overlaps the other's scan, 5.3-5.9e5 vs 4.0e5), profiles/r04zp, r04zn, r04zf.
+            # SPG_GPU_INFLATE=0 keeps the host inflate.  (The hook is process-wide: the last caller constructed decides.)
+            self._gpu_inflate = os.environ.get("SPG_GPU_INFLATE", "") != "0"
             self._inflate_dev = device if device is not None else 0
-            if self._gpu_inflate == "1":
-                N.use_gpu_inflate(self._inflate_dev)
+            N.use_gpu_inflate(self._inflate_dev, on=self._gpu_inflate)
         self._inflight = collections.deque()     # (input ticket, records plan) whose copy may still be running
         self.reset_memory()
 
@@ -282,22 +281,15 @@ class LiveVariantCaller:
                 return bam.pileup_plan(contig, params)
 
         window = workers + 1                  # plans in flight (each holds its BAM's inflated records, ~0.5 GB at 10,000x)
-        gpu_inflate = self.device_pileup and self._gpu_inflate == "" and workers > 1
-        self.last_gpu_inflate = gpu_inflate or (self.device_pileup and self._gpu_inflate == "1")
-        if gpu_inflate:
-            N.use_gpu_inflate(self._inflate_dev)
-        try:
-            with ThreadPoolExecutor(workers) as ex:
-                pending = [ex.submit(plan, p) for p in paths[:window]]
-                for i in range(len(paths)):
-                    batch = pending[i].result()
-                    if i + window < len(paths):
-                        pending.append(ex.submit(plan, paths[i + window]))
-                    pending[i] = None
-                    self._accumulate_plan(batch, referenceIndex)
-        finally:
-            if gpu_inflate:
-                N.use_gpu_inflate(self._inflate_dev, on=False)
+        self.last_gpu_inflate = self.device_pileup and self._gpu_inflate
+        with ThreadPoolExecutor(workers) as ex:
+            pending = [ex.submit(plan, p) for p in paths[:window]]
+            for i in range(len(paths)):
+                batch = pending[i].result()
+                if i + window < len(paths):
+                    pending.append(ex.submit(plan, paths[i + window]))
+                pending[i] = None
+                self._accumulate_plan(batch, referenceIndex)
 
     def _accumulate_plan(self, batch, referenceIndex):
         with self._lock:

@@ -277,15 +277,17 @@ def test_pinned_ingest_stream_vs_oracle(planted):
     assert list(mem) == list(omem) and all(mem[p] == omem[p] for p in omem)
 
 
-@pytest.mark.parametrize("gpu_inflate_min", [None, "1"])
+@pytest.mark.parametrize("gpu_inflate_min", [None, "1", "host"])
 def test_process_bams_equals_sequential_process_bam(tmp_path, monkeypatch, gpu_inflate_min):
     """process_bams (the many-BAM ingest: plans on a thread pool, accumulated in order, counted at
     prepare_variants) == one process_bam per BAM == the oracle, on 7 BAMs whose depth caps bind and whose
     first visits differ (BAM 3 covers a region no earlier BAM does), then more BAMs after a prepare_variants.
-    gpu_inflate_min "1": process_bams inflates every BAM's members on the GPU (spg_bgzf_inflate; by default only
-    BAMs of >= 4096 members)."""
+    gpu_inflate_min "1": every BAM's members are inflated on the GPU (spg_bgzf_inflate; by default only BAMs of
+    >= 4096 members); "host": SPG_GPU_INFLATE=0, every BAM inflated on the host whatever its size."""
     if gpu_inflate_min:
-        monkeypatch.setenv("SPP_GPU_INFLATE_MIN", gpu_inflate_min)
+        monkeypatch.setenv("SPP_GPU_INFLATE_MIN", "1")
+    if gpu_inflate_min == "host":
+        monkeypatch.setenv("SPG_GPU_INFLATE", "0")
     L = 900
     ref = _ref(L, 31)
     fasta = str(tmp_path / "ref.fa")
