@@ -16,4 +16,9 @@ for pass in FETCH_SIZE WRITE_SIZE; do
       python3 $ROOT/tools/e2e_only.py 2 0 16 > $OUT/e2e_pmc$i.log 2>&1 || { echo "e2e pmc $pass failed"; tail -20 $OUT/e2e_pmc$i.log; exit 1; }
 done
 bash $ROOT/tools/prof_bench.sh gpurun_out/${1:-r04zr}/main || { echo "prof_bench failed"; exit 1; }
-find $OUT -name "*kernel_stats.csv" | head
+
+python3 $ROOT/tools/prof_sum.py $OUT > $OUT/summary.txt 2>&1
+# keep the summaries only (the traces exceed what gpurun copies back)
+find $OUT -name "*.csv" ! -name "*kernel_stats.csv" -delete
+find $OUT -name "*.log" -size +1M -delete
+cat $OUT/summary.txt
