@@ -16,7 +16,12 @@ Also on the same line (nested, never `value`), one per BASELINE config:
   vc_queue.py:142-144 (``per_bam_finalize``), and the column-major layout as an aside; coordinate-sharded over
   the N ranks (each rank: its range of every BAM);
 * ``chr1_30x`` (config 5);
+* ``multi_device``: the drop-in's own multi-GPU path (spg_multi, one process over devices 0..N-1: the same N stacked
+  samples cut at equal entries, one ncclGather per step) — run by rank 0 while the other ranks wait (always at N > 1);
 * ``end_to_end`` (host BAM -> calls) and ``cpu_baseline`` (the oracle restatements on host cores).
+
+``--gpus N`` without a launcher (no WORLD_SIZE in the environment) starts N rank processes of this script before
+anything touches a GPU (127.0.0.1 rendezvous), as ``torch.distributed.run --nproc-per-node N`` would.
 
 Timing: W untimed warm-up steps; then 20 measurements, each of K steps (K = max(--steps, enough
 steps for >= 100 ms)) between barrier + device synchronize, max over ranks; the median measurement is
@@ -74,7 +79,7 @@ def parse():
     ap.add_argument("--e2e-many", type=int, default=64,
                     help="config 4 end to end: 100x SARS-CoV-2 BAM files through process_bams (0 = skip)")
     ap.add_argument("--full-table", action="store_true", help="also accumulate every table GL term")
-    ap.add_argument("--legs", default="parity,sars1k,sars100k,sars100k_capped,config4,chr1,e2e,cpu",
+    ap.add_argument("--legs", default="parity,sars1k,sars100k,sars100k_capped,config4,chr1,multi,e2e,cpu",
                     help="nested legs of the default sars10k line (comma list; 'none' = the main point only)")
     ap.add_argument("--no-main", action="store_true", help="profiling: skip the main point (nested legs only)")
     ap.add_argument("--sars1k-samples", type=int, default=64, help="stacked samples per GPU step at 1,000x")
@@ -91,17 +96,64 @@ WORKLOADS = {   # BASELINE.json configs (the metric is quoted on sars10k)
 }
 
 
+def rank_envs(n: int, port: int, base=None):
+    """The environments of n local ranks (what torch.distributed.run exports), rendezvous on 127.0.0.1:port."""
+    base = dict(os.environ if base is None else base)
+    return [dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port)) for r in range(n)]
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE): start N rank processes of this script — one per
+    GPU, before this process has touched any GPU — and return the first failing exit code (0 when all succeed).
+    Rank 0 prints the JSON line on the inherited stdout.  If one rank fails, the others are terminated (by PID)."""
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env)
+             for env in rank_envs(n, free_port())]
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                r = p.poll()
+                if r is None:
+                    continue
+                pending.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    for q in pending:
+                        q.terminate()
+            if pending:
+                time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
 class Dist:
-    """torch.distributed helpers (no-ops at N = 1)."""
+    """torch.distributed helpers (no-ops at N = 1).  Beside the data path's group (RCCL for nccl), a gloo group for
+    host-side waits: ranks that sit out a leg rank 0 runs on every device (spg_multi) wait there, not in an RCCL
+    collective that would hold a kernel on their GPU."""
 
     def __init__(self, world, rank, backend, device):
         self.world, self.rank, self.backend, self.device = world, rank, backend, device
         self.dist = None
+        self.cpu_group = None
         if world > 1:
             import torch
             import torch.distributed as dist
             if backend == "nccl":
                 dist.init_process_group("nccl", device_id=device)
+                self.cpu_group = dist.new_group(backend="gloo")
             else:
                 dist.init_process_group(backend)
             self.dist = dist
@@ -110,6 +162,17 @@ class Dist:
     def barrier(self):
         if self.dist is not None:
             self.dist.barrier()
+
+    def host_barrier(self):
+        if self.dist is not None:
+            self.dist.barrier(group=self.cpu_group)
+
+    def all_gather_object(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj, group=self.cpu_group)
+        return out
 
     def max(self, x: float) -> float:
         if self.dist is None:
@@ -375,6 +438,125 @@ def run_point(args, D, L, depth, max_depth, local, world, rank, contig, samples=
         "finalize_ms": fin, "n_cand": n_cand, "n_replay": n_replay, "gathered": gathered,
         "host_enqueue_ms_per_step": measure.host_enqueue_ms_per_step,
     }
+
+
+def multi_devices(world: int, backend: str):
+    """The devices rank 0's spg_multi leg spans: one per rank (0..N-1); with a non-RCCL backend on fewer GPUs (a
+    functional run of the N > 1 path) the ranks' devices modulo the GPUs present, as the ranks themselves map them."""
+    import torch
+    n_dev = max(1, torch.cuda.device_count())
+    return [d if backend == "nccl" else d % n_dev for d in range(world)]
+
+
+def run_multi_device(args, world, L, depth, max_depth):
+    """The drop-in's own multi-GPU path (LiveVariantCaller(devices=...) -> multi.MultiEngine -> spg_multi_*), driven
+    by ONE process over devices 0..N-1: the same weak-scaling step as the main point — N samples stacked into one
+    coordinate space of N x L positions, cut at equal entries (spg_multi_plan), each device holding its slice in its
+    own HBM — with reset + spg_multi_accumulate_slices (borrowed) + spg_multi_finalize + spg_multi_get_candidates (the
+    merged call table: one ncclGather over xGMI to devices[0] when the devices are distinct, device copies when one GPU
+    stands in for several) per step.  Unlike the per-rank path, every step ends with the table on the host (what
+    prepare_variants returns), so the host's launch and gather latency are inside the step."""
+    import torch
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.multi import MultiEngine
+    from covid_spings_variant_caller_amd.pileup import synth_batch
+    devices = multi_devices(world, args.backend)
+    ref = synth.reference(L, seed=1)
+    t0 = time.perf_counter()
+    distinct = min(world, 2)
+    threads = min(16, len(os.sched_getaffinity(0)))
+    gen = []
+    for s in range(distinct):
+        b = synth_batch(ref, depth, lo=0, hi=L, seed=2 + s, n_threads=threads, max_depth=max_depth)
+        gen.append((b.offsets.astype(np.uint64).copy(), b.codes.copy(), b.quals.copy()))
+        b.close()
+    samples = [gen[s % distinct] for s in range(world)]
+    full_off = np.zeros(world * L + 1, np.uint64)
+    base = 0
+    for s, (o, _, _) in enumerate(samples):
+        full_off[s * L + 1:(s + 1) * L + 1] = o[1:] + np.uint64(base)
+        base += int(o[-1])
+    E = base
+    mm = MultiEngine(devices, world * L, 30, 10, 5, 0.10, reference=ref * world, calls_only=True)
+    cuts = mm.plan(0, full_off)
+    slices, hold = [], []
+    for d, dev in enumerate(devices):
+        lo, hi = int(cuts[d]), int(cuts[d + 1])
+        pc, pq, lens = [], [], []
+        for s in range(world):
+            a, b = max(lo, s * L), min(hi, (s + 1) * L)
+            if b <= a:
+                continue
+            o, c, q = samples[s]
+            pc.append(c[int(o[a - s * L]):int(o[b - s * L])])
+            pq.append(q[int(o[a - s * L]):int(o[b - s * L])])
+            lens.append(np.diff(o[a - s * L:b - s * L + 1].astype(np.int64)))
+        tdev = torch.device("cuda", dev)
+        off_d = np.zeros(hi - lo + 1, np.uint64)
+        np.cumsum(np.concatenate(lens), out=off_d[1:])
+        pad = np.zeros(16, np.uint8)
+        t_off = torch.from_numpy(off_d.view(np.int64)).to(tdev)
+        t_c = torch.from_numpy(np.concatenate(pc + [pad + 0xFF])).to(tdev)
+        t_q = torch.from_numpy(np.concatenate(pq + [pad])).to(tdev)
+        slices.append((lo, t_off, t_c, t_q))
+        hold.append((t_off, t_c, t_q))
+    del gen, samples
+    for dev in set(devices):
+        torch.cuda.synchronize(dev)
+    t_gen = time.perf_counter() - t0
+
+    def step():
+        mm.reset()
+        mm.accumulate_slices(0, full_off, slices, borrow=True)
+        mm.finalize()
+        return mm.candidates()
+
+    calls = step()
+    assert np.array_equal(mm.partition(), cuts), "spg_multi re-planned the stacked sample's cuts"
+    for _ in range(max(1, args.warmup)):
+        step()
+    mm.sync()
+    t = time.perf_counter()
+    for _ in range(3):
+        step()
+    est = (time.perf_counter() - t) / 3
+    K = max(args.steps, int(math.ceil(args.min_ms * 1e-3 / max(est, 1e-7))))
+    mm.kernel_times()
+    mm.set_timing(1)
+    times, kern = [], []
+    for _ in range(max(5, args.reps // 2)):
+        mm.sync()
+        t = time.perf_counter()
+        for _ in range(K):
+            step()
+        mm.sync()
+        times.append(time.perf_counter() - t)
+        per_dev = [a for a, _ in mm.kernel_times()]
+        n = min(len(a) for a in per_dev)
+        if n:
+            kern.extend(np.max(np.stack([a[-n:] for a in per_dev]), axis=0).tolist())   # slowest device per step
+    mm.set_timing(0)
+    med = float(np.median(times))
+    t_k = float(np.mean(kern)) * 1e-3 if kern else float("nan")
+    algo = 2 * E + 8 * (world * L + len(devices)) + world * L + 56 * len(calls)
+    per_dev_bytes = algo / len(devices)
+    mm.close()
+    del slices, hold
+    torch.cuda.empty_cache()
+    return {"workload": f"{world} samples x {L} positions at {depth:.0f}x ({'uncapped' if not max_depth else f'max_depth {max_depth}'}) "
+                        f"stacked into one spg_multi coordinate space, sliced at equal-entry cuts, slices resident in "
+                        f"each device's HBM (borrowed)",
+            "devices": devices, "rccl": len(set(devices)) == len(devices) and len(devices) > 1,
+            "cuts": [int(x) for x in cuts], "value": world * L * K / med, "unit": "positions/s",
+            "ms_per_step": med / K * 1e3, "steps": K * len(times), "steps_per_measurement": K,
+            "measurement_ms": [round(x * 1e3, 3) for x in times], "entries_per_step": E, "datagen_s": t_gen,
+            "calls_per_step": len(calls),
+            "step": "spg_multi_reset + spg_multi_accumulate_slices + spg_multi_finalize + spg_multi_get_candidates "
+                    "(call table merged on the host)",
+            "kernel_ms_slowest_device": t_k * 1e3,
+            "roofline": {"bound": "hbm", "achieved": per_dev_bytes / t_k / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                         "frac": per_dev_bytes / t_k / PEAK_HBM,
+                         "frac_basis": "mean bytes per device / slowest device's accumulate kernel"}}
 
 
 def nested_point(args, D, workload, local, world, rank, max_depth=0, samples=1, distinct=None, step_frac=False):
@@ -790,6 +972,9 @@ def main():
     if args.no_e2e: legs.discard("e2e")
     if args.no_cpu_baseline: legs.discard("cpu")
     if args.many_batches <= 0 and args.runs_batches <= 0: legs.discard("config4")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: one rank process per GPU, started before anything here touches a GPU
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     import torch
     import spings  # noqa: F401
     if not args.e2e_threads:
@@ -799,10 +984,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and rank == 0:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}: timing {world} rank(s)", file=sys.stderr)
     if args.backend != "nccl":                  # functional runs of the N > 1 path on fewer GPUs
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     D = Dist(world, rank, args.backend, torch.device("cuda", local))
+    props = torch.cuda.get_device_properties(local)
+    rank_devices = D.all_gather_object({"rank": rank, "device": local, "pci_bus_id": getattr(props, "pci_bus_id", None),
+                                        "name": props.name})
 
     if args.workload == "sars_many":
         c4 = run_config4(args, D, local, world, rank)
@@ -840,6 +1030,9 @@ def main():
                                + ", 1 sample per GPU per step (coordinate-sharded)",
                    "positions_per_step": world * L, "entries_per_gpu_step": E, "columns_per_gpu": C,
                    "parallelism": f"coord-shard x{world}",
+                   "ranks": rank_devices,
+                   "collective": (f"torch.distributed {args.backend} ({'RCCL over xGMI' if args.backend == 'nccl' else 'host'}) "
+                                  f"gather of the call tables to rank 0, one per step" if world > 1 else "none (N = 1)"),
                    "engine_mode": "full_table" if args.full_table else "calls_only"},
         "timing": {"measurements": len(main_pt["measurements_ms"]), "steps_per_measurement": main_pt["steps"],
                    "steps_timed_total": main_pt["steps"] * main_pt["reps"],
@@ -871,6 +1064,16 @@ def main():
         res["config4"] = run_config4(args, D, local, world, rank)
     if "chr1" in legs and nested:             # BASELINE config 5
         res["chr1_30x"] = nested_point(args, D, "chr1_30x", local, world, rank, step_frac=True)
+    if ("multi" in legs or world > 1) and not args.no_main and args.workload != "sars_many":
+        # the drop-in's one-process multi-GPU path over devices 0..N-1 (always with N > 1), on rank 0 while the other
+        # ranks wait on the host
+        D.host_barrier()
+        if rank == 0:
+            try:
+                res["multi_device"] = run_multi_device(args, world, L, depth, args.max_depth)
+            except Exception as e:        # (reported, never fatal to the per-rank line)
+                res["multi_device"] = {"error": f"{type(e).__name__}: {e}"}
+        D.host_barrier()
     if rank == 0 and world == 1 and "e2e" in legs and L == L_SARS:
         res["end_to_end"] = end_to_end(args, 0)
     if rank == 0 and world == 1 and "cpu" in legs:

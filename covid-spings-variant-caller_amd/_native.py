@@ -11,8 +11,8 @@ import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIBDIR = os.path.join(PKG, "_lib")
-GPU_LIB = os.environ.get("SPG_GPU_LIB") or os.path.join(LIBDIR, "libspings_gpu.so")   # override: A/B builds
-PILEUP_LIB = os.environ.get("SPP_PILEUP_LIB") or os.path.join(LIBDIR, "libspings_pileup.so")   # override: A/B builds
+GPU_LIB = os.path.join(LIBDIR, "libspings_gpu.so")
+PILEUP_LIB = os.path.join(LIBDIR, "libspings_pileup.so")
 
 SPG_NSLOT = 5
 SPG_NCOUNT = 8
@@ -111,6 +111,8 @@ def gpu_lib():
     _sig(L.spg_multi_partition, i32, vp, C.POINTER(i64))
     _sig(L.spg_multi_context, i32, vp, i32, C.POINTER(vp))
     _sig(L.spg_multi_accumulate_records, i32, vp, C.POINTER(SpgRecords), C.c_uint32)
+    _sig(L.spg_multi_plan, i32, vp, i64, i64, vp, C.POINTER(i64))
+    _sig(L.spg_multi_accumulate_slices, i32, vp, i64, i64, vp, vp, C.c_uint32)
     _sig(L.spg_multi_wait_input, i32, vp)
     _sig(L.spg_multi_set_rebalance, i32, vp, C.c_double, i64)
     _sig(L.spg_multi_replans, i32, vp, C.POINTER(i64))
@@ -118,10 +120,9 @@ def gpu_lib():
     _sig(L.spg_set_history_cap, i32, vp, i64)
     _sig(L.spg_history_resident, i32, vp, C.POINTER(i64), C.POINTER(i64), C.POINTER(i64))
     _sig(L.spg_path_counters, i32, vp, C.POINTER(i64), i64)
-    if hasattr(L, "spg_bgzf_inflate"):              # (older A/B builds loaded through SPG_GPU_LIB lack it)
-        _sig(L.spg_bgzf_inflate, i32, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp, C.POINTER(C.c_float))
-        _sig(L.spg_bgzf_last_error, C.c_char_p)
-        _sig(L.spg_bgzf_inflate_check, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp)
+    _sig(L.spg_bgzf_inflate, i32, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp, C.POINTER(C.c_float))
+    _sig(L.spg_bgzf_last_error, C.c_char_p)
+    _sig(L.spg_bgzf_inflate_check, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp)
     _sig(L.spg_position_entries, i32, vp, i64, vp, vp, i64, C.POINTER(i64))
     _sig(L.spg_input_ticket, i32, vp, C.POINTER(u64))
     _sig(L.spg_wait_ticket, i32, vp, u64)
@@ -140,6 +141,7 @@ def gpu_lib():
     _sig(L.spg_history_count, i32, vp, C.POINTER(i64))
     _sig(L.spg_history_info, i32, vp, i64, C.POINTER(i64), C.POINTER(i64), C.POINTER(u64))
     _sig(L.spg_history_copy, i32, vp, i64, vp, vp, vp)
+    _sig(L.spg_history_copy_compact, i32, vp, i64, i32, vp, vp, vp, C.POINTER(u64))
     _sig(L.spg_device_count, i32, C.POINTER(i32))
     _sig(L.spg_sizeof_candidate, C.c_size_t)
     _sig(L.spg_sizeof_detail, C.c_size_t)

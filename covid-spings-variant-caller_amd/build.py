@@ -21,16 +21,34 @@ LIBDIR = os.path.join(PKG, "_lib")
 INC = os.path.join(ROOT, "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-GPU_SOURCES = ["spg_kernels.hip", "spg_tile.hip", "spg_lite.hip", "spg_fill.hip", "spg_inflate.hip", "spg_api.cpp", "spg_multi.cpp"]
+GPU_SOURCES = ["spg_kernels.hip", "spg_tile.hip", "spg_lite.hip", "spg_fill.hip", "spg_inflate.hip", "spg_ckpt.hip", "spg_api.cpp", "spg_multi.cpp"]
 GPU_HEADERS = ["spg_device.h", "spg_common.h"]
 PILEUP_SOURCES = ["spp_pileup.cpp"]
 
 
-def _stale(out, deps):
-    if not os.path.exists(out):
+def _digest(deps, cmd) -> str:
+    """Content hash of a build step: its inputs' bytes and its command line."""
+    import hashlib
+    h = hashlib.sha256(" ".join(cmd).encode())
+    for d in deps:
+        with open(d, "rb") as f:
+            h.update(os.path.basename(d).encode() + b"\0" + f.read())
+    return h.hexdigest()
+
+
+def _stale(out, deps, cmd=()):
+    """An output is rebuilt when it is missing or when its recorded input hash (`<out>.sha256`) differs from the
+    inputs' and command's now: content, not mtimes (the snapshot that travels to the GPU box keeps mtimes it did
+    not produce)."""
+    if not os.path.exists(out) or not os.path.exists(out + ".sha256"):
         return True
-    t = os.path.getmtime(out)
-    return any(os.path.getmtime(d) > t for d in deps)
+    with open(out + ".sha256") as f:
+        return f.read().strip() != _digest(deps, cmd)
+
+
+def _stamp(out, deps, cmd=()):
+    with open(out + ".sha256", "w") as f:
+        f.write(_digest(deps, cmd))
 
 
 def _run(cmd):
@@ -53,7 +71,7 @@ def build_gpu(force=False, verbose=False) -> str:
     jobs = []
     for f in GPU_SOURCES:
         src, obj = os.path.join(CSRC, f), os.path.join(objdir, f + ".o")
-        if force or _stale(obj, [src] + hdrs):
+        if force or _stale(obj, [src] + hdrs, base):
             jobs.append(base + ["-c", src, "-o", obj + ".tmp", "-Rpass-analysis=kernel-resource-usage"])
     objs = [os.path.join(objdir, f + ".o") for f in GPU_SOURCES]
 
@@ -61,7 +79,10 @@ def build_gpu(force=False, verbose=False) -> str:
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = _run(cmd)
-        os.replace(cmd[-2], cmd[-2][:-4])
+        obj = cmd[-2][:-4]
+        os.replace(cmd[-2], obj)
+        src = cmd[cmd.index("-c") + 1]
+        _stamp(obj, [src] + hdrs, base)
         return r.stderr
 
     res_path = os.path.join(LIBDIR, "kernel_resources.json")
@@ -85,13 +106,14 @@ def build_gpu(force=False, verbose=False) -> str:
         for k, v in new.items():
             if v.get("scratch", 0) and any(h in k for h in HOT_KERNELS):
                 print(f"WARNING: hot kernel {k} spills to scratch ({v['scratch']} B/lane)", file=sys.stderr)
-    if force or jobs or _stale(out, objs):
-        # (-z defs: a kernel launcher the C-ABI declares but no source defines fails the build, not the load)
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-Wl,-z,defs", "-o", out + ".tmp"] + objs + ["-lrccl"]
+    # (-z defs: a kernel launcher the C-ABI declares but no source defines fails the build, not the load)
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-Wl,-z,defs", "-o", out + ".tmp"] + objs + ["-lrccl"]
+    if force or jobs or _stale(out, objs, cmd):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         _run(cmd)
         os.replace(out + ".tmp", out)
+        _stamp(out, objs, cmd)
     return out
 
 
@@ -131,13 +153,14 @@ def build_pileup(force=False, verbose=False) -> str:
     if not all(os.path.exists(s) for s in srcs):
         return ""
     deps = srcs + [os.path.join(INC, "spings_pileup.h"), os.path.join(INC, "spings_gpu.h")]
-    if force or _stale(out, deps):
-        cxx = shutil.which("g++") or "g++"
-        cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{INC}", "-o", out + ".tmp"] + srcs + ["-lz", "-ldl", "-pthread"]
+    cxx = shutil.which("g++") or "g++"
+    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-I{INC}", "-o", out + ".tmp"] + srcs + ["-lz", "-ldl", "-pthread"]
+    if force or _stale(out, deps, cmd):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         _run(cmd)
         os.replace(out + ".tmp", out)
+        _stamp(out, deps, cmd)
     return out
 
 
@@ -146,4 +169,4 @@ def build_all(force=False, verbose=False):
 
 
 if __name__ == "__main__":
-    print(build_all(force="--force" in sys.argv, verbose=True))
+    print(build_all(force="--force" in sys.argv or os.environ.get("SPG_FORCE_BUILD") == "1", verbose=True))

@@ -42,6 +42,8 @@ hipError_t launch_pileup_fill(const FillArgs &A, hipStream_t st);
 hipError_t launch_pos_bounds(const Hist *H, const int32_t *items, int32_t n, int64_t pos, uint64_t *rng, hipStream_t st);
 hipError_t launch_pos_copy(const Hist *H, const int32_t *items, int32_t n, const uint64_t *rng, const uint64_t *dst,
                            uint8_t *oc, uint8_t *oq, hipStream_t st);
+hipError_t launch_ck_compact(const Hist &h, uint32_t min_bq, uint64_t *kept, uint64_t *noff, void *scan_tmp,
+                             size_t *scan_bytes, uint8_t *oc, uint8_t *oq, hipStream_t st);
 }  // namespace spg
 
 using namespace spg;
@@ -1869,6 +1871,18 @@ int spg_path_counters(spg_ctx *c, int64_t *out, int64_t n) {
     return 0;
 }
 
+// The context's device scratch for the history readers (spg_position_entries, spg_history_copy_compact): grow-only,
+// doubled when it grows (a lookup no longer allocates and frees per call)
+static int grow_scratch(spg_ctx *c, size_t need) {
+    if (need <= c->pe_cap) return 0;
+    if (c->pe_buf) { HIPCHK(hipStreamSynchronize(c->stream)); HIPCHK(hipFree(c->pe_buf)); }
+    c->pe_buf = nullptr;
+    c->pe_cap = 0;
+    HIPCHK(hipMalloc(&c->pe_buf, need * 2));
+    c->pe_cap = need * 2;
+    return 0;
+}
+
 int spg_position_entries(spg_ctx *c, int64_t pos, uint8_t *codes, uint8_t *quals, int64_t cap, int64_t *n_out) {
     if (!c || !n_out || cap < 0 || (cap > 0 && (!codes || !quals))) return fail("spg_position_entries: bad argument");
     if (pos < 0 || pos >= c->n_pos) return fail("spg_position_entries: position outside the context");
@@ -1885,13 +1899,7 @@ int spg_position_entries(spg_ctx *c, int64_t pos, uint8_t *codes, uint8_t *quals
     HIPCHK(hipEventRecord(c->hist_ev, c->stream));
     c->hist_up = true;
     const size_t need = sizeof(int32_t) * n + 3 * sizeof(uint64_t) * n + 64;
-    if (need > c->pe_cap) {
-        if (c->pe_buf) { HIPCHK(hipStreamSynchronize(c->stream)); HIPCHK(hipFree(c->pe_buf)); }
-        c->pe_buf = nullptr;
-        c->pe_cap = 0;
-        HIPCHK(hipMalloc(&c->pe_buf, need * 2));
-        c->pe_cap = need * 2;
-    }
+    if (int rc = grow_scratch(c, need)) return rc;
     uint64_t *d_rng = reinterpret_cast<uint64_t *>(c->pe_buf);
     uint64_t *d_dst = d_rng + 2 * n;
     int32_t *d_items = reinterpret_cast<int32_t *>(d_dst + n);
@@ -1952,6 +1960,73 @@ int spg_history_resident(spg_ctx *c, int64_t *device_bytes, int64_t *n_spilled, 
         *n_spilled = n;
     }
     if (arena_bytes) *arena_bytes = (int64_t)c->arena.bytes();
+    return 0;
+}
+
+// Batch i as the checkpoint keeps it (live_variant_caller.py:40-45, :89, :77-85): the entries with q >= min_bq plus a
+// first-entry marker per column whose entries all fail it, compacted on the device (spg_ckpt.hip) in column ranges of
+// at most ~256 M entries (bounded scratch); only the kept bytes cross PCIe.
+int spg_history_copy_compact(spg_ctx *c, int64_t i, int32_t min_bq, uint64_t *offsets, uint8_t *base_code, uint8_t *qual,
+                             uint64_t *n_kept) {
+    if (!c || !offsets || !n_kept) return fail("spg_history_copy_compact: null argument");
+    if (i < 0 || i >= (int64_t)c->hist.size()) return fail("spg_history_copy_compact: batch index out of range");
+    if (min_bq < 0 || min_bq > 256) return fail("spg_history_copy_compact: min_bq out of range");
+    HIPCHK(hipSetDevice(c->device));
+    if (int rc = wait_copies(c)) return rc;
+    const HistBatch &h = c->hist[(size_t)i];
+    *n_kept = 0;
+    // the batch's offsets first (the chunk boundaries come from them), then overwritten by the compact ones
+    HIPCHK(hipMemcpyAsync(offsets, h.off, sizeof(uint64_t) * (h.n_cols + 1), hipMemcpyDefault, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (h.n_entries && (!base_code || !qual)) return fail("spg_history_copy_compact: null output buffer");
+    const uint64_t chunk_entries = (uint64_t)256 << 20;
+    std::vector<int64_t> cuts{0};
+    for (int64_t k = 0; k < h.n_cols;) {
+        // the next cut: the last column start within chunk_entries of this one (at least one column)
+        const uint64_t lim = offsets[k] + chunk_entries;
+        int64_t lo = k + 1, hi = h.n_cols;
+        while (lo < hi) {
+            const int64_t mid = lo + (hi - lo + 1) / 2;
+            if (offsets[mid] <= lim) lo = mid; else hi = mid - 1;
+        }
+        k = lo;
+        cuts.push_back(k);
+    }
+    int64_t max_cols = 1;
+    uint64_t max_e = 16;
+    for (size_t k = 1; k < cuts.size(); k++) {
+        max_cols = std::max(max_cols, cuts[k] - cuts[k - 1]);
+        max_e = std::max<uint64_t>(max_e, offsets[cuts[k]] - offsets[cuts[k - 1]]);
+    }
+    size_t scan_bytes = 0;
+    Hist probe{0, max_cols, nullptr, nullptr, nullptr};
+    HIPCHK(launch_ck_compact(probe, 0, nullptr, nullptr, nullptr, &scan_bytes, nullptr, nullptr, c->stream));
+    const size_t ob = ((sizeof(uint64_t) * (size_t)(max_cols + 1)) + 255) & ~size_t(255);
+    const size_t sb = (scan_bytes + 255) & ~size_t(255), eb = ((size_t)max_e + 255) & ~size_t(255);
+    if (int rc = grow_scratch(c, 2 * ob + sb + 2 * eb)) return rc;
+    uint64_t *kept = reinterpret_cast<uint64_t *>(c->pe_buf), *noff = reinterpret_cast<uint64_t *>(c->pe_buf + ob);
+    void *tmp = c->pe_buf + 2 * ob;
+    uint8_t *oc = c->pe_buf + 2 * ob + sb, *oq = oc + eb;
+    std::vector<uint64_t> loc((size_t)max_cols + 1);
+    uint64_t base = 0;
+    for (size_t k = 1; k < cuts.size(); k++) {
+        const int64_t c0 = cuts[k - 1], n = cuts[k] - c0;
+        Hist sub{h.pos_begin + c0, n, h.off + c0, h.code, h.qual};
+        size_t tb = sb;
+        HIPCHK(launch_ck_compact(sub, (uint32_t)min_bq, kept, noff, tmp, &tb, oc, oq, c->stream));
+        HIPCHK(hipMemcpyAsync(loc.data(), noff, sizeof(uint64_t) * (size_t)(n + 1), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        const uint64_t m = loc[(size_t)n];
+        if (m) {
+            HIPCHK(hipMemcpyAsync(base_code + base, oc, m, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(qual + base, oq, m, hipMemcpyDeviceToHost, c->stream));
+        }
+        for (int64_t j = 0; j < n; j++) offsets[c0 + j] = base + loc[(size_t)j];
+        base += m;
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    offsets[h.n_cols] = base;
+    *n_kept = base;
     return 0;
 }
 

@@ -481,6 +481,65 @@ int spg_multi_accumulate_records(spg_multi *m, const spg_records *r, uint32_t fl
     return maybe_rebalance(m);
 }
 
+// The cuts a batch over [pos_begin, pos_begin + n_cols) with these (host) offsets gets: the sample's cuts when it
+// is already planned, else the plan spg_multi_accumulate would make for it (the contexts are created over them).
+// A caller whose batch is already resident in HBM slices it at these cuts for spg_multi_accumulate_slices.
+int spg_multi_plan(spg_multi *m, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets, int64_t *cuts) {
+    if (!m || !offsets || !cuts || n_cols < 0 || pos_begin < 0 || pos_begin + n_cols > m->n_pos)
+        return mfail("spg_multi_plan: bad argument");
+    if (!m->lut_set || !m->ref_set) return mfail("spg_multi_plan: eps LUT / reference not set");
+    if (m->cut.empty())
+        if (int rc = plan_sample(m, pos_begin, n_cols, offsets)) return rc;
+    std::copy(m->cut.begin(), m->cut.end(), cuts);
+    return 0;
+}
+
+// One batch already resident in HBM, as one slice per device (slices[d]: device pointers on devices[d], pos_begin in
+// reference coordinates, exactly the batch's columns inside [cuts[d], cuts[d+1]) — spg_multi_plan — with offsets
+// rebased to 0; a device whose range the batch misses passes n_cols 0).  `offsets` is the whole batch's CSR on the
+// host (n_cols + 1; it feeds the entry histogram that plans and re-plans the cuts).  flags: SPG_IN_DEVICE, optionally
+// SPG_IN_BORROW (the slices stay the caller's and are the replay history: keep them until reset).
+int spg_multi_accumulate_slices(spg_multi *m, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
+                                const spg_batch *slices, uint32_t flags) {
+    if (!m || !offsets || !slices || n_cols < 0 || pos_begin < 0 || pos_begin + n_cols > m->n_pos)
+        return mfail("spg_multi_accumulate_slices: bad argument");
+    if (!(flags & SPG_IN_DEVICE) || (flags & ~(uint32_t)(SPG_IN_DEVICE | SPG_IN_BORROW | SPG_IN_TRUSTED)))
+        return mfail("spg_multi_accumulate_slices: flags must be SPG_IN_DEVICE [| SPG_IN_BORROW]");
+    if (!m->lut_set || !m->ref_set) return mfail("spg_multi_accumulate_slices: eps LUT / reference not set");
+    if (pos_begin + n_cols > m->ref_len)
+        return mfail("spg_multi_accumulate_slices: column range beyond the reference sequence");
+    if (offsets[0] != 0) return mfail("spg_multi_accumulate_slices: offsets[0] must be 0");
+    if (n_cols == 0) return 0;
+    if (m->cut.empty())
+        if (int rc = plan_sample(m, pos_begin, n_cols, offsets)) return rc;
+    // every slice checked before anything is enqueued (a mismatch leaves no device with the batch)
+    for (int d = 0; d < m->n; d++) {
+        const int64_t lo = std::max(pos_begin, m->cut[d]), hi = std::min(pos_begin + n_cols, m->cut[d + 1]);
+        const spg_batch &s = slices[d];
+        if (hi <= lo) {
+            if (s.n_cols != 0) return mfail("spg_multi_accumulate_slices: slice " + std::to_string(d) + " outside its cut");
+            continue;
+        }
+        const uint64_t e = offsets[hi - pos_begin] - offsets[lo - pos_begin];
+        if (s.pos_begin != lo || s.n_cols != hi - lo || s.n_entries != e || !s.offsets || (e && (!s.base_code || !s.qual)))
+            return mfail("spg_multi_accumulate_slices: slice " + std::to_string(d) + " is not the batch's columns [" +
+                         std::to_string(lo) + ", " + std::to_string(hi) + ") (spg_multi_plan)");
+    }
+    for (int d = 0; d < m->n; d++) {
+        const spg_batch &s = slices[d];
+        if (s.n_cols == 0) {
+            static const uint64_t none[2] = {0, 0};
+            MCTX(spg_accumulate_ex(m->ctx[d], 0, 1, none, nullptr, nullptr, 0, 0));
+            continue;
+        }
+        MCTX(spg_accumulate_ex(m->ctx[d], s.pos_begin - m->cut[d], s.n_cols, s.offsets, s.base_code, s.qual, s.n_entries,
+                               flags & (SPG_IN_DEVICE | SPG_IN_BORROW)));
+    }
+    m->batches.push_back(MBatch{pos_begin, n_cols});
+    add_weights(m->w_cur, m->bucket, pos_begin, n_cols, offsets);
+    return maybe_rebalance(m);
+}
+
 int spg_multi_wait_input(spg_multi *m) {
     if (!m) return mfail("spg_multi_wait_input: null");
     for (spg_ctx *c : m->ctx)

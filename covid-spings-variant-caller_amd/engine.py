@@ -298,24 +298,33 @@ class PileupEngine:
             N.check(self._L.spg_history_count(self._h, C.byref(n)), "spg_history_count")
         return n.value
 
-    def history(self, start: int = 0):
+    def history(self, start: int = 0, min_bq: Optional[int] = None):
         """The accumulated batches since reset() from batch `start` on, as host copies:
-        [(pos_begin, offsets, codes, quals)]."""
-        out = []
-        with self._lock:
-            n = C.c_int64()
-            N.check(self._L.spg_history_count(self._h, C.byref(n)), "spg_history_count")
-            for i in range(max(0, int(start)), n.value):
+        [(pos_begin, offsets, codes, quals)] (min_bq: compacted as the checkpoint keeps them, iter_history)."""
+        return list(self.iter_history(start, min_bq))
+
+    def iter_history(self, start: int = 0, min_bq: Optional[int] = None):
+        """The batches one at a time (a long history never sits on the host at once).  min_bq: each batch as
+        create_checkpoint keeps it — the entries with q >= min_bq plus a first-entry marker per column whose entries all
+        fail (spg_history_copy_compact: compacted in HBM, only the kept bytes cross PCIe)."""
+        n = self.history_count()
+        for i in range(max(0, int(start)), n):
+            with self._lock:
                 pb, nc, ne = C.c_int64(), C.c_int64(), C.c_uint64()
                 N.check(self._L.spg_history_info(self._h, i, C.byref(pb), C.byref(nc), C.byref(ne)),
                         "spg_history_info")
                 off = np.zeros(nc.value + 1, np.uint64)
-                codes = np.zeros(ne.value, np.uint8)
-                quals = np.zeros(ne.value, np.uint8)
-                N.check(self._L.spg_history_copy(self._h, i, N.ptr(off), N.ptr(codes), N.ptr(quals)),
-                        "spg_history_copy")
-                out.append((pb.value, off, codes, quals))
-        return out
+                codes = np.empty(ne.value, np.uint8)
+                quals = np.empty(ne.value, np.uint8)
+                if min_bq is None:
+                    N.check(self._L.spg_history_copy(self._h, i, N.ptr(off), N.ptr(codes), N.ptr(quals)),
+                            "spg_history_copy")
+                else:
+                    k = C.c_uint64()
+                    N.check(self._L.spg_history_copy_compact(self._h, i, int(min_bq), N.ptr(off), N.ptr(codes),
+                                                             N.ptr(quals), C.byref(k)), "spg_history_copy_compact")
+                    codes, quals = codes[:k.value], quals[:k.value]   # (pages past k never touched)
+            yield pb.value, off, codes, quals
 
     # -- results ------------------------------------------------------------------------------
     def table(self, pos0: int = 0, n: Optional[int] = None) -> Dict[str, np.ndarray]:

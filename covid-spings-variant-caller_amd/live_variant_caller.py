@@ -190,6 +190,7 @@ class LiveVariantCaller:
             self._inflate_dev = device if device is not None else 0
             N.use_gpu_inflate(self._inflate_dev, on=self._gpu_inflate)
         self._inflight = collections.deque()     # (input ticket, records plan) whose copy may still be running
+        self.last_checkpoint_bytes = 0           # shard bytes the last create_checkpoint wrote
         self.reset_memory()
 
     def __del__(self):
@@ -216,6 +217,7 @@ class LiveVariantCaller:
             self._batch_contig = []
             self._current_ref = None
             self._ck_token = uuid.uuid4().hex     # identity of this memory for incremental checkpoints
+            self._ck_chain = {}                   # directory -> this memory's shards there [(file, first, count)]
 
     def _use_reference(self, index: int):
         if self._current_ref != index:
@@ -330,40 +332,49 @@ class LiveVariantCaller:
         """:40-45 — the accumulated batches (exact engine state) as numpy .npz files.  Like the reference's
         pickled `memory`, which holds only the base qualities that passed the filter (:96-103), each batch keeps
         only its entries with q >= minBaseQuality — plus, for a column whose every entry fails it, its first
-        entry, so that the position's first visit (:77-85) survives the round trip.
+        entry, so that the position's first visit (:77-85) survives the round trip.  The compaction runs on the GPU
+        (spg_history_copy_compact): only the kept bytes cross PCIe, no per-entry host arrays.
 
         Incremental: `filename` is a small manifest (FASTA names, contig of every batch, the shard files); the
-        batches live in shards beside it (`<filename>.<token>.<first batch>.npz`).  vc_queue.py:142-144 writes a
-        checkpoint after every BAM: when `filename` already holds this memory's earlier checkpoint (same
-        memory token — a reset or a load starts a new one), only the batches accumulated since are written,
-        so a call costs O(new entries), not O(everything accumulated).  A loaded checkpoint is a new memory (its first
-checkpoint writes every batch once): two callers that load one file never append to each other's shards.  The manifest is replaced atomically
-        after its shards are on disk; shards no manifest lists any more are removed."""
+        batches live in shard files beside it (`spgck-<memory token>-<first batch>-<count>.npz`), which belong to
+        this memory, not to one manifest name.  vc_queue.py:134-144 writes a checkpoint after every BAM, under a new
+        name per BAM (`<temp dir>/<bam name><ext>`): each call writes only the batches accumulated since this
+        memory's previous checkpoint in that directory (whatever its name), and its manifest lists the earlier
+        shards too — O(new entries) per BAM, and every manifest stays a complete, loadable state.  A reset or a load
+        starts a new memory (a new token: its first checkpoint writes every batch once).  Manifests are replaced
+        atomically after their shards are on disk; shards an overwritten manifest listed are removed when no
+        manifest in the directory lists them any more."""
         log.info("Creating checkpoint %s", filename)
         with self._lock:
             n = self.engine.history_count()
             names = list(self.fastaFile.references)
-            old = _read_manifest(filename)
-            keep = []
-            if (old is not None and old["token"] == self._ck_token and old["names"] == names
-                    and old["min_base_quality"] == self.minBaseQuality and old["n"] <= n
-                    and old["contig"] == self._batch_contig[:old["n"]]):
-                keep = old["shards"]
-            first = sum(k for _, _, k in keep)
-            shards = list(keep)
-            base = os.path.basename(filename)
+            d = os.path.dirname(os.path.abspath(filename))
+            shards = []                                  # this memory's shard chain in d, while its files exist
+            for sh in self._ck_chain.get(d, []):
+                if not os.path.exists(os.path.join(d, sh[0])):
+                    break
+                shards.append(sh)
+            first = sum(k for _, _, k in shards)
+            if first > n:
+                shards, first = [], 0
+            self.last_checkpoint_bytes = 0
             if first < n:
                 arrays = {}
-                for i, (pb, off, codes, quals) in enumerate(self.engine.history(start=first)):
-                    off, codes, quals = _bq_compact(off, codes, quals, self.minBaseQuality)
+                for i, (pb, off, codes, quals) in enumerate(self.engine.iter_history(first, min_bq=self.minBaseQuality)):
                     arrays[f"b{i}_pos"] = np.int64(pb)
                     arrays[f"b{i}_off"] = off
                     arrays[f"b{i}_codes"] = codes
                     arrays[f"b{i}_quals"] = quals
-                shard = f"{base}.{self._ck_token[:12]}.{first}.npz"
-                with open(os.path.join(os.path.dirname(os.path.abspath(filename)), shard), "wb") as f:
+                shard = f"spgck-{self._ck_token[:16]}-{first}-{n - first}.npz"
+                path = os.path.join(d, shard)
+                with open(path + ".tmp", "wb") as f:
                     np.savez(f, **arrays)
+                os.replace(path + ".tmp", path)
+                self.last_checkpoint_bytes = os.path.getsize(path)
+                del arrays
                 shards.append((shard, first, n - first))
+            self._ck_chain[d] = list(shards)
+            old = _read_manifest(filename)
             tmp = filename + ".tmp"
             with open(tmp, "wb") as f:
                 np.savez(f, format=np.int64(2), token=np.array(self._ck_token),
@@ -373,13 +384,9 @@ checkpoint writes every batch once): two callers that load one file never append
                          shard_ranges=np.array([[a, k] for _, a, k in shards], np.int64).reshape(-1, 2))
             os.replace(tmp, filename)
             if old is not None:
-                live = {s for s, _, _ in shards}
-                for s, _, _ in old["shards"]:
-                    if s not in live:
-                        try:
-                            os.remove(os.path.join(os.path.dirname(os.path.abspath(filename)), s))
-                        except OSError:
-                            pass
+                gone = {s for s, _, _ in old["shards"]} - {s for s, _, _ in shards}
+                if gone:
+                    _remove_unlisted(d, gone)
 
     def load_checkpoint(self, filename):
         """:47-52 — replaces memory with the checkpoint's (replays its batches).  Reads the incremental
@@ -469,23 +476,23 @@ def _is_bgzf(path: str) -> bool:
         return f.read(2) == b"\x1f\x8b"
 
 
-def _bq_compact(off, codes, quals, min_bq: int):
-    """A CSR batch without the entries the base-quality filter drops (:96-103 never sees them); a column whose
-    every entry is dropped keeps its first one (its q < min_bq: the engine filters it again), which records the
-    position's first visit (:77-85)."""
-    off = np.asarray(off, np.uint64)
-    if min_bq <= 0 or len(codes) == 0:
-        return off, codes, quals
-    lens = np.diff(off.astype(np.int64))
-    col = np.repeat(np.arange(len(lens), dtype=np.int64), lens)
-    keep = quals >= min_bq
-    kept = np.bincount(col[keep], minlength=len(lens))
-    marker = (lens > 0) & (kept == 0)
-    keep[off[:-1][marker].astype(np.int64)] = True
-    new_lens = np.bincount(col[keep], minlength=len(lens))
-    new_off = np.zeros(len(off), np.uint64)
-    np.cumsum(new_lens, out=new_off[1:])
-    return new_off, np.ascontiguousarray(codes[keep]), np.ascontiguousarray(quals[keep])
+def _remove_unlisted(d: str, files):
+    """Delete the shard files among `files` that no manifest in directory d lists (several manifests share one
+    memory's shards).  Runs only when a manifest was overwritten with a different shard list (a reset, a load, or a
+    foreign memory under the same name), so its O(files in d) scan is off the per-BAM path."""
+    listed = set()
+    with os.scandir(d) as it:
+        for ent in it:
+            if not ent.is_file() or ent.name.startswith("spgck-") or ent.name.endswith(".tmp"):
+                continue
+            m = _read_manifest(ent.path)
+            if m is not None:
+                listed.update(s for s, _, _ in m["shards"])
+    for s in set(files) - listed:
+        try:
+            os.remove(os.path.join(d, s))
+        except OSError:
+            pass
 
 
 def _hval(v: str) -> str:

@@ -97,6 +97,40 @@ class MultiEngine:
                                                      len(c), N.SPG_IN_TRUSTED if trusted else 0), "spg_multi_accumulate")
             self._seq += 1
 
+    def plan(self, pos_begin: int, offsets) -> np.ndarray:
+        """The cuts (n + 1 reference positions) a batch with these host offsets gets (spg_multi_plan): the sample's
+        cuts, planned now from this batch when the sample has none yet."""
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        cuts = np.zeros(len(self.devices) + 1, np.int64)
+        with self._lock:
+            self._check(self._L.spg_multi_plan(self._h, int(pos_begin), len(o) - 1, N.ptr(o),
+                                               cuts.ctypes.data_as(C.POINTER(C.c_int64))), "spg_multi_plan")
+        return cuts
+
+    def accumulate_slices(self, pos_begin: int, offsets, slices, borrow: bool = True):
+        """A batch resident in HBM, one slice per device at the plan's cuts (spg_multi_accumulate_slices):
+        slices[d] = (pos_begin, offsets, codes, quals) as device tensors on devices[d] (offsets rebased to 0; None
+        where the batch misses the device's range).  ``offsets``: the whole batch's CSR on the host."""
+        o = np.ascontiguousarray(offsets, dtype=np.uint64)
+        arr = np.zeros(len(self.devices), N.BATCH_DTYPE)
+        for d, s in enumerate(slices):
+            if s is None:
+                continue
+            pb, off, codes, quals = s
+            arr[d] = (int(pb), int(off.numel()) - 1, int(off.data_ptr()), int(codes.data_ptr()), int(quals.data_ptr()),
+                      int(self._slice_entries(d, pb, off, o, pos_begin)))
+        flags = N.SPG_IN_DEVICE | (N.SPG_IN_BORROW if borrow else 0)
+        with self._lock:
+            self._check(self._L.spg_multi_accumulate_slices(self._h, int(pos_begin), len(o) - 1, N.ptr(o), N.ptr(arr),
+                                                            flags), "spg_multi_accumulate_slices")
+            self._seq += 1
+
+    @staticmethod
+    def _slice_entries(d, pb, off, o, pos_begin):
+        """Entries of the slice starting at reference position pb with off.numel() - 1 columns (from the host CSR)."""
+        a = int(pb) - int(pos_begin)
+        return int(o[a + int(off.numel()) - 1]) - int(o[a])
+
     def accumulate_bam_records(self, batch):
         """A records plan (pileup.AlignmentFile.pileup_records) sharded over the devices: each decodes the reads that
         reach its range (spg_multi_accumulate_records).  Keep ``batch`` open until wait_ticket(input_ticket())."""
@@ -125,6 +159,22 @@ class MultiEngine:
         with self._lock:
             for ctx in self._contexts():
                 N.check(self._L.spg_sync(ctx), "spg_sync")
+
+    def set_timing(self, level: int):
+        with self._lock:
+            for ctx in self._contexts():
+                N.check(self._L.spg_set_timing(ctx, int(level)), "spg_set_timing")
+
+    def kernel_times(self, cap: int = 4096):
+        """Per device: (accumulate ms, finalize ms) of every finalize step since the last call (spg_kernel_times)."""
+        out = []
+        with self._lock:
+            for ctx in self._contexts():
+                a, f = np.zeros(cap, np.float32), np.zeros(cap, np.float32)
+                n = C.c_int64()
+                N.check(self._L.spg_kernel_times(ctx, N.ptr(a), N.ptr(f), cap, C.byref(n)), "spg_kernel_times")
+                out.append((a[:n.value].copy(), f[:n.value].copy()))
+        return out
 
     # -- results ---------------------------------------------------------------------------------
     def partition(self) -> np.ndarray:
@@ -210,35 +260,45 @@ class MultiEngine:
             N.check(self._L.spg_history_count(ctxs[0], C.byref(n)), "spg_history_count")
             return n.value
 
-    def history(self, start: int = 0):
+    def history(self, start: int = 0, min_bq=None):
         """The accumulated batches, reassembled from the devices' slices in reference coordinates:
         [(pos_begin, offsets, codes, quals)] (a batch's extent spans the slices that hold entries)."""
-        out = []
+        return list(self.iter_history(start, min_bq))
+
+    def iter_history(self, start: int = 0, min_bq=None):
+        """history() one batch at a time; min_bq: each device compacts its slice as the checkpoint keeps it
+        (spg_history_copy_compact) before the slices are reassembled."""
         with self._lock:
             ctxs, cuts = self._contexts(), self._cuts_of_contexts()
-            if not ctxs or cuts is None:
-                return out
-            for i in range(max(0, int(start)), self.history_count()):
-                parts = []
+            n_hist = self.history_count() if ctxs and cuts is not None else 0
+        for i in range(max(0, int(start)), n_hist):
+            parts = []
+            with self._lock:
                 for d, ctx in enumerate(ctxs):
                     pb, nc, ne = C.c_int64(), C.c_int64(), C.c_uint64()
                     N.check(self._L.spg_history_info(ctx, i, C.byref(pb), C.byref(nc), C.byref(ne)), "spg_history_info")
                     if ne.value == 0:
                         continue
                     off = np.zeros(nc.value + 1, np.uint64)
-                    codes = np.zeros(ne.value, np.uint8)
-                    quals = np.zeros(ne.value, np.uint8)
-                    N.check(self._L.spg_history_copy(ctx, i, N.ptr(off), N.ptr(codes), N.ptr(quals)), "spg_history_copy")
+                    codes = np.empty(ne.value, np.uint8)
+                    quals = np.empty(ne.value, np.uint8)
+                    if min_bq is None:
+                        N.check(self._L.spg_history_copy(ctx, i, N.ptr(off), N.ptr(codes), N.ptr(quals)),
+                                "spg_history_copy")
+                    else:
+                        k = C.c_uint64()
+                        N.check(self._L.spg_history_copy_compact(ctx, i, int(min_bq), N.ptr(off), N.ptr(codes),
+                                                                 N.ptr(quals), C.byref(k)), "spg_history_copy_compact")
+                        codes, quals = codes[:k.value], quals[:k.value]
                     parts.append((int(cuts[d]) + pb.value, off, codes, quals))
-                if not parts:
-                    out.append((0, np.zeros(1, np.uint64), np.zeros(0, np.uint8), np.zeros(0, np.uint8)))
-                    continue
-                p0 = parts[0][0]
-                p1 = parts[-1][0] + len(parts[-1][1]) - 1
-                lens = np.zeros(p1 - p0, np.int64)
-                for pb, off, _, _ in parts:
-                    lens[pb - p0:pb - p0 + len(off) - 1] = np.diff(off.astype(np.int64))
-                offs = np.zeros(p1 - p0 + 1, np.uint64)
-                np.cumsum(lens, out=offs[1:])
-                out.append((p0, offs, np.concatenate([p[2] for p in parts]), np.concatenate([p[3] for p in parts])))
-        return out
+            if not parts:
+                yield (0, np.zeros(1, np.uint64), np.zeros(0, np.uint8), np.zeros(0, np.uint8))
+                continue
+            p0 = parts[0][0]
+            p1 = parts[-1][0] + len(parts[-1][1]) - 1
+            lens = np.zeros(p1 - p0, np.int64)
+            for pb, off, _, _ in parts:
+                lens[pb - p0:pb - p0 + len(off) - 1] = np.diff(off.astype(np.int64))
+            offs = np.zeros(p1 - p0 + 1, np.uint64)
+            np.cumsum(lens, out=offs[1:])
+            yield (p0, offs, np.concatenate([p[2] for p in parts]), np.concatenate([p[3] for p in parts]))

@@ -257,6 +257,13 @@ int spg_history_resident(spg_ctx *ctx, int64_t *device_bytes, int64_t *n_spilled
 int spg_history_count(spg_ctx *ctx, int64_t *n_batches);
 int spg_history_info(spg_ctx *ctx, int64_t i, int64_t *pos_begin, int64_t *n_cols, uint64_t *n_entries);
 int spg_history_copy(spg_ctx *ctx, int64_t i, uint64_t *offsets, uint8_t *base_code, uint8_t *qual);
+/* Batch i as create_checkpoint keeps it (live_variant_caller.py:40-45; the pickled memory holds only the qualities
+ * that passed the base-quality filter, :89/:96-103, and every first visit, :77-85): its entries with q >= min_bq, plus
+ * the first entry of a column whose entries all fail the filter (a marker that records the visit; the engine filters
+ * it again on resume).  Compacted on the device; offsets (n_cols + 1, host) always, base_code / qual (host, room
+ * for the batch's n_entries) get *n_kept entries.  Synchronises. */
+int spg_history_copy_compact(spg_ctx *ctx, int64_t i, int32_t min_bq, uint64_t *offsets, uint8_t *base_code,
+                             uint8_t *qual, uint64_t *n_kept);
 /* One position's entries over the whole history, in accumulate order (the q list behind memory[pos], before the
  * base-quality filter): *n_out = their number; codes / quals get them when n_out <= cap (cap 0: count only).
  * Synchronises.  LiveVariantCaller.memory builds a Site from this per lookup instead of expanding every entry. */
@@ -338,6 +345,15 @@ int spg_multi_accumulate(spg_multi *m, int64_t pos_begin, int64_t n_cols, const 
 /* A BAM records plan (spg_accumulate_records, pos_origin 0), sharded: each device decodes the reads that reach its
  * range on the GPU.  The plan's buffers are read asynchronously: keep them until spg_multi_wait_input. */
 int spg_multi_accumulate_records(spg_multi *m, const spg_records *r, uint32_t flags);
+/* The cuts a batch (host offsets) gets — the sample's, planned now when it has none yet (cuts: n + 1 values). */
+int spg_multi_plan(spg_multi *m, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets, int64_t *cuts);
+/* A batch already resident in HBM, one slice per device (slices[d]: device pointers on devices[d], pos_begin in
+ * reference coordinates, exactly the batch's columns inside [cuts[d], cuts[d+1]) with offsets rebased to 0, n_cols 0
+ * where the batch misses the device's range); offsets: the whole batch's CSR on the host (the entry histogram).
+ * flags: SPG_IN_DEVICE [| SPG_IN_BORROW].  The per-rank shards of north_star's "positions shard by coordinate
+ * range" when each GPU already holds its part of the pileup. */
+int spg_multi_accumulate_slices(spg_multi *m, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
+                                const spg_batch *slices, uint32_t flags);
 int spg_multi_wait_input(spg_multi *m);
 int spg_multi_finalize(spg_multi *m);
 /* The merged call table (needs n_out <= cap; *n_out is set either way). */

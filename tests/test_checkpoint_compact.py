@@ -1,4 +1,4 @@
-"""Checkpoint compaction (live_variant_caller._bq_compact): a batch stored without the entries the
+"""Checkpoint compaction (tests/ck_util.bq_compact, the host restatement of spg_history_copy_compact): a batch stored without the entries the
 base-quality filter drops gives the same memory (counts, q lists, dict order, first visits) and the same
 calls as the full batch, for the C oracle (CPU; the GPU round trip is tests/test_live_caller_gpu.py)."""
 import numpy as np
@@ -11,7 +11,7 @@ from oracle.c_oracle import COracle
 @pytest.mark.parametrize("bq", [0, 13, 30])
 def test_compacted_batches_same_memory_and_calls(bq):
     from covid_spings_variant_caller_amd import synth
-    from covid_spings_variant_caller_amd.live_variant_caller import _bq_compact
+    from ck_util import bq_compact as _bq_compact
     L = 3000
     ref = synth.reference(L, seed=5)
     batches = []

@@ -152,7 +152,9 @@ def test_checkpoint_incremental_per_bam(planted):
     """vc_queue.py:142-144's loop — process_bam then create_checkpoint(same file) per BAM: each checkpoint
     writes only the batches accumulated since the previous one (earlier shards untouched), a reset or a load
     starts a fresh set (the old shards removed), and the resumed memory matches the oracle."""
-    d, ref, fasta, files = planted
+    d0, ref, fasta, files = planted
+    d = d0 / "inc"
+    d.mkdir(exist_ok=True)
     ck = str(d / "inc.npz")
     seq = [files[0], files[1], files[0]]
     a = _caller(fasta)
@@ -160,7 +162,7 @@ def test_checkpoint_incremental_per_bam(planted):
     for f in seq:
         a.process_bam(f)
         a.create_checkpoint(ck)
-        shards = sorted(x for x in os.listdir(d) if x.startswith("inc.npz.") and x.endswith(".npz"))
+        shards = sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".npz"))
         listed.append(shards)
     assert [len(x) for x in listed] == [1, 2, 3]
     assert listed[1][:1] == listed[0] and set(listed[1]) < set(listed[2])
@@ -168,7 +170,7 @@ def test_checkpoint_incremental_per_bam(planted):
     m0 = os.stat(first).st_mtime_ns
     a.create_checkpoint(ck)                      # nothing new: only the manifest is rewritten
     assert os.stat(first).st_mtime_ns == m0
-    assert sorted(x for x in os.listdir(d) if x.startswith("inc.npz.") and x.endswith(".npz")) == listed[2]
+    assert sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".npz")) == listed[2]
     b = _caller(fasta)
     b.load_checkpoint(ck)
     o = _oracle(ref, seq)
@@ -177,11 +179,11 @@ def test_checkpoint_incremental_per_bam(planted):
     assert list(mem) == list(o.memory) and all(mem[p] == o.memory[p] for p in o.memory)
     b.process_bam(files[1])                      # a loaded memory is a new one: its first checkpoint writes all
     b.create_checkpoint(ck)                      # its batches once, then appends
-    now = sorted(x for x in os.listdir(d) if x.startswith("inc.npz.") and x.endswith(".npz"))
+    now = sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".npz"))
     assert len(now) == 1 and now[0] not in listed[2]
     b.process_bam(files[0])
     b.create_checkpoint(ck)
-    now2 = sorted(x for x in os.listdir(d) if x.startswith("inc.npz.") and x.endswith(".npz"))
+    now2 = sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".npz"))
     assert len(now2) == 2 and set(now) < set(now2)
     c = _caller(fasta)
     c.load_checkpoint(ck)
@@ -189,16 +191,53 @@ def test_checkpoint_incremental_per_bam(planted):
     a.reset_memory()                             # a new memory: a fresh shard set, the old shards removed
     a.process_bam(files[1])
     a.create_checkpoint(ck)
-    now = sorted(x for x in os.listdir(d) if x.startswith("inc.npz.") and x.endswith(".npz"))
+    now = sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".npz"))
     assert len(now) == 1 and now[0] not in now2
     c.load_checkpoint(ck)
+    compare_variants(c.prepare_variants(), _oracle(ref, files[1:]).prepare_variants(), RTOL)
+
+
+def test_checkpoint_vcqueue_per_bam_names(planted):
+    """client_server/vc_queue.py:134-144 names the checkpoint after each BAM (`<temp dir>/<bam name><ext>`): each call
+    writes only that BAM's batch (its shard's bytes are O(that BAM), equal for equal BAMs however many came before),
+    every per-BAM manifest is a complete state (loading the k-th equals the oracle after k + 1 BAMs), and overwriting
+    one manifest with another memory keeps the shards the other manifests still list."""
+    d0, ref, fasta, files = planted
+    d = d0 / "vcq"
+    d.mkdir(exist_ok=True)
+    seq = [files[0], files[1], files[0], files[1], files[0]]
+    a = _caller(fasta)
+    names, sizes = [], []
+    for k, f in enumerate(seq):
+        a.process_bam(f)
+        ck = str(d / f"{k}_{os.path.basename(f)}.pkl")
+        a.create_checkpoint(ck)
+        names.append(ck)
+        sizes.append(a.last_checkpoint_bytes)
+        shards = [x for x in os.listdir(d) if x.startswith("spgck-")]
+        assert len(shards) == k + 1
+    assert all(x > 0 for x in sizes)
+    for k in range(2, len(seq)):                  # the same BAM again: the same bytes, not the cumulative memory
+        assert sizes[k] <= 1.02 * sizes[k - 2] + 512, sizes
+    assert sizes[4] < 1.5 * sizes[0] and sum(sizes) < 3.5 * max(sizes[0], sizes[1])
+    for k in range(len(seq)):
+        b = _caller(fasta)
+        b.load_checkpoint(names[k])
+        compare_variants(b.prepare_variants(), _oracle(ref, seq[:k + 1]).prepare_variants(), RTOL)
+    a.reset_memory()                              # another memory under the first BAM's name
+    a.process_bam(files[1])
+    a.create_checkpoint(names[0])
+    c = _caller(fasta)
+    c.load_checkpoint(names[-1])                  # its shards (shared with names[0]'s old manifest) are still there
+    compare_variants(c.prepare_variants(), _oracle(ref, seq).prepare_variants(), RTOL)
+    c.load_checkpoint(names[0])
     compare_variants(c.prepare_variants(), _oracle(ref, files[1:]).prepare_variants(), RTOL)
 
 
 def test_checkpoint_single_file_format_still_loads(planted):
     """A checkpoint in the earlier single-file layout (every batch inside the named .npz) loads as before."""
     d, ref, fasta, files = planted
-    from covid_spings_variant_caller_amd.live_variant_caller import _bq_compact
+    from ck_util import bq_compact as _bq_compact
     a = _caller(fasta)
     for f in files:
         a.process_bam(f)

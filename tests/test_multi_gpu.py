@@ -182,3 +182,58 @@ def test_multi_records_path_vs_oracle(tmp_path, devices):
     mc2 = LiveVariantCaller(fasta, 30, 20, 10, 5, 0.10, 1, devices=devices)
     mc2.load_checkpoint(ck)
     _variants_equal(mc2.prepare_variants(), orc.variants())
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_device_slices_vs_single_context(devices):
+    """spg_multi_plan + spg_multi_accumulate_slices (bench.py's multi_device leg): a batch resident in HBM, sliced at the
+    plan's cuts into per-device tensors (borrowed), stacked samples over one coordinate space — the merged table equals
+    one context's on the whole batch, every step after a reset; a slice that does not match its cut is refused before
+    any device takes the batch."""
+    import torch
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.multi import MultiEngine
+    L, S = 5000, 3
+    ref = synth.reference(L, seed=81)
+    smp = [synth.pileup(L, 400, seed=82 + s, ref=ref, snv_every=41) for s in range(S)]
+    off = np.zeros(S * L + 1, np.uint64)
+    base = 0
+    for s, (_, o, _, _) in enumerate(smp):
+        off[s * L + 1:(s + 1) * L + 1] = o[1:] + np.uint64(base)
+        base += int(o[-1])
+    codes = np.concatenate([c for _, _, c, _ in smp])
+    quals = np.concatenate([q for _, _, _, q in smp])
+    m = MultiEngine(devices, S * L, reference=ref * S)
+    cuts = m.plan(0, off)
+    assert cuts[0] == 0 and cuts[-1] == S * L and np.all(np.diff(cuts) > 0)
+    dev = torch.device("cuda", 0)
+    pad = np.zeros(16, np.uint8)
+    slices = []
+    for d in range(len(devices)):
+        lo, hi = int(cuts[d]), int(cuts[d + 1])
+        a, b = int(off[lo]), int(off[hi])
+        so = (off[lo:hi + 1] - off[lo]).astype(np.int64)
+        slices.append((lo, torch.from_numpy(so).to(dev), torch.from_numpy(np.concatenate([codes[a:b], pad + 0xFF])).to(dev),
+                       torch.from_numpy(np.concatenate([quals[a:b], pad])).to(dev)))
+    s = PileupEngine(S * L, 30, 10, 5, 0.10, device=0, reference=ref * S, calls_only=True)
+    s.accumulate(0, off, codes, quals)
+    s.finalize()
+    one = s.candidates()
+    assert len(one) > 30
+    for _ in range(3):
+        m.reset()
+        m.accumulate_slices(0, off, slices, borrow=True)
+        m.finalize()
+        got = m.candidates()
+        assert got.tobytes() == one.tobytes()
+        assert np.array_equal(m.partition(), cuts)
+    if len(devices) > 1:
+        bad = list(slices)
+        lo, so, c, q = bad[1]
+        bad[1] = (lo + 1, so[1:] - so[1], c, q)
+        m.reset()
+        with pytest.raises(Exception, match="not the batch's columns"):
+            m.accumulate_slices(0, off, bad, borrow=True)
+    m.close()
+    s.close()
