@@ -817,6 +817,48 @@ def cpu_baseline(args):
             **res, "cores_in_affinity_mask": cores, "omp_num_threads": omp or None, "cpu_model": cpu_model()}
 
 
+def vcqueue_loop(caller, paths, work_dir):
+    """client_server/vc_queue.py:134-144 per BAM, in its order and with its file names: process_bam, then
+    create_checkpoint(<temp dir>/<bam name>.pkl), then write_vcf(<output dir>/<bam name>.vcf) — per-stage wall time
+    (the GPU work included: write_vcf's prepare_variants reads the call table back)."""
+    import contextlib
+    import io
+    tmp = os.path.join(work_dir, "vcq_tmp")
+    out = os.path.join(work_dir, "vcq_out")
+    os.makedirs(tmp, exist_ok=True)
+    os.makedirs(out, exist_ok=True)
+    caller.reset_memory()
+    caller.engine.sync()
+    st = np.zeros((len(paths), 3))
+    ck_bytes = np.zeros(len(paths))
+    t_all = time.perf_counter()
+    for k, p in enumerate(paths):
+        name = os.path.basename(p)
+        t0 = time.perf_counter()
+        caller.process_bam(p)
+        t1 = time.perf_counter()
+        caller.create_checkpoint(os.path.join(tmp, name + ".pkl"))
+        t2 = time.perf_counter()
+        with contextlib.redirect_stdout(io.StringIO()):          # (write_vcf prints the path, :234)
+            caller.write_vcf(os.path.join(out, name + ".vcf"))
+        t3 = time.perf_counter()
+        st[k] = (t1 - t0, t2 - t1, t3 - t2)
+        ck_bytes[k] = caller.last_checkpoint_bytes
+    total = time.perf_counter() - t_all
+    n_calls = sum(1 for ln in open(os.path.join(out, os.path.basename(paths[-1]) + ".vcf")) if not ln.startswith("#"))
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
+    shutil.rmtree(out, ignore_errors=True)
+    return {"bams": len(paths), "positions_per_s_per_bam": len(paths) * L_SARS / total, "ms_per_bam": total / len(paths) * 1e3,
+            "process_bam_ms": float(st[:, 0].mean()) * 1e3, "create_checkpoint_ms": float(st[:, 1].mean()) * 1e3,
+            "write_vcf_ms": float(st[:, 2].mean()) * 1e3,
+            "per_bam_ms": [[round(x * 1e3, 2) for x in r] for r in st],
+            "checkpoint_shard_mb_per_bam": [round(x / 1e6, 2) for x in ck_bytes],
+            "calls_last_vcf": n_calls,
+            "path": "process_bam (device pileup) -> create_checkpoint (this BAM's batch compacted on the GPU, one shard; "
+                    "the per-BAM manifest lists the memory's earlier shards) -> write_vcf (prepare_variants + VCF text)"}
+
+
 def end_to_end(args, device):
     """BAM -> calls through the drop-in (LiveVariantCaller.process_bam, live_variant_caller.py:54-72).
     Product path (device pileup): host BGZF inflate straight into pinned memory + record scan +
@@ -844,12 +886,12 @@ def end_to_end(args, device):
     t_sim = time.perf_counter() - t0
     res = {}
     n_bams = max(1, args.e2e_bams)
-    def stream(cap, device_pileup):
-        os.environ["SPG_DEVICE_PILEUP"] = "1" if device_pileup else "0"
+    def stream(cap, mode):
         caller = LiveVariantCaller(fasta, 30, 20, 10, 5, 0.10, 1, device=device, max_depth=cap,
-                                   n_threads=args.e2e_threads)
+                                   n_threads=args.e2e_threads, pileup=mode)
         for _ in range(3):                         # warm-up: pinned staging / record buffers, library state
             caller.process_bam(bam)
+        assert caller.last_bam_path == mode, (caller.last_bam_path, mode)
         caller.reset_memory()
         caller.engine.sync()
         t0 = time.perf_counter()
@@ -861,25 +903,65 @@ def end_to_end(args, device):
         t1 = time.perf_counter()
         return caller, calls, t0, t_in, t1
 
+    def device_breakdown(caller, reps=3):
+        """One BAM through the device path's stages, each synchronised (their sum exceeds the pipelined per-BAM time:
+        process_bam returns once the fill is enqueued)."""
+        eng, prm = caller.engine, caller.pileup_params
+        rows = []
+        for _ in range(reps):
+            eng.reset()
+            eng.sync()
+            t = [time.perf_counter()]
+            with AlignmentFile(bam) as f:
+                tid = f.tid("NC_045512.2")
+                m = f.bam_map(prm.n_threads)
+                t.append(time.perf_counter())
+                n = eng.bam_open(m, tid, prm)
+                m.close()
+                t.append(time.perf_counter())
+                reads = eng.bam_reads(n)
+                t.append(time.perf_counter())
+                pb = f.pileup_fields("NC_045512.2", reads, prm)
+                t.append(time.perf_counter())
+            assert eng.bam_accumulate(pb)
+            eng.wait_input()
+            eng.sync()
+            t.append(time.perf_counter())
+            eng.finalize()
+            eng.sync()
+            t.append(time.perf_counter())
+            pb.close()
+            rows.append(np.diff(t) * 1e3)
+        r = np.median(np.array(rows), axis=0)
+        return {"map_and_pinned_copy_ms": r[0], "bam_open_ms (H2D + inflate + CRC + record scan + fields)": r[1],
+                "inflate_kernels_ms": eng.bam_inflate_ms(), "reads_fields_d2h_ms": r[2],
+                "host_depth_cap_and_pairing_ms": r[3], "plan_h2d_tweak_fill_ms": r[4], "finalize_ms": r[5],
+                "reads": int(n), "sum_ms": float(r.sum())}
+
     for cap, tag in ((8000, "parity_mode_max_depth_8000"), (0, "uncapped")):
         # the host-fill path first (r02's product path: the host writes every entry into pinned staging)
-        caller, calls_h, t0, t_in, t1 = stream(cap, False)
+        caller, calls_h, t0, t_in, t1 = stream(cap, "host")
         host_leg = {"positions_per_s_per_bam": n_bams * L_SARS / (t1 - t0), "s_per_bam": (t1 - t0) / n_bams}
+        caller.engine.close()
+        del caller
+        # r03-r04's product path: the host plans the records (GPU inflate), the GPU writes the entries
+        caller, calls_r, t0, t_in, t1 = stream(cap, "records")
+        assert [v["start"] for v in calls_r] == [v["start"] for v in calls_h], "records / host pileup calls differ"
+        rec_leg = {"positions_per_s_per_bam": n_bams * L_SARS / (t1 - t0), "s_per_bam": (t1 - t0) / n_bams}
         p = caller.pileup_params
         b0 = time.perf_counter()
         with AlignmentFile(bam) as f:
-            b = f.pileup_plan("NC_045512.2", p)
+            b = f.pileup_records("NC_045512.2", p)
         b1 = time.perf_counter()
-        codes, quals = pinned_empty(b.n_entries + 16), pinned_empty(b.n_entries + 16)
-        b.fill(codes, quals)
-        b2 = time.perf_counter()
-        host_leg.update(host_plan_s=b1 - b0, host_fill_pinned_s=b2 - b1)
+        rec_leg["host_plan_records_s"] = b1 - b0
+        rec_leg["inflated_mb"] = b.records().data_bytes / 1e6
         b.close()
         caller.engine.close()
         del caller
-        # the product path: device-side pileup (spg_accumulate_records)
-        caller, calls, t0, t_in, t1 = stream(cap, True)
+        # the product path: the BAM kept in HBM (spg_bam_*)
+        caller, calls, t0, t_in, t1 = stream(cap, "device")
         assert [v["start"] for v in calls] == [v["start"] for v in calls_h], "device / host pileup calls differ"
+        brk = device_breakdown(caller)
         # the same BAMs through process_bams (the drop-in's many-BAM call: plans of two BAMs overlap on the host; their
         # BGZF members inflate on the GPU, spg_bgzf_inflate); a warm-up call first (the inflater's device buffers)
         caller.process_bams([bam] * 2)
@@ -891,38 +973,31 @@ def end_to_end(args, device):
         caller.engine.sync()
         m1 = time.perf_counter()
         assert [v["start"] for v in calls_m] == [v["start"] for v in calls_h], "process_bams calls differ"
+        # vc_queue.py:134-144's loop over BAM files with their own names (hard links of the simulated BAM)
+        vq = []
+        for k in range(max(2, n_bams)):
+            pth = os.path.join(d, f"vq{k}.bam")
+            os.link(bam, pth)
+            vq.append(pth)
+        vq_leg = vcqueue_loop(caller, vq, d)
+        for pth in vq:
+            os.remove(pth)
         many_leg = {"bams": 2 * n_bams, "positions_per_s_per_bam": 2 * n_bams * L_SARS / (m1 - m0),
                     "s_per_bam": (m1 - m0) / (2 * n_bams),
-                    "bgzf_inflate": "gpu (spg_bgzf_inflate, k_inflate)" if caller.last_gpu_inflate else "host"}
-        p = caller.pileup_params
-        b0 = time.perf_counter()
-        with AlignmentFile(bam) as f:
-            b = f.pileup_records("NC_045512.2", p)
-        b1 = time.perf_counter()
-        eng = caller.engine
-        eng.reset()
-        eng.sync()
-        g0 = time.perf_counter()
-        eng.accumulate_bam_records(b)
-        eng.finalize()
-        eng.sync()
-        g1 = time.perf_counter()
-        E = b.n_entries
-        data_mb = b.records().data_bytes / 1e6
-        b.close()
+                    "path": "records plans (two at once on the host threads), BGZF inflate " +
+                            ("on the GPU (spg_bgzf_inflate)" if caller.last_gpu_inflate else "on the host")}
         res[tag] = {"bams": n_bams, "positions_per_s_per_bam": n_bams * L_SARS / (t1 - t0),
                     "s_per_bam": (t1 - t0) / n_bams, "ingest_s": t_in, "finalize_s": t1 - t0 - t_in,
-                    "calls": len(calls), "entries_per_bam": int(E),
-                    "path": "device pileup: BGZF inflate (" + ("GPU, k_inflate" if caller._gpu_inflate else "host") +
-                            ") + record scan + depth cap (spp_pileup_plan_records) -> pinned inflated BAM -> H2D -> "
-                            "k_pileup_fill (decode + CIGAR walk) -> accumulate",
-                    "breakdown_one_bam": {"host_plan_records_s": b1 - b0, "inflated_mb": data_mb,
-                                          "h2d_records_plus_gpu_s": g1 - g0,
-                                          "pcie_inclusive_gpu_positions_per_s": L_SARS / (g1 - g0)},
-                    "host_fill_path": host_leg, "process_bams": many_leg}
+                    "calls": len(calls), "reads_per_bam": int(brk["reads"]),
+                    "path": "BAM kept in HBM (process_bam, pileup='device'): compressed file H2D -> k_inflate + k_crc32 "
+                            "-> record scan + stepper filter + fields on the GPU -> fields D2H -> host depth cap / mate "
+                            "pairing (spp_pileup_plan_fields) -> plan H2D -> mate-overlap tweak + k_pileup_fill -> "
+                            "accumulate",
+                    "breakdown_one_bam_device": brk,
+                    "records_plan_path": rec_leg, "host_fill_path": host_leg, "process_bams": many_leg,
+                    "vcqueue_loop": vq_leg}
         caller.engine.close()
         del caller
-    os.environ.pop("SPG_DEVICE_PILEUP", None)
     res["bam_bytes"] = os.path.getsize(bam)
     res["reads"] = n_reads
     res["simulate_s"] = t_sim
@@ -949,12 +1024,14 @@ def end_to_end(args, device):
         calls = caller.prepare_variants()
         caller.engine.sync()
         t1 = time.perf_counter()
+        vq_many = vcqueue_loop(caller, paths[:16], d)
         res["config4_process_bams"] = {
             "bams": len(paths), "depth": 100, "positions_per_s": len(paths) * L_SARS / (t1 - t0),
             "s_per_bam": (t1 - t0) / len(paths), "ingest_s": t_in, "prepare_variants_s": t1 - t0 - t_in,
             "calls": len(calls), "bam_bytes_each": os.path.getsize(paths[0]), "simulate_s": t_sim,
             "path": "process_bams: host plans on a thread pool -> pinned staging -> per-BAM batches -> "
-                    "counted mode (k_acc_lite_run + k_count_list + k_fold_hist) + sparse finalize"}
+                    "counted mode (k_acc_lite_run + k_count_list + k_fold_hist) + sparse finalize",
+            "vcqueue_loop": vq_many}
         caller.engine.close()
         del caller
         for pth in paths:

@@ -50,6 +50,39 @@ class SpgRecords(C.Structure):
                 ("pos_origin", C.c_int64), ("reserved", C.c_int64 * 3)]
 
 
+class SpgBamFilter(C.Structure):
+    _fields_ = [("stepper", C.c_int32), ("flag_filter", C.c_uint32), ("min_mapping_quality", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+class SpgBamReads(C.Structure):
+    """spg_bam_reads / spp_read_fields arrays (host), n_reads each."""
+    _fields_ = [("pos", C.c_void_p), ("end", C.c_void_p), ("mtid", C.c_void_p), ("mpos", C.c_void_p),
+                ("isize", C.c_void_p), ("flag", C.c_void_p), ("l_seq", C.c_void_p), ("name_hash", C.c_void_p)]
+
+
+class SppReadFields(C.Structure):
+    _fields_ = [("n", C.c_int64), ("pos", C.c_void_p), ("end", C.c_void_p), ("mtid", C.c_void_p), ("mpos", C.c_void_p),
+                ("isize", C.c_void_p), ("flag", C.c_void_p), ("l_seq", C.c_void_p), ("name_hash", C.c_void_p)]
+
+
+class SpgBamPlan(C.Structure):
+    _fields_ = [("pos_begin", C.c_int64), ("n_cols", C.c_int64), ("n_entries", C.c_uint64), ("offsets", C.c_void_p),
+                ("n_kept", C.c_int64), ("kept", C.c_void_p), ("n_pairs", C.c_int64), ("pair_a", C.c_void_p),
+                ("pair_b", C.c_void_p), ("pair_col", C.c_void_p), ("pair_orig", C.c_void_p), ("orig_bytes", C.c_uint64),
+                ("max_span", C.c_int64), ("reserved", C.c_int64 * 4)]
+
+
+class SppBamMapInfo(C.Structure):
+    _fields_ = [("comp", C.c_void_p), ("comp_bytes", C.c_uint64), ("members", C.c_void_p), ("n_members", C.c_int64),
+                ("inflated_bytes", C.c_uint64), ("body", C.c_uint64), ("n_ref", C.c_int32), ("reserved", C.c_int32)]
+
+
+# the fields spg_bam_reads_copy returns (name, dtype)
+BAM_READ_FIELDS = (("pos", np.int32), ("end", np.int32), ("mtid", np.int32), ("mpos", np.int32), ("isize", np.int32),
+                   ("flag", np.uint16), ("l_seq", np.uint32), ("name_hash", np.uint64))
+
+
 DETAIL_DTYPE = np.dtype([("pos", "<i8"), ("depth", "<u4"), ("n_alleles", "u1"), ("pad", "u1", 3),
                          ("code", "u1", 16), ("count", "<u4", 16), ("gl", "<f8", 16)])
 
@@ -123,6 +156,12 @@ def gpu_lib():
     _sig(L.spg_bgzf_inflate, i32, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp, C.POINTER(C.c_float))
     _sig(L.spg_bgzf_last_error, C.c_char_p)
     _sig(L.spg_bgzf_inflate_check, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp)
+    _sig(L.spg_bgzf_release, i32, i32)
+    _sig(L.spg_bam_open, i32, vp, vp, u64, vp, i64, u64, i32, i32, C.POINTER(SpgBamFilter), C.POINTER(i64))
+    _sig(L.spg_bam_reads_copy, i32, vp, C.POINTER(SpgBamReads))
+    _sig(L.spg_bam_accumulate, i32, vp, C.POINTER(SpgBamPlan), C.c_uint32)
+    _sig(L.spg_bam_inflate_ms, i32, vp, C.POINTER(C.c_float))
+    _sig(L.spg_bam_release, i32, vp)
     _sig(L.spg_position_entries, i32, vp, i64, vp, vp, i64, C.POINTER(i64))
     _sig(L.spg_input_ticket, i32, vp, C.POINTER(u64))
     _sig(L.spg_wait_ticket, i32, vp, u64)
@@ -176,7 +215,7 @@ SPP_STEPPER = {"all": 0, "nofilter": 1, "samtools": 2}
 class SppParams(C.Structure):
     _fields_ = [("stepper", C.c_int32), ("min_mapping_quality", C.c_int32), ("max_depth", C.c_int32),
                 ("ignore_overlaps", C.c_int32), ("flag_filter", C.c_uint32), ("n_threads", C.c_int32),
-                ("reserved", C.c_int64 * 2)]
+                ("inflate_device", C.c_int32), ("inflate_min_members", C.c_int32), ("reserved", C.c_int64 * 1)]
 
 
 class SimParams(C.Structure):
@@ -214,6 +253,10 @@ def pileup_lib():
     _sig(L.spp_batch_records, C.c_int, vp, C.POINTER(SpgRecords))
     _sig(L.spp_set_host_allocator, C.c_int, vp, vp)
     _sig(L.spp_set_inflater, C.c_int, vp, C.c_int)
+    _sig(L.spp_bam_map_open, C.c_int, vp, C.c_int, C.POINTER(vp), C.POINTER(SppBamMapInfo))
+    _sig(L.spp_bam_map_close, C.c_int, vp)
+    _sig(L.spp_pileup_plan_fields, C.c_int, vp, i32, C.POINTER(SppReadFields), C.POINTER(SppParams), C.POINTER(vp))
+    _sig(L.spp_batch_device_plan, C.c_int, vp, C.POINTER(SpgBamPlan))
     _sig(L.spp_default_sim_params, None, C.POINTER(SimParams))
     _sig(L.spp_simulate_bam, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, i64, C.POINTER(SimParams),
          C.POINTER(i64))
@@ -237,20 +280,19 @@ def use_pinned_records():
     _pinned_records = True
 
 
-_gpu_inflate_dev = None
+_inflater_set = False
 
 
-def use_gpu_inflate(device: int = 0, on: bool = True):
-    """Records plans inflate the BAM's BGZF members on `device` (spg_bgzf_inflate, csrc/spg_inflate.hip) instead of
-    on the host; members the GPU reports bad are inflated on the host.  on=False restores the host inflate."""
-    global _gpu_inflate_dev
+def register_gpu_inflater():
+    """Register spg_bgzf_inflate as the records plans' BGZF inflater (spp_set_inflater).  Registering does not turn it
+    on: each plan selects it through its own parameters (PileupParams.inflate_device), so callers with different
+    choices do not override one another.  Idempotent."""
+    global _inflater_set
+    if _inflater_set:
+        return
     G, P = gpu_lib(), pileup_lib()
-    if on:
-        pcheck(P.spp_set_inflater(C.cast(G.spg_bgzf_inflate, C.c_void_p), int(device)), "spp_set_inflater")
-        _gpu_inflate_dev = int(device)
-    else:
-        pcheck(P.spp_set_inflater(None, 0), "spp_set_inflater")
-        _gpu_inflate_dev = None
+    pcheck(P.spp_set_inflater(C.cast(G.spg_bgzf_inflate, C.c_void_p), 0), "spp_set_inflater")
+    _inflater_set = True
 
 
 def pcheck(rc: int, what: str = ""):

@@ -44,6 +44,11 @@ hipError_t launch_pos_copy(const Hist *H, const int32_t *items, int32_t n, const
                            uint8_t *oc, uint8_t *oq, hipStream_t st);
 hipError_t launch_ck_compact(const Hist &h, uint32_t min_bq, uint64_t *kept, uint64_t *noff, void *scan_tmp,
                              size_t *scan_bytes, uint8_t *oc, uint8_t *oq, hipStream_t st);
+hipError_t launch_inflate(const uint8_t *comp, const spg_bgzf_member *mem, int64_t n, uint8_t *out, uint32_t *status,
+                          hipStream_t st);
+hipError_t launch_bam_scan(const BamArgs &A, int pass, hipStream_t st);
+hipError_t launch_bam_pairs(const BamPairArgs &P, bool tweak, hipStream_t st);
+hipError_t launch_bam_gather(const BamGatherArgs &G, hipStream_t st);
 }  // namespace spg
 
 using namespace spg;
@@ -134,6 +139,45 @@ struct Arena {
     }
 };
 
+// Device buffers of spg_bam_* (one BAM at a time per context; grow-only, freed by spg_bam_release / spg_destroy)
+struct DBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t need(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) { hipError_t e = hipFree(p); if (e != hipSuccess) return e; }
+        p = nullptr;
+        cap = 0;
+        const size_t c = n + n / 8 + 256;
+        hipError_t e = hipMalloc(&p, c);
+        if (e == hipSuccess) cap = c;
+        return e;
+    }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+struct BamDev {
+    DBuf comp, out, mem, status, uoff, start, cnt, base, lohi, rec, fields, err;
+    DBuf kept, pairs, orig, twof, recs_k, tile_first;
+    bool open = false;                 // a BAM is loaded (spg_bam_open succeeded)
+    uint64_t total = 0;                // inflated bytes
+    int64_t n_members = 0;
+    uint32_t n_reads = 0;
+    // field arrays inside `fields`
+    int32_t *pos = nullptr, *end = nullptr, *mtid = nullptr, *mpos = nullptr, *isize = nullptr;
+    uint16_t *flag = nullptr;
+    uint32_t *l_seq = nullptr;
+    uint64_t *nhash = nullptr;
+    float inflate_ms = 0.f;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    void release() {
+        for (DBuf *b : {&comp, &out, &mem, &status, &uoff, &start, &cnt, &base, &lohi, &rec, &fields, &err, &kept, &pairs,
+                        &orig, &twof, &recs_k, &tile_first})
+            b->release();
+        open = false;
+    }
+};
+
 struct spg_ctx {
     int device = 0;
     int n_cu = 256;                     // compute units (the tile kernel's resident grid: 5 workgroups per CU)
@@ -198,6 +242,7 @@ struct spg_ctx {
     int64_t hist_cap = 0;               // 0 = no cap
     int64_t hist_dev_bytes = 0;         // owned history bytes resident in HBM
     int64_t n_spilled = 0;
+    BamDev bam;                         // spg_bam_*: the BAM in HBM
     // spg_accumulate_records: HBM staging of the last records batch (inflated BAM + per-read index), grow-only
     uint8_t *rs = nullptr;
     size_t rs_cap = 0;
@@ -360,6 +405,9 @@ int spg_destroy(spg_ctx *c) {
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     free_spilled(c);
     c->arena.release();
+    c->bam.release();
+    for (hipEvent_t e : c->bam.ev)
+        if (e) (void)hipEventDestroy(e);
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
                     c->d_fused, c->deep_list, c->deep_n, c->cdep, c->cmcf, c->fwm, c->fold_part, c->fold_arrived, c->rs,
@@ -597,14 +645,14 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
                       bool listed = false, bool *list_mode = nullptr, uint32_t t_listed = 128u) {
     if (list_mode) *list_mode = false;
     const HistBatch &hb0 = c->hist[(size_t)idx];
-    static const int64_t target_waves = env_i64("SPG_TARGET_WAVES", 16384);
+    constexpr int64_t target_waves = 16384;
     // Each wave owns G consecutive columns.  A new wave costs a workgroup dispatch (median 1.4 us from
     // the previous wave's end in its slot) and its setup (LUT + CSR offsets, then its first chunk: two
     // memory round trips), so a deep wave gets ~22-30 chunks where that still leaves one grid generation
     // of <= 4,096 waves (16 per CU) to fill the chip; otherwise G targets 16,384 waves.  10,000x: G = 3
     // (interleaved A/B on one box: 109.5 us vs 114.7 us for G = 2, 113.5 us for G = 5).
     int64_t g = std::max<int64_t>(1, (hb0.n_cols + target_waves - 1) / target_waves);
-    if (deep_batch && !getenv("SPG_TARGET_WAVES")) {
+    if (deep_batch) {
         // ~22-30 chunks per wave: G = 3 at both 10,000x (10 chunks a column) and the 8000-capped
         // 7,960x (8 chunks; G = 4 there measured 103.5 vs 95.9 us); 1,000x: G = 16 (list mode below)
         const double avg0 = (double)hb0.n_entries / (double)std::max<int64_t>(1, hb0.n_cols);
@@ -615,8 +663,7 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     // fused (records kept in the wave's finishing ring for the finalize) only when a wave's columns fit the ring;
     // a wider group finishes its ring NB columns at a time, lists the positions that may call, and the caller
     // runs the sparse k_finalize over them (list mode: mid-depth batches such as 1,000x, G = 16)
-    static const bool list_on = [] { const char *e = getenv("SPG_LIST"); return !(e && atoi(e) == 0); }();   // (A/B)
-    if (F && g > NB_RING && deep_batch && !listed && list_on) {
+    if (F && g > NB_RING && deep_batch && !listed) {
         if (list_mode) *list_mode = true;
         F = nullptr;
         O = nullptr;
@@ -657,8 +704,8 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     P.w1 = (uint32_t)std::min<int64_t>(UINT32_MAX, (n_cols + G - 1) / G);
     // Deep batches with G >= 2: the last grid generation (#CUs x 16 waves) gets groups of G / 2 columns,
     // so the waves that start last end sooner (the launch's tail)
-    static const int64_t tail_waves = [] { const char *e = getenv("SPG_TAIL_WAVES"); return e ? atoll(e) : 4096ll; }();
-    if (deep_batch && G >= 2 && tail_waves > 0) {
+    constexpr int64_t tail_waves = 4096;
+    if (deep_batch && G >= 2) {
         const int64_t G2 = G / 2;
         const int64_t tail_cols = std::min<int64_t>(n_cols, tail_waves * G2);
         const int64_t w1 = (n_cols - tail_cols + G - 1) / G;
@@ -670,7 +717,6 @@ static int launch_seg(spg_ctx *c, int64_t idx, bool deep_batch, const FParams *F
     int64_t n_launch_waves = 0;
     P.t_deep = deep_batch ? 1u : 128u;
     P.calls_only = (c->p.flags & SPG_P_CALLS_ONLY) ? 1u : 0u;
-    if (const char *e = getenv("SPG_WAVE_ROT")) P.rot = (uint32_t)atoi(e);
     P.n_entries = hb.n_entries;
     P.dbg = trace_on() ? trace_dbg() : nullptr;
     if (list_mode && *list_mode) {
@@ -744,14 +790,13 @@ struct RunPlan {
     int64_t n_groups, S, kper, tc;
 };
 static int64_t tile_blocks(const spg_ctx *c, int lpc, bool one) {
-    static const int64_t env = [] { const char *e = getenv("SPG_TILE_BLOCKS"); return e ? atoll(e) : 0ll; }();
-    return env > 0 ? env : (int64_t)c->n_cu * tile_blocks_per_cu(lpc, one);
+    return (int64_t)c->n_cu * tile_blocks_per_cu(lpc, one);
 }
 static RunPlan plan_run(const spg_ctx *c, int64_t h0, int64_t h1, int64_t u0, int64_t u1, uint64_t run_entries) {
     const int64_t K = h1 - h0, L = u1 - u0;
     RunPlan R{1, 0, 1, K, 64};
     // bytes of one batch in a tile: TC x mean column length (whole 16-B blocks around it)
-    static const double fill = [] { const char *e = getenv("SPG_TILE_FILL"); return e ? atof(e) : 1984.0; }();
+    constexpr double fill = 1984.0;
     const double mean = (double)run_entries / ((double)K * (double)std::max<int64_t>(1, L));
     while (R.lpc < 8 && (64.0 / R.lpc) * mean > fill) R.lpc *= 2;
     R.tc = 64 / R.lpc;
@@ -858,10 +903,8 @@ static int flush_run(spg_ctx *c, int64_t h1, bool fused) {
     // entries): k_acc_lite, counts + the exact fold of the columns that may call
     const bool lite = fused;
     if (lite) {
-        static const int64_t lb = env_i64("SPG_LITE_BLOCKS", 0);
         P.n_groups = (int32_t)((u1 - u0 + 63) / 64);
-        HIPCHK(launch_lite(P, c->h_hist[h0], c->ref, c->tables, c->acc, lb > 0 ? lb : (int64_t)c->n_cu * lite_blocks_per_cu(),
-                           c->stream));
+        HIPCHK(launch_lite(P, c->h_hist[h0], c->ref, c->tables, c->acc, (int64_t)c->n_cu * lite_blocks_per_cu(), c->stream));
         // the listed positions' exact fold (their records; deep columns are k_acc_seg<1>'s below)
         HIPCHK(launch_lite_fold(P, c->h_hist[h0], c->ref, c->tables, c->acc, 2 * (int64_t)c->n_cu, c->stream));
     } else {
@@ -1059,9 +1102,9 @@ static int upload_records(spg_ctx *c, const spg_records *R, const HistBatch &hb,
 static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64_t *offsets,
                      const uint8_t *base_code, const uint8_t *qual, uint64_t n_entries, uint32_t flags,
                      bool *pageable_copy, int64_t n_samples = 1, const uint32_t *first_sample = nullptr,
-                     const spg_records *recs = nullptr) {
+                     const spg_records *recs = nullptr, const FillArgs *dfill = nullptr) {
     if (n_samples < 1 || n_samples > (1 << 30)) return fail("spg_accumulate_samples: n_samples out of range");
-    static const double deep_min = [] { const char *e = getenv("SPG_DEEP_MIN"); return e ? atof(e) : 256.0; }();
+    constexpr double deep_min = 256.0;
     const bool deep_batch = (n_cols > 0 && (double)n_entries / (double)n_cols >= deep_min) || n_samples > 1 || first_sample;
     // a shallow batch into a countable sample leaves the records stale (it is counted at the next finalize)
     if (deep_batch || n_samples > 1 || !countable(c))
@@ -1072,11 +1115,11 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
     if (pos_begin + n_cols > c->ref_len)
         return fail("spg_accumulate: column range beyond the reference sequence (IndexError in the reference)");
     if (n_cols == 0) return 0;
-    if (!offsets || (n_entries && !recs && (!base_code || !qual))) return fail("spg_accumulate: null buffer");
+    if (!offsets || (n_entries && !recs && !dfill && (!base_code || !qual))) return fail("spg_accumulate: null buffer");
     if (n_entries >= (1ull << 40)) return fail("spg_accumulate: batch too large");
-    const bool dev = !recs && (flags & SPG_IN_DEVICE);
+    const bool dev = !recs && !dfill && (flags & SPG_IN_DEVICE);
     const bool borrow = dev && (flags & SPG_IN_BORROW);
-    if (!dev && !recs && !(flags & SPG_IN_TRUSTED)) {
+    if (!dev && !recs && !dfill && !(flags & SPG_IN_TRUSTED)) {
         // validate the host CSR (offsets O(n_cols), codes O(E)); device inputs are trusted
         if (offsets[0] != 0 || offsets[n_cols] != n_entries)
             return fail("spg_accumulate: offsets[0] must be 0 and offsets[n_cols] == n_entries");
@@ -1119,6 +1162,14 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
         HIPCHK(hipMemcpyAsync(hb.off, offsets, sizeof(uint64_t) * (n_cols + 1), k, cs));
         if (recs) {
             if (int rc = upload_records(c, recs, hb, cs)) return rc;
+        } else if (dfill) {                    // spg_bam_accumulate: the records are in HBM already
+            FillArgs A = *dfill;
+            A.off = hb.off;
+            A.code = hb.code;
+            A.qual = hb.qual;
+            A.err = c->ferr;
+            c->ferr_dirty = true;
+            HIPCHK(launch_pileup_fill(A, cs));
         } else if (n_entries) {
             HIPCHK(hipMemcpyAsync(hb.code, base_code, n_entries, k, cs));
             HIPCHK(hipMemcpyAsync(hb.qual, qual, n_entries, k, cs));
@@ -1140,6 +1191,8 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
         if (recs) {
             if (!(is_pinned(offsets) && (!recs->data_bytes || is_pinned(recs->data)) && (!recs->n_reads || is_pinned(recs->rec))))
                 *pageable_copy = true;
+        } else if (dfill) {
+            if (!is_pinned(offsets)) *pageable_copy = true;
         } else if (!dev && !(is_pinned(offsets) && (!n_entries || (is_pinned(base_code) && is_pinned(qual))))) {
             *pageable_copy = true;
         }
@@ -1178,7 +1231,7 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
     }
     c->pend_entries += n_entries;
     // (calls-only: the pending run waits for the finalize, which counts it — see finalize_counted)
-    static const int64_t run_max = env_i64("SPG_RUN_MAX", 4096);
+    constexpr int64_t run_max = 4096;
     if (!(c->p.flags & SPG_P_CALLS_ONLY) && (int64_t)c->hist.size() - c->pend0 >= run_max)
         if (int rc = flush_run(c)) return rc;
     return enforce_history_cap(c);
@@ -1422,11 +1475,8 @@ static int count_pending(spg_ctx *c) {
         const int64_t K = nh - h0, L = u1 - u0;
         const double mean = (double)run_entries / ((double)K * (double)std::max<int64_t>(1, L));
         // (LPC 2 stages 4 KiB per array: up to ~3,500 B of a batch per 32-column tile)
-        static const int64_t force_lpc = env_i64("SPG_RUN_LPC", 0);
         int lpc = 1;
         while (lpc < 8 && (64.0 / lpc) * mean > (lpc == 2 ? 3500.0 : 2200.0)) lpc *= 2;
-        if (force_lpc == 1 || force_lpc == 2 || force_lpc == 4 || force_lpc == 8) lpc = (int)force_lpc;
-        if (force_lpc == 7) lpc = 0;                   // (A/B: one lane per column, 7 KiB slots)
         const int64_t tc = lpc ? 64 / lpc : 64, n_tiles = (L + tc - 1) / tc;
         const int64_t blocks = (int64_t)c->n_cu * count_run_blocks_per_cu(lpc);
         const int64_t want_items = 2 * blocks * 4;
@@ -2042,6 +2092,272 @@ int spg_history_copy(spg_ctx *c, int64_t i, uint64_t *offsets, uint8_t *base_cod
     if (qual && h.n_entries) HIPCHK(hipMemcpyAsync(qual, h.qual, h.n_entries, hipMemcpyDefault, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
+}
+
+
+// ------------------------------------------------------------------------------------------------------------------
+// spg_bam_*: a BAM kept in HBM (include/spings_gpu.h; kernels in spg_bam.hip, spg_inflate.hip, spg_fill.hip)
+// ------------------------------------------------------------------------------------------------------------------
+static int bam_fallback(const std::string &m) {
+    g_err = m;
+    return 1;
+}
+
+int spg_bam_release(spg_ctx *c) {
+    if (!c) return fail("spg_bam_release: null ctx");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->copy_stream));
+    c->bam.release();
+    return 0;
+}
+
+int spg_bam_inflate_ms(spg_ctx *c, float *ms) {
+    if (!c || !ms) return fail("spg_bam_inflate_ms: null argument");
+    *ms = c->bam.inflate_ms;
+    return 0;
+}
+
+int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *members, int64_t n,
+                 uint64_t body, int32_t tid, int32_t n_ref, const spg_bam_filter *flt, int64_t *n_reads) {
+    if (!c || !comp || !members || !flt || !n_reads || n < 1 || tid < 0 || tid >= n_ref)
+        return fail("spg_bam_open: bad argument");
+    if (flt->stepper < 0 || flt->stepper > 2) return fail("spg_bam_open: bad stepper");
+    HIPCHK(hipSetDevice(c->device));
+    BamDev &B = c->bam;
+    B.open = false;
+    *n_reads = 0;
+    std::vector<uint64_t> uoff((size_t)n + 1, 0);
+    for (int64_t i = 0; i < n; i++) {
+        const spg_bgzf_member &m = members[i];
+        if (m.coff + m.clen + 8 > comp_bytes || m.ulen > 65536) return fail("spg_bam_open: member outside the file");
+        if (m.uoff != uoff[(size_t)i]) return fail("spg_bam_open: members' inflated offsets are not contiguous");
+        uoff[(size_t)i + 1] = uoff[(size_t)i] + m.ulen;
+    }
+    const uint64_t total = uoff[(size_t)n];
+    if (body >= total || total >= ((uint64_t)1 << 40)) return fail("spg_bam_open: bad header end");
+    hipStream_t cs = c->copy_stream;
+    if (!B.ev[0]) { HIPCHK(hipEventCreate(&B.ev[0])); HIPCHK(hipEventCreate(&B.ev[1])); }
+    const size_t nm = (size_t)n;
+    HIPCHK(B.comp.need(comp_bytes + 64));
+    HIPCHK(B.out.need(total + 64));
+    HIPCHK(B.mem.need(sizeof(spg_bgzf_member) * nm));
+    HIPCHK(B.status.need(sizeof(uint32_t) * nm));
+    HIPCHK(B.uoff.need(sizeof(uint64_t) * (nm + 1)));
+    HIPCHK(B.start.need(sizeof(uint64_t) * nm));
+    HIPCHK(B.cnt.need(sizeof(uint32_t) * nm));
+    HIPCHK(B.base.need(sizeof(uint32_t) * (nm + 1)));
+    HIPCHK(B.lohi.need(sizeof(int64_t) * 2 * nm));
+    HIPCHK(B.err.need(64));
+    HIPCHK(hipMemcpyAsync(B.comp.p, comp, comp_bytes, hipMemcpyHostToDevice, cs));
+    HIPCHK(hipMemsetAsync(B.comp.as<uint8_t>() + comp_bytes, 0, 64, cs));
+    HIPCHK(hipMemcpyAsync(B.mem.p, members, sizeof(spg_bgzf_member) * nm, hipMemcpyHostToDevice, cs));
+    HIPCHK(hipMemcpyAsync(B.uoff.p, uoff.data(), sizeof(uint64_t) * (nm + 1), hipMemcpyHostToDevice, cs));
+    HIPCHK(hipMemsetAsync(B.out.as<uint8_t>() + total, 0, 64, cs));
+    HIPCHK(hipMemsetAsync(B.err.p, 0, 64, cs));
+    HIPCHK(hipEventRecord(B.ev[0], cs));
+    HIPCHK(launch_inflate(B.comp.as<uint8_t>(), B.mem.as<spg_bgzf_member>(), n, B.out.as<uint8_t>(), B.status.as<uint32_t>(), cs));
+    HIPCHK(hipEventRecord(B.ev[1], cs));
+    BamArgs A{};
+    A.data = B.out.as<uint8_t>();
+    A.total = total;
+    A.body = body;
+    A.uoff = B.uoff.as<uint64_t>();
+    A.n_members = n;
+    A.tid = tid;
+    A.n_ref = n_ref;
+    A.stepper = flt->stepper;
+    A.flag_filter = flt->flag_filter;
+    A.min_mapq = flt->min_mapping_quality;
+    A.start = B.start.as<uint64_t>();
+    A.cnt = B.cnt.as<uint32_t>();
+    A.base = B.base.as<uint32_t>();
+    A.pos_lo = B.lohi.as<int64_t>();
+    A.pos_hi = A.pos_lo + nm;
+    A.err = B.err.as<uint32_t>();
+    HIPCHK(launch_bam_scan(A, 0, cs));
+    HIPCHK(launch_bam_scan(A, 1, cs));
+    std::vector<uint32_t> st(nm), cnt(nm), err(1);
+    std::vector<int64_t> lohi(2 * nm);
+    HIPCHK(hipMemcpyAsync(st.data(), B.status.p, sizeof(uint32_t) * nm, hipMemcpyDeviceToHost, cs));
+    HIPCHK(hipMemcpyAsync(cnt.data(), B.cnt.p, sizeof(uint32_t) * nm, hipMemcpyDeviceToHost, cs));
+    HIPCHK(hipMemcpyAsync(lohi.data(), B.lohi.p, sizeof(int64_t) * 2 * nm, hipMemcpyDeviceToHost, cs));
+    HIPCHK(hipMemcpyAsync(err.data(), B.err.p, sizeof(uint32_t), hipMemcpyDeviceToHost, cs));
+    HIPCHK(hipStreamSynchronize(cs));
+    if (hipEventElapsedTime(&B.inflate_ms, B.ev[0], B.ev[1]) != hipSuccess) B.inflate_ms = -1.f;
+    for (size_t i = 0; i < nm; i++)
+        if (st[i] != 0)
+            return bam_fallback("spg_bam_open: member " + std::to_string(i) + " did not inflate on the GPU (status " +
+                                std::to_string(st[i]) + ")");
+    if (err[0] & 1u) return bam_fallback("spg_bam_open: the record chains of the members disagree");
+    int64_t last = -1;
+    for (size_t i = 0; i < nm; i++) {
+        if (lohi[i] == INT64_MAX) continue;
+        if (lohi[i] < last || (err[0] & 2u)) return fail("spg_bam_open: BAM is not coordinate-sorted");
+        last = lohi[nm + i];
+    }
+    std::vector<uint32_t> base(nm + 1, 0);
+    uint64_t tot = 0;
+    for (size_t i = 0; i < nm; i++) { base[i] = (uint32_t)tot; tot += cnt[i]; }
+    if (tot >= ((uint64_t)1 << 31)) return fail("spg_bam_open: more than 2^31 reads");
+    base[nm] = (uint32_t)tot;
+    const size_t nr = (size_t)tot;
+    HIPCHK(B.rec.need(sizeof(uint64_t) * (nr + 1)));
+    // fields: pos end mtid mpos isize (i32), l_seq (u32), nhash (u64), flag (u16)
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t f32 = al(4 * (nr + 1)), f64 = al(8 * (nr + 1)), f16 = al(2 * (nr + 1));
+    HIPCHK(B.fields.need(6 * f32 + f64 + f16));
+    uint8_t *fb = B.fields.as<uint8_t>();
+    B.pos = reinterpret_cast<int32_t *>(fb);
+    B.end = reinterpret_cast<int32_t *>(fb + f32);
+    B.mtid = reinterpret_cast<int32_t *>(fb + 2 * f32);
+    B.mpos = reinterpret_cast<int32_t *>(fb + 3 * f32);
+    B.isize = reinterpret_cast<int32_t *>(fb + 4 * f32);
+    B.l_seq = reinterpret_cast<uint32_t *>(fb + 5 * f32);
+    B.nhash = reinterpret_cast<uint64_t *>(fb + 6 * f32);
+    B.flag = reinterpret_cast<uint16_t *>(fb + 6 * f32 + f64);
+    HIPCHK(hipMemcpyAsync(B.base.p, base.data(), sizeof(uint32_t) * (nm + 1), hipMemcpyHostToDevice, cs));
+    A.rec = B.rec.as<uint64_t>();
+    A.n_reads = (uint32_t)nr;
+    A.pos = B.pos; A.end = B.end; A.mtid = B.mtid; A.mpos = B.mpos; A.isize = B.isize;
+    A.flag = B.flag; A.l_seq = B.l_seq; A.nhash = B.nhash;
+    HIPCHK(launch_bam_scan(A, 2, cs));
+    HIPCHK(launch_bam_scan(A, 3, cs));
+    HIPCHK(hipMemcpyAsync(err.data(), B.err.p, sizeof(uint32_t), hipMemcpyDeviceToHost, cs));
+    HIPCHK(hipStreamSynchronize(cs));
+    if (err[0] & 4u) return fail("spg_bam_open: corrupt BAM record (field lengths exceed block_size)");
+    B.total = total;
+    B.n_members = n;
+    B.n_reads = (uint32_t)nr;
+    B.open = true;
+    *n_reads = (int64_t)nr;
+    return 0;
+}
+
+int spg_bam_reads_copy(spg_ctx *c, const spg_bam_reads *o) {
+    if (!c || !o) return fail("spg_bam_reads_copy: null argument");
+    BamDev &B = c->bam;
+    if (!B.open) return fail("spg_bam_reads_copy: no BAM open (spg_bam_open)");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t cs = c->copy_stream;
+    const size_t n = B.n_reads;
+    if (n) {
+        struct { void *h; const void *d; size_t w; } cp[] = {
+            {o->pos, B.pos, 4}, {o->end, B.end, 4}, {o->mtid, B.mtid, 4}, {o->mpos, B.mpos, 4}, {o->isize, B.isize, 4},
+            {o->flag, B.flag, 2}, {o->l_seq, B.l_seq, 4}, {o->name_hash, B.nhash, 8}};
+        for (auto &x : cp)
+            if (x.h) HIPCHK(hipMemcpyAsync(x.h, x.d, x.w * n, hipMemcpyDeviceToHost, cs));
+    }
+    HIPCHK(hipStreamSynchronize(cs));
+    return 0;
+}
+
+int spg_bam_accumulate(spg_ctx *c, const spg_bam_plan *P, uint32_t flags) {
+    (void)flags;
+    if (!c || !P) return fail("spg_bam_accumulate: null argument");
+    if (!c->lut_set) return fail("spg_accumulate: spg_set_eps_lut not called");
+    if (!c->ref) return fail("spg_accumulate: spg_set_reference not called");
+    BamDev &B = c->bam;
+    if (!B.open) return fail("spg_bam_accumulate: no BAM open (spg_bam_open)");
+    if (P->n_cols < 0 || P->n_cols > ((int64_t)1 << 31) - 128) return fail("spg_bam_accumulate: n_cols out of range");
+    if (P->n_kept < 0 || P->n_kept > (int64_t)B.n_reads || P->n_pairs < 0 || P->n_pairs > P->n_kept || P->max_span < 0)
+        return fail("spg_bam_accumulate: bad read / pair counts");
+    if (P->n_cols > 0 && (!P->offsets || (P->n_kept && !P->kept) ||
+                          (P->n_pairs && (!P->pair_a || !P->pair_b || !P->pair_col || !P->pair_orig))))
+        return fail("spg_bam_accumulate: null buffer");
+    if (P->n_cols == 0) { B.open = false; return 0; }
+    if (P->offsets[0] != 0 || P->offsets[P->n_cols] != P->n_entries)
+        return fail("spg_bam_accumulate: offsets[0] must be 0 and offsets[n_cols] == n_entries");
+    uint64_t desc = 0;
+    for (int64_t i = 0; i < P->n_cols; i++) desc |= (uint64_t)(P->offsets[i + 1] < P->offsets[i]);
+    if (desc) return fail("spg_bam_accumulate: offsets not monotone");
+    uint64_t need_orig = 0;
+    for (int64_t j = 0; j < P->n_pairs; j++) {
+        if (P->pair_a[j] >= B.n_reads || P->pair_b[j] >= B.n_reads) return fail("spg_bam_accumulate: pair read out of range");
+        need_orig = std::max<uint64_t>(need_orig, P->pair_orig[j]);
+    }
+    if (P->n_pairs && P->orig_bytes < need_orig) return fail("spg_bam_accumulate: orig_bytes too small");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t cs = c->copy_stream;
+    const size_t nk = (size_t)P->n_kept, np = (size_t)P->n_pairs, nr = B.n_reads;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    HIPCHK(B.kept.need(4 * nk + 16));
+    const size_t o_pb = al(4 * np), o_col = o_pb + al(4 * np), o_oq = o_col + al(8 * np);
+    HIPCHK(B.pairs.need(o_oq + al(8 * np) + 16));
+    HIPCHK(B.orig.need(P->orig_bytes + 64));
+    HIPCHK(B.twof.need(4 * nr + 16));
+    const size_t o_pos = al(8 * nk), o_end = o_pos + al(4 * nk), o_tw = o_end + al(4 * nk);
+    HIPCHK(B.recs_k.need(o_tw + al(4 * nk) + 16));
+    const int64_t n_tiles = (P->n_cols + 63) / 64;
+    HIPCHK(B.tile_first.need(4 * (size_t)(n_tiles + 1)));
+    if (nk) HIPCHK(hipMemcpyAsync(B.kept.p, P->kept, 4 * nk, hipMemcpyHostToDevice, cs));
+    uint8_t *pb = B.pairs.as<uint8_t>();
+    if (np) {
+        HIPCHK(hipMemcpyAsync(pb, P->pair_a, 4 * np, hipMemcpyHostToDevice, cs));
+        HIPCHK(hipMemcpyAsync(pb + o_pb, P->pair_b, 4 * np, hipMemcpyHostToDevice, cs));
+        HIPCHK(hipMemcpyAsync(pb + o_col, P->pair_col, 8 * np, hipMemcpyHostToDevice, cs));
+        HIPCHK(hipMemcpyAsync(pb + o_oq, P->pair_orig, 8 * np, hipMemcpyHostToDevice, cs));
+        BamPairArgs Q{};
+        Q.data = B.out.as<uint8_t>();
+        Q.wdata = B.out.as<uint8_t>();
+        Q.rec = B.rec.as<uint64_t>();
+        Q.n_reads = (uint32_t)nr;
+        Q.n_pairs = (uint32_t)np;
+        Q.pa = reinterpret_cast<const uint32_t *>(pb);
+        Q.pb = reinterpret_cast<const uint32_t *>(pb + o_pb);
+        Q.oq = reinterpret_cast<const uint64_t *>(pb + o_oq);
+        Q.orig = B.orig.as<uint8_t>();
+        Q.err = B.err.as<uint32_t>() + 1;
+        // names first (a hash collision must not tweak anything): the plan is refused before any change
+        uint32_t e = 0;
+        HIPCHK(hipMemsetAsync(Q.err, 0, 4, cs));
+        HIPCHK(launch_bam_pairs(Q, false, cs));
+        HIPCHK(hipMemcpyAsync(&e, Q.err, 4, hipMemcpyDeviceToHost, cs));
+        HIPCHK(hipStreamSynchronize(cs));
+        if (e & 8u) return bam_fallback("spg_bam_accumulate: paired reads with equal name hashes have different names");
+        HIPCHK(launch_bam_pairs(Q, true, cs));
+    }
+    uint8_t *rk = B.recs_k.as<uint8_t>();
+    BamGatherArgs G{};
+    G.n_reads = (uint32_t)nr;
+    G.n_kept = (uint32_t)nk;
+    G.n_pairs = (uint32_t)np;
+    G.kept = B.kept.as<uint32_t>();
+    G.pa = reinterpret_cast<const uint32_t *>(pb);
+    G.rec = B.rec.as<uint64_t>();
+    G.pos = B.pos;
+    G.end = B.end;
+    G.twof = B.twof.as<int32_t>();
+    G.rec_k = reinterpret_cast<uint64_t *>(rk);
+    G.rpos_k = reinterpret_cast<int32_t *>(rk + o_pos);
+    G.rend_k = reinterpret_cast<int32_t *>(rk + o_end);
+    G.tw_k = reinterpret_cast<int32_t *>(rk + o_tw);
+    G.err = c->ferr;
+    HIPCHK(hipMemsetAsync(G.twof, 0xFF, 4 * nr, cs));
+    HIPCHK(launch_bam_gather(G, cs));
+    FillArgs F{};
+    F.data = B.out.as<uint8_t>();
+    F.data_bytes = B.total;
+    F.rec = G.rec_k;
+    F.rpos = G.rpos_k;
+    F.rend = G.rend_k;
+    F.tweak = G.tw_k;
+    F.tw_col = reinterpret_cast<const int64_t *>(pb + o_col);
+    F.tw_q = reinterpret_cast<const uint64_t *>(pb + o_oq);
+    F.orig = B.orig.as<uint8_t>();
+    F.orig_bytes = P->orig_bytes;
+    F.tile_first = B.tile_first.as<uint32_t>();
+    F.pos_begin = P->pos_begin;
+    F.n_cols = (int32_t)P->n_cols;
+    F.n_tiles = (int32_t)n_tiles;
+    F.n_reads = (uint32_t)nk;
+    F.back = (int32_t)((P->max_span + 63) / 64);
+    c->ferr_dirty = true;
+    bool pageable = false;
+    B.open = false;                        // (the next spg_bam_open reuses the buffers after this fill: same stream)
+    int rc = add_batch(c, P->pos_begin, P->n_cols, P->offsets, nullptr, nullptr, P->n_entries, SPG_IN_TRUSTED, &pageable,
+                       1, nullptr, nullptr, &F);
+    if (pageable) HIPCHK(hipStreamSynchronize(c->copy_stream));
+    return rc;
 }
 
 }  // extern "C"

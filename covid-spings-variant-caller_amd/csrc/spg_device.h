@@ -257,4 +257,47 @@ struct FillArgs {
     uint32_t *err;                 // |= 2: the records disagree with the offsets (inconsistent plan)
 };
 
+// A BAM in HBM (spg_bam.hip, include/spings_gpu.h spg_bam_*)
+constexpr uint64_t BAM_NONE = ~0ull;
+struct BamArgs {
+    const uint8_t *data;           // the inflated stream (64 readable pad bytes past total)
+    uint64_t total, body;          // its length; the first record's offset (after the header)
+    const uint64_t *uoff;          // [n_members + 1] members' inflated offsets
+    int64_t n_members;
+    int32_t tid, n_ref;
+    int32_t stepper;               // SPP_STEPPER_*: 0 all, 1 nofilter, 2 samtools
+    uint32_t flag_filter;
+    int32_t min_mapq;
+    uint32_t n_reads;              // fields pass: listed reads
+    uint64_t *start;               // [n_members] first record start in the member's range (BAM_NONE: none)
+    uint32_t *cnt, *base;          // kept records per member's chain; their exclusive prefix
+    int64_t *pos_lo, *pos_hi;      // first / last position of the contig's records per chain (sort order)
+    uint64_t *rec;                 // listed reads: offset of the refID field
+    int32_t *pos, *end, *mtid, *mpos, *isize;
+    uint16_t *flag;
+    uint32_t *l_seq;
+    uint64_t *nhash;
+    uint32_t *err;                 // 1: chains disagree / truncated record; 2: not sorted; 4: corrupt lengths
+};
+struct BamPairArgs {
+    const uint8_t *data;
+    uint8_t *wdata;                // the same stream, written (tweak)
+    const uint64_t *rec;
+    uint32_t n_reads, n_pairs;
+    const uint32_t *pa, *pb;       // pair j: first mate's / second mate's read index
+    const uint64_t *oq;            // pair j: offset of the first mate's saved qualities in orig
+    uint8_t *orig;
+    uint32_t *err;                 // 8: a pair's names differ (a name-hash collision)
+};
+struct BamGatherArgs {
+    uint32_t n_reads, n_kept, n_pairs;
+    const uint32_t *kept, *pa;
+    const uint64_t *rec;
+    const int32_t *pos, *end;
+    int32_t *twof;                 // [n_reads] pair index of a first mate (-1: none)
+    uint64_t *rec_k;
+    int32_t *rpos_k, *rend_k, *tw_k;
+    uint32_t *err;
+};
+
 }  // namespace spg

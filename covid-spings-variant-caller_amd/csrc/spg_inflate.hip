@@ -324,10 +324,11 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
 }
 
 // status: 0 ok; 1 bad block type; 2 bad stored length; 3 bad code lengths; 4 bad table; 5 bad symbol;
-// 6 distance too far back; 7 output overrun; 8 input overrun; 9 wrong size.
+// 6 distance too far back; 7 output overrun; 8 input overrun; 9 wrong size; 10 CRC32 mismatch (k_crc32).
 // mpw members per block, one per lane (lanes >= mpw idle), each with its SLICE of the block's LDS.  Latency-bound
 // (a member's symbols are a dependent chain): 96 VGPRs for 5 waves per SIMD, 3 members per block (r04ze: 19.3 ms on
 // the 10,000x BAM vs 20.0 at 4 waves, 23.4 at 4 members per block)
+constexpr int INFLATE_MPW = 3;
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_inflate(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
                                                 int64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ status, int mpw) {
     extern __shared__ __align__(16) uint8_t inf_lds[];
@@ -335,6 +336,76 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     const int64_t m = (int64_t)blockIdx.x * mpw + threadIdx.x;
     if (m >= n) return;
     status[m] = inflate_member(comp, mem[m], out, inf_lds + (size_t)threadIdx.x * SLICE);
+}
+
+// CRC-32 (zlib's reflected polynomial) arithmetic: a * b mod P and x^(8 n) mod P, as zlib's multmodp / x2nmodp
+__device__ __forceinline__ uint32_t crc_multmodp(uint32_t a, uint32_t b) {
+    uint32_t m = 1u << 31, p = 0;
+    for (int i = 0; i < 32; i++) {
+        if (a & m) p ^= b;
+        m >>= 1;
+        b = (b & 1u) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+    }
+    return p;
+}
+__device__ __forceinline__ uint32_t crc_x8n(uint32_t n) {     // x^(8 n) mod P
+    uint32_t r = 1u << 31, base = 1u << 30;                     // 1, x
+    for (uint64_t e = 8ull * n; e; e >>= 1) {
+        if (e & 1) r = crc_multmodp(base, r);
+        base = crc_multmodp(base, base);
+    }
+    return r;
+}
+
+// Each member's output checked against the CRC32 in its BGZF trailer (a member the decoder got wrong with the right
+// length would otherwise pass): one wave per member, lane j the CRC of bytes [1 KiB j, 1 KiB (j + 1)) through an LDS
+// table, the 64 partial CRCs combined in order (crc32_combine: crc(A B) = crc(A) x^(8 |B|) + crc(B) mod P).
+__global__ __launch_bounds__(256) void k_crc32(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
+                                               int64_t n, const uint8_t *__restrict__ out, uint32_t *__restrict__ status) {
+    __shared__ uint32_t T[256];
+    __shared__ uint32_t part[4][64];
+    for (int i = threadIdx.x; i < 256; i += 256) {
+        uint32_t c = (uint32_t)i;
+        for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
+        T[i] = c;
+    }
+    __syncthreads();
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t m = (int64_t)blockIdx.x * 4 + w;
+    if (m >= n) return;                                         // (wave-uniform; no barrier below)
+    if (status[m] != 0) return;
+    const spg_bgzf_member M = mem[m];
+    const uint32_t a = (uint32_t)lane * 1024u, e = min(M.ulen, a + 1024u);
+    typedef __attribute__((address_space(1))) const uint8_t gu8;
+    gu8 *o = (gu8 *)(out + M.uoff);
+    uint32_t c = 0xFFFFFFFFu;
+    for (uint32_t i = a; i < e; i++) c = T[(c ^ o[i]) & 0xFFu] ^ (c >> 8);
+    part[w][lane] = ~c;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (lane == 0) {
+        const uint32_t nseg = (M.ulen + 1023u) / 1024u;
+        uint32_t crc = 0;                                       // crc32 of the empty string
+        const uint32_t op1k = crc_x8n(1024);
+        for (uint32_t j = 0; j < nseg; j++) {
+            const uint32_t len = min(1024u, M.ulen - 1024u * j);
+            crc = crc_multmodp(len == 1024u ? op1k : crc_x8n(len), crc) ^ part[w][j];
+        }
+        const uint8_t *t = comp + M.coff + M.clen;
+        const uint32_t want = (uint32_t)t[0] | (uint32_t)t[1] << 8 | (uint32_t)t[2] << 16 | (uint32_t)t[3] << 24;
+        if (crc != want) status[m] = 10;
+    }
+}
+
+hipError_t launch_inflate(const uint8_t *comp, const spg_bgzf_member *mem, int64_t n, uint8_t *out, uint32_t *status,
+                          hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_inflate, dim3((unsigned)((n + INFLATE_MPW - 1) / INFLATE_MPW)), dim3(64),
+                       (size_t)INFLATE_MPW * SLICE, st, comp, mem, n, out, status, INFLATE_MPW);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_crc32, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, comp, mem, n, (const uint8_t *)out, status);
+    return hipGetLastError();
 }
 
 }  // namespace spg
@@ -398,42 +469,67 @@ int spg_bgzf_inflate_check(const uint8_t *comp, size_t comp_bytes, const spg_bgz
 int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const spg_bgzf_member *members, int64_t n,
                      uint8_t *out, size_t out_bytes, uint32_t *status, float *kernel_ms) {
     if (n < 0 || (n && (!comp || !members || !out || !status))) return ifail("spg_bgzf_inflate: bad argument");
+    for (int64_t i = 0; i < n; i++) {
+        const spg_bgzf_member &m = members[i];
+        if (m.coff + m.clen + 8 > comp_bytes || m.uoff + m.ulen > out_bytes || m.ulen > 65536)
+            return ifail("spg_bgzf_inflate: member " + std::to_string(i) + " outside the buffers");
+    }
+    if (kernel_ms) *kernel_ms = 0.f;
+    if (n == 0) return 0;
+    // one caller per device at a time (the device's scratch buffers are shared); the caller's current device is restored
     std::lock_guard<std::mutex> lk(g_inf_mu);
-    int nd = 0;
+    int prev = 0, nd = 0;
+    ICHK(hipGetDevice(&prev));
     ICHK(hipGetDeviceCount(&nd));
     if (device < 0 || device >= nd) return ifail("spg_bgzf_inflate: bad device");
     if ((int)g_inf.size() < nd) g_inf.resize((size_t)nd);
     InflateDev &D = g_inf[(size_t)device];
+    struct Restore { int d; ~Restore() { (void)hipSetDevice(d); } } restore{prev};
     ICHK(hipSetDevice(device));
     if (!D.st) {
         ICHK(hipStreamCreateWithFlags(&D.st, hipStreamNonBlocking));
         ICHK(hipEventCreate(&D.ev[0]));
         ICHK(hipEventCreate(&D.ev[1]));
     }
-    for (int64_t i = 0; i < n; i++) {
-        const spg_bgzf_member &m = members[i];
-        if (m.coff + m.clen + 8 > comp_bytes || m.uoff + m.ulen > out_bytes || m.ulen > 65536)
-            return ifail("spg_bgzf_inflate: member " + std::to_string(i) + " outside the buffers");
-    }
-    if (n == 0) return 0;
     if (grow(D.comp, D.comp_cap, comp_bytes + 64) || grow(D.out, D.out_cap, out_bytes + 64) ||
         grow(D.mem, D.mem_bytes, (size_t)n * sizeof(spg_bgzf_member)) ||
         grow(D.status, D.status_bytes, (size_t)n * sizeof(uint32_t)))
         return ifail("spg_bgzf_inflate: out of device memory");
-    ICHK(hipMemcpyAsync(D.comp, comp, comp_bytes, hipMemcpyHostToDevice, D.st));
-    ICHK(hipMemsetAsync(D.comp + comp_bytes, 0, 64, D.st));
-    ICHK(hipMemcpyAsync(D.mem, members, (size_t)n * sizeof(spg_bgzf_member), hipMemcpyHostToDevice, D.st));
-    ICHK(hipEventRecord(D.ev[0], D.st));
-    // members per block (one per lane, SLICE bytes of LDS each): few per wave diverge less and spread over more SIMDs
-    static const int mpw = [] { const char *e = getenv("SPG_INFLATE_MPW"); const int v = e ? atoi(e) : 3; return v >= 1 && v <= 16 ? v : 3; }();
-    hipLaunchKernelGGL(spg::k_inflate, dim3((unsigned)((n + mpw - 1) / mpw)), dim3(64), (size_t)mpw * spg::SLICE, D.st, D.comp,
-                       D.mem, n, D.out, D.status, mpw);
-    ICHK(hipGetLastError());
-    ICHK(hipEventRecord(D.ev[1], D.st));
-    ICHK(hipMemcpyAsync(out, D.out, out_bytes, hipMemcpyDeviceToHost, D.st));
-    ICHK(hipMemcpyAsync(status, D.status, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, D.st));
-    ICHK(hipStreamSynchronize(D.st));
-    if (kernel_ms) ICHK(hipEventElapsedTime(kernel_ms, D.ev[0], D.ev[1]));
+    // after the first enqueue every failure drains the stream before returning: the caller's `out` may be the target of a
+    // queued copy, and it inflates failed members into it next
+    auto drained = [&](int rc) { (void)hipStreamSynchronize(D.st); return rc; };
+#define IQ(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return drained(ifail(std::string("spg_bgzf_inflate: ") + #x + ": " + hipGetErrorString(e_))); } while (0)
+    IQ(hipMemcpyAsync(D.comp, comp, comp_bytes, hipMemcpyHostToDevice, D.st));
+    IQ(hipMemsetAsync(D.comp + comp_bytes, 0, 64, D.st));
+    IQ(hipMemcpyAsync(D.mem, members, (size_t)n * sizeof(spg_bgzf_member), hipMemcpyHostToDevice, D.st));
+    IQ(hipEventRecord(D.ev[0], D.st));
+    IQ(spg::launch_inflate(D.comp, D.mem, n, D.out, D.status, D.st));
+    IQ(hipEventRecord(D.ev[1], D.st));
+    IQ(hipMemcpyAsync(out, D.out, out_bytes, hipMemcpyDeviceToHost, D.st));
+    IQ(hipMemcpyAsync(status, D.status, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, D.st));
+    IQ(hipStreamSynchronize(D.st));
+#undef IQ
+    if (kernel_ms && hipEventElapsedTime(kernel_ms, D.ev[0], D.ev[1]) != hipSuccess) *kernel_ms = -1.f;   // (timing only)
+    return 0;
+}
+
+// The device's inflate scratch freed (it only grows otherwise: one large BAM would keep its size in HBM)
+int spg_bgzf_release(int device) {
+    std::lock_guard<std::mutex> lk(g_inf_mu);
+    if (device < 0 || (size_t)device >= g_inf.size()) return 0;
+    InflateDev &D = g_inf[(size_t)device];
+    if (!D.st) return 0;
+    int prev = 0;
+    ICHK(hipGetDevice(&prev));
+    ICHK(hipSetDevice(device));
+    (void)hipStreamSynchronize(D.st);
+    for (void *p : {(void *)D.comp, (void *)D.out, (void *)D.mem, (void *)D.status})
+        if (p) (void)hipFree(p);
+    D.comp = D.out = nullptr;
+    D.mem = nullptr;
+    D.status = nullptr;
+    D.comp_cap = D.out_cap = D.mem_bytes = D.status_bytes = 0;
+    ICHK(hipSetDevice(prev));
     return 0;
 }
 }

@@ -180,8 +180,12 @@ struct Reads {                 // one contig's reads, structure of arrays
         memcpy(&v, raw + rec[r] + 32 + raw[rec[r] + 8] + 4 * (size_t)i, 4);
         return v;
     }
+    // device plans (spp_pileup_plan_fields): names known by their 64-bit hash only (pairs verified on the device)
+    Vec<uint64_t> nhash;
+    bool hashed = false;
     std::string name(size_t r) const { return std::string(name_view(r)); }
     std::string_view name_view(size_t r) const {        // (valid while the reads are: no copy)
+        if (hashed) return std::string_view(reinterpret_cast<const char *>(nhash.data() + r), sizeof(uint64_t));
         if (!raw) return std::string_view(names.data() + name_off[r]);
         const uint8_t ln = raw[rec[r] + 8];
         return std::string_view((const char *)raw + rec[r] + 32, ln ? ln - 1u : 0u);
@@ -197,8 +201,9 @@ struct Reads {                 // one contig's reads, structure of arrays
     void clear() {                      // empty, keeping every array's capacity (and its resident pages)
         pos.clear(); end.clear(); mpos.clear(); isize.clear(); mtid.clear(); flag.clear(); mapq.clear();
         cig_off.clear(); name_off.clear(); n_cig.clear(); l_seq.clear(); cigar.clear(); bases.clear();
-        names.clear(); rec.clear();
+        names.clear(); rec.clear(); nhash.clear();
         raw = nullptr;
+        hashed = false;
         dlo = INT64_MIN; dhi = INT64_MAX; max_span = 0;
         arena.clear();
     }
@@ -635,7 +640,6 @@ void read_bam(const spp_file *f, int32_t tid, const spp_params &p, Reads &R) {
 spp_alloc_fn g_alloc = nullptr;
 spp_free_fn g_free = nullptr;
 std::atomic<spp_inflate_fn> g_inflate{nullptr};  // GPU inflater of the records plans (spp_set_inflater)
-std::atomic<int> g_inflate_dev{0};
 
 struct HostBuf {
     uint8_t *p = nullptr;
@@ -724,27 +728,42 @@ template <class Fn> void par_tasks(size_t n, int nt, Fn &&fn) {
 // members in file order; this thread scans the records as the inflated prefix grows, inflating members
 // itself while it waits), then the kept records' fixed fields parsed in parallel.  Bases and qualities
 // stay packed in `out`.
-size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &R, HostBuf &out) {
-    const int nt = std::max(1, std::min(p.n_threads, 64));
-    const auto tm0 = std::chrono::steady_clock::now();
-    const int fd = open(f->path.c_str(), O_RDONLY);
-    if (fd < 0) throw std::runtime_error("cannot open " + f->path);
+// A BGZF BAM mapped and its members located (each member's payload offset / length and inflated length; uoff: the
+// members' offsets in the inflated stream).  The mapping is released on a helper thread.
+struct Blk { size_t off, clen, ulen; };
+struct BamMap {
+    const uint8_t *m = nullptr;
+    size_t fsz = 0;
+    std::vector<Blk> blks;
+    std::vector<size_t> uoff;
+    size_t total = 0;
+    std::chrono::steady_clock::time_point tmm, tms;      // (SPP_TIMING) after the page touch / the parallel search
+    BamMap() = default;
+    BamMap(const BamMap &) = delete;
+    BamMap &operator=(const BamMap &) = delete;
+    ~BamMap() {
+        if (!m) return;
+        // (unmapped on a helper thread: tearing down the mapped pages took 5-12 ms per 0.2 GB; parallel preads into a
+        // buffer instead of the mapping were slower still, 4 GB/s)
+        void *mp = const_cast<uint8_t *>(m);
+        const size_t n = fsz;
+        try { std::thread([mp, n] { munmap(mp, n); }).detach(); } catch (...) { munmap(mp, n); }
+    }
+};
+
+void map_bam(const std::string &path, int nt, BamMap &M) {
+    const int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) throw std::runtime_error("cannot open " + path);
     struct stat st;
-    if (fstat(fd, &st) != 0) { close(fd); throw std::runtime_error("cannot stat " + f->path); }
+    if (fstat(fd, &st) != 0) { close(fd); throw std::runtime_error("cannot stat " + path); }
     const size_t fsz = (size_t)st.st_size;
     if (fsz == 0) { close(fd); throw std::runtime_error("not a BAM file"); }
     void *mp = mmap(nullptr, fsz, PROT_READ, MAP_PRIVATE, fd, 0);
     close(fd);
-    if (mp == MAP_FAILED) throw std::runtime_error("cannot map " + f->path);
-    // (unmapped on a helper thread: tearing down the mapped pages took 5-12 ms per 0.2 GB; parallel preads into a
-    // buffer instead of the mapping were slower still, 4 GB/s)
-    struct Unmap {
-        void *m; size_t n;
-        ~Unmap() {
-            try { std::thread([m = m, n = n] { munmap(m, n); }).detach(); } catch (...) { munmap(m, n); }
-        }
-    } unmap{mp, fsz};
-    const uint8_t *m = (const uint8_t *)mp;
+    if (mp == MAP_FAILED) throw std::runtime_error("cannot map " + path);
+    M.m = (const uint8_t *)mp;
+    M.fsz = fsz;
+    const uint8_t *m = M.m;
     // The mapped file's pages faulted in by all threads at once, one touch per page: the member walk below
     // (a dependent chain per thread) and the inflate then run on mapped pages
     static const bool pretouch = [] { const char *e = getenv("SPP_PRETOUCH"); return !e || atoi(e) != 0; }();
@@ -757,8 +776,7 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
     }
     const auto tmm = std::chrono::steady_clock::now();
     auto tms = tmm;
-    struct Blk { size_t off, clen, ulen; };
-    std::vector<Blk> blks;
+    std::vector<Blk> &blks = M.blks;
     // Members located in parallel: each thread finds the first member header in its byte range (a BGZF header
     // whose BSIZE chain reaches the next header), walks the chain to the next thread's start, and the chains
     // must meet exactly; otherwise (a false header inside compressed data, a damaged file) the serial walk
@@ -832,9 +850,55 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
         q += bsize;
     }
     const size_t nb = blks.size();
-    std::vector<size_t> uoff(nb + 1, 0);
-    for (size_t i = 0; i < nb; i++) uoff[i + 1] = uoff[i] + blks[i].ulen;
-    const size_t total = uoff[nb];
+    M.uoff.assign(nb + 1, 0);
+    for (size_t i = 0; i < nb; i++) M.uoff[i + 1] = M.uoff[i] + blks[i].ulen;
+    M.total = M.uoff[nb];
+    M.tmm = tmm;
+    M.tms = tms;
+}
+
+// Offset of the first record in the inflated stream (the header's end) and the header's reference count: the first
+// members inflated on this thread until the header is complete
+uint64_t header_end(const BamMap &M, int32_t *n_ref) {
+    std::vector<uint8_t> h;
+    Inflater inf;
+    size_t k = 0;
+    auto need = [&](size_t n) -> bool {
+        while (h.size() < n) {
+            if (k >= M.blks.size()) return false;
+            const Blk &b = M.blks[k++];
+            const size_t at = h.size();
+            h.resize(at + b.ulen);
+            if (b.ulen && !inf.run(M.m + b.off, b.clen, h.data() + at, b.ulen)) throw std::runtime_error("BGZF inflate failed");
+        }
+        return true;
+    };
+    if (!need(12) || memcmp(h.data(), "BAM\1", 4) != 0) throw std::runtime_error("not a BAM file");
+    size_t cur = 8 + (size_t)(uint32_t)rd32(h.data() + 4);
+    if (!need(cur + 4)) throw std::runtime_error("truncated BAM header");
+    const int32_t nr = rd32(h.data() + cur);
+    cur += 4;
+    for (int32_t i = 0; i < nr; i++) {
+        if (!need(cur + 4)) throw std::runtime_error("truncated BAM header");
+        const size_t l_name = (size_t)(uint32_t)rd32(h.data() + cur);
+        if (!need(cur + 8 + l_name)) throw std::runtime_error("truncated BAM header");
+        cur += 8 + l_name;
+    }
+    *n_ref = nr;
+    return cur;
+}
+
+size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &R, HostBuf &out) {
+    const int nt = std::max(1, std::min(p.n_threads, 64));
+    const auto tm0 = std::chrono::steady_clock::now();
+    BamMap M;
+    map_bam(f->path, nt, M);
+    const uint8_t *m = M.m;
+    const size_t fsz = M.fsz;
+    const std::vector<Blk> &blks = M.blks;
+    const std::vector<size_t> &uoff = M.uoff;
+    const size_t nb = blks.size(), total = M.total;
+    const auto tmm = M.tmm, tms = M.tms;
     const auto tm1 = std::chrono::steady_clock::now();
     out = buf_get(total + 64);
     const auto tm2 = std::chrono::steady_clock::now();
@@ -853,10 +917,9 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
     // if the call fails — are inflated here below.  The host's threads are then free for the record scan.
     // Only BAMs of many members: a member is a dependent chain of ~17k symbols on the GPU (~19 ms however few there
     // are), the host's threads inflate ~80 members per ms (r04zf); SPP_GPU_INFLATE_MIN overrides the 4096 floor.
-    const char *gme = getenv("SPP_GPU_INFLATE_MIN");
-    const size_t gpu_min = gme ? (size_t)atoll(gme) : (size_t)4096;
+    const size_t gpu_min = p.inflate_min_members > 0 ? (size_t)p.inflate_min_members : (size_t)4096;
     bool gpu_inflated = false;
-    if (const spp_inflate_fn gfn = g_inflate.load(); gfn && nb > 0 && nb >= gpu_min) {
+    if (const spp_inflate_fn gfn = g_inflate.load(); gfn && p.inflate_device >= 0 && nb > 0 && nb >= gpu_min) {
         struct GM { uint64_t coff; uint32_t clen, ulen; uint64_t uoff; };
         std::vector<GM> gm(nb);
         for (size_t i = 0; i < nb; i++) gm[i] = {blks[i].off, (uint32_t)blks[i].clen, (uint32_t)blks[i].ulen, uoff[i]};
@@ -868,7 +931,7 @@ size_t read_bam_raw(const spp_file *f, int32_t tid, const spp_params &p, Reads &
         const auto g2 = std::chrono::steady_clock::now();
         std::vector<uint32_t> gst(nb, 1);
         float kms = 0.f;
-        const bool ok_call = gfn(g_inflate_dev.load(), cb.p, fsz, gm.data(), (int64_t)nb, buf, total, gst.data(), &kms) == 0;
+        const bool ok_call = gfn(p.inflate_device, cb.p, fsz, gm.data(), (int64_t)nb, buf, total, gst.data(), &kms) == 0;
         const auto g3 = std::chrono::steady_clock::now();
         buf_put(cb);
         size_t nbad = nb;
@@ -1233,6 +1296,8 @@ void tweak_overlap(Reads &R, size_t a, size_t b) {
 struct Tweaks {
     std::vector<int64_t> col;                                   // per read; INT64_MAX = none
     std::unordered_map<size_t, std::vector<uint8_t>> orig;      // first mate -> qualities before
+    bool defer = false;                                         // device plans: record the pairs, tweak nothing here
+    std::vector<std::pair<size_t, size_t>> pairs;               // (first mate, second mate) in push order
 };
 
 // The live buffer's reads keyed by end, for "free every read with end <= col" (the order among equal
@@ -1361,9 +1426,13 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
                         // region pileups decode the reads within a read span of the region: a pair with
                         // an undecoded mate shares no aligned base with the region's reads
                         if (R.bases[a] && R.bases[r]) {
-                            T.orig.emplace(a, std::vector<uint8_t>(R.qual(a), R.qual(a) + R.l_seq[a]));
                             T.col[a] = it_pos;
-                            tweak_overlap(R, a, r);
+                            if (T.defer) {
+                                T.pairs.emplace_back(a, r);     // (the device applies it: spg_bam_accumulate)
+                            } else {
+                                T.orig.emplace(a, std::vector<uint8_t>(R.qual(a), R.qual(a) + R.l_seq[a]));
+                                tweak_overlap(R, a, r);
+                            }
                         }
                         olap.erase(itr);
                     }
@@ -1392,13 +1461,18 @@ struct spp_plan {
     HostBuf data, idx;
     size_t data_len = 0;           // inflated bytes in `data`
     spg_records view{};
+    // device plan (spp_pileup_plan_fields): the reads live in HBM (spg_bam_open); `idx` holds the plan's arrays
+    bool device = false;
+    spg_bam_plan dview{};
     void clear() {
-        R.clear(); keep.clear(); T.col.clear(); T.orig.clear(); kept.clear();
+        R.clear(); keep.clear(); T.col.clear(); T.orig.clear(); T.pairs.clear(); T.defer = false; kept.clear();
         rlo = INT64_MIN; rhi = INT64_MAX;
         buf_put(data);
         buf_put(idx);
         raw = false;
+        device = false;
         view = spg_records{};
+        dview = spg_bam_plan{};
     }
 };
 
@@ -1638,6 +1712,52 @@ void plan_records(spp_plan &P, spp_batch *B, int threads) {
 }
 
 
+// The device plan's arrays (spg_bam_plan): kept reads (u32 read indices), CSR offsets, the overlapping mate pairs with
+// their tweak columns and the offsets of the first mates' saved qualities — one host buffer (pinned under the hook).
+void plan_device(spp_plan &P, spp_batch *B) {
+    const Reads &R = P.R;
+    const std::vector<size_t> &kept = P.kept;
+    const size_t n = kept.size(), np = P.T.pairs.size(), C = (size_t)B->n_cols;
+    auto al = [](size_t x) { return (x + 63) & ~(size_t)63; };
+    const size_t o_off = 0, o_kept = al(8 * (C + 1)), o_pa = al(o_kept + 4 * n), o_pb = al(o_pa + 4 * np),
+                 o_col = al(o_pb + 4 * np), o_oq = al(o_col + 8 * np), bytes = al(o_oq + 8 * np) + 64;
+    P.idx = buf_get(bytes);
+    uint8_t *m = P.idx.p;
+    uint64_t *off = (uint64_t *)(m + o_off), *oq = (uint64_t *)(m + o_oq);
+    uint32_t *kp = (uint32_t *)(m + o_kept), *pa = (uint32_t *)(m + o_pa), *pb = (uint32_t *)(m + o_pb);
+    int64_t *col = (int64_t *)(m + o_col);
+    memcpy(off, B->off.data(), 8 * (C + 1));
+    int64_t span = 0;
+    for (size_t i = 0; i < n; i++) {
+        kp[i] = (uint32_t)kept[i];
+        span = std::max(span, R.end[kept[i]] - R.pos[kept[i]]);
+    }
+    uint64_t o = 0;
+    for (size_t j = 0; j < np; j++) {
+        const size_t a = P.T.pairs[j].first, b = P.T.pairs[j].second;
+        pa[j] = (uint32_t)a;
+        pb[j] = (uint32_t)b;
+        col[j] = P.T.col[a];
+        oq[j] = o;
+        o += R.l_seq[a];
+    }
+    spg_bam_plan &v = P.dview;
+    v = spg_bam_plan{};
+    v.pos_begin = B->pos_begin;
+    v.n_cols = B->n_cols;
+    v.n_entries = B->n_entries;
+    v.offsets = off;
+    v.n_kept = (int64_t)n;
+    v.kept = kp;
+    v.n_pairs = (int64_t)np;
+    v.pair_a = pa;
+    v.pair_b = pb;
+    v.pair_col = col;
+    v.pair_orig = oq;
+    v.orig_bytes = o;
+    v.max_span = span;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Read simulator -> BGZF BAM
 // ---------------------------------------------------------------------------------------------
@@ -1724,6 +1844,8 @@ void spp_default_params(spp_params *p) {
     p->ignore_overlaps = 1;
     p->flag_filter = F_UNMAP | F_SECONDARY | F_QCFAIL | F_DUP;
     p->n_threads = 1;
+    p->inflate_device = -1;
+    p->inflate_min_members = 0;
 }
 
 int spp_open(const char *path, spp_file **out) {
@@ -1850,6 +1972,7 @@ int spp_batch_fill(spp_batch *b, uint8_t *base_code, uint8_t *qual) {
     if (!b) return fail("spp_batch_fill: null batch");
     if (!b->plan) return fail("spp_batch_fill: the batch is already filled");
     if (b->plan->raw) return fail("spp_batch_fill: a records plan is filled on the GPU (spg_accumulate_records)");
+    if (b->plan->device) return fail("spp_batch_fill: a device plan is filled on the GPU (spg_bam_accumulate)");
     if ((base_code == nullptr) != (qual == nullptr)) return fail("spp_batch_fill: give both buffers or neither");
     try {
         static const bool timing = getenv("SPP_TIMING") != nullptr;
@@ -1895,8 +2018,129 @@ int spp_batch_records(spp_batch *b, spg_records *out) {
     return 0;
 }
 
+struct spp_bam_map {
+    HostBuf comp;                                  // the file's bytes (pinned under the allocator hook)
+    std::vector<spg_bgzf_member> mem;
+};
+
+int spp_bam_map_open(spp_file *f, int n_threads, spp_bam_map **out, spp_bam_map_info *info) {
+    if (!f || !out || !info) return fail("spp_bam_map_open: null argument");
+    if (!f->bam) return fail("spp_bam_map_open: not a BAM (BGZF) file");
+    *out = nullptr;
+    spp_bam_map *h = nullptr;
+    try {
+        const int nt = std::max(1, std::min(n_threads, 64));
+        BamMap M;
+        map_bam(f->path, nt, M);
+        int32_t n_ref = 0;
+        const uint64_t body = header_end(M, &n_ref);
+        h = new spp_bam_map();
+        h->comp = buf_get(M.fsz + 64);
+        par_chunks(M.fsz, nt, [&](int, size_t a, size_t b) { memcpy(h->comp.p + a, M.m + a, b - a); });
+        memset(h->comp.p + M.fsz, 0, 64);
+        h->mem.resize(M.blks.size());
+        for (size_t i = 0; i < M.blks.size(); i++)
+            h->mem[i] = spg_bgzf_member{M.blks[i].off, (uint32_t)M.blks[i].clen, (uint32_t)M.blks[i].ulen, M.uoff[i]};
+        *info = spp_bam_map_info{};
+        info->comp = h->comp.p;
+        info->comp_bytes = M.fsz;
+        info->members = h->mem.data();
+        info->n_members = (int64_t)h->mem.size();
+        info->inflated_bytes = M.total;
+        info->body = body;
+        info->n_ref = n_ref;
+        *out = h;
+        return 0;
+    } catch (const std::exception &e) {
+        if (h) { buf_put(h->comp); delete h; }
+        return fail(std::string("spp_bam_map_open: ") + e.what());
+    }
+}
+
+int spp_bam_map_close(spp_bam_map *h) {
+    if (!h) return 0;
+    buf_put(h->comp);
+    delete h;
+    return 0;
+}
+
+int spp_pileup_plan_fields(spp_file *f, int32_t tid, const spp_read_fields *F, const spp_params *p, spp_batch **out) {
+    if (!f || !F || !p || !out) return fail("spp_pileup_plan_fields: null argument");
+    if (tid < 0 || (size_t)tid >= f->targets.size()) return fail("spp_pileup_plan_fields: tid out of range");
+    if (F->n < 0 || (F->n && (!F->pos || !F->end || !F->mtid || !F->mpos || !F->isize || !F->flag || !F->l_seq ||
+                              !F->name_hash)))
+        return fail("spp_pileup_plan_fields: null field array");
+    *out = nullptr;
+    spp_plan *P = nullptr;
+    try {
+        static const bool timing = getenv("SPP_TIMING") != nullptr;
+        auto now = [] { return std::chrono::steady_clock::now(); };
+        const auto t0 = now();
+        P = plan_get();
+        Reads &R = P->R;
+        const size_t n = (size_t)F->n;
+        static uint8_t present = 0;               // (bases stay in HBM: a non-null mark that the read is decoded)
+        R.pos.resize(n); R.end.resize(n); R.mpos.resize(n); R.isize.resize(n); R.mtid.resize(n); R.flag.resize(n);
+        R.l_seq.resize(n); R.nhash.resize(n); R.bases.resize(n);
+        const int nt = std::max(1, std::min(p->n_threads, 64));
+        std::vector<int64_t> spans((size_t)nt, 0);
+        par_chunks(n, nt, [&](int t, size_t i0, size_t i1) {
+            int64_t sp = 0;
+            for (size_t i = i0; i < i1; i++) {
+                R.pos[i] = F->pos[i];
+                R.end[i] = F->end[i];
+                R.mpos[i] = F->mpos[i];
+                R.isize[i] = F->isize[i];
+                R.mtid[i] = F->mtid[i];
+                R.flag[i] = F->flag[i];
+                R.l_seq[i] = F->l_seq[i];
+                R.nhash[i] = F->name_hash[i];
+                R.bases[i] = &present;
+                sp = std::max(sp, R.end[i] - R.pos[i]);
+            }
+            spans[(size_t)t] = sp;
+        });
+        for (int64_t v : spans) R.max_span = std::max(R.max_span, v);
+        R.hashed = true;
+        P->device = true;
+        P->T.defer = true;
+        const auto t1 = now();
+        P->keep = simulate(R, *p, tid, P->T);
+        const auto t2 = now();
+        auto *B = new spp_batch();
+        int64_t used = 0;
+        for (uint8_t k : P->keep) used += k;
+        B->n_used = used;
+        B->n_dropped = (int64_t)n - used;
+        B->threads = nt;
+        plan_csr(*P, B, B->threads);
+        const auto t3 = now();
+        plan_device(*P, B);
+        B->plan = P;
+        P = nullptr;
+        if (timing) {
+            auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+            fprintf(stderr, "[spp timing] plan_fields: fields %.1f ms, simulate %.1f ms, offsets %.1f ms, device plan %.1f ms "
+                    "(%zu reads, %zu pairs)\n", ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, now()), n,
+                    B->plan->T.pairs.size());
+        }
+        *out = B;
+        return 0;
+    } catch (const std::exception &e) {
+        release_plan(P);
+        return fail(std::string("spp_pileup_plan_fields: ") + e.what());
+    }
+}
+
+int spp_batch_device_plan(spp_batch *b, spg_bam_plan *out) {
+    if (!b || !out) return fail("spp_batch_device_plan: null argument");
+    if (!b->plan || !b->plan->device) return fail("spp_batch_device_plan: not a device plan (spp_pileup_plan_fields)");
+    *out = b->plan->dview;
+    return 0;
+}
+
 int spp_set_inflater(spp_inflate_fn fn, int device) {
-    g_inflate_dev = device;
+    (void)device;
     g_inflate = fn;
     return 0;
 }

@@ -193,6 +193,60 @@ class PileupEngine:
         with self._lock:
             N.check(self._L.spg_accumulate_records(self._h, C.byref(r), 0), "spg_accumulate_records")
 
+    # -- a BAM kept in HBM (spg_bam_*) ------------------------------------------------------
+    def bam_open(self, bmap, tid: int, params) -> Optional[int]:
+        """spg_bam_open: the BAM's compressed bytes (pileup.BamMap) to HBM, inflated and scanned there; returns the
+        number of reads of contig ``tid`` the stepper keeps, or None when the BAM is not handled on the device (a
+        member the GPU could not inflate, record chains that disagree: plan it on the host instead)."""
+        i = bmap.info
+        flt = N.SpgBamFilter(N.SPP_STEPPER[params.stepper], int(params.flag_filter), int(params.min_mapping_quality), 0)
+        n = C.c_int64()
+        with self._lock:
+            rc = self._L.spg_bam_open(self._h, i.comp, i.comp_bytes, i.members, i.n_members, i.body, int(tid), i.n_ref,
+                                      C.byref(flt), C.byref(n))
+            if rc == 1:
+                self.bam_fallback = self._L.spg_last_error().decode(errors="replace")
+                return None
+            N.check(rc, "spg_bam_open")
+        return n.value
+
+    def bam_reads(self, n: int) -> Dict[str, np.ndarray]:
+        """spg_bam_reads_copy: the open BAM's kept reads' fixed fields (pinned host arrays, reused across BAMs)."""
+        bufs = getattr(self, "_bam_bufs", None)
+        if bufs is None or len(bufs["pos"]) < n:
+            cap = max(1024, int(n * 1.125))
+            bufs = {name: pinned_empty(cap, dt) for name, dt in N.BAM_READ_FIELDS}
+            self._bam_bufs = bufs
+        out = {name: a[:n] for name, a in bufs.items()}
+        r = N.SpgBamReads(*[out[name].ctypes.data for name, _ in N.BAM_READ_FIELDS])
+        with self._lock:
+            N.check(self._L.spg_bam_reads_copy(self._h, C.byref(r)), "spg_bam_reads_copy")
+        return out
+
+    def bam_accumulate(self, batch) -> bool:
+        """spg_bam_accumulate: a device plan (pileup.AlignmentFile.pileup_fields) — mate-overlap tweak, then the CSR
+        entries written from the BAM in HBM (k_pileup_fill) and accumulated.  False when the plan was refused (two
+        paired reads whose names differ behind equal hashes: plan the BAM on the host).  Keep ``batch`` open until
+        wait_ticket(input_ticket()) taken after this call."""
+        v = batch.device_plan()
+        with self._lock:
+            rc = self._L.spg_bam_accumulate(self._h, C.byref(v), 0)
+            if rc == 1:
+                self.bam_fallback = self._L.spg_last_error().decode(errors="replace")
+                return False
+            N.check(rc, "spg_bam_accumulate")
+        return True
+
+    def bam_inflate_ms(self) -> float:
+        ms = C.c_float()
+        N.check(self._L.spg_bam_inflate_ms(self._h, C.byref(ms)), "spg_bam_inflate_ms")
+        return ms.value
+
+    def bam_release(self):
+        """Free the BAM buffers in HBM (spg_bam_release)."""
+        with self._lock:
+            N.check(self._L.spg_bam_release(self._h), "spg_bam_release")
+
     def wait_input(self):
         """Block until every input copy enqueued so far has landed (pinned host buffers are free)."""
         with self._lock:

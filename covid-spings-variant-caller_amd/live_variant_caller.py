@@ -145,11 +145,26 @@ class LiveVariantCaller:
     def __init__(self, referenceFasta: str, minBaseQuality: int, minMappingQuality: int, minTotalDepth: int,
                  minAlleleDepth: int, minEvidenceRatio: float, maxVariants: int, device: Optional[int] = None,
                  max_depth: int = 8000, stepper: str = "all", ignore_overlaps: bool = True,
-                 n_threads: Optional[int] = None, devices: Optional[List[int]] = None):
+                 n_threads: Optional[int] = None, devices: Optional[List[int]] = None, pileup: str = "device",
+                 gpu_inflate: bool = True):
         """The reference's 7 arguments (:22-32), then the engine's: ``device`` (default LOCAL_RANK or 0), or
         ``devices`` — several GPUs of this host, each owning a coordinate range of the contig (multi.MultiEngine,
         spg_multi_*: BAM records and host batches sliced at equal-entry cuts, one RCCL gather of the call tables);
-        pileup()'s ``max_depth`` / stepper / ``ignore_overlaps``; host threads of the BAM plan."""
+        pileup()'s ``max_depth`` / stepper / ``ignore_overlaps``; host threads of the BAM plan.
+
+        ``pileup`` — where a BAM's pileup is built (SAM input always takes "host"):
+          "device"  (default) a lone process_bam keeps the BAM in HBM: the compressed file goes up, the GPU inflates
+                    and scans it, only the reads' fixed fields come down for the host's depth-cap / mate-pairing
+                    replay, and the entries are written on the GPU (spg_bam_*); process_bams and multi-device callers
+                    use the records plan below.  A BAM the device path cannot take (a member it cannot inflate,
+                    record chains that disagree, a name-hash collision) falls back to the records plan.
+          "records" the host inflates and scans the BAM and takes the read decisions; the inflated records go to HBM
+                    and the GPU decodes bases / qualities and walks the CIGARs (spg_accumulate_records);
+          "host"    the host also writes every entry (spp_batch_fill) into pinned staging.
+        ``gpu_inflate`` — records plans inflate BAMs of >= 4,096 BGZF members on this caller's (first) GPU
+        (spg_bgzf_inflate) instead of on the host's threads."""
+        if pileup not in ("device", "records", "host"):
+            raise ValueError(f"pileup must be 'device', 'records' or 'host', not {pileup!r}")
         self.minBaseQuality = minBaseQuality
         self.minMappingQuality = minMappingQuality
         self.minTotalDepth = minTotalDepth
@@ -157,11 +172,12 @@ class LiveVariantCaller:
         self.minEvidenceRatio = minEvidenceRatio
         self.maxVariants = maxVariants
         self.fastaFile = FastaFile(referenceFasta)
-        self.pileup_params = PileupParams(stepper=stepper, min_mapping_quality=minMappingQuality, max_depth=max_depth,
-                                          ignore_overlaps=ignore_overlaps,
-                                          n_threads=n_threads or min(16, cpu_share()))
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", "0"))
+        inflate_dev = (int(devices[0]) if devices else int(device)) if gpu_inflate else -1
+        self.pileup_params = PileupParams(stepper=stepper, min_mapping_quality=minMappingQuality, max_depth=max_depth,
+                                          ignore_overlaps=ignore_overlaps,
+                                          n_threads=n_threads or min(16, cpu_share()), inflate_device=inflate_dev)
         n_pos = max(self.fastaFile.lengths) if self.fastaFile.lengths else 1
         # calls-only engine: prepare_variants() is the class's only statistical output
         if devices is not None and len(devices) > 0:
@@ -174,21 +190,13 @@ class LiveVariantCaller:
         self._lock = threading.RLock()
         self._ingest = PinnedIngest(self.engine)
         self._batch_contig: List[int] = []       # FASTA reference index of each accumulated batch
-        # device-side pileup: a BAM's records go to HBM and the GPU decodes bases / qualities and
-        # walks the CIGARs (spg_accumulate_records); the host keeps the read filter, depth cap and overlap
-        # tweak.  SPG_DEVICE_PILEUP=0 selects the host fill (SAM input always uses it).
-        self.device_pileup = os.environ.get("SPG_DEVICE_PILEUP", "1") != "0"
-        self._gpu_inflate, self.last_gpu_inflate = False, False
+        self.pileup = pileup
+        self.device_pileup = pileup != "host"
+        self._device_bam = pileup == "device" and devices is None
+        self.last_bam_path = None                # which path the last BAM took: "device", "records" or "host"
+        self.last_gpu_inflate = False
         if self.device_pileup:
             N.use_pinned_records()
-            # BGZF members inflated on the GPU (spg_bgzf_inflate; BAMs of >= 4096 members, SPP_GPU_INFLATE_MIN): the
-            # host's threads then only scan the records (in parallel) and take the read decisions.  Faster for a lone
-            # process_bam (3.8e5 vs 3.5e5 positions/s per 10,000x BAM) and for process_bams (two plans at once: one's
-            # inflate on the GPU overlaps the other's scan, 5.3-5.9e5 vs 4.0e5), profiles/r04zp, r04zn, r04zf.
-            # SPG_GPU_INFLATE=0 keeps the host inflate.  (The hook is process-wide: the last caller constructed decides.)
-            self._gpu_inflate = os.environ.get("SPG_GPU_INFLATE", "") != "0"
-            self._inflate_dev = device if device is not None else 0
-            N.use_gpu_inflate(self._inflate_dev, on=self._gpu_inflate)
         self._inflight = collections.deque()     # (input ticket, records plan) whose copy may still be running
         self.last_checkpoint_bytes = 0           # shard bytes the last create_checkpoint wrote
         self.reset_memory()
@@ -248,13 +256,50 @@ class LiveVariantCaller:
         with AlignmentFile(inputBam) as bam:
             if contig not in bam.references:
                 raise ValueError(f"invalid contig `{contig}`")
-            if self.device_pileup and _is_bgzf(inputBam):
+            bgzf = _is_bgzf(inputBam)
+            if self._device_bam and bgzf and self._process_bam_device(bam, contig, referenceIndex):
+                self.last_bam_path = "device"
+                return
+            if self.device_pileup and bgzf:
                 batch = bam.pileup_records(contig, self.pileup_params)
+                self.last_bam_path = "records"
             else:
                 batch = bam.pileup_plan(contig, self.pileup_params)
+                self.last_bam_path = "host"
         # the entries go straight into pinned staging (double-buffered): the copy to HBM runs on the engine's
         # copy stream while the next BAM is read
         self._accumulate_plan(batch, referenceIndex)
+
+    def _process_bam_device(self, bam: AlignmentFile, contig: str, referenceIndex: int) -> bool:
+        """The BAM kept in HBM (spg_bam_*): compressed bytes up, inflate + record scan + stepper filter on the GPU, the
+        kept reads' fixed fields down, htslib's depth cap / mate pairing replayed on them on the host
+        (spp_pileup_plan_fields), the plan up, mate-overlap tweak + entries + accumulate on the GPU.  False when the
+        device declined the BAM (nothing accumulated: the caller plans it on the host)."""
+        bmap = bam.bam_map(self.pileup_params.n_threads)
+        try:
+            with self._lock:
+                n = self.engine.bam_open(bmap, bam.tid(contig), self.pileup_params)
+        finally:
+            bmap.close()                         # (spg_bam_open has copied it)
+        if n is None:
+            log.info("device BAM path declined %s: %s", contig, self.engine.bam_fallback)
+            return False
+        with self._lock:
+            reads = self.engine.bam_reads(n)
+            batch = bam.pileup_fields(contig, reads, self.pileup_params)
+            if batch.n_cols == 0:
+                batch.close()
+                return True
+            self._use_reference(referenceIndex)
+            if not self.engine.bam_accumulate(batch):
+                batch.close()
+                log.info("device BAM plan declined: %s", self.engine.bam_fallback)
+                return False
+            # the plan's pinned arrays are copied on the engine's copy stream: keep them until that copy lands
+            self._inflight.append((self.engine.input_ticket(), batch))
+            self._drain(keep=2)
+            self._batch_contig.append(referenceIndex)
+        return True
 
     def process_bams(self, inputBams, referenceIndex=0, workers: Optional[int] = None):
         """vc_queue.py:142-144's loop of process_bam (:54-72) over many BAMs, as one call: the BAMs'
@@ -283,7 +328,8 @@ class LiveVariantCaller:
                 return bam.pileup_plan(contig, params)
 
         window = workers + 1                  # plans in flight (each holds its BAM's inflated records, ~0.5 GB at 10,000x)
-        self.last_gpu_inflate = self.device_pileup and self._gpu_inflate
+        self.last_gpu_inflate = self.device_pileup and self.pileup_params.inflate_device >= 0
+        self.last_bam_path = "records" if self.device_pileup else "host"
         with ThreadPoolExecutor(workers) as ex:
             pending = [ex.submit(plan, p) for p in paths[:window]]
             for i in range(len(paths)):

@@ -41,6 +41,8 @@ class PileupParams:
     ignore_overlaps: bool = True
     flag_filter: int = 0x704
     n_threads: int = 8
+    inflate_device: int = -1          # records plans: BGZF members inflated on this GPU (-1: on the host's threads) ...
+    inflate_min_members: int = 0      # ... for BAMs of at least this many members (0: 4096)
 
     def native(self) -> N.SppParams:
         p = N.SppParams()
@@ -51,6 +53,10 @@ class PileupParams:
         p.ignore_overlaps = 1 if self.ignore_overlaps else 0
         p.flag_filter = int(self.flag_filter)
         p.n_threads = int(self.n_threads)
+        p.inflate_device = int(self.inflate_device)
+        p.inflate_min_members = int(self.inflate_min_members)
+        if p.inflate_device >= 0:
+            N.register_gpu_inflater()
         return p
 
 
@@ -58,9 +64,10 @@ class PileupBatch:
     """CSR batch owned by the native library: ``offsets`` u64[n_cols+1], ``codes``/``quals`` u8[E]
     (16 padding bytes follow both arrays), columns [pos_begin, pos_begin + n_cols)."""
 
-    def __init__(self, handle, planned=False, records=False):
+    def __init__(self, handle, planned=False, records=False, device=False):
         L = N.pileup_lib()
         self.is_records = bool(records)
+        self.is_device = bool(device)
         self._h = C.c_void_p(handle)
         pb, nc, ne, nu, nd = C.c_int64(), C.c_int64(), C.c_uint64(), C.c_int64(), C.c_int64()
         N.pcheck(L.spp_batch_info(self._h, C.byref(pb), C.byref(nc), C.byref(ne), C.byref(nu), C.byref(nd)),
@@ -94,6 +101,14 @@ class PileupBatch:
         r = N.SpgRecords()
         N.pcheck(N.pileup_lib().spp_batch_records(self._h, C.byref(r)), "spp_batch_records")
         return r
+
+    def device_plan(self) -> N.SpgBamPlan:
+        """A device plan's spg_bam_plan view (AlignmentFile.pileup_fields; valid until close())."""
+        if not self.is_device:
+            raise ValueError("device_plan(): not a device plan (AlignmentFile.pileup_fields)")
+        v = N.SpgBamPlan()
+        N.pcheck(N.pileup_lib().spp_batch_device_plan(self._h, C.byref(v)), "spp_batch_device_plan")
+        return v
 
     def _arrays(self):
         L = N.pileup_lib()
@@ -188,6 +203,31 @@ class AlignmentFile:
         N.pcheck(L.spp_pileup_plan_records(self._h, tid.value, lo, hi, C.byref(prm), C.byref(b)), "pileup")
         return PileupBatch(b.value, planned=True, records=True)
 
+    def tid(self, reference: str) -> int:
+        t = C.c_int32()
+        N.pcheck(N.pileup_lib().spp_target_id(self._h, reference.encode(), C.byref(t)), "pileup")
+        return t.value
+
+    def bam_map(self, n_threads: int = 8) -> "BamMap":
+        """The BAM's compressed bytes (pinned under the allocator hook) and BGZF member table for spg_bam_open."""
+        return BamMap(self, n_threads)
+
+    def pileup_fields(self, reference: str, reads: dict, params: PileupParams | None = None) -> PileupBatch:
+        """The device plan (spp_pileup_plan_fields): htslib's depth cap and mate pairing replayed on the reads' fixed
+        fields (PileupEngine.bam_reads), the CSR offsets and the overlapping mate pairs — for
+        PileupEngine.bam_accumulate, which writes the entries from the BAM in HBM."""
+        f = N.SppReadFields()
+        f.n = int(len(reads["pos"]))
+        for name, dt in N.BAM_READ_FIELDS:
+            a = reads[name]
+            assert a.dtype == dt and a.flags.c_contiguous and len(a) >= f.n
+            setattr(f, name, a.ctypes.data)
+        prm = (params or PileupParams()).native()
+        b = C.c_void_p()
+        N.pcheck(N.pileup_lib().spp_pileup_plan_fields(self._h, self.tid(reference), C.byref(f), C.byref(prm), C.byref(b)),
+                 "pileup")
+        return PileupBatch(b.value, planned=True, device=True)
+
     def close(self):
         if self._h:
             N.pileup_lib().spp_close(self._h)
@@ -198,6 +238,27 @@ class AlignmentFile:
 
     def __exit__(self, *a):
         self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class BamMap:
+    """spp_bam_map_open: a BAM's bytes in one host buffer + its BGZF members and header end (spg_bam_open's input)."""
+
+    def __init__(self, f: AlignmentFile, n_threads: int = 8):
+        self.info = N.SppBamMapInfo()
+        h = C.c_void_p()
+        N.pcheck(N.pileup_lib().spp_bam_map_open(f._h, int(n_threads), C.byref(h), C.byref(self.info)), "spp_bam_map_open")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            N.pileup_lib().spp_bam_map_close(self._h)
+            self._h = None
 
     def __del__(self):
         try:

@@ -143,7 +143,7 @@ int spg_accumulate_ex(spg_ctx *ctx, int64_t pos_begin, int64_t n_cols, const uin
  * through the binding (process_bam over a list of BAMs, vc_queue.py:142-144 repeated).  Shallow
  * batches (mean < 256 entries per column) are not launched one by one: the context folds a run of
  * them per position in one pass (each record read and written once per run), when the run reaches
- * SPG_RUN_MAX (env, default 4096) batches, before a deep batch, and at spg_finalize. */
+ * 4,096 batches, before a deep batch, and at spg_finalize. */
 typedef struct {
     int64_t pos_begin, n_cols;
     const uint64_t *offsets;       /* n_cols + 1 */
@@ -296,8 +296,9 @@ int spg_path_counters(spg_ctx *ctx, int64_t *out, int64_t n);
 
 /* BGZF members inflated on the GPU (the records plan's BAM read).  comp: the file's bytes (each
  * member's raw-DEFLATE payload at coff, clen bytes, followed by its 8-byte CRC32/ISIZE trailer); out: the inflated
- * stream (member m at uoff, exactly ulen <= 65536 bytes).  status[m] = 0 when member m inflated to ulen bytes
- * (else the caller inflates it on the host).  kernel_ms: the inflate kernel's time (may be null).  Synchronous. */
+ * stream (member m at uoff, exactly ulen <= 65536 bytes).  status[m] = 0 when member m inflated to ulen bytes whose
+ * CRC32 matches the trailer's (else the caller inflates it on the host).  kernel_ms: the inflate + CRC kernels' time
+ * (may be null; -1 when the timing failed).  Synchronous; the caller's current device is kept. */
 typedef struct spg_bgzf_member {
     uint64_t coff;
     uint32_t clen;
@@ -307,10 +308,62 @@ typedef struct spg_bgzf_member {
 int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const spg_bgzf_member *members, int64_t n,
                      uint8_t *out, size_t out_bytes, uint32_t *status, float *kernel_ms);
 const char *spg_bgzf_last_error(void);
+/* Free spg_bgzf_inflate's scratch on `device` (grow-only otherwise). */
+int spg_bgzf_release(int device);
 /* The same decoder compiled for the host (CPU tests of its logic only; comp needs 8 readable bytes past each
  * member's payload, as in a BGZF file). */
 int spg_bgzf_inflate_check(const uint8_t *comp, size_t comp_bytes, const spg_bgzf_member *members, int64_t n,
                            uint8_t *out, size_t out_bytes, uint32_t *status);
+
+/* ---- a BAM kept in HBM (the lone process_bam, live_variant_caller.py:54-72) ---------------------------
+ * Only the compressed file goes up and the reads' fixed fields come down: spg_bam_open copies the BGZF bytes to the
+ * context's device, inflates every member there (k_inflate + a CRC32 check per member), locates the records of contig
+ * `tid` in the inflated stream (parallel block_size chains from each member's first record, which must meet exactly)
+ * and applies the stepper's read filter; spg_bam_reads_copy hands the kept reads' fields to the host, which replays
+ * htslib's depth cap and mate pairing on them (spp_pileup_plan_fields, include/spings_pileup.h); spg_bam_accumulate
+ * takes that plan — the kept reads, the CSR offsets, the overlapping mate pairs — applies the mate-overlap quality
+ * tweak in HBM and writes the batch's entries with k_pileup_fill, then accumulates it like spg_accumulate_records
+ * (bit-identical batch).  One BAM per context at a time; its device buffers are reused by the next spg_bam_open
+ * (stream-ordered after this BAM's fill).  Return 1 (not < 0) means "not handled here, nothing accumulated": a member
+ * the GPU could not inflate (corrupt, CRC mismatch), record chains that disagree, or two paired reads whose names
+ * differ behind an equal name hash — the caller then plans the BAM on the host (spp_pileup_plan_records). */
+typedef struct {
+    int32_t stepper;               /* SPP_STEPPER_*: 0 all, 1 nofilter, 2 samtools */
+    uint32_t flag_filter;          /* samtools stepper */
+    int32_t min_mapping_quality;   /* samtools stepper */
+    int32_t reserved;
+} spg_bam_filter;
+/* comp: the whole file (each member's payload at members[m].coff with its 8-byte trailer after it); body: offset of the
+ * first record in the inflated stream (after the header); n_ref: the header's reference count.  *n_reads: the kept
+ * reads of contig tid. */
+int spg_bam_open(spg_ctx *ctx, const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *members, int64_t n_members,
+                 uint64_t body, int32_t tid, int32_t n_ref, const spg_bam_filter *filter, int64_t *n_reads);
+typedef struct {                   /* host arrays with room for n_reads values each, in BAM order */
+    int32_t *pos, *end, *mtid, *mpos, *isize;   /* end: pos + the CIGAR's reference length */
+    uint16_t *flag;
+    uint32_t *l_seq;
+    uint64_t *name_hash;           /* FNV-1a 64 of the read name */
+} spg_bam_reads;
+int spg_bam_reads_copy(spg_ctx *ctx, const spg_bam_reads *out);
+typedef struct spg_bam_plan {
+    int64_t pos_begin, n_cols;
+    uint64_t n_entries;
+    const uint64_t *offsets;       /* n_cols + 1 */
+    int64_t n_kept;
+    const uint32_t *kept;          /* reads (indices into spg_bam_open's reads) with entries, BAM order */
+    int64_t n_pairs;
+    const uint32_t *pair_a, *pair_b;   /* overlapping mates: a (pushed first) and b */
+    const int64_t *pair_col;       /* a's D / N entries in columns < pair_col read its qualities before the tweak */
+    const uint64_t *pair_orig;     /* offset of a's saved qualities (sum of the earlier pairs' a l_seq) */
+    uint64_t orig_bytes;
+    int64_t max_span;              /* max(end - pos) over the kept reads */
+    int64_t reserved[4];
+} spg_bam_plan;
+int spg_bam_accumulate(spg_ctx *ctx, const spg_bam_plan *plan, uint32_t flags);
+/* ms of the last spg_bam_open's inflate + CRC kernels (HIP events) */
+int spg_bam_inflate_ms(spg_ctx *ctx, float *ms);
+/* Free the BAM buffers (the next spg_bam_open allocates them again). */
+int spg_bam_release(spg_ctx *ctx);
 
 /* Introspection for tests. */
 int spg_device_count(int *n);

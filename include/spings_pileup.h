@@ -42,7 +42,10 @@ typedef struct {
     int32_t ignore_overlaps;       /* 1 = htslib overlap quality tweak (pysam default) */
     uint32_t flag_filter;          /* samtools stepper flag filter (pysam default 0x704) */
     int32_t n_threads;             /* BGZF inflate / CSR fill threads (<= 0: 1) */
-    int64_t reserved[2];
+    int32_t inflate_device;        /* records plans: inflate the BGZF members with the inflater spp_set_inflater
+                                      registered, on this GPU (-1, the default: on the host's threads) ... */
+    int32_t inflate_min_members;   /* ... when the BAM has at least this many members (<= 0: 4096) */
+    int64_t reserved[1];
 } spp_params;
 
 typedef struct spp_file spp_file;
@@ -98,13 +101,47 @@ int spp_batch_records(spp_batch *b, struct spg_records *out);
 typedef int (*spp_alloc_fn)(size_t bytes, void **out);
 typedef int (*spp_free_fn)(void *p);
 int spp_set_host_allocator(spp_alloc_fn alloc, spp_free_fn release);
-/* BGZF inflater for the records plans (e.g. spg_bgzf_inflate on `device`): called once per BAM with the mapped
- * file, its members ({u64 coff, u32 clen, u32 ulen, u64 uoff}, layout of spg_bgzf_member) and the record buffer;
- * members whose status is not 0 are inflated on the host.  NULL restores the host inflate.  Used for BAMs of at least
- * 4096 members (SPP_GPU_INFLATE_MIN): fewer inflate faster on the host's threads. */
+/* BGZF inflater for the records plans (e.g. spg_bgzf_inflate): called once per BAM with the plan's
+ * spp_params.inflate_device, the mapped file, its members ({u64 coff, u32 clen, u32 ulen, u64 uoff}, layout of
+ * spg_bgzf_member) and the record buffer; members whose status is not 0 are inflated on the host.  Each plan chooses
+ * through its spp_params (inflate_device >= 0, at least inflate_min_members members: fewer inflate faster on the
+ * host's threads), so callers with different choices do not override one another; NULL unregisters it.  `device` is
+ * kept for the ABI and ignored. */
 typedef int (*spp_inflate_fn)(int device, const uint8_t *comp, size_t comp_bytes, const void *members, int64_t n,
                               uint8_t *out, size_t out_bytes, uint32_t *status, float *kernel_ms);
 int spp_set_inflater(spp_inflate_fn fn, int device);
+
+/* A BAM kept in HBM (include/spings_gpu.h spg_bam_*).  spp_bam_map_open maps the file, locates its
+ * BGZF members (parallel header search, chains that must meet) and the header's end, and copies the file into one
+ * host buffer (pinned under the allocator hook) for spg_bam_open; the handle keeps it until spp_bam_map_close.
+ * spp_pileup_plan_fields replays htslib's depth cap and mate pairing (spp_pileup_plan's rules) on the reads' fixed
+ * fields as spg_bam_reads_copy returns them — names compared by their 64-bit hash (the device verifies every pair's
+ * names) — computes the CSR offsets, and returns the overlapping mate pairs instead of tweaking qualities on the host;
+ * spp_batch_device_plan exposes the plan as an spg_bam_plan for spg_bam_accumulate.  spp_batch_fill / records are not
+ * available on such a batch. */
+typedef struct {
+    const uint8_t *comp;           /* the file's bytes (64 zero bytes of padding past comp_bytes) */
+    uint64_t comp_bytes;
+    const void *members;           /* spg_bgzf_member[n_members] (include/spings_gpu.h), in file order */
+    int64_t n_members;
+    uint64_t inflated_bytes;       /* the inflated stream's length */
+    uint64_t body;                 /* offset of the first record in it (the header's end) */
+    int32_t n_ref;                 /* the header's reference count */
+    int32_t reserved;
+} spp_bam_map_info;
+typedef struct spp_bam_map spp_bam_map;
+int spp_bam_map_open(spp_file *f, int n_threads, spp_bam_map **out, spp_bam_map_info *info);
+int spp_bam_map_close(spp_bam_map *h);
+typedef struct {                   /* one contig's reads after the stepper filter, in BAM order (spg_bam_reads) */
+    int64_t n;
+    const int32_t *pos, *end, *mtid, *mpos, *isize;
+    const uint16_t *flag;
+    const uint32_t *l_seq;
+    const uint64_t *name_hash;
+} spp_read_fields;
+int spp_pileup_plan_fields(spp_file *f, int32_t tid, const spp_read_fields *reads, const spp_params *p, spp_batch **out);
+struct spg_bam_plan;
+int spp_batch_device_plan(spp_batch *b, struct spg_bam_plan *out);
 
 /* Synthetic read simulator (SURVEY.md §8 d "Synthetic inputs"): writes a coordinate-sorted BGZF
  * BAM of single-end reads (flag 0, MAPQ 60) over one contig — starts uniform on [0, L-read_len],

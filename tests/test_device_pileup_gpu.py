@@ -6,6 +6,7 @@ CIGAR op / '*' SEQ+QUAL / stacks / overlapping pairs under each stepper and dept
 restatement-generated fixture — and, on every fixture, against spp_batch_fill's host CSR (regions, long
 skips, the simulator's BAMs up to 10,000x).  Then process_bam through it vs the host fill.  (Parity with
 pysam itself stays unpinned: pysam/htslib is absent here and on the GPU box.)"""
+import ctypes as C
 import os
 
 import numpy as np
@@ -52,6 +53,35 @@ def device_fill(path, contig, start=None, stop=None, pinned=False, **kw):
         eng.close()
 
 
+def bam_device_fill(path, contig, **kw):
+    """The BAM kept in HBM (spg_bam_open -> spg_bam_reads_copy -> spp_pileup_plan_fields -> spg_bam_accumulate):
+    the batch the engine then holds, or None for a contig without entries."""
+    params = PileupParams(n_threads=kw.pop("n_threads", 4), **kw)
+    with AlignmentFile(path) as f:
+        L = f.get_reference_length(contig)
+        eng = PileupEngine(L + 1, reference="A" * (L + 1))
+        try:
+            bmap = f.bam_map(4)
+            n = eng.bam_open(bmap, f.tid(contig), params)
+            bmap.close()
+            assert n is not None, eng.bam_fallback
+            b = f.pileup_fields(contig, eng.bam_reads(n), params)
+            try:
+                if b.n_cols == 0:
+                    return None
+                assert eng.bam_accumulate(b), eng.bam_fallback
+                eng.sync()
+                hist = eng.history()
+                assert len(hist) == 1
+                eng.finalize()
+                eng.counts()                  # settles: raises if the fill flagged an inconsistent plan
+                return hist[0]
+            finally:
+                b.close()
+        finally:
+            eng.close()
+
+
 def assert_same(a, b):
     assert a[0] == b[0]
     np.testing.assert_array_equal(a[1], b[1])
@@ -80,6 +110,7 @@ def test_testfile_config1(tmp_path):
     got = device_fill(bam, "NC_045512.2")
     assert got[0] == 10 and len(got[1]) == 422 and int(got[1][-1]) == 1642
     assert_same(got, host_fill(bam, "NC_045512.2"))
+    assert_same(bam_device_fill(bam, "NC_045512.2"), got)
     z = np.load(os.path.join(GOLD, "testfile_pileup.npz"))
     np.testing.assert_array_equal(got[2], z["codes"])
     np.testing.assert_array_equal(got[3], z["quals"])
@@ -145,6 +176,7 @@ def test_hand_derived_fixtures(tmp_path, case):
     samgen.write_bam(bam, [("c", 60)], recs)
     got = device_fill(bam, "c", **kw)
     H.expect(got, pb, cols)
+    H.expect(bam_device_fill(bam, "c", **kw), pb, cols)
     if all(ord(ch) - 33 <= 93 for r in recs for ch in r["qual"]):
         assert_same(got, _port(recs, "c", [("c", 60)], tmp_path, **kw))
     assert_same(got, host_fill(bam, "c", **kw))
@@ -168,6 +200,7 @@ def test_random_reads(tmp_path, seed, kw):
             continue
         assert_same(got, port)
         assert_same(got, host_fill(bam, c, **kw))
+        assert_same(bam_device_fill(bam, c, **kw), port)
 
 
 @pytest.mark.parametrize("region", [(100, 300), (0, 50), (550, 700), (250, 251)])
@@ -190,6 +223,7 @@ def test_long_spans_and_gaps(tmp_path):
     bam = str(tmp_path / "g.bam")
     samgen.write_bam(bam, [("c", 20000)], recs)
     assert_same(device_fill(bam, "c", max_depth=0), host_fill(bam, "c", max_depth=0))
+    assert_same(bam_device_fill(bam, "c", max_depth=0), host_fill(bam, "c", max_depth=0))
 
 
 @pytest.mark.parametrize("depth,max_depth", [(200, 8000), (10000, 8000), (10000, 0)])
@@ -199,13 +233,38 @@ def test_simulated_bams(tmp_path, depth, max_depth):
     from covid_spings_variant_caller_amd.pileup import simulate_bam
     bam = str(tmp_path / "s.bam")
     simulate_bam(bam, "NC_045512.2", synth.reference(3000, seed=1), depth=depth, seed=5, n_threads=8)
-    assert_same(device_fill(bam, "NC_045512.2", pinned=True, max_depth=max_depth),
-                host_fill(bam, "NC_045512.2", max_depth=max_depth))
+    host = host_fill(bam, "NC_045512.2", max_depth=max_depth)
+    assert_same(device_fill(bam, "NC_045512.2", pinned=True, max_depth=max_depth), host)
+    assert_same(bam_device_fill(bam, "NC_045512.2", max_depth=max_depth), host)
 
 
-def test_process_bam_device_pileup_matches_host(tmp_path, monkeypatch):
-    """LiveVariantCaller.process_bam (live_variant_caller.py:54-72) over 3 BAMs with the device pileup vs
-    the host fill (SPG_DEVICE_PILEUP=0): identical prepare_variants() and memory."""
+def test_bam_device_declines_corrupt_member(tmp_path):
+    """A member whose compressed bytes were damaged (its CRC32 no longer matches, or it fails to decode): spg_bam_open
+    declines the BAM (return 1, nothing accumulated) and process_bam takes the records plan, whose host inflate
+    reports the damage as the reference's pysam would (an exception), or recovers when the damage was harmless."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.pileup import simulate_bam
+    bam = str(tmp_path / "s.bam")
+    ref = synth.reference(3000, seed=1)
+    simulate_bam(bam, "NC_045512.2", ref, depth=300, seed=5, n_threads=4)
+    with AlignmentFile(bam) as f:
+        bmap = f.bam_map(4)
+        mem = np.ctypeslib.as_array(C.cast(bmap.info.members, C.POINTER(C.c_uint64)), (bmap.info.n_members * 3,))
+        k = bmap.info.n_members // 2
+        coff, clen = int(mem[3 * k]), int(mem[3 * k + 1] & 0xFFFFFFFF)
+        comp = np.ctypeslib.as_array(C.cast(bmap.info.comp, C.POINTER(C.c_uint8)), (bmap.info.comp_bytes,))
+        comp[coff + clen] ^= 0x5A                    # the member's stored CRC32: the data decodes, the check fails
+        eng = PileupEngine(3001, reference=ref + "A")
+        assert eng.bam_open(bmap, f.tid("NC_045512.2"), PileupParams()) is None
+        assert "did not inflate" in eng.bam_fallback and "status 10" in eng.bam_fallback
+        bmap.close()
+        eng.close()
+
+
+def test_process_bam_device_pileup_matches_host(tmp_path):
+    """LiveVariantCaller.process_bam (live_variant_caller.py:54-72) over 3 BAMs with the BAM kept in HBM
+    (pileup="device", spg_bam_*), the records plan (pileup="records", with and without the GPU inflater) and the host
+    fill (pileup="host"): identical prepare_variants() and memory."""
     from covid_spings_variant_caller_amd import synth
     from covid_spings_variant_caller_amd.live_variant_caller import LiveVariantCaller
     from covid_spings_variant_caller_amd.pileup import simulate_bam
@@ -218,13 +277,15 @@ def test_process_bam_device_pileup_matches_host(tmp_path, monkeypatch):
         simulate_bam(p, "NC_045512.2", ref, depth=300, seed=10 + k, n_threads=4, snv_every=97)
         bams.append(p)
     out = []
-    for dev in ("1", "0"):
-        monkeypatch.setenv("SPG_DEVICE_PILEUP", dev)
-        vc = LiveVariantCaller(fa, 20, 0, 10, 5, 0.1, 0)
-        assert vc.device_pileup == (dev == "1")
+    for mode, gi in (("device", True), ("records", True), ("records", False), ("host", True)):
+        vc = LiveVariantCaller(fa, 20, 0, 10, 5, 0.1, 0, pileup=mode, gpu_inflate=gi)
+        assert vc.device_pileup == (mode != "host")
         for p in bams:
             vc.process_bam(p)
+            assert vc.last_bam_path == mode
         out.append((vc.prepare_variants(), {k: (v["reference"], v["totalDepth"]) for k, v in vc.memory.items()}))
         del vc
-    assert out[0][0] == out[1][0] and len(out[0][0]) > 0
-    assert out[0][1] == out[1][1]
+    assert len(out[0][0]) > 0
+    for o in out[1:]:
+        assert o[0] == out[0][0]
+        assert o[1] == out[0][1]
