@@ -39,6 +39,7 @@ hipError_t launch_tile(const MParams &P, const Hist *H, const uint8_t *ref, int6
 hipError_t launch_merge(const MParams &P, const uint8_t *ref, Acc *acc, hipStream_t st);
 int tile_blocks_per_cu(int lpc, bool one);
 hipError_t launch_pileup_fill(const FillArgs &A, hipStream_t st);
+size_t fill_scratch_bytes(int64_t n_cols, int64_t n_reads, int64_t max_span);
 hipError_t launch_pos_bounds(const Hist *H, const int32_t *items, int32_t n, int64_t pos, uint64_t *rng, hipStream_t st);
 hipError_t launch_pos_copy(const Hist *H, const int32_t *items, int32_t n, const uint64_t *rng, const uint64_t *dst,
                            uint8_t *oc, uint8_t *oq, hipStream_t st);
@@ -1051,7 +1052,8 @@ static int upload_records(spg_ctx *c, const spg_records *R, const HistBatch &hb,
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t o_data = 0, o_rec = al(R->data_bytes + 64), o_pos = al(o_rec + 8 * n), o_end = al(o_pos + 4 * n),
                  o_tw = al(o_end + 4 * n), o_tcol = al(o_tw + 4 * n), o_tq = al(o_tcol + 8 * nt),
-                 o_orig = al(o_tq + 8 * nt), o_tf = al(o_orig + R->orig_bytes), need = al(o_tf + 4 * (n_tiles + 1));
+                 o_orig = al(o_tq + 8 * nt), o_tf = al(o_orig + R->orig_bytes),
+                 need = al(o_tf + fill_scratch_bytes(R->n_cols, (int64_t)n, R->max_span));
     if (need > c->rs_cap) {
         if (c->rs) HIPCHK(hipFree(c->rs));      // (synchronous: the previous fill has run)
         c->rs = nullptr;
@@ -1084,7 +1086,8 @@ static int upload_records(spg_ctx *c, const spg_records *R, const HistBatch &hb,
     A.tw_q = reinterpret_cast<const uint64_t *>(m + o_tq);
     A.orig = m + o_orig;
     A.orig_bytes = R->orig_bytes;
-    A.tile_first = reinterpret_cast<uint32_t *>(m + o_tf);
+    A.scratch = m + o_tf;
+    A.scratch_bytes = need - o_tf;
     A.off = hb.off;
     A.code = hb.code;
     A.qual = hb.qual;
@@ -2288,7 +2291,8 @@ int spg_bam_accumulate(spg_ctx *c, const spg_bam_plan *P, uint32_t flags) {
     const size_t o_pos = al(8 * nk), o_end = o_pos + al(4 * nk), o_tw = o_end + al(4 * nk);
     HIPCHK(B.recs_k.need(o_tw + al(4 * nk) + 16));
     const int64_t n_tiles = (P->n_cols + 63) / 64;
-    HIPCHK(B.tile_first.need(4 * (size_t)(n_tiles + 1)));
+    const size_t fsb = fill_scratch_bytes(P->n_cols, P->n_kept, P->max_span);
+    HIPCHK(B.tile_first.need(fsb));
     if (nk) HIPCHK(hipMemcpyAsync(B.kept.p, P->kept, 4 * nk, hipMemcpyHostToDevice, cs));
     uint8_t *pb = B.pairs.as<uint8_t>();
     if (np) {
@@ -2345,7 +2349,8 @@ int spg_bam_accumulate(spg_ctx *c, const spg_bam_plan *P, uint32_t flags) {
     F.tw_q = reinterpret_cast<const uint64_t *>(pb + o_oq);
     F.orig = B.orig.as<uint8_t>();
     F.orig_bytes = P->orig_bytes;
-    F.tile_first = B.tile_first.as<uint32_t>();
+    F.scratch = B.tile_first.p;
+    F.scratch_bytes = fsb;
     F.pos_begin = P->pos_begin;
     F.n_cols = (int32_t)P->n_cols;
     F.n_tiles = (int32_t)n_tiles;

@@ -247,7 +247,9 @@ struct FillArgs {
     const uint64_t *tw_q;
     const uint8_t *orig;
     uint64_t orig_bytes;
-    uint32_t *tile_first;          // [n_tiles + 1]: first read starting at or after the tile (0 for tile 0)
+    void *scratch;                 // fill_scratch_bytes(): tile_first [n_tiles + 1] (first read starting at or after
+                                   // the tile), item offsets [n_tiles + 1], the scan's temporary, group starts
+    size_t scratch_bytes;
     const uint64_t *off;           // CSR offsets [n_cols + 1]
     uint8_t *code, *qual;
     int64_t pos_begin;

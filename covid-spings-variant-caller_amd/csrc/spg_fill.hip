@@ -1,25 +1,29 @@
 // spg_fill.hip — device-side pileup of BAM records into the CSR batch (include/spings_gpu.h
-// spg_accumulate_records).
+// spg_accumulate_records, spg_bam_accumulate).
 //
 // Replaces the host CIGAR walk behind LiveVariantCaller.process_bam (variant_caller/live_variant_caller.py:
 // 54-72, pysam's pileup columns :74-90): the host keeps what decides WHICH reads enter a column (stepper
-// filter, htslib's depth cap, mate-overlap tweak, CSR offsets — spp_pileup_plan_records) and this kernel
-// writes WHAT they contribute: per covered column the read's BAM nibble and quality, or 16 / 17 for a
-// CIGAR D / N with the quality of the next query base (0 past the read end), in htslib's per-column order
-// (the column's reads in BAM order).  Bit-identical to spp_batch_fill of the same plan (tests/
-// test_device_pileup_gpu.py).
+// filter, htslib's depth cap, mate-overlap tweak, CSR offsets) and these kernels write WHAT they contribute: per
+// covered column the read's BAM nibble and quality, or 16 / 17 for a CIGAR D / N with the quality of the next query
+// base (0 past the read end), in htslib's per-column order (the column's reads in BAM order).  Bit-identical to
+// spp_batch_fill of the same plan (tests/test_device_pileup_gpu.py).
 //
-// Layout: one wave per tile of 64 consecutive columns; lane j holds column c0 + j's write cursor (CSR
-// offset + entries written).  The tile's reads — those starting at most max_span before it, up to its end
-// (tile_first) — are taken 64 at a time in BAM order, one per lane; the wave steps the columns the chunk
-// covers, each lane walking its own CIGAR, and the covering lanes of a column write consecutive entries
-// at (cursor + rank among them): one coalesced byte store per array per column.  Consecutive tiles go to
-// one XCD (its L2 holds the records they share).  HBM-bound: the records are read once per tile they
-// overlap and each entry is written once.
+// Work items: a tile of 64 consecutive columns x a group of `fg` consecutive reads of the tile's read range (the
+// reads starting at most max_span before the tile, up to its end: tile_first), so a 10,000x batch spreads over ~30k
+// waves instead of one wave per tile.  A column's entries of a group are its covering reads of that group in BAM
+// order, starting at the count of covering reads of the tile's earlier groups (k_fill_starts: one wave per tile,
+// lanes = columns, a running count over the tile's reads, recorded at every group boundary).  k_fill: lanes =
+// columns; per read (wave-uniform, its header and first CIGAR ops staged in LDS for 64 reads at a time) every lane
+// finds the CIGAR op covering its column and loads its quality / packed base — consecutive lanes read consecutive
+// bytes of the read, one coalesced load per array — four reads' loads in flight before their entries are used.
+// Entries are staged per column in LDS and written out every 32 reads, one contiguous store per column (a column's
+// entries of a group are contiguous in the CSR).  HBM-bound: records read once per tile they overlap, 2 B written
+// per entry.
+#include <hipcub/hipcub.hpp>
+
 #include "spg_device.h"
 
 namespace spg {
-
 
 namespace {
 
@@ -35,23 +39,26 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t *base, uint64_t off) {
     return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(off & 3));
 }
 
-__device__ __forceinline__ int32_t wave_min_i32(int32_t v) {
-    for (int o = 32; o; o >>= 1) v = min(v, __shfl_xor(v, o));
-    return __builtin_amdgcn_readfirstlane(v);
-}
-__device__ __forceinline__ int32_t wave_max_i32(int32_t v) {
-    for (int o = 32; o; o >>= 1) v = max(v, __shfl_xor(v, o));
-    return __builtin_amdgcn_readfirstlane(v);
-}
-
 __device__ __forceinline__ bool eats_ref(uint32_t op) { return op == 0 || op == 2 || op == 3 || op == 7 || op == 8; }
 __device__ __forceinline__ bool eats_query(uint32_t op) { return op == 0 || op == 1 || op == 4 || op == 7 || op == 8; }
+
+constexpr int FILL_SB = 32;              // staged entries per column between write-outs (one per read: every 32 reads)
+constexpr int FILL_ST = FILL_SB + 4;     // LDS row stride (9 dwords: the lanes' rows spread over the banks)
+constexpr int FILL_OPS = 4;              // CIGAR ops staged per read (longer CIGARs read the rest from memory)
+
+struct FillLay {                         // fill_scratch_bytes' layout
+    uint32_t *tile_first, *item_off, *gstart;
+    void *scan_tmp;
+    size_t scan_bytes;
+    int64_t items_cap;
+};
+__host__ __device__ __forceinline__ size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 }  // namespace
 
 // tile_first[k] = first read with rpos >= pos_begin + 64k (k >= 1), tile_first[0] = 0: thread r writes the
 // boundaries between read r - 1's tile and its own (thread n_reads: those after the last read).
-__global__ void k_tile_first(FillArgs A) {
+__global__ void k_tile_first(FillArgs A, uint32_t *tile_first) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r > A.n_reads) return;
     auto tile_of = [&](uint64_t i) -> int64_t {
@@ -60,112 +67,212 @@ __global__ void k_tile_first(FillArgs A) {
         return d < 0 ? -1 : min(d >> 6, (int64_t)A.n_tiles);
     };
     const int64_t hi = tile_of(r), lo = r ? tile_of(r - 1) : -1;
-    if (r == 0) A.tile_first[0] = 0;
-    for (int64_t k = max(lo + 1, (int64_t)1); k <= hi; k++) A.tile_first[k] = (uint32_t)r;
+    if (r == 0) tile_first[0] = 0;
+    for (int64_t k = max(lo + 1, (int64_t)1); k <= hi; k++) tile_first[k] = (uint32_t)r;
 }
 
-__global__ __launch_bounds__(256) void k_pileup_fill(FillArgs A) {
+// groups per tile (items), for the scan into item offsets; ng[n_tiles] = 0
+__global__ void k_fill_ngroups(FillArgs A, const uint32_t *tile_first, uint32_t *ng, int32_t fg) {
+    const int32_t t = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (t > A.n_tiles) return;
+    if (t == A.n_tiles) { ng[t] = 0; return; }
+    const uint32_t r0 = tile_first[max(t - A.back, 0)], r1 = tile_first[t + 1];
+    ng[t] = r1 > r0 ? (r1 - r0 + (uint32_t)fg - 1) / (uint32_t)fg : 0u;
+}
+
+// one wave per tile, lane = column: covering reads counted in BAM order; at each group boundary the count so far is
+// that group's start (relative to the column's CSR offset); the total must be the column's entry count
+__global__ __launch_bounds__(256) void k_fill_starts(FillArgs A, const uint32_t *tile_first, const uint32_t *item_off,
+                                                     uint32_t *gstart, int32_t fg) {
     const int lane = threadIdx.x & 63;
-    // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs; consecutive tiles land on one
-    const uint32_t nb = gridDim.x, per = nb >> 3, b = blockIdx.x;
-    const uint32_t blk = (b & 7) * per + (b >> 3);
-    const int32_t tile = (int32_t)(blk * 4 + (threadIdx.x >> 6));
-    if (tile >= A.n_tiles) return;   // wave-uniform
-    const int32_t c0 = tile * 64, W = min(64, A.n_cols - c0);
-    uint64_t cur = 0, cend = 0;
-    if (lane < W) {
-        cur = A.off[c0 + lane];
-        cend = A.off[c0 + lane + 1];
-    }
-    const int32_t kb = max(tile - A.back, 0);
-    const uint32_t r0 = A.tile_first[kb], r1 = A.tile_first[tile + 1];
+    const int32_t t = (int32_t)(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (t >= A.n_tiles) return;
+    const int32_t c0 = t * 64, W = min(64, A.n_cols - c0);
     const int64_t P0 = A.pos_begin + c0;
-    uint32_t bad = 0;
+    const uint32_t r0 = tile_first[max(t - A.back, 0)], r1 = tile_first[t + 1];
+    uint32_t *gs = gstart + (size_t)item_off[t] * 64;
+    uint32_t cnt = 0;
     for (uint32_t rb = r0; rb < r1; rb += 64) {
-        const uint32_t r = rb + (uint32_t)lane;
-        int32_t s = 0, e = 0, x = 0;             // tile-relative: covered columns [s, e); CIGAR op start x
-        if (r < r1) {
-            x = (int32_t)((int64_t)A.rpos[r] - P0);
-            s = max(x, 0);
-            e = (int32_t)min((int64_t)A.rend[r] - P0, (int64_t)W);
+        int32_t s = INT32_MAX, e = INT32_MIN;
+        if (rb + lane < r1) {
+            s = (int32_t)max((int64_t)A.rpos[rb + lane] - P0, (int64_t)INT32_MIN + 1);
+            e = (int32_t)min((int64_t)A.rend[rb + lane] - P0, (int64_t)INT32_MAX);
         }
-        bool act = s < e;
-        if (__ballot(act) == 0) continue;
-        const int32_t smin = wave_min_i32(act ? s : INT32_MAX), emax = wave_max_i32(act ? e : 0);
-        uint64_t co = 0, so = 0, qo = 0, oq = 0;
-        uint32_t ncig = 0, ls = 0, y = 0, ci = 0, op = 0, len = 0;
-        int32_t tcol = INT32_MIN;                // D/N entries in columns < tcol read orig (none: no tweak)
-        if (act) {
-            const uint64_t ro = min(A.rec[r], A.data_bytes);    // (the host checked rec + 36 <= data_bytes)
-            const uint32_t l_name = ld32u(A.data, ro + 8) & 0xFF;
-            ncig = ld32u(A.data, ro + 12) & 0xFFFF;
-            ls = ld32u(A.data, ro + 16);
-            co = ro + 32 + l_name;
-            so = co + 4ull * ncig;
-            qo = so + (ls + 1) / 2;
-            if (ncig == 0 || ls > (1u << 30) || qo + ls > A.data_bytes) { act = false; bad = 1; }
-            const int32_t tw = A.tweak[r];
-            if (act && tw >= 0) {
-                const int64_t tc = A.tw_col[tw] - P0;
-                tcol = (int32_t)max(min(tc, (int64_t)INT32_MAX), (int64_t)INT32_MIN);
-                oq = A.tw_q[tw];
-                if (oq + ls > A.orig_bytes) { act = false; bad = 1; }
-            }
-            if (act) {
-                const uint32_t cg = ld32u(A.data, co);
-                op = cg & 15;
-                len = cg >> 4;
+        const uint32_t n = min(64u, r1 - rb);
+        for (uint32_t j = 0; j < n; j++) {
+            if (((rb + j - r0) % (uint32_t)fg) == 0) gs[(size_t)((rb + j - r0) / (uint32_t)fg) * 64 + lane] = cnt;
+            const int32_t sj = __builtin_amdgcn_readlane(s, j), ej = __builtin_amdgcn_readlane(e, j);
+            cnt += (uint32_t)(lane >= sj && lane < ej);
+        }
+    }
+    if (lane < W && (uint64_t)cnt != A.off[c0 + lane + 1] - A.off[c0 + lane]) atomicOr(A.err, 2u);
+}
+
+// (tile, group) items: lanes = the tile's columns, the group's reads one at a time (wave-uniform)
+__global__ __launch_bounds__(256) void k_fill(FillArgs A, const uint32_t *tile_first, const uint32_t *item_off,
+                                              const uint32_t *gstart, int32_t fg) {
+    __shared__ uint8_t stq[4][64 * FILL_ST], stc[4][64 * FILL_ST];
+    __shared__ uint64_t s_co[4][64], s_qo[4][64], s_oq[4][64];
+    __shared__ int32_t s_x[4][64], s_e[4][64], s_tc[4][64];
+    __shared__ uint32_t s_ncig[4][64], s_ls[4][64], s_ops[4][64][FILL_OPS];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs; consecutive items (the same tile's groups and
+    // the next tile's, which share reads) land on one XCD
+    const uint32_t nb = gridDim.x, per = nb >> 3, b = blockIdx.x;
+    const uint32_t blk = (b < (per << 3)) ? (b & 7) * per + (b >> 3) : b;
+    const uint32_t item = blk * 4 + (uint32_t)w;
+    const uint32_t total = item_off[A.n_tiles];
+    if (item >= total) return;                                    // (wave-uniform; no barrier below)
+    int32_t lo = 0, hi = A.n_tiles;                               // the tile: last t with item_off[t] <= item
+    while (hi - lo > 1) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (item_off[mid] <= item) lo = mid; else hi = mid;
+    }
+    const int32_t t = lo;
+    const uint32_t grp = item - item_off[t];
+    const int32_t c0 = t * 64, W = min(64, A.n_cols - c0);
+    const int64_t P0 = A.pos_begin + c0;
+    const uint32_t rt0 = tile_first[max(t - A.back, 0)], rt1 = tile_first[t + 1];
+    const uint32_t ra = rt0 + grp * (uint32_t)fg, rz = min(rt1, ra + (uint32_t)fg);
+    uint64_t cur = 0;
+    if (lane < W) cur = A.off[c0 + lane] + gstart[(size_t)item * 64 + lane];
+    uint8_t *Sq = stq[w], *Sc = stc[w];
+    uint32_t k = 0, bad = 0;                                       // entries staged for this lane's column
+    auto flush = [&]() {
+        // column by column: lanes j < n write the column's staged bytes j (one contiguous store per array)
+        for (int cc = 0; cc < 64; cc++) {
+            const uint32_t n = __builtin_amdgcn_readlane(k, cc);
+            if (n == 0) continue;
+            const uint64_t at = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(cur >> 32), cc) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cur, cc);
+            if ((uint32_t)lane < n) {
+                A.code[at + lane] = Sc[cc * FILL_ST + lane];
+                A.qual[at + lane] = Sq[cc * FILL_ST + lane];
             }
         }
-        for (int32_t c = smin; c < emax; c++) {
-            const bool cov = act && c >= s && c < e;
-            uint32_t cd = 0, q = 0;
-            if (cov) {
-                for (;;) {                        // the op covering column c (skipping I / S / H / P)
-                    if (eats_ref(op)) {
-                        if (c < x + (int32_t)len) break;
+        cur += k;
+        k = 0;
+    };
+    for (uint32_t rb = ra; rb < rz; rb += 64) {
+        const uint32_t n = min(64u, rz - rb);
+        // the chunk's read headers, one read per lane, into LDS
+        {
+            const uint32_t r = rb + (uint32_t)lane;
+            int32_t x = INT32_MAX, e = INT32_MIN, tc = INT32_MIN;
+            uint32_t ncig = 0, ls = 0;
+            uint64_t co = 0, qo = 0, oq = 0;
+            if ((uint32_t)lane < n) {
+                x = (int32_t)max(min((int64_t)A.rpos[r] - P0, (int64_t)INT32_MAX), (int64_t)INT32_MIN + 1);
+                e = (int32_t)max(min((int64_t)A.rend[r] - P0, (int64_t)W), (int64_t)INT32_MIN + 1);
+                if (max(x, 0) < e) {                                 // covers a column of the tile
+                    const uint64_t ro = min(A.rec[r], A.data_bytes);  // (the host checked rec + 36 <= data_bytes)
+                    const uint32_t l_name = ld32u(A.data, ro + 8) & 0xFF;
+                    ncig = ld32u(A.data, ro + 12) & 0xFFFF;
+                    ls = ld32u(A.data, ro + 16);
+                    co = ro + 32 + l_name;
+                    qo = co + 4ull * ncig + (ls + 1) / 2;
+                    if (ncig == 0 || ls > (1u << 30) || qo + ls > A.data_bytes) { bad = 1; e = INT32_MIN; }
+                    const int32_t tw = A.tweak[r];
+                    if (e != INT32_MIN && tw >= 0) {
+                        const int64_t tcl = A.tw_col[tw] - P0;
+                        tc = (int32_t)max(min(tcl, (int64_t)INT32_MAX), (int64_t)INT32_MIN);
+                        oq = A.tw_q[tw];
+                        if (oq + ls > A.orig_bytes) { bad = 1; e = INT32_MIN; }
+                    }
+                    for (int o = 0; o < FILL_OPS; o++) s_ops[w][lane][o] = (uint32_t)o < ncig ? ld32u(A.data, co + 4ull * o) : 0u;
+                } else {
+                    e = INT32_MIN;
+                }
+            }
+            s_x[w][lane] = x; s_e[w][lane] = e; s_tc[w][lane] = tc;
+            s_ncig[w][lane] = ncig; s_ls[w][lane] = ls;
+            s_co[w][lane] = co; s_qo[w][lane] = qo; s_oq[w][lane] = oq;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // four reads at a time: addresses and loads for all four, then their entries
+        for (uint32_t i0 = 0; i0 < n; i0 += 4) {
+            uint32_t cd[4], qv[4], sv[4];
+            bool cov[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t i = i0 + (uint32_t)u;
+                cov[u] = false;
+                cd[u] = 0; qv[u] = 0; sv[u] = 0;
+                if (i >= n) continue;
+                const int32_t x0 = s_x[w][i], e = s_e[w][i];
+                if (e == INT32_MIN) continue;                        // (wave-uniform)
+                const int32_t col = lane;
+                cov[u] = col >= max(x0, 0) && col < e;
+                const uint32_t ncig = s_ncig[w][i], ls = s_ls[w][i];
+                const uint64_t co = s_co[w][i], qo = s_qo[w][i];
+                const uint64_t so = co + 4ull * ncig;
+                // the op covering this lane's column: a wave-uniform walk over the ops until past the tile
+                int32_t x = x0;
+                uint32_t y = 0, op = 15, ox = 0, oy = 0;
+                for (uint32_t o = 0; o < ncig && x < W; o++) {
+                    const uint32_t c = o < (uint32_t)FILL_OPS ? s_ops[w][i][o] : ld32u(A.data, co + 4ull * o);
+                    const uint32_t cop = c & 15u, len = c >> 4;
+                    if (eats_ref(cop)) {
+                        if (col >= x && col < x + (int32_t)len && op == 15) { op = cop; ox = (uint32_t)(col - x); oy = y; }
                         x += (int32_t)len;
                     }
-                    if (eats_query(op)) y += len;
-                    if (++ci >= ncig) { bad = 1; break; }
-                    const uint32_t cg = ld32u(A.data, co + 4ull * ci);
-                    op = cg & 15;
-                    len = cg >> 4;
+                    if (eats_query(cop)) y += len;
                 }
-                if (op == 2 || op == 3) {         // D / N: the next query base's quality
-                    cd = op == 2 ? 16u : 17u;
-                    q = y < ls ? (c < tcol ? g(A.orig)[oq + y] : g(A.data)[qo + y]) : 0u;
+                if (cov[u] && op == 15) { bad = 1; cov[u] = false; }    // the CIGAR ends before the column
+                if (!cov[u]) continue;
+                if (op == 2 || op == 3) {                            // D / N: the next query base's quality
+                    cd[u] = op == 2 ? 16u : 17u;
+                    if (oy < ls) {
+                        const int32_t tc = s_tc[w][i];
+                        qv[u] = col < tc ? g(A.orig)[s_oq[w][i] + oy] : g(A.data)[qo + oy];
+                    }
+                    sv[u] = 0x100u;                                  // (code already final)
                 } else {
-                    const uint32_t qp = y + (uint32_t)(c - x);
+                    const uint32_t qp = oy + ox;
                     if (qp < ls) {
-                        const uint32_t bb = g(A.data)[so + (qp >> 1)];
-                        cd = (qp & 1) ? (bb & 15u) : (bb >> 4);
-                        q = g(A.data)[qo + qp];
+                        qv[u] = g(A.data)[qo + qp];
+                        sv[u] = g(A.data)[so + (qp >> 1)] | ((qp & 1) << 9);
                     } else {
-                        cd = 15u;
+                        cd[u] = 15u;
+                        sv[u] = 0x100u;
                     }
                 }
             }
-            const uint64_t m = __ballot(cov);
-            if (m == 0) continue;
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            const uint64_t base = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(cur >> 32), c) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cur, c);
-            const uint64_t lim = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(cend >> 32), c) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)cend, c);
-            if (cov) {
-                const uint64_t i = base + rank;
-                if (i < lim) {
-                    A.code[i] = (uint8_t)cd;
-                    A.qual[i] = (uint8_t)q;
-                } else {
-                    bad = 1;
-                }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (!cov[u]) continue;
+                const uint32_t code = (sv[u] & 0x100u) ? cd[u] : ((sv[u] & 0x200u) ? (sv[u] & 15u) : ((sv[u] >> 4) & 15u));
+                Sc[lane * FILL_ST + k] = (uint8_t)code;
+                Sq[lane * FILL_ST + k] = (uint8_t)qv[u];
+                k++;
             }
-            if (lane == c) cur += (uint64_t)__popcll(m);
+            if (__builtin_amdgcn_readfirstlane(__ballot(k > FILL_SB - 4) != 0)) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                flush();
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
         }
+        // (the next chunk's headers overwrite the LDS arrays: every lane is done with them)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (lane < W && cur != cend) bad = 1;         // every column's entries written exactly
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    flush();
+    // the group's entries end where the next group's start (the tile's last group: the column's end)
+    if (lane < W) {
+        const uint64_t want = grp + 1 < item_off[t + 1] - item_off[t] ? A.off[c0 + lane] + gstart[(size_t)(item + 1) * 64 + lane]
+                                                                    : A.off[c0 + lane + 1];
+        if (cur != want) bad = 1;
+    }
     if (__ballot(bad) && lane == 0) atomicOr(A.err, 2u);
 }
 
@@ -206,11 +313,57 @@ hipError_t launch_pos_copy(const Hist *H, const int32_t *items, int32_t n, const
     return hipGetLastError();
 }
 
+namespace {
+int32_t fill_group(int64_t n_tiles, int64_t n_reads, int32_t back, int64_t *items_cap) {
+    // items <= n_tiles + n_reads (back + 1) / fg (a read is in back + 1 tiles' read ranges); group starts take 256 B per
+    // item: fg grows so that they stay within ~1 GiB
+    int32_t fg = 256;
+    for (;;) {
+        const int64_t cap = n_tiles + 1 + (n_reads * (int64_t)(back + 1) + fg - 1) / fg;
+        if (cap <= ((int64_t)4 << 20) || fg >= (1 << 20)) { *items_cap = cap; return fg; }
+        fg *= 2;
+    }
+}
+FillLay fill_layout(void *base, int64_t n_tiles, int64_t n_reads, int32_t back, int32_t *fg) {
+    FillLay L{};
+    *fg = fill_group(n_tiles, n_reads, back, &L.items_cap);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, L.scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (int)(n_tiles + 1));
+    uint8_t *p = static_cast<uint8_t *>(base);
+    size_t o = 0;
+    L.tile_first = reinterpret_cast<uint32_t *>(p + o);
+    o += al256(4 * (size_t)(n_tiles + 1));
+    L.item_off = reinterpret_cast<uint32_t *>(p + o);
+    o += al256(4 * (size_t)(n_tiles + 1));
+    L.scan_tmp = p + o;
+    o += al256(L.scan_bytes);
+    L.gstart = reinterpret_cast<uint32_t *>(p + o);
+    o += al256(256 * (size_t)L.items_cap);
+    return L;
+}
+}  // namespace
+
+size_t fill_scratch_bytes(int64_t n_cols, int64_t n_reads, int64_t max_span) {
+    const int64_t n_tiles = (n_cols + 63) / 64;
+    int32_t fg = 0;
+    FillLay L = fill_layout(nullptr, n_tiles, n_reads, (int32_t)((max_span + 63) / 64), &fg);
+    return al256(4 * (size_t)(n_tiles + 1)) * 2 + al256(L.scan_bytes) + al256(256 * (size_t)L.items_cap) + 256;
+}
+
 hipError_t launch_pileup_fill(const FillArgs &A, hipStream_t st) {
     if (A.n_tiles <= 0) return hipSuccess;
-    k_tile_first<<<(unsigned)((A.n_reads + 1 + 255) / 256), 256, 0, st>>>(A);
-    const uint32_t blocks = (((uint32_t)A.n_tiles + 3) / 4 + 7) & ~7u;
-    k_pileup_fill<<<blocks, 256, 0, st>>>(A);
+    int32_t fg = 0;
+    FillLay L = fill_layout(A.scratch, A.n_tiles, A.n_reads, A.back, &fg);
+    k_tile_first<<<(unsigned)((A.n_reads + 1 + 255) / 256), 256, 0, st>>>(A, L.tile_first);
+    k_fill_ngroups<<<(unsigned)((A.n_tiles + 1 + 255) / 256), 256, 0, st>>>(A, L.tile_first, L.gstart, fg);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // (group counts written into the start of gstart, scanned into item_off, before gstart is filled)
+    e = hipcub::DeviceScan::ExclusiveSum(L.scan_tmp, L.scan_bytes, L.gstart, L.item_off, (int)(A.n_tiles + 1), st);
+    if (e != hipSuccess) return e;
+    k_fill_starts<<<(unsigned)((A.n_tiles + 3) / 4), 256, 0, st>>>(A, L.tile_first, L.item_off, L.gstart, fg);
+    const unsigned blocks = (unsigned)(((L.items_cap + 3) / 4 + 7) & ~7ll);
+    k_fill<<<blocks, 256, 0, st>>>(A, L.tile_first, L.item_off, L.gstart, fg);
     return hipGetLastError();
 }
 

@@ -13,6 +13,10 @@
 
 #include "spings_gpu.h"
 
+#ifndef SPG_INFLATE_MATCH_HOOK
+#define SPG_INFLATE_MATCH_HOOK(dist, len)     // (tools/inflate_stats.cpp: match statistics of a host run)
+#endif
+
 namespace spg {
 
 // Per-member decode tables: one slice of SLICE bytes (LDS on the device: mpw slices per block; a host array in the
@@ -270,6 +274,7 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
             const int ds = decode(B, distp, dcnt, dsym, IB_DIST);
             if (ds < 0 || ds > 29) { st = 5; break; }
             const uint32_t dist = dist_base(ds) + B.get((int)dist_ext(ds));
+            SPG_INFLATE_MATCH_HOOK(dist, len);
             if (dist > w) { st = 6; break; }
             if (w + len > ulen) { st = 7; break; }
             uint8_t *dst = o + w;

@@ -32,7 +32,7 @@ def _arr(p, n, t):
 
 
 def fill_from_records(r):
-    """Python restatement of k_pileup_fill over one spg_records view -> (pos_begin, offsets, codes, quals)."""
+    """Python restatement of k_fill over one spg_records view -> (pos_begin, offsets, codes, quals)."""
     nc, E, n = r.n_cols, r.n_entries, r.n_reads
     off = _arr(r.offsets, nc + 1, np.uint64)
     data = _arr(r.data, r.data_bytes, np.uint8).tobytes()
