@@ -1937,11 +1937,21 @@ static int grow_scratch(spg_ctx *c, size_t need) {
 }
 
 int spg_position_entries(spg_ctx *c, int64_t pos, uint8_t *codes, uint8_t *quals, int64_t cap, int64_t *n_out) {
-    if (!c || !n_out || cap < 0 || (cap > 0 && (!codes || !quals))) return fail("spg_position_entries: bad argument");
+    return spg_position_entries_upto(c, pos, INT64_MAX, codes, quals, cap, n_out);
+}
+
+int spg_position_entries_upto(spg_ctx *c, int64_t pos, int64_t n_batches, uint8_t *codes, uint8_t *quals, int64_t cap,
+                              int64_t *n_out) {
+    if (!c || !n_out || cap < 0 || (cap > 0 && (!codes || !quals)) || n_batches < 0)
+        return fail("spg_position_entries: bad argument");
     if (pos < 0 || pos >= c->n_pos) return fail("spg_position_entries: position outside the context");
     HIPCHK(hipSetDevice(c->device));
     *n_out = 0;
-    const std::vector<int32_t> &items = c->buckets[(size_t)(pos >> RIDX_SHIFT)];
+    // the batches that may cover pos (bucket list, accumulate order), the first n_batches of the history only (a view
+    // taken before later batches)
+    const std::vector<int32_t> &all = c->buckets[(size_t)(pos >> RIDX_SHIFT)];
+    const std::vector<int32_t> items(all.begin(), std::lower_bound(all.begin(), all.end(),
+                                                                   (int32_t)std::min<int64_t>(n_batches, INT32_MAX)));
     const int32_t n = (int32_t)items.size();
     if (n == 0) return 0;
     if (int rc = wait_copies(c)) return rc;
@@ -1966,15 +1976,23 @@ int spg_position_entries(spg_ctx *c, int64_t pos, uint8_t *codes, uint8_t *quals
     *n_out = (int64_t)tot;
     if ((int64_t)tot > cap) return cap == 0 ? 0 : fail("spg_position_entries: output capacity too small");
     if (tot == 0) return 0;
-    uint8_t *oc = nullptr;
-    HIPCHK(hipMalloc(&oc, 2 * tot));
+    // the output in the same scratch, after the index arrays (grown when needed: no allocation per lookup)
+    const size_t ob = (need + 255) & ~(size_t)255;
+    if (ob + 2 * tot > c->pe_cap) {
+        std::vector<int32_t> keep(items);          // (the scratch is reallocated: the index arrays go up again)
+        if (int rc = grow_scratch(c, ob + 2 * tot)) return rc;
+        d_rng = reinterpret_cast<uint64_t *>(c->pe_buf);
+        d_dst = d_rng + 2 * n;
+        d_items = reinterpret_cast<int32_t *>(d_dst + n);
+        HIPCHK(hipMemcpyAsync(d_items, keep.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(d_rng, rng.data(), sizeof(uint64_t) * 2 * n, hipMemcpyHostToDevice, c->stream));
+    }
+    uint8_t *oc = c->pe_buf + ob;
     HIPCHK(hipMemcpyAsync(d_dst, dst.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice, c->stream));
-    hipError_t e = launch_pos_copy(c->d_hist, d_items, n, d_rng, d_dst, oc, oc + tot, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(codes, oc, tot, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(quals, oc + tot, tot, hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    (void)hipFree(oc);
-    if (e != hipSuccess) return fail(std::string("spg_position_entries: ") + hipGetErrorString(e));
+    HIPCHK(launch_pos_copy(c->d_hist, d_items, n, d_rng, d_dst, oc, oc + tot, c->stream));
+    HIPCHK(hipMemcpyAsync(codes, oc, tot, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(quals, oc + tot, tot, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
 

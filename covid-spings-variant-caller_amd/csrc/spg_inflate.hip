@@ -515,6 +515,12 @@ int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const s
     IQ(hipStreamSynchronize(D.st));
 #undef IQ
     if (kernel_ms && hipEventElapsedTime(kernel_ms, D.ev[0], D.ev[1]) != hipSuccess) *kernel_ms = -1.f;   // (timing only)
+    // (the scratch only grows; after a BAM above 2 GiB inflated it is given back rather than held in HBM)
+    if (D.out_cap > ((size_t)2 << 30)) {
+        for (void *p : {(void *)D.comp, (void *)D.out}) (void)hipFree(p);
+        D.comp = D.out = nullptr;
+        D.comp_cap = D.out_cap = 0;
+    }
     return 0;
 }
 

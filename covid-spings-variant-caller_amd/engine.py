@@ -333,16 +333,19 @@ class PileupEngine:
             N.check(self._L.spg_kernel_times(self._h, N.ptr(a), N.ptr(f), int(cap), C.byref(n)), "spg_kernel_times")
         return a[:n.value].astype(np.float64), f[:n.value].astype(np.float64)
 
-    def position_entries(self, pos: int):
-        """(codes, quals) of every entry at ``pos`` over the history, in accumulate order (spg_position_entries)."""
+    def position_entries(self, pos: int, upto: Optional[int] = None):
+        """(codes, quals) of every entry at ``pos`` over the history (its first ``upto`` batches), in accumulate order
+        (spg_position_entries_upto)."""
         n = C.c_int64()
+        ub = (1 << 62) if upto is None else int(upto)
         with self._lock:
-            N.check(self._L.spg_position_entries(self._h, int(pos), None, None, 0, C.byref(n)), "spg_position_entries")
+            N.check(self._L.spg_position_entries_upto(self._h, int(pos), ub, None, None, 0, C.byref(n)),
+                    "spg_position_entries")
             codes = np.zeros(n.value, np.uint8)
             quals = np.zeros(n.value, np.uint8)
             if n.value:
-                N.check(self._L.spg_position_entries(self._h, int(pos), N.ptr(codes), N.ptr(quals), n.value, C.byref(n)),
-                        "spg_position_entries")
+                N.check(self._L.spg_position_entries_upto(self._h, int(pos), ub, N.ptr(codes), N.ptr(quals), n.value,
+                                                          C.byref(n)), "spg_position_entries")
         return codes, quals
 
     def history_count(self) -> int:

@@ -110,13 +110,16 @@ class PinnedIngest:
 class MemoryView(Mapping):
     """``memory`` (live_variant_caller.py:32, dict[int, Site]) as a lazy mapping: iteration in insertion order (first
     visit) from the device table; a position's Site is built when it is read, from that position's entries over the
-    history (spg_position_entries: one device gather per lookup) — O(the position's entries), never O(all entries)."""
+    history (spg_position_entries_upto: one device gather per lookup) — O(the position's entries), never O(all
+    entries).  A snapshot: lookups see the batches accumulated when the view was taken, also after later process_bam
+    calls (the view's totalDepth and quality lists stay consistent); a reset or a load invalidates it."""
 
-    def __init__(self, order, depth, first_batch, refs, entries, min_bq):
+    def __init__(self, order, depth, first_batch, refs, entries, min_bq, n_hist=None, valid=None):
         self._order = order
         self._sorted = np.sort(order)
         self._depth, self._fb, self._refs = depth, first_batch, refs
         self._entries, self._min_bq = entries, min_bq
+        self._n_hist, self._valid = n_hist, valid
 
     def __len__(self):
         return len(self._order)
@@ -131,8 +134,10 @@ class MemoryView(Mapping):
     def __getitem__(self, p) -> Site:
         if not isinstance(p, (int, np.integer)) or p not in self:
             raise KeyError(p)
+        if self._valid is not None and not self._valid():
+            raise RuntimeError("memory view taken before reset_memory / load_checkpoint: read memory again")
         p = int(p)
-        codes, quals = self._entries(p)
+        codes, quals = self._entries(p, self._n_hist)
         keep = (quals >= self._min_bq) & (codes < 16)           # pileups' bq filter (:75, :89); D/N: depth only
         c, q = codes[keep], quals[keep]
         u, first = np.unique(c, return_index=True)
@@ -201,11 +206,18 @@ class LiveVariantCaller:
         self.last_checkpoint_bytes = 0           # shard bytes the last create_checkpoint wrote
         self.reset_memory()
 
-    def __del__(self):
-        try:
+    def close(self):
+        """Release the engine (HBM accumulators, history, BAM buffers) and this caller's GPU inflate scratch."""
+        with self._lock:
             self._drain()
             self.fastaFile.close()
             self.engine.close()
+            if self.pileup_params.inflate_device >= 0:
+                N.gpu_lib().spg_bgzf_release(self.pileup_params.inflate_device)
+
+    def __del__(self):
+        try:
+            self.close()
         except Exception:
             pass
 
@@ -244,8 +256,10 @@ class LiveVariantCaller:
             present = np.nonzero(t["flags"] & N.SPG_F_PRESENT)[0]
             order = present[np.lexsort((present, t["first_batch"][present]))]
             refs = [self.fastaFile.fetch(self.fastaFile.references[i]) for i in self._batch_contig]
+            token = self._ck_token
             return MemoryView(order, t["depth"], t["first_batch"], refs, self.engine.position_entries,
-                              self.minBaseQuality)
+                              self.minBaseQuality, n_hist=self.engine.history_count(),
+                              valid=lambda: self._ck_token == token)
 
     # -- hot path -----------------------------------------------------------------------------
     def process_bam(self, inputBam: str, referenceIndex=0):

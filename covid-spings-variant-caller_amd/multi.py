@@ -235,8 +235,9 @@ class MultiEngine:
                                                                    "first_batch")]), "spg_get_table")
         return out
 
-    def position_entries(self, pos: int):
-        """(codes, quals) of every entry at reference position ``pos``, from the device whose range holds it."""
+    def position_entries(self, pos: int, upto=None):
+        """(codes, quals) of every entry at reference position ``pos`` (over the first ``upto`` batches), from the device
+        whose range holds it."""
         with self._lock:
             ctxs, cuts = self._contexts(), self._cuts_of_contexts()
             if not ctxs or cuts is None:
@@ -244,11 +245,13 @@ class MultiEngine:
             d = int(np.searchsorted(cuts[1:-1], pos, side="right"))
             local = int(pos) - int(cuts[d])
             n = C.c_int64()
-            N.check(self._L.spg_position_entries(ctxs[d], local, None, None, 0, C.byref(n)), "spg_position_entries")
+            ub = (1 << 62) if upto is None else int(upto)
+            N.check(self._L.spg_position_entries_upto(ctxs[d], local, ub, None, None, 0, C.byref(n)),
+                    "spg_position_entries")
             codes, quals = np.zeros(n.value, np.uint8), np.zeros(n.value, np.uint8)
             if n.value:
-                N.check(self._L.spg_position_entries(ctxs[d], local, N.ptr(codes), N.ptr(quals), n.value, C.byref(n)),
-                        "spg_position_entries")
+                N.check(self._L.spg_position_entries_upto(ctxs[d], local, ub, N.ptr(codes), N.ptr(quals), n.value,
+                                                          C.byref(n)), "spg_position_entries")
         return codes, quals
 
     def history_count(self) -> int:

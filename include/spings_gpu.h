@@ -268,6 +268,9 @@ int spg_history_copy_compact(spg_ctx *ctx, int64_t i, int32_t min_bq, uint64_t *
  * base-quality filter): *n_out = their number; codes / quals get them when n_out <= cap (cap 0: count only).
  * Synchronises.  LiveVariantCaller.memory builds a Site from this per lookup instead of expanding every entry. */
 int spg_position_entries(spg_ctx *ctx, int64_t pos, uint8_t *codes, uint8_t *quals, int64_t cap, int64_t *n_out);
+/* The same over the first n_batches batches of the history only (a memory view taken before later batches). */
+int spg_position_entries_upto(spg_ctx *ctx, int64_t pos, int64_t n_batches, uint8_t *codes, uint8_t *quals, int64_t cap,
+                              int64_t *n_out);
 /* Samples of history batch i (1 unless it came from spg_accumulate_samples) and, if first_sample is
  * not NULL, its per-column first samples (n_cols; zeros for a single-sample batch). */
 int spg_history_samples(spg_ctx *ctx, int64_t i, int64_t *n_samples, uint32_t *first_sample);

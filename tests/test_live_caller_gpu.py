@@ -234,6 +234,27 @@ def test_checkpoint_vcqueue_per_bam_names(planted):
     compare_variants(c.prepare_variants(), _oracle(ref, files[1:]).prepare_variants(), RTOL)
 
 
+def test_memory_view_is_a_snapshot(planted):
+    """a memory view taken after BAM 1 keeps BAM 1's quality lists after more BAMs are accumulated (its
+    lookups are bounded to the history it saw), and refuses lookups after reset_memory."""
+    d, ref, fasta, files = planted
+    c = _caller(fasta)
+    c.process_bam(files[0])
+    view = c.memory
+    o1 = _oracle(ref, files[:1]).memory
+    c.process_bam(files[1])
+    c.prepare_variants()
+    assert list(view) == list(o1)
+    assert all(view[p] == o1[p] for p in list(o1)[::5])
+    now = c.memory
+    o2 = _oracle(ref, files[:2]).memory
+    assert all(now[p] == o2[p] for p in list(o2)[::5])
+    c.reset_memory()
+    with pytest.raises(RuntimeError):
+        view[next(iter(o1))]
+    c.close()
+
+
 def test_checkpoint_single_file_format_still_loads(planted):
     """A checkpoint in the earlier single-file layout (every batch inside the named .npz) loads as before."""
     d, ref, fasta, files = planted
