@@ -307,10 +307,16 @@ def kernel_name(E, C, calls_only=True):
             "spg::k_acc_seg<4, true")
 
 
-def pmc_traffic(key, E):
+TRAFFIC_NOTE = ("not read in this run: HBM bytes per launch looked up from the newest committed PMC summary of this "
+                "kernel on this workload (profiles/rNN_*_pmc.json: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+                "tools/summarize_prof.py); null when none was committed")
+
+
+def pmc_traffic(key, E, with_source=False):
     """HBM bytes per launch of the accumulate kernel from the newest committed PMC summary
     (profiles/rNN_*pmc.json, tools/summarize_prof.py over rocprofv3 --pmc passes of this bench:
-    FETCH_SIZE x2 + WRITE_SIZE), when it was measured on this workload; else None."""
+    FETCH_SIZE x2 + WRITE_SIZE), when it was measured on this workload; else None.  A lookup, not a counter read in
+    this run (the line labels it: traffic_source)."""
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")), reverse=True):
         try:
@@ -319,8 +325,9 @@ def pmc_traffic(key, E):
             continue
         for k, v in d.items():
             if k.startswith(key) and v.get("entries") == E:
-                return v.get("hbm_bytes_per_launch")
-    return None
+                val = v.get("hbm_bytes_per_launch")
+                return (val, os.path.relpath(f, ROOT)) if with_source else val
+    return (None, None) if with_source else None
 
 
 def pmc_traffic_sum(keys, E):
@@ -1119,6 +1126,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": main_pt["achieved"] / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                      "frac": main_pt["achieved"] / PEAK_HBM,
                      "traffic": pmc_traffic(kernel_name(E, C, not args.full_table)[1], E),
+                     "traffic_source": pmc_traffic(kernel_name(E, C, not args.full_table)[1], E, True)[1],
+                     "traffic_note": TRAFFIC_NOTE,
                      "kernel": kernel_name(E, C, not args.full_table)[0], "kernel_ms": main_pt["kernel_ms"],
                      "kernel_ms_median": main_pt["kernel_ms_median"], "kernel_samples": main_pt["kernel_samples"],
                      "algorithmic_bytes": main_pt["algo_bytes"]},

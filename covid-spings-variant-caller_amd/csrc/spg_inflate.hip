@@ -16,6 +16,9 @@
 #ifndef SPG_INFLATE_MATCH_HOOK
 #define SPG_INFLATE_MATCH_HOOK(dist, len)     // (tools/inflate_stats.cpp: match statistics of a host run)
 #endif
+#ifndef SPG_INFLATE_SLOW_HOOK
+#define SPG_INFLATE_SLOW_HOOK(pb)             // (tools/inflate_stats.cpp: codes longer than the primary table)
+#endif
 
 namespace spg {
 
@@ -146,6 +149,7 @@ __host__ __device__ __forceinline__ int decode(IBits &B, const uint16_t *prim, c
         return e & 0x1FF;
     }
     // longer than the primary table (or invalid): the canonical walk, one bit at a time (first bit read = MSB)
+    SPG_INFLATE_SLOW_HOOK(pb);
     int code = 0, first = 0, index = 0;
     for (int l = 1; l <= 15; l++) {
         code |= (int)B.peek(1);

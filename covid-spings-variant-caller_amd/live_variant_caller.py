@@ -330,7 +330,7 @@ class LiveVariantCaller:
         contig = self.fastaFile.references[referenceIndex]
         # concurrent plans: one per 8 CPUs this process may use (the GPU box's 16-CPU quota: two), so one plan's serial
         # phases (record scan, depth-cap sweep) overlap the other's inflate; the host threads split between them
-        workers = workers or int(os.environ.get("SPG_PLAN_WORKERS", "0")) or max(1, min(4, cpu_share() // 8))
+        workers = workers or max(1, min(4, cpu_share() // 8))
         params = dataclasses.replace(self.pileup_params, n_threads=max(1, self.pileup_params.n_threads // workers))
 
         def plan(path):

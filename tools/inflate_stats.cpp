@@ -18,6 +18,15 @@ __host__ __device__ inline void match_hook(uint32_t d, uint32_t l) {
 #endif
 }
 #define SPG_INFLATE_MATCH_HOOK(d, l) match_hook(d, l)
+static uint64_t g_slow[16];
+__host__ __device__ inline void slow_hook(int pb) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    g_slow[pb]++;
+#else
+    (void)pb;
+#endif
+}
+#define SPG_INFLATE_SLOW_HOOK(pb) slow_hook(pb)
 #include "../covid-spings-variant-caller_amd/csrc/spg_inflate.hip"
 
 int main(int argc, char **argv) {
@@ -60,5 +69,7 @@ int main(int argc, char **argv) {
     }
     const char *ln[] = {"<16", "16-31", "32-63", "64-127", ">=128"};
     for (int k = 0; k < 5; k++) printf("len %s: %.2f %%\n", ln[k], 100.0 * g_len[k] / g_matches);
+    printf("slow-path decodes: lit/len (10-bit table) %llu, dist (8-bit) %llu, code-length (7-bit) %llu\n",
+           (unsigned long long)g_slow[10], (unsigned long long)g_slow[8], (unsigned long long)g_slow[7]);
     return 0;
 }
