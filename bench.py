@@ -83,6 +83,8 @@ def parse():
                     help="nested legs of the default sars10k line (comma list; 'none' = the main point only)")
     ap.add_argument("--no-main", action="store_true", help="profiling: skip the main point (nested legs only)")
     ap.add_argument("--sars1k-samples", type=int, default=64, help="stacked samples per GPU step at 1,000x")
+    ap.add_argument("--multi-helper", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--multi-timeout", type=float, default=300.0, help="time limit of the multi-device leg at N > 1 (s)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
                                                       "gloo only to exercise the path on one GPU)")
     return ap.parse_args()
@@ -564,6 +566,53 @@ def run_multi_device(args, world, L, depth, max_depth):
             "roofline": {"bound": "hbm", "achieved": per_dev_bytes / t_k / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                          "frac": per_dev_bytes / t_k / PEAK_HBM,
                          "frac_basis": "mean bytes per device / slowest device's accumulate kernel"}}
+
+
+def multi_helper(args) -> int:
+    """bench.py --multi-helper: wait for "go" on stdin (rank 0's signal, after the per-rank measurements), then run the
+    multi-device leg over devices 0..WORLD_SIZE-1 and print its result as one JSON line."""
+    go = sys.stdin.readline().strip()
+    if go != "go":
+        return 0
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    L, depth, _ = WORKLOADS[args.workload]
+    L = args.length or L
+    depth = args.depth or depth
+    try:
+        import spings  # noqa: F401
+        out = run_multi_device(args, world, L, depth, args.max_depth)
+    except Exception as e:
+        out = {"error": f"{type(e).__name__}: {e}"}
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+def run_helper(helper, timeout_s: float):
+    """Signal rank 0's helper and collect its JSON line; a helper past the time limit is killed (its PID) and the leg
+    reported as timed out."""
+    import threading
+    out = {}
+
+    def read():
+        out["line"] = helper.stdout.readline()
+
+    try:
+        helper.stdin.write("go\n")
+        helper.stdin.flush()
+    except OSError as e:
+        return {"error": f"helper: {e}"}
+    th = threading.Thread(target=read, daemon=True)
+    th.start()
+    th.join(timeout_s)
+    if th.is_alive():
+        helper.kill()
+        helper.wait()
+        return {"error": f"multi-device leg did not finish within {timeout_s:.0f} s (helper killed)"}
+    helper.wait(timeout=60)
+    try:
+        return json.loads(out.get("line") or "{}")
+    except ValueError:
+        return {"error": f"helper output: {out.get('line', '')[:200]!r}"}
 
 
 def nested_point(args, D, workload, local, world, rank, max_depth=0, samples=1, distinct=None, step_frac=False):
@@ -1056,9 +1105,19 @@ def main():
     if args.no_e2e: legs.discard("e2e")
     if args.no_cpu_baseline: legs.discard("cpu")
     if args.many_batches <= 0 and args.runs_batches <= 0: legs.discard("config4")
+    if args.multi_helper:
+        sys.exit(multi_helper(args))
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no launcher: one rank process per GPU, started before anything here touches a GPU
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    world0 = int(os.environ.get("WORLD_SIZE", "1"))
+    helper = None
+    if world0 > 1 and int(os.environ.get("RANK", "0")) == 0 and not args.no_main and args.workload != "sars_many":
+        # rank 0's helper for the multi-device leg, started before this process touches a GPU (it waits for a line on
+        # its stdin before it does): RCCL's one-process init over every device then runs in a process that rank 0 can
+        # stop after a time limit, and a hang there cannot take the per-rank line with it
+        helper = subprocess.Popen([sys.executable, os.path.abspath(__file__), "--multi-helper"] + sys.argv[1:],
+                                  stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
     import torch
     import spings  # noqa: F401
     if not args.e2e_threads:
@@ -1155,11 +1214,18 @@ def main():
         # ranks wait on the host
         D.host_barrier()
         if rank == 0:
-            try:
-                res["multi_device"] = run_multi_device(args, world, L, depth, args.max_depth)
-            except Exception as e:        # (reported, never fatal to the per-rank line)
-                res["multi_device"] = {"error": f"{type(e).__name__}: {e}"}
+            if helper is not None:
+                res["multi_device"] = run_helper(helper, args.multi_timeout)
+                helper = None
+            else:
+                try:
+                    res["multi_device"] = run_multi_device(args, world, L, depth, args.max_depth)
+                except Exception as e:        # (reported, never fatal to the per-rank line)
+                    res["multi_device"] = {"error": f"{type(e).__name__}: {e}"}
         D.host_barrier()
+    if helper is not None:                        # (the leg did not run: let the helper go)
+        helper.stdin.close()
+        helper.wait(timeout=30)
     if rank == 0 and world == 1 and "e2e" in legs and L == L_SARS:
         res["end_to_end"] = end_to_end(args, 0)
     if rank == 0 and world == 1 and "cpu" in legs:

@@ -90,3 +90,20 @@ def test_multi_devices(monkeypatch):
     assert bench.multi_devices(4, "nccl") == [0, 1, 2, 3]
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)
     assert bench.multi_devices(3, "gloo") == [0, 1, 0]
+
+
+def test_multi_helper_protocol():
+    """Rank 0's multi-device helper: it touches nothing until it reads "go"; rank 0 collects its JSON line, and kills it
+    (by PID) past the time limit, reporting the leg as timed out instead of losing the per-rank line."""
+    ok = subprocess.Popen([sys.executable, "-c", "import sys, json; sys.stdin.readline(); print(json.dumps({'value': 3}))"],
+                          stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    assert bench.run_helper(ok, 60) == {"value": 3}
+    hang = subprocess.Popen([sys.executable, "-c", "import sys, time; sys.stdin.readline(); time.sleep(600)"],
+                            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    out = bench.run_helper(hang, 2)
+    assert "did not finish" in out["error"] and hang.poll() is not None
+    # a helper whose rank 0 goes away without the signal exits on its own
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--multi-helper", "--gpus", "2"], input="",
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and p.stdout == ""
