@@ -45,8 +45,8 @@ hipError_t launch_pos_copy(const Hist *H, const int32_t *items, int32_t n, const
                            uint8_t *oc, uint8_t *oq, hipStream_t st);
 hipError_t launch_ck_compact(const Hist &h, uint32_t min_bq, uint64_t *kept, uint64_t *noff, void *scan_tmp,
                              size_t *scan_bytes, uint8_t *oc, uint8_t *oq, hipStream_t st);
-hipError_t launch_inflate(const uint8_t *comp, const spg_bgzf_member *mem, int64_t n, uint8_t *out, uint32_t *status,
-                          hipStream_t st);
+hipError_t launch_inflate(const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *mem, int64_t n, uint8_t *out,
+                          uint32_t *status, hipStream_t st);
 hipError_t launch_bam_scan(const BamArgs &A, int pass, hipStream_t st);
 hipError_t launch_bam_pairs(const BamPairArgs &P, bool tweak, hipStream_t st);
 hipError_t launch_bam_gather(const BamGatherArgs &G, hipStream_t st);
@@ -2176,7 +2176,8 @@ int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg
     HIPCHK(hipMemsetAsync(B.out.as<uint8_t>() + total, 0, 64, cs));
     HIPCHK(hipMemsetAsync(B.err.p, 0, 64, cs));
     HIPCHK(hipEventRecord(B.ev[0], cs));
-    HIPCHK(launch_inflate(B.comp.as<uint8_t>(), B.mem.as<spg_bgzf_member>(), n, B.out.as<uint8_t>(), B.status.as<uint32_t>(), cs));
+    HIPCHK(launch_inflate(B.comp.as<uint8_t>(), comp_bytes, B.mem.as<spg_bgzf_member>(), n, B.out.as<uint8_t>(),
+                          B.status.as<uint32_t>(), cs));
     HIPCHK(hipEventRecord(B.ev[1], cs));
     BamArgs A{};
     A.data = B.out.as<uint8_t>();

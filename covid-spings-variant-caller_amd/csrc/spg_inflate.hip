@@ -347,6 +347,308 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     status[m] = inflate_member(comp, mem[m], out, inf_lds + (size_t)threadIdx.x * SLICE);
 }
 
+// ------------------------------------------------------------------------------------------------------------------
+// k_inflate_w: one member per wave, its DEFLATE window in LDS.  The lane-per-member kernel above reads every match
+// source back from global memory — the member's own output of up to 32 KiB before, which ~8k concurrent members do not
+// keep in L2 — and a match's load waits for every store the lane issued before it (one in-order counter for loads and
+// stores): ~1 us per symbol.  Here the decoder state is wave-uniform (all 64 lanes decode the same symbol stream, no
+// divergence) and everything the symbol loop touches is in LDS: the 32 KiB window ring (match sources; a match's bytes
+// copied by up to 64 lanes at once), the Huffman tables, and a 2 KiB ring of the compressed stream that the wave
+// refills 1 KiB at a time from a global load issued 1 KiB of input earlier.  The window is written out to global memory
+// 1 KiB at a time by the whole wave.  ~38.5 KiB of LDS per wave: 4 members per CU.
+// ------------------------------------------------------------------------------------------------------------------
+constexpr int W_WIN = 32768, W_IN = 2048, W_HALF = 1024;
+
+struct WaveIn {                   // the compressed stream in LDS: bytes [lo, lo + W_IN) of the member (relative to base)
+    const uint8_t *g;             // comp + base (global)
+    uint64_t gmax;                // readable bytes from g
+    uint8_t *ring;                // LDS [W_IN]
+    uint32_t lo;
+    uint32_t nxt[4];              // the next half [lo + W_IN, lo + W_IN + W_HALF), 16 B per lane, loaded ahead
+    int lane;
+    __device__ __forceinline__ void load_next() {
+        const uint64_t at = (uint64_t)lo + W_IN + 16u * (uint32_t)lane;
+        typedef __attribute__((address_space(1))) const uint32_t gu32;
+        for (int k = 0; k < 4; k++)
+            nxt[k] = at + 4u * k + 4 <= gmax ? ((gu32 *)(const void *)(g + at))[k] : 0u;
+    }
+    // bytes [lo, lo + W_IN) into the ring (synchronous), the half after them in flight
+    __device__ __forceinline__ void reset(uint32_t at) {
+        lo = at & ~(uint32_t)(W_HALF - 1);
+        typedef __attribute__((address_space(1))) const uint32_t gu32;
+        for (int h = 0; h < W_IN; h += W_HALF) {
+            const uint64_t a = (uint64_t)lo + h + 16u * (uint32_t)lane;
+            uint32_t v[4];
+            for (int k = 0; k < 4; k++) v[k] = a + 4u * k + 4 <= gmax ? ((gu32 *)(const void *)(g + a))[k] : 0u;
+            uint32_t *d = reinterpret_cast<uint32_t *>(ring + ((lo + h + 16u * (uint32_t)lane) & (W_IN - 1)));
+            d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+        }
+        load_next();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    // the chunk at a (16-B aligned, relative) is about to be read: slide the ring when a enters its second half
+    __device__ __forceinline__ void need(uint32_t a) {
+        while (a >= lo + W_HALF) {
+            uint32_t *d = reinterpret_cast<uint32_t *>(ring + ((lo + 16u * (uint32_t)lane) & (W_IN - 1)));
+            d[0] = nxt[0]; d[1] = nxt[1]; d[2] = nxt[2]; d[3] = nxt[3];
+            lo += W_HALF;
+            load_next();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __syncthreads();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+    }
+};
+
+struct WBits {                    // IBits over the LDS ring (offsets relative to the member's aligned base)
+    WaveIn *in;
+    uint32_t qa, end;
+    uint64_t buf, r0, r1, q0, q1;
+    int n, rn;
+    __device__ __forceinline__ void chunk(uint32_t a, uint64_t &x0, uint64_t &x1) {
+        const uint32_t lastc = (end - 1) & ~15u;
+        a = a < end ? a : lastc;
+        in->need(a);
+        const uint64_t *c = reinterpret_cast<const uint64_t *>(in->ring + (a & (W_IN - 1)));
+        x0 = c[0];
+        x1 = c[1];
+    }
+    __device__ __forceinline__ void start(uint32_t s) {
+        const uint32_t a = s & ~15u;
+        const int skip = (int)(s - a) * 8;
+        chunk(a, r0, r1);
+        if (skip >= 64) { r0 = r1 >> (skip - 64); r1 = 0; }
+        else if (skip) { r0 = (r0 >> skip) | (r1 << (64 - skip)); r1 >>= skip; }
+        rn = 128 - skip;
+        qa = a + 16;
+        chunk(qa, q0, q1);
+        buf = 0;
+        n = 0;
+    }
+    __device__ __forceinline__ void fill() {
+        if (n > 32) return;
+        uint32_t v;
+        if (rn >= 32) {
+            v = (uint32_t)r0;
+            r0 = (r0 >> 32) | (r1 << 32);
+            r1 >>= 32;
+            rn -= 32;
+        } else {
+            const int k = 32 - rn;
+            v = (uint32_t)((rn ? (r0 & ((1ull << rn) - 1)) : 0) | (q0 << rn));
+            r0 = (q0 >> k) | (q1 << (64 - k));
+            r1 = q1 >> k;
+            rn = 128 - k;
+            qa += 16;
+            chunk(qa, q0, q1);
+        }
+        buf |= (uint64_t)v << n;
+        n += 32;
+    }
+    __device__ __forceinline__ uint32_t peek(int k) const { return (uint32_t)(buf & ((1ull << k) - 1)); }
+    __device__ __forceinline__ void drop(int k) { buf >>= k; n -= k; }
+    __device__ __forceinline__ uint32_t get(int k) { fill(); const uint32_t v = peek(k); drop(k); return v; }
+    __device__ __forceinline__ uint32_t byte_pos() const { return qa - (uint32_t)(rn >> 3) - (uint32_t)(n >> 3); }
+};
+
+__device__ __forceinline__ int decode_w(WBits &B, const uint16_t *prim, const uint16_t *count, const uint16_t *sym, int pb) {
+    const uint16_t e = prim[B.peek(pb)];
+    if (e >> 9) {
+        B.drop(e >> 9);
+        return e & 0x1FF;
+    }
+    int code = 0, first = 0, index = 0;
+    for (int l = 1; l <= 15; l++) {
+        code |= (int)B.peek(1);
+        B.drop(1);
+        const int c = count[l];
+        if (code - first < c) return sym[index + (code - first)];
+        index += c;
+        first = (first + c) << 1;
+        code <<= 1;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__global__ __launch_bounds__(64) void k_inflate_w(const uint8_t *__restrict__ comp, uint64_t comp_bytes,
+                                                  const spg_bgzf_member *__restrict__ mem, int64_t n,
+                                                  uint8_t *__restrict__ out, uint32_t *__restrict__ status) {
+    __shared__ __align__(16) uint8_t win[W_WIN];
+    __shared__ __align__(16) uint8_t inr[W_IN];
+    __shared__ __align__(16) uint8_t slice[SLICE];
+    const int64_t m = blockIdx.x;
+    if (m >= n) return;
+    const int lane = threadIdx.x;
+    uint16_t *const litp = reinterpret_cast<uint16_t *>(slice + SL_LITP);
+    uint16_t *const distp = reinterpret_cast<uint16_t *>(slice + SL_DISTP);
+    uint16_t *const lcnt = reinterpret_cast<uint16_t *>(slice + SL_LCNT);
+    uint16_t *const dcnt = reinterpret_cast<uint16_t *>(slice + SL_DCNT);
+    uint16_t *const lsym = reinterpret_cast<uint16_t *>(slice + SL_LSYM);
+    uint16_t *const dsym = reinterpret_cast<uint16_t *>(slice + SL_DSYM);
+    uint8_t *const lens = slice + SL_LENS;
+    const spg_bgzf_member M = mem[m];
+    const uint64_t base = M.coff & ~15ull;
+    WaveIn in;
+    in.g = comp + base;
+    in.gmax = comp_bytes + 64 > base ? comp_bytes + 64 - base : 0;   // (the buffer is padded by 64 bytes)
+    in.ring = inr;
+    in.lane = lane;
+    in.reset(0);
+    WBits B;
+    B.in = &in;
+    const uint32_t cend = (uint32_t)(M.coff + M.clen - base);
+    B.end = cend + 8;
+    B.start((uint32_t)(M.coff - base));
+    uint8_t *const o = out + M.uoff;
+    const uint32_t ulen = M.ulen;
+    uint32_t w = 0, flushed = 0, st = 0;
+    int bfinal = 0;
+    bool fixed_built = false;
+    // the window's completed 1 KiB blocks to global memory (coalesced bytes: lane j writes bytes j, j + 64, ...)
+    auto flush_to = [&](uint32_t upto) {
+        while (flushed + W_HALF <= upto || (upto == ulen && flushed < upto)) {
+            const uint32_t e = min(flushed + (uint32_t)W_HALF, upto);
+            for (uint32_t p = flushed + (uint32_t)lane; p < e; p += 64) o[p] = win[p & (W_WIN - 1)];
+            flushed = e;
+        }
+    };
+    do {
+        bfinal = (int)B.get(1);
+        const uint32_t type = B.get(2);
+        if (type == 0) {                                 // stored: LEN bytes straight from the compressed stream
+            B.drop(B.n & 7);
+            const uint32_t ln = B.get(16), nl = B.get(16);
+            if ((ln ^ 0xFFFFu) != nl) { st = 2; break; }
+            const uint32_t src = B.byte_pos();
+            if (w + ln > ulen) { st = 7; break; }
+            if (src + ln > cend) { st = 8; break; }
+            typedef __attribute__((address_space(1))) const uint8_t gu8;
+            for (uint32_t i0 = 0; i0 < ln; i0 += W_HALF) {     // (1 KiB at a time: the window ring holds 32 KiB)
+                const uint32_t e = min(ln, i0 + (uint32_t)W_HALF);
+                wave_lds_sync();
+                for (uint32_t i = i0 + (uint32_t)lane; i < e; i += 64) win[(w + i - i0) & (W_WIN - 1)] = ((gu8 *)(in.g))[src + i];
+                w += e - i0;
+                wave_lds_sync();
+                flush_to(w);
+            }
+            in.reset(src + ln);
+            B.start(src + ln);
+            continue;
+        }
+        if (type == 1) {
+            if (!fixed_built) {
+                if (lane == 0) {
+                    for (int s2 = 0; s2 < 288; s2++) lens[s2] = s2 < 144 ? 8 : s2 < 256 ? 9 : s2 < 280 ? 7 : 8;
+                    build(litp, lcnt, lsym, lens, 288, IB_LIT);
+                    for (int s2 = 0; s2 < 32; s2++) lens[s2] = 5;
+                    build(distp, dcnt, dsym, lens, 32, IB_DIST);
+                }
+                wave_lds_sync();
+                fixed_built = true;
+            }
+        } else if (type == 2) {
+            fixed_built = false;
+            const int hlit = (int)B.get(5) + 257, hdist = (int)B.get(5) + 1, hclen = (int)B.get(4) + 4;
+            uint8_t *const cl = lens;
+            uint32_t clv[19];
+            for (int i = 0; i < 19; i++) clv[i] = 0;
+            for (int i = 0; i < hclen; i++) {
+                const int ord = i < 3 ? 16 + i : i == 3 ? 0 : (i & 1) ? 7 - (i - 5) / 2 : 8 + (i - 4) / 2;
+                clv[ord] = B.get(3);
+            }
+            bool ok = true;
+            if (lane == 0) {
+                for (int i = 0; i < 19; i++) cl[i] = (uint8_t)clv[i];
+                ok = build(litp, dcnt, dsym, cl, 19, IB_CL);
+            }
+            wave_lds_sync();
+            if (!__builtin_amdgcn_readfirstlane((int)ok)) { st = 3; break; }
+            int k = 0;
+            while (k < hlit + hdist) {
+                B.fill();
+                const int s2 = decode_w(B, litp, dcnt, dsym, IB_CL);
+                if (s2 < 0) { st = 3; break; }
+                if (s2 < 16) { if (lane == 0) lens[k] = (uint8_t)s2; k++; continue; }
+                int rep;
+                uint8_t v = 0;
+                if (s2 == 16) {
+                    if (k == 0) { st = 3; break; }
+                    wave_lds_sync();
+                    v = lens[k - 1];
+                    rep = 3 + (int)B.get(2);
+                } else if (s2 == 17) {
+                    rep = 3 + (int)B.get(3);
+                } else {
+                    rep = 11 + (int)B.get(7);
+                }
+                if (k + rep > hlit + hdist) { st = 3; break; }
+                if (lane == 0)
+                    for (int r2 = 0; r2 < rep; r2++) lens[k + r2] = v;
+                k += rep;
+            }
+            if (st) break;
+            wave_lds_sync();
+            bool ok2 = lens[256] != 0;
+            if (lane == 0 && ok2)
+                ok2 = build(distp, dcnt, dsym, lens + hlit, hdist, IB_DIST) && build(litp, lcnt, lsym, lens, hlit, IB_LIT);
+            wave_lds_sync();
+            if (!__builtin_amdgcn_readfirstlane((int)ok2)) { st = lens[256] == 0 ? 3 : 4; break; }
+        } else {
+            st = 1;
+            break;
+        }
+        while (true) {                                   // the block's codes
+            B.fill();
+            const int s2 = decode_w(B, litp, lcnt, lsym, IB_LIT);
+            if (s2 < 256) {
+                if (s2 < 0) { st = 5; break; }
+                if (w >= ulen) { st = 7; break; }
+                if (lane == 0) win[w & (W_WIN - 1)] = (uint8_t)s2;
+                w++;
+                if ((w & (W_HALF - 1)) == 0) { wave_lds_sync(); flush_to(w); }
+                continue;
+            }
+            if (s2 == 256) break;
+            if (s2 > 285) { st = 5; break; }
+            B.fill();
+            const uint32_t len = len_base(s2 - 257) + B.peek((int)len_ext(s2 - 257));
+            B.drop((int)len_ext(s2 - 257));
+            const int ds = decode_w(B, distp, dcnt, dsym, IB_DIST);
+            if (ds < 0 || ds > 29) { st = 5; break; }
+            const uint32_t dist = dist_base(ds) + B.get((int)dist_ext(ds));
+            if (dist > w) { st = 6; break; }
+            if (w + len > ulen) { st = 7; break; }
+            wave_lds_sync();                             // (literals lane 0 wrote since the last sync)
+            // lanes copy bytes j = lane, lane + 64, ...: byte j of the match is the source's byte j mod dist
+            for (uint32_t j0 = 0; j0 < len; j0 += 64) {
+                const uint32_t j = j0 + (uint32_t)lane;
+                uint8_t v = 0;
+                if (j < len) v = win[(w - dist + (dist >= len ? j : j % dist)) & (W_WIN - 1)];
+                if (j < len) win[(w + j) & (W_WIN - 1)] = v;
+            }
+            const uint32_t w0 = w;
+            w += len;
+            if ((w0 >> 10) != (w >> 10)) { wave_lds_sync(); flush_to(w); }
+        }
+        if (st) break;
+        if (B.byte_pos() > cend) { st = 8; break; }
+    } while (!bfinal);
+    if (!st && w != ulen) st = 9;
+    if (!st) {
+        wave_lds_sync();
+        flush_to(ulen);
+    }
+    if (lane == 0) status[m] = st;
+}
+
 // CRC-32 (zlib's reflected polynomial) arithmetic: a * b mod P and x^(8 n) mod P, as zlib's multmodp / x2nmodp
 __device__ __forceinline__ uint32_t crc_multmodp(uint32_t a, uint32_t b) {
     uint32_t m = 1u << 31, p = 0;
@@ -406,11 +708,16 @@ __global__ __launch_bounds__(256) void k_crc32(const uint8_t *__restrict__ comp,
     }
 }
 
-hipError_t launch_inflate(const uint8_t *comp, const spg_bgzf_member *mem, int64_t n, uint8_t *out, uint32_t *status,
-                          hipStream_t st) {
+hipError_t launch_inflate(const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *mem, int64_t n, uint8_t *out,
+                          uint32_t *status, hipStream_t st) {
     if (n <= 0) return hipSuccess;
+#if defined(SPG_INFLATE_LANE)        // (A/B builds: the lane-per-member kernel)
+    (void)comp_bytes;
     hipLaunchKernelGGL(k_inflate, dim3((unsigned)((n + INFLATE_MPW - 1) / INFLATE_MPW)), dim3(64),
                        (size_t)INFLATE_MPW * SLICE, st, comp, mem, n, out, status, INFLATE_MPW);
+#else
+    hipLaunchKernelGGL(k_inflate_w, dim3((unsigned)n), dim3(64), 0, st, comp, comp_bytes, mem, n, out, status);
+#endif
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_crc32, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, comp, mem, n, (const uint8_t *)out, status);
@@ -512,7 +819,7 @@ int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const s
     IQ(hipMemsetAsync(D.comp + comp_bytes, 0, 64, D.st));
     IQ(hipMemcpyAsync(D.mem, members, (size_t)n * sizeof(spg_bgzf_member), hipMemcpyHostToDevice, D.st));
     IQ(hipEventRecord(D.ev[0], D.st));
-    IQ(spg::launch_inflate(D.comp, D.mem, n, D.out, D.status, D.st));
+    IQ(spg::launch_inflate(D.comp, comp_bytes, D.mem, n, D.out, D.status, D.st));
     IQ(hipEventRecord(D.ev[1], D.st));
     IQ(hipMemcpyAsync(out, D.out, out_bytes, hipMemcpyDeviceToHost, D.st));
     IQ(hipMemcpyAsync(status, D.status, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, D.st));
