@@ -226,7 +226,13 @@ def test_multi_device_slices_vs_single_context(devices):
         m.accumulate_slices(0, off, slices, borrow=True)
         m.finalize()
         got = m.candidates()
-        assert got.tobytes() == one.tobytes()
+        # integer fields exact; GL / QUAL within the parity bar (a slice starts its columns at another 16-B alignment
+        # than the whole batch: the deep kernel's chunks, and so its fp64 summation order, differ)
+        assert len(got) == len(one)
+        for f in ("pos", "dp", "ad", "pl", "score", "ref", "alt", "rank", "first_batch", "gl_zero"):
+            np.testing.assert_array_equal(got[f], one[f])
+        for f in ("gl", "gl_linear", "qual"):
+            np.testing.assert_allclose(got[f], one[f], rtol=1e-9, atol=0)
         assert np.array_equal(m.partition(), cuts)
     if len(devices) > 1:
         bad = list(slices)
