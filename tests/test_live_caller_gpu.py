@@ -219,7 +219,8 @@ def test_checkpoint_vcqueue_per_bam_names(planted):
     assert all(x > 0 for x in sizes)
     for k in range(2, len(seq)):                  # the same BAM again: the same bytes, not the cumulative memory
         assert sizes[k] <= 1.02 * sizes[k - 2] + 512, sizes
-    assert sizes[4] < 1.5 * sizes[0] and sum(sizes) < 3.5 * max(sizes[0], sizes[1])
+    # (cumulative shards would grow with every BAM: the five here sum to the five BAMs' own batches)
+    assert sum(sizes) <= 1.05 * (3 * sizes[0] + 2 * sizes[1])
     for k in range(len(seq)):
         b = _caller(fasta)
         b.load_checkpoint(names[k])
