@@ -141,6 +141,21 @@ def spawn_ranks(n: int, argv) -> int:
     return rc
 
 
+class _StdoutToStderr:
+    """fd 1 pointed at stderr for the duration (gloo prints its "connected to N peer ranks" lines on stdout: rank 0's
+    stdout must hold exactly the one JSON line)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *a):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 class Dist:
     """torch.distributed helpers (no-ops at N = 1).  Beside the data path's group (RCCL for nccl), a gloo group for
     host-side waits: ranks that sit out a leg rank 0 runs on every device (spg_multi) wait there, not in an RCCL
@@ -153,11 +168,12 @@ class Dist:
         if world > 1:
             import torch
             import torch.distributed as dist
-            if backend == "nccl":
-                dist.init_process_group("nccl", device_id=device)
-                self.cpu_group = dist.new_group(backend="gloo")
-            else:
-                dist.init_process_group(backend)
+            with _StdoutToStderr():
+                if backend == "nccl":
+                    dist.init_process_group("nccl", device_id=device)
+                    self.cpu_group = dist.new_group(backend="gloo")
+                else:
+                    dist.init_process_group(backend)
             self.dist = dist
             self.tdev = device if backend == "nccl" else torch.device("cpu")
 

@@ -741,8 +741,9 @@ struct BamMap {
     BamMap() = default;
     BamMap(const BamMap &) = delete;
     BamMap &operator=(const BamMap &) = delete;
+    bool mapped = true;                                   // (false: m is the caller's buffer)
     ~BamMap() {
-        if (!m) return;
+        if (!m || !mapped) return;
         // (unmapped on a helper thread: tearing down the mapped pages took 5-12 ms per 0.2 GB; parallel preads into a
         // buffer instead of the mapping were slower still, 4 GB/s)
         void *mp = const_cast<uint8_t *>(m);
@@ -751,23 +752,32 @@ struct BamMap {
     }
 };
 
-void map_bam(const std::string &path, int nt, BamMap &M) {
-    const int fd = open(path.c_str(), O_RDONLY);
-    if (fd < 0) throw std::runtime_error("cannot open " + path);
-    struct stat st;
-    if (fstat(fd, &st) != 0) { close(fd); throw std::runtime_error("cannot stat " + path); }
-    const size_t fsz = (size_t)st.st_size;
-    if (fsz == 0) { close(fd); throw std::runtime_error("not a BAM file"); }
-    void *mp = mmap(nullptr, fsz, PROT_READ, MAP_PRIVATE, fd, 0);
-    close(fd);
-    if (mp == MAP_FAILED) throw std::runtime_error("cannot map " + path);
-    M.m = (const uint8_t *)mp;
+// preloaded: the file's bytes already in memory (fsz of them; spp_bam_map_open reads them into pinned memory), else
+// the file is mapped
+void map_bam(const std::string &path, int nt, BamMap &M, const uint8_t *preloaded = nullptr, size_t pre_size = 0) {
+    size_t fsz = pre_size;
+    if (!preloaded) {
+        const int fd = open(path.c_str(), O_RDONLY);
+        if (fd < 0) throw std::runtime_error("cannot open " + path);
+        struct stat st;
+        if (fstat(fd, &st) != 0) { close(fd); throw std::runtime_error("cannot stat " + path); }
+        fsz = (size_t)st.st_size;
+        if (fsz == 0) { close(fd); throw std::runtime_error("not a BAM file"); }
+        void *mp = mmap(nullptr, fsz, PROT_READ, MAP_PRIVATE, fd, 0);
+        close(fd);
+        if (mp == MAP_FAILED) throw std::runtime_error("cannot map " + path);
+        M.m = (const uint8_t *)mp;
+    } else {
+        if (fsz == 0) throw std::runtime_error("not a BAM file");
+        M.m = preloaded;
+        M.mapped = false;
+    }
     M.fsz = fsz;
     const uint8_t *m = M.m;
     // The mapped file's pages faulted in by all threads at once, one touch per page: the member walk below
     // (a dependent chain per thread) and the inflate then run on mapped pages
     static const bool pretouch = [] { const char *e = getenv("SPP_PRETOUCH"); return !e || atoi(e) != 0; }();
-    if (pretouch) {
+    if (pretouch && !preloaded) {
         par_chunks((fsz + 4095) >> 12, nt, [&](int, size_t i0, size_t i1) {
             uint32_t acc = 0;
             for (size_t i = i0; i < i1; i++) acc += ((const volatile uint8_t *)m)[i << 12];
@@ -2030,14 +2040,37 @@ int spp_bam_map_open(spp_file *f, int n_threads, spp_bam_map **out, spp_bam_map_
     spp_bam_map *h = nullptr;
     try {
         const int nt = std::max(1, std::min(n_threads, 64));
+        // the file read straight into the (pinned) buffer by every thread (pread: no mapping, no page-table set-up and
+        // tear-down; the mapped form cost 10-11 ms per 10,000x BAM, r05e), then its members walked there
+        const int fd = open(f->path.c_str(), O_RDONLY);
+        if (fd < 0) throw std::runtime_error("cannot open " + f->path);
+        struct stat st;
+        if (fstat(fd, &st) != 0) { close(fd); throw std::runtime_error("cannot stat " + f->path); }
+        const size_t fsz = (size_t)st.st_size;
+        h = new spp_bam_map();
+        try {
+            h->comp = buf_get(fsz + 64);
+        } catch (...) {
+            close(fd);
+            throw;
+        }
+        std::atomic<bool> rd_ok{true};
+        par_tasks((fsz + ((size_t)1 << 20) - 1) >> 20, nt, [&](size_t i) {   // (1 MiB blocks, taken in turn)
+            size_t a = i << 20;
+            const size_t e = std::min(fsz, a + ((size_t)1 << 20));
+            while (a < e && rd_ok) {
+                const ssize_t r = pread(fd, h->comp.p + a, e - a, (off_t)a);
+                if (r <= 0) { rd_ok = false; break; }
+                a += (size_t)r;
+            }
+        });
+        close(fd);
+        if (!rd_ok) throw std::runtime_error("cannot read " + f->path);
+        memset(h->comp.p + fsz, 0, 64);
         BamMap M;
-        map_bam(f->path, nt, M);
+        map_bam(f->path, nt, M, h->comp.p, fsz);
         int32_t n_ref = 0;
         const uint64_t body = header_end(M, &n_ref);
-        h = new spp_bam_map();
-        h->comp = buf_get(M.fsz + 64);
-        par_chunks(M.fsz, nt, [&](int, size_t a, size_t b) { memcpy(h->comp.p + a, M.m + a, b - a); });
-        memset(h->comp.p + M.fsz, 0, 64);
         h->mem.resize(M.blks.size());
         for (size_t i = 0; i < M.blks.size(); i++)
             h->mem[i] = spg_bgzf_member{M.blks[i].off, (uint32_t)M.blks[i].clen, (uint32_t)M.blks[i].ulen, M.uoff[i]};

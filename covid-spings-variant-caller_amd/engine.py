@@ -360,19 +360,23 @@ class PileupEngine:
         [(pos_begin, offsets, codes, quals)] (min_bq: compacted as the checkpoint keeps them, iter_history)."""
         return list(self.iter_history(start, min_bq))
 
-    def iter_history(self, start: int = 0, min_bq: Optional[int] = None):
+    def iter_history(self, start: int = 0, min_bq: Optional[int] = None, staged: bool = False):
         """The batches one at a time (a long history never sits on the host at once).  min_bq: each batch as
         create_checkpoint keeps it — the entries with q >= min_bq plus a first-entry marker per column whose entries all
-        fail (spg_history_copy_compact: compacted in HBM, only the kept bytes cross PCIe)."""
+        fail (spg_history_copy_compact: compacted in HBM, only the kept bytes cross PCIe).  staged: the arrays are views
+        of the engine's pinned staging (DMA'd, no bounce copy), valid until the next batch is yielded."""
         n = self.history_count()
         for i in range(max(0, int(start)), n):
             with self._lock:
                 pb, nc, ne = C.c_int64(), C.c_int64(), C.c_uint64()
                 N.check(self._L.spg_history_info(self._h, i, C.byref(pb), C.byref(nc), C.byref(ne)),
                         "spg_history_info")
-                off = np.zeros(nc.value + 1, np.uint64)
-                codes = np.empty(ne.value, np.uint8)
-                quals = np.empty(ne.value, np.uint8)
+                if staged:
+                    off, codes, quals = self._staging(nc.value + 1, ne.value)
+                else:
+                    off = np.zeros(nc.value + 1, np.uint64)
+                    codes = np.empty(ne.value, np.uint8)
+                    quals = np.empty(ne.value, np.uint8)
                 if min_bq is None:
                     N.check(self._L.spg_history_copy(self._h, i, N.ptr(off), N.ptr(codes), N.ptr(quals)),
                             "spg_history_copy")
@@ -382,6 +386,15 @@ class PileupEngine:
                                                              N.ptr(quals), C.byref(k)), "spg_history_copy_compact")
                     codes, quals = codes[:k.value], quals[:k.value]   # (pages past k never touched)
             yield pb.value, off, codes, quals
+
+    def _staging(self, n_off: int, n_entries: int):
+        """Pinned host views (offsets, codes, quals) for history copies, grown as needed and reused."""
+        st = getattr(self, "_stage", None)
+        if st is None or len(st[0]) < n_off or len(st[1]) < n_entries:
+            st = (pinned_empty(max(n_off, int(n_off * 1.125)), np.uint64), pinned_empty(max(16, int(n_entries * 1.125))),
+                  pinned_empty(max(16, int(n_entries * 1.125))))
+            self._stage = st
+        return st[0][:n_off], st[1][:n_entries], st[2][:n_entries]
 
     # -- results ------------------------------------------------------------------------------
     def table(self, pos0: int = 0, n: Optional[int] = None) -> Dict[str, np.ndarray]:

@@ -419,19 +419,11 @@ class LiveVariantCaller:
                 shards, first = [], 0
             self.last_checkpoint_bytes = 0
             if first < n:
-                arrays = {}
-                for i, (pb, off, codes, quals) in enumerate(self.engine.iter_history(first, min_bq=self.minBaseQuality)):
-                    arrays[f"b{i}_pos"] = np.int64(pb)
-                    arrays[f"b{i}_off"] = off
-                    arrays[f"b{i}_codes"] = codes
-                    arrays[f"b{i}_quals"] = quals
-                shard = f"spgck-{self._ck_token[:16]}-{first}-{n - first}.npz"
+                shard = f"spgck-{self._ck_token[:16]}-{first}-{n - first}.spgck"
                 path = os.path.join(d, shard)
-                with open(path + ".tmp", "wb") as f:
-                    np.savez(f, **arrays)
-                os.replace(path + ".tmp", path)
-                self.last_checkpoint_bytes = os.path.getsize(path)
-                del arrays
+                staged = isinstance(self.engine, PileupEngine)
+                self.last_checkpoint_bytes = _write_shard(
+                    path, self.engine.iter_history(first, min_bq=self.minBaseQuality, **({"staged": True} if staged else {})))
                 shards.append((shard, first, n - first))
             self._ck_chain[d] = list(shards)
             old = _read_manifest(filename)
@@ -464,6 +456,12 @@ class LiveVariantCaller:
             d = os.path.dirname(os.path.abspath(filename))
             contig, batches = man["contig"], []
             for s, a, k in man["shards"]:
+                if s.endswith(".spgck"):
+                    got = _read_shard(os.path.join(d, s))
+                    if len(got) != k:
+                        raise ValueError(f"checkpoint shard {s}: {len(got)} batches, the manifest lists {k}")
+                    batches += got
+                    continue
                 with np.load(os.path.join(d, s), allow_pickle=False) as z:
                     batches += [(int(z[f"b{i}_pos"]), z[f"b{i}_off"], z[f"b{i}_codes"], z[f"b{i}_quals"])
                                 for i in range(k)]
@@ -534,6 +532,64 @@ def _read_manifest(filename):
 def _is_bgzf(path: str) -> bool:
     with open(path, "rb") as f:
         return f.read(2) == b"\x1f\x8b"
+
+
+_SHARD_MAGIC, _SHARD_END = b"SPGCKv1\0", b"SPGCKEND"
+
+
+def _write_shard(path: str, batches) -> int:
+    """A checkpoint shard: each batch's offsets / codes / quals written as they come (64-B aligned raw arrays, no
+    per-array CRC or copy — np.savez's zip CRC and buffer copies took most of a 10,000x BAM's checkpoint), then a JSON
+    index and its offset.  Written to <path>.tmp and renamed.  Returns the file's size."""
+    import json
+    import struct
+    index = []
+    with open(path + ".tmp", "wb") as f:
+        f.write(_SHARD_MAGIC)
+        for pb, off, codes, quals in batches:
+            ent = {"pos": int(pb)}
+            for name, a in (("off", off), ("codes", codes), ("quals", quals)):
+                a = np.ascontiguousarray(a)
+                pad = (-f.tell()) % 64
+                if pad:
+                    f.write(b"\0" * pad)
+                ent[name] = [f.tell(), int(a.size), a.dtype.str]
+                f.write(memoryview(a).cast("B"))
+            index.append(ent)
+        at = f.tell()
+        f.write(json.dumps(index).encode())
+        f.write(struct.pack("<Q", at) + _SHARD_END)
+        size = f.tell()
+    os.replace(path + ".tmp", path)
+    return size
+
+
+def _read_shard(path: str):
+    """[(pos_begin, offsets, codes, quals)] of a _write_shard file (no code from the file is executed: raw arrays of
+    the dtypes its index names, u64 / u8 only)."""
+    import json
+    import struct
+    with open(path, "rb") as f:
+        if f.read(8) != _SHARD_MAGIC:
+            raise ValueError(f"{path}: not a checkpoint shard")
+        f.seek(-16, os.SEEK_END)
+        at, end = struct.unpack("<Q8s", f.read(16))
+        if end != _SHARD_END:
+            raise ValueError(f"{path}: truncated checkpoint shard")
+        size = f.tell()
+        f.seek(at)
+        index = json.loads(f.read(size - 16 - at))
+        out = []
+        for ent in index:
+            arrs = []
+            for name in ("off", "codes", "quals"):
+                pos, n, dt = ent[name]
+                if dt not in ("<u8", "|u1"):
+                    raise ValueError(f"{path}: unexpected dtype {dt}")
+                f.seek(pos)
+                arrs.append(np.fromfile(f, dtype=np.dtype(dt), count=n))
+            out.append((int(ent["pos"]), *arrs))
+    return out
 
 
 def _remove_unlisted(d: str, files):

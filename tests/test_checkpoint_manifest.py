@@ -35,3 +35,40 @@ def test_not_a_manifest(tmp_path):
     pk = tmp_path / "p.npz"
     pk.write_bytes(pickle.dumps({"memory": {}}))      # the reference's pickle: never unpickled
     assert _read_manifest(str(pk)) is None
+
+
+def test_shard_roundtrip_and_refusals(tmp_path):
+    """The raw checkpoint shard (live_variant_caller._write_shard / _read_shard): batches written as they come read back
+    identical; a file that is not a shard, a truncated one, or one naming another dtype is refused."""
+    from covid_spings_variant_caller_amd.live_variant_caller import _read_shard, _write_shard
+    rng = np.random.default_rng(3)
+    batches = []
+    for k in range(4):
+        n = int(rng.integers(0, 50))
+        lens = rng.integers(0, 9, n)
+        off = np.zeros(n + 1, np.uint64)
+        np.cumsum(lens, out=off[1:])
+        batches.append((int(rng.integers(0, 1000)), off, rng.integers(0, 18, int(off[-1]), dtype=np.uint8),
+                        rng.integers(0, 60, int(off[-1]), dtype=np.uint8)))
+    p = str(tmp_path / "a.spgck")
+    size = _write_shard(p, iter(batches))
+    assert size == (tmp_path / "a.spgck").stat().st_size
+    got = _read_shard(p)
+    assert len(got) == len(batches)
+    for (pa, oa, ca, qa), (pb, ob, cb, qb) in zip(got, batches):
+        assert pa == pb and oa.dtype == np.uint64
+        np.testing.assert_array_equal(oa, ob)
+        np.testing.assert_array_equal(ca, cb)
+        np.testing.assert_array_equal(qa, qb)
+    import pytest
+    bad = tmp_path / "b.spgck"
+    bad.write_bytes(b"not a shard at all, just bytes")
+    with pytest.raises(ValueError):
+        _read_shard(str(bad))
+    raw = (tmp_path / "a.spgck").read_bytes()
+    (tmp_path / "t.spgck").write_bytes(raw[:-5])
+    with pytest.raises(ValueError):
+        _read_shard(str(tmp_path / "t.spgck"))
+    (tmp_path / "d.spgck").write_bytes(raw.replace(b'"<u8"', b'"|O8"'))
+    with pytest.raises(ValueError):
+        _read_shard(str(tmp_path / "d.spgck"))

@@ -162,7 +162,7 @@ def test_checkpoint_incremental_per_bam(planted):
     for f in seq:
         a.process_bam(f)
         a.create_checkpoint(ck)
-        shards = sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".npz"))
+        shards = sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".spgck"))
         listed.append(shards)
     assert [len(x) for x in listed] == [1, 2, 3]
     assert listed[1][:1] == listed[0] and set(listed[1]) < set(listed[2])
@@ -170,7 +170,7 @@ def test_checkpoint_incremental_per_bam(planted):
     m0 = os.stat(first).st_mtime_ns
     a.create_checkpoint(ck)                      # nothing new: only the manifest is rewritten
     assert os.stat(first).st_mtime_ns == m0
-    assert sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".npz")) == listed[2]
+    assert sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".spgck")) == listed[2]
     b = _caller(fasta)
     b.load_checkpoint(ck)
     o = _oracle(ref, seq)
@@ -179,11 +179,11 @@ def test_checkpoint_incremental_per_bam(planted):
     assert list(mem) == list(o.memory) and all(mem[p] == o.memory[p] for p in o.memory)
     b.process_bam(files[1])                      # a loaded memory is a new one: its first checkpoint writes all
     b.create_checkpoint(ck)                      # its batches once, then appends
-    now = sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".npz"))
+    now = sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".spgck"))
     assert len(now) == 1 and now[0] not in listed[2]
     b.process_bam(files[0])
     b.create_checkpoint(ck)
-    now2 = sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".npz"))
+    now2 = sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".spgck"))
     assert len(now2) == 2 and set(now) < set(now2)
     c = _caller(fasta)
     c.load_checkpoint(ck)
@@ -191,7 +191,7 @@ def test_checkpoint_incremental_per_bam(planted):
     a.reset_memory()                             # a new memory: a fresh shard set, the old shards removed
     a.process_bam(files[1])
     a.create_checkpoint(ck)
-    now = sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".npz"))
+    now = sorted(x for x in os.listdir(d) if x.startswith("spgck-") and x.endswith(".spgck"))
     assert len(now) == 1 and now[0] not in now2
     c.load_checkpoint(ck)
     compare_variants(c.prepare_variants(), _oracle(ref, files[1:]).prepare_variants(), RTOL)
