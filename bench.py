@@ -926,8 +926,8 @@ def vcqueue_loop(caller, paths, work_dir):
             "write_vcf_ms": float(st[:, 2].mean()) * 1e3,
             "per_bam_ms": [[round(x * 1e3, 2) for x in r] for r in st],
             "checkpoint_shard_mb_per_bam": [round(x / 1e6, 2) for x in ck_bytes],
-            "calls_last_vcf": n_calls,
-            "path": "process_bam (device pileup) -> create_checkpoint (this BAM's batch compacted on the GPU, one shard; "
+            "calls_last_vcf": n_calls, "bam_path": caller.last_bam_path,
+            "path": "process_bam (BAM in HBM from 32 MiB files, else the records plan) -> create_checkpoint (this BAM's batch compacted on the GPU, one shard; "
                     "the per-BAM manifest lists the memory's earlier shards) -> write_vcf (prepare_variants + VCF text)"}
 
 

@@ -190,6 +190,9 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
     B.end = cend + 8;
     B.start(comp + M.coff);
     uint32_t w = 0;                                      // bytes written
+#if defined(SPG_INFLATE_TOKEN_STORES)
+    uint32_t ntk = 0;
+#endif
     uint32_t st = 0;
     int bfinal = 0;
     bool fixed_built = false;
@@ -267,7 +270,14 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
             if (s < 256) {
                 if (s < 0) { st = 5; break; }
                 if (w >= ulen) { st = 7; break; }
+#if defined(SPG_INFLATE_DECODE_ONLY)                     // (A/B: decode cost alone — no output written)
+                w++;
+#elif defined(SPG_INFLATE_TOKEN_STORES)                  // (A/B: one byte store per symbol, no match reads)
+                o[ntk++] = (uint8_t)s;
+                w++;
+#else
                 o[w++] = (uint8_t)s;
+#endif
                 continue;
             }
             if (s == 256) break;
@@ -281,6 +291,14 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
             SPG_INFLATE_MATCH_HOOK(dist, len);
             if (dist > w) { st = 6; break; }
             if (w + len > ulen) { st = 7; break; }
+#if defined(SPG_INFLATE_DECODE_ONLY)
+            w += len;
+            continue;
+#elif defined(SPG_INFLATE_TOKEN_STORES)
+            o[ntk++] = (uint8_t)(len ^ dist);
+            w += len;
+            continue;
+#endif
             uint8_t *dst = o + w;
             const uint8_t *from = dst - dist;
             if (dist >= 16 && w + len + 15 <= ulen) {
@@ -337,7 +355,11 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
 // mpw members per block, one per lane (lanes >= mpw idle), each with its SLICE of the block's LDS.  Latency-bound
 // (a member's symbols are a dependent chain): 96 VGPRs for 5 waves per SIMD, 3 members per block (r04ze: 19.3 ms on
 // the 10,000x BAM vs 20.0 at 4 waves, 23.4 at 4 members per block)
+#if defined(SPG_INFLATE_MPW_AB)
+constexpr int INFLATE_MPW = SPG_INFLATE_MPW_AB;          // (A/B builds only)
+#else
 constexpr int INFLATE_MPW = 3;
+#endif
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_inflate(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
                                                 int64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ status, int mpw) {
     extern __shared__ __align__(16) uint8_t inf_lds[];

@@ -151,7 +151,7 @@ class LiveVariantCaller:
                  minAlleleDepth: int, minEvidenceRatio: float, maxVariants: int, device: Optional[int] = None,
                  max_depth: int = 8000, stepper: str = "all", ignore_overlaps: bool = True,
                  n_threads: Optional[int] = None, devices: Optional[List[int]] = None, pileup: str = "device",
-                 gpu_inflate: bool = True):
+                 gpu_inflate: bool = True, device_min_bytes: int = 32 << 20):
         """The reference's 7 arguments (:22-32), then the engine's: ``device`` (default LOCAL_RANK or 0), or
         ``devices`` — several GPUs of this host, each owning a coordinate range of the contig (multi.MultiEngine,
         spg_multi_*: BAM records and host batches sliced at equal-entry cuts, one RCCL gather of the call tables);
@@ -162,7 +162,11 @@ class LiveVariantCaller:
                     and scans it, only the reads' fixed fields come down for the host's depth-cap / mate-pairing
                     replay, and the entries are written on the GPU (spg_bam_*); process_bams and multi-device callers
                     use the records plan below.  A BAM the device path cannot take (a member it cannot inflate,
-                    record chains that disagree, a name-hash collision) falls back to the records plan.
+                    record chains that disagree, a name-hash collision) falls back to the records plan, and so does
+                    a BAM file smaller than ``device_min_bytes`` (default 32 MiB, ~1,300 BGZF members): the GPU
+                    inflate takes ~19 ms however few members there are (one member's serial decode chain), which
+                    the host's threads match at about that size (r05f: a 100x BAM took 20.6 ms on the device path,
+                    ~2 ms on the records plan).
           "records" the host inflates and scans the BAM and takes the read decisions; the inflated records go to HBM
                     and the GPU decodes bases / qualities and walks the CIGARs (spg_accumulate_records);
           "host"    the host also writes every entry (spp_batch_fill) into pinned staging.
@@ -198,6 +202,7 @@ class LiveVariantCaller:
         self.pileup = pileup
         self.device_pileup = pileup != "host"
         self._device_bam = pileup == "device" and devices is None
+        self.device_min_bytes = int(device_min_bytes)
         self.last_bam_path = None                # which path the last BAM took: "device", "records" or "host"
         self.last_gpu_inflate = False
         if self.device_pileup:
@@ -271,7 +276,8 @@ class LiveVariantCaller:
             if contig not in bam.references:
                 raise ValueError(f"invalid contig `{contig}`")
             bgzf = _is_bgzf(inputBam)
-            if self._device_bam and bgzf and self._process_bam_device(bam, contig, referenceIndex):
+            if (self._device_bam and bgzf and os.path.getsize(inputBam) >= self.device_min_bytes
+                    and self._process_bam_device(bam, contig, referenceIndex)):
                 self.last_bam_path = "device"
                 return
             if self.device_pileup and bgzf:

@@ -111,9 +111,10 @@ typedef int (*spp_inflate_fn)(int device, const uint8_t *comp, size_t comp_bytes
                               uint8_t *out, size_t out_bytes, uint32_t *status, float *kernel_ms);
 int spp_set_inflater(spp_inflate_fn fn, int device);
 
-/* A BAM kept in HBM (include/spings_gpu.h spg_bam_*).  spp_bam_map_open maps the file, locates its
- * BGZF members (parallel header search, chains that must meet) and the header's end, and copies the file into one
- * host buffer (pinned under the allocator hook) for spg_bam_open; the handle keeps it until spp_bam_map_close.
+/* A BAM kept in HBM (include/spings_gpu.h spg_bam_*).  spp_bam_map_open reads the file (parallel pread)
+ * into one host buffer (pinned under the allocator hook) for spg_bam_open, and locates its BGZF members there
+ * (parallel header search, chains that must meet) and the header's end; the handle keeps the buffer until
+ * spp_bam_map_close.
  * spp_pileup_plan_fields replays htslib's depth cap and mate pairing (spp_pileup_plan's rules) on the reads' fixed
  * fields as spg_bam_reads_copy returns them — names compared by their 64-bit hash (the device verifies every pair's
  * names) — computes the CSR offsets, and returns the overlapping mate pairs instead of tweaking qualities on the host;

@@ -278,7 +278,7 @@ def test_process_bam_device_pileup_matches_host(tmp_path):
         bams.append(p)
     out = []
     for mode, gi in (("device", True), ("records", True), ("records", False), ("host", True)):
-        vc = LiveVariantCaller(fa, 20, 0, 10, 5, 0.1, 0, pileup=mode, gpu_inflate=gi)
+        vc = LiveVariantCaller(fa, 20, 0, 10, 5, 0.1, 0, pileup=mode, gpu_inflate=gi, device_min_bytes=0)
         assert vc.device_pileup == (mode != "host")
         for p in bams:
             vc.process_bam(p)

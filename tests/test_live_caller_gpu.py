@@ -35,7 +35,9 @@ def _oracle(ref, files, contig="chrS", minbq=30, **pk):
 
 
 def _caller(fasta, **kw):
+    """A caller whose small test BAMs take the device path too (device_min_bytes=0) unless a test says otherwise."""
     from covid_spings_variant_caller_amd.live_variant_caller import LiveVariantCaller
+    kw.setdefault("device_min_bytes", 0)
     return LiveVariantCaller(fasta, 30, 20, 10, 5, 0.10, 1, **kw)
 
 
@@ -380,3 +382,19 @@ def test_process_bams_equals_sequential_process_bam(tmp_path, gpu_inflate_min):
     compare_variants(va, _oracle(ref, files, max_depth=250).prepare_variants(), RTOL)
     mem, omem = a.memory, _oracle(ref, files, max_depth=250).memory
     assert list(mem) == list(omem) and all(mem[p] == omem[p] for p in omem)
+
+
+@pytest.mark.gpu
+def test_small_bam_takes_records_plan(planted):
+    """pileup="device" keeps a BAM in HBM only from device_min_bytes (default 32 MiB): below it the records plan
+    (host inflate) is faster; the calls are the same either way."""
+    d, ref, fasta, files = planted
+    bam = [f for f in files if f.endswith(".bam")][0]
+    out = []
+    for kw, path in ((dict(device_min_bytes=32 << 20), "records"), (dict(), "device")):
+        c = _caller(fasta, **kw)
+        c.process_bam(bam)
+        assert c.last_bam_path == path
+        out.append(c.prepare_variants())
+        c.close()
+    assert out[0] == out[1]

@@ -12,7 +12,8 @@ for f in sorted(glob.glob(os.path.join(OUT, '**', '*counter_collection.csv'), re
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(f)):
         k = r.get('Kernel_Name', '')
-        for key in ('k_inflate', 'k_pileup_fill', 'k_tile_first', 'k_acc_seg<4'):
+        for key in ('k_inflate', 'k_pileup_fill', 'k_tile_first', 'k_acc_seg<4', 'k_fill(', 'k_fill<', 'k_fill_starts',
+                    'k_crc32', 'k_bam_'):
             if key in k:
                 acc[(key, r['Counter_Name'])][r['Dispatch_Id']] += float(r['Counter_Value'])
     print('==', os.path.relpath(f, OUT))
