@@ -1358,21 +1358,150 @@ struct EndQueue {
     }
 };
 
+// htslib's overlap hash (read name -> the first mate still waiting for its partner) as a flat open-addressing table:
+// linear probing over 64-bit name keys (the reads' FNV-1a name hashes when the names are hashed, a hash of the name
+// otherwise, equal keys confirmed by comparing the names), backward-shift deletion, no allocation per entry.  The
+// node-based map it replaces cost ~10 ms per 10,000x BAM at max_depth 8000 (every read the cap drops is looked up).
+struct OlapTable {
+    std::vector<uint64_t> key;
+    std::vector<uint32_t> val;                 // read index + 1; 0 = empty slot
+    size_t mask = 0, n = 0;
+    explicit OlapTable(size_t cap = (size_t)1 << 16) { reset(cap); }
+    void reset(size_t cap) {
+        key.assign(cap, 0);
+        val.assign(cap, 0);
+        mask = cap - 1;
+        n = 0;
+    }
+    static size_t slot0(uint64_t k) { return (size_t)((k * 0x9E3779B97F4A7C15ull) >> 20); }
+    // the slot holding a read whose name equals r's (same key, eq(read) true), or SIZE_MAX
+    template <class Eq> size_t find(uint64_t k, Eq &&eq) const {
+        for (size_t i = slot0(k) & mask;; i = (i + 1) & mask) {
+            if (!val[i]) return SIZE_MAX;
+            if (key[i] == k && eq((size_t)val[i] - 1)) return i;
+        }
+    }
+    void insert(uint64_t k, size_t r) {
+        if (2 * (n + 1) > mask + 1) grow();
+        size_t i = slot0(k) & mask;
+        while (val[i]) i = (i + 1) & mask;
+        key[i] = k;
+        val[i] = (uint32_t)(r + 1);
+        n++;
+    }
+    size_t at(size_t i) const { return (size_t)val[i] - 1; }
+    void erase(size_t i) {                     // backward shift: later entries of the probe run move up
+        size_t j = i;
+        while (true) {
+            j = (j + 1) & mask;
+            if (!val[j]) break;
+            const size_t h = slot0(key[j]) & mask;
+            // entry j may fill the hole at i when its home slot h is not cyclically in (i, j]
+            if ((j > i && (h <= i || h > j)) || (j < i && (h <= i && h > j))) {
+                key[i] = key[j];
+                val[i] = val[j];
+                i = j;
+            }
+        }
+        val[i] = 0;
+        n--;
+    }
+    bool empty() const { return n == 0; }
+    void grow() {
+        std::vector<uint64_t> k0;
+        std::vector<uint32_t> v0;
+        k0.swap(key);
+        v0.swap(val);
+        reset(2 * (mask + 1));
+        for (size_t i = 0; i < v0.size(); i++)
+            if (v0[i]) insert(k0[i], (size_t)v0[i] - 1);
+    }
+};
+
+// The depth cap alone, per position instead of per read, when nothing else of simulate() below applies: reads sorted,
+// each spanning >= 1 column, and no read a mate-overlap candidate (single-end data, or ignore_overlaps off).  Then the
+// replay reduces to: the iterator stands at the previous read position when the first read at p is pushed (never
+// dropped), and at p for the others, with every read ending before p freed; so the i-th read at p (i >= 1) is dropped
+// iff B_p + i + 1 > maxcnt, where B_p counts the kept reads with pos < p and end >= p — k_p = min(n_p, max(1, maxcnt -
+// B_p)) reads kept at p, in BAM order.  B_p is carried in a ring of kept-read ends.  ~5x faster than the per-read
+// replay at 10,000x (the ring, the push list and the iterator walk per read); false: take the general replay.
+bool capped_no_pairs(const Reads &R, const spp_params &p, int32_t tid, int64_t maxcnt, std::vector<uint8_t> &keep) {
+    const size_t n = R.size();
+    const int nt = std::max(1, std::min(p.n_threads, 64));
+    std::atomic<bool> ok{true};
+    std::vector<int64_t> spans((size_t)nt, 1);
+    par_chunks(n, nt, [&](int t, size_t i0, size_t i1) {
+        int64_t sp = 1;
+        for (size_t r = i0; r < i1 && ok.load(std::memory_order_relaxed); r++) {
+            bool bad = R.end[r] <= R.pos[r] || (r && R.pos[r] < R.pos[r - 1]);
+            if (p.ignore_overlaps) {
+                const uint16_t fl = R.flag[r];
+                bad |= !(fl & F_MUNMAP) && (fl & F_PROPER) && !(R.mtid[r] >= 0 && R.mtid[r] != tid) &&
+                       !(std::llabs(R.isize[r]) >= 2 * (int64_t)R.l_seq[r] && R.mpos[r] >= R.end[r]);
+            }
+            if (bad) ok = false;
+            sp = std::max(sp, R.end[r] - R.pos[r]);
+        }
+        spans[(size_t)t] = sp;
+    });
+    if (!ok) return false;
+    const int64_t max_span = *std::max_element(spans.begin(), spans.end());
+    keep.assign(n, 0);
+    size_t ring = 2;
+    while ((int64_t)ring < max_span + 2) ring <<= 1;
+    const size_t mask = ring - 1;
+    std::vector<int64_t> ends(ring, 0);          // kept reads ending at e (slot e & mask), e >= the current position
+    int64_t alive = 0, at = INT64_MIN;           // kept reads with end >= at
+    for (size_t r0 = 0; r0 < n;) {
+        const int64_t pos = R.pos[r0];
+        size_t r1 = r0 + 1;
+        while (r1 < n && R.pos[r1] == pos) r1++;
+        if (alive > 0) {                          // free the reads ending in [at, pos)
+            if (pos - at >= (int64_t)ring) {
+                std::fill(ends.begin(), ends.end(), 0);
+                alive = 0;
+            } else {
+                for (int64_t e = at; e < pos; e++) {
+                    int64_t &c = ends[(size_t)e & mask];
+                    alive -= c;
+                    c = 0;
+                }
+            }
+        }
+        at = pos;
+        const int64_t k = std::min<int64_t>((int64_t)(r1 - r0), std::max<int64_t>(1, maxcnt - alive));
+        for (size_t r = r0; r < r0 + (size_t)k; r++) {
+            keep[r] = 1;
+            ends[(size_t)R.end[r] & mask]++;
+        }
+        alive += k;
+        r0 = r1;
+    }
+    return true;
+}
+
 // Replay of bam_plp_push / bam_plp_next: which reads enter the buffer (maxcnt) and the overlap
 // pairing.  Returns keep[r].
 std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks &T) {
     const size_t n = R.size();
-    T.col.assign(n, INT64_MAX);
+    T.col.clear();                             // (empty: no read tweaked; else one column per read, INT64_MAX: none)
     // Uncapped, every read spans >= 1 column and no overlap pairing can happen: every read is pushed
     // (sorted starts keep the pending position <= each read's start < its end) and nothing is tweaked
     if (p.max_depth <= 0) {
-        bool simple = true;
-        for (size_t r = 0; r < n && simple; r++)
-            simple = R.end[r] > R.pos[r] && !(p.ignore_overlaps && (R.flag[r] & F_PROPER));
+        std::atomic<bool> simple{true};
+        par_chunks(n, std::max(1, std::min(p.n_threads, 64)), [&](int, size_t i0, size_t i1) {
+            for (size_t r = i0; r < i1 && simple.load(std::memory_order_relaxed); r++)
+                if (!(R.end[r] > R.pos[r] && !(p.ignore_overlaps && (R.flag[r] & F_PROPER)))) simple = false;
+        });
         if (simple) return std::vector<uint8_t>(n, 1);
     }
-    std::vector<uint8_t> keep(n, 0);
     const int64_t maxcnt = p.max_depth > 0 ? p.max_depth : INT64_MAX;
+    if (p.max_depth > 0) {
+        std::vector<uint8_t> keep;
+        if (capped_no_pairs(R, p, tid, maxcnt, keep)) return keep;
+    }
+    T.col.assign(n, INT64_MAX);
+    std::vector<uint8_t> keep(n, 0);
     // live buffer: reads pushed and not yet freed.  Freed while scanning column c when end <= c.
     int64_t max_span = 0;
     for (size_t r = 0; r < n; r++) max_span = std::max(max_span, R.end[r] - R.pos[r]);
@@ -1385,15 +1514,26 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
     // to that read's position.
     int64_t it_pos = 0, max_pos = -1;
     bool started = tid == 0;
-    // (keyed by views of the names in place: no string built per read — the std::string keys cost about half of
-    // this sweep at 10,000x)
-    std::unordered_map<std::string_view, size_t> olap;
-    if (p.ignore_overlaps) olap.reserve(1u << 16);
+    // (keyed by the names in place: no string built per read — the std::string keys cost about half of this sweep at
+    // 10,000x)
+    OlapTable olap(p.ignore_overlaps ? (size_t)1 << 16 : 2);
     auto name = [&](size_t r) { return R.name_view(r); };
+    auto name_key = [&](size_t r) -> uint64_t {
+        if (R.hashed) return R.nhash[r];
+        const std::string_view v = R.name_view(r);
+        uint64_t h = 0xcbf29ce484222325ull;
+        for (const char ch : v) h = (h ^ (uint8_t)ch) * 0x100000001b3ull;
+        return h;
+    };
+    auto olap_find = [&](size_t r, uint64_t k) {
+        if (R.hashed) return olap.find(k, [](size_t) { return true; });
+        const std::string_view nm = name(r);
+        return olap.find(k, [&](size_t a) { return name(a) == nm; });
+    };
     auto olap_remove = [&](size_t r) {
         if (!p.ignore_overlaps || olap.empty()) return;
-        auto itr = olap.find(name(r));
-        if (itr != olap.end()) olap.erase(itr);
+        const size_t i = olap_find(r, name_key(r));
+        if (i != SIZE_MAX) olap.erase(i);
     };
     auto scan = [&](int64_t col) {            // free reads with end <= col (bam_plp_next)
         by_end.pop_upto(col, [&](size_t r) {
@@ -1427,12 +1567,12 @@ std::vector<uint8_t> simulate(Reads &R, const spp_params &p, int32_t tid, Tweaks
                                   !(R.mtid[r] >= 0 && R.mtid[r] != tid) &&
                                   !(std::llabs(R.isize[r]) >= 2 * (int64_t)R.l_seq[r] && R.mpos[r] >= R.end[r]);
                 if (cand) {
-                    const std::string_view nm = name(r);
-                    auto itr = olap.find(nm);
-                    if (itr == olap.end()) {
-                        if (R.mpos[r] >= R.pos[r] || ((fl & F_PAIRED) && R.mpos[r] == -1)) olap.emplace(nm, r);
+                    const uint64_t k = name_key(r);
+                    const size_t itr = olap_find(r, k);
+                    if (itr == SIZE_MAX) {
+                        if (R.mpos[r] >= R.pos[r] || ((fl & F_PAIRED) && R.mpos[r] == -1)) olap.insert(k, r);
                     } else {
-                        const size_t a = itr->second;
+                        const size_t a = olap.at(itr);
                         // region pileups decode the reads within a read span of the region: a pair with
                         // an undecoded mate shares no aligned base with the region's reads
                         if (R.bases[a] && R.bases[r]) {
@@ -1609,7 +1749,7 @@ void fill_csr(const spp_plan &P, spp_batch *B, uint8_t *code, uint8_t *qual, int
             const uint32_t *cg = R.cigar.data() + R.cig_off[r];
             const uint8_t *sq = R.seq(r), *ql = R.qual(r);
             const uint32_t ls = R.l_seq[r];
-            const int64_t tcol = T.col[r];
+            const int64_t tcol = T.col.empty() ? INT64_MAX : T.col[r];
             const uint8_t *ql0 = tcol == INT64_MAX ? ql : T.orig.at(r).data();
             for (uint32_t i = 0; i < R.n_cig[r] && x < lo + c1; i++) {
                 const uint32_t op = cg[i] & 0xF, l = cg[i] >> 4;

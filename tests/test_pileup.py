@@ -72,6 +72,22 @@ def test_random_sam_vs_port(tmp_path, seed, kw):
         assert_same(product(sam, c, **kw), oracle(sam, c, **kw))
 
 
+@pytest.mark.parametrize("seed", [6, 7])
+@pytest.mark.parametrize("max_depth", [1, 2, 4, 7, 30])
+def test_unpaired_depth_cap_vs_port(tmp_path, seed, max_depth):
+    """Single-end reads (no mate-overlap candidate): the depth cap takes its per-position form
+    (capped_no_pairs in spp_pileup.cpp) — equal to the column-by-column simulation, stacks of reads sharing a start
+    included."""
+    contigs = [("chrA", 700), ("chrB", 700)]
+    recs = samgen.random_records(seed, contigs, n_reads=600, pair_frac=0.0, stack_every=3)
+    sam = str(tmp_path / "r.sam")
+    samgen.write_sam(sam, contigs, recs)
+    for c, _ in contigs:
+        assert_same(product(sam, c, max_depth=max_depth), oracle(sam, c, max_depth=max_depth))
+        assert_same(product(sam, c, max_depth=max_depth, ignore_overlaps=False),
+                    oracle(sam, c, max_depth=max_depth, ignore_overlaps=False))
+
+
 @pytest.mark.parametrize("seed", [4, 5])
 def test_bam_equals_sam(tmp_path, seed):
     contigs = [("chrA", 700), ("chrB", 700)]
