@@ -157,10 +157,13 @@ def gpu_lib():
     _sig(L.spg_bgzf_last_error, C.c_char_p)
     _sig(L.spg_bgzf_inflate_check, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp)
     _sig(L.spg_bgzf_release, i32, i32)
+    _sig(L.spg_bgzf_inflate_par_check, i32, vp, C.c_size_t, vp, i64, vp, C.c_size_t, vp, vp)
+    _sig(L.spg_bgzf_fallbacks, i32, i32, C.POINTER(i64))
     _sig(L.spg_bam_open, i32, vp, vp, u64, vp, i64, u64, i32, i32, C.POINTER(SpgBamFilter), C.POINTER(i64))
     _sig(L.spg_bam_reads_copy, i32, vp, C.POINTER(SpgBamReads))
     _sig(L.spg_bam_accumulate, i32, vp, C.POINTER(SpgBamPlan), C.c_uint32)
     _sig(L.spg_bam_inflate_ms, i32, vp, C.POINTER(C.c_float))
+    _sig(L.spg_bam_inflate_fallbacks, i32, vp, C.POINTER(i64))
     _sig(L.spg_bam_release, i32, vp)
     _sig(L.spg_position_entries, i32, vp, i64, vp, vp, i64, C.POINTER(i64))
     _sig(L.spg_position_entries_upto, i32, vp, i64, i64, vp, vp, i64, C.POINTER(i64))

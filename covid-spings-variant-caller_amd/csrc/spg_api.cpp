@@ -45,8 +45,9 @@ hipError_t launch_pos_copy(const Hist *H, const int32_t *items, int32_t n, const
                            uint8_t *oc, uint8_t *oq, hipStream_t st);
 hipError_t launch_ck_compact(const Hist &h, uint32_t min_bq, uint64_t *kept, uint64_t *noff, void *scan_tmp,
                              size_t *scan_bytes, uint8_t *oc, uint8_t *oq, hipStream_t st);
+size_t inflate_scratch_bytes(uint64_t comp_bytes, int64_t n);
 hipError_t launch_inflate(const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *mem, int64_t n, uint8_t *out,
-                          uint32_t *status, hipStream_t st);
+                          uint32_t *status, void *scratch, hipStream_t st);
 hipError_t launch_bam_scan(const BamArgs &A, int pass, hipStream_t st);
 hipError_t launch_bam_pairs(const BamPairArgs &P, bool tweak, hipStream_t st);
 hipError_t launch_bam_gather(const BamGatherArgs &G, hipStream_t st);
@@ -159,7 +160,7 @@ struct DBuf {
 };
 struct BamDev {
     DBuf comp, out, mem, status, uoff, start, cnt, base, lohi, rec, fields, err;
-    DBuf kept, pairs, orig, twof, recs_k, tile_first;
+    DBuf kept, pairs, orig, twof, recs_k, tile_first, iscr;
     bool open = false;                 // a BAM is loaded (spg_bam_open succeeded)
     uint64_t total = 0;                // inflated bytes
     int64_t n_members = 0;
@@ -170,10 +171,11 @@ struct BamDev {
     uint32_t *l_seq = nullptr;
     uint64_t *nhash = nullptr;
     float inflate_ms = 0.f;
+    int64_t inflate_fallbacks = 0;     // members k_inflate_par left to the lane kernel (the last spg_bam_open)
     hipEvent_t ev[2] = {nullptr, nullptr};
     void release() {
         for (DBuf *b : {&comp, &out, &mem, &status, &uoff, &start, &cnt, &base, &lohi, &rec, &fields, &err, &kept, &pairs,
-                        &orig, &twof, &recs_k, &tile_first})
+                        &orig, &twof, &recs_k, &tile_first, &iscr})
             b->release();
         open = false;
     }
@@ -2138,6 +2140,12 @@ int spg_bam_inflate_ms(spg_ctx *c, float *ms) {
     return 0;
 }
 
+int spg_bam_inflate_fallbacks(spg_ctx *c, int64_t *n) {
+    if (!c || !n) return fail("spg_bam_inflate_fallbacks: null argument");
+    *n = c->bam.inflate_fallbacks;
+    return 0;
+}
+
 int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *members, int64_t n,
                  uint64_t body, int32_t tid, int32_t n_ref, const spg_bam_filter *flt, int64_t *n_reads) {
     if (!c || !comp || !members || !flt || !n_reads || n < 1 || tid < 0 || tid >= n_ref)
@@ -2169,6 +2177,7 @@ int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg
     HIPCHK(B.base.need(sizeof(uint32_t) * (nm + 1)));
     HIPCHK(B.lohi.need(sizeof(int64_t) * 2 * nm));
     HIPCHK(B.err.need(64));
+    HIPCHK(B.iscr.need(inflate_scratch_bytes(comp_bytes, n)));
     HIPCHK(hipMemcpyAsync(B.comp.p, comp, comp_bytes, hipMemcpyHostToDevice, cs));
     HIPCHK(hipMemsetAsync(B.comp.as<uint8_t>() + comp_bytes, 0, 64, cs));
     HIPCHK(hipMemcpyAsync(B.mem.p, members, sizeof(spg_bgzf_member) * nm, hipMemcpyHostToDevice, cs));
@@ -2177,7 +2186,7 @@ int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg
     HIPCHK(hipMemsetAsync(B.err.p, 0, 64, cs));
     HIPCHK(hipEventRecord(B.ev[0], cs));
     HIPCHK(launch_inflate(B.comp.as<uint8_t>(), comp_bytes, B.mem.as<spg_bgzf_member>(), n, B.out.as<uint8_t>(),
-                          B.status.as<uint32_t>(), cs));
+                          B.status.as<uint32_t>(), B.iscr.p, cs));
     HIPCHK(hipEventRecord(B.ev[1], cs));
     BamArgs A{};
     A.data = B.out.as<uint8_t>();
@@ -2198,13 +2207,15 @@ int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg
     A.err = B.err.as<uint32_t>();
     HIPCHK(launch_bam_scan(A, 0, cs));
     HIPCHK(launch_bam_scan(A, 1, cs));
-    std::vector<uint32_t> st(nm), cnt(nm), err(1);
+    std::vector<uint32_t> st(nm), cnt(nm), err(1), fbk(1);
     std::vector<int64_t> lohi(2 * nm);
     HIPCHK(hipMemcpyAsync(st.data(), B.status.p, sizeof(uint32_t) * nm, hipMemcpyDeviceToHost, cs));
     HIPCHK(hipMemcpyAsync(cnt.data(), B.cnt.p, sizeof(uint32_t) * nm, hipMemcpyDeviceToHost, cs));
     HIPCHK(hipMemcpyAsync(lohi.data(), B.lohi.p, sizeof(int64_t) * 2 * nm, hipMemcpyDeviceToHost, cs));
     HIPCHK(hipMemcpyAsync(err.data(), B.err.p, sizeof(uint32_t), hipMemcpyDeviceToHost, cs));
+    HIPCHK(hipMemcpyAsync(fbk.data(), B.iscr.p, sizeof(uint32_t), hipMemcpyDeviceToHost, cs));
     HIPCHK(hipStreamSynchronize(cs));
+    B.inflate_fallbacks = fbk[0];
     if (hipEventElapsedTime(&B.inflate_ms, B.ev[0], B.ev[1]) != hipSuccess) B.inflate_ms = -1.f;
     for (size_t i = 0; i < nm; i++)
         if (st[i] != 0)

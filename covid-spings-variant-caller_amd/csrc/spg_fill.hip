@@ -92,18 +92,32 @@ __global__ __launch_bounds__(256) void k_fill_starts(FillArgs A, const uint32_t 
     const uint32_t r0 = tile_first[max(t - A.back, 0)], r1 = tile_first[t + 1];
     uint32_t *gs = gstart + (size_t)item_off[t] * 64;
     uint32_t cnt = 0;
-    for (uint32_t rb = r0; rb < r1; rb += 64) {
+    // fg is a multiple of 64 (fill_group): group boundaries fall on chunk starts only, so the inner loop is just the count
+    // (a per-read `% fg` there made this pass 1.6 ms per 10,000x BAM, r05g)
+    for (uint32_t rb = r0, gi = 0, gl = 0; rb < r1; rb += 64) {
         int32_t s = INT32_MAX, e = INT32_MIN;
         if (rb + lane < r1) {
             s = (int32_t)max((int64_t)A.rpos[rb + lane] - P0, (int64_t)INT32_MIN + 1);
             e = (int32_t)min((int64_t)A.rend[rb + lane] - P0, (int64_t)INT32_MAX);
         }
+        if (gl == 0) gs[(size_t)gi * 64 + lane] = cnt;
+        gl += 64;
+        if (gl == (uint32_t)fg) { gl = 0; gi++; }
         const uint32_t n = min(64u, r1 - rb);
-        for (uint32_t j = 0; j < n; j++) {
-            if (((rb + j - r0) % (uint32_t)fg) == 0) gs[(size_t)((rb + j - r0) / (uint32_t)fg) * 64 + lane] = cnt;
-            const int32_t sj = __builtin_amdgcn_readlane(s, j), ej = __builtin_amdgcn_readlane(e, j);
-            cnt += (uint32_t)(lane >= sj && lane < ej);
+        // two counters so consecutive reads' compares do not chain on one add
+        uint32_t c0 = 0, c1 = 0;
+        uint32_t j = 0;
+        for (; j + 2 <= n; j += 2) {
+            const int32_t s0 = __builtin_amdgcn_readlane(s, j), e0 = __builtin_amdgcn_readlane(e, j);
+            const int32_t s1 = __builtin_amdgcn_readlane(s, j + 1), e1 = __builtin_amdgcn_readlane(e, j + 1);
+            c0 += (uint32_t)(lane >= s0 && lane < e0);
+            c1 += (uint32_t)(lane >= s1 && lane < e1);
         }
+        if (j < n) {
+            const int32_t s0 = __builtin_amdgcn_readlane(s, j), e0 = __builtin_amdgcn_readlane(e, j);
+            c0 += (uint32_t)(lane >= s0 && lane < e0);
+        }
+        cnt += c0 + c1;
     }
     if (lane < W && (uint64_t)cnt != A.off[c0 + lane + 1] - A.off[c0 + lane]) atomicOr(A.err, 2u);
 }

@@ -11,6 +11,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "spings_gpu.h"
 
 #ifndef SPG_INFLATE_MATCH_HOOK
@@ -173,6 +176,62 @@ __host__ __device__ __forceinline__ uint32_t dist_base(int d) {
     return d < 4 ? (uint32_t)d + 1u : ((2u | (uint32_t)(d & 1)) << dist_ext(d)) + 1u;
 }
 
+// A fixed (type 1) or dynamic (type 2) block's header read after its 3 header bits, and its decode tables built into
+// slice; status 0, 3 bad code lengths, 4 bad table.  fixed_built: the fixed tables are still in the slice (a member's
+// later fixed blocks skip the rebuild).  The device's parallel inflater runs it on every lane of a wave alike (the same
+// bits, the same LDS writes).
+__host__ __device__ __forceinline__ uint32_t block_tables(IBits &B, uint8_t *slice, uint32_t type, bool &fixed_built) {
+    uint16_t *const litp = reinterpret_cast<uint16_t *>(slice + SL_LITP);
+    uint16_t *const distp = reinterpret_cast<uint16_t *>(slice + SL_DISTP);
+    uint16_t *const lcnt = reinterpret_cast<uint16_t *>(slice + SL_LCNT);
+    uint16_t *const dcnt = reinterpret_cast<uint16_t *>(slice + SL_DCNT);
+    uint16_t *const lsym = reinterpret_cast<uint16_t *>(slice + SL_LSYM);
+    uint16_t *const dsym = reinterpret_cast<uint16_t *>(slice + SL_DSYM);
+    uint8_t *const lens = slice + SL_LENS;
+    if (type == 1) {                                     // the fixed codes (RFC 1951 3.2.6), built once per member
+        if (!fixed_built) {
+            for (int s = 0; s < 288; s++) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+            build(litp, lcnt, lsym, lens, 288, IB_LIT);
+            for (int s = 0; s < 32; s++) lens[s] = 5;    // (30 and 31 complete the code; decoding them fails)
+            build(distp, dcnt, dsym, lens, 32, IB_DIST);
+            fixed_built = true;
+        }
+        return 0;
+    }
+    fixed_built = false;
+    const int hlit = (int)B.get(5) + 257, hdist = (int)B.get(5) + 1, hclen = (int)B.get(4) + 4;
+    uint8_t *const cl = lens;                            // 19 code-length code lengths, in RFC order
+    for (int i = 0; i < 19; i++) cl[i] = 0;
+    for (int i = 0; i < hclen; i++) {
+        const int ord = i < 3 ? 16 + i : i == 3 ? 0 : (i & 1) ? 7 - (i - 5) / 2 : 8 + (i - 4) / 2;   // RFC 1951 3.2.7
+        cl[ord] = (uint8_t)B.get(3);
+    }
+    if (!build(litp, dcnt, dsym, cl, 19, IB_CL)) return 3;
+    int k = 0;
+    while (k < hlit + hdist) {
+        B.fill();
+        const int s = decode(B, litp, dcnt, dsym, IB_CL);
+        if (s < 0) return 3;
+        if (s < 16) { lens[k++] = (uint8_t)s; continue; }
+        int rep;
+        uint8_t v = 0;
+        if (s == 16) {
+            if (k == 0) return 3;
+            v = lens[k - 1];
+            rep = 3 + (int)B.get(2);
+        } else if (s == 17) {
+            rep = 3 + (int)B.get(3);
+        } else {
+            rep = 11 + (int)B.get(7);
+        }
+        if (k + rep > hlit + hdist) return 3;
+        while (rep--) lens[k++] = v;
+    }
+    if (lens[256] == 0) return 3;                        // no end-of-block code
+    if (!build(distp, dcnt, dsym, lens + hlit, hdist, IB_DIST) || !build(litp, lcnt, lsym, lens, hlit, IB_LIT)) return 4;
+    return 0;
+}
+
 // one member into out + M.uoff; status (see k_inflate).  slice: SLICE bytes, 8-byte aligned.
 __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp, const spg_bgzf_member &M, uint8_t *out,
                                                             uint8_t *slice) {
@@ -182,7 +241,6 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
     uint16_t *const dcnt = reinterpret_cast<uint16_t *>(slice + SL_DCNT);
     uint16_t *const lsym = reinterpret_cast<uint16_t *>(slice + SL_LSYM);
     uint16_t *const dsym = reinterpret_cast<uint16_t *>(slice + SL_DSYM);
-    uint8_t *const lens = slice + SL_LENS;
     uint8_t *o = out + M.uoff;
     const uint32_t ulen = M.ulen;
     const uint8_t *const cend = comp + M.coff + M.clen;
@@ -216,54 +274,8 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
             B.start(src + ln);
             continue;
         }
-        if (type == 1) {                                 // the fixed codes (RFC 1951 3.2.6), built once per member
-            if (!fixed_built) {
-                for (int s = 0; s < 288; s++) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-                build(litp, lcnt, lsym, lens, 288, IB_LIT);
-                for (int s = 0; s < 32; s++) lens[s] = 5;   // (30 and 31 complete the code; decoding them fails)
-                build(distp, dcnt, dsym, lens, 32, IB_DIST);
-                fixed_built = true;
-            }
-        } else if (type == 2) {
-            fixed_built = false;
-            const int hlit = (int)B.get(5) + 257, hdist = (int)B.get(5) + 1, hclen = (int)B.get(4) + 4;
-            uint8_t *const cl = lens;                    // 19 code-length code lengths, in RFC order
-            for (int i = 0; i < 19; i++) cl[i] = 0;
-            for (int i = 0; i < hclen; i++) {
-                const int ord = i < 3 ? 16 + i : i == 3 ? 0 : (i & 1) ? 7 - (i - 5) / 2 : 8 + (i - 4) / 2;   // RFC 1951 3.2.7
-                cl[ord] = (uint8_t)B.get(3);
-            }
-            if (!build(litp, dcnt, dsym, cl, 19, IB_CL)) { st = 3; break; }
-            int k = 0;
-            while (k < hlit + hdist) {
-                B.fill();
-                const int s = decode(B, litp, dcnt, dsym, IB_CL);
-                if (s < 0) { st = 3; break; }
-                if (s < 16) { lens[k++] = (uint8_t)s; continue; }
-                int rep;
-                uint8_t v = 0;
-                if (s == 16) {
-                    if (k == 0) { st = 3; break; }
-                    v = lens[k - 1];
-                    rep = 3 + (int)B.get(2);
-                } else if (s == 17) {
-                    rep = 3 + (int)B.get(3);
-                } else {
-                    rep = 11 + (int)B.get(7);
-                }
-                if (k + rep > hlit + hdist) { st = 3; break; }
-                while (rep--) lens[k++] = v;
-            }
-            if (st) break;
-            if (lens[256] == 0) { st = 3; break; }       // no end-of-block code
-            if (!build(distp, dcnt, dsym, lens + hlit, hdist, IB_DIST) || !build(litp, lcnt, lsym, lens, hlit, IB_LIT)) {
-                st = 4;
-                break;
-            }
-        } else {
-            st = 1;
-            break;
-        }
+        if (type == 3) { st = 1; break; }
+        if ((st = block_tables(B, slice, type, fixed_built)) != 0) break;
         while (true) {                                   // the block's codes
             B.fill();
             const int s = decode(B, litp, lcnt, lsym, IB_LIT);
@@ -353,322 +365,536 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
 // status: 0 ok; 1 bad block type; 2 bad stored length; 3 bad code lengths; 4 bad table; 5 bad symbol;
 // 6 distance too far back; 7 output overrun; 8 input overrun; 9 wrong size; 10 CRC32 mismatch (k_crc32).
 // mpw members per block, one per lane (lanes >= mpw idle), each with its SLICE of the block's LDS.  Latency-bound
-// (a member's symbols are a dependent chain): 96 VGPRs for 5 waves per SIMD, 3 members per block (r04ze: 19.3 ms on
-// the 10,000x BAM vs 20.0 at 4 waves, 23.4 at 4 members per block)
+// (a member's symbols are a dependent chain; r04ze: 19.3 ms on the 10,000x BAM at 3 members per block).  Since r05 the
+// fallback of k_inflate_par (only_fallback: the members it left) and the whole inflater of SPG_INFLATE_LANE A/B builds.
 #if defined(SPG_INFLATE_MPW_AB)
 constexpr int INFLATE_MPW = SPG_INFLATE_MPW_AB;          // (A/B builds only)
 #else
 constexpr int INFLATE_MPW = 3;
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_inflate(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
-                                                int64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ status, int mpw) {
+constexpr uint32_t ST_FALLBACK = 100;   // (k_inflate_par) this member is left to the lane kernel
+__global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
+                                                int64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ status, int mpw,
+                                                int only_fallback) {
     extern __shared__ __align__(16) uint8_t inf_lds[];
     if ((int)threadIdx.x >= mpw) return;
     const int64_t m = (int64_t)blockIdx.x * mpw + threadIdx.x;
     if (m >= n) return;
+    if (only_fallback && status[m] != ST_FALLBACK) return;
     status[m] = inflate_member(comp, mem[m], out, inf_lds + (size_t)threadIdx.x * SLICE);
 }
 
 // ------------------------------------------------------------------------------------------------------------------
-// k_inflate_w: one member per wave, its DEFLATE window in LDS.  The lane-per-member kernel above reads every match
-// source back from global memory — the member's own output of up to 32 KiB before, which ~8k concurrent members do not
-// keep in L2 — and a match's load waits for every store the lane issued before it (one in-order counter for loads and
-// stores): ~1 us per symbol.  Here the decoder state is wave-uniform (all 64 lanes decode the same symbol stream, no
-// divergence) and everything the symbol loop touches is in LDS: the 32 KiB window ring (match sources; a match's bytes
-// copied by up to 64 lanes at once), the Huffman tables, and a 2 KiB ring of the compressed stream that the wave
-// refills 1 KiB at a time from a global load issued 1 KiB of input earlier.  The window is written out to global memory
-// 1 KiB at a time by the whole wave.  ~38.5 KiB of LDS per wave: 4 members per CU.
+// k_inflate_par: one member per wave, its DEFLATE stream decoded by all 64 lanes at once.
+//
+// The lane-per-member kernel above runs a member's ~16k symbols as one dependent chain on one lane, three members per
+// wave: every instruction of a symbol costs the wave its 4 issue cycles for one member's progress (r05h: the symbol decode
+// alone 12 ms of 19.7 per 10,000x BAM).  Here a block's data bits are cut into K <= 64 equal segments (at least
+// PAR_MIN_SEG bits each) and lane k decodes segment k on its own, starting at the segment's first bit as if a token began
+// there.  Huffman codes self-synchronise: a decode begun at a wrong bit soon lands on a true token boundary and from there
+// on reads the true tokens (measured on the 2,000x simulator BAM, /tmp-free harness in tests/test_inflate_check.py: ~95 %
+// of lanes within 32 tokens, all within ~128 but for segments shorter than the distance).
+//  * Phase A (every lane): the segment's tokens (literal, match (length, distance), end of block) and their start
+//    positions; the lane's tokens end at the first token start past the segment (its `end`).
+//  * Sync (every lane k >= 1): decode the true stream from the end of lane k - 1's true tokens until it meets one of lane
+//    k's phase-A token starts; lane k's true tokens are these redo tokens plus its own tokens from that start on.  A lane
+//    that never meets its own tokens (its redo covers the segment) moves its end: the lanes after it synchronise again
+//    (rounds until no end moves).  More than PAR_RCAP redo tokens, a token overflow, a stored block or anything malformed
+//    sends the member to the lane-per-member kernel (status ST_FALLBACK), which also reports real errors.
+//  * The block ends at the first true end-of-block token; lanes past it decoded the next block with this block's tables
+//    and are ignored; the next block's header follows the end-of-block code.
+//  * Phase B (resolve): the true token lists in order, 64 tokens (at most PAR_BATCH output bytes) at a time, into the
+//    member's 32 KiB window in LDS (a ring of PAR_RING bytes indexed by global output address): literals and matches whose
+//    source lies before the batch are written at once (lane-parallel; matches longer than 32 bytes by the whole wave),
+//    matches whose source is an earlier token of the same batch in rounds as their sources complete.  Completed 1 KiB
+//    blocks of global memory are written from the ring with 16-byte stores.
+// Token lists, positions and redo tokens live in global scratch (inflate_scratch_bytes: 12 B per compressed byte + 76 KiB
+// per member).  ~37.5 KiB of LDS per wave: 4 members per CU at a time.
 // ------------------------------------------------------------------------------------------------------------------
-constexpr int W_WIN = 32768, W_IN = 2048, W_HALF = 1024;
+constexpr uint32_t TK_EOB = 0x40000000u, TK_MATCH = 0x80000000u;   // tokens: literal byte | EOB | match (len-3)<<16 | dist-1
+constexpr uint32_t PAR_RCAP = 256;                                  // redo tokens per lane
+constexpr uint32_t PAR_MIN_SEG = 1024;                              // data bits per lane at least (fewer lanes for short blocks)
+constexpr uint32_t PAR_RING = 33792, PAR_BATCH = 1024;              // window ring (32 KiB + one batch), batch output cap
+// scratch per member m (u32 units unless noted): token lists at 2 coff + 2048 m (2 clen + 2048 of them, split evenly
+// over the block's lanes), token start positions (u16, relative to the lane's first bit) at the same index of a u16 array,
+// redo tokens at 64 RCAP m
+__host__ __device__ __forceinline__ uint64_t par_tok_at(const spg_bgzf_member &M, uint64_t m) { return 2ull * M.coff + 2048ull * m; }
+__host__ __device__ __forceinline__ uint32_t par_area(const spg_bgzf_member &M) { return 2u * M.clen + 2048u; }
 
-struct WaveIn {                   // the compressed stream in LDS: bytes [lo, lo + W_IN) of the member (relative to base)
-    const uint8_t *g;             // comp + base (global)
-    uint64_t gmax;                // readable bytes from g
-    uint8_t *ring;                // LDS [W_IN]
-    uint32_t lo;
-    uint32_t nxt[4];              // the next half [lo + W_IN, lo + W_IN + W_HALF), 16 B per lane, loaded ahead
-    int lane;
-    __device__ __forceinline__ void load_next() {
-        const uint64_t at = (uint64_t)lo + W_IN + 16u * (uint32_t)lane;
-        typedef __attribute__((address_space(1))) const uint32_t gu32;
-        for (int k = 0; k < 4; k++)
-            nxt[k] = at + 4u * k + 4 <= gmax ? ((gu32 *)(const void *)(g + at))[k] : 0u;
-    }
-    // bytes [lo, lo + W_IN) into the ring (synchronous), the half after them in flight
-    __device__ __forceinline__ void reset(uint32_t at) {
-        lo = at & ~(uint32_t)(W_HALF - 1);
-        typedef __attribute__((address_space(1))) const uint32_t gu32;
-        for (int h = 0; h < W_IN; h += W_HALF) {
-            const uint64_t a = (uint64_t)lo + h + 16u * (uint32_t)lane;
-            uint32_t v[4];
-            for (int k = 0; k < 4; k++) v[k] = a + 4u * k + 4 <= gmax ? ((gu32 *)(const void *)(g + a))[k] : 0u;
-            uint32_t *d = reinterpret_cast<uint32_t *>(ring + ((lo + h + 16u * (uint32_t)lane) & (W_IN - 1)));
-            d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
-        }
-        load_next();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    }
-    // the chunk at a (16-B aligned, relative) is about to be read: slide the ring when a enters its second half
-    __device__ __forceinline__ void need(uint32_t a) {
-        while (a >= lo + W_HALF) {
-            uint32_t *d = reinterpret_cast<uint32_t *>(ring + ((lo + 16u * (uint32_t)lane) & (W_IN - 1)));
-            d[0] = nxt[0]; d[1] = nxt[1]; d[2] = nxt[2]; d[3] = nxt[3];
-            lo += W_HALF;
-            load_next();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __syncthreads();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        }
-    }
+struct Tabs {
+    const uint16_t *litp, *lcnt, *lsym, *distp, *dcnt, *dsym;
 };
-
-struct WBits {                    // IBits over the LDS ring (offsets relative to the member's aligned base)
-    WaveIn *in;
-    uint32_t qa, end;
-    uint64_t buf, r0, r1, q0, q1;
-    int n, rn;
-    __device__ __forceinline__ void chunk(uint32_t a, uint64_t &x0, uint64_t &x1) {
-        const uint32_t lastc = (end - 1) & ~15u;
-        a = a < end ? a : lastc;
-        in->need(a);
-        const uint64_t *c = reinterpret_cast<const uint64_t *>(in->ring + (a & (W_IN - 1)));
-        x0 = c[0];
-        x1 = c[1];
-    }
-    __device__ __forceinline__ void start(uint32_t s) {
-        const uint32_t a = s & ~15u;
-        const int skip = (int)(s - a) * 8;
-        chunk(a, r0, r1);
-        if (skip >= 64) { r0 = r1 >> (skip - 64); r1 = 0; }
-        else if (skip) { r0 = (r0 >> skip) | (r1 << (64 - skip)); r1 >>= skip; }
-        rn = 128 - skip;
-        qa = a + 16;
-        chunk(qa, q0, q1);
-        buf = 0;
-        n = 0;
-    }
-    __device__ __forceinline__ void fill() {
-        if (n > 32) return;
-        uint32_t v;
-        if (rn >= 32) {
-            v = (uint32_t)r0;
-            r0 = (r0 >> 32) | (r1 << 32);
-            r1 >>= 32;
-            rn -= 32;
-        } else {
-            const int k = 32 - rn;
-            v = (uint32_t)((rn ? (r0 & ((1ull << rn) - 1)) : 0) | (q0 << rn));
-            r0 = (q0 >> k) | (q1 << (64 - k));
-            r1 = q1 >> k;
-            rn = 128 - k;
-            qa += 16;
-            chunk(qa, q0, q1);
-        }
-        buf |= (uint64_t)v << n;
-        n += 32;
-    }
-    __device__ __forceinline__ uint32_t peek(int k) const { return (uint32_t)(buf & ((1ull << k) - 1)); }
-    __device__ __forceinline__ void drop(int k) { buf >>= k; n -= k; }
-    __device__ __forceinline__ uint32_t get(int k) { fill(); const uint32_t v = peek(k); drop(k); return v; }
-    __device__ __forceinline__ uint32_t byte_pos() const { return qa - (uint32_t)(rn >> 3) - (uint32_t)(n >> 3); }
-};
-
-__device__ __forceinline__ int decode_w(WBits &B, const uint16_t *prim, const uint16_t *count, const uint16_t *sym, int pb) {
-    const uint16_t e = prim[B.peek(pb)];
-    if (e >> 9) {
-        B.drop(e >> 9);
-        return e & 0x1FF;
-    }
-    int code = 0, first = 0, index = 0;
-    for (int l = 1; l <= 15; l++) {
-        code |= (int)B.peek(1);
-        B.drop(1);
-        const int c = count[l];
-        if (code - first < c) return sym[index + (code - first)];
-        index += c;
-        first = (first + c) << 1;
-        code <<= 1;
-    }
-    return -1;
+__host__ __device__ __forceinline__ Tabs tabs_of(const uint8_t *slice) {
+    return Tabs{reinterpret_cast<const uint16_t *>(slice + SL_LITP), reinterpret_cast<const uint16_t *>(slice + SL_LCNT),
+                reinterpret_cast<const uint16_t *>(slice + SL_LSYM), reinterpret_cast<const uint16_t *>(slice + SL_DISTP),
+                reinterpret_cast<const uint16_t *>(slice + SL_DCNT), reinterpret_cast<const uint16_t *>(slice + SL_DSYM)};
 }
 
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+// the next unread bit, relative to base (IBits: buf holds n bits, r rn bits, then the chunk at qa)
+__host__ __device__ __forceinline__ uint32_t ib_pos(const IBits &B, const uint8_t *base) {
+    return (uint32_t)(B.qa - base) * 8u - (uint32_t)B.rn - (uint32_t)B.n;
+}
+__host__ __device__ __forceinline__ void ib_seek(IBits &B, const uint8_t *base, uint32_t p) {
+    B.start(base + (p >> 3));
+    B.fill();
+    B.drop((int)(p & 7u));
 }
 
-__global__ __launch_bounds__(64) void k_inflate_w(const uint8_t *__restrict__ comp, uint64_t comp_bytes,
-                                                  const spg_bgzf_member *__restrict__ mem, int64_t n,
-                                                  uint8_t *__restrict__ out, uint32_t *__restrict__ status) {
-    __shared__ __align__(16) uint8_t win[W_WIN];
-    __shared__ __align__(16) uint8_t inr[W_IN];
+// one token at the reader's position; false: no valid token starts here
+__host__ __device__ __forceinline__ bool next_token(IBits &B, const Tabs &T, uint32_t &t) {
+    B.fill();
+    const int s = decode(B, T.litp, T.lcnt, T.lsym, IB_LIT);
+    if (s < 256) {
+        t = (uint32_t)s;
+        return s >= 0;
+    }
+    if (s == 256) {
+        t = TK_EOB;
+        return true;
+    }
+    if (s > 285) return false;
+    B.fill();
+    const uint32_t len = len_base(s - 257) + B.peek((int)len_ext(s - 257));
+    B.drop((int)len_ext(s - 257));
+    const int ds = decode(B, T.distp, T.dcnt, T.dsym, IB_DIST);
+    if (ds < 0 || ds > 29) return false;
+    const uint32_t dist = dist_base(ds) + B.get((int)dist_ext(ds));
+    t = TK_MATCH | (len - 3u) << 16 | (dist - 1u);
+    return true;
+}
+
+// phase A of one lane: tokens from bit s while they start before stop, with their start positions (pos[i] = start - s).
+// A position where no valid token starts (only before the lane has synchronised) is skipped bit by bit.  The first
+// end-of-block token is recorded (index, the bit after it); ne counts them.
+struct SegOut {
+    uint32_t end, n, ne, e0i, e0p;
+    bool ovf;
+};
+__host__ __device__ __forceinline__ SegOut decode_seg(IBits &B, const uint8_t *base, uint32_t s, uint32_t stop, const Tabs &T,
+                                                      uint32_t *tok, uint16_t *pos, uint32_t cap) {
+    SegOut o{};
+    uint32_t p = s, n = 0;
+    ib_seek(B, base, p);
+    while (p < stop) {
+        uint32_t t;
+        if (!next_token(B, T, t)) {
+            ib_seek(B, base, ++p);
+            continue;
+        }
+        if (n >= cap) {
+            o.ovf = true;
+            break;
+        }
+        pos[n] = (uint16_t)(p - s);
+        tok[n++] = t;
+        p = ib_pos(B, base);
+        if (t == TK_EOB) {
+            if (o.ne == 0) { o.e0i = n - 1; o.e0p = p; }
+            o.ne++;
+        }
+    }
+    o.end = p;
+    o.n = n;
+    return o;
+}
+
+// sync of lane k >= 1: the true stream from `start` (where the previous lane's true tokens end) until it meets one of
+// the lane's phase-A token starts.  The lane's true tokens: redo[0, r) then its phase-A tokens [i, n).  end: where they
+// end (phase A's end when they met, else the redo's).  eob >= 0: the true list's end-of-block token at that index (eobp:
+// the bit after it).  fail: more than PAR_RCAP redo tokens, or no valid token on the true stream.
+struct SyncOut {
+    uint32_t i, r, end, eobp;
+    int32_t eob;
+    bool fail;
+};
+__host__ __device__ __forceinline__ SyncOut resync(IBits &B, const uint8_t *base, uint32_t s, uint32_t start, uint32_t stop,
+                                                   const SegOut &so, const uint32_t *tok, const uint16_t *pos, const Tabs &T,
+                                                   uint32_t *redo) {
+    SyncOut y{};
+    y.eob = -1;
+    uint32_t cur = start, ii = 0, r = 0;
+    bool seeked = false;
+    for (;;) {
+        while (ii < so.n && s + pos[ii] < cur) ii++;
+        if (ii < so.n && s + pos[ii] == cur) break;                // met: the rest of phase A's tokens are true
+        if (cur >= stop) {                                          // never met: the redo is the lane's whole list
+            y.i = so.n;
+            y.r = r;
+            y.end = cur;
+            return y;
+        }
+        if (r == PAR_RCAP) { y.fail = true; return y; }
+        if (!seeked) {
+            ib_seek(B, base, cur);
+            seeked = true;
+        }
+        uint32_t t;
+        if (!next_token(B, T, t)) { y.fail = true; return y; }
+        redo[r++] = t;
+        cur = ib_pos(B, base);
+        if (t == TK_EOB) {
+            y.eob = (int32_t)(r - 1);
+            y.eobp = cur;
+            y.i = so.n;
+            y.r = r;
+            y.end = cur;
+            return y;
+        }
+    }
+    y.i = ii;
+    y.r = r;
+    y.end = so.end;
+    // the first end-of-block token among phase A's from index ii on
+    if (so.ne && so.e0i >= ii) {
+        y.eob = (int32_t)(r + so.e0i - ii);
+        y.eobp = so.e0p;
+    } else if (so.ne > 1) {                                         // (rare: an end of block in the lane's garbage prefix)
+        for (uint32_t j = ii; j < so.n; j++)
+            if (tok[j] == TK_EOB) {
+                y.eob = (int32_t)(r + j - ii);
+                y.eobp = j + 1 < so.n ? s + pos[j + 1] : so.end;
+                break;
+            }
+    }
+    return y;
+}
+
+// lane 0 starts on the true stream: its list is its phase-A tokens
+__host__ __device__ __forceinline__ SyncOut sync_lane0(const SegOut &so) {
+    SyncOut y{};
+    y.eob = -1;
+    y.end = so.end;
+    if (so.ne) {
+        y.eob = (int32_t)so.e0i;
+        y.eobp = so.e0p;
+    }
+    return y;
+}
+
+// The same algorithm on the host, lane after lane, with a plain sequential resolve (tests/test_inflate_check.py: the
+// token lists against zlib, and how often a member would fall back).  stats[0] members inflated, [1] token overflow,
+// [2] no sync, [3] stored block, [4] bad header, [5] no end of block, [6] bad resolve, [7] redo tokens, [8] blocks,
+// [9] sync rounds beyond the first.
+__host__ uint32_t par_member_host(const uint8_t *comp, const spg_bgzf_member &M, uint8_t *out, uint8_t *slice,
+                                  uint64_t *stats, std::vector<uint32_t> &tok, std::vector<uint16_t> &pos,
+                                  std::vector<uint32_t> &redo) {
+    const uint8_t *const base = reinterpret_cast<const uint8_t *>(reinterpret_cast<uintptr_t>(comp + M.coff) & ~(uintptr_t)15);
+    const uint32_t pay0 = (uint32_t)((comp + M.coff) - base) * 8u, dend = pay0 + M.clen * 8u;
+    IBits B;
+    B.end = comp + M.coff + M.clen + 8;
+    tok.assign(par_area(M), 0);
+    pos.assign(par_area(M), 0);
+    redo.assign(64ull * PAR_RCAP, 0);
+    const Tabs T = tabs_of(slice);
+    uint8_t *const o = out + M.uoff;
+    uint32_t w = 0, p = pay0;
+    bool fixed_built = false;
+    int bfinal = 0;
+    auto fb = [&](int why) {
+        stats[why]++;
+        return ST_FALLBACK;
+    };
+    do {
+        ib_seek(B, base, p);
+        bfinal = (int)B.get(1);
+        const uint32_t type = B.get(2);
+        if (type == 0 || type == 3) return fb(3);
+        if (block_tables(B, slice, type, fixed_built) != 0) return fb(4);
+        stats[8]++;
+        const uint32_t d0 = ib_pos(B, base);
+        if (d0 >= dend) return fb(4);
+        const uint32_t K = std::min(64u, std::max(1u, (dend - d0) / PAR_MIN_SEG)), L = (dend - d0 + K - 1) / K;
+        const uint32_t cap = par_area(M) / K;
+        SegOut so[64];
+        SyncOut sy[64];
+        uint32_t used[64];
+        for (uint32_t k = 0; k < K; k++) {
+            const uint32_t s = d0 + k * L, stop = k + 1 == K ? dend : s + L;
+            IBits Bk = B;
+            so[k] = decode_seg(Bk, base, s, stop, T, &tok[k * cap], &pos[k * cap], cap);
+            sy[k] = sync_lane0(so[k]);
+            used[k] = s;                                            // (the start lane k's list was synchronised from)
+        }
+        // rounds: a lane whose predecessor's end moved synchronises again
+        for (int round = 0;; round++) {
+            bool any = false;
+            for (uint32_t k = 1; k < K; k++) {
+                if (sy[k - 1].end == used[k]) continue;
+                any = true;
+                const uint32_t s = d0 + k * L, stop = k + 1 == K ? dend : s + L;
+                IBits Bk = B;
+                used[k] = sy[k - 1].end;
+                sy[k] = resync(Bk, base, s, used[k], stop, so[k], &tok[k * cap], &pos[k * cap], T, &redo[k * PAR_RCAP]);
+                stats[7] += sy[k].r;
+            }
+            if (!any) break;
+            if (round) stats[9]++;
+        }
+        int kend = -1;
+        for (uint32_t k = 0; k < K; k++) {
+            if (so[k].ovf) return fb(1);
+            if (sy[k].fail) return fb(2);
+            if (sy[k].eob >= 0) {
+                kend = (int)k;
+                break;
+            }
+        }
+        if (kend < 0) return fb(5);
+        for (int k = 0; k <= kend; k++) {
+            const uint32_t c = k == kend ? (uint32_t)sy[k].eob : sy[k].r + so[k].n - sy[k].i;
+            for (uint32_t g = 0; g < c; g++) {
+                const uint32_t t = g < sy[k].r ? redo[k * PAR_RCAP + g] : tok[k * cap + sy[k].i + g - sy[k].r];
+                if (!(t & TK_MATCH)) {
+                    if (w >= M.ulen) return fb(6);
+                    o[w++] = (uint8_t)t;
+                    continue;
+                }
+                const uint32_t len = ((t >> 16) & 255u) + 3u, dist = (t & 0x7FFFu) + 1u;
+                if (dist > w || w + len > M.ulen) return fb(6);
+                for (uint32_t q = 0; q < len; q++, w++) o[w] = o[w - dist];
+            }
+        }
+        p = sy[kend].eobp;
+    } while (!bfinal);
+    if (w != M.ulen) return fb(6);
+    stats[0]++;
+    return 0;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)v, d, 64);
+        if (lane >= d) v += t;
+    }
+    return v;
+}
+
+#if defined(SPG_INFLATE_PROF)          // (A/B builds: k_inflate_par's phase cycles summed over members, spg_bgzf_prof)
+__device__ unsigned long long g_inf_prof[8];
+#define PAR_PROF_T(v) const uint64_t v = clock64()
+#define PAR_PROF_ADD(i, x) do { if (lane == 0) atomicAdd(&g_inf_prof[i], (unsigned long long)(x)); } while (0)
+#else
+#define PAR_PROF_T(v)
+#define PAR_PROF_ADD(i, x)
+#endif
+
+__device__ __forceinline__ uint32_t ring_slot(uint32_t g0, uint32_t x) {   // (g0 + x) mod PAR_RING, g0 + x < 3 PAR_RING
+    uint32_t y = g0 + x;
+    y = y >= PAR_RING ? y - PAR_RING : y;
+    return y >= PAR_RING ? y - PAR_RING : y;
+}
+
+__global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
+                                                    int64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ status,
+                                                    uint32_t *__restrict__ scr_tok, uint16_t *__restrict__ scr_pos,
+                                                    uint32_t *__restrict__ scr_redo, uint32_t *__restrict__ n_fallback) {
     __shared__ __align__(16) uint8_t slice[SLICE];
+    __shared__ __align__(16) uint8_t ring[PAR_RING];
+    __shared__ uint32_t boff[64];
     const int64_t m = blockIdx.x;
     if (m >= n) return;
     const int lane = threadIdx.x;
-    uint16_t *const litp = reinterpret_cast<uint16_t *>(slice + SL_LITP);
-    uint16_t *const distp = reinterpret_cast<uint16_t *>(slice + SL_DISTP);
-    uint16_t *const lcnt = reinterpret_cast<uint16_t *>(slice + SL_LCNT);
-    uint16_t *const dcnt = reinterpret_cast<uint16_t *>(slice + SL_DCNT);
-    uint16_t *const lsym = reinterpret_cast<uint16_t *>(slice + SL_LSYM);
-    uint16_t *const dsym = reinterpret_cast<uint16_t *>(slice + SL_DSYM);
-    uint8_t *const lens = slice + SL_LENS;
     const spg_bgzf_member M = mem[m];
-    const uint64_t base = M.coff & ~15ull;
-    WaveIn in;
-    in.g = comp + base;
-    in.gmax = comp_bytes + 64 > base ? comp_bytes + 64 - base : 0;   // (the buffer is padded by 64 bytes)
-    in.ring = inr;
-    in.lane = lane;
-    in.reset(0);
-    WBits B;
-    B.in = &in;
-    const uint32_t cend = (uint32_t)(M.coff + M.clen - base);
-    B.end = cend + 8;
-    B.start((uint32_t)(M.coff - base));
-    uint8_t *const o = out + M.uoff;
+    const uint8_t *const base = comp + (M.coff & ~15ull);
+    const uint32_t pay0 = (uint32_t)(M.coff & 15ull) * 8u, dend = pay0 + M.clen * 8u;
+    IBits B;
+    B.end = comp + M.coff + M.clen + 8;
+    uint32_t *const tok0 = scr_tok + par_tok_at(M, (uint64_t)m);                // lane k's list: tok0 + k cap
+    uint16_t *const pos0 = scr_pos + par_tok_at(M, (uint64_t)m);
+    uint32_t *const redo0 = scr_redo + (uint64_t)m * 64u * PAR_RCAP;            // lane k's redo: redo0 + k RCAP
+    const Tabs T = tabs_of(slice);
     const uint32_t ulen = M.ulen;
-    uint32_t w = 0, flushed = 0, st = 0;
-    int bfinal = 0;
+    const uint64_t gbeg = M.uoff;                                               // the member's first global output byte
+    const uint32_t g0 = (uint32_t)(gbeg % PAR_RING);
+    uint32_t w = 0, flushed = 0, p = pay0, st = 0;
     bool fixed_built = false;
-    // the window's completed 1 KiB blocks to global memory (coalesced bytes: lane j writes bytes j, j + 64, ...)
-    auto flush_to = [&](uint32_t upto) {
-        while (flushed + W_HALF <= upto || (upto == ulen && flushed < upto)) {
-            const uint32_t e = min(flushed + (uint32_t)W_HALF, upto);
-            for (uint32_t p = flushed + (uint32_t)lane; p < e; p += 64) o[p] = win[p & (W_WIN - 1)];
-            flushed = e;
+    int bfinal = 0;
+
+    // global bytes [flushed, upto) of the member from the ring: whole 16-byte aligned chunks of global memory per lane,
+    // one aligned 1 KiB block of global memory per pass
+    auto flush = [&](uint32_t upto) {
+        while (flushed < upto) {
+            const uint64_t ga = gbeg + flushed;
+            const uint64_t blk = ga & ~1023ull;
+            const uint32_t bend = (uint32_t)min((uint64_t)upto, blk + 1024 - gbeg);    // member coordinates
+            const uint64_t c = blk + 16ull * (uint64_t)lane;                          // this lane's chunk (global)
+            const uint64_t lo = max(c, ga), hi = min(c + 16, gbeg + bend);
+            if (lo == c && hi == c + 16) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(ring + (uint32_t)(c % PAR_RING));
+                *reinterpret_cast<uint4 *>(out + c) = v;
+            } else {
+                for (uint64_t x = lo; x < hi; x++) out[x] = ring[(uint32_t)(x % PAR_RING)];
+            }
+            flushed = bend;
         }
     };
+
+    PAR_PROF_T(t_beg);
     do {
+        PAR_PROF_T(t_h0);
+        ib_seek(B, base, p);
         bfinal = (int)B.get(1);
         const uint32_t type = B.get(2);
-        if (type == 0) {                                 // stored: LEN bytes straight from the compressed stream
-            B.drop(B.n & 7);
-            const uint32_t ln = B.get(16), nl = B.get(16);
-            if ((ln ^ 0xFFFFu) != nl) { st = 2; break; }
-            const uint32_t src = B.byte_pos();
-            if (w + ln > ulen) { st = 7; break; }
-            if (src + ln > cend) { st = 8; break; }
-            typedef __attribute__((address_space(1))) const uint8_t gu8;
-            for (uint32_t i0 = 0; i0 < ln; i0 += W_HALF) {     // (1 KiB at a time: the window ring holds 32 KiB)
-                const uint32_t e = min(ln, i0 + (uint32_t)W_HALF);
-                wave_lds_sync();
-                for (uint32_t i = i0 + (uint32_t)lane; i < e; i += 64) win[(w + i - i0) & (W_WIN - 1)] = ((gu8 *)(in.g))[src + i];
-                w += e - i0;
-                wave_lds_sync();
-                flush_to(w);
-            }
-            in.reset(src + ln);
-            B.start(src + ln);
-            continue;
+        if (type == 0 || type == 3) { st = ST_FALLBACK; break; }
+        // (every lane reads the same header and writes the same tables)
+        const uint32_t hs = block_tables(B, slice, type, fixed_built);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (hs != 0) { st = ST_FALLBACK; break; }
+        const uint32_t d0 = ib_pos(B, base);
+        if (d0 >= dend) { st = ST_FALLBACK; break; }
+        const uint32_t K = min(64u, max(1u, (dend - d0) / PAR_MIN_SEG)), L = (dend - d0 + K - 1) / K;
+        const uint32_t cap = par_area(M) / K;
+        const uint32_t s = d0 + (uint32_t)lane * L, stop = (uint32_t)lane + 1 == K ? dend : s + L;
+        uint32_t *const tokl = tok0 + (uint64_t)lane * cap;
+        uint16_t *const posl = pos0 + (uint64_t)lane * cap;
+        SegOut so{};
+        SyncOut sy{};
+        sy.eob = -1;
+        PAR_PROF_T(t_a0);
+        PAR_PROF_ADD(0, t_a0 - t_h0);
+        if ((uint32_t)lane < K) {
+            so = decode_seg(B, base, s, stop, T, tokl, posl, cap);
+            sy = sync_lane0(so);
         }
-        if (type == 1) {
-            if (!fixed_built) {
-                if (lane == 0) {
-                    for (int s2 = 0; s2 < 288; s2++) lens[s2] = s2 < 144 ? 8 : s2 < 256 ? 9 : s2 < 280 ? 7 : 8;
-                    build(litp, lcnt, lsym, lens, 288, IB_LIT);
-                    for (int s2 = 0; s2 < 32; s2++) lens[s2] = 5;
-                    build(distp, dcnt, dsym, lens, 32, IB_DIST);
-                }
-                wave_lds_sync();
-                fixed_built = true;
+        __builtin_amdgcn_wave_barrier();
+        PAR_PROF_T(t_s0);
+        PAR_PROF_ADD(1, t_s0 - t_a0);
+        // sync rounds: a lane whose predecessor's true tokens end elsewhere than where it last synchronised from runs again
+        // (the first round: every lane but 0; later rounds only behind a lane that never met its own phase-A tokens)
+        uint32_t used = s;
+        for (;;) {
+            const uint32_t eprev = (uint32_t)__shfl_up((int)sy.end, 1, 64);
+            const bool again = lane >= 1 && (uint32_t)lane < K && eprev != used;
+            if (!__ballot(again)) break;
+            if (again) {
+                used = eprev;
+                sy = resync(B, base, s, used, stop, so, tokl, posl, T, redo0 + (uint32_t)lane * PAR_RCAP);
             }
-        } else if (type == 2) {
-            fixed_built = false;
-            const int hlit = (int)B.get(5) + 257, hdist = (int)B.get(5) + 1, hclen = (int)B.get(4) + 4;
-            uint8_t *const cl = lens;
-            uint32_t clv[19];
-            for (int i = 0; i < 19; i++) clv[i] = 0;
-            for (int i = 0; i < hclen; i++) {
-                const int ord = i < 3 ? 16 + i : i == 3 ? 0 : (i & 1) ? 7 - (i - 5) / 2 : 8 + (i - 4) / 2;
-                clv[ord] = B.get(3);
-            }
-            bool ok = true;
-            if (lane == 0) {
-                for (int i = 0; i < 19; i++) cl[i] = (uint8_t)clv[i];
-                ok = build(litp, dcnt, dsym, cl, 19, IB_CL);
-            }
-            wave_lds_sync();
-            if (!__builtin_amdgcn_readfirstlane((int)ok)) { st = 3; break; }
-            int k = 0;
-            while (k < hlit + hdist) {
-                B.fill();
-                const int s2 = decode_w(B, litp, dcnt, dsym, IB_CL);
-                if (s2 < 0) { st = 3; break; }
-                if (s2 < 16) { if (lane == 0) lens[k] = (uint8_t)s2; k++; continue; }
-                int rep;
-                uint8_t v = 0;
-                if (s2 == 16) {
-                    if (k == 0) { st = 3; break; }
-                    wave_lds_sync();
-                    v = lens[k - 1];
-                    rep = 3 + (int)B.get(2);
-                } else if (s2 == 17) {
-                    rep = 3 + (int)B.get(3);
-                } else {
-                    rep = 11 + (int)B.get(7);
-                }
-                if (k + rep > hlit + hdist) { st = 3; break; }
-                if (lane == 0)
-                    for (int r2 = 0; r2 < rep; r2++) lens[k + r2] = v;
-                k += rep;
-            }
-            if (st) break;
-            wave_lds_sync();
-            bool ok2 = lens[256] != 0;
-            if (lane == 0 && ok2)
-                ok2 = build(distp, dcnt, dsym, lens + hlit, hdist, IB_DIST) && build(litp, lcnt, lsym, lens, hlit, IB_LIT);
-            wave_lds_sync();
-            if (!__builtin_amdgcn_readfirstlane((int)ok2)) { st = lens[256] == 0 ? 3 : 4; break; }
-        } else {
-            st = 1;
-            break;
+            PAR_PROF_ADD(7, 1);
         }
-        while (true) {                                   // the block's codes
-            B.fill();
-            const int s2 = decode_w(B, litp, lcnt, lsym, IB_LIT);
-            if (s2 < 256) {
-                if (s2 < 0) { st = 5; break; }
-                if (w >= ulen) { st = 7; break; }
-                if (lane == 0) win[w & (W_WIN - 1)] = (uint8_t)s2;
-                w++;
-                if ((w & (W_HALF - 1)) == 0) { wave_lds_sync(); flush_to(w); }
-                continue;
+        __builtin_amdgcn_wave_barrier();
+        PAR_PROF_T(t_b0);
+        PAR_PROF_ADD(2, t_b0 - t_s0);
+        PAR_PROF_ADD(5, 1);
+        const bool bad = (uint32_t)lane < K && (so.ovf || sy.fail);
+        const uint64_t badm = __ballot(bad), eobm = __ballot((uint32_t)lane < K && sy.eob >= 0);
+        // a lane past the first lane with an end of block decoded another block: only lanes up to it count
+        const int kend = eobm ? __builtin_ctzll(eobm) : 64;
+        if (kend == 64 || (badm & ((kend == 63 ? ~0ull : (2ull << kend) - 1)))) { st = ST_FALLBACK; break; }
+        const uint32_t cnt = lane < kend ? sy.r + so.n - sy.i : lane == kend ? (uint32_t)sy.eob : 0u;
+        const uint32_t pnext = (uint32_t)__builtin_amdgcn_readlane((int)sy.eobp, kend);
+        // phase-A tokens and redo tokens were written by other lanes: visible to every lane from here
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+
+        // ---- phase B: the true token lists of lanes 0 .. kend, in order
+        for (int k = 0; k <= kend && !st; k++) {
+            const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cnt, k);
+            const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)sy.r, k);
+            const uint32_t i0 = (uint32_t)__builtin_amdgcn_readlane((int)sy.i, k);
+            const uint32_t *const tl = tok0 + (int64_t)k * cap + (int64_t)i0 - (int64_t)r;   // (g >= r: tl[g])
+            const uint32_t *const rl = redo0 + (uint32_t)k * PAR_RCAP;
+            auto load = [&](uint32_t g) -> uint32_t { return g < c ? (g < r ? rl[g] : tl[g]) : 0u; };
+            uint32_t t0 = 0, nxt = load((uint32_t)lane);
+            while (t0 < c) {
+                const bool valid = t0 + (uint32_t)lane < c;
+                const uint32_t tk = nxt;
+                const bool isM = (tk & TK_MATCH) != 0;
+                const uint32_t len = valid ? (isM ? ((tk >> 16) & 255u) + 3u : 1u) : 0u;
+                const uint32_t dist = (tk & 0x7FFFu) + 1u;
+                const uint32_t incl = wave_incl_scan(len, lane);
+                const bool in = valid && incl <= PAR_BATCH;
+                const uint64_t inm = __ballot(in);
+                const uint32_t nb = (uint32_t)__builtin_popcountll(inm);                 // (a prefix of the lanes)
+                const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, (int)nb - 1);
+                const uint32_t t1 = t0 + nb;
+                nxt = load(t1 + (uint32_t)lane);                                         // the next batch, in flight
+                const uint32_t excl = incl - len, o = w + excl;
+                if (__ballot(in && isM && dist > o) || w + total > ulen) { st = ST_FALLBACK; break; }
+                boff[lane] = excl;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t sb = o - dist;                                            // a match's source start
+                bool ready = in && (!isM || sb + min(len, dist) <= w);
+                bool pend = in;
+                uint32_t a = 0;                                                          // first token of the source
+                if (in && !ready) {
+                    const uint32_t rel = sb > w ? sb - w : 0u;
+                    uint32_t lo = 0, hi = nb;
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (boff[mid] <= rel) lo = mid; else hi = mid;
+                    }
+                    a = lo;
+                }
+                uint64_t done = 0;
+                for (;;) {
+                    const uint64_t rm = __ballot(ready);
+                    if (!rm) { st = ST_FALLBACK; break; }
+                    if (ready && len <= 32) {
+                        if (!isM) {
+                            ring[ring_slot(g0, o)] = (uint8_t)tk;
+                        } else {
+                            uint32_t mq = 0;
+                            for (uint32_t q = 0; q < len; q += 4) {
+                                uint8_t v[4];
+#pragma unroll
+                                for (int u = 0; u < 4; u++) {
+                                    v[u] = q + u < len ? ring[ring_slot(g0, sb + mq)] : 0;
+                                    mq = mq + 1 == dist ? 0 : mq + 1;
+                                }
+#pragma unroll
+                                for (int u = 0; u < 4; u++)
+                                    if (q + u < len) ring[ring_slot(g0, o + q + u)] = v[u];
+                            }
+                        }
+                    }
+                    uint64_t lm = __ballot(ready && len > 32);
+                    while (lm) {                                                         // long matches: the whole wave
+                        const int j = __builtin_ctzll(lm);
+                        lm &= lm - 1;
+                        const uint32_t oj = (uint32_t)__builtin_amdgcn_readlane((int)o, j);
+                        const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)len, j);
+                        const uint32_t dj = (uint32_t)__builtin_amdgcn_readlane((int)dist, j);
+                        for (uint32_t q0 = 0; q0 < lj; q0 += 64) {
+                            const uint32_t q = q0 + (uint32_t)lane;
+                            uint8_t v = 0;
+                            if (q < lj) v = ring[ring_slot(g0, oj - dj + (dj >= lj ? q : q % dj))];
+                            if (q < lj) ring[ring_slot(g0, oj + q)] = v;
+                        }
+                    }
+                    done |= rm;
+                    pend = pend && !ready;
+                    if (!__ballot(pend)) break;
+                    const uint64_t need = ((1ull << lane) - 1) & ~((1ull << a) - 1);
+                    ready = pend && (done & need) == need;
+                }
+                if (st) break;
+                PAR_PROF_ADD(6, 1);
+                w += total;
+                t0 = t1;
+                const uint64_t gb = (gbeg + w) & ~1023ull;    // whole global blocks only; the rest stays in the ring
+                if (gb > gbeg + flushed) flush((uint32_t)(gb - gbeg));
             }
-            if (s2 == 256) break;
-            if (s2 > 285) { st = 5; break; }
-            B.fill();
-            const uint32_t len = len_base(s2 - 257) + B.peek((int)len_ext(s2 - 257));
-            B.drop((int)len_ext(s2 - 257));
-            const int ds = decode_w(B, distp, dcnt, dsym, IB_DIST);
-            if (ds < 0 || ds > 29) { st = 5; break; }
-            const uint32_t dist = dist_base(ds) + B.get((int)dist_ext(ds));
-            if (dist > w) { st = 6; break; }
-            if (w + len > ulen) { st = 7; break; }
-            wave_lds_sync();                             // (literals lane 0 wrote since the last sync)
-            // lanes copy bytes j = lane, lane + 64, ...: byte j of the match is the source's byte j mod dist
-            for (uint32_t j0 = 0; j0 < len; j0 += 64) {
-                const uint32_t j = j0 + (uint32_t)lane;
-                uint8_t v = 0;
-                if (j < len) v = win[(w - dist + (dist >= len ? j : j % dist)) & (W_WIN - 1)];
-                if (j < len) win[(w + j) & (W_WIN - 1)] = v;
-            }
-            const uint32_t w0 = w;
-            w += len;
-            if ((w0 >> 10) != (w >> 10)) { wave_lds_sync(); flush_to(w); }
         }
         if (st) break;
-        if (B.byte_pos() > cend) { st = 8; break; }
+        p = pnext;
+        PAR_PROF_T(t_b1);
+        PAR_PROF_ADD(3, t_b1 - t_b0);
     } while (!bfinal);
-    if (!st && w != ulen) st = 9;
-    if (!st) {
-        wave_lds_sync();
-        flush_to(ulen);
+    if (!st && w != ulen) st = ST_FALLBACK;
+    if (!st) flush(ulen);
+    PAR_PROF_T(t_end);
+    PAR_PROF_ADD(4, t_end - t_beg);
+    if (lane == 0) {
+        status[m] = st;
+        if (st) atomicAdd(n_fallback, 1u);
     }
-    if (lane == 0) status[m] = st;
 }
 
 // CRC-32 (zlib's reflected polynomial) arithmetic: a * b mod P and x^(8 n) mod P, as zlib's multmodp / x2nmodp
@@ -782,18 +1008,37 @@ static uint32_t host_crc_x8n(uint32_t n) {
     return r;
 }
 
+// scratch of launch_inflate: the fallback counter, per member the parallel kernel's redo tokens (64 KiB), its token lists
+// (u32) and their start positions (u16): 2 clen + 2048 each (par_area)
+size_t inflate_scratch_bytes(uint64_t comp_bytes, int64_t n) {
+    return 256 + 4 * (size_t)n * 64 * PAR_RCAP + 6 * (2 * (size_t)comp_bytes + 2048 * (size_t)n + 64);
+}
+
+// k_inflate_par over every member, the lane kernel over the members it left (status ST_FALLBACK), then every member's
+// CRC32.  *fallbacks (device u32 at the start of scratch): members the lane kernel inflated.
 hipError_t launch_inflate(const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *mem, int64_t n, uint8_t *out,
-                          uint32_t *status, hipStream_t st) {
+                          uint32_t *status, void *scratch, hipStream_t st) {
     if (n <= 0) return hipSuccess;
-#if defined(SPG_INFLATE_WAVE)        // (A/B builds: one member per wave, its window in LDS — r05c: 73.7 ms vs 27.0 on the
-                                     // 10,000x BAM: 4 members per CU leave the decode's dependent chain exposed)
-    hipLaunchKernelGGL(k_inflate_w, dim3((unsigned)n), dim3(64), 0, st, comp, comp_bytes, mem, n, out, status);
+    uint32_t *const cnt = static_cast<uint32_t *>(scratch);
+    uint32_t *const redo = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(scratch) + 256);
+    uint32_t *const tok = redo + (size_t)n * 64 * PAR_RCAP;
+    uint16_t *const pos = reinterpret_cast<uint16_t *>(tok + 2 * (size_t)comp_bytes + 2048 * (size_t)n + 64);
+    hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+#if defined(SPG_INFLATE_LANE)        // (A/B builds: every member on the lane kernel)
+    (void)comp_bytes;
+    (void)redo;
+    (void)tok;
+    (void)pos;
+    hipLaunchKernelGGL(k_inflate, dim3((unsigned)((n + INFLATE_MPW - 1) / INFLATE_MPW)), dim3(64),
+                       (size_t)INFLATE_MPW * SLICE, st, comp, mem, n, out, status, INFLATE_MPW, 0);
 #else
     (void)comp_bytes;
+    hipLaunchKernelGGL(k_inflate_par, dim3((unsigned)n), dim3(64), 0, st, comp, mem, n, out, status, tok, pos, redo, cnt);
     hipLaunchKernelGGL(k_inflate, dim3((unsigned)((n + INFLATE_MPW - 1) / INFLATE_MPW)), dim3(64),
-                       (size_t)INFLATE_MPW * SLICE, st, comp, mem, n, out, status, INFLATE_MPW);
+                       (size_t)INFLATE_MPW * SLICE, st, comp, mem, n, out, status, INFLATE_MPW, 1);
 #endif
-    hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     if (e != hipSuccess) return e;
     static const uint32_t op1k = host_crc_x8n(1024);
     hipLaunchKernelGGL(k_crc32, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, comp, mem, n, (const uint8_t *)out, status,
@@ -814,15 +1059,17 @@ hipError_t launch_inflate(const uint8_t *comp, uint64_t comp_bytes, const spg_bg
 
 namespace {
 struct InflateDev {
+    std::mutex mu;                // one caller per device at a time (the device's scratch buffers are shared)
     hipStream_t st = nullptr;
-    uint8_t *comp = nullptr, *out = nullptr;
-    size_t comp_cap = 0, out_cap = 0, mem_bytes = 0, status_bytes = 0;
+    uint8_t *comp = nullptr, *out = nullptr, *scr = nullptr;
+    size_t comp_cap = 0, out_cap = 0, mem_bytes = 0, status_bytes = 0, scr_cap = 0;
     spg_bgzf_member *mem = nullptr;
     uint32_t *status = nullptr;
     hipEvent_t ev[2] = {nullptr, nullptr};
+    int64_t fallbacks = 0;        // the last call's members the parallel kernel left to the lane kernel
 };
-std::mutex g_inf_mu;
-std::vector<InflateDev> g_inf;
+constexpr int MAX_INF_DEV = 64;
+InflateDev g_inf[MAX_INF_DEV];
 thread_local std::string g_inf_err;
 int ifail(const std::string &m) { g_inf_err = m; return -1; }
 #define ICHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return ifail(std::string("spg_bgzf_inflate: ") + #x + ": " + hipGetErrorString(e_)); } while (0)
@@ -839,6 +1086,45 @@ template <class T> int grow(T *&p, size_t &cap, size_t need) {
 
 extern "C" {
 const char *spg_bgzf_last_error(void) { return g_inf_err.c_str(); }
+
+// The parallel inflater's algorithm on the host (k_inflate_par's phase A / sync functions lane after lane, a sequential
+// resolve): status 0 or 100 (left to the lane kernel); stats[10] as spg::par_member_host (CPU tests)
+int spg_bgzf_inflate_par_check(const uint8_t *comp, size_t comp_bytes, const spg_bgzf_member *members, int64_t n,
+                               uint8_t *out, size_t out_bytes, uint32_t *status, uint64_t *stats) {
+    if (n < 0 || !stats || (n && (!comp || !members || !out || !status))) return ifail("spg_bgzf_inflate_par_check: bad argument");
+    for (int64_t i = 0; i < n; i++) {
+        const spg_bgzf_member &m = members[i];
+        if (m.coff + m.clen + 8 > comp_bytes || m.uoff + m.ulen > out_bytes || m.ulen > 65536)
+            return ifail("spg_bgzf_inflate_par_check: member " + std::to_string(i) + " outside the buffers");
+    }
+    std::vector<uint64_t> padded((comp_bytes + 64) / 8 + 1, 0);
+    std::memcpy(padded.data(), comp, comp_bytes);
+    std::vector<uint64_t> slice(spg::SLICE / 8);
+    std::vector<uint32_t> tok, redo;
+    std::vector<uint16_t> pos;
+    for (int k = 0; k < 10; k++) stats[k] = 0;
+    for (int64_t i = 0; i < n; i++)
+        status[i] = spg::par_member_host(reinterpret_cast<const uint8_t *>(padded.data()), members[i], out,
+                                         reinterpret_cast<uint8_t *>(slice.data()), stats, tok, pos, redo);
+    return 0;
+}
+
+#if defined(SPG_INFLATE_PROF)
+// (A/B builds) k_inflate_par's summed phase cycles since the last call: header + tables, phase A, sync, phase B, total,
+// blocks, batches, sync rounds
+extern "C" int spg_bgzf_prof(uint64_t *out8) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(spg::g_inf_prof), 8 * sizeof(uint64_t)) != hipSuccess) return -1;
+    static const uint64_t zero[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(spg::g_inf_prof), zero, sizeof zero) == hipSuccess ? 0 : -1;
+}
+#endif
+
+int spg_bgzf_fallbacks(int device, int64_t *n) {
+    if (!n || device < 0 || device >= MAX_INF_DEV) return ifail("spg_bgzf_fallbacks: bad argument");
+    std::lock_guard<std::mutex> lk(g_inf[device].mu);
+    *n = g_inf[device].fallbacks;
+    return 0;
+}
 
 // The device decoder compiled for the host, member by member (CPU tests of its logic; the product inflates on the GPU)
 int spg_bgzf_inflate_check(const uint8_t *comp, size_t comp_bytes, const spg_bgzf_member *members, int64_t n,
@@ -870,13 +1156,12 @@ int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const s
     if (kernel_ms) *kernel_ms = 0.f;
     if (n == 0) return 0;
     // one caller per device at a time (the device's scratch buffers are shared); the caller's current device is restored
-    std::lock_guard<std::mutex> lk(g_inf_mu);
     int prev = 0, nd = 0;
     ICHK(hipGetDevice(&prev));
     ICHK(hipGetDeviceCount(&nd));
-    if (device < 0 || device >= nd) return ifail("spg_bgzf_inflate: bad device");
-    if ((int)g_inf.size() < nd) g_inf.resize((size_t)nd);
-    InflateDev &D = g_inf[(size_t)device];
+    if (device < 0 || device >= nd || device >= MAX_INF_DEV) return ifail("spg_bgzf_inflate: bad device");
+    InflateDev &D = g_inf[device];
+    std::lock_guard<std::mutex> lk(D.mu);
     struct Restore { int d; ~Restore() { (void)hipSetDevice(d); } } restore{prev};
     ICHK(hipSetDevice(device));
     if (!D.st) {
@@ -886,7 +1171,8 @@ int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const s
     }
     if (grow(D.comp, D.comp_cap, comp_bytes + 64) || grow(D.out, D.out_cap, out_bytes + 64) ||
         grow(D.mem, D.mem_bytes, (size_t)n * sizeof(spg_bgzf_member)) ||
-        grow(D.status, D.status_bytes, (size_t)n * sizeof(uint32_t)))
+        grow(D.status, D.status_bytes, (size_t)n * sizeof(uint32_t)) ||
+        grow(D.scr, D.scr_cap, spg::inflate_scratch_bytes(comp_bytes, n)))
         return ifail("spg_bgzf_inflate: out of device memory");
     // after the first enqueue every failure drains the stream before returning: the caller's `out` may be the target of a
     // queued copy, and it inflates failed members into it next
@@ -896,38 +1182,41 @@ int spg_bgzf_inflate(int device, const uint8_t *comp, size_t comp_bytes, const s
     IQ(hipMemsetAsync(D.comp + comp_bytes, 0, 64, D.st));
     IQ(hipMemcpyAsync(D.mem, members, (size_t)n * sizeof(spg_bgzf_member), hipMemcpyHostToDevice, D.st));
     IQ(hipEventRecord(D.ev[0], D.st));
-    IQ(spg::launch_inflate(D.comp, comp_bytes, D.mem, n, D.out, D.status, D.st));
+    IQ(spg::launch_inflate(D.comp, comp_bytes, D.mem, n, D.out, D.status, D.scr, D.st));
     IQ(hipEventRecord(D.ev[1], D.st));
+    uint32_t fbk = 0;
     IQ(hipMemcpyAsync(out, D.out, out_bytes, hipMemcpyDeviceToHost, D.st));
     IQ(hipMemcpyAsync(status, D.status, sizeof(uint32_t) * (size_t)n, hipMemcpyDeviceToHost, D.st));
+    IQ(hipMemcpyAsync(&fbk, D.scr, sizeof(uint32_t), hipMemcpyDeviceToHost, D.st));
     IQ(hipStreamSynchronize(D.st));
 #undef IQ
+    D.fallbacks = fbk;
     if (kernel_ms && hipEventElapsedTime(kernel_ms, D.ev[0], D.ev[1]) != hipSuccess) *kernel_ms = -1.f;   // (timing only)
     // (the scratch only grows; after a BAM above 2 GiB inflated it is given back rather than held in HBM)
     if (D.out_cap > ((size_t)2 << 30)) {
-        for (void *p : {(void *)D.comp, (void *)D.out}) (void)hipFree(p);
-        D.comp = D.out = nullptr;
-        D.comp_cap = D.out_cap = 0;
+        for (void *p : {(void *)D.comp, (void *)D.out, (void *)D.scr}) (void)hipFree(p);
+        D.comp = D.out = D.scr = nullptr;
+        D.comp_cap = D.out_cap = D.scr_cap = 0;
     }
     return 0;
 }
 
 // The device's inflate scratch freed (it only grows otherwise: one large BAM would keep its size in HBM)
 int spg_bgzf_release(int device) {
-    std::lock_guard<std::mutex> lk(g_inf_mu);
-    if (device < 0 || (size_t)device >= g_inf.size()) return 0;
-    InflateDev &D = g_inf[(size_t)device];
+    if (device < 0 || device >= MAX_INF_DEV) return 0;
+    InflateDev &D = g_inf[device];
+    std::lock_guard<std::mutex> lk(D.mu);
     if (!D.st) return 0;
     int prev = 0;
     ICHK(hipGetDevice(&prev));
     ICHK(hipSetDevice(device));
     (void)hipStreamSynchronize(D.st);
-    for (void *p : {(void *)D.comp, (void *)D.out, (void *)D.mem, (void *)D.status})
+    for (void *p : {(void *)D.comp, (void *)D.out, (void *)D.mem, (void *)D.status, (void *)D.scr})
         if (p) (void)hipFree(p);
-    D.comp = D.out = nullptr;
+    D.comp = D.out = D.scr = nullptr;
     D.mem = nullptr;
     D.status = nullptr;
-    D.comp_cap = D.out_cap = D.mem_bytes = D.status_bytes = 0;
+    D.comp_cap = D.out_cap = D.mem_bytes = D.status_bytes = D.scr_cap = 0;
     ICHK(hipSetDevice(prev));
     return 0;
 }

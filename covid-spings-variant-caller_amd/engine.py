@@ -242,6 +242,12 @@ class PileupEngine:
         N.check(self._L.spg_bam_inflate_ms(self._h, C.byref(ms)), "spg_bam_inflate_ms")
         return ms.value
 
+    def bam_inflate_fallbacks(self) -> int:
+        """members of the last BAM opened in HBM that the parallel inflater left to the one-lane-per-member decoder"""
+        n = C.c_int64()
+        N.check(self._L.spg_bam_inflate_fallbacks(self._h, C.byref(n)), "spg_bam_inflate_fallbacks")
+        return n.value
+
     def bam_release(self):
         """Free the BAM buffers in HBM (spg_bam_release)."""
         with self._lock:

@@ -317,6 +317,14 @@ int spg_bgzf_release(int device);
  * member's payload, as in a BGZF file). */
 int spg_bgzf_inflate_check(const uint8_t *comp, size_t comp_bytes, const spg_bgzf_member *members, int64_t n,
                            uint8_t *out, size_t out_bytes, uint32_t *status);
+/* The parallel inflater (k_inflate_par: 64 lanes per member, self-synchronising segment decode) run on the host lane
+ * after lane (CPU tests of its algorithm only): status[m] 0, or 100 when the GPU would leave member m to the
+ * one-lane-per-member decoder; stats[10]: members inflated, token overflows, segments that did not synchronise, stored
+ * blocks, bad headers, no end of block, bad resolve, redo tokens, blocks, phase-A tokens before the meeting points. */
+int spg_bgzf_inflate_par_check(const uint8_t *comp, size_t comp_bytes, const spg_bgzf_member *members, int64_t n,
+                               uint8_t *out, size_t out_bytes, uint32_t *status, uint64_t *stats);
+/* Members of the last spg_bgzf_inflate on `device` that the parallel kernel left to the one-lane-per-member decoder. */
+int spg_bgzf_fallbacks(int device, int64_t *n);
 
 /* ---- a BAM kept in HBM (the lone process_bam, live_variant_caller.py:54-72) ---------------------------
  * Only the compressed file goes up and the reads' fixed fields come down: spg_bam_open copies the BGZF bytes to the
@@ -365,6 +373,8 @@ typedef struct spg_bam_plan {
 int spg_bam_accumulate(spg_ctx *ctx, const spg_bam_plan *plan, uint32_t flags);
 /* ms of the last spg_bam_open's inflate + CRC kernels (HIP events) */
 int spg_bam_inflate_ms(spg_ctx *ctx, float *ms);
+/* members of the last spg_bam_open that the parallel inflater left to the one-lane-per-member decoder */
+int spg_bam_inflate_fallbacks(spg_ctx *ctx, int64_t *n);
 /* Free the BAM buffers (the next spg_bam_open allocates them again). */
 int spg_bam_release(spg_ctx *ctx);
 

@@ -29,6 +29,31 @@ def inflate(comp: bytes, members, gpu=True):
     return out[:total].tobytes(), st[:len(members)], ms.value
 
 
+def inflate_par_host(comp: bytes, members):
+    """spg_bgzf_inflate_par_check: the parallel inflater's algorithm run on the host (status 0 or 100 = left to the
+    lane-per-member decoder), and its stats (include/spings_gpu.h)."""
+    from covid_spings_variant_caller_amd import _native as N
+    L = N.gpu_lib()
+    arr = (Member * max(1, len(members)))(*[Member(*m) for m in members])
+    total = sum(m[2] for m in members)
+    out = np.zeros(total + 16, np.uint8)
+    st = np.full(max(1, len(members)), 99, np.uint32)
+    stats = np.zeros(10, np.uint64)
+    cbuf = np.frombuffer(comp, np.uint8)
+    rc = L.spg_bgzf_inflate_par_check(cbuf.ctypes.data, len(comp), C.addressof(arr), len(members), out.ctypes.data,
+                                      total, st.ctypes.data, stats.ctypes.data)
+    assert rc == 0, L.spg_bgzf_last_error()
+    return out[:total].tobytes(), st[:len(members)], stats
+
+
+def fallbacks(device=0):
+    """members of the last spg_bgzf_inflate that the parallel kernel left to the lane-per-member decoder"""
+    from covid_spings_variant_caller_amd import _native as N
+    n = C.c_int64(-1)
+    assert N.gpu_lib().spg_bgzf_fallbacks(device, C.byref(n)) == 0
+    return n.value
+
+
 def pack(payloads):
     """members laid out as in a BGZF file: payload then an 8-byte trailer (CRC32, ISIZE)."""
     comp, members, uoff = bytearray(), [], 0

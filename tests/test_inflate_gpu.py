@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import spings  # noqa: F401
-from inflate_util import all_block_types, bgzf_members, corrupt_set, inflate, pack
+from inflate_util import all_block_types, bgzf_members, corrupt_set, fallbacks, inflate, pack
 
 pytestmark = pytest.mark.gpu
 
@@ -19,6 +19,7 @@ def test_every_block_type_and_strategy_matches_zlib():
     out, st, _ = inflate(comp, members)
     assert (st == 0).all(), [(i, int(s)) for i, s in enumerate(st) if s]
     assert out == b"".join(d for _, d in payloads)
+    assert 0 < fallbacks() < len(members) // 2     # stored blocks and token overflows went to the lane decoder
 
 
 def test_simulated_bam_members_match_gzip(tmp_path):
@@ -33,6 +34,22 @@ def test_simulated_bam_members_match_gzip(tmp_path):
     out, st, _ = inflate(raw, members)
     assert (st == 0).all()
     assert out == gzip.decompress(raw)
+    assert fallbacks() == 0                         # every member went through k_inflate_par
+
+
+def test_simulated_deep_bam_parallel_kernel_only(tmp_path):
+    """A 1,500x BAM (two-block members of 5-6-bit quality codes): k_inflate_par inflates every member itself."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.pileup import simulate_bam
+    ref = synth.reference(6000, seed=3)
+    bam = str(tmp_path / "s.bam")
+    simulate_bam(bam, "NC_045512.2", ref, depth=1500.0, seed=5, n_threads=4)
+    raw = open(bam, "rb").read()
+    members = bgzf_members(raw)
+    out, st, _ = inflate(raw, members)
+    assert (st == 0).all()
+    assert out == gzip.decompress(raw)
+    assert fallbacks() == 0
 
 
 def test_corrupt_members_are_reported():
