@@ -20,20 +20,23 @@
 #define SPG_INFLATE_MATCH_HOOK(dist, len)     // (tools/inflate_stats.cpp: match statistics of a host run)
 #endif
 #ifndef SPG_INFLATE_SLOW_HOOK
-#define SPG_INFLATE_SLOW_HOOK(pb)             // (tools/inflate_stats.cpp: codes longer than the primary table)
+#define SPG_INFLATE_SLOW_HOOK(pb)             // (tools/inflate_stats.cpp: codes longer than the root table)
 #endif
 
 namespace spg {
 
-// Per-member decode tables: one slice of SLICE bytes (LDS on the device: mpw slices per block; a host array in the
-// check).  u16 entries of a primary table are symbol | code length << 9 (0: a longer code or no code); the counts and
-// length-sorted symbols serve the canonical walk for codes longer than the primary table.  The code-length code's
-// tables borrow the literal table's primary area and the distance code's count / symbol areas (it is done with
-// before those codes are built); its 19 code lengths are read into the lengths area.
-constexpr int IB_LIT = 10, IB_DIST = 8, IB_CL = 7;      // primary table bits
-constexpr int SL_LITP = 0, SL_DISTP = 2048, SL_LCNT = 2560, SL_DCNT = 2592, SL_LSYM = 2624, SL_DSYM = 3200,
-              SL_LENS = 3264, SLICE = 3584;
-static_assert(SL_LENS + 320 == SLICE && SL_DSYM + 64 == SL_LENS && SL_LSYM + 576 == SL_DSYM, "slice layout");
+// Per-member decode tables: one slice of SLICE bytes (LDS on the device: one per member; a host array in the check).
+// Two-level tables of u16 entries: a root table indexed by the next pb bits and, for codes longer than pb, sub-tables
+// indexed by the bits after them (zlib's inflate_table layout), so every symbol is one or two lookups — no bit-by-bit
+// walk whose loop would stall a whole wave whenever one lane meets a long code.  Entry: symbol | code length << 9
+// (length 0: no code), or a link 0x8000 | sub-table bits << 11 | sub-table offset.  The counts and sorted symbols are
+// build scratch; the code-length code's table borrows the literal table's area (it is done with before that is built);
+// the code lengths are read into the lengths area.
+constexpr int IB_LIT = 10, IB_DIST = 8, IB_CL = 7;      // root table bits
+constexpr int TAB_LIT = 1536, TAB_DIST = 512;           // entries: root + sub-tables (zlib's bounds for these roots: 1332, 402)
+constexpr int SL_LITP = 0, SL_DISTP = 2 * TAB_LIT, SL_CNT = SL_DISTP + 2 * TAB_DIST, SL_SYM = SL_CNT + 32,
+              SL_LENS = SL_SYM + 576, SLICE = SL_LENS + 320;
+static_assert(SLICE % 8 == 0 && SLICE == 5024, "slice layout");
 
 // The bit stream: a 64-bit buffer refilled 32 bits at a time from a 128-bit reservoir r, which is refilled from the
 // next 16-byte aligned chunk q, loaded one chunk ahead (its address never depends on the bits consumed, so its
@@ -109,13 +112,14 @@ struct IBits {
     __host__ __device__ __forceinline__ const uint8_t *byte_pos() const { return qa - (rn >> 3) - (n >> 3); }
 };
 
-// canonical Huffman tables from code lengths (RFC 1951 3.2.2); false: over-subscribed, or an incomplete code with
-// more than one symbol (a single-code distance alphabet may be incomplete)
-__host__ __device__ __forceinline__ bool build(uint16_t *prim, uint16_t *count, uint16_t *sym, const uint8_t *len, int n,
-                                               int pb) {
+// canonical Huffman tables from code lengths (RFC 1951 3.2.2) into tab (cap entries, root pb bits); false:
+// over-subscribed, an incomplete code with more than one symbol (a single-code distance alphabet may be incomplete), or
+// sub-tables past cap.  count[16] / sym[n]: scratch.
+__host__ __device__ __forceinline__ bool build(uint16_t *tab, int cap, uint16_t *count, uint16_t *sym, const uint8_t *len,
+                                               int n, int pb) {
     for (int i = 0; i < 16; i++) count[i] = 0;
     for (int s = 0; s < n; s++) count[len[s]]++;
-    uint64_t *p8 = reinterpret_cast<uint64_t *>(prim);
+    uint64_t *p8 = reinterpret_cast<uint64_t *>(tab);
     for (int i = 0; i < (1 << pb) / 4; i++) p8[i] = 0;
     if (count[0] == n) return true;                      // no codes: every lookup fails (only a distance code may)
     int left = 1;
@@ -129,14 +133,36 @@ __host__ __device__ __forceinline__ bool build(uint16_t *prim, uint16_t *count, 
     for (int l = 1; l < 15; l++) offs[l + 1] = (uint16_t)(offs[l] + count[l]);
     for (int s = 0; s < n; s++)
         if (len[s]) sym[offs[len[s]]++] = (uint16_t)s;
-    // each code of length <= pb fills 2^(pb - len) entries at its bit-reversed code
-    uint32_t code = 0;
-    int k = 0;
-    for (int l = 1; l <= pb; l++) {
-        for (int c = 0; c < count[l]; c++, k++, code++) {
+    // codes in canonical order; count[l] becomes the codes of length l not yet placed (sub-table sizing, as zlib)
+    uint32_t code = 0, prefix = ~0u, sub = 0, sbits = 0;
+    int next = 1 << pb, k = 0;
+    for (int l = 1; l <= 15; l++) {
+        for (; count[l]; count[l]--, k++, code++) {
             const uint32_t rev = __builtin_bitreverse32(code) >> (32 - l);
             const uint16_t e = (uint16_t)(sym[k] | (l << 9));
-            for (uint32_t x = rev; x < (1u << pb); x += 1u << l) prim[x] = e;
+            if (l <= pb) {
+                for (uint32_t x = rev; x < (1u << pb); x += 1u << l) tab[x] = e;
+                continue;
+            }
+            const uint32_t pre = rev & ((1u << pb) - 1);
+            if (pre != prefix) {                         // a new sub-table for this root prefix
+                uint32_t cur = (uint32_t)(l - pb);
+                int lf = 1 << cur;
+                while ((int)cur + pb < 15) {
+                    lf -= count[cur + pb];
+                    if (lf <= 0) break;
+                    cur++;
+                    lf <<= 1;
+                }
+                if (next + (1 << cur) > cap) return false;
+                for (int x = 0; x < (1 << cur); x++) tab[next + x] = 0;
+                tab[pre] = (uint16_t)(0x8000u | cur << 11 | (uint32_t)next);
+                prefix = pre;
+                sub = (uint32_t)next;
+                sbits = cur;
+                next += 1 << cur;
+            }
+            for (uint32_t x = rev >> pb; x < (1u << sbits); x += 1u << (l - pb)) tab[sub + x] = e;
         }
         code <<= 1;
     }
@@ -144,26 +170,14 @@ __host__ __device__ __forceinline__ bool build(uint16_t *prim, uint16_t *count, 
 }
 
 // one symbol; -1 on an invalid code.  Needs >= 15 bits in the buffer (the caller's fill()).
-__host__ __device__ __forceinline__ int decode(IBits &B, const uint16_t *prim, const uint16_t *count, const uint16_t *sym,
-                                               int pb) {
-    const uint16_t e = prim[B.peek(pb)];
-    if (e >> 9) {
-        B.drop(e >> 9);
-        return e & 0x1FF;
-    }
-    // longer than the primary table (or invalid): the canonical walk, one bit at a time (first bit read = MSB)
-    SPG_INFLATE_SLOW_HOOK(pb);
-    int code = 0, first = 0, index = 0;
-    for (int l = 1; l <= 15; l++) {
-        code |= (int)B.peek(1);
-        B.drop(1);
-        const int c = count[l];
-        if (code - first < c) return sym[index + (code - first)];
-        index += c;
-        first = (first + c) << 1;
-        code <<= 1;
-    }
-    return -1;
+__host__ __device__ __forceinline__ int decode(IBits &B, const uint16_t *tab, int pb) {
+    uint32_t e = tab[B.peek(pb)];
+    if (e & 0x8000u) e = tab[(e & 0x7FFu) + (B.peek(pb + (int)((e >> 11) & 7u)) >> pb)];
+    const int l = (int)((e >> 9) & 15u);
+    if (!l) return -1;
+    if (l > pb) SPG_INFLATE_SLOW_HOOK(pb);
+    B.drop(l);
+    return (int)(e & 0x1FFu);
 }
 
 // length / distance bases and extra bits (RFC 1951 3.2.5), computed: c = length code - 257, d = distance code
@@ -183,17 +197,15 @@ __host__ __device__ __forceinline__ uint32_t dist_base(int d) {
 __host__ __device__ __forceinline__ uint32_t block_tables(IBits &B, uint8_t *slice, uint32_t type, bool &fixed_built) {
     uint16_t *const litp = reinterpret_cast<uint16_t *>(slice + SL_LITP);
     uint16_t *const distp = reinterpret_cast<uint16_t *>(slice + SL_DISTP);
-    uint16_t *const lcnt = reinterpret_cast<uint16_t *>(slice + SL_LCNT);
-    uint16_t *const dcnt = reinterpret_cast<uint16_t *>(slice + SL_DCNT);
-    uint16_t *const lsym = reinterpret_cast<uint16_t *>(slice + SL_LSYM);
-    uint16_t *const dsym = reinterpret_cast<uint16_t *>(slice + SL_DSYM);
+    uint16_t *const cnt = reinterpret_cast<uint16_t *>(slice + SL_CNT);
+    uint16_t *const sym = reinterpret_cast<uint16_t *>(slice + SL_SYM);
     uint8_t *const lens = slice + SL_LENS;
     if (type == 1) {                                     // the fixed codes (RFC 1951 3.2.6), built once per member
         if (!fixed_built) {
             for (int s = 0; s < 288; s++) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-            build(litp, lcnt, lsym, lens, 288, IB_LIT);
+            build(litp, TAB_LIT, cnt, sym, lens, 288, IB_LIT);
             for (int s = 0; s < 32; s++) lens[s] = 5;    // (30 and 31 complete the code; decoding them fails)
-            build(distp, dcnt, dsym, lens, 32, IB_DIST);
+            build(distp, TAB_DIST, cnt, sym, lens, 32, IB_DIST);
             fixed_built = true;
         }
         return 0;
@@ -206,11 +218,11 @@ __host__ __device__ __forceinline__ uint32_t block_tables(IBits &B, uint8_t *sli
         const int ord = i < 3 ? 16 + i : i == 3 ? 0 : (i & 1) ? 7 - (i - 5) / 2 : 8 + (i - 4) / 2;   // RFC 1951 3.2.7
         cl[ord] = (uint8_t)B.get(3);
     }
-    if (!build(litp, dcnt, dsym, cl, 19, IB_CL)) return 3;
+    if (!build(litp, TAB_LIT, cnt, sym, cl, 19, IB_CL)) return 3;
     int k = 0;
     while (k < hlit + hdist) {
         B.fill();
-        const int s = decode(B, litp, dcnt, dsym, IB_CL);
+        const int s = decode(B, litp, IB_CL);
         if (s < 0) return 3;
         if (s < 16) { lens[k++] = (uint8_t)s; continue; }
         int rep;
@@ -228,19 +240,16 @@ __host__ __device__ __forceinline__ uint32_t block_tables(IBits &B, uint8_t *sli
         while (rep--) lens[k++] = v;
     }
     if (lens[256] == 0) return 3;                        // no end-of-block code
-    if (!build(distp, dcnt, dsym, lens + hlit, hdist, IB_DIST) || !build(litp, lcnt, lsym, lens, hlit, IB_LIT)) return 4;
+    if (!build(distp, TAB_DIST, cnt, sym, lens + hlit, hdist, IB_DIST) || !build(litp, TAB_LIT, cnt, sym, lens, hlit, IB_LIT))
+        return 4;
     return 0;
 }
 
 // one member into out + M.uoff; status (see k_inflate).  slice: SLICE bytes, 8-byte aligned.
 __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp, const spg_bgzf_member &M, uint8_t *out,
                                                             uint8_t *slice) {
-    uint16_t *const litp = reinterpret_cast<uint16_t *>(slice + SL_LITP);
-    uint16_t *const distp = reinterpret_cast<uint16_t *>(slice + SL_DISTP);
-    uint16_t *const lcnt = reinterpret_cast<uint16_t *>(slice + SL_LCNT);
-    uint16_t *const dcnt = reinterpret_cast<uint16_t *>(slice + SL_DCNT);
-    uint16_t *const lsym = reinterpret_cast<uint16_t *>(slice + SL_LSYM);
-    uint16_t *const dsym = reinterpret_cast<uint16_t *>(slice + SL_DSYM);
+    const uint16_t *const litp = reinterpret_cast<const uint16_t *>(slice + SL_LITP);
+    const uint16_t *const distp = reinterpret_cast<const uint16_t *>(slice + SL_DISTP);
     uint8_t *o = out + M.uoff;
     const uint32_t ulen = M.ulen;
     const uint8_t *const cend = comp + M.coff + M.clen;
@@ -278,7 +287,7 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
         if ((st = block_tables(B, slice, type, fixed_built)) != 0) break;
         while (true) {                                   // the block's codes
             B.fill();
-            const int s = decode(B, litp, lcnt, lsym, IB_LIT);
+            const int s = decode(B, litp, IB_LIT);
             if (s < 256) {
                 if (s < 0) { st = 5; break; }
                 if (w >= ulen) { st = 7; break; }
@@ -297,7 +306,7 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
             B.fill();                                    // <= 5 extra bits, then <= 15 of the distance code
             const uint32_t len = len_base(s - 257) + B.peek((int)len_ext(s - 257));
             B.drop((int)len_ext(s - 257));
-            const int ds = decode(B, distp, dcnt, dsym, IB_DIST);
+            const int ds = decode(B, distp, IB_DIST);
             if (ds < 0 || ds > 29) { st = 5; break; }
             const uint32_t dist = dist_base(ds) + B.get((int)dist_ext(ds));
             SPG_INFLATE_MATCH_HOOK(dist, len);
@@ -403,18 +412,22 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp
 //    sends the member to the lane-per-member kernel (status ST_FALLBACK), which also reports real errors.
 //  * The block ends at the first true end-of-block token; lanes past it decoded the next block with this block's tables
 //    and are ignored; the next block's header follows the end-of-block code.
-//  * Phase B (resolve): the true token lists in order, 64 tokens (at most PAR_BATCH output bytes) at a time, into the
-//    member's 32 KiB window in LDS (a ring of PAR_RING bytes indexed by global output address): literals and matches whose
-//    source lies before the batch are written at once (lane-parallel; matches longer than 32 bytes by the whole wave),
-//    matches whose source is an earlier token of the same batch in rounds as their sources complete.  Completed 1 KiB
-//    blocks of global memory are written from the ring with 16-byte stores.
+//  * Phase B (resolve): the true token lists in order, 64 tokens (at most PAR_BATCH output bytes) at a time, into an LDS
+//    ring of the last PAR_RING output bytes (indexed by global output address): literals and matches whose source lies
+//    before the batch are written at once (lane-parallel; matches longer than 32 bytes by the whole wave), then the
+//    matches whose source is an earlier token of the batch, in order, each by the whole wave.  Completed 1 KiB blocks of
+//    global memory are written from the ring with 16-byte stores; sources more than PAR_RECENT bytes back (~40 % of the
+//    matches in BAM data: DEFLATE reaches 32 KiB back) are read from that written output.  A small ring keeps ~13 KiB of
+//    LDS per wave, so three waves per SIMD hide each other's latency: 10,000x BAM 8.56 ms (a 32 KiB ring allowed one
+//    wave per SIMD: 14.0 ms; a 4 KiB ring 8.8 ms, and with 128 VGPRs for 4 waves per SIMD 9.1 ms; r05n).
 // Token lists, positions and redo tokens live in global scratch (inflate_scratch_bytes: 12 B per compressed byte + 76 KiB
-// per member).  ~37.5 KiB of LDS per wave: 4 members per CU at a time.
+// per member).
 // ------------------------------------------------------------------------------------------------------------------
 constexpr uint32_t TK_EOB = 0x40000000u, TK_MATCH = 0x80000000u;   // tokens: literal byte | EOB | match (len-3)<<16 | dist-1
 constexpr uint32_t PAR_RCAP = 256;                                  // redo tokens per lane
 constexpr uint32_t PAR_MIN_SEG = 1024;                              // data bits per lane at least (fewer lanes for short blocks)
-constexpr uint32_t PAR_RING = 33792, PAR_BATCH = 1024;              // window ring (32 KiB + one batch), batch output cap
+constexpr uint32_t PAR_RING = 8192, PAR_BATCH = 1024;               // LDS window ring (power of two), batch output cap
+constexpr uint32_t PAR_RECENT = PAR_RING - PAR_BATCH;               // match sources this close to the batch come from LDS
 // scratch per member m (u32 units unless noted): token lists at 2 coff + 2048 m (2 clen + 2048 of them, split evenly
 // over the block's lanes), token start positions (u16, relative to the lane's first bit) at the same index of a u16 array,
 // redo tokens at 64 RCAP m
@@ -422,12 +435,10 @@ __host__ __device__ __forceinline__ uint64_t par_tok_at(const spg_bgzf_member &M
 __host__ __device__ __forceinline__ uint32_t par_area(const spg_bgzf_member &M) { return 2u * M.clen + 2048u; }
 
 struct Tabs {
-    const uint16_t *litp, *lcnt, *lsym, *distp, *dcnt, *dsym;
+    const uint16_t *litp, *distp;
 };
 __host__ __device__ __forceinline__ Tabs tabs_of(const uint8_t *slice) {
-    return Tabs{reinterpret_cast<const uint16_t *>(slice + SL_LITP), reinterpret_cast<const uint16_t *>(slice + SL_LCNT),
-                reinterpret_cast<const uint16_t *>(slice + SL_LSYM), reinterpret_cast<const uint16_t *>(slice + SL_DISTP),
-                reinterpret_cast<const uint16_t *>(slice + SL_DCNT), reinterpret_cast<const uint16_t *>(slice + SL_DSYM)};
+    return Tabs{reinterpret_cast<const uint16_t *>(slice + SL_LITP), reinterpret_cast<const uint16_t *>(slice + SL_DISTP)};
 }
 
 // the next unread bit, relative to base (IBits: buf holds n bits, r rn bits, then the chunk at qa)
@@ -443,7 +454,7 @@ __host__ __device__ __forceinline__ void ib_seek(IBits &B, const uint8_t *base, 
 // one token at the reader's position; false: no valid token starts here
 __host__ __device__ __forceinline__ bool next_token(IBits &B, const Tabs &T, uint32_t &t) {
     B.fill();
-    const int s = decode(B, T.litp, T.lcnt, T.lsym, IB_LIT);
+    const int s = decode(B, T.litp, IB_LIT);
     if (s < 256) {
         t = (uint32_t)s;
         return s >= 0;
@@ -456,7 +467,7 @@ __host__ __device__ __forceinline__ bool next_token(IBits &B, const Tabs &T, uin
     B.fill();
     const uint32_t len = len_base(s - 257) + B.peek((int)len_ext(s - 257));
     B.drop((int)len_ext(s - 257));
-    const int ds = decode(B, T.distp, T.dcnt, T.dsym, IB_DIST);
+    const int ds = decode(B, T.distp, IB_DIST);
     if (ds < 0 || ds > 29) return false;
     const uint32_t dist = dist_base(ds) + B.get((int)dist_ext(ds));
     t = TK_MATCH | (len - 3u) << 16 | (dist - 1u);
@@ -661,12 +672,15 @@ __host__ uint32_t par_member_host(const uint8_t *comp, const spg_bgzf_member &M,
     return 0;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)v, d, 64);
-        if (lane >= d) v += t;
-    }
+// inclusive prefix sum over the wave's 64 lanes: DPP row shifts within each row of 16, then the row totals broadcast
+// (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3); disabled lanes take `old` = 0
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);    // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);    // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);    // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);    // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);    // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);    // row_bcast:31
     return v;
 }
 
@@ -679,11 +693,7 @@ __device__ unsigned long long g_inf_prof[8];
 #define PAR_PROF_ADD(i, x)
 #endif
 
-__device__ __forceinline__ uint32_t ring_slot(uint32_t g0, uint32_t x) {   // (g0 + x) mod PAR_RING, g0 + x < 3 PAR_RING
-    uint32_t y = g0 + x;
-    y = y >= PAR_RING ? y - PAR_RING : y;
-    return y >= PAR_RING ? y - PAR_RING : y;
-}
+__device__ __forceinline__ uint32_t ring_slot(uint32_t g0, uint32_t x) { return (g0 + x) & (PAR_RING - 1); }
 
 __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
                                                     int64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ status,
@@ -691,7 +701,6 @@ __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ 
                                                     uint32_t *__restrict__ scr_redo, uint32_t *__restrict__ n_fallback) {
     __shared__ __align__(16) uint8_t slice[SLICE];
     __shared__ __align__(16) uint8_t ring[PAR_RING];
-    __shared__ uint32_t boff[64];
     const int64_t m = blockIdx.x;
     if (m >= n) return;
     const int lane = threadIdx.x;
@@ -706,7 +715,9 @@ __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ 
     const Tabs T = tabs_of(slice);
     const uint32_t ulen = M.ulen;
     const uint64_t gbeg = M.uoff;                                               // the member's first global output byte
-    const uint32_t g0 = (uint32_t)(gbeg % PAR_RING);
+    const uint32_t g0 = (uint32_t)(gbeg & (PAR_RING - 1));
+    typedef __attribute__((address_space(1))) const uint8_t gu8;
+    gu8 *const gout = (gu8 *)(out + gbeg);                                      // the member's output written so far
     uint32_t w = 0, flushed = 0, p = pay0, st = 0;
     bool fixed_built = false;
     int bfinal = 0;
@@ -721,10 +732,10 @@ __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ 
             const uint64_t c = blk + 16ull * (uint64_t)lane;                          // this lane's chunk (global)
             const uint64_t lo = max(c, ga), hi = min(c + 16, gbeg + bend);
             if (lo == c && hi == c + 16) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(ring + (uint32_t)(c % PAR_RING));
+                const uint4 v = *reinterpret_cast<const uint4 *>(ring + (uint32_t)(c & (PAR_RING - 1)));
                 *reinterpret_cast<uint4 *>(out + c) = v;
             } else {
-                for (uint64_t x = lo; x < hi; x++) out[x] = ring[(uint32_t)(x % PAR_RING)];
+                for (uint64_t x = lo; x < hi; x++) out[x] = ring[(uint32_t)(x & (PAR_RING - 1))];
             }
             flushed = bend;
         }
@@ -806,7 +817,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ 
                 const bool isM = (tk & TK_MATCH) != 0;
                 const uint32_t len = valid ? (isM ? ((tk >> 16) & 255u) + 3u : 1u) : 0u;
                 const uint32_t dist = (tk & 0x7FFFu) + 1u;
-                const uint32_t incl = wave_incl_scan(len, lane);
+                const uint32_t incl = wave_incl_scan(len);
                 const bool in = valid && incl <= PAR_BATCH;
                 const uint64_t inm = __ballot(in);
                 const uint32_t nb = (uint32_t)__builtin_popcountll(inm);                 // (a prefix of the lanes)
@@ -815,64 +826,49 @@ __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ 
                 nxt = load(t1 + (uint32_t)lane);                                         // the next batch, in flight
                 const uint32_t excl = incl - len, o = w + excl;
                 if (__ballot(in && isM && dist > o) || w + total > ulen) { st = ST_FALLBACK; break; }
-                boff[lane] = excl;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 const uint32_t sb = o - dist;                                            // a match's source start
-                bool ready = in && (!isM || sb + min(len, dist) <= w);
-                bool pend = in;
-                uint32_t a = 0;                                                          // first token of the source
-                if (in && !ready) {
-                    const uint32_t rel = sb > w ? sb - w : 0u;
-                    uint32_t lo = 0, hi = nb;
-                    while (hi - lo > 1) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (boff[mid] <= rel) lo = mid; else hi = mid;
-                    }
-                    a = lo;
-                }
-                uint64_t done = 0;
-                for (;;) {
-                    const uint64_t rm = __ballot(ready);
-                    if (!rm) { st = ST_FALLBACK; break; }
-                    if (ready && len <= 32) {
-                        if (!isM) {
-                            ring[ring_slot(g0, o)] = (uint8_t)tk;
-                        } else {
-                            uint32_t mq = 0;
-                            for (uint32_t q = 0; q < len; q += 4) {
-                                uint8_t v[4];
+                // independent: a literal, or a match whose source lies before the batch.  A source within PAR_RECENT bytes
+                // of the batch is in the LDS ring; one further back was written to global memory already (at most one
+                // partial 1 KiB block stays unflushed) and is read from there (L2)
+                const bool indep = in && (!isM || sb + min(len, dist) <= w);
+                const bool far = sb + PAR_RECENT < w;
+                if (indep && len <= 32) {                                                // lane by lane
+                    if (!isM) {
+                        ring[ring_slot(g0, o)] = (uint8_t)tk;
+                    } else {
+                        uint32_t mq = 0;
+                        for (uint32_t q = 0; q < len; q += 4) {
+                            uint8_t v[4];
 #pragma unroll
-                                for (int u = 0; u < 4; u++) {
-                                    v[u] = q + u < len ? ring[ring_slot(g0, sb + mq)] : 0;
-                                    mq = mq + 1 == dist ? 0 : mq + 1;
-                                }
-#pragma unroll
-                                for (int u = 0; u < 4; u++)
-                                    if (q + u < len) ring[ring_slot(g0, o + q + u)] = v[u];
+                            for (int u = 0; u < 4; u++) {
+                                v[u] = q + u < len ? (far ? gout[sb + mq] : ring[ring_slot(g0, sb + mq)]) : 0;
+                                mq = mq + 1 == dist ? 0 : mq + 1;
                             }
+#pragma unroll
+                            for (int u = 0; u < 4; u++)
+                                if (q + u < len) ring[ring_slot(g0, o + q + u)] = v[u];
                         }
                     }
-                    uint64_t lm = __ballot(ready && len > 32);
-                    while (lm) {                                                         // long matches: the whole wave
-                        const int j = __builtin_ctzll(lm);
-                        lm &= lm - 1;
-                        const uint32_t oj = (uint32_t)__builtin_amdgcn_readlane((int)o, j);
-                        const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)len, j);
-                        const uint32_t dj = (uint32_t)__builtin_amdgcn_readlane((int)dist, j);
-                        for (uint32_t q0 = 0; q0 < lj; q0 += 64) {
-                            const uint32_t q = q0 + (uint32_t)lane;
-                            uint8_t v = 0;
-                            if (q < lj) v = ring[ring_slot(g0, oj - dj + (dj >= lj ? q : q % dj))];
-                            if (q < lj) ring[ring_slot(g0, oj + q)] = v;
-                        }
+                }
+                // then one match at a time by the whole wave: the long independent ones, then in order those whose
+                // source is an earlier token of this batch (every earlier token is written by then); byte q of a match
+                // is its source's byte q mod dist, so a match never reads its own bytes
+                uint64_t lm = __ballot(indep && len > 32), dm = __ballot(in && !indep);
+                while (lm | dm) {
+                    uint64_t &mk = lm ? lm : dm;
+                    const int j = __builtin_ctzll(mk);
+                    mk &= mk - 1;
+                    const uint32_t oj = (uint32_t)__builtin_amdgcn_readlane((int)o, j);
+                    const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)len, j);
+                    const uint32_t dj = (uint32_t)__builtin_amdgcn_readlane((int)dist, j);
+                    const bool farj = oj - dj + PAR_RECENT < w;                         // (wave-uniform)
+                    for (uint32_t q0 = 0; q0 < lj; q0 += 64) {
+                        const uint32_t q = q0 + (uint32_t)lane;
+                        uint8_t v = 0;
+                        const uint32_t x = oj - dj + (dj >= lj ? q : q % dj);
+                        if (q < lj) v = farj ? gout[x] : ring[ring_slot(g0, x)];
+                        if (q < lj) ring[ring_slot(g0, oj + q)] = v;
                     }
-                    done |= rm;
-                    pend = pend && !ready;
-                    if (!__ballot(pend)) break;
-                    const uint64_t need = ((1ull << lane) - 1) & ~((1ull << a) - 1);
-                    ready = pend && (done & need) == need;
                 }
                 if (st) break;
                 PAR_PROF_ADD(6, 1);
