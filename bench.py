@@ -1034,8 +1034,8 @@ def end_to_end(args, device):
         caller, calls, t0, t_in, t1 = stream(cap, "device")
         assert [v["start"] for v in calls] == [v["start"] for v in calls_h], "device / host pileup calls differ"
         brk = device_breakdown(caller)
-        # the same BAMs through process_bams (the drop-in's many-BAM call: plans of two BAMs overlap on the host; their
-        # BGZF members inflate on the GPU, spg_bgzf_inflate); a warm-up call first (the inflater's device buffers)
+        # the same BAMs through process_bams (the drop-in's many-BAM call: the BAM-in-HBM path pipelined over two device
+        # BAM slots, the next BAM opening on the GPU while the host plans this one); a warm-up call first (device buffers)
         caller.process_bams([bam] * 2)
         caller.reset_memory()
         caller.engine.sync()
@@ -1056,12 +1056,14 @@ def end_to_end(args, device):
             os.remove(pth)
         many_leg = {"bams": 2 * n_bams, "positions_per_s_per_bam": 2 * n_bams * L_SARS / (m1 - m0),
                     "s_per_bam": (m1 - m0) / (2 * n_bams),
-                    "path": "records plans (two at once on the host threads), BGZF inflate " +
-                            ("on the GPU (spg_bgzf_inflate)" if caller.last_gpu_inflate else "on the host")}
+                    "path": ("BAMs kept in HBM, pipelined over two device BAM slots (spg_bam_slot): BAM i + 1 opens on "
+                             "the GPU while the host plans BAM i" if caller.last_bam_path == "device" else
+                             "records plans (two at once on the host threads), BGZF inflate " +
+                             ("on the GPU (spg_bgzf_inflate)" if caller.last_gpu_inflate else "on the host"))}
         res[tag] = {"bams": n_bams, "positions_per_s_per_bam": n_bams * L_SARS / (t1 - t0),
                     "s_per_bam": (t1 - t0) / n_bams, "ingest_s": t_in, "finalize_s": t1 - t0 - t_in,
                     "calls": len(calls), "reads_per_bam": int(brk["reads"]),
-                    "path": "BAM kept in HBM (process_bam, pileup='device'): compressed file H2D -> k_inflate + k_crc32 "
+                    "path": "BAM kept in HBM (process_bam, pileup='device'): compressed file H2D -> k_inflate_par + k_crc32 "
                             "-> record scan + stepper filter + fields on the GPU -> fields D2H -> host depth cap / mate "
                             "pairing (spp_pileup_plan_fields) -> plan H2D -> mate-overlap tweak + k_pileup_fill -> "
                             "accumulate",

@@ -245,7 +245,9 @@ struct spg_ctx {
     int64_t hist_cap = 0;               // 0 = no cap
     int64_t hist_dev_bytes = 0;         // owned history bytes resident in HBM
     int64_t n_spilled = 0;
-    BamDev bam;                         // spg_bam_*: the BAM in HBM
+    BamDev bams[2];                     // spg_bam_*: BAMs in HBM (two slots: process_bams opens the next BAM while the
+    int bam_slot = 0;                   // host plans the last one), the current slot (spg_bam_slot)
+    BamDev &bam_cur() { return bams[bam_slot]; }
     // spg_accumulate_records: HBM staging of the last records batch (inflated BAM + per-read index), grow-only
     uint8_t *rs = nullptr;
     size_t rs_cap = 0;
@@ -408,9 +410,11 @@ int spg_destroy(spg_ctx *c) {
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     free_spilled(c);
     c->arena.release();
-    c->bam.release();
-    for (hipEvent_t e : c->bam.ev)
-        if (e) (void)hipEventDestroy(e);
+    for (BamDev &b : c->bams) {
+        b.release();
+        for (hipEvent_t e : b.ev)
+            if (e) (void)hipEventDestroy(e);
+    }
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
                     c->d_fused, c->deep_list, c->deep_n, c->cdep, c->cmcf, c->fwm, c->fold_part, c->fold_arrived, c->rs,
@@ -2130,19 +2134,25 @@ int spg_bam_release(spg_ctx *c) {
     if (!c) return fail("spg_bam_release: null ctx");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->copy_stream));
-    c->bam.release();
+    for (BamDev &b : c->bams) b.release();
+    return 0;
+}
+
+int spg_bam_slot(spg_ctx *c, int slot) {
+    if (!c || slot < 0 || slot > 1) return fail("spg_bam_slot: bad argument");
+    c->bam_slot = slot;
     return 0;
 }
 
 int spg_bam_inflate_ms(spg_ctx *c, float *ms) {
     if (!c || !ms) return fail("spg_bam_inflate_ms: null argument");
-    *ms = c->bam.inflate_ms;
+    *ms = c->bam_cur().inflate_ms;
     return 0;
 }
 
 int spg_bam_inflate_fallbacks(spg_ctx *c, int64_t *n) {
     if (!c || !n) return fail("spg_bam_inflate_fallbacks: null argument");
-    *n = c->bam.inflate_fallbacks;
+    *n = c->bam_cur().inflate_fallbacks;
     return 0;
 }
 
@@ -2152,7 +2162,7 @@ int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg
         return fail("spg_bam_open: bad argument");
     if (flt->stepper < 0 || flt->stepper > 2) return fail("spg_bam_open: bad stepper");
     HIPCHK(hipSetDevice(c->device));
-    BamDev &B = c->bam;
+    BamDev &B = c->bam_cur();
     B.open = false;
     *n_reads = 0;
     std::vector<uint64_t> uoff((size_t)n + 1, 0);
@@ -2268,7 +2278,7 @@ int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg
 
 int spg_bam_reads_copy(spg_ctx *c, const spg_bam_reads *o) {
     if (!c || !o) return fail("spg_bam_reads_copy: null argument");
-    BamDev &B = c->bam;
+    BamDev &B = c->bam_cur();
     if (!B.open) return fail("spg_bam_reads_copy: no BAM open (spg_bam_open)");
     HIPCHK(hipSetDevice(c->device));
     hipStream_t cs = c->copy_stream;
@@ -2289,7 +2299,7 @@ int spg_bam_accumulate(spg_ctx *c, const spg_bam_plan *P, uint32_t flags) {
     if (!c || !P) return fail("spg_bam_accumulate: null argument");
     if (!c->lut_set) return fail("spg_accumulate: spg_set_eps_lut not called");
     if (!c->ref) return fail("spg_accumulate: spg_set_reference not called");
-    BamDev &B = c->bam;
+    BamDev &B = c->bam_cur();
     if (!B.open) return fail("spg_bam_accumulate: no BAM open (spg_bam_open)");
     if (P->n_cols < 0 || P->n_cols > ((int64_t)1 << 31) - 128) return fail("spg_bam_accumulate: n_cols out of range");
     if (P->n_kept < 0 || P->n_kept > (int64_t)B.n_reads || P->n_pairs < 0 || P->n_pairs > P->n_kept || P->max_span < 0)

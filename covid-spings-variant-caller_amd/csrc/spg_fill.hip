@@ -80,49 +80,65 @@ __global__ void k_fill_ngroups(FillArgs A, const uint32_t *tile_first, uint32_t 
     ng[t] = r1 > r0 ? (r1 - r0 + (uint32_t)fg - 1) / (uint32_t)fg : 0u;
 }
 
-// one wave per tile, lane = column: covering reads counted in BAM order; at each group boundary the count so far is
-// that group's start (relative to the column's CSR offset); the total must be the column's entry count
+// one wave per tile: covering reads counted in BAM order, 64 reads per step, as a difference array over the tile's
+// columns in LDS (+1 at a read's first covered column, -1 after its last); at each group boundary the prefix sum over
+// the columns is every column's count so far — that group's start (relative to the column's CSR offset); the total must
+// be the column's entry count.  (r05: two readlanes per read per column made this pass 0.85 ms per 10,000x BAM.)
 __global__ __launch_bounds__(256) void k_fill_starts(FillArgs A, const uint32_t *tile_first, const uint32_t *item_off,
                                                      uint32_t *gstart, int32_t fg) {
-    const int lane = threadIdx.x & 63;
-    const int32_t t = (int32_t)(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (t >= A.n_tiles) return;
+    __shared__ int32_t diff[4][65];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int32_t t = (int32_t)(blockIdx.x * 4 + w);
+    if (t >= A.n_tiles) return;                                        // (wave-uniform; no barrier below)
     const int32_t c0 = t * 64, W = min(64, A.n_cols - c0);
     const int64_t P0 = A.pos_begin + c0;
     const uint32_t r0 = tile_first[max(t - A.back, 0)], r1 = tile_first[t + 1];
     uint32_t *gs = gstart + (size_t)item_off[t] * 64;
-    uint32_t cnt = 0;
-    // fg is a multiple of 64 (fill_group): group boundaries fall on chunk starts only, so the inner loop is just the count
-    // (a per-read `% fg` there made this pass 1.6 ms per 10,000x BAM, r05g)
-    // the next chunk's read bounds are loaded while this chunk is counted (each chunk's load was a full memory round trip)
+    int32_t *const d = diff[w];
+    d[lane] = 0;
+    if (lane == 0) d[64] = 0;
+    // fg is a multiple of 64 (fill_group): group boundaries fall on chunk starts
     int64_t nps = 0, npe = 0;
     if (r0 + lane < r1) { nps = A.rpos[r0 + lane]; npe = A.rend[r0 + lane]; }
+    uint32_t cnt = 0;
     for (uint32_t rb = r0, gi = 0, gl = 0; rb < r1; rb += 64) {
-        int32_t s = INT32_MAX, e = INT32_MIN;
-        if (rb + lane < r1) {
-            s = (int32_t)max(nps - P0, (int64_t)INT32_MIN + 1);
-            e = (int32_t)min(npe - P0, (int64_t)INT32_MAX);
-        }
+        const bool have = rb + lane < r1;
+        const int64_t s = nps - P0, e = npe - P0;
         if (rb + 64 + lane < r1) { nps = A.rpos[rb + 64 + lane]; npe = A.rend[rb + 64 + lane]; }
-        if (gl == 0) gs[(size_t)gi * 64 + lane] = cnt;
+        if (gl == 0) {                                                 // a group starts here: counts so far
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t v = (uint32_t)d[lane];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)v, o);
+                if (lane >= o) v += y;
+            }
+            cnt = v;
+            gs[(size_t)gi * 64 + lane] = cnt;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
         gl += 64;
         if (gl == (uint32_t)fg) { gl = 0; gi++; }
-        const uint32_t n = min(64u, r1 - rb);
-        // two counters so consecutive reads' compares do not chain on one add
-        uint32_t c0 = 0, c1 = 0;
-        uint32_t j = 0;
-        for (; j + 2 <= n; j += 2) {
-            const int32_t s0 = __builtin_amdgcn_readlane(s, j), e0 = __builtin_amdgcn_readlane(e, j);
-            const int32_t s1 = __builtin_amdgcn_readlane(s, j + 1), e1 = __builtin_amdgcn_readlane(e, j + 1);
-            c0 += (uint32_t)(lane >= s0 && lane < e0);
-            c1 += (uint32_t)(lane >= s1 && lane < e1);
+        const int64_t cs = s < 0 ? 0 : s, ce = e > 64 ? 64 : e;
+        if (have && cs < ce) {
+            atomicAdd(&d[cs], 1);
+            atomicAdd(&d[ce], -1);
         }
-        if (j < n) {
-            const int32_t s0 = __builtin_amdgcn_readlane(s, j), e0 = __builtin_amdgcn_readlane(e, j);
-            c0 += (uint32_t)(lane >= s0 && lane < e0);
-        }
-        cnt += c0 + c1;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t v = (uint32_t)d[lane];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)v, o);
+        if (lane >= o) v += y;
+    }
+    cnt = v;
     if (lane < W && (uint64_t)cnt != A.off[c0 + lane + 1] - A.off[c0 + lane]) atomicOr(A.err, 2u);
 }
 

@@ -210,13 +210,24 @@ class PileupEngine:
             N.check(rc, "spg_bam_open")
         return n.value
 
+    def bam_slot(self, slot: int):
+        """spg_bam_slot: the device BAM slot (0 / 1) the next bam_* calls use (two BAMs open at once)."""
+        with self._lock:
+            N.check(self._L.spg_bam_slot(self._h, int(slot)), "spg_bam_slot")
+            self._bam_slot = int(slot)
+
     def bam_reads(self, n: int) -> Dict[str, np.ndarray]:
-        """spg_bam_reads_copy: the open BAM's kept reads' fixed fields (pinned host arrays, reused across BAMs)."""
-        bufs = getattr(self, "_bam_bufs", None)
+        """spg_bam_reads_copy: the open BAM's kept reads' fixed fields (pinned host arrays per BAM slot, reused
+        across that slot's BAMs)."""
+        slot = getattr(self, "_bam_slot", 0)
+        allb = getattr(self, "_bam_bufs", None)
+        if allb is None:
+            allb = self._bam_bufs = {}
+        bufs = allb.get(slot)
         if bufs is None or len(bufs["pos"]) < n:
             cap = max(1024, int(n * 1.125))
             bufs = {name: pinned_empty(cap, dt) for name, dt in N.BAM_READ_FIELDS}
-            self._bam_bufs = bufs
+            allb[slot] = bufs
         out = {name: a[:n] for name, a in bufs.items()}
         r = N.SpgBamReads(*[out[name].ctypes.data for name, _ in N.BAM_READ_FIELDS])
         with self._lock:

@@ -158,10 +158,11 @@ class LiveVariantCaller:
         pileup()'s ``max_depth`` / stepper / ``ignore_overlaps``; host threads of the BAM plan.
 
         ``pileup`` — where a BAM's pileup is built (SAM input always takes "host"):
-          "device"  (default) a lone process_bam keeps the BAM in HBM: the compressed file goes up, the GPU inflates
+          "device"  (default) process_bam keeps the BAM in HBM: the compressed file goes up, the GPU inflates
                     and scans it, only the reads' fixed fields come down for the host's depth-cap / mate-pairing
-                    replay, and the entries are written on the GPU (spg_bam_*); process_bams and multi-device callers
-                    use the records plan below.  A BAM the device path cannot take (a member it cannot inflate,
+                    replay, and the entries are written on the GPU (spg_bam_*); process_bams pipelines it over two
+                    device BAM slots (the next BAM opens on the GPU while the host plans this one); multi-device
+                    callers use the records plan below.  A BAM the device path cannot take (a member it cannot inflate,
                     record chains that disagree, a name-hash collision) falls back to the records plan, and so does
                     a BAM file smaller than ``device_min_bytes`` (default 32 MiB, ~1,300 BGZF members): the GPU
                     inflate takes ~19 ms however few members there are (one member's serial decode chain), which
@@ -334,6 +335,9 @@ class LiveVariantCaller:
                 raise FileNotFoundError(f"[Errno 2] could not open alignment file `{f}`: No such file or directory")
         import dataclasses
         contig = self.fastaFile.references[referenceIndex]
+        if (self._device_bam and paths and
+                all(_is_bgzf(f) and os.path.getsize(f) >= self.device_min_bytes for f in paths)):
+            return self._process_bams_device(paths, contig, referenceIndex)
         # concurrent plans: one per 8 CPUs this process may use (the GPU box's 16-CPU quota: two), so one plan's serial
         # phases (record scan, depth-cap sweep) overlap the other's inflate; the host threads split between them
         workers = workers or max(1, min(4, cpu_share() // 8))
@@ -358,6 +362,92 @@ class LiveVariantCaller:
                     pending.append(ex.submit(plan, paths[i + window]))
                 pending[i] = None
                 self._accumulate_plan(batch, referenceIndex)
+
+    def _process_bams_device(self, paths, contig: str, referenceIndex: int):
+        """process_bams with every BAM kept in HBM (as the lone process_bam), pipelined over the engine's two device BAM
+        slots: BAM i + 1 is opened on the GPU (compressed bytes up, inflate, record scan, fields down) while the host
+        replays BAM i's depth cap / mate pairing on a worker thread; BAM i is then accumulated, before BAM i + 2 reuses
+        its slot.  The next BAMs' bytes are read into pinned memory on another thread.  Accumulation stays in the given
+        order (the same history as one process_bam per BAM); a BAM the device path declines takes the records plan in
+        its turn."""
+        from concurrent.futures import ThreadPoolExecutor
+        prm = self.pileup_params
+        nt = max(1, prm.n_threads // 2)
+
+        def read(path):
+            bam = AlignmentFile(path)
+            if contig not in bam.references:
+                bam.close()
+                raise ValueError(f"invalid contig `{contig}`")
+            return bam, bam.bam_map(nt)
+
+        def finish(job):
+            slot, bam, fut = job
+            try:
+                batch = fut.result()
+                with self._lock:
+                    if batch.n_cols == 0:
+                        batch.close()
+                        return
+                    self._use_reference(referenceIndex)
+                    self.engine.bam_slot(slot)
+                    if self.engine.bam_accumulate(batch):
+                        self._inflight.append((self.engine.input_ticket(), batch))
+                        self._drain(keep=2)
+                        self._batch_contig.append(referenceIndex)
+                        return
+                    batch.close()
+                    log.info("device BAM plan declined: %s", self.engine.bam_fallback)
+                self._accumulate_plan(bam.pileup_records(contig, prm), referenceIndex)
+            finally:
+                bam.close()
+
+        self.last_bam_path = "device"
+        with ThreadPoolExecutor(1) as io, ThreadPoolExecutor(1) as planner:
+            maps = [io.submit(read, p) for p in paths[:2]]
+            pending = None
+            try:
+                for i in range(len(paths)):
+                    bam, bmap = maps[i].result()
+                    maps[i] = None
+                    if i + 2 < len(paths):
+                        maps.append(io.submit(read, paths[i + 2]))
+                    slot = i & 1
+                    try:
+                        with self._lock:
+                            self.engine.bam_slot(slot)
+                            n = self.engine.bam_open(bmap, bam.tid(contig), prm)
+                            reads = self.engine.bam_reads(n) if n is not None else None
+                    finally:
+                        bmap.close()
+                    if pending is not None:           # BAM i - 1: planned on the worker while BAM i opened
+                        job, pending = pending, None
+                        finish(job)
+                    if reads is None:                 # declined: the records plan, in order
+                        log.info("device BAM path declined %s: %s", paths[i], self.engine.bam_fallback)
+                        try:
+                            self._accumulate_plan(bam.pileup_records(contig, prm), referenceIndex)
+                        finally:
+                            bam.close()
+                        continue
+                    pending = (slot, bam, planner.submit(bam.pileup_fields, contig, reads, prm))
+                if pending is not None:
+                    job, pending = pending, None
+                    finish(job)
+            finally:
+                if pending is not None:
+                    pending[2].cancel()
+                    pending[1].close()
+                for f in maps:
+                    if f is not None:
+                        try:
+                            b, m = f.result()
+                            m.close()
+                            b.close()
+                        except Exception:
+                            pass
+                with self._lock:
+                    self.engine.bam_slot(0)
 
     def _accumulate_plan(self, batch, referenceIndex):
         with self._lock:

@@ -334,8 +334,8 @@ int spg_bgzf_fallbacks(int device, int64_t *n);
  * htslib's depth cap and mate pairing on them (spp_pileup_plan_fields, include/spings_pileup.h); spg_bam_accumulate
  * takes that plan — the kept reads, the CSR offsets, the overlapping mate pairs — applies the mate-overlap quality
  * tweak in HBM and writes the batch's entries with k_pileup_fill, then accumulates it like spg_accumulate_records
- * (bit-identical batch).  One BAM per context at a time; its device buffers are reused by the next spg_bam_open
- * (stream-ordered after this BAM's fill).  Return 1 (not < 0) means "not handled here, nothing accumulated": a member
+ * (bit-identical batch).  One BAM per slot at a time (spg_bam_slot: two slots per context); its device buffers are
+ * reused by the slot's next spg_bam_open (stream-ordered after this BAM's fill).  Return 1 (not < 0) means "not handled here, nothing accumulated": a member
  * the GPU could not inflate (corrupt, CRC mismatch), record chains that disagree, or two paired reads whose names
  * differ behind an equal name hash — the caller then plans the BAM on the host (spp_pileup_plan_records). */
 typedef struct {
@@ -375,8 +375,13 @@ int spg_bam_accumulate(spg_ctx *ctx, const spg_bam_plan *plan, uint32_t flags);
 int spg_bam_inflate_ms(spg_ctx *ctx, float *ms);
 /* members of the last spg_bam_open that the parallel inflater left to the one-lane-per-member decoder */
 int spg_bam_inflate_fallbacks(spg_ctx *ctx, int64_t *n);
-/* Free the BAM buffers (the next spg_bam_open allocates them again). */
+/* Free the BAM buffers of both slots (the next spg_bam_open allocates them again). */
 int spg_bam_release(spg_ctx *ctx);
+/* The BAM slot (0 or 1, default 0) the next spg_bam_* calls use: each slot holds one open BAM's device buffers, so a
+ * caller can open the next BAM in the other slot while the host plans this one (LiveVariantCaller.process_bams); a
+ * slot's buffers are reused by its next spg_bam_open, ordered after that slot's spg_bam_accumulate on the context's
+ * copy stream. */
+int spg_bam_slot(spg_ctx *ctx, int slot);
 
 /* Introspection for tests. */
 int spg_device_count(int *n);

@@ -340,13 +340,15 @@ def test_pinned_ingest_stream_vs_oracle(planted):
     assert list(mem) == list(omem) and all(mem[p] == omem[p] for p in omem)
 
 
-@pytest.mark.parametrize("gpu_inflate_min", [None, "1", "host"])
-def test_process_bams_equals_sequential_process_bam(tmp_path, gpu_inflate_min):
-    """process_bams (the many-BAM ingest: plans on a thread pool, accumulated in order, counted at
-    prepare_variants) == one process_bam per BAM == the oracle, on 7 BAMs whose depth caps bind and whose
-    first visits differ (BAM 3 covers a region no earlier BAM does), then more BAMs after a prepare_variants.
-    gpu_inflate_min "1": every BAM's members are inflated on the GPU (spg_bgzf_inflate; by default only BAMs of
-    >= 4096 members); "host": gpu_inflate=False, every BAM inflated on the host whatever its size."""
+@pytest.mark.parametrize("pileup,gpu_inflate_min", [("device", None), ("records", None), ("records", "1"),
+                                                    ("records", "host")])
+def test_process_bams_equals_sequential_process_bam(tmp_path, pileup, gpu_inflate_min):
+    """process_bams (the many-BAM ingest, accumulated in order, counted at prepare_variants) == one process_bam per
+    BAM == the oracle, on 7 BAMs whose depth caps bind and whose first visits differ (BAM 3 covers a region no earlier
+    BAM does), then more BAMs after a prepare_variants.  pileup "device": every BAM kept in HBM, pipelined over the two
+    device BAM slots (the next BAM opens while the host plans this one); "records": records plans on a thread pool,
+    gpu_inflate_min "1": every BAM's members inflated on the GPU (spg_bgzf_inflate; by default only BAMs of >= 4096
+    members); "host": gpu_inflate=False, every BAM inflated on the host whatever its size."""
     L = 900
     ref = _ref(L, 31)
     fasta = str(tmp_path / "ref.fa")
@@ -362,11 +364,12 @@ def test_process_bams_equals_sequential_process_bam(tmp_path, gpu_inflate_min):
         samgen.write_bam(p, [("chrS", L)], recs)
         samgen.write_sam(str(tmp_path / f"m{k}.sam"), [("chrS", L)], recs)
         files.append(p)
-    a = _caller(fasta, max_depth=250, gpu_inflate=gpu_inflate_min != "host")
+    a = _caller(fasta, max_depth=250, gpu_inflate=gpu_inflate_min != "host", pileup=pileup)
     b = _caller(fasta, max_depth=250)
     if gpu_inflate_min == "1":
         a.pileup_params.inflate_min_members = 1
     a.process_bams(files[:7], workers=3)
+    assert a.last_bam_path == pileup
     for f in files[:7]:
         b.process_bam(f)
     va, vb = a.prepare_variants(), b.prepare_variants()
