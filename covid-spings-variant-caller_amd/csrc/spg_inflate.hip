@@ -1,13 +1,15 @@
 // spg_inflate.hip — BGZF members inflated on the GPU (process_bam's BAM read,
-// live_variant_caller.py:54-72, whose host BGZF inflate bounds the end-to-end stream at the GPU box's 16-CPU share).
+// live_variant_caller.py:54-72, which htslib's BGZF reader serves in the reference).
 //
-// A BGZF file is a sequence of independent raw-DEFLATE members (RFC 1951) of at most 64 KiB of output each: one
-// lane per member decodes its blocks (stored, fixed Huffman, dynamic Huffman) into the member's output range.  All
-// per-member state lives in registers and the lane's LDS slice: the Huffman tables (10-bit primary table for the
-// literal/length code, 8-bit for distances, a canonical walk for the rare longer codes), the code lengths; length and
-// distance bases are computed, not looked up.  The compressed stream is read as aligned 16-byte chunks one ahead of
-// use.  A member's status word is 0 when it inflated to exactly its ISIZE bytes; anything else (a corrupt stream) is
-// reported and the caller inflates that member on the host.
+// A BGZF file is a sequence of independent raw-DEFLATE members (RFC 1951) of at most 64 KiB of output each.
+// k_inflate_par (the product path): one wave per member, its blocks' data bits decoded by 64 lanes at once — segments
+// that resynchronise on token starts — then the tokens resolved into the member's output through an LDS window ring
+// (the comment above the kernel).  k_inflate: one lane per member, the whole member as one serial decode; it takes the
+// members k_inflate_par leaves (stored blocks, token overflows, anything malformed) and reports real errors.  k_crc32
+// checks every member's output against its trailer.  Both decoders share the bit reader, the two-level Huffman tables
+// and the block-header code, compiled for the host too (spg_bgzf_inflate_check / _par_check: CPU tests against zlib).
+// A member's status word is 0 when it inflated to exactly its ISIZE bytes with the trailer's CRC32; anything else (a
+// corrupt stream) is reported and the caller inflates that member on the host (or plans the BAM there).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -257,9 +259,6 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
     B.end = cend + 8;
     B.start(comp + M.coff);
     uint32_t w = 0;                                      // bytes written
-#if defined(SPG_INFLATE_TOKEN_STORES)
-    uint32_t ntk = 0;
-#endif
     uint32_t st = 0;
     int bfinal = 0;
     bool fixed_built = false;
@@ -291,14 +290,7 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
             if (s < 256) {
                 if (s < 0) { st = 5; break; }
                 if (w >= ulen) { st = 7; break; }
-#if defined(SPG_INFLATE_DECODE_ONLY)                     // (A/B: decode cost alone — no output written)
-                w++;
-#elif defined(SPG_INFLATE_TOKEN_STORES)                  // (A/B: one byte store per symbol, no match reads)
-                o[ntk++] = (uint8_t)s;
-                w++;
-#else
                 o[w++] = (uint8_t)s;
-#endif
                 continue;
             }
             if (s == 256) break;
@@ -312,14 +304,6 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
             SPG_INFLATE_MATCH_HOOK(dist, len);
             if (dist > w) { st = 6; break; }
             if (w + len > ulen) { st = 7; break; }
-#if defined(SPG_INFLATE_DECODE_ONLY)
-            w += len;
-            continue;
-#elif defined(SPG_INFLATE_TOKEN_STORES)
-            o[ntk++] = (uint8_t)(len ^ dist);
-            w += len;
-            continue;
-#endif
             uint8_t *dst = o + w;
             const uint8_t *from = dst - dist;
             if (dist >= 16 && w + len + 15 <= ulen) {
@@ -376,11 +360,7 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
 // mpw members per block, one per lane (lanes >= mpw idle), each with its SLICE of the block's LDS.  Latency-bound
 // (a member's symbols are a dependent chain; r04ze: 19.3 ms on the 10,000x BAM at 3 members per block).  Since r05 the
 // fallback of k_inflate_par (only_fallback: the members it left) and the whole inflater of SPG_INFLATE_LANE A/B builds.
-#if defined(SPG_INFLATE_MPW_AB)
-constexpr int INFLATE_MPW = SPG_INFLATE_MPW_AB;          // (A/B builds only)
-#else
 constexpr int INFLATE_MPW = 3;
-#endif
 constexpr uint32_t ST_FALLBACK = 100;   // (k_inflate_par) this member is left to the lane kernel
 __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
                                                 int64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ status, int mpw,
