@@ -118,7 +118,7 @@ def build_gpu(force=False, verbose=False) -> str:
 
 
 # kernels on the measured paths: a scratch spill there costs occupancy and time (tests/test_cabi.py)
-HOT_KERNELS = ("k_acc_seg<4", "k_acc_tile", "k_acc_lite", "k_fold_hist", "k_fill", "k_finalize", "k_inflate", "k_bam_")
+HOT_KERNELS = ("k_acc_seg<4", "k_acc_tile", "k_acc_lite", "k_fold_hist", "k_fill", "k_f2_", "k_finalize", "k_inflate", "k_bam_")
 
 
 def kernel_resources(remarks: str) -> dict:

@@ -8,7 +8,9 @@
 // base (0 past the read end), in htslib's per-column order (the column's reads in BAM order).  Bit-identical to
 // spp_batch_fill of the same plan (tests/test_device_pileup_gpu.py).
 //
-// Work items: a tile of 64 consecutive columns x a group of `fg` consecutive reads of the tile's read range (the
+// r05: the transposed fill (k_f2_*, below: one wave per 64-read chunk, lane = read) is the path; the tile kernels that
+// follow remain for batches whose reads span too many columns for its per-chunk rows (F2_SPAN_LIMIT).
+// Work items (tile kernels): a tile of 64 consecutive columns x a group of `fg` consecutive reads of the tile's read range (the
 // reads starting at most max_span before the tile, up to its end: tile_first), so a 10,000x batch spreads over ~30k
 // waves instead of one wave per tile.  A column's entries of a group are its covering reads of that group in BAM
 // order, starting at the count of covering reads of the tile's earlier groups (k_fill_starts: one wave per tile,
@@ -347,6 +349,287 @@ hipError_t launch_pos_copy(const Hist *H, const int32_t *items, int32_t n, const
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------------------------
+// The transposed fill (r05): one wave per chunk of 64 consecutive reads (BAM order), lane = read.  Each lane walks its
+// own CIGAR once, column by column over the chunk's column span, with its quality and packed-base bytes in 8-byte
+// windows (the next window loaded one ahead); at every column the covering lanes' entries are ranked by a ballot and
+// written as one contiguous run at off[c] + base(chunk, c) + rank, base(chunk, c) being the covering reads of column c
+// in earlier chunks.  That base comes from three small passes: each chunk's column span (k_f2_span), its per-column
+// counts (k_f2_count, into rows of a scanned span layout), and per column a running sum along the chunks that cover it
+// (k_f2_base, which also checks the total against the CSR offsets).  The tile kernels above made one wave-iteration of
+// all 64 lanes per (read, tile) pair with a wave-uniform CIGAR walk each (1.98 ms per 10,000x BAM, r05q).
+// ------------------------------------------------------------------------------------------------------------------
+struct F2Lay {                           // fill_scratch_bytes' layout of the transposed fill
+    int32_t *cbeg, *cend;                // per chunk: first / past-last column of its span (clamped to the batch)
+    uint32_t *span, *row;                // per chunk: span length; its row's offset (exclusive scan of span)
+    uint8_t *cnt;                        // [sum of spans]: covering reads per (chunk, column) (<= 64)
+    uint32_t *base;                      // [sum of spans]: covering reads of the column in earlier chunks
+    void *scan_tmp;
+    size_t scan_bytes;
+    uint64_t span_cap;
+    int64_t n_chunks;
+};
+constexpr uint64_t F2_SPAN_LIMIT = (uint64_t)1 << 28;    // beyond this bound on the spans' sum the tile kernels run
+
+__host__ __device__ __forceinline__ uint64_t f2_span_cap(int64_t n_cols, int64_t n_reads, int32_t back) {
+    // a chunk's span <= its reads' start spread + max_span; the spreads of consecutive chunks do not overlap
+    const int64_t n_chunks = (n_reads + 63) / 64;
+    return (uint64_t)n_cols + (uint64_t)n_chunks * ((uint64_t)back * 64 + 2) + 64;
+}
+
+F2Lay f2_layout(void *base, int64_t n_cols, int64_t n_reads, int32_t back) {
+    F2Lay L{};
+    L.n_chunks = (n_reads + 63) / 64;
+    L.span_cap = f2_span_cap(n_cols, n_reads, back);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, L.scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (int)(L.n_chunks + 1));
+    uint8_t *p = static_cast<uint8_t *>(base);
+    size_t o = 0;
+    const size_t nc = (size_t)L.n_chunks + 1;
+    L.cbeg = reinterpret_cast<int32_t *>(p + o); o += al256(4 * nc);
+    L.cend = reinterpret_cast<int32_t *>(p + o); o += al256(4 * nc);
+    L.span = reinterpret_cast<uint32_t *>(p + o); o += al256(4 * nc);
+    L.row = reinterpret_cast<uint32_t *>(p + o); o += al256(4 * nc);
+    L.scan_tmp = p + o; o += al256(L.scan_bytes);
+    L.base = reinterpret_cast<uint32_t *>(p + o); o += al256(4 * L.span_cap);
+    L.cnt = p + o; o += al256(L.span_cap);
+    return L;
+}
+size_t f2_bytes(int64_t n_cols, int64_t n_reads, int32_t back) {
+    F2Lay L = f2_layout(nullptr, n_cols, n_reads, back);
+    return reinterpret_cast<size_t>(L.cnt) + al256(L.span_cap) + 256;
+}
+
+__device__ __forceinline__ int32_t f2_rel(int64_t x, int64_t P0) {
+    const int64_t d = x - P0;
+    return (int32_t)max(min(d, (int64_t)INT32_MAX - 1), (int64_t)INT32_MIN + 1);
+}
+
+// per chunk: the span [cbeg, cend) of the columns its reads cover, clamped to the batch
+__global__ __launch_bounds__(256) void k_f2_span(FillArgs A, F2Lay L) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q > L.n_chunks) return;
+    if (q == L.n_chunks) {                                        // (the scan's last element)
+        if (lane == 0) L.span[q] = 0;
+        return;
+    }
+    const uint64_t r = (uint64_t)q * 64 + (uint64_t)lane;
+    const bool valid = r < A.n_reads;
+    const int32_t rp = valid ? f2_rel(A.rpos[r], A.pos_begin) : INT32_MAX;
+    const int32_t re = valid ? f2_rel(A.rend[r], A.pos_begin) : INT32_MIN;
+    const int32_t cb = min(max(__builtin_amdgcn_readfirstlane(rp), 0), A.n_cols);
+    int32_t ce = min(re, A.n_cols);
+    for (int o = 32; o; o >>= 1) ce = max(ce, __shfl_xor(ce, o));
+    ce = max(ce, cb);
+    if (lane == 0) {
+        L.cbeg[q] = cb;
+        L.cend[q] = ce;
+        L.span[q] = (uint32_t)(ce - cb);
+    }
+}
+
+// per chunk: covering reads per column of its span, into its row
+__global__ __launch_bounds__(256) void k_f2_count(FillArgs A, F2Lay L) {
+    const int lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= L.n_chunks) return;
+    const uint64_t r = (uint64_t)q * 64 + (uint64_t)lane;
+    const bool valid = r < A.n_reads;
+    const int32_t rp = valid ? f2_rel(A.rpos[r], A.pos_begin) : INT32_MAX;
+    const int32_t re = valid ? f2_rel(A.rend[r], A.pos_begin) : INT32_MIN;
+    const int32_t cb = L.cbeg[q], ce = L.cend[q];
+    if ((uint64_t)L.row[q] + (uint64_t)(ce - cb) > L.span_cap) return;   // (k_f2_base reports it)
+    uint8_t *const row = L.cnt + L.row[q];
+    const int nr = (int)min((uint64_t)64, A.n_reads - (uint64_t)q * 64);
+    for (int32_t c0 = cb; c0 < ce; c0 += 64) {
+        const int32_t c = c0 + lane;
+        uint32_t n = 0;
+        for (int k = 0; k < nr; k++) {
+            const int32_t x = __builtin_amdgcn_readlane(rp, k), e = __builtin_amdgcn_readlane(re, k);
+            n += (uint32_t)(c >= x && c < e);
+        }
+        if (c < ce) row[c - cb] = (uint8_t)n;
+    }
+}
+
+// per 64-column tile (lane = column): running sums along the chunks that cover each column; the total must be the
+// column's entry count
+__global__ __launch_bounds__(256) void k_f2_base(FillArgs A, F2Lay L) {
+    const int lane = threadIdx.x & 63;
+    const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int32_t c_lo = (int32_t)(t * 64);
+    if (c_lo >= A.n_cols) return;
+    const int32_t c_hi = min(c_lo + 63, A.n_cols - 1), c = c_lo + lane;
+    uint32_t run = 0;
+    if (L.n_chunks == 0) {
+        if (c < A.n_cols && A.off[c + 1] != A.off[c]) atomicOr(A.err, 2u);
+        return;
+    }
+    // chunks that may cover the tile: from the one before the first whose span starts past c_lo - max_span, to the last
+    // whose span starts at or before c_hi (cbeg is non-decreasing: the reads are in coordinate order)
+    auto first_gt = [&](int64_t v) {                              // first chunk with cbeg > v
+        int64_t lo = 0, hi = L.n_chunks;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)L.cbeg[mid] > v) hi = mid; else lo = mid + 1;
+        }
+        return lo;
+    };
+    const int64_t qa = max(first_gt((int64_t)c_lo - (int64_t)A.back * 64 - 1) - 1, (int64_t)0);
+    const int64_t qb = first_gt(c_hi);                            // (exclusive)
+    if ((uint64_t)L.row[L.n_chunks] > L.span_cap) {              // (a plan whose max_span understates a read's span)
+        if (lane == 0) atomicOr(A.err, 2u);
+        return;
+    }
+    int32_t ncb = 0, nce = 0;
+    uint32_t nro = 0;
+    if (qa < qb) { ncb = L.cbeg[qa]; nce = L.cend[qa]; nro = L.row[qa]; }
+    for (int64_t q = qa; q < qb; q++) {
+        const int32_t cb = ncb, ce = nce;
+        const uint32_t ro = nro;
+        if (q + 1 < qb) { ncb = L.cbeg[q + 1]; nce = L.cend[q + 1]; nro = L.row[q + 1]; }
+        if (c >= cb && c < ce) {
+            L.base[ro + (uint32_t)(c - cb)] = run;
+            run += L.cnt[ro + (uint32_t)(c - cb)];
+        }
+    }
+    if (c < A.n_cols && (uint64_t)run != A.off[c + 1] - A.off[c]) atomicOr(A.err, 2u);
+}
+
+// the chunk's entries: lanes = reads, columns of the span in order
+__global__ __launch_bounds__(256) void k_f2_fill(FillArgs A, F2Lay L) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs; consecutive chunks (which write adjacent runs of
+    // the same columns) land on one XCD
+    const uint32_t nb = gridDim.x, per = nb >> 3, b = blockIdx.x;
+    const uint32_t blk = (b < (per << 3)) ? (b & 7) * per + (b >> 3) : b;
+    const int64_t q = (int64_t)blk * 4 + w;
+    if (q >= L.n_chunks) return;                                  // (wave-uniform; no barrier below)
+    const uint64_t r = (uint64_t)q * 64 + (uint64_t)lane;
+    bool valid = r < A.n_reads;
+    const int32_t cb = L.cbeg[q], ce = L.cend[q];
+    const uint32_t ro = L.row[q];
+    if ((uint64_t)L.row[L.n_chunks] > L.span_cap) return;        // (k_f2_base reports it)
+    int32_t rp = INT32_MAX, re = INT32_MIN, tc = INT32_MIN;
+    uint32_t ncig = 0, ls = 0, bad = 0;
+    uint64_t co = 0, qo = 0, so = 0, oq = 0;
+    if (valid) {
+        rp = f2_rel(A.rpos[r], A.pos_begin);
+        re = f2_rel(A.rend[r], A.pos_begin);
+        const uint64_t rr = min(A.rec[r], A.data_bytes);          // (the host checked rec + 36 <= data_bytes)
+        const uint32_t l_name = ld32u(A.data, rr + 8) & 0xFF;
+        ncig = ld32u(A.data, rr + 12) & 0xFFFF;
+        ls = ld32u(A.data, rr + 16);
+        co = rr + 32 + l_name;
+        so = co + 4ull * ncig;
+        qo = so + (ls + 1) / 2;
+        if (ncig == 0 || ls > (1u << 30) || qo + ls > A.data_bytes) { bad = 1; valid = false; }
+        const int32_t tw = A.tweak[r];
+        if (valid && tw >= 0) {
+            tc = f2_rel(A.tw_col[tw], A.pos_begin);
+            oq = A.tw_q[tw];
+            if (oq + ls > A.orig_bytes) { bad = 1; valid = false; }
+        }
+    }
+    if (!valid) { rp = INT32_MAX; re = INT32_MIN; }
+    // the CIGAR cursor: op k (15: past the end) of ref length / query length L at ref column x, query offset y
+    uint32_t o = 0, k = 15, len = 0, nxt = 0;
+    int32_t x = rp;
+    uint32_t y = 0;
+    if (valid) {
+        nxt = ld32u(A.data, co);
+        k = nxt & 15u;
+        len = nxt >> 4;
+        nxt = ncig > 1 ? ld32u(A.data, co + 4) : 0u;
+    }
+    auto advance = [&]() {                                        // to the next op (the following one preloaded)
+        if (eats_ref(k)) x += (int32_t)len;
+        if (eats_query(k)) y += len;
+        o++;
+        if (o < ncig) {
+            k = nxt & 15u;
+            len = nxt >> 4;
+            nxt = o + 1 < ncig ? ld32u(A.data, co + 4ull * (o + 1)) : 0u;
+        } else {
+            k = 15;
+            len = 0;
+        }
+    };
+    // 8-byte windows of the qualities and the packed bases, the next one in flight
+    typedef __attribute__((address_space(1))) const uint64_t gu64;
+    auto ld8 = [&](uint64_t a) -> uint64_t { return *(gu64 *)(const void *)(A.data + a); };
+    uint64_t qwa = qo & ~7ull, swa = so & ~7ull, qwin = 0, qnx = 0, swin = 0, snx = 0;
+    if (valid) {
+        qwin = ld8(qwa); qnx = ld8(qwa + 8);
+        swin = ld8(swa); snx = ld8(swa + 8);
+    }
+    const uint64_t below = ((uint64_t)1 << lane) - 1;
+    for (int32_t c0 = cb; c0 < ce; c0 += 64) {
+        // the next 64 columns' CSR offsets and chunk bases, one per lane (read per column with readlane)
+        uint64_t offv = 0;
+        uint32_t basev = 0;
+        if (c0 + lane < ce) {
+            offv = A.off[c0 + lane];
+            basev = L.base[ro + (uint32_t)(c0 + lane - cb)];
+        }
+        const int32_t nc = min(64, ce - c0);
+        for (int32_t j = 0; j < nc; j++) {
+            const int32_t c = c0 + j;
+            bool cov = c >= rp && c < re;
+            uint32_t cd = 0, qv = 0;
+            if (cov) {
+                while (k != 15 && (!eats_ref(k) || c >= x + (int32_t)len)) advance();
+                if (k == 15) {                                    // the CIGAR ends before the column
+                    bad = 1;
+                    cov = false;
+                } else if (k == 2 || k == 3) {                    // D / N: the next query base's quality
+                    cd = k == 2 ? 16u : 17u;
+                    if (y < ls) {
+                        if (c < tc) {
+                            qv = ((const __attribute__((address_space(1))) uint8_t *)(const void *)A.orig)[oq + y];
+                        } else {
+                            const uint64_t a = qo + y;
+                            if (a - qwa >= 8) {
+                                if (a - qwa < 16) { qwin = qnx; qwa += 8; } else { qwa = a & ~7ull; qwin = ld8(qwa); }
+                                qnx = ld8(qwa + 8);
+                            }
+                            qv = (uint32_t)(qwin >> (8 * (a - qwa))) & 0xFFu;
+                        }
+                    }
+                } else {
+                    const uint32_t qp = y + (uint32_t)(c - x);
+                    if (qp < ls) {
+                        const uint64_t a = qo + qp, sa = so + (qp >> 1);
+                        if (a - qwa >= 8) {
+                            if (a - qwa < 16) { qwin = qnx; qwa += 8; } else { qwa = a & ~7ull; qwin = ld8(qwa); }
+                            qnx = ld8(qwa + 8);
+                        }
+                        if (sa - swa >= 8) {
+                            if (sa - swa < 16) { swin = snx; swa += 8; } else { swa = sa & ~7ull; swin = ld8(swa); }
+                            snx = ld8(swa + 8);
+                        }
+                        qv = (uint32_t)(qwin >> (8 * (a - qwa))) & 0xFFu;
+                        const uint32_t sb = (uint32_t)(swin >> (8 * (sa - swa))) & 0xFFu;
+                        cd = (qp & 1) ? (sb & 15u) : (sb >> 4);
+                    } else {
+                        cd = 15u;                                 // (a CIGAR longer than the sequence)
+                    }
+                }
+            }
+            const uint64_t m = __ballot(cov);
+            const uint64_t at = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(offv >> 32), j) << 32 |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)offv, j)) +
+                                (uint32_t)__builtin_amdgcn_readlane((int)basev, j) + (uint64_t)__builtin_popcountll(m & below);
+            if (cov) {
+                A.code[at] = (uint8_t)cd;
+                A.qual[at] = (uint8_t)qv;
+            }
+        }
+    }
+    if (__ballot(bad) && lane == 0) atomicOr(A.err, 2u);
+}
+
 namespace {
 int32_t fill_group(int64_t n_tiles, int64_t n_reads, int32_t back, int64_t *items_cap) {
     // items <= n_tiles + n_reads (back + 1) / fg (a read is in back + 1 tiles' read ranges); group starts take 256 B per
@@ -379,13 +662,33 @@ FillLay fill_layout(void *base, int64_t n_tiles, int64_t n_reads, int32_t back, 
 
 size_t fill_scratch_bytes(int64_t n_cols, int64_t n_reads, int64_t max_span) {
     const int64_t n_tiles = (n_cols + 63) / 64;
+    const int32_t back = (int32_t)((max_span + 63) / 64);
+    if (f2_span_cap(n_cols, n_reads, back) <= F2_SPAN_LIMIT) return f2_bytes(n_cols, n_reads, back);
     int32_t fg = 0;
-    FillLay L = fill_layout(nullptr, n_tiles, n_reads, (int32_t)((max_span + 63) / 64), &fg);
+    FillLay L = fill_layout(nullptr, n_tiles, n_reads, back, &fg);
     return al256(4 * (size_t)(n_tiles + 1)) * 2 + al256(L.scan_bytes) + al256(256 * (size_t)L.items_cap) + 256;
 }
 
 hipError_t launch_pileup_fill(const FillArgs &A, hipStream_t st) {
     if (A.n_tiles <= 0) return hipSuccess;
+    if (f2_span_cap(A.n_cols, A.n_reads, A.back) <= F2_SPAN_LIMIT) {
+        // the transposed fill: spans, scan into row offsets, counts, bases, entries
+        F2Lay L = f2_layout(A.scratch, A.n_cols, A.n_reads, A.back);
+        if (L.n_chunks == 0) {                   // no reads: every column must be empty (k_f2_base checks)
+            k_f2_base<<<(unsigned)((A.n_tiles + 3) / 4), 256, 0, st>>>(A, L);
+            return hipGetLastError();
+        }
+        k_f2_span<<<(unsigned)((L.n_chunks + 1 + 3) / 4), 256, 0, st>>>(A, L);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        e = hipcub::DeviceScan::ExclusiveSum(L.scan_tmp, L.scan_bytes, L.span, L.row, (int)(L.n_chunks + 1), st);
+        if (e != hipSuccess) return e;
+        const unsigned cb = (unsigned)((L.n_chunks + 3) / 4);
+        k_f2_count<<<cb, 256, 0, st>>>(A, L);
+        k_f2_base<<<(unsigned)((A.n_tiles + 3) / 4), 256, 0, st>>>(A, L);
+        k_f2_fill<<<(unsigned)((cb + 7) & ~7u), 256, 0, st>>>(A, L);
+        return hipGetLastError();
+    }
     int32_t fg = 0;
     FillLay L = fill_layout(A.scratch, A.n_tiles, A.n_reads, A.back, &fg);
     k_tile_first<<<(unsigned)((A.n_reads + 1 + 255) / 256), 256, 0, st>>>(A, L.tile_first);
