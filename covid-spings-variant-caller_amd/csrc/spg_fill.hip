@@ -533,17 +533,12 @@ __global__ __launch_bounds__(256) void k_f2_fill(FillArgs A, F2Lay L) {
         }
     }
     if (!valid) { rp = INT32_MAX; re = INT32_MIN; }
-    // the CIGAR cursor: op k (15: past the end) of ref length / query length L at ref column x, query offset y
+    // the CIGAR cursor, kept on a reference-consuming op (M / D / N / = / X; 15: past the CIGAR's end): op k of length
+    // len covering ref columns [x, xe), query offset y at its start; the next op preloaded
     uint32_t o = 0, k = 15, len = 0, nxt = 0;
-    int32_t x = rp;
+    int32_t x = rp, xe = rp;
     uint32_t y = 0;
-    if (valid) {
-        nxt = ld32u(A.data, co);
-        k = nxt & 15u;
-        len = nxt >> 4;
-        nxt = ncig > 1 ? ld32u(A.data, co + 4) : 0u;
-    }
-    auto advance = [&]() {                                        // to the next op (the following one preloaded)
+    auto step = [&]() {                                           // to the next op
         if (eats_ref(k)) x += (int32_t)len;
         if (eats_query(k)) y += len;
         o++;
@@ -556,7 +551,15 @@ __global__ __launch_bounds__(256) void k_f2_fill(FillArgs A, F2Lay L) {
             len = 0;
         }
     };
-    // 8-byte windows of the qualities and the packed bases, the next one in flight
+    if (valid) {
+        nxt = ld32u(A.data, co);
+        k = nxt & 15u;
+        len = nxt >> 4;
+        nxt = ncig > 1 ? ld32u(A.data, co + 4) : 0u;
+        while (k != 15 && !eats_ref(k)) step();
+        xe = x + (int32_t)len;
+    }
+    // 8-byte windows of the qualities and the packed bases, the next one in flight; offsets into them in 32 bits
     typedef __attribute__((address_space(1))) const uint64_t gu64;
     auto ld8 = [&](uint64_t a) -> uint64_t { return *(gu64 *)(const void *)(A.data + a); };
     uint64_t qwa = qo & ~7ull, swa = so & ~7ull, qwin = 0, qnx = 0, swin = 0, snx = 0;
@@ -564,53 +567,52 @@ __global__ __launch_bounds__(256) void k_f2_fill(FillArgs A, F2Lay L) {
         qwin = ld8(qwa); qnx = ld8(qwa + 8);
         swin = ld8(swa); snx = ld8(swa + 8);
     }
+    const uint32_t qo32 = (uint32_t)qo, so32 = (uint32_t)so;
+    // the quality byte at query offset p (windows only move forward)
+    auto qual_at = [&](uint32_t p) -> uint32_t {
+        uint32_t d = qo32 + p - (uint32_t)qwa;
+        if (d >= 8) {
+            if (d < 16) { qwin = qnx; qwa += 8; } else { qwa = (qo + p) & ~7ull; qwin = ld8(qwa); }
+            qnx = ld8(qwa + 8);
+            d = qo32 + p - (uint32_t)qwa;
+        }
+        return (uint32_t)(qwin >> (8 * d)) & 0xFFu;
+    };
     const uint64_t below = ((uint64_t)1 << lane) - 1;
     for (int32_t c0 = cb; c0 < ce; c0 += 64) {
-        // the next 64 columns' CSR offsets and chunk bases, one per lane (read per column with readlane)
-        uint64_t offv = 0;
-        uint32_t basev = 0;
-        if (c0 + lane < ce) {
-            offv = A.off[c0 + lane];
-            basev = L.base[ro + (uint32_t)(c0 + lane - cb)];
-        }
+        // the next 64 columns' first entry of this chunk (CSR offset + the earlier chunks' entries), one per lane
+        uint64_t at0 = 0;
+        if (c0 + lane < ce) at0 = A.off[c0 + lane] + L.base[ro + (uint32_t)(c0 + lane - cb)];
+        const uint32_t at_lo = (uint32_t)at0, at_hi = (uint32_t)(at0 >> 32);
         const int32_t nc = min(64, ce - c0);
         for (int32_t j = 0; j < nc; j++) {
             const int32_t c = c0 + j;
             bool cov = c >= rp && c < re;
             uint32_t cd = 0, qv = 0;
             if (cov) {
-                while (k != 15 && (!eats_ref(k) || c >= x + (int32_t)len)) advance();
+                if (c >= xe) {                                    // (rare) the next reference-consuming op
+                    do step(); while (k != 15 && (!eats_ref(k) || c >= x + (int32_t)len));
+                    xe = x + (int32_t)len;
+                }
                 if (k == 15) {                                    // the CIGAR ends before the column
                     bad = 1;
                     cov = false;
                 } else if (k == 2 || k == 3) {                    // D / N: the next query base's quality
-                    cd = k == 2 ? 16u : 17u;
-                    if (y < ls) {
-                        if (c < tc) {
-                            qv = ((const __attribute__((address_space(1))) uint8_t *)(const void *)A.orig)[oq + y];
-                        } else {
-                            const uint64_t a = qo + y;
-                            if (a - qwa >= 8) {
-                                if (a - qwa < 16) { qwin = qnx; qwa += 8; } else { qwa = a & ~7ull; qwin = ld8(qwa); }
-                                qnx = ld8(qwa + 8);
-                            }
-                            qv = (uint32_t)(qwin >> (8 * (a - qwa))) & 0xFFu;
-                        }
-                    }
+                    cd = 14u + k;
+                    if (y < ls)
+                        qv = c < tc ? ((const __attribute__((address_space(1))) uint8_t *)(const void *)A.orig)[oq + y]
+                                    : qual_at(y);
                 } else {
                     const uint32_t qp = y + (uint32_t)(c - x);
                     if (qp < ls) {
-                        const uint64_t a = qo + qp, sa = so + (qp >> 1);
-                        if (a - qwa >= 8) {
-                            if (a - qwa < 16) { qwin = qnx; qwa += 8; } else { qwa = a & ~7ull; qwin = ld8(qwa); }
-                            qnx = ld8(qwa + 8);
-                        }
-                        if (sa - swa >= 8) {
-                            if (sa - swa < 16) { swin = snx; swa += 8; } else { swa = sa & ~7ull; swin = ld8(swa); }
+                        qv = qual_at(qp);
+                        uint32_t d = so32 + (qp >> 1) - (uint32_t)swa;
+                        if (d >= 8) {
+                            if (d < 16) { swin = snx; swa += 8; } else { swa = (so + (qp >> 1)) & ~7ull; swin = ld8(swa); }
                             snx = ld8(swa + 8);
+                            d = so32 + (qp >> 1) - (uint32_t)swa;
                         }
-                        qv = (uint32_t)(qwin >> (8 * (a - qwa))) & 0xFFu;
-                        const uint32_t sb = (uint32_t)(swin >> (8 * (sa - swa))) & 0xFFu;
+                        const uint32_t sb = (uint32_t)(swin >> (8 * d)) & 0xFFu;
                         cd = (qp & 1) ? (sb & 15u) : (sb >> 4);
                     } else {
                         cd = 15u;                                 // (a CIGAR longer than the sequence)
@@ -618,9 +620,8 @@ __global__ __launch_bounds__(256) void k_f2_fill(FillArgs A, F2Lay L) {
                 }
             }
             const uint64_t m = __ballot(cov);
-            const uint64_t at = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(offv >> 32), j) << 32 |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)offv, j)) +
-                                (uint32_t)__builtin_amdgcn_readlane((int)basev, j) + (uint64_t)__builtin_popcountll(m & below);
+            const uint64_t at = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)at_hi, j) << 32 |
+                                 (uint32_t)__builtin_amdgcn_readlane((int)at_lo, j)) + (uint64_t)__builtin_popcountll(m & below);
             if (cov) {
                 A.code[at] = (uint8_t)cd;
                 A.qual[at] = (uint8_t)qv;

@@ -12,10 +12,12 @@ for f in sorted(glob.glob(os.path.join(OUT, '**', '*counter_collection.csv'), re
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(f)):
         k = r.get('Kernel_Name', '')
-        for key in ('k_inflate', 'k_pileup_fill', 'k_tile_first', 'k_acc_seg<4', 'k_fill(', 'k_fill<', 'k_fill_starts',
-                    'k_crc32', 'k_bam_'):
+        for key in ('k_inflate_par', 'k_inflate(', 'k_pileup_fill', 'k_tile_first', 'k_acc_seg<4', 'k_fill(', 'k_fill<',
+                    'k_fill_starts', 'k_f2_fill', 'k_f2_count', 'k_f2_base', 'k_crc32', 'k_bam_'):
             if key in k:
                 acc[(key, r['Counter_Name'])][r['Dispatch_Id']] += float(r['Counter_Value'])
     print('==', os.path.relpath(f, OUT))
     for (k, c), d in sorted(acc.items()):
-        print(f"  {k:16s} {c:12s} mean per dispatch {sum(d.values())/len(d):.4g} (x2 gfx950 correction for FETCH: {2*sum(d.values())/len(d):.4g}) dispatches {len(d)}")
+        m = sum(d.values()) / len(d)
+        corr = f" (x2 gfx950 correction: {2 * m:.4g})" if c.startswith("FETCH") else ""
+        print(f"  {k:16s} {c:12s} mean per dispatch {m:.4g} KB{corr} dispatches {len(d)}")
