@@ -186,6 +186,7 @@ def gpu_lib():
     _sig(L.spg_history_info, i32, vp, i64, C.POINTER(i64), C.POINTER(i64), C.POINTER(u64))
     _sig(L.spg_history_copy, i32, vp, i64, vp, vp, vp)
     _sig(L.spg_history_copy_compact, i32, vp, i64, i32, vp, vp, vp, C.POINTER(u64))
+    _sig(L.spg_history_copy_packed, i32, vp, i64, i32, vp, vp, C.POINTER(C.c_uint64), vp, vp, vp, i64, C.POINTER(i64))
     _sig(L.spg_device_count, i32, C.POINTER(i32))
     _sig(L.spg_sizeof_candidate, C.c_size_t)
     _sig(L.spg_sizeof_detail, C.c_size_t)

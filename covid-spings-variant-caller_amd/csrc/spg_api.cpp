@@ -45,6 +45,8 @@ hipError_t launch_pos_copy(const Hist *H, const int32_t *items, int32_t n, const
                            uint8_t *oc, uint8_t *oq, hipStream_t st);
 hipError_t launch_ck_compact(const Hist &h, uint32_t min_bq, uint64_t *kept, uint64_t *noff, void *scan_tmp,
                              size_t *scan_bytes, uint8_t *oc, uint8_t *oq, hipStream_t st);
+hipError_t launch_ck_pack(uint8_t *oc, const uint8_t *oq, uint64_t m, uint64_t base, uint64_t *xi, uint8_t *xc, uint8_t *xq,
+                          uint32_t *xn, uint32_t xcap, hipStream_t st);
 size_t inflate_scratch_bytes(uint64_t comp_bytes, int64_t n);
 hipError_t launch_inflate(const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *mem, int64_t n, uint8_t *out,
                           uint32_t *status, void *scratch, hipStream_t st);
@@ -2043,8 +2045,11 @@ int spg_history_resident(spg_ctx *c, int64_t *device_bytes, int64_t *n_spilled, 
 // Batch i as the checkpoint keeps it (live_variant_caller.py:40-45, :89, :77-85): the entries with q >= min_bq plus a
 // first-entry marker per column whose entries all fail it, compacted on the device (spg_ckpt.hip) in column ranges of
 // at most ~256 M entries (bounded scratch); only the kept bytes cross PCIe.
-int spg_history_copy_compact(spg_ctx *c, int64_t i, int32_t min_bq, uint64_t *offsets, uint8_t *base_code, uint8_t *qual,
-                             uint64_t *n_kept) {
+// spg_history_copy_compact and spg_history_copy_packed: the compaction in HBM, then either both arrays down or, packed,
+// one byte per entry (k_ck_pack) plus the exception list
+static int history_compact(spg_ctx *c, int64_t i, int32_t min_bq, uint64_t *offsets, uint8_t *base_code, uint8_t *qual,
+                           uint64_t *n_kept, uint8_t *packed, uint64_t *exc_index, uint8_t *exc_code, uint8_t *exc_qual,
+                           int64_t exc_cap, int64_t *n_exc) {
     if (!c || !offsets || !n_kept) return fail("spg_history_copy_compact: null argument");
     if (i < 0 || i >= (int64_t)c->hist.size()) return fail("spg_history_copy_compact: batch index out of range");
     if (min_bq < 0 || min_bq > 256) return fail("spg_history_copy_compact: min_bq out of range");
@@ -2055,7 +2060,9 @@ int spg_history_copy_compact(spg_ctx *c, int64_t i, int32_t min_bq, uint64_t *of
     // the batch's offsets first (the chunk boundaries come from them), then overwritten by the compact ones
     HIPCHK(hipMemcpyAsync(offsets, h.off, sizeof(uint64_t) * (h.n_cols + 1), hipMemcpyDefault, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    if (h.n_entries && (!base_code || !qual)) return fail("spg_history_copy_compact: null output buffer");
+    if (h.n_entries && !packed && (!base_code || !qual)) return fail("spg_history_copy_compact: null output buffer");
+    if (h.n_entries && packed && exc_cap > 0 && (!exc_index || !exc_code || !exc_qual))
+        return fail("spg_history_copy_packed: null exception buffer");
     const uint64_t chunk_entries = (uint64_t)256 << 20;
     std::vector<int64_t> cuts{0};
     for (int64_t k = 0; k < h.n_cols;) {
@@ -2080,10 +2087,17 @@ int spg_history_copy_compact(spg_ctx *c, int64_t i, int32_t min_bq, uint64_t *of
     HIPCHK(launch_ck_compact(probe, 0, nullptr, nullptr, nullptr, &scan_bytes, nullptr, nullptr, c->stream));
     const size_t ob = ((sizeof(uint64_t) * (size_t)(max_cols + 1)) + 255) & ~size_t(255);
     const size_t sb = (scan_bytes + 255) & ~size_t(255), eb = ((size_t)max_e + 255) & ~size_t(255);
-    if (int rc = grow_scratch(c, 2 * ob + sb + 2 * eb)) return rc;
+    // (packed: a device exception list of up to 1 Mi entries; more than the caller's capacity reports the count only)
+    const uint32_t xcap = packed ? (uint32_t)std::min<int64_t>(std::max<int64_t>(exc_cap, 0), (int64_t)1 << 20) : 0u;
+    const size_t xb = packed ? (((size_t)xcap * 10 + 256 + 255) & ~size_t(255)) : 0;
+    if (int rc = grow_scratch(c, 2 * ob + sb + 2 * eb + xb)) return rc;
     uint64_t *kept = reinterpret_cast<uint64_t *>(c->pe_buf), *noff = reinterpret_cast<uint64_t *>(c->pe_buf + ob);
     void *tmp = c->pe_buf + 2 * ob;
     uint8_t *oc = c->pe_buf + 2 * ob + sb, *oq = oc + eb;
+    uint32_t *xn = reinterpret_cast<uint32_t *>(oq + eb);
+    uint64_t *xi = reinterpret_cast<uint64_t *>(oq + eb + 256);
+    uint8_t *xc = reinterpret_cast<uint8_t *>(xi + xcap), *xq = xc + xcap;
+    if (packed) HIPCHK(hipMemsetAsync(xn, 0, sizeof(uint32_t), c->stream));
     std::vector<uint64_t> loc((size_t)max_cols + 1);
     uint64_t base = 0;
     for (size_t k = 1; k < cuts.size(); k++) {
@@ -2094,7 +2108,10 @@ int spg_history_copy_compact(spg_ctx *c, int64_t i, int32_t min_bq, uint64_t *of
         HIPCHK(hipMemcpyAsync(loc.data(), noff, sizeof(uint64_t) * (size_t)(n + 1), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         const uint64_t m = loc[(size_t)n];
-        if (m) {
+        if (m && packed) {
+            HIPCHK(launch_ck_pack(oc, oq, m, base, xi, xc, xq, xn, xcap, c->stream));
+            HIPCHK(hipMemcpyAsync(packed + base, oc, m, hipMemcpyDeviceToHost, c->stream));
+        } else if (m) {
             HIPCHK(hipMemcpyAsync(base_code + base, oc, m, hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipMemcpyAsync(qual + base, oq, m, hipMemcpyDeviceToHost, c->stream));
         }
@@ -2104,8 +2121,36 @@ int spg_history_copy_compact(spg_ctx *c, int64_t i, int32_t min_bq, uint64_t *of
     }
     offsets[h.n_cols] = base;
     *n_kept = base;
+    if (packed) {
+        uint32_t nx = 0;
+        HIPCHK(hipMemcpyAsync(&nx, xn, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        *n_exc = nx;
+        if ((int64_t)nx <= exc_cap && nx <= xcap && nx) {
+            HIPCHK(hipMemcpyAsync(exc_index, xi, sizeof(uint64_t) * nx, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(exc_code, xc, nx, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(exc_qual, xq, nx, hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+        } else if (nx > xcap) {
+            *n_exc = std::max<int64_t>((int64_t)nx, exc_cap + 1);   // (more than the device list held: not usable)
+        }
+    }
     return 0;
 }
+
+int spg_history_copy_compact(spg_ctx *c, int64_t i, int32_t min_bq, uint64_t *offsets, uint8_t *base_code, uint8_t *qual,
+                             uint64_t *n_kept) {
+    return history_compact(c, i, min_bq, offsets, base_code, qual, n_kept, nullptr, nullptr, nullptr, nullptr, 0, nullptr);
+}
+
+int spg_history_copy_packed(spg_ctx *c, int64_t i, int32_t min_bq, uint64_t *offsets, uint8_t *packed, uint64_t *n_kept,
+                            uint64_t *exc_index, uint8_t *exc_code, uint8_t *exc_qual, int64_t exc_cap, int64_t *n_exc) {
+    if (!packed || !n_exc) return fail("spg_history_copy_packed: null argument");
+    *n_exc = 0;
+    return history_compact(c, i, min_bq, offsets, nullptr, nullptr, n_kept, packed, exc_index, exc_code, exc_qual, exc_cap,
+                           n_exc);
+}
+
 
 int spg_history_copy(spg_ctx *c, int64_t i, uint64_t *offsets, uint8_t *base_code, uint8_t *qual) {
     if (!c) return fail("spg_history_copy: null ctx");

@@ -111,6 +111,37 @@ __global__ __launch_bounds__(256) void k_ck_scatter(Hist h, uint32_t min_bq, con
     }
 }
 
+// One byte per compacted entry for the packed checkpoint: base A/C/G/T (BAM nibbles 1/2/4/8) as 2 bits over a 6-bit
+// quality 0..62; any other code or a quality >= 63 is an exception — its byte is 63 and (index, code, quality) goes to
+// the exception list (slot from an atomic counter: the index makes the order irrelevant).  In place over the codes.
+__global__ __launch_bounds__(256) void k_ck_pack(uint8_t *__restrict__ oc, const uint8_t *__restrict__ oq, uint64_t m,
+                                                 uint64_t base, uint64_t *__restrict__ xi, uint8_t *__restrict__ xc,
+                                                 uint8_t *__restrict__ xq, uint32_t *__restrict__ xn, uint32_t xcap) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+        const uint32_t c = oc[i], q = oq[i];
+        const uint32_t b2 = c == 1 ? 0u : c == 2 ? 1u : c == 4 ? 2u : c == 8 ? 3u : 4u;
+        const bool esc = b2 == 4u || q >= 63u;
+        if (esc) {
+            const uint32_t k = atomicAdd(xn, 1u);
+            if (k < xcap) {
+                xi[k] = base + i;
+                xc[k] = (uint8_t)c;
+                xq[k] = (uint8_t)q;
+            }
+        }
+        oc[i] = esc ? (uint8_t)63 : (uint8_t)(b2 << 6 | q);
+    }
+}
+
+hipError_t launch_ck_pack(uint8_t *oc, const uint8_t *oq, uint64_t m, uint64_t base, uint64_t *xi, uint8_t *xc, uint8_t *xq,
+                          uint32_t *xn, uint32_t xcap, hipStream_t st) {
+    if (m == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((m + 255) / 256, 16384);
+    k_ck_pack<<<blocks, 256, 0, st>>>(oc, oq, m, base, xi, xc, xq, xn, xcap);
+    return hipGetLastError();
+}
+
 hipError_t launch_ck_compact(const Hist &h, uint32_t min_bq, uint64_t *kept, uint64_t *noff, void *scan_tmp,
                              size_t *scan_bytes, uint8_t *oc, uint8_t *oq, hipStream_t st) {
     // scan_tmp null: only the scan's scratch size

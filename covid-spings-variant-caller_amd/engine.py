@@ -404,6 +404,36 @@ class PileupEngine:
                     codes, quals = codes[:k.value], quals[:k.value]   # (pages past k never touched)
             yield pb.value, off, codes, quals
 
+    def iter_history_packed(self, start: int, min_bq: int, exc_cap: int = 1 << 20):
+        """The batches as create_checkpoint writes them, packed (spg_history_copy_packed): per batch a dict of the
+        compact CSR offsets, one byte per kept entry and the exception list (index, code, quality) of the entries the
+        byte cannot hold — or, when the exceptions exceed exc_cap, the unpacked codes / quals.  Arrays are views of
+        pinned staging, valid until the next batch is yielded."""
+        n = self.history_count()
+        for i in range(max(0, int(start)), n):
+            with self._lock:
+                pb, nc, ne = C.c_int64(), C.c_int64(), C.c_uint64()
+                N.check(self._L.spg_history_info(self._h, i, C.byref(pb), C.byref(nc), C.byref(ne)), "spg_history_info")
+                off, packed, _ = self._staging(nc.value + 1, ne.value)
+                xs = getattr(self, "_xstage", None)
+                if xs is None or len(xs[1]) < exc_cap:
+                    xs = (pinned_empty(exc_cap, np.uint64), pinned_empty(exc_cap), pinned_empty(exc_cap))
+                    self._xstage = xs
+                k, nx = C.c_uint64(), C.c_int64()
+                N.check(self._L.spg_history_copy_packed(self._h, i, int(min_bq), N.ptr(off), N.ptr(packed), C.byref(k),
+                                                        N.ptr(xs[0]), N.ptr(xs[1]), N.ptr(xs[2]), int(exc_cap),
+                                                        C.byref(nx)), "spg_history_copy_packed")
+                if nx.value <= exc_cap:
+                    m = nx.value
+                    ent = {"pos": pb.value, "off": off, "packed": packed[:k.value], "xi": xs[0][:m], "xc": xs[1][:m],
+                           "xq": xs[2][:m]}
+                else:
+                    off, codes, quals = self._staging(nc.value + 1, ne.value)
+                    N.check(self._L.spg_history_copy_compact(self._h, i, int(min_bq), N.ptr(off), N.ptr(codes),
+                                                             N.ptr(quals), C.byref(k)), "spg_history_copy_compact")
+                    ent = {"pos": pb.value, "off": off, "codes": codes[:k.value], "quals": quals[:k.value]}
+            yield ent
+
     def _staging(self, n_off: int, n_entries: int):
         """Pinned host views (offsets, codes, quals) for history copies, grown as needed and reused."""
         st = getattr(self, "_stage", None)

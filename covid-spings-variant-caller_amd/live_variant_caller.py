@@ -517,9 +517,11 @@ class LiveVariantCaller:
             if first < n:
                 shard = f"spgck-{self._ck_token[:16]}-{first}-{n - first}.spgck"
                 path = os.path.join(d, shard)
-                staged = isinstance(self.engine, PileupEngine)
-                self.last_checkpoint_bytes = _write_shard(
-                    path, self.engine.iter_history(first, min_bq=self.minBaseQuality, **({"staged": True} if staged else {})))
+                # a single-device engine packs the kept entries one byte each on the GPU (A/C/G/T with q < 63; the rest
+                # as exceptions): half the bytes down and on disk
+                it = (self.engine.iter_history_packed(first, self.minBaseQuality) if isinstance(self.engine, PileupEngine)
+                      else self.engine.iter_history(first, min_bq=self.minBaseQuality))
+                self.last_checkpoint_bytes = _write_shard(path, it)
                 shards.append((shard, first, n - first))
             self._ck_chain[d] = list(shards)
             old = _read_manifest(filename)
@@ -634,17 +636,22 @@ _SHARD_MAGIC, _SHARD_END = b"SPGCKv1\0", b"SPGCKEND"
 
 
 def _write_shard(path: str, batches) -> int:
-    """A checkpoint shard: each batch's offsets / codes / quals written as they come (64-B aligned raw arrays, no
-    per-array CRC or copy — np.savez's zip CRC and buffer copies took most of a 10,000x BAM's checkpoint), then a JSON
-    index and its offset.  Written to <path>.tmp and renamed.  Returns the file's size."""
+    """A checkpoint shard: each batch's arrays written as they come (64-B aligned raw arrays, no per-array CRC or copy —
+    np.savez's zip CRC and buffer copies took most of a 10,000x BAM's checkpoint), then a JSON index and its offset.  A
+    batch is (pos, offsets, codes, quals) or a dict of named arrays (engine.iter_history_packed: offsets, the packed
+    bytes and the exception list).  Written to <path>.tmp and renamed.  Returns the file's size."""
     import json
     import struct
     index = []
     with open(path + ".tmp", "wb") as f:
         f.write(_SHARD_MAGIC)
-        for pb, off, codes, quals in batches:
-            ent = {"pos": int(pb)}
-            for name, a in (("off", off), ("codes", codes), ("quals", quals)):
+        for b in batches:
+            if not isinstance(b, dict):
+                b = {"pos": b[0], "off": b[1], "codes": b[2], "quals": b[3]}
+            ent = {"pos": int(b["pos"])}
+            for name, a in b.items():
+                if name == "pos":
+                    continue
                 a = np.ascontiguousarray(a)
                 pad = (-f.tell()) % 64
                 if pad:
@@ -660,9 +667,13 @@ def _write_shard(path: str, batches) -> int:
     return size
 
 
+_PACKED_CODE = np.array([1, 2, 4, 8], np.uint8)
+
+
 def _read_shard(path: str):
     """[(pos_begin, offsets, codes, quals)] of a _write_shard file (no code from the file is executed: raw arrays of
-    the dtypes its index names, u64 / u8 only)."""
+    the dtypes its index names, u64 / u8 only); packed batches are decoded (byte >> 6 -> A/C/G/T, byte & 63 -> q, then
+    the exceptions)."""
     import json
     import struct
     with open(path, "rb") as f:
@@ -677,14 +688,26 @@ def _read_shard(path: str):
         index = json.loads(f.read(size - 16 - at))
         out = []
         for ent in index:
-            arrs = []
-            for name in ("off", "codes", "quals"):
+            arrs = {}
+            for name in ("off", "codes", "quals", "packed", "xi", "xc", "xq"):
+                if name not in ent:
+                    continue
                 pos, n, dt = ent[name]
                 if dt not in ("<u8", "|u1"):
                     raise ValueError(f"{path}: unexpected dtype {dt}")
                 f.seek(pos)
-                arrs.append(np.fromfile(f, dtype=np.dtype(dt), count=n))
-            out.append((int(ent["pos"]), *arrs))
+                arrs[name] = np.fromfile(f, dtype=np.dtype(dt), count=n)
+            if "packed" in arrs:
+                pk = arrs["packed"]
+                codes, quals = _PACKED_CODE[pk >> 6], pk & np.uint8(63)
+                xi = arrs["xi"].astype(np.int64)
+                if len(xi) and (xi.min() < 0 or xi.max() >= len(pk)):
+                    raise ValueError(f"{path}: exception index out of range")
+                codes[xi] = arrs["xc"]
+                quals[xi] = arrs["xq"]
+            else:
+                codes, quals = arrs["codes"], arrs["quals"]
+            out.append((int(ent["pos"]), arrs["off"], codes, quals))
     return out
 
 

@@ -264,6 +264,13 @@ int spg_history_copy(spg_ctx *ctx, int64_t i, uint64_t *offsets, uint8_t *base_c
  * for the batch's n_entries) get *n_kept entries.  Synchronises. */
 int spg_history_copy_compact(spg_ctx *ctx, int64_t i, int32_t min_bq, uint64_t *offsets, uint8_t *base_code,
                              uint8_t *qual, uint64_t *n_kept);
+/* The same kept entries packed one byte each (the checkpoint shard's packed form): (b << 6) | q for base A/C/G/T
+ * (BAM nibble 1/2/4/8 -> b 0..3) with q <= 62; any other entry is byte 63 plus an exception (its index in the batch's
+ * kept entries, its code, its quality) in exc_* — *n_exc of them, in no particular order.  packed: room for the batch's
+ * n_entries; when *n_exc > exc_cap the exceptions were not copied (call again with more room, or use
+ * spg_history_copy_compact).  Synchronises. */
+int spg_history_copy_packed(spg_ctx *ctx, int64_t i, int32_t min_bq, uint64_t *offsets, uint8_t *packed, uint64_t *n_kept,
+                            uint64_t *exc_index, uint8_t *exc_code, uint8_t *exc_qual, int64_t exc_cap, int64_t *n_exc);
 /* One position's entries over the whole history, in accumulate order (the q list behind memory[pos], before the
  * base-quality filter): *n_out = their number; codes / quals get them when n_out <= cap (cap 0: count only).
  * Synchronises.  LiveVariantCaller.memory builds a Site from this per lookup instead of expanding every entry. */

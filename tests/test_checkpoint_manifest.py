@@ -72,3 +72,30 @@ def test_shard_roundtrip_and_refusals(tmp_path):
     (tmp_path / "d.spgck").write_bytes(raw.replace(b'"<u8"', b'"|O8"'))
     with pytest.raises(ValueError):
         _read_shard(str(tmp_path / "d.spgck"))
+
+
+def test_packed_shard_roundtrip(tmp_path):
+    """The packed batch form (engine.iter_history_packed / spg_history_copy_packed): one byte per kept entry —
+    A/C/G/T (BAM nibbles 1/2/4/8) in the top 2 bits over q 0..62 — and an exception list for everything else
+    (other codes, D / N entries 16 / 17, q >= 63), decoded on read; mixed with an unpacked batch in one shard."""
+    import numpy as np
+    from covid_spings_variant_caller_amd import live_variant_caller as LV
+    rng = np.random.default_rng(5)
+    codes = rng.choice(np.array([1, 2, 4, 8, 15, 16, 17, 3], np.uint8), size=5000, p=[.24, .24, .24, .24, .01, .01, .01, .01])
+    quals = rng.integers(0, 94, 5000).astype(np.uint8)
+    b2 = np.full(5000, 4, np.uint8)
+    for k, c in enumerate((1, 2, 4, 8)):
+        b2[codes == c] = k
+    esc = (b2 == 4) | (quals >= 63)
+    packed = np.where(esc, 63, (b2 << 6) | quals).astype(np.uint8)
+    xi = np.nonzero(esc)[0].astype(np.uint64)
+    perm = rng.permutation(len(xi))                      # (exceptions come in no particular order)
+    ent = {"pos": 100, "off": np.array([0, 2000, 5000], np.uint64), "packed": packed, "xi": xi[perm],
+           "xc": codes[esc][perm], "xq": quals[esc][perm]}
+    plain = (7, np.array([0, 3], np.uint64), np.array([1, 16, 2], np.uint8), np.array([40, 0, 99], np.uint8))
+    path = str(tmp_path / "s.spgck")
+    LV._write_shard(path, [ent, plain])
+    got = LV._read_shard(path)
+    assert got[0][0] == 100 and (got[0][1] == ent["off"]).all()
+    assert (got[0][2] == codes).all() and (got[0][3] == quals).all()
+    assert got[1][0] == 7 and (got[1][2] == plain[2]).all() and (got[1][3] == plain[3]).all()

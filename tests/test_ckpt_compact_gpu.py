@@ -21,6 +21,22 @@ def _check(eng, bq):
         np.testing.assert_array_equal(ob, eo)
         np.testing.assert_array_equal(cb, ec)
         np.testing.assert_array_equal(qb, eq)
+    # the packed form (spg_history_copy_packed: one byte per kept entry + exceptions), decoded, is the same; and with
+    # too small an exception capacity it hands back the unpacked arrays instead
+    for cap in (1 << 20, 3):
+        for (pa, oa, ca, qa), ent in zip(full, eng.iter_history_packed(0, bq, exc_cap=cap)):
+            eo, ec, eq = bq_compact(oa, ca, qa, bq)
+            np.testing.assert_array_equal(ent["off"], eo)
+            if "packed" in ent:
+                pk = ent["packed"]
+                codes, quals = np.array([1, 2, 4, 8], np.uint8)[pk >> 6], pk & 63
+                codes[ent["xi"].astype(np.int64)] = ent["xc"]
+                quals[ent["xi"].astype(np.int64)] = ent["xq"]
+                assert cap > 3 or len(ent["xi"]) <= 3
+            else:
+                codes, quals = ent["codes"], ent["quals"]
+            np.testing.assert_array_equal(codes, ec)
+            np.testing.assert_array_equal(quals, eq)
 
 
 @pytest.mark.parametrize("bq", [0, 1, 13, 30, 60])
@@ -39,6 +55,8 @@ def test_compact_matches_host(bq):
         for col in rng.choice(len(off) - 1, size=min(60, len(off) - 1), replace=False):   # all-fail columns
             q[off64[col]:off64[col + 1]] = rng.integers(0, max(1, bq), off64[col + 1] - off64[col])
         q[rng.integers(0, len(q), 200)] = 255
+        c = c.copy()
+        c[rng.integers(0, len(c), 150)] = rng.choice(np.array([3, 15, 16, 17], np.uint8), 150)   # packed exceptions
         if s == 2:                                  # borrowed device batch
             dev = torch.device("cuda", 0)
             pad = np.zeros(16, np.uint8)
