@@ -165,6 +165,7 @@ def gpu_lib():
     _sig(L.spg_bam_inflate_ms, i32, vp, C.POINTER(C.c_float))
     _sig(L.spg_bam_inflate_fallbacks, i32, vp, C.POINTER(i64))
     _sig(L.spg_bam_slot, i32, vp, i32)
+    _sig(L.spg_bam_upload, i32, vp, i32, vp, u64, vp, i64)
     _sig(L.spg_bam_release, i32, vp)
     _sig(L.spg_position_entries, i32, vp, i64, vp, vp, i64, C.POINTER(i64))
     _sig(L.spg_position_entries_upto, i32, vp, i64, i64, vp, vp, i64, C.POINTER(i64))

@@ -175,7 +175,13 @@ struct BamDev {
     float inflate_ms = 0.f;
     int64_t inflate_fallbacks = 0;     // members k_inflate_par left to the lane kernel (the last spg_bam_open)
     hipEvent_t ev[2] = {nullptr, nullptr};
+    hipEvent_t ev_up = nullptr;        // spg_bam_upload's copies into this slot done
+    bool up_pending = false;           // comp / mem hold an upload of (up_comp, up_bytes, up_n) for the next spg_bam_open
+    const uint8_t *up_comp = nullptr;
+    uint64_t up_bytes = 0;
+    int64_t up_n = 0;
     void release() {
+        up_pending = false;
         for (DBuf *b : {&comp, &out, &mem, &status, &uoff, &start, &cnt, &base, &lohi, &rec, &fields, &err, &kept, &pairs,
                         &orig, &twof, &recs_k, &tile_first, &iscr})
             b->release();
@@ -190,6 +196,7 @@ struct spg_ctx {
     spg_params p{};
     hipStream_t stream = nullptr;       // kernels
     hipStream_t copy_stream = nullptr;  // host -> device batch copies
+    hipStream_t up_stream = nullptr;    // spg_bam_upload: the next BAM's compressed bytes (created on first use)
     hipEvent_t copy_ev = nullptr;       // after the latest batch copy
     hipEvent_t compute_ev = nullptr;    // reset fence: recycled arena copies wait for the old kernels
     hipEvent_t hist_ev = nullptr;       // after the latest descriptor upload (pinned mirror -> d_hist)
@@ -410,12 +417,17 @@ int spg_destroy(spg_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+    if (c->up_stream) {
+        (void)hipStreamSynchronize(c->up_stream);
+        (void)hipStreamDestroy(c->up_stream);
+    }
     free_spilled(c);
     c->arena.release();
     for (BamDev &b : c->bams) {
         b.release();
         for (hipEvent_t e : b.ev)
             if (e) (void)hipEventDestroy(e);
+        if (b.ev_up) (void)hipEventDestroy(b.ev_up);
     }
     void *bufs[] = {c->acc, c->tables, c->ref, c->d_hist, c->o_depth, c->o_counts, c->o_order, c->o_first,
                     c->o_gl, c->o_flags, c->cand, c->band, c->detail, c->ctr, c->part, c->d_ridx, c->kerr, c->nlist,
@@ -2201,6 +2213,32 @@ int spg_bam_inflate_fallbacks(spg_ctx *c, int64_t *n) {
     return 0;
 }
 
+int spg_bam_upload(spg_ctx *c, int slot, const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *members,
+                   int64_t n) {
+    if (!c || !comp || !members || n < 1 || slot < 0 || slot > 1) return fail("spg_bam_upload: bad argument");
+    for (int64_t i = 0; i < n; i++)
+        if (members[i].coff + members[i].clen + 8 > comp_bytes || members[i].ulen > 65536)
+            return fail("spg_bam_upload: member outside the file");
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->up_stream) HIPCHK(hipStreamCreateWithFlags(&c->up_stream, hipStreamNonBlocking));
+    BamDev &B = c->bams[slot];
+    B.up_pending = false;
+    if (!B.ev_up) HIPCHK(hipEventCreateWithFlags(&B.ev_up, hipEventDisableTiming));
+    // (the slot's previous BAM: its inflate read comp / mem on the kernel stream, and spg_bam_open synchronised on it
+    // before returning; growing a buffer frees the old one, which waits for the device)
+    HIPCHK(B.comp.need(comp_bytes + 64));
+    HIPCHK(B.mem.need(sizeof(spg_bgzf_member) * (size_t)n));
+    HIPCHK(hipMemcpyAsync(B.comp.p, comp, comp_bytes, hipMemcpyHostToDevice, c->up_stream));
+    HIPCHK(hipMemsetAsync(B.comp.as<uint8_t>() + comp_bytes, 0, 64, c->up_stream));
+    HIPCHK(hipMemcpyAsync(B.mem.p, members, sizeof(spg_bgzf_member) * (size_t)n, hipMemcpyHostToDevice, c->up_stream));
+    HIPCHK(hipEventRecord(B.ev_up, c->up_stream));
+    B.up_pending = true;
+    B.up_comp = comp;
+    B.up_bytes = comp_bytes;
+    B.up_n = n;
+    return 0;
+}
+
 int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *members, int64_t n,
                  uint64_t body, int32_t tid, int32_t n_ref, const spg_bam_filter *flt, int64_t *n_reads) {
     if (!c || !comp || !members || !flt || !n_reads || n < 1 || tid < 0 || tid >= n_ref)
@@ -2233,9 +2271,17 @@ int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg
     HIPCHK(B.lohi.need(sizeof(int64_t) * 2 * nm));
     HIPCHK(B.err.need(64));
     HIPCHK(B.iscr.need(inflate_scratch_bytes(comp_bytes, n)));
-    HIPCHK(hipMemcpyAsync(B.comp.p, comp, comp_bytes, hipMemcpyHostToDevice, cs));
-    HIPCHK(hipMemsetAsync(B.comp.as<uint8_t>() + comp_bytes, 0, 64, cs));
-    HIPCHK(hipMemcpyAsync(B.mem.p, members, sizeof(spg_bgzf_member) * nm, hipMemcpyHostToDevice, cs));
+    // the compressed bytes and member table: already on their way when spg_bam_upload sent this same file to this slot
+    // (process_bams sends BAM i + 1 while BAM i inflates); else copied here
+    const bool up = B.up_pending && B.up_comp == comp && B.up_bytes == comp_bytes && B.up_n == n;
+    B.up_pending = false;
+    if (up) {
+        HIPCHK(hipStreamWaitEvent(cs, B.ev_up, 0));
+    } else {
+        HIPCHK(hipMemcpyAsync(B.comp.p, comp, comp_bytes, hipMemcpyHostToDevice, cs));
+        HIPCHK(hipMemsetAsync(B.comp.as<uint8_t>() + comp_bytes, 0, 64, cs));
+        HIPCHK(hipMemcpyAsync(B.mem.p, members, sizeof(spg_bgzf_member) * nm, hipMemcpyHostToDevice, cs));
+    }
     HIPCHK(hipMemcpyAsync(B.uoff.p, uoff.data(), sizeof(uint64_t) * (nm + 1), hipMemcpyHostToDevice, cs));
     HIPCHK(hipMemsetAsync(B.out.as<uint8_t>() + total, 0, 64, cs));
     HIPCHK(hipMemsetAsync(B.err.p, 0, 64, cs));

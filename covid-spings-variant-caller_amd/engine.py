@@ -216,6 +216,14 @@ class PileupEngine:
             N.check(self._L.spg_bam_slot(self._h, int(slot)), "spg_bam_slot")
             self._bam_slot = int(slot)
 
+    def bam_upload(self, bmap, slot: int):
+        """spg_bam_upload: start copying a BAM's compressed bytes (pileup.BamMap, kept open until its bam_open in that
+        slot returns) into device slot ``slot``; that bam_open then waits for the copy instead of making its own."""
+        i = bmap.info
+        with self._lock:
+            N.check(self._L.spg_bam_upload(self._h, int(slot), i.comp, i.comp_bytes, i.members, i.n_members),
+                    "spg_bam_upload")
+
     def bam_reads(self, n: int) -> Dict[str, np.ndarray]:
         """spg_bam_reads_copy: the open BAM's kept reads' fixed fields (pinned host arrays per BAM slot, reused
         across that slot's BAMs)."""

@@ -413,6 +413,11 @@ class LiveVariantCaller:
                     if i + 2 < len(paths):
                         maps.append(io.submit(read, paths[i + 2]))
                     slot = i & 1
+                    # BAM i + 1's compressed bytes start up into the other slot (its previous BAM, i - 1, has been
+                    # opened; its fill reads only the inflated records), overlapping BAM i's inflate
+                    if i + 1 < len(paths):
+                        nb, nm = maps[i + 1].result()
+                        self.engine.bam_upload(nm, slot ^ 1)
                     try:
                         with self._lock:
                             self.engine.bam_slot(slot)

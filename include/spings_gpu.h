@@ -356,6 +356,12 @@ typedef struct {
  * reads of contig tid. */
 int spg_bam_open(spg_ctx *ctx, const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *members, int64_t n_members,
                  uint64_t body, int32_t tid, int32_t n_ref, const spg_bam_filter *filter, int64_t *n_reads);
+/* Optional prefetch: start copying a BAM's compressed bytes and member table into device slot `slot` on the context's
+ * upload stream and return; a later spg_bam_open of the same (comp, comp_bytes, n_members) in that slot waits for these
+ * copies instead of making its own.  comp must stay valid until that spg_bam_open returns.  process_bams sends BAM i + 1
+ * this way (into the other slot) before opening BAM i, so the upload overlaps BAM i's inflate. */
+int spg_bam_upload(spg_ctx *ctx, int slot, const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *members,
+                   int64_t n_members);
 typedef struct {                   /* host arrays with room for n_reads values each, in BAM order */
     int32_t *pos, *end, *mtid, *mpos, *isize;   /* end: pos + the CIGAR's reference length */
     uint16_t *flag;
