@@ -162,7 +162,7 @@ struct DBuf {
 };
 struct BamDev {
     DBuf comp, out, mem, status, uoff, start, cnt, base, lohi, rec, fields, err;
-    DBuf kept, pairs, orig, twof, recs_k, tile_first, iscr;
+    DBuf kept, pairs, orig, twof, recs_k, tile_first, iscr, rtmp;
     bool open = false;                 // a BAM is loaded (spg_bam_open succeeded)
     uint64_t total = 0;                // inflated bytes
     int64_t n_members = 0;
@@ -183,7 +183,7 @@ struct BamDev {
     void release() {
         up_pending = false;
         for (DBuf *b : {&comp, &out, &mem, &status, &uoff, &start, &cnt, &base, &lohi, &rec, &fields, &err, &kept, &pairs,
-                        &orig, &twof, &recs_k, &tile_first, &iscr})
+                        &orig, &twof, &recs_k, &tile_first, &iscr, &rtmp})
             b->release();
         open = false;
     }
@@ -2271,6 +2271,7 @@ int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg
     HIPCHK(B.lohi.need(sizeof(int64_t) * 2 * nm));
     HIPCHK(B.err.need(64));
     HIPCHK(B.iscr.need(inflate_scratch_bytes(comp_bytes, n)));
+    HIPCHK(B.rtmp.need(sizeof(uint64_t) * BAM_RTMP * nm));
     // the compressed bytes and member table: already on their way when spg_bam_upload sent this same file to this slot
     // (process_bams sends BAM i + 1 while BAM i inflates); else copied here
     const bool up = B.up_pending && B.up_comp == comp && B.up_bytes == comp_bytes && B.up_n == n;
@@ -2306,6 +2307,7 @@ int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg
     A.pos_lo = B.lohi.as<int64_t>();
     A.pos_hi = A.pos_lo + nm;
     A.err = B.err.as<uint32_t>();
+    A.rtmp = B.rtmp.as<uint64_t>();
     HIPCHK(launch_bam_scan(A, 0, cs));
     HIPCHK(launch_bam_scan(A, 1, cs));
     std::vector<uint32_t> st(nm), cnt(nm), err(1), fbk(1);
@@ -2354,7 +2356,9 @@ int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg
     A.n_reads = (uint32_t)nr;
     A.pos = B.pos; A.end = B.end; A.mtid = B.mtid; A.mpos = B.mpos; A.isize = B.isize;
     A.flag = B.flag; A.l_seq = B.l_seq; A.nhash = B.nhash;
-    HIPCHK(launch_bam_scan(A, 2, cs));
+    // the counting walk listed each member's records (<= BAM_RTMP of them): copy the lists; else walk again
+    const bool lists = std::all_of(cnt.begin(), cnt.end(), [](uint32_t v) { return v <= BAM_RTMP; });
+    HIPCHK(launch_bam_scan(A, lists ? 4 : 2, cs));
     HIPCHK(launch_bam_scan(A, 3, cs));
     HIPCHK(hipMemcpyAsync(err.data(), B.err.p, sizeof(uint32_t), hipMemcpyDeviceToHost, cs));
     HIPCHK(hipStreamSynchronize(cs));

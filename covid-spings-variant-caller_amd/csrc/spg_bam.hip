@@ -3,13 +3,15 @@
 // only the compressed file going up and the reads' fixed fields coming down.
 //
 // After k_inflate has written the inflated stream into HBM:
-//   k_bam_starts  one lane per BGZF member: the first record that starts inside the member's inflated range — the
+//   k_bam_starts  one wave per BGZF member: the first record that starts inside the member's inflated range — the
 //                 offset where a block_size hop lands on a plausible record eight times in a row (or on the stream's
 //                 end); the member holding the header's end starts there.
 //   k_bam_walk    one lane per member with a start: the block_size chain from its start to the next member's start,
-//                 counting (pass 1) then listing (pass 2, at the exclusive prefix of the counts) the records of the
-//                 contig the stepper keeps; every chain must land exactly on the next start (else the host plans
-//                 this BAM); the first / last position of the contig's records per member (sort order, on the host).
+//                 counting the records of the contig the stepper keeps and listing them per member (pass 1; k_bam_copy
+//                 moves the lists to the exclusive prefix of the counts — or, for a chain of more than BAM_RTMP, a
+//                 second walk lists them there, pass 2); every chain must land exactly on the next start (else the
+//                 host plans this BAM); the first / last position of the contig's records per member (sort order, on
+//                 the host).
 //   k_bam_fields  one lane per listed read: pos, reference end (CIGAR walk), flag, mate fields, l_seq and a 64-bit
 //                 FNV-1a hash of the name — what htslib's depth cap and the mate pairing decide on (the host replays
 //                 them on these fields: spp_pileup_plan_fields).
@@ -72,8 +74,11 @@ __device__ __forceinline__ uint64_t rec_len(const BamArgs &A, uint64_t x) {
 
 }  // namespace
 
-__global__ __launch_bounds__(64) void k_bam_starts(BamArgs A) {
-    const int64_t m = (int64_t)blockIdx.x * 64 + threadIdx.x;
+// one wave per member: 64 candidate offsets tested at a time, the first (lowest) that validates wins — the same answer as
+// testing them one after another (r05: one lane per member scanning serially took 0.56 ms per 10,000x BAM)
+__global__ __launch_bounds__(256) void k_bam_starts(BamArgs A) {
+    const int lane = threadIdx.x & 63;
+    const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (m >= A.n_members) return;
     const uint64_t lo = A.uoff[m], hi = A.uoff[m + 1];
     uint64_t s = BAM_NONE;
@@ -82,19 +87,28 @@ __global__ __launch_bounds__(64) void k_bam_starts(BamArgs A) {
             s = A.body;
         } else {
             const uint64_t lim = min(hi, lo + 65536ull);
-            for (uint64_t x = lo; x < lim; x++) {
-                uint64_t y = x;
-                int k = 0;
-                for (; k < 8 && y < A.total; k++) {
-                    const uint64_t len = rec_len(A, y);
-                    if (!len) break;
-                    y += len;
+            for (uint64_t x0 = lo; x0 < lim; x0 += 64) {
+                const uint64_t x = x0 + (uint64_t)lane;
+                bool ok = false;
+                if (x < lim) {
+                    uint64_t y = x;
+                    int k = 0;
+                    for (; k < 8 && y < A.total; k++) {
+                        const uint64_t len = rec_len(A, y);
+                        if (!len) break;
+                        y += len;
+                    }
+                    ok = k == 8 || y == A.total;
                 }
-                if (k == 8 || y == A.total) { s = x; break; }
+                const uint64_t okm = __ballot(ok);
+                if (okm) {
+                    s = x0 + (uint64_t)__builtin_ctzll(okm);
+                    break;
+                }
             }
         }
     }
-    A.start[m] = s;
+    if (lane == 0) A.start[m] = s;
 }
 
 template <bool WRITE>
@@ -127,6 +141,7 @@ __global__ __launch_bounds__(64) void k_bam_walk(BamArgs A) {
             const uint32_t w8 = ldu32(A.data, b + 8), w12 = ldu32(A.data, b + 12);
             if (keeps(A, w12 >> 16, (w8 >> 8) & 0xFFu)) {
                 if (WRITE) A.rec[at + kept] = b;
+                else if (kept < BAM_RTMP) A.rtmp[(uint64_t)m * BAM_RTMP + kept] = b;
                 kept++;
             }
         }
@@ -139,6 +154,15 @@ __global__ __launch_bounds__(64) void k_bam_walk(BamArgs A) {
         A.pos_hi[m] = last;
         if (bad) atomicOr(A.err, bad);
     }
+}
+
+// the counting walk's lists to their place in rec (every member's count <= BAM_RTMP; else pass 2 walks again)
+__global__ __launch_bounds__(256) void k_bam_copy(BamArgs A) {
+    const int lane = threadIdx.x & 63;
+    const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (m >= A.n_members) return;
+    const uint32_t n = A.cnt[m], at = A.base[m];
+    for (uint32_t k = (uint32_t)lane; k < n; k += 64) A.rec[at + k] = A.rtmp[(uint64_t)m * BAM_RTMP + k];
 }
 
 __global__ __launch_bounds__(256) void k_bam_fields(BamArgs A) {
@@ -288,11 +312,13 @@ __global__ __launch_bounds__(256) void k_bam_gather2(BamGatherArgs G) {
     G.tw_k[i] = G.twof[r];
 }
 
+// pass 0 starts, 1 counting walk (+ lists), 2 listing walk, 3 fields, 4 the lists copied (instead of pass 2)
 hipError_t launch_bam_scan(const BamArgs &A, int pass, hipStream_t st) {
-    const unsigned mb = (unsigned)((A.n_members + 63) / 64);
-    if (pass == 0) k_bam_starts<<<mb, 64, 0, st>>>(A);
+    const unsigned mb = (unsigned)((A.n_members + 63) / 64), mw = (unsigned)((A.n_members + 3) / 4);
+    if (pass == 0) k_bam_starts<<<mw, 256, 0, st>>>(A);
     else if (pass == 1) k_bam_walk<false><<<mb, 64, 0, st>>>(A);
     else if (pass == 2) k_bam_walk<true><<<mb, 64, 0, st>>>(A);
+    else if (pass == 4) k_bam_copy<<<mw, 256, 0, st>>>(A);
     else if (A.n_reads) k_bam_fields<<<(A.n_reads + 255) / 256, 256, 0, st>>>(A);
     return hipGetLastError();
 }

@@ -261,6 +261,7 @@ struct FillArgs {
 
 // A BAM in HBM (spg_bam.hip, include/spings_gpu.h spg_bam_*)
 constexpr uint64_t BAM_NONE = ~0ull;
+constexpr uint32_t BAM_RTMP = 2048;  // kept records the counting walk lists per member (a 64 KiB member holds <= 1,821)
 struct BamArgs {
     const uint8_t *data;           // the inflated stream (64 readable pad bytes past total)
     uint64_t total, body;          // its length; the first record's offset (after the header)
@@ -275,6 +276,7 @@ struct BamArgs {
     uint32_t *cnt, *base;          // kept records per member's chain; their exclusive prefix
     int64_t *pos_lo, *pos_hi;      // first / last position of the contig's records per chain (sort order)
     uint64_t *rec;                 // listed reads: offset of the refID field
+    uint64_t *rtmp;                // [n_members * BAM_RTMP] the counting walk's kept records per member (pass 4 copies)
     int32_t *pos, *end, *mtid, *mpos, *isize;
     uint16_t *flag;
     uint32_t *l_seq;
