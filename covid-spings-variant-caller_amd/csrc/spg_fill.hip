@@ -497,15 +497,23 @@ __global__ __launch_bounds__(256) void k_f2_base(FillArgs A, F2Lay L) {
     if (c < A.n_cols && (uint64_t)run != A.off[c + 1] - A.off[c]) atomicOr(A.err, 2u);
 }
 
-// the chunk's entries: lanes = reads, columns of the span in order
-__global__ __launch_bounds__(256) void k_f2_fill(FillArgs A, F2Lay L) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// the chunk's entries: lanes = reads, columns of the span in order.  One wave per workgroup: each lane first copies
+// its record's CIGAR, packed bases and qualities (one contiguous range of the record) — and, for a read the mate-overlap
+// tweak touches, its original qualities — into the wave's LDS as 16-B blocks, so the column loop reads bytes from LDS and
+// issues no vector-memory load: its only vector-memory instructions are the entry stores, which nothing waits for.  (The
+// r05 form kept 8-byte windows in registers with the next one in flight; a refill in any lane waited for every memory
+// operation the wave had issued, its entry stores included — about one L2 round trip per column, 1.12 ms per
+// 10,000x BAM.)  A chunk whose ranges exceed F2_LDS takes those windows.
+constexpr uint32_t F2_LDS = 20480;
+
+__global__ __launch_bounds__(64) void k_f2_fill(FillArgs A, F2Lay L) {
+    __shared__ __align__(16) uint8_t sb[F2_LDS];
+    const int lane = threadIdx.x;
     // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs; consecutive chunks (which write adjacent runs of
     // the same columns) land on one XCD
     const uint32_t nb = gridDim.x, per = nb >> 3, b = blockIdx.x;
-    const uint32_t blk = (b < (per << 3)) ? (b & 7) * per + (b >> 3) : b;
-    const int64_t q = (int64_t)blk * 4 + w;
-    if (q >= L.n_chunks) return;                                  // (wave-uniform; no barrier below)
+    const int64_t q = (b < (per << 3)) ? (b & 7) * per + (b >> 3) : b;
+    if (q >= L.n_chunks) return;                                  // (workgroup-uniform)
     const uint64_t r = (uint64_t)q * 64 + (uint64_t)lane;
     bool valid = r < A.n_reads;
     const int32_t cb = L.cbeg[q], ce = L.cend[q];
@@ -532,7 +540,102 @@ __global__ __launch_bounds__(256) void k_f2_fill(FillArgs A, F2Lay L) {
             if (oq + ls > A.orig_bytes) { bad = 1; valid = false; }
         }
     }
-    if (!valid) { rp = INT32_MAX; re = INT32_MIN; }
+    if (!valid) { rp = INT32_MAX; re = INT32_MIN; tc = INT32_MIN; }
+    // the lane's LDS ranges: [ga, ga + gn) of the record (CIGAR .. qualities), [oa, oa + on) of the original qualities
+    const uint64_t ga = co & ~15ull, oa = oq & ~15ull;
+    const uint32_t gn = valid ? (uint32_t)(((qo + ls + 15) & ~15ull) - ga) : 0u;
+    const uint32_t on = (valid && tc != INT32_MIN) ? (uint32_t)(((oq + ls + 15) & ~15ull) - oa) : 0u;
+    uint32_t lb = gn + on;                                        // exclusive prefix over the lanes: the lane's base
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(lb, o);
+        if (lane >= o) lb += t;
+    }
+    // lane l's region starts 4 l bytes past the prefix: lanes reading the same query offset of equal-length reads then hit
+    // different banks (unskewed, regions of 16 k bytes put every lane's byte on one bank: 3.3 conflict cycles per LDS
+    // cycle, r05zg)
+    const uint32_t need = __builtin_amdgcn_readlane(lb, 63) + 256u;
+    lb += 4u * (uint32_t)lane - (gn + on);
+    const bool lds = need <= F2_LDS;                              // (uniform)
+    if (lds) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(1))) const u32x4 gu128;
+        // 16-B blocks, four loads in flight; a block past the array's readable end is copied byte by byte
+        auto copy = [&](uint32_t dst, const uint8_t *src, uint64_t a, uint32_t n, uint64_t lim) {
+            for (uint32_t i = 0; i < n; i += 64) {
+                uint4 v[4];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint64_t x = a + i + 16u * k;
+                    if (i + 16u * k < n && x + 16 <= lim) {
+                        const u32x4 t = *(gu128 *)(const void *)(src + x);
+                        v[k] = make_uint4(t.x, t.y, t.z, t.w);
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint64_t x = a + i + 16u * k;
+                    if (i + 16u * k >= n) continue;
+                    if (x + 16 > lim) {
+                        uint32_t w[4] = {0, 0, 0, 0};
+                        for (uint32_t j = 0; j < 16 && x + j < lim; j++) w[j >> 2] |= (uint32_t)src[x + j] << (8 * (j & 3));
+                        v[k] = make_uint4(w[0], w[1], w[2], w[3]);
+                    }
+                    uint32_t *d = reinterpret_cast<uint32_t *>(sb + dst + i + 16u * k);   // (4-B aligned)
+                    d[0] = v[k].x; d[1] = v[k].y; d[2] = v[k].z; d[3] = v[k].w;
+                }
+            }
+        };
+        if (gn) copy(lb, A.data, ga, gn, A.data_bytes + 64);
+        if (on) copy(lb + gn, A.orig, oa, on, A.orig_bytes);
+    }
+    __syncthreads();
+    // LDS offsets of the lane's CIGAR, packed bases, qualities and original qualities
+    const uint32_t lc = lb + (uint32_t)(co - ga), lsq = lb + (uint32_t)(so - ga), lq = lb + (uint32_t)(qo - ga);
+    const uint32_t lo_ = lb + gn + (uint32_t)(oq - oa);
+    // The column loop, instantiated twice so that the LDS form holds no vector-memory load the waits would count
+    auto body = [&](auto lds_tag) __attribute__((always_inline)) {
+    constexpr bool LDS = decltype(lds_tag)::value;
+    // 8-byte windows of the qualities and the packed bases, the next one in flight (chunks beyond F2_LDS)
+    typedef __attribute__((address_space(1))) const uint64_t gu64;
+    auto ld8 = [&](uint64_t a) -> uint64_t { return *(gu64 *)(const void *)(A.data + a); };
+    uint64_t qwa = qo & ~7ull, swa = so & ~7ull, qwin = 0, qnx = 0, swin = 0, snx = 0;
+    if (valid && !LDS) {
+        qwin = ld8(qwa); qnx = ld8(qwa + 8);
+        swin = ld8(swa); snx = ld8(swa + 8);
+    }
+    const uint32_t qo32 = (uint32_t)qo, so32 = (uint32_t)so;
+    // the quality byte at query offset p (windows only move forward)
+    auto qual_at = [&](uint32_t p) -> uint32_t {
+        if constexpr (LDS) return sb[lq + p];
+        uint32_t d = qo32 + p - (uint32_t)qwa;
+        if (d >= 8) {
+            if (d < 16) { qwin = qnx; qwa += 8; } else { qwa = (qo + p) & ~7ull; qwin = ld8(qwa); }
+            qnx = ld8(qwa + 8);
+            d = qo32 + p - (uint32_t)qwa;
+        }
+        return (uint32_t)(qwin >> (8 * d)) & 0xFFu;
+    };
+    // the packed-base byte holding query offset p
+    auto seq_at = [&](uint32_t p) -> uint32_t {
+        if constexpr (LDS) return sb[lsq + (p >> 1)];
+        uint32_t d = so32 + (p >> 1) - (uint32_t)swa;
+        if (d >= 8) {
+            if (d < 16) { swin = snx; swa += 8; } else { swa = (so + (p >> 1)) & ~7ull; swin = ld8(swa); }
+            snx = ld8(swa + 8);
+            d = so32 + (p >> 1) - (uint32_t)swa;
+        }
+        return (uint32_t)(swin >> (8 * d)) & 0xFFu;
+    };
+    auto orig_at = [&](uint32_t y) -> uint32_t {
+        if constexpr (LDS) return sb[lo_ + y];
+        return ((const __attribute__((address_space(1))) uint8_t *)(const void *)A.orig)[oq + y];
+    };
+    auto cig = [&](uint32_t o) -> uint32_t {                      // CIGAR op o (o < ncig)
+        if constexpr (!LDS) return ld32u(A.data, co + 4ull * o);
+        const uint32_t a = lc + 4 * o;
+        return (uint32_t)sb[a] | ((uint32_t)sb[a + 1] << 8) | ((uint32_t)sb[a + 2] << 16) | ((uint32_t)sb[a + 3] << 24);
+    };
     // the CIGAR cursor, kept on a reference-consuming op (M / D / N / = / X; 15: past the CIGAR's end): op k of length
     // len covering ref columns [x, xe), query offset y at its start; the next op preloaded
     uint32_t o = 0, k = 15, len = 0, nxt = 0;
@@ -545,40 +648,20 @@ __global__ __launch_bounds__(256) void k_f2_fill(FillArgs A, F2Lay L) {
         if (o < ncig) {
             k = nxt & 15u;
             len = nxt >> 4;
-            nxt = o + 1 < ncig ? ld32u(A.data, co + 4ull * (o + 1)) : 0u;
+            nxt = o + 1 < ncig ? cig(o + 1) : 0u;
         } else {
             k = 15;
             len = 0;
         }
     };
     if (valid) {
-        nxt = ld32u(A.data, co);
+        nxt = cig(0);
         k = nxt & 15u;
         len = nxt >> 4;
-        nxt = ncig > 1 ? ld32u(A.data, co + 4) : 0u;
+        nxt = ncig > 1 ? cig(1) : 0u;
         while (k != 15 && !eats_ref(k)) step();
         xe = x + (int32_t)len;
     }
-    // 8-byte windows of the qualities and the packed bases, the next one in flight; offsets into them in 32 bits
-    typedef __attribute__((address_space(1))) const uint64_t gu64;
-    auto ld8 = [&](uint64_t a) -> uint64_t { return *(gu64 *)(const void *)(A.data + a); };
-    uint64_t qwa = qo & ~7ull, swa = so & ~7ull, qwin = 0, qnx = 0, swin = 0, snx = 0;
-    if (valid) {
-        qwin = ld8(qwa); qnx = ld8(qwa + 8);
-        swin = ld8(swa); snx = ld8(swa + 8);
-    }
-    const uint32_t qo32 = (uint32_t)qo, so32 = (uint32_t)so;
-    // the quality byte at query offset p (windows only move forward)
-    auto qual_at = [&](uint32_t p) -> uint32_t {
-        uint32_t d = qo32 + p - (uint32_t)qwa;
-        if (d >= 8) {
-            if (d < 16) { qwin = qnx; qwa += 8; } else { qwa = (qo + p) & ~7ull; qwin = ld8(qwa); }
-            qnx = ld8(qwa + 8);
-            d = qo32 + p - (uint32_t)qwa;
-        }
-        return (uint32_t)(qwin >> (8 * d)) & 0xFFu;
-    };
-    const uint64_t below = ((uint64_t)1 << lane) - 1;
     for (int32_t c0 = cb; c0 < ce; c0 += 64) {
         // the next 64 columns' first entry of this chunk (CSR offset + the earlier chunks' entries), one per lane
         uint64_t at0 = 0;
@@ -589,7 +672,27 @@ __global__ __launch_bounds__(256) void k_f2_fill(FillArgs A, F2Lay L) {
             const int32_t c = c0 + j;
             bool cov = c >= rp && c < re;
             uint32_t cd = 0, qv = 0;
-            if (cov) {
+            if constexpr (LDS) {
+                // branch-free but for the (rare, wave-uniform) CIGAR step: both bytes read from LDS in every lane
+                const bool adv = cov && c >= xe;
+                if (__ballot(adv)) {
+                    if (adv) {
+                        do step(); while (k != 15 && (!eats_ref(k) || c >= x + (int32_t)len));
+                        xe = x + (int32_t)len;
+                    }
+                }
+                bad |= (uint32_t)(cov && k == 15);                // the CIGAR ends before the column
+                cov = cov && k != 15;
+                const bool dn = (k | 1u) == 3u;                   // D / N: the next query base's quality
+                const uint32_t qp = y + (dn ? 0u : (uint32_t)(c - x));
+                const bool rd = cov && qp < ls;
+                const uint32_t qa = rd ? ((dn && c < tc) ? lo_ + y : lq + qp) : 0u;
+                const uint32_t q0 = sb[qa];
+                const uint32_t sbyte = sb[rd ? lsq + (qp >> 1) : 0u];
+                const uint32_t nib = (qp & 1) ? (sbyte & 15u) : (sbyte >> 4);
+                cd = dn ? 14u + k : (rd ? nib : 15u);          // (15: a CIGAR longer than the sequence)
+                qv = rd ? q0 : 0u;
+            } else if (cov) {
                 if (c >= xe) {                                    // (rare) the next reference-consuming op
                     do step(); while (k != 15 && (!eats_ref(k) || c >= x + (int32_t)len));
                     xe = x + (int32_t)len;
@@ -599,35 +702,31 @@ __global__ __launch_bounds__(256) void k_f2_fill(FillArgs A, F2Lay L) {
                     cov = false;
                 } else if (k == 2 || k == 3) {                    // D / N: the next query base's quality
                     cd = 14u + k;
-                    if (y < ls)
-                        qv = c < tc ? ((const __attribute__((address_space(1))) uint8_t *)(const void *)A.orig)[oq + y]
-                                    : qual_at(y);
+                    if (y < ls) qv = c < tc ? orig_at(y) : qual_at(y);
                 } else {
                     const uint32_t qp = y + (uint32_t)(c - x);
                     if (qp < ls) {
                         qv = qual_at(qp);
-                        uint32_t d = so32 + (qp >> 1) - (uint32_t)swa;
-                        if (d >= 8) {
-                            if (d < 16) { swin = snx; swa += 8; } else { swa = (so + (qp >> 1)) & ~7ull; swin = ld8(swa); }
-                            snx = ld8(swa + 8);
-                            d = so32 + (qp >> 1) - (uint32_t)swa;
-                        }
-                        const uint32_t sb = (uint32_t)(swin >> (8 * d)) & 0xFFu;
-                        cd = (qp & 1) ? (sb & 15u) : (sb >> 4);
+                        const uint32_t sbyte = seq_at(qp);
+                        cd = (qp & 1) ? (sbyte & 15u) : (sbyte >> 4);
                     } else {
                         cd = 15u;                                 // (a CIGAR longer than the sequence)
                     }
                 }
             }
             const uint64_t m = __ballot(cov);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
             const uint64_t at = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)at_hi, j) << 32 |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)at_lo, j)) + (uint64_t)__builtin_popcountll(m & below);
+                                 (uint32_t)__builtin_amdgcn_readlane((int)at_lo, j)) + (uint64_t)rank;
             if (cov) {
                 A.code[at] = (uint8_t)cd;
                 A.qual[at] = (uint8_t)qv;
             }
         }
     }
+    };
+    if (lds) body(std::true_type{});
+    else body(std::false_type{});
     if (__ballot(bad) && lane == 0) atomicOr(A.err, 2u);
 }
 
@@ -687,7 +786,7 @@ hipError_t launch_pileup_fill(const FillArgs &A, hipStream_t st) {
         const unsigned cb = (unsigned)((L.n_chunks + 3) / 4);
         k_f2_count<<<cb, 256, 0, st>>>(A, L);
         k_f2_base<<<(unsigned)((A.n_tiles + 3) / 4), 256, 0, st>>>(A, L);
-        k_f2_fill<<<(unsigned)((cb + 7) & ~7u), 256, 0, st>>>(A, L);
+        k_f2_fill<<<(unsigned)((L.n_chunks + 7) & ~7ll), 64, 0, st>>>(A, L);
         return hipGetLastError();
     }
     int32_t fg = 0;

@@ -129,11 +129,34 @@ __device__ __forceinline__ void replay_walk(const FParams &F, const Hist *__rest
             const int64_t col = pos - h.pos_begin;
             if (col < 0 || col >= h.n_cols) continue;
             const uint64_t lo = h.off[col], hi = h.off[col + 1];
-            for (uint64_t e0 = lo; e0 < hi; e0 += 64) {
+            // 64 entries a step, the next two steps' loads in flight (a step waited for its own load: a column of
+            // 8,000 entries is 125 dependent round trips)
+            auto ld = [&](uint64_t e0, uint32_t &c, uint32_t &q) {
                 const uint64_t e = e0 + (uint64_t)lane;
-                const bool valid = e < hi;
-                const uint32_t c = valid ? h.code[e] : 0xFFu, q = valid ? h.qual[e] : 0u;
-                fn(c, q, valid, ord + (e0 - lo));
+                c = e < hi ? h.code[e] : 0xFFu;
+                q = e < hi ? h.qual[e] : 0u;
+            };
+#ifdef SPG_REPLAY_NOPF                                         // A/B builds: one step at a time
+            for (uint64_t e0 = lo; e0 < hi; e0 += 64) {
+                uint32_t c, q;
+                ld(e0, c, q);
+                fn(c, q, e0 + (uint64_t)lane < hi, ord + (e0 - lo));
+            }
+            ord += hi - lo;
+            continue;
+#endif
+            uint32_t cA, qA, cB, qB, cC, qC;
+            ld(lo, cA, qA);
+            ld(lo + 64, cB, qB);
+            for (uint64_t e0 = lo; e0 < hi; e0 += 192) {
+                ld(e0 + 128, cC, qC);
+                fn(cA, qA, e0 + (uint64_t)lane < hi, ord + (e0 - lo));
+                if (e0 + 64 >= hi) break;
+                ld(e0 + 192, cA, qA);
+                fn(cB, qB, e0 + 64 + (uint64_t)lane < hi, ord + (e0 + 64 - lo));
+                if (e0 + 128 >= hi) break;
+                ld(e0 + 256, cB, qB);
+                fn(cC, qC, e0 + 128 + (uint64_t)lane < hi, ord + (e0 + 128 - lo));
             }
             ord += hi - lo;
         }
@@ -788,8 +811,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         wave_sync();
     };
 
+    // The ring's n records from their LDS images (16 B per lane, ten lanes per record).
+    auto store_ring = [&](uint32_t n) __attribute__((always_inline)) {
+        Acc *base = acc + P.pos_begin + g0;
+        for (uint32_t t = (uint32_t)lane; t < 10u * n; t += 64u) {
+            const uint32_t r = t / 10u, piece = t - 10u * r;
+            if (P.dbg && CS[r].cj >= (uint32_t)ng) {                   // SPG_TRACE: record outside the group
+                atomicAdd(P.dbg + 2, 1u);
+                P.dbg[3] = CS[r].cj | ((uint32_t)ng << 8) | (r << 16) | (n << 24);
+                continue;
+            }
+            reinterpret_cast<uint4 *>(base + CS[r].cj)[piece] = reinterpret_cast<const uint4 *>(img + r)[piece];
+        }
+    };
     // Finish the ring: drain the queue, lane j assembles column j's record in LDS, the wave stores the
-    // records (16 B per lane, ten lanes per record).
+    // records.
     auto finish = [&]() __attribute__((always_inline)) {
         if (qn) drain();
         else wave_sync();
@@ -799,16 +835,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
         }
         wave_sync();
         prog(4, nb, CS[0].cj, CS[nb - 1].cj);
-        Acc *base = acc + P.pos_begin + g0;
-        for (uint32_t t = (uint32_t)lane; t < 10u * nb; t += 64u) {
-            const uint32_t r = t / 10u, piece = t - 10u * r;
-            if (P.dbg && CS[r].cj >= (uint32_t)ng) {                   // SPG_TRACE: record outside the group
-                atomicAdd(P.dbg + 2, 1u);
-                P.dbg[3] = CS[r].cj | ((uint32_t)ng << 8) | (r << 16) | (nb << 24);
-                continue;
-            }
-            reinterpret_cast<uint4 *>(base + CS[r].cj)[piece] = reinterpret_cast<const uint4 *>(img + r)[piece];
-        }
+        store_ring(nb);
         if (!FUSE && P.list) {                  // calls-only listing: the ring's records that may call
             const bool maybe = (uint32_t)lane < nb && may_call_img(P, img + lane);
             const uint64_t bm = __ballot(maybe);
@@ -1150,24 +1177,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
     }
 #undef SPG_LD
     prog(5, total, nb, qn);
+    const uint64_t wt1 = P.wtime ? __builtin_amdgcn_s_memrealtime() : 0;   // SPG_WAVE_TIMES: the chunk loop's end
     const uint32_t nfin = nb;                          // FUSE: every column of the wave (G <= NB)
     if (nb) finish();
+    uint32_t tailed = 0;                               // SPG_WAVE_TIMES: the wave ran the fused finalize
     if constexpr (FUSE) {
         // Division-free pre-check from the images (LDS) and the kernel's scalar parameters: most positions
         // cannot produce a call.  Only a wave holding a possible call reads the finalize parameters (vector
         // loads from memory, whose wait would also wait for the record stores just issued).
         const bool maybe = (uint32_t)lane < nfin && may_call_img(P, img + lane);
-        if (__ballot(maybe))
+        if (__ballot(maybe)) {
+            tailed = 1;
             fused_tail(P.fused->F, P.fused->O, T, P.pos_begin + g0, maybe ? nfin : 0u, CS, img,
                        reinterpret_cast<ReplayWs *>(Q), &hdl, lut);
+        }
     }
     if (P.wtime && lane == 0) {
         const uint64_t wt2 = __builtin_amdgcn_s_memrealtime();
         const uint32_t hw = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
         const uint32_t xcc = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (15 << 11));  // HW_REG_XCC_ID
-        // {entry, first column, lifetime from entry (bits 0-19) | entry-to-loop ticks (bits 20-31), hw id}
+        // {entry, first column (bits 0-14) | entry-to-loop-end ticks (bits 15-31), lifetime from entry (bits 0-19) |
+        //  entry-to-loop ticks (bits 20-31), hw id (bits 0-19) | fused finalize ran (bit 20) | XCC (bits 24-31)}
         const uint64_t pro = min(wt0 - we, (uint64_t)0xFFF), life = min(wt2 - we, (uint64_t)0xFFFFF);
-        P.wtime[wave] = make_uint4((uint32_t)we, (uint32_t)g0, (uint32_t)(life | (pro << 20)), (hw & 0xFFFFFu) | (xcc << 24));
+        const uint64_t lend = min(wt1 - we, (uint64_t)0x1FFFF);
+        P.wtime[wave] = make_uint4((uint32_t)we, ((uint32_t)g0 & 0x7FFFu) | (uint32_t)(lend << 15),
+                                   (uint32_t)(life | (pro << 20)), (hw & 0xFFFFFu) | (tailed << 20) | (xcc << 24));
     }
     prog(6, 0, 0, 0);
     }   // items

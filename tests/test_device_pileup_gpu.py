@@ -238,6 +238,20 @@ def test_simulated_bams(tmp_path, depth, max_depth):
     assert_same(bam_device_fill(bam, "NC_045512.2", max_depth=max_depth), host)
 
 
+@pytest.mark.parametrize("read_len", [60, 300])
+def test_simulated_read_lengths(tmp_path, read_len):
+    """k_f2_fill stages each chunk's record bytes in LDS when they fit (20 KiB a chunk: 64 reads of ~150 bp) and keeps
+    register windows over global memory otherwise: 60 bp reads take the LDS form, 300 bp reads (~30 KiB a chunk) the
+    window form — both bit-identical to the host fill."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.pileup import simulate_bam
+    bam = str(tmp_path / "s.bam")
+    simulate_bam(bam, "NC_045512.2", synth.reference(3000, seed=1), depth=2000, seed=7, n_threads=8, read_len=read_len)
+    host = host_fill(bam, "NC_045512.2", max_depth=0)
+    assert_same(device_fill(bam, "NC_045512.2", pinned=True, max_depth=0), host)
+    assert_same(bam_device_fill(bam, "NC_045512.2", max_depth=0), host)
+
+
 def test_bam_device_declines_corrupt_member(tmp_path):
     """A member whose compressed bytes were damaged (its CRC32 no longer matches, or it fails to decode): spg_bam_open
     declines the BAM (return 1, nothing accumulated) and process_bam takes the records plan, whose host inflate

@@ -3,7 +3,8 @@
 Runs the bench's 10,000x SARS-CoV-2 batch through the fused accumulate a few times with
 SPG_WAVE_TIMES=<file> (k_acc_seg records per wave: entry, lifetime from entry and entry-to-loop prologue in
 s_memrealtime ticks of 10 ns, its first column, and HW_ID / XCC_ID), then reports the launch's span, the wave generations, setup and lifetime
-distributions, and how the tail ends.  Usage: python tools/wavetimes.py [depth] [out.json]
+distributions, and how the tail ends.  Usage: python tools/wavetimes.py [depth] [out.json] [max_depth]
+(max_depth 8000: the parity-mode batch the bench's nested parity_mode line runs)
 """
 import json
 import os
@@ -16,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(depth, path):
+def run(depth, path, max_depth=0):
     import torch
     import spings  # noqa: F401
     from covid_spings_variant_caller_amd import synth
@@ -24,7 +25,7 @@ def run(depth, path):
     from covid_spings_variant_caller_amd.pileup import synth_batch
     L = 29903
     ref = synth.reference(L, seed=1)
-    b = synth_batch(ref, depth, seed=2, n_threads=16)
+    b = synth_batch(ref, depth, seed=2, n_threads=16, max_depth=max_depth)
     dc = torch.from_numpy(b.codes_padded).cuda()
     dq = torch.from_numpy(b.quals_padded).cuda()
     do = torch.from_numpy(b.offsets.view(np.int64).copy()).cuda()
@@ -58,7 +59,9 @@ def analyse(path):
     w = w[w[:, 2] != 0]                              # (dynamic-tail waves that found no unit exit unrecorded)
     t0 = w[:, 0].astype(np.int64)
     t0 = (t0 - t0.min()) * 10e-3                     # us
-    col = w[:, 1].astype(np.int64)
+    col = (w[:, 1] & 0x7FFF).astype(np.int64)        # (first column mod 2^15: SARS-CoV-2 fits)
+    lend = (w[:, 1] >> 15) * 10e-3                   # entry -> the chunk loop's end
+    tailed = ((w[:, 3] >> 20) & 1).astype(bool)      # the wave ran the fused finalize (a possible call)
     life = (w[:, 2] & 0xFFFFF) * 10e-3              # from the wave's entry
     pro = (w[:, 2] >> 20) * 10e-3                    # entry -> first chunk loop setup (LUT, CSR offsets)
     end = t0 + life
@@ -68,7 +71,16 @@ def analyse(path):
     res = {"waves": int(len(w)), "waves_launched": int(n_all), "G": g, "span_us": round(span, 2),
            "start_us": q(t0), "life_us": q(life), "prologue_us": q(pro), "end_us": q(end),
            "longest_waves": [{"first_column": int(col[i]), "life_us": round(float(life[i]), 2),
-                              "start_us": round(float(t0[i]), 2)} for i in np.argsort(-life)[:8]],
+                              "loop_end_us": round(float(lend[i]), 2), "fused_finalize": bool(tailed[i]),
+                              "start_us": round(float(t0[i]), 2)} for i in np.argsort(-life)[:12]],
+           "fused_finalize_waves": int(tailed.sum()),
+           "finalize_us_of_those": q(life[tailed] - lend[tailed]) if tailed.any() else None,
+           "loop_us_of_those": q(lend[tailed] - pro[tailed]) if tailed.any() else None,
+           "loop_us_all": q(lend - pro),
+           "last_10_waves_to_end": [{"first_column": int(col[i]), "start_us": round(float(t0[i]), 2),
+                                     "loop_end_us": round(float(lend[i]), 2), "life_us": round(float(life[i]), 2),
+                                     "fused_finalize": bool(tailed[i]), "xcc": int(xcc[i])}
+                                    for i in np.argsort(-end)[:10]],
            "waves_ending_after_span_minus_5us": int((end > span - 5).sum()),
            "waves_starting_after_span_minus_10us": int((t0 > span - 10).sum()),
            "busy_wave_us_over_span": round(float(life.sum()) / span, 1),
@@ -100,16 +112,17 @@ def analyse(path):
 if __name__ == "__main__":
     depth = float(sys.argv[1]) if len(sys.argv) > 1 else 10000.0
     out = sys.argv[2] if len(sys.argv) > 2 else None
+    max_depth = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     path = os.environ.get("SPG_WAVE_TIMES")
     if not path:
         path = os.path.join(tempfile.mkdtemp(), "wt.bin")
         os.environ["SPG_WAVE_TIMES"] = path
         import subprocess
-        r = subprocess.run([sys.executable, __file__, str(depth)] + ([out] if out else []), env=os.environ)
+        r = subprocess.run([sys.executable, __file__, str(depth), out or "", str(max_depth)], env=os.environ)
         sys.exit(r.returncode)
     if os.path.exists(path):
         os.remove(path)
-    run(depth, path)
+    run(depth, path, max_depth)
     res = analyse(path)
     print(json.dumps(res, indent=1))
     if out:
