@@ -462,6 +462,50 @@ def test_fused_deep_finalize_replays(depth):
     eng.close()
 
 
+def _cut_column(batch, pos, keep):
+    """Keep only the first `keep` entries of column `pos` of a CSR batch."""
+    pb, off, c, qq = batch
+    a, e = int(off[pos - pb]), int(off[pos - pb + 1])
+    n = (e - a) - keep
+    if n <= 0:
+        return batch
+    c = np.delete(c, np.s_[a + keep:e])
+    qq = np.delete(qq, np.s_[a + keep:e])
+    off = off.copy()
+    off[pos - pb + 1:] -= np.uint64(n)
+    return pb, off, c, qq
+
+
+@pytest.mark.parametrize("depth", [6000, 10000])
+def test_fused_tail_columns_ragged(depth):
+    """The fused deep launch's last columns (its tail waves: G / 2 columns each at 10,000x and above, the columns
+    a split-tail experiment (profiles/r05zj_split_tail) cut four ways): an IUPAC call, a lone exotic allele, a P
+    product in the subnormal band, SNVs (dual mode) and ragged lengths — empty, under one 1,024-entry chunk, one to
+    five chunks.  Every position's counts, dict order and first visits (memory_summary) and the calls equal the
+    oracle's; a second, unfused finalize gives the same calls."""
+    from covid_spings_variant_caller_amd import synth
+    L = 1400
+    ref = synth.reference(L, seed=171)
+    b = synth.pileup(L, depth, seed=172, ref=ref, snv_every=17, lo=0, hi=L)
+    b = _plant_many(b, 1250, 5, 35, depth // 5)             # 'R' x 20 %: an IUPAC call near the batch's end
+    b = _plant_many(b, 1251, 3, 33, 1)                      # one 'M': exotic, replayed, no call
+    alt = 2 if ref[1300] != "C" else 4
+    b = _plant_many(b, 1300, alt, 31, 100)                  # sum q = 3100: P in the subnormal band
+    for pos, keep in [(1380, 0), (1381, 700), (1382, 1024), (1383, 1500), (1384, 2100), (1385, 3000),
+                      (1386, 4100), (1387, 5200), (1388, 1)]:
+        b = _cut_column(b, pos, keep)
+    p = dict(DEF, minEvidenceRatio=0.01)
+    eng, orc = _vs_oracle(ref, [b], p, calls_only=True)
+    fused = eng.variants()
+    assert any(v["alleles"][1] == "R" for v in fused)
+    assert sum(1 for v in fused if v["start"] >= 700) > 20
+    eng.finalize()                                           # unfused: from the records in memory
+    compare_variants(eng.variants(), fused, rtol=0)
+    t = eng.table()
+    assert t["flags"][1250] & 12 == 12 and t["flags"][1251] & 12 == 12   # exotic + replayed
+    eng.close()
+
+
 @pytest.mark.parametrize("shift", [0, 3, 8, 13])
 def test_fused_dual_second_allele_eps_only(shift):
     """FUSE dual mode: a column's frequent second allele (an SNV at AF 0.05-0.5) accumulates counts,

@@ -113,13 +113,11 @@ if __name__ == "__main__":
     depth = float(sys.argv[1]) if len(sys.argv) > 1 else 10000.0
     out = sys.argv[2] if len(sys.argv) > 2 else None
     max_depth = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    # (set before the library is loaded, in this process: an A/B build loaded by tools/ab_run.py is the one timed)
     path = os.environ.get("SPG_WAVE_TIMES")
     if not path:
         path = os.path.join(tempfile.mkdtemp(), "wt.bin")
         os.environ["SPG_WAVE_TIMES"] = path
-        import subprocess
-        r = subprocess.run([sys.executable, __file__, str(depth), out or "", str(max_depth)], env=os.environ)
-        sys.exit(r.returncode)
     if os.path.exists(path):
         os.remove(path)
     run(depth, path, max_depth)
