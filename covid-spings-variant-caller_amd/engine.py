@@ -442,6 +442,39 @@ class PileupEngine:
                     ent = {"pos": pb.value, "off": off, "codes": codes[:k.value], "quals": quals[:k.value]}
             yield ent
 
+    def copy_history_packed(self, start: int, min_bq: int, exc_cap: int = 1 << 22):
+        """The batches [start, history_count()) packed as iter_history_packed yields them, all copied at once into
+        pinned buffers of their own (reused by the next call: a write-behind checkpoint holds them until its file is
+        written).  None when the batches' exceptions exceed exc_cap (the caller then streams iter_history_packed)."""
+        n = self.history_count()
+        infos = []
+        with self._lock:
+            for i in range(max(0, int(start)), n):
+                pb, nc, ne = C.c_int64(), C.c_int64(), C.c_uint64()
+                N.check(self._L.spg_history_info(self._h, i, C.byref(pb), C.byref(nc), C.byref(ne)), "spg_history_info")
+                infos.append((i, pb.value, nc.value, ne.value))
+            n_off = sum(nc + 1 for _, _, nc, _ in infos)
+            n_ent = sum(ne for _, _, _, ne in infos)
+            st = getattr(self, "_ckstage", None)
+            if st is None or len(st[0]) < n_off or len(st[1]) < n_ent:
+                st = (pinned_empty(max(n_off, int(n_off * 1.125)), np.uint64), pinned_empty(max(16, int(n_ent * 1.125))),
+                      pinned_empty(exc_cap, np.uint64), pinned_empty(exc_cap), pinned_empty(exc_cap))
+                self._ckstage = st
+            out, o0, e0, x0 = [], 0, 0, 0
+            for i, pb, nc, ne in infos:
+                off, packed = st[0][o0:o0 + nc + 1], st[1][e0:e0 + ne]
+                xi, xc, xq = st[2][x0:], st[3][x0:], st[4][x0:]
+                k, nx = C.c_uint64(), C.c_int64()
+                N.check(self._L.spg_history_copy_packed(self._h, i, int(min_bq), N.ptr(off), N.ptr(packed), C.byref(k),
+                                                        N.ptr(xi), N.ptr(xc), N.ptr(xq), int(len(xi)), C.byref(nx)),
+                        "spg_history_copy_packed")
+                if nx.value > len(xi):
+                    return None
+                m = nx.value
+                out.append({"pos": pb, "off": off, "packed": packed[:k.value], "xi": xi[:m], "xc": xc[:m], "xq": xq[:m]})
+                o0, e0, x0 = o0 + nc + 1, e0 + ne, x0 + m
+        return out
+
     def _staging(self, n_off: int, n_entries: int):
         """Pinned host views (offsets, codes, quals) for history copies, grown as needed and reused."""
         st = getattr(self, "_stage", None)

@@ -151,7 +151,7 @@ class LiveVariantCaller:
                  minAlleleDepth: int, minEvidenceRatio: float, maxVariants: int, device: Optional[int] = None,
                  max_depth: int = 8000, stepper: str = "all", ignore_overlaps: bool = True,
                  n_threads: Optional[int] = None, devices: Optional[List[int]] = None, pileup: str = "device",
-                 gpu_inflate: bool = True, device_min_bytes: int = 32 << 20):
+                 gpu_inflate: bool = True, device_min_bytes: int = 32 << 20, checkpoint_write_behind: bool = False):
         """The reference's 7 arguments (:22-32), then the engine's: ``device`` (default LOCAL_RANK or 0), or
         ``devices`` — several GPUs of this host, each owning a coordinate range of the contig (multi.MultiEngine,
         spg_multi_*: BAM records and host batches sliced at equal-entry cuts, one RCCL gather of the call tables);
@@ -172,7 +172,12 @@ class LiveVariantCaller:
                     and the GPU decodes bases / qualities and walks the CIGARs (spg_accumulate_records);
           "host"    the host also writes every entry (spp_batch_fill) into pinned staging.
         ``gpu_inflate`` — records plans inflate BAMs of >= 4,096 BGZF members on this caller's (first) GPU
-        (spg_bgzf_inflate) instead of on the host's threads."""
+        (spg_bgzf_inflate) instead of on the host's threads.
+        ``checkpoint_write_behind`` (default off: the reference's create_checkpoint returns with its file written) —
+        create_checkpoint returns once the new batches are packed into pinned host memory; a helper thread writes the
+        shard and then the manifest (a crash leaves the previous checkpoint, whole) while the caller moves on to the next
+        BAM.  This caller's next create_checkpoint, reset_memory, close or flush_checkpoints(), and any caller's
+        load_checkpoint of that file in this process, wait for it first (and raise the error it met, if any)."""
         if pileup not in ("device", "records", "host"):
             raise ValueError(f"pileup must be 'device', 'records' or 'host', not {pileup!r}")
         self.minBaseQuality = minBaseQuality
@@ -209,15 +214,24 @@ class LiveVariantCaller:
         if self.device_pileup:
             N.use_pinned_records()
         self._inflight = collections.deque()     # (input ticket, records plan) whose copy may still be running
-        self.last_checkpoint_bytes = 0           # shard bytes the last create_checkpoint wrote
+        self._ck_bytes = 0                       # shard bytes the last create_checkpoint wrote
+        self.checkpoint_write_behind = bool(checkpoint_write_behind)
+        self._ck_job = None                      # the write-behind checkpoint in flight (a Future)
+        self._ck_pool = None
         self.reset_memory()
 
     def close(self):
         """Release the engine (HBM accumulators, history, BAM buffers) and this caller's GPU inflate scratch."""
         with self._lock:
-            self._drain()
-            self.fastaFile.close()
-            self.engine.close()
+            try:
+                self.flush_checkpoints()
+            finally:
+                if self._ck_pool is not None:
+                    self._ck_pool.shutdown(wait=True)
+                    self._ck_pool = None
+                self._drain()
+                self.fastaFile.close()
+                self.engine.close()
             if self.pileup_params.inflate_device >= 0:
                 N.gpu_lib().spg_bgzf_release(self.pileup_params.inflate_device)
 
@@ -238,6 +252,7 @@ class LiveVariantCaller:
     def reset_memory(self):
         """:37-38"""
         with self._lock:
+            self.flush_checkpoints()
             self._drain()
             self.engine.reset()
             self._batch_contig = []
@@ -507,6 +522,7 @@ class LiveVariantCaller:
         manifest in the directory lists them any more."""
         log.info("Creating checkpoint %s", filename)
         with self._lock:
+            self.flush_checkpoints()                     # (the previous one's files are complete from here on)
             n = self.engine.history_count()
             names = list(self.fastaFile.references)
             d = os.path.dirname(os.path.abspath(filename))
@@ -518,35 +534,83 @@ class LiveVariantCaller:
             first = sum(k for _, _, k in shards)
             if first > n:
                 shards, first = [], 0
-            self.last_checkpoint_bytes = 0
+            self._ck_bytes = 0
+            path, batches, behind = None, None, False
             if first < n:
                 shard = f"spgck-{self._ck_token[:16]}-{first}-{n - first}.spgck"
                 path = os.path.join(d, shard)
                 # a single-device engine packs the kept entries one byte each on the GPU (A/C/G/T with q < 63; the rest
                 # as exceptions): half the bytes down and on disk
-                it = (self.engine.iter_history_packed(first, self.minBaseQuality) if isinstance(self.engine, PileupEngine)
-                      else self.engine.iter_history(first, min_bq=self.minBaseQuality))
-                self.last_checkpoint_bytes = _write_shard(path, it)
+                if isinstance(self.engine, PileupEngine):
+                    if self.checkpoint_write_behind:
+                        batches = self.engine.copy_history_packed(first, self.minBaseQuality)
+                        behind = batches is not None
+                    if batches is None:
+                        batches = self.engine.iter_history_packed(first, self.minBaseQuality)
+                else:
+                    batches = self.engine.iter_history(first, min_bq=self.minBaseQuality)
                 shards.append((shard, first, n - first))
+            elif self.checkpoint_write_behind:
+                behind = True
             self._ck_chain[d] = list(shards)
-            old = _read_manifest(filename)
-            tmp = filename + ".tmp"
-            with open(tmp, "wb") as f:
-                np.savez(f, format=np.int64(2), token=np.array(self._ck_token),
-                         contig=np.array(self._batch_contig, np.int64), names=np.array(names),
-                         min_base_quality=np.int64(self.minBaseQuality),
-                         shard_files=np.array([s for s, _, _ in shards] or [""]),
-                         shard_ranges=np.array([[a, k] for _, a, k in shards], np.int64).reshape(-1, 2))
-            os.replace(tmp, filename)
-            if old is not None:
-                gone = {s for s, _, _ in old["shards"]} - {s for s, _, _ in shards}
-                if gone:
-                    _remove_unlisted(d, gone)
+            man = dict(format=np.int64(2), token=np.array(self._ck_token),
+                       contig=np.array(self._batch_contig, np.int64), names=np.array(names),
+                       min_base_quality=np.int64(self.minBaseQuality),
+                       shard_files=np.array([s for s, _, _ in shards] or [""]),
+                       shard_ranges=np.array([[a, k] for _, a, k in shards], np.int64).reshape(-1, 2))
+
+            def write():
+                size = _write_shard(path, batches) if path is not None else 0
+                old = _read_manifest(filename)
+                tmp = filename + ".tmp"
+                with open(tmp, "wb") as f:
+                    np.savez(f, **man)
+                os.replace(tmp, filename)
+                if old is not None:
+                    gone = {s for s, _, _ in old["shards"]} - {s for s, _, _ in shards}
+                    if gone:
+                        _remove_unlisted(d, gone)
+                return size
+
+            if behind:
+                if self._ck_pool is None:
+                    from concurrent.futures import ThreadPoolExecutor
+                    self._ck_pool = ThreadPoolExecutor(1, thread_name_prefix="spg-checkpoint")
+                self._ck_job = self._ck_pool.submit(write)
+                key, job = os.path.abspath(filename), self._ck_job
+                with _PENDING_LOCK:
+                    _PENDING[key] = job
+
+                def _done(_f, key=key, job=job):
+                    with _PENDING_LOCK:
+                        if _PENDING.get(key) is job:
+                            del _PENDING[key]
+                job.add_done_callback(_done)
+            else:
+                self._ck_bytes = write()
+
+    def flush_checkpoints(self):
+        """Wait for the write-behind checkpoint in flight (create_checkpoint) and raise the error it met, if any."""
+        with self._lock:
+            job, self._ck_job = self._ck_job, None
+            if job is not None:
+                self._ck_bytes = job.result()
+
+    @property
+    def last_checkpoint_bytes(self) -> int:
+        """Shard bytes the last create_checkpoint wrote (waits for a write-behind checkpoint)."""
+        self.flush_checkpoints()
+        return self._ck_bytes
 
     def load_checkpoint(self, filename):
         """:47-52 — replaces memory with the checkpoint's (replays its batches).  Reads the incremental
         manifest format and the single-file format of earlier versions."""
         log.info("Loading checkpoint %s", filename)
+        self.flush_checkpoints()
+        with _PENDING_LOCK:                              # another caller's write-behind checkpoint of this file
+            job = _PENDING.get(os.path.abspath(filename))
+        if job is not None:
+            job.result()
         man = _read_manifest(filename)
         if man is not None:
             if man["names"] != self.fastaFile.references:
@@ -612,6 +676,10 @@ INFO_META = [
                            "defined precisely as the GL field)"),
     ("SCORE", "1", "Float", "Custom scoring function"),
 ]
+
+
+_PENDING_LOCK = threading.Lock()
+_PENDING: Dict[str, object] = {}      # manifest path -> the write-behind checkpoint (Future) that last wrote it
 
 
 def _read_manifest(filename):

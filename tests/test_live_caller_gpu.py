@@ -199,23 +199,25 @@ def test_checkpoint_incremental_per_bam(planted):
     compare_variants(c.prepare_variants(), _oracle(ref, files[1:]).prepare_variants(), RTOL)
 
 
-def test_checkpoint_vcqueue_per_bam_names(planted):
+@pytest.mark.parametrize("behind", [False, True])
+def test_checkpoint_vcqueue_per_bam_names(planted, behind):
     """client_server/vc_queue.py:134-144 names the checkpoint after each BAM (`<temp dir>/<bam name><ext>`): each call
     writes only that BAM's batch (its shard's bytes are O(that BAM), equal for equal BAMs however many came before),
     every per-BAM manifest is a complete state (loading the k-th equals the oracle after k + 1 BAMs), and overwriting
-    one manifest with another memory keeps the shards the other manifests still list."""
+    one manifest with another memory keeps the shards the other manifests still list.  ``behind``: the write-behind
+    checkpoint (a helper thread writes each shard and manifest while the next BAM runs; reads of its files wait)."""
     d0, ref, fasta, files = planted
-    d = d0 / "vcq"
+    d = d0 / f"vcq{int(behind)}"
     d.mkdir(exist_ok=True)
     seq = [files[0], files[1], files[0], files[1], files[0]]
-    a = _caller(fasta)
+    a = _caller(fasta, checkpoint_write_behind=behind)
     names, sizes = [], []
     for k, f in enumerate(seq):
         a.process_bam(f)
         ck = str(d / f"{k}_{os.path.basename(f)}.pkl")
         a.create_checkpoint(ck)
         names.append(ck)
-        sizes.append(a.last_checkpoint_bytes)
+        sizes.append(a.last_checkpoint_bytes)           # (waits for a write-behind checkpoint)
         shards = [x for x in os.listdir(d) if x.startswith("spgck-")]
         assert len(shards) == k + 1
     assert all(x > 0 for x in sizes)
@@ -235,6 +237,30 @@ def test_checkpoint_vcqueue_per_bam_names(planted):
     compare_variants(c.prepare_variants(), _oracle(ref, seq).prepare_variants(), RTOL)
     c.load_checkpoint(names[0])
     compare_variants(c.prepare_variants(), _oracle(ref, files[1:]).prepare_variants(), RTOL)
+
+
+def test_checkpoint_write_behind_reads_and_errors(planted):
+    """Write-behind checkpoints: another caller's load_checkpoint right after create_checkpoint waits for the file and
+    equals the oracle; an error of the helper thread (here: the manifest's directory does not exist) is raised by the
+    next flush, and the caller's later checkpoints work."""
+    d0, ref, fasta, files = planted
+    d = d0 / "behind"
+    d.mkdir(exist_ok=True)
+    a = _caller(fasta, checkpoint_write_behind=True)
+    a.process_bam(files[0])
+    ck = str(d / "wb.pkl")
+    a.create_checkpoint(ck)
+    b = _caller(fasta)
+    b.load_checkpoint(ck)                         # waits for a's helper thread
+    compare_variants(b.prepare_variants(), _oracle(ref, files[:1]).prepare_variants(), RTOL)
+    a.process_bam(files[1])
+    a.create_checkpoint(str(d / "missing" / "x.pkl"))
+    with pytest.raises(OSError):
+        a.flush_checkpoints()
+    a.create_checkpoint(ck)
+    a.close()                                     # (flushes)
+    b.load_checkpoint(ck)
+    compare_variants(b.prepare_variants(), _oracle(ref, files).prepare_variants(), RTOL)
 
 
 def test_memory_view_is_a_snapshot(planted):
