@@ -35,6 +35,8 @@
 #include <string>
 #include <string_view>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
@@ -695,13 +697,49 @@ void buf_put(HostBuf &b) {
     b = HostBuf{};
 }
 
+// Persistent worker threads for par_chunks (a BAM's plan runs ~6 parallel loops; spawning 15 threads for each cost
+// ~0.3-0.5 ms a loop).  A job's chunks are taken from its counter by its caller and by the workers that pop one of its
+// queue entries; several host threads may run jobs at once (process_bams: the reader and the planner).  The caller
+// returns only after every worker that took an entry of its job has left it (entries still queued are withdrawn).
+struct ParJob {
+    const std::function<void(int)> *run;
+    int nt;
+    std::atomic<int> next{1};
+    std::atomic<int> left{0};            // queue entries not yet finished or withdrawn
+};
+struct ParPool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<ParJob *> q;
+    size_t n_threads = 0;
+    static void work(ParJob *j) {
+        for (int t; (t = j->next.fetch_add(1)) < j->nt;) (*j->run)(t);
+    }
+    void grow(size_t want) {              // (called under mu)
+        for (; n_threads < want; n_threads++)
+            std::thread([this] {
+                for (;;) {
+                    ParJob *j;
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return !q.empty(); });
+                        j = q.front();
+                        q.pop_front();
+                    }
+                    work(j);
+                    j->left.fetch_sub(1, std::memory_order_release);
+                }
+            }).detach();
+    }
+};
+ParPool &g_par = *new ParPool;           // (never destroyed: its detached workers wait on it until the process ends)
+
 // Parallel chunked loop: fn(t, i0, i1) on nt threads over [0, n)
 template <class Fn> void par_chunks(size_t n, int nt, Fn &&fn) {
     nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, (n + 16383) / 16384));
-    std::vector<std::thread> pool;
     std::exception_ptr err;
     std::mutex emu;
-    auto run = [&](int t) {
+    const std::function<void(int)> run = [&](int t) {
         try {
             fn(t, n * (size_t)t / (size_t)nt, n * (size_t)(t + 1) / (size_t)nt);
         } catch (...) {
@@ -709,9 +747,30 @@ template <class Fn> void par_chunks(size_t n, int nt, Fn &&fn) {
             if (!err) err = std::current_exception();
         }
     };
-    for (int t = 1; t < nt; t++) pool.emplace_back(run, t);
-    run(0);
-    for (auto &t : pool) t.join();
+    if (nt == 1) {
+        run(0);
+    } else {
+        ParJob j;
+        j.run = &run;
+        j.nt = nt;
+        j.left.store(nt - 1);
+        {
+            std::lock_guard<std::mutex> lk(g_par.mu);
+            g_par.grow((size_t)std::min(nt - 1, 63));
+            for (int t = 1; t < nt; t++) g_par.q.push_back(&j);
+        }
+        g_par.cv.notify_all();
+        run(0);
+        ParPool::work(&j);
+        {
+            std::lock_guard<std::mutex> lk(g_par.mu);     // withdraw the entries no worker took
+            for (auto it = g_par.q.begin(); it != g_par.q.end();) {
+                if (*it == &j) { it = g_par.q.erase(it); j.left.fetch_sub(1); }
+                else ++it;
+            }
+        }
+        while (j.left.load(std::memory_order_acquire) > 0) std::this_thread::yield();
+    }
     if (err) std::rethrow_exception(err);
 }
 
@@ -1877,11 +1936,18 @@ void plan_device(spp_plan &P, spp_batch *B) {
     uint32_t *kp = (uint32_t *)(m + o_kept), *pa = (uint32_t *)(m + o_pa), *pb = (uint32_t *)(m + o_pb);
     int64_t *col = (int64_t *)(m + o_col);
     memcpy(off, B->off.data(), 8 * (C + 1));
+    const int nw = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(1, B->threads), (n + 65535) / 65536));
+    std::vector<int64_t> spans((size_t)nw, 0);
+    par_chunks(n, nw, [&](int t, size_t i0, size_t i1) {
+        int64_t sp = 0;
+        for (size_t i = i0; i < i1; i++) {
+            kp[i] = (uint32_t)kept[i];
+            sp = std::max(sp, R.end[kept[i]] - R.pos[kept[i]]);
+        }
+        spans[(size_t)t] = sp;
+    });
     int64_t span = 0;
-    for (size_t i = 0; i < n; i++) {
-        kp[i] = (uint32_t)kept[i];
-        span = std::max(span, R.end[kept[i]] - R.pos[kept[i]]);
-    }
+    for (int64_t v : spans) span = std::max(span, v);
     uint64_t o = 0;
     for (size_t j = 0; j < np; j++) {
         const size_t a = P.T.pairs[j].first, b = P.T.pairs[j].second;
