@@ -705,7 +705,14 @@ struct ParJob {
     const std::function<void(int)> *run;
     int nt;
     std::atomic<int> next{1};
-    std::atomic<int> left{0};            // queue entries not yet finished or withdrawn
+    std::mutex m;                        // guards left; the caller sleeps on cv until it is 0 (no spinning: the
+    std::condition_variable cv;          // process's CPU quota is the workers')
+    int left = 0;                        // queue entries not yet finished or withdrawn
+    void leave(int k) {
+        std::lock_guard<std::mutex> lk(m);
+        left -= k;
+        if (left == 0) cv.notify_one();
+    }
 };
 struct ParPool {
     std::mutex mu;
@@ -727,7 +734,7 @@ struct ParPool {
                         q.pop_front();
                     }
                     work(j);
-                    j->left.fetch_sub(1, std::memory_order_release);
+                    j->leave(1);
                 }
             }).detach();
     }
@@ -753,7 +760,7 @@ template <class Fn> void par_chunks(size_t n, int nt, Fn &&fn) {
         ParJob j;
         j.run = &run;
         j.nt = nt;
-        j.left.store(nt - 1);
+        j.left = nt - 1;
         {
             std::lock_guard<std::mutex> lk(g_par.mu);
             g_par.grow((size_t)std::min(nt - 1, 63));
@@ -763,13 +770,16 @@ template <class Fn> void par_chunks(size_t n, int nt, Fn &&fn) {
         run(0);
         ParPool::work(&j);
         {
+            int withdrawn = 0;
             std::lock_guard<std::mutex> lk(g_par.mu);     // withdraw the entries no worker took
             for (auto it = g_par.q.begin(); it != g_par.q.end();) {
-                if (*it == &j) { it = g_par.q.erase(it); j.left.fetch_sub(1); }
+                if (*it == &j) { it = g_par.q.erase(it); withdrawn++; }
                 else ++it;
             }
+            if (withdrawn) j.leave(withdrawn);
         }
-        while (j.left.load(std::memory_order_acquire) > 0) std::this_thread::yield();
+        std::unique_lock<std::mutex> lk(j.m);
+        j.cv.wait(lk, [&] { return j.left == 0; });
     }
     if (err) std::rethrow_exception(err);
 }
