@@ -125,3 +125,32 @@ def test_bam_map_members_and_header(tmp_path):
         comp = np.ctypeslib.as_array(C.cast(i.comp, C.POINTER(C.c_uint8)), (i.comp_bytes,))
         assert comp.tobytes() == open(bam, "rb").read()
         m.close()
+
+
+def test_concurrent_plans_on_the_worker_pool(tmp_path):
+    """The pileup library's parallel loops run on one pool of persistent workers shared by every host thread
+    (process_bams reads the next BAM while it plans this one): four host plans of a 60,000-read BAM made at once from
+    four Python threads (ctypes releases the GIL) equal the same plan made alone — CSR offsets, entries, codes, quals."""
+    from concurrent.futures import ThreadPoolExecutor
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.pileup import simulate_bam
+    bam = str(tmp_path / "s.bam")
+    simulate_bam(bam, "NC_045512.2", synth.reference(3000, seed=3), depth=3000, seed=9, n_threads=4)
+
+    def plan(max_depth):
+        with AlignmentFile(bam) as f:
+            b = f.pileup_plan("NC_045512.2", PileupParams(n_threads=4, max_depth=max_depth)).fill()
+            out = (b.pos_begin, b.offsets.copy(), b.codes.copy(), b.quals.copy())
+            b.close()
+            return out
+
+    for md in (0, 1500):
+        want = plan(md)
+        assert len(want[2]) > 1_000_000
+        with ThreadPoolExecutor(4) as ex:
+            got = list(ex.map(plan, [md] * 4))
+        for g in got:
+            assert g[0] == want[0]
+            np.testing.assert_array_equal(g[1], want[1])
+            np.testing.assert_array_equal(g[2], want[2])
+            np.testing.assert_array_equal(g[3], want[3])
