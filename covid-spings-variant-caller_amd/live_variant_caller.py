@@ -708,15 +708,33 @@ def _is_bgzf(path: str) -> bool:
 _SHARD_MAGIC, _SHARD_END = b"SPGCKv1\0", b"SPGCKEND"
 
 
+_SHARD_SPLIT = 64 << 20      # arrays of at least this many bytes are written in _SHARD_PARTS files at once
+_SHARD_PARTS = 4
+
+
+def _shard_side(path: str, j: int) -> str:
+    return f"{path}.x{j}"
+
+
 def _write_shard(path: str, batches) -> int:
     """A checkpoint shard: each batch's arrays written as they come (64-B aligned raw arrays, no per-array CRC or copy —
     np.savez's zip CRC and buffer copies took most of a 10,000x BAM's checkpoint), then a JSON index and its offset.  A
     batch is (pos, offsets, codes, quals) or a dict of named arrays (engine.iter_history_packed: offsets, the packed
-    bytes and the exception list).  Written to <path>.tmp and renamed.  Returns the file's size."""
+    bytes and the exception list).  An array of >= _SHARD_SPLIT bytes goes out in _SHARD_PARTS pieces at once: the
+    first in this file, the others in side files <path>.x<j> written by helper threads (the page-cache copy into one
+    file is serial in the kernel; parallel writes into one file measured no faster); its index entry lists them.  Side
+    files are complete before <path>.tmp is renamed to <path>.  Returns the bytes written (main + side files)."""
     import json
     import struct
-    index = []
-    with open(path + ".tmp", "wb") as f:
+    from concurrent.futures import ThreadPoolExecutor
+    index, sides, jobs = [], [], []
+
+    def write_side(j, view):
+        with open(_shard_side(path, j) + ".tmp", "wb") as g:
+            g.write(view)
+        os.replace(_shard_side(path, j) + ".tmp", _shard_side(path, j))
+
+    with ThreadPoolExecutor(_SHARD_PARTS - 1) as ex, open(path + ".tmp", "wb") as f:
         f.write(_SHARD_MAGIC)
         for b in batches:
             if not isinstance(b, dict):
@@ -730,14 +748,29 @@ def _write_shard(path: str, batches) -> int:
                 if pad:
                     f.write(b"\0" * pad)
                 ent[name] = [f.tell(), int(a.size), a.dtype.str]
-                f.write(memoryview(a).cast("B"))
+                mv = memoryview(a).cast("B")
+                if mv.nbytes >= _SHARD_SPLIT:
+                    step = ((mv.nbytes + _SHARD_PARTS - 1) // _SHARD_PARTS + 4095) // 4096 * 4096
+                    parts = []
+                    for k in range(1, _SHARD_PARTS):
+                        lo, hi = min(mv.nbytes, k * step), min(mv.nbytes, (k + 1) * step)
+                        j = len(sides)
+                        sides.append(hi - lo)
+                        parts.append([os.path.basename(_shard_side(path, j)), hi - lo])
+                        jobs.append(ex.submit(write_side, j, mv[lo:hi]))
+                    ent[name] += [min(step, mv.nbytes), parts]
+                    f.write(mv[:min(step, mv.nbytes)])
+                else:
+                    f.write(mv)
             index.append(ent)
         at = f.tell()
         f.write(json.dumps(index).encode())
         f.write(struct.pack("<Q", at) + _SHARD_END)
         size = f.tell()
+        for j in jobs:
+            j.result()
     os.replace(path + ".tmp", path)
-    return size
+    return size + sum(sides)
 
 
 _PACKED_CODE = np.array([1, 2, 4, 8], np.uint8)
@@ -765,11 +798,30 @@ def _read_shard(path: str):
             for name in ("off", "codes", "quals", "packed", "xi", "xc", "xq"):
                 if name not in ent:
                     continue
-                pos, n, dt = ent[name]
+                pos, n, dt = ent[name][:3]
                 if dt not in ("<u8", "|u1"):
                     raise ValueError(f"{path}: unexpected dtype {dt}")
                 f.seek(pos)
-                arrs[name] = np.fromfile(f, dtype=np.dtype(dt), count=n)
+                if len(ent[name]) == 3:
+                    arrs[name] = np.fromfile(f, dtype=np.dtype(dt), count=n)
+                    continue
+                # an array in pieces (_write_shard): this file's, then the side files' (names checked: <shard>.x<j>)
+                a = np.empty(n, np.dtype(dt))
+                buf = memoryview(a).cast("B")
+                n0, parts = int(ent[name][3]), ent[name][4]
+                if n0 + sum(int(k) for _, k in parts) != buf.nbytes:
+                    raise ValueError(f"{path}: array pieces do not add up")
+                if f.readinto(buf[:n0]) != n0:
+                    raise ValueError(f"{path}: truncated checkpoint shard")
+                o = n0
+                for side, k in parts:
+                    if not (isinstance(side, str) and side.startswith(os.path.basename(path) + ".x") and "/" not in side):
+                        raise ValueError(f"{path}: bad side file name {side!r}")
+                    with open(os.path.join(os.path.dirname(path), side), "rb") as g:
+                        if g.readinto(buf[o:o + int(k)]) != int(k):
+                            raise ValueError(f"{path}: truncated side file {side}")
+                    o += int(k)
+                arrs[name] = a
             if "packed" in arrs:
                 pk = arrs["packed"]
                 codes, quals = _PACKED_CODE[pk >> 6], pk & np.uint8(63)
@@ -797,10 +849,11 @@ def _remove_unlisted(d: str, files):
             if m is not None:
                 listed.update(s for s, _, _ in m["shards"])
     for s in set(files) - listed:
-        try:
-            os.remove(os.path.join(d, s))
-        except OSError:
-            pass
+        for p in [os.path.join(d, s)] + [os.path.join(d, x) for x in os.listdir(d) if x.startswith(s + ".x")]:
+            try:
+                os.remove(p)
+            except OSError:
+                pass
 
 
 def _hval(v: str) -> str:

@@ -99,3 +99,44 @@ def test_packed_shard_roundtrip(tmp_path):
     assert got[0][0] == 100 and (got[0][1] == ent["off"]).all()
     assert (got[0][2] == codes).all() and (got[0][3] == quals).all()
     assert got[1][0] == 7 and (got[1][2] == plain[2]).all() and (got[1][3] == plain[3]).all()
+
+
+def test_shard_split_arrays_roundtrip(tmp_path, monkeypatch):
+    """Large arrays go out in pieces written at once (the shard file and side files <shard>.x<j>): read back identical
+    for ragged sizes (a piece may be empty), the byte count covers every file, a missing or short side file and a side
+    name outside the shard's are refused, and _remove_unlisted deletes a shard's side files with it."""
+    import os
+    import pytest
+    from covid_spings_variant_caller_amd import live_variant_caller as LV
+    monkeypatch.setattr(LV, "_SHARD_SPLIT", 1000)
+    rng = np.random.default_rng(11)
+    batches = []
+    for n_ent in (999, 1000, 4097, 12289, 3 * 4096 + 1):
+        off = np.array([0, n_ent // 2, n_ent], np.uint64)
+        batches.append((int(rng.integers(0, 100)), off, rng.integers(0, 18, n_ent, dtype=np.uint8),
+                        rng.integers(0, 60, n_ent, dtype=np.uint8)))
+    p = str(tmp_path / "spgck-t-0-5.spgck")
+    size = LV._write_shard(p, batches)
+    files = sorted(x for x in os.listdir(tmp_path) if x.startswith("spgck-t-0-5.spgck"))
+    assert len(files) > 1 and not any(x.endswith(".tmp") for x in files)
+    assert size == sum((tmp_path / x).stat().st_size for x in files)
+    got = LV._read_shard(p)
+    for (pa, oa, ca, qa), (pb, ob, cb, qb) in zip(got, batches):
+        assert pa == pb
+        np.testing.assert_array_equal(oa, ob)
+        np.testing.assert_array_equal(ca, cb)
+        np.testing.assert_array_equal(qa, qb)
+    side = max((tmp_path / x for x in files[1:]), key=lambda q: q.stat().st_size)
+    data = side.read_bytes()
+    side.write_bytes(data[:-1])
+    with pytest.raises(ValueError):
+        LV._read_shard(p)
+    side.unlink()
+    with pytest.raises(OSError):
+        LV._read_shard(p)
+    raw = (tmp_path / "spgck-t-0-5.spgck").read_bytes()
+    (tmp_path / "spgck-t-0-5.spgck").write_bytes(raw.replace(b"spgck-t-0-5.spgck.x", b"../../../etc/x"))
+    with pytest.raises(ValueError):
+        LV._read_shard(p)
+    LV._remove_unlisted(str(tmp_path), {"spgck-t-0-5.spgck"})
+    assert not [x for x in os.listdir(tmp_path) if x.startswith("spgck-t-0-5.spgck")]
