@@ -20,12 +20,14 @@ Also on the same line (nested, never `value`), one per BASELINE config:
   samples cut at equal entries, one ncclGather per step) — run by rank 0 while the other ranks wait (always at N > 1);
 * ``end_to_end`` (host BAM -> calls) and ``cpu_baseline`` (the oracle restatements on host cores).
 
+Output: rank 0 prints ONE compact JSON line (compact_line: the headline keys, roofline, a compact cpu_baseline and
+{value, ms_per_step, frac} per nested leg, under LINE_LIMIT bytes); the full nested result goes to --detail-out.
+
 ``--gpus N`` without a launcher (no WORLD_SIZE in the environment) starts N rank processes of this script before
 anything touches a GPU (127.0.0.1 rendezvous), as ``torch.distributed.run --nproc-per-node N`` would.
 
-Timing: W untimed warm-up steps; then 20 measurements, each of K steps (K = max(--steps, enough
-steps for >= 100 ms)) between barrier + device synchronize, max over ranks; the median measurement is
-reported.  The dominant kernel's duration comes from HIP events on the engine's stream (every
+Timing: W untimed warm-up steps; then --reps measurements, each of exactly K = --steps steps between barrier + device
+synchronize, max over ranks; the median measurement is reported (the nested legs: measurements of >= --leg-min-ms).  The dominant kernel's duration comes from HIP events on the engine's stream (every
 --time-every-th step, so the events do not idle the GPU between steps).
 """
 from __future__ import annotations
@@ -53,7 +55,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20, help="minimum steps per timed measurement")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--reps", type=int, default=20, help="timed measurements (median reported)")
-    ap.add_argument("--min-ms", type=float, default=100.0, help="minimum duration of one measurement")
+    ap.add_argument("--min-ms", type=float, default=0.0,
+                    help="headline: minimum duration of one measurement (0 = each measurement is exactly --steps steps)")
+    ap.add_argument("--leg-min-ms", type=float, default=100.0, help="nested legs: minimum duration of one measurement")
     ap.add_argument("--workload", default="sars10k", choices=["sars10k", "sars1k", "sars100k", "chr1_30x", "sars_many"],
                     help="sars_many: BASELINE config 4 as the main line (the --many-* options)")
     ap.add_argument("--depth", type=float, default=0.0, help="override the workload's depth")
@@ -87,6 +91,8 @@ def parse():
     ap.add_argument("--multi-timeout", type=float, default=300.0, help="time limit of the multi-device leg at N > 1 (s)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; "
                                                       "gloo only to exercise the path on one GPU)")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail_n{n}.json"),
+                    help="file for the full nested result (the printed line is the compact form); '' = none")
     return ap.parse_args()
 
 
@@ -355,7 +361,7 @@ def pmc_traffic_sum(keys, E):
     return None if any(v is None for v in vals) else float(sum(vals))
 
 
-def run_point(args, D, L, depth, max_depth, local, world, rank, contig, samples=1, distinct=None):
+def run_point(args, D, L, depth, max_depth, local, world, rank, contig, samples=1, distinct=None, min_ms=None):
     """The metric point (`samples` stacked samples per GPU per step, each coordinate-sharded): returns the
     result dict."""
     import torch
@@ -410,7 +416,8 @@ def run_point(args, D, L, depth, max_depth, local, world, rank, contig, samples=
 
     for k in range(args.warmup):
         step(k)
-    K, times, acc = measure(D, step, eng, args.steps, args.reps, args.min_ms, max(1, args.time_every))
+    K, times, acc = measure(D, step, eng, args.steps, args.reps, args.min_ms if min_ms is None else min_ms,
+                            max(1, args.time_every))
     fin = finalize_ms(step, eng)
     gathered = None
     if world > 1:
@@ -545,7 +552,7 @@ def run_multi_device(args, world, L, depth, max_depth):
     for _ in range(3):
         step()
     est = (time.perf_counter() - t) / 3
-    K = max(args.steps, int(math.ceil(args.min_ms * 1e-3 / max(est, 1e-7))))
+    K = max(args.steps, int(math.ceil(args.leg_min_ms * 1e-3 / max(est, 1e-7))))
     mm.kernel_times()
     mm.set_timing(1)
     times, kern = [], []
@@ -636,7 +643,7 @@ def nested_point(args, D, workload, local, world, rank, max_depth=0, samples=1, 
     `step_frac`: the roofline fraction is taken over the whole step's kernels (accumulate + finalize launches),
     for paths where the finalize is a launch of its own (chr1: k_acc_lite + k_lite_fold + sparse k_finalize)."""
     L, depth, contig = WORKLOADS[workload]
-    p = run_point(args, D, L, depth, max_depth, local, world, rank, contig, samples, distinct)
+    p = run_point(args, D, L, depth, max_depth, local, world, rank, contig, samples, distinct, min_ms=args.leg_min_ms)
     name, key = kernel_name(p["E"], p["C"], not args.full_table)
     frac_k = p["achieved"] / PEAK_HBM
     frac_s = p["algo_bytes"] / ((p["kernel_ms"] + p["finalize_ms"]) * 1e-3) / PEAK_HBM
@@ -701,7 +708,7 @@ def run_config4_columns(args, D, local, world, rank, ref, lo, hi):
     n_cand, n_replay = eng.counts()
     for k in range(args.warmup):
         step(k)
-    K, times, acc = measure(D, step, eng, args.steps, args.reps, args.min_ms, max(1, args.time_every))
+    K, times, acc = measure(D, step, eng, args.steps, args.reps, args.leg_min_ms, max(1, args.time_every))
     fin = finalize_ms(step, eng)
     med = float(np.median(times))
     t_acc = float(np.mean(acc)) * 1e-3 if len(acc) else float("nan")
@@ -749,7 +756,7 @@ def run_config4_runs(args, D, local, world, rank, ref, lo, hi):
     step(0)
     n_cand = eng.counts()[0]
     final_calls = eng.candidates()
-    K, times, acc = measure(D, step, eng, 1, max(5, args.reps // 4), args.min_ms, 1)
+    K, times, acc = measure(D, step, eng, 1, max(5, args.reps // 4), args.leg_min_ms, 1)
     med = float(np.median(times))
     t_acc = float(np.mean(acc)) * 1e-3 if len(acc) else float("nan")
     # bytes the run must move: each BAM's base_code + qual + u64 offsets, the REF chars, the candidate records
@@ -1119,6 +1126,119 @@ def end_to_end(args, device):
     return res
 
 
+LINE_LIMIT = 4096      # bytes of the printed line (the driver parses the tail of stdout: r05's 20.5 KB line was lost)
+HEAD_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+             "vs_baseline", "dtype", "data")
+
+
+def _r(x, nd=4):
+    """A number rounded to nd significant digits (the compact line carries no 17-digit floats)."""
+    if isinstance(x, float) and math.isfinite(x) and x != 0.0:
+        return float(f"{x:.{nd}g}")
+    return x
+
+
+def _leg(d, frac=True):
+    """{value, ms_per_step, frac} of one nested leg (None entries dropped)."""
+    if not isinstance(d, dict):
+        return None
+    if "error" in d:
+        return {"error": str(d["error"])[:160]}
+    out = {"value": _r(d.get("value")), "ms_per_step": _r(d.get("ms_per_step"))}
+    if frac and isinstance(d.get("roofline"), dict):
+        out["frac"] = _r(d["roofline"].get("frac"), 3)
+    return {k: v for k, v in out.items() if v is not None}
+
+
+def _e2e(e):
+    """The end-to-end leg in a few numbers: positions/s per 10,000x BAM through the lone process_bam, process_bams, and
+    the VCQueue loop's ms per BAM (uncapped / max_depth 8000)."""
+    out = {}
+    for tag, key in (("uncapped", "uncapped"), ("capped", "parity_mode_max_depth_8000")):
+        s = e.get(key)
+        if not isinstance(s, dict):
+            continue
+        o = {"process_bam_pos_s": _r(s.get("positions_per_s_per_bam"))}
+        if isinstance(s.get("process_bams"), dict):
+            o["process_bams_pos_s"] = _r(s["process_bams"].get("positions_per_s_per_bam"))
+        if isinstance(s.get("vcqueue_loop"), dict):
+            o["vcqueue_ms_per_bam"] = _r(s["vcqueue_loop"].get("ms_per_bam"))
+        b = s.get("breakdown_one_bam_device")
+        if isinstance(b, dict):
+            o["host_cap_pairing_ms"] = _r(b.get("host_depth_cap_and_pairing_ms"), 3)
+            o["inflate_ms"] = _r(b.get("inflate_kernels_ms"), 3)
+        out[tag] = o
+    c4 = e.get("config4_process_bams")
+    if isinstance(c4, dict):
+        out["config4_process_bams_pos_s"] = _r(c4.get("positions_per_s"))
+    return out
+
+
+def compact_line(res):
+    """The one JSON line rank 0 prints: the contract's headline keys, `config`, `roofline` (without prose), a compact
+    `cpu_baseline`, and {value, ms_per_step, frac} per nested leg — under LINE_LIMIT bytes.  Everything else (per-
+    measurement times, breakdowns, per-BAM arrays, the multi-device detail) goes to the detail file (`detail`)."""
+    line = {k: res[k] for k in HEAD_KEYS if k in res}
+    for k in ("value", "ms_per_step"):
+        if isinstance(line.get(k), float):
+            line[k] = float(f"{line[k]:.6g}")
+    cfg = dict(res.get("config", {}))
+    if isinstance(cfg.get("ranks"), list):
+        cfg["ranks"] = len(cfg["ranks"])
+    line["config"] = cfg
+    tm = res.get("timing")
+    if isinstance(tm, dict):
+        line["timing"] = {k: tm[k] for k in ("measurements", "steps_per_measurement") if k in tm}
+    rf = res.get("roofline")
+    if isinstance(rf, dict):
+        line["roofline"] = {k: _r(rf[k], 5) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                       "traffic_source", "kernel", "kernel_ms", "algorithmic_bytes")
+                            if k in rf}
+    cb = res.get("cpu_baseline")
+    if isinstance(cb, dict):
+        line["cpu_baseline"] = {k: _r(cb[k]) for k in ("value", "unit", "cores", "kind") if k in cb}
+        line["cpu_baseline"]["sample"] = str(cb.get("sample", ""))[:200]
+        for k in ("c_restatement", "c_restatement_16_threads"):
+            if isinstance(cb.get(k), dict):
+                line["cpu_baseline"][k] = {"value": _r(cb[k].get("value")), "cores": cb[k].get("cores")}
+    legs = {}
+    for k in ("parity_mode", "sars1k", "sars100k", "chr1_30x", "multi_device"):
+        if k in res:
+            legs[k] = _leg(res[k])
+    if isinstance(res.get("sars100k"), dict) and "parity_mode" in res["sars100k"]:
+        legs["sars100k_capped"] = _leg(res["sars100k"]["parity_mode"])
+    if isinstance(res.get("config4"), dict):
+        legs["config4"] = _leg(res["config4"])
+        pb = res["config4"].get("per_bam_finalize")
+        if isinstance(pb, dict):
+            legs["config4_per_bam_finalize"] = {"ms_per_bam": _r(pb.get("ms_per_bam"))}
+    if isinstance(res.get("end_to_end"), dict):
+        legs["end_to_end"] = _e2e(res["end_to_end"])
+    if legs:
+        line["legs"] = legs
+    if "detail" in res:
+        line["detail"] = res["detail"]
+    s = json.dumps(line)
+    if len(s) > LINE_LIMIT:                      # (never expected: drop the legs before the headline)
+        line.pop("legs", None)
+        line["legs_dropped"] = "line limit"
+    return line
+
+
+def emit(res, detail_out):
+    """Write the full nested result to `detail_out` (when it can be written) and print the compact line."""
+    if detail_out:
+        detail_out = detail_out.format(n=res.get("n_gpus", 1))
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(detail_out)), exist_ok=True)
+            with open(detail_out, "w") as f:
+                json.dump(res, f)
+            res = dict(res, detail=os.path.relpath(os.path.abspath(detail_out), ROOT))
+        except OSError as e:
+            print(f"bench: detail file {detail_out}: {e}", file=sys.stderr)
+    print(json.dumps(compact_line(res)), flush=True)
+
+
 def main():
     args = parse()
     legs = set() if args.legs == "none" else set(args.legs.split(","))
@@ -1167,7 +1287,7 @@ def main():
                "scaling": "strong", "vs_baseline": None, "dtype": "u8/f64", "data": "synthetic",
                "config": {"workload": c4["workload"], "parallelism": f"coord-shard x{world}"}, **c4}
         if rank == 0:
-            print(json.dumps(res), flush=True)
+            emit(res, args.detail_out)
         D.close()
         return
     L, depth, contig = WORKLOADS[args.workload]
@@ -1187,7 +1307,7 @@ def main():
         "metric": ("pileup positions/s at 10,000x depth (SARS-CoV-2, synthetic)" if args.workload == "sars10k"
                    and depth == 10000 and L == L_SARS else f"pileup positions/s at {depth:,.0f}x depth ({contig} "
                    f"L={L:,}, synthetic)"),
-        "value": main_pt["value"], "unit": "positions/s", "n_gpus": world, "steps": main_pt["steps"] * main_pt["reps"],
+        "value": main_pt["value"], "unit": "positions/s", "n_gpus": world, "steps": main_pt["steps"],
         "warmup": args.warmup, "ms_per_step": main_pt["ms_per_step"], "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8/f64", "data": "synthetic",
         "config": {"workload": f"{args.workload}: {contig} L={L}, {depth:.0f}x, 150-bp reads, "
@@ -1202,8 +1322,8 @@ def main():
         "timing": {"measurements": len(main_pt["measurements_ms"]), "steps_per_measurement": main_pt["steps"],
                    "steps_timed_total": main_pt["steps"] * main_pt["reps"],
                    "steps_requested": args.steps, "measurement_ms": main_pt["measurements_ms"],
-                   "statistic": "median measurement (each >= --min-ms of back-to-back steps); max over ranks; "
-                                "`steps` = every timed step of the 20 measurements"},
+                   "statistic": "median of --reps measurements, each exactly `steps` back-to-back steps between "
+                                "barrier + device synchronize (--min-ms 0); max over ranks"},
         "roofline": {"bound": "hbm", "achieved": main_pt["achieved"] / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                      "frac": main_pt["achieved"] / PEAK_HBM,
                      "traffic": pmc_traffic(kernel_name(E, C, not args.full_table)[1], E),
@@ -1253,7 +1373,7 @@ def main():
     if rank == 0 and world == 1 and "cpu" in legs:
         res["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        emit(res, args.detail_out)
     D.close()
 
 

@@ -1944,15 +1944,28 @@ int spg_path_counters(spg_ctx *c, int64_t *out, int64_t n) {
     return 0;
 }
 
-// The context's device scratch for the history readers (spg_position_entries, spg_history_copy_compact): grow-only,
-// doubled when it grows (a lookup no longer allocates and frees per call)
+// The context's device scratch for the history readers (spg_position_entries, spg_history_copy_compact): grows with
+// headroom (doubled while small, +1/8 past 64 MiB) so a lookup does not allocate and free per call
+static constexpr size_t SCRATCH_BIG = (size_t)64 << 20;
 static int grow_scratch(spg_ctx *c, size_t need) {
     if (need <= c->pe_cap) return 0;
     if (c->pe_buf) { HIPCHK(hipStreamSynchronize(c->stream)); HIPCHK(hipFree(c->pe_buf)); }
     c->pe_buf = nullptr;
     c->pe_cap = 0;
-    HIPCHK(hipMalloc(&c->pe_buf, need * 2));
-    c->pe_cap = need * 2;
+    const size_t cap = need < SCRATCH_BIG ? need * 2 : need + need / 8;
+    HIPCHK(hipMalloc(&c->pe_buf, cap));
+    c->pe_cap = cap;
+    return 0;
+}
+
+// A context with a history cap (spg_set_history_cap) budgets its HBM by that cap: a large scratch taken by one
+// compaction (~0.6 GB for a 10,000x batch) is not kept behind the cap's back
+static int trim_scratch(spg_ctx *c) {
+    if (!c->hist_cap || c->pe_cap <= SCRATCH_BIG) return 0;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipFree(c->pe_buf));
+    c->pe_buf = nullptr;
+    c->pe_cap = 0;
     return 0;
 }
 
@@ -2147,7 +2160,7 @@ static int history_compact(spg_ctx *c, int64_t i, int32_t min_bq, uint64_t *offs
             *n_exc = std::max<int64_t>((int64_t)nx, exc_cap + 1);   // (more than the device list held: not usable)
         }
     }
-    return 0;
+    return trim_scratch(c);
 }
 
 int spg_history_copy_compact(spg_ctx *c, int64_t i, int32_t min_bq, uint64_t *offsets, uint8_t *base_code, uint8_t *qual,
@@ -2191,6 +2204,9 @@ int spg_bam_release(spg_ctx *c) {
     if (!c) return fail("spg_bam_release: null ctx");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->copy_stream));
+    // an spg_bam_upload still in flight reads the caller's host buffer: done before the caller may free it, and the
+    // slot forgets it (a later BAM at the same address and size must not take it for its own upload)
+    if (c->up_stream) HIPCHK(hipStreamSynchronize(c->up_stream));
     for (BamDev &b : c->bams) b.release();
     return 0;
 }

@@ -49,6 +49,10 @@ class PileupEngine:
 
     # -- lifecycle --------------------------------------------------------------------------
     def close(self):
+        pool = getattr(self, "_stage_pool", None)
+        if pool is not None:                           # (a staging reservation in flight finishes first)
+            pool.shutdown(wait=True)
+            self._stage_pool = self._stage_job = None
         with self._lock:
             self._ext = None
             if getattr(self, "_h", None):
@@ -422,7 +426,7 @@ class PileupEngine:
             with self._lock:
                 pb, nc, ne = C.c_int64(), C.c_int64(), C.c_uint64()
                 N.check(self._L.spg_history_info(self._h, i, C.byref(pb), C.byref(nc), C.byref(ne)), "spg_history_info")
-                off, packed, _ = self._staging(nc.value + 1, ne.value)
+                off, packed, _ = self._staging(nc.value + 1, ne.value, two=False)
                 xs = getattr(self, "_xstage", None)
                 if xs is None or len(xs[1]) < exc_cap:
                     xs = (pinned_empty(exc_cap, np.uint64), pinned_empty(exc_cap), pinned_empty(exc_cap))
@@ -442,7 +446,9 @@ class PileupEngine:
                     ent = {"pos": pb.value, "off": off, "codes": codes[:k.value], "quals": quals[:k.value]}
             yield ent
 
-    def copy_history_packed(self, start: int, min_bq: int, exc_cap: int = 1 << 22):
+    CK_EXC_CAP = 1 << 22
+
+    def copy_history_packed(self, start: int, min_bq: int, exc_cap: int = CK_EXC_CAP):
         """The batches [start, history_count()) packed as iter_history_packed yields them, all copied at once into
         pinned buffers of their own (reused by the next call: a write-behind checkpoint holds them until its file is
         written).  None when the batches' exceptions exceed exc_cap (the caller then streams iter_history_packed)."""
@@ -455,8 +461,9 @@ class PileupEngine:
                 infos.append((i, pb.value, nc.value, ne.value))
             n_off = sum(nc + 1 for _, _, nc, _ in infos)
             n_ent = sum(ne for _, _, _, ne in infos)
+            self._take_reservation()
             st = getattr(self, "_ckstage", None)
-            if st is None or len(st[0]) < n_off or len(st[1]) < n_ent:
+            if st is None or len(st[0]) < n_off or len(st[1]) < n_ent or len(st[2]) < exc_cap:
                 st = (pinned_empty(max(n_off, int(n_off * 1.125)), np.uint64), pinned_empty(max(16, int(n_ent * 1.125))),
                       pinned_empty(exc_cap, np.uint64), pinned_empty(exc_cap), pinned_empty(exc_cap))
                 self._ckstage = st
@@ -475,14 +482,62 @@ class PileupEngine:
                 o0, e0, x0 = o0 + nc + 1, e0 + ne, x0 + m
         return out
 
-    def _staging(self, n_off: int, n_entries: int):
-        """Pinned host views (offsets, codes, quals) for history copies, grown as needed and reused."""
+    def _staging(self, n_off: int, n_entries: int, two: bool = True):
+        """Pinned host views (offsets, codes, quals) for history copies, grown as needed and reused (the quals array
+        only when `two`: a packed checkpoint needs one byte per entry; else None).  A reservation made ahead of time
+        (reserve_staging) is taken over here."""
+        self._take_reservation()
         st = getattr(self, "_stage", None)
         if st is None or len(st[0]) < n_off or len(st[1]) < n_entries:
-            st = (pinned_empty(max(n_off, int(n_off * 1.125)), np.uint64), pinned_empty(max(16, int(n_entries * 1.125))),
-                  pinned_empty(max(16, int(n_entries * 1.125))))
+            st = [pinned_empty(max(n_off, int(n_off * 1.125)), np.uint64), pinned_empty(max(16, int(n_entries * 1.125))),
+                  None]
             self._stage = st
-        return st[0][:n_off], st[1][:n_entries], st[2][:n_entries]
+        if two and (st[2] is None or len(st[2]) < n_entries):
+            st[2] = pinned_empty(max(16, len(st[1])))
+        return st[0][:n_off], st[1][:n_entries], (st[2][:n_entries] if two else None)
+
+    def _take_reservation(self):
+        """Install the staging reserve_staging allocated (waits for it) where it is larger than the current one."""
+        job = getattr(self, "_stage_job", None)
+        if job is None:
+            return
+        self._stage_job = None
+        got = job.result()
+        if got is None:
+            return
+        name, arrs = got
+        cur = getattr(self, name, None)
+        if cur is None or len(arrs[1]) > len(cur[1]) or len(arrs[0]) > len(cur[0]):
+            setattr(self, name, arrs)
+
+    def reserve_staging(self, n_off: int, n_entries, write_behind: bool = False):
+        """Allocate the checkpoint's pinned staging (iter_history_packed: offsets + one byte per entry) for a batch of
+        about this size on a helper thread, while the caller goes on (pinning ~0.4 GB of pages takes tens of ms: the
+        first create_checkpoint of a caller used to pay it).  `n_entries`: a number, or a callable the helper evaluates
+        (an estimate from arrays the caller keeps unchanged meanwhile).  No-op when the staging already holds that size;
+        a short estimate only means the checkpoint grows the staging itself, as before.  `write_behind`: the staging of
+        copy_history_packed (a write-behind checkpoint) instead of iter_history_packed's."""
+        if getattr(self, "_stage_job", None) is not None:
+            return
+        if getattr(self, "_stage_pool", None) is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._stage_pool = ThreadPoolExecutor(1, thread_name_prefix="spg-stage")
+        name = "_ckstage" if write_behind else "_stage"
+        st = getattr(self, name, None)
+        have = (len(st[0]), len(st[1])) if st is not None else (0, 0)
+
+        def alloc():
+            ne = int(n_entries() if callable(n_entries) else n_entries)
+            if have[0] >= n_off and have[1] >= ne:
+                return None
+            arrs = [pinned_empty(max(n_off, int(n_off * 1.125)), np.uint64), pinned_empty(max(16, int(ne * 1.125)))]
+            if write_behind:
+                xc = self.CK_EXC_CAP
+                arrs += [pinned_empty(xc, np.uint64), pinned_empty(xc), pinned_empty(xc)]
+            else:
+                arrs.append(None)
+            return name, arrs
+        self._stage_job = self._stage_pool.submit(alloc)
 
     # -- results ------------------------------------------------------------------------------
     def table(self, pos0: int = 0, n: Optional[int] = None) -> Dict[str, np.ndarray]:

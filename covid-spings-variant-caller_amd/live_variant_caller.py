@@ -151,7 +151,8 @@ class LiveVariantCaller:
                  minAlleleDepth: int, minEvidenceRatio: float, maxVariants: int, device: Optional[int] = None,
                  max_depth: int = 8000, stepper: str = "all", ignore_overlaps: bool = True,
                  n_threads: Optional[int] = None, devices: Optional[List[int]] = None, pileup: str = "device",
-                 gpu_inflate: bool = True, device_min_bytes: int = 32 << 20, checkpoint_write_behind: bool = False):
+                 gpu_inflate: bool = True, device_min_bytes: int = 32 << 20, checkpoint_write_behind: bool = False,
+                 checkpoint_prealloc: bool = True):
         """The reference's 7 arguments (:22-32), then the engine's: ``device`` (default LOCAL_RANK or 0), or
         ``devices`` — several GPUs of this host, each owning a coordinate range of the contig (multi.MultiEngine,
         spg_multi_*: BAM records and host batches sliced at equal-entry cuts, one RCCL gather of the call tables);
@@ -177,7 +178,10 @@ class LiveVariantCaller:
         create_checkpoint returns once the new batches are packed into pinned host memory; a helper thread writes the
         shard and then the manifest (a crash leaves the previous checkpoint, whole) while the caller moves on to the next
         BAM.  This caller's next create_checkpoint, reset_memory, close or flush_checkpoints(), and any caller's
-        load_checkpoint of that file in this process, wait for it first (and raise the error it met, if any)."""
+        load_checkpoint of that file in this process, wait for it first (and raise the error it met, if any).
+        ``checkpoint_prealloc`` (default on: vc_queue.py:134 checkpoints after every BAM) — a BAM kept in HBM reserves the
+        pinned staging its checkpoint will need on a helper thread while the host plans it, so a caller's first
+        create_checkpoint does not pin ~0.4 GB of pages itself."""
         if pileup not in ("device", "records", "host"):
             raise ValueError(f"pileup must be 'device', 'records' or 'host', not {pileup!r}")
         self.minBaseQuality = minBaseQuality
@@ -216,6 +220,7 @@ class LiveVariantCaller:
         self._inflight = collections.deque()     # (input ticket, records plan) whose copy may still be running
         self._ck_bytes = 0                       # shard bytes the last create_checkpoint wrote
         self.checkpoint_write_behind = bool(checkpoint_write_behind)
+        self.checkpoint_prealloc = bool(checkpoint_prealloc)
         self._ck_job = None                      # the write-behind checkpoint in flight (a Future)
         self._ck_pool = None
         self.reset_memory()
@@ -322,6 +327,12 @@ class LiveVariantCaller:
             return False
         with self._lock:
             reads = self.engine.bam_reads(n)
+            if self.checkpoint_prealloc and isinstance(self.engine, PileupEngine):
+                # the checkpoint's pinned staging for this BAM's batch, allocated while the host plans it (entries <=
+                # the kept reads' aligned spans; vc_queue.py:134 checkpoints after every BAM)
+                self.engine.reserve_staging(self.fastaFile.get_reference_length(contig) + 1,
+                                            lambda r=reads: int(r["end"].sum(dtype=np.int64) - r["pos"].sum(dtype=np.int64)),
+                                            write_behind=self.checkpoint_write_behind)
             batch = bam.pileup_fields(contig, reads, self.pileup_params)
             if batch.n_cols == 0:
                 batch.close()
@@ -421,6 +432,7 @@ class LiveVariantCaller:
         with ThreadPoolExecutor(1) as io, ThreadPoolExecutor(1) as planner:
             maps = [io.submit(read, p) for p in paths[:2]]
             pending = None
+            done = False
             try:
                 for i in range(len(paths)):
                     bam, bmap = maps[i].result()
@@ -454,10 +466,18 @@ class LiveVariantCaller:
                 if pending is not None:
                     job, pending = pending, None
                     finish(job)
+                done = True
             finally:
                 if pending is not None:
                     pending[2].cancel()
                     pending[1].close()
+                if not done:
+                    # an error: an upload of the next BAM may still read its pinned map — wait for it and drop it from
+                    # its slot (spg_bam_release) before the maps are closed
+                    try:
+                        self.engine.bam_release()
+                    except Exception as e:          # (never masks the error that got us here)
+                        log.warning("spg_bam_release after an error: %s", e)
                 for f in maps:
                     if f is not None:
                         try:
@@ -696,7 +716,7 @@ def _read_manifest(filename):
             return {"token": str(z["token"]), "names": [str(x) for x in z["names"].tolist()],
                     "contig": contig, "n": len(contig), "min_base_quality": int(z["min_base_quality"]),
                     "shards": shards}
-    except (OSError, ValueError, KeyError):
+    except (OSError, ValueError, KeyError, TypeError, AttributeError):   # (a plain .npy holds an ndarray, not a zip)
         return None
 
 
@@ -762,13 +782,16 @@ def _write_shard(path: str, batches) -> int:
                     f.write(mv[:min(step, mv.nbytes)])
                 else:
                     f.write(mv)
+            # the side files of this batch are written before the next batch is asked for: a generator may hand out
+            # views of one reused buffer (engine.iter_history_packed's pinned staging), which its next batch overwrites
+            for j in jobs:
+                j.result()
+            jobs.clear()
             index.append(ent)
         at = f.tell()
         f.write(json.dumps(index).encode())
         f.write(struct.pack("<Q", at) + _SHARD_END)
         size = f.tell()
-        for j in jobs:
-            j.result()
     os.replace(path + ".tmp", path)
     return size + sum(sides)
 

@@ -107,3 +107,48 @@ def test_multi_helper_protocol():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--multi-helper", "--gpus", "2"], input="",
                        env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and p.stdout == ""
+
+
+def _full_result():
+    """The r05 default run's full nested result (20.5 KB when printed whole: the line the driver could not parse)."""
+    import json
+    with open(os.path.join(ROOT, "profiles", "r05zy_final_bench", "bench.json")) as f:
+        return json.load(f)
+
+
+def test_compact_line_under_limit_and_complete(tmp_path, capsys):
+    import json
+    res = _full_result()
+    assert len(json.dumps(res)) > 16000
+    bench.emit(res, str(tmp_path / "detail_n{n}.json"))
+    out = capsys.readouterr().out
+    lines = out.splitlines()
+    assert len(lines) == 1 and len(lines[0].encode()) < bench.LINE_LIMIT < 8192
+    line = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype", "config",
+              "higher_is_better", "scaling", "vs_baseline", "data"):
+        assert k in line, k
+    assert line["value"] == pytest.approx(res["value"], rel=1e-5)
+    assert line["ms_per_step"] == pytest.approx(res["ms_per_step"], rel=1e-5)
+    rf = line["roofline"]
+    assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(rf)
+    assert rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"], rel=1e-3)
+    assert {"value", "unit", "cores", "kind", "sample"} <= set(line["cpu_baseline"])
+    for leg in ("parity_mode", "sars1k", "sars100k", "chr1_30x", "config4", "multi_device"):
+        assert {"value", "ms_per_step", "frac"} <= set(line["legs"][leg]), leg
+    assert line["legs"]["end_to_end"]["uncapped"]["process_bam_pos_s"] > 0
+    # the full result is in the detail file, byte for byte what the run produced
+    detail = tmp_path / "detail_n1.json"
+    assert json.loads(detail.read_text()) == res
+    assert line["detail"].endswith("detail_n1.json")
+
+
+def test_compact_line_bounded_with_long_fields():
+    import json
+    res = _full_result()
+    res["multi_device"] = {"error": "x" * 50000}
+    res["config"]["workload"] = "w" * 3000
+    res["end_to_end"]["uncapped"]["path"] = "p" * 50000
+    s = json.dumps(bench.compact_line(res))
+    assert len(s) < 8192
+    assert json.loads(s)["value"] == pytest.approx(res["value"], rel=1e-5)

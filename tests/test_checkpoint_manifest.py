@@ -140,3 +140,55 @@ def test_shard_split_arrays_roundtrip(tmp_path, monkeypatch):
         LV._read_shard(p)
     LV._remove_unlisted(str(tmp_path), {"spgck-t-0-5.spgck"})
     assert not [x for x in os.listdir(tmp_path) if x.startswith("spgck-t-0-5.spgck")]
+
+
+def test_shard_split_reused_buffer_generator(tmp_path, monkeypatch):
+    """engine.iter_history_packed yields views of ONE pinned staging buffer that its next batch
+    overwrites.  Side-file pieces of a batch must be on disk before the generator is resumed: a generator that reuses
+    one buffer over 3 batches (side writers slowed down) reads back every batch's own bytes."""
+    import threading
+    import time
+    from covid_spings_variant_caller_amd import live_variant_caller as LV
+    monkeypatch.setattr(LV, "_SHARD_SPLIT", 1000)
+    orig = LV._shard_side
+
+    def slow_side(path, j):
+        if threading.current_thread() is not threading.main_thread():
+            time.sleep(0.05)                          # (a helper thread still writing when the next batch arrives)
+        return orig(path, j)
+
+    monkeypatch.setattr(LV, "_shard_side", slow_side)
+    n = 20000
+    staging = np.zeros(2 * n, np.uint8)
+    expect = []
+
+    def gen():
+        rng = np.random.default_rng(17)
+        for k in range(3):
+            codes = staging[:n]
+            quals = staging[n:]
+            codes[:] = rng.integers(0, 18, n, dtype=np.uint8)
+            quals[:] = rng.integers(0, 60, n, dtype=np.uint8)
+            expect.append((k, codes.copy(), quals.copy()))
+            yield (k, np.array([0, n // 3, n], np.uint64), codes, quals)
+
+    p = str(tmp_path / "spgck-r-0-3.spgck")
+    LV._write_shard(p, gen())
+    got = LV._read_shard(p)
+    assert len(got) == 3
+    for (pa, _, ca, qa), (k, ce, qe) in zip(got, expect):
+        assert pa == k
+        np.testing.assert_array_equal(ca, ce)
+        np.testing.assert_array_equal(qa, qe)
+
+
+def test_stray_npy_in_checkpoint_dir(tmp_path):
+    """a plain .npy file beside the manifests is not a manifest (np.load returns an ndarray) and does
+    not break _remove_unlisted."""
+    from covid_spings_variant_caller_amd import live_variant_caller as LV
+    stray = tmp_path / "stray.npy"
+    np.save(str(stray), np.arange(5))
+    assert _read_manifest(str(stray)) is None
+    (tmp_path / "spgck-z-0-1.spgck").write_bytes(b"x")
+    LV._remove_unlisted(str(tmp_path), {"spgck-z-0-1.spgck"})
+    assert not (tmp_path / "spgck-z-0-1.spgck").exists() and stray.exists()
