@@ -141,6 +141,8 @@ def gpu_lib():
     _sig(L.spg_multi_accumulate, i32, vp, i64, i64, vp, vp, vp, u64, C.c_uint32)
     _sig(L.spg_multi_finalize, i32, vp)
     _sig(L.spg_multi_get_candidates, i32, vp, vp, i64, C.POINTER(i64))
+    _sig(L.spg_multi_get_candidates_async, i32, vp, C.POINTER(u64))
+    _sig(L.spg_multi_wait_candidates, i32, vp, u64, vp, i64, C.POINTER(i64))
     _sig(L.spg_multi_partition, i32, vp, C.POINTER(i64))
     _sig(L.spg_multi_context, i32, vp, i32, C.POINTER(vp))
     _sig(L.spg_multi_accumulate_records, i32, vp, C.POINTER(SpgRecords), C.c_uint32)
@@ -180,6 +182,7 @@ def gpu_lib():
     _sig(L.spg_get_details, i32, vp, vp, i64, C.POINTER(i64))
     _sig(L.spg_device_results, i32, vp, C.POINTER(vp), C.POINTER(vp))
     _sig(L.spg_copy_candidates_device, i32, vp, vp, i64)
+    _sig(L.spg_copy_table_device, i32, vp, vp, i64, C.POINTER(i64))
     _sig(L.spg_last_kernel_ms, i32, vp, C.POINTER(C.c_float), C.POINTER(C.c_float))
     _sig(L.spg_kernel_times, i32, vp, vp, vp, i64, C.POINTER(i64))
     _sig(L.spg_set_timing, i32, vp, i32)

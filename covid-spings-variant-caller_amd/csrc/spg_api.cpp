@@ -47,6 +47,8 @@ hipError_t launch_ck_compact(const Hist &h, uint32_t min_bq, uint64_t *kept, uin
                              size_t *scan_bytes, uint8_t *oc, uint8_t *oq, hipStream_t st);
 hipError_t launch_ck_pack(uint8_t *oc, const uint8_t *oq, uint64_t m, uint64_t base, uint64_t *xi, uint8_t *xc, uint8_t *xq,
                           uint32_t *xn, uint32_t xcap, hipStream_t st);
+hipError_t launch_table_copy(const Counters *ctr, const uint32_t *kerr, const uint32_t *ferr, const void *cand, int64_t cap,
+                             int64_t detail_cap, void *dst, hipStream_t st);
 size_t inflate_scratch_bytes(uint64_t comp_bytes, int64_t n);
 hipError_t launch_inflate(const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *mem, int64_t n, uint8_t *out,
                           uint32_t *status, void *scratch, hipStream_t st);
@@ -1888,6 +1890,16 @@ int spg_copy_candidates_device(spg_ctx *c, void *dst, int64_t cap) {
     HIPCHK(hipMemcpyAsync(dst, &c->ctr[c->cslot].n_cand, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
     const int64_t n = std::min<int64_t>(cap, c->cand_cap);
     if (n) HIPCHK(hipMemcpyAsync((char *)dst + 8, c->cand, sizeof(spg_candidate) * n, hipMemcpyDeviceToDevice, c->stream));
+    return 0;
+}
+
+int spg_copy_table_device(spg_ctx *c, void *dst, int64_t cap, int64_t *n_copy_cap) {
+    if (!c || !dst || cap < 0) return fail("spg_copy_table_device: bad argument");
+    if (!c->finalized) return fail("spg_copy_table_device: spg_finalize has not been called since the last accumulate/reset");
+    HIPCHK(hipSetDevice(c->device));
+    const int64_t n = std::min<int64_t>(cap, c->cand_cap);
+    HIPCHK(launch_table_copy(c->ctr + c->cslot, c->kerr, c->ferr, c->cand, n, c->detail_cap, dst, c->stream));
+    if (n_copy_cap) *n_copy_cap = n;
     return 0;
 }
 

@@ -349,6 +349,36 @@ hipError_t launch_pos_copy(const Hist *H, const int32_t *items, int32_t n, const
     return hipGetLastError();
 }
 
+// spg_copy_table_device: the finalize's call table and its status in one device-side copy, so a consumer (the
+// multi-device gather) needs no host round trip per context: a 16-B header {n_cand, status, n_detail, records copied}
+// and min(n_cand, cap) 56-B records (7 u64 each).  status: 1 replay depth mismatch, 2 run error word, 4 fill error word,
+// 8 more candidates than the copy holds, 16 more details than the context's buffer (its finalize must run again).
+__global__ __launch_bounds__(256) void k_table_copy(const Counters *__restrict__ ctr, const uint32_t *__restrict__ kerr,
+                                                    const uint32_t *__restrict__ ferr, const uint64_t *__restrict__ cand,
+                                                    int64_t cap, int64_t detail_cap, uint32_t *__restrict__ dst) {
+    const Counters h = *ctr;
+    const uint64_t n = std::min<uint64_t>(h.n_cand, (uint64_t)cap);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const uint32_t st = (h.err ? 1u : 0u) | (*kerr ? 2u : 0u) | (*ferr ? 4u : 0u) | ((int64_t)h.n_cand > cap ? 8u : 0u) |
+                            ((int64_t)h.n_detail > detail_cap ? 16u : 0u);
+        dst[0] = h.n_cand;
+        dst[1] = st;
+        dst[2] = h.n_detail;
+        dst[3] = (uint32_t)n;
+    }
+    uint64_t *out = reinterpret_cast<uint64_t *>(dst + 4);
+    const uint64_t words = n * (sizeof(spg_candidate) / 8);
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < words; i += (uint64_t)gridDim.x * 256) out[i] = cand[i];
+}
+hipError_t launch_table_copy(const Counters *ctr, const uint32_t *kerr, const uint32_t *ferr, const void *cand, int64_t cap,
+                             int64_t detail_cap, void *dst, hipStream_t st) {
+    const int64_t words = cap * (int64_t)(sizeof(spg_candidate) / 8);
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((words + 255) / 256, 64));
+    k_table_copy<<<blocks, 256, 0, st>>>(ctr, kerr, ferr, static_cast<const uint64_t *>(cand), cap, detail_cap,
+                                         static_cast<uint32_t *>(dst));
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------------------------------
 // The transposed fill (r05): one wave per chunk of 64 consecutive reads (BAM order), lane = read.  Each lane walks its
 // own CIGAR once, column by column over the chunk's column span, with its quality and packed-base bytes in 8-byte

@@ -41,6 +41,20 @@ struct MBatch {
     int64_t pos_begin, n_cols;
 };
 
+// One call table in flight (spg_multi_get_candidates_async): every device's table copied on its stream
+// (spg_copy_table_device), gathered, and copied into this slot's pinned host buffer; `ev` marks the copies done.
+struct TSlot {
+    uint64_t ticket = 0;                   // 0: free
+    bool collected = false;                // the host bytes were parsed (merged / bad)
+    bool bad = false;                      // a table outgrew its copy or carried an error word
+    std::vector<hipEvent_t> ev;            // per device (RCCL: [0] only, after the gather's copy)
+    std::vector<int> ev_used;
+    std::vector<int64_t> cut;              // the device ranges the tables were made over
+    std::vector<spg_candidate> merged;     // memory order
+};
+
+constexpr size_t TABLE_HEAD = 16;          // spg_copy_table_device's header
+
 }  // namespace
 
 struct spg_multi {
@@ -66,9 +80,12 @@ struct spg_multi {
     double rebalance_ratio = 1.25;         // max device load / mean that triggers a re-plan
     int64_t rebalance_max_batches = 256;   // ... while the sample holds at most this many batches
     int64_t n_replans = 0;
-    std::vector<void *> send;              // per device: [u64 count][cap x spg_candidate]
+    std::vector<void *> send;              // per device: [16-B table header][cap x spg_candidate]
     void *recv = nullptr;                  // device 0: n x send size
-    int64_t cap = 0;
+    int64_t cap = 0;                       // records per device table copy (grown from the tables seen)
+    uint8_t *host[2] = {nullptr, nullptr}; // pinned: n x send size per table slot
+    TSlot slot[2];
+    uint64_t tseq = 0;                     // tickets handed out
 };
 
 static thread_local std::string g_merr;
@@ -141,6 +158,15 @@ int spg_multi_plan_cuts(const uint64_t *w, int64_t n_buckets, int64_t bucket, in
 
 int spg_multi_destroy(spg_multi *m) {
     if (!m) return 0;
+    for (TSlot &t : m->slot) {             // (copies in flight into the pinned buffers end first)
+        for (size_t d = 0; d < t.ev.size(); d++)
+            if (t.ev[d]) {
+                if (t.ev_used[d]) (void)hipEventSynchronize(t.ev[d]);
+                (void)hipEventDestroy(t.ev[d]);
+            }
+    }
+    for (uint8_t *h : m->host)
+        if (h) (void)hipHostFree(h);
     for (size_t i = 0; i < m->ctx.size(); i++) {
         if (m->send.size() > i && m->send[i]) { (void)hipSetDevice(m->dev[i]); (void)hipFree(m->send[i]); }
         if (m->ctx[i]) spg_destroy(m->ctx[i]);
@@ -203,12 +229,15 @@ int spg_multi_set_reference(spg_multi *m, const char *seq, int64_t len) {
     return 0;
 }
 
+static int collect_all(spg_multi *m);
+
 // (Re)create the device contexts over the current cuts (kept when the cuts did not change: a reset then suffices).
 static int build_contexts(spg_multi *m) {
     if (!m->ctx_cut.empty() && m->ctx_cut == m->cut) {
         for (int d = 0; d < m->n; d++) MCTX(spg_reset(m->ctx[d]));
         return 0;
     }
+    if (int rc = collect_all(m)) return rc;    // (tables in flight were enqueued on the streams destroyed here)
     for (int d = 0; d < m->n; d++) {
         if (m->ctx[d]) spg_destroy(m->ctx[d]);
         m->ctx[d] = nullptr;
@@ -560,74 +589,202 @@ int spg_multi_finalize(spg_multi *m) {
     return 0;
 }
 
-// The merged call table: every device's table packed on its own stream, one ncclGather to device 0 (devices
-// listed twice: device copies), then in memory order — (first_batch, pos, allele rank), as the shim orders one
-// context's table; positions are reference positions (each device's local position + its cut).
-int spg_multi_get_candidates(spg_multi *m, spg_candidate *out, int64_t cap, int64_t *n_out) {
-    if (!m || !n_out) return mfail("spg_multi_get_candidates: null");
-    if (!m->ctx[0]) { *n_out = 0; return 0; }
-    int64_t need = 1;
-    for (spg_ctx *c : m->ctx) {
-        int64_t nc = 0, nd = 0;
-        MCTX(spg_count(c, &nc, &nd));
-        need = std::max(need, nc);
+}  // extern "C"
+
+// The table copies sized for `need` records per device: send buffers on every device, the gather's receive buffer on
+// devices[0], two pinned host slots.  Tables in flight are collected first (their buffers are replaced).
+static int ensure_table_bufs(spg_multi *m, int64_t need) {
+    if (need <= m->cap && m->host[0]) return 0;
+    if (int rc = collect_all(m)) return rc;
+    const int64_t cap = std::max<int64_t>({need, m->cap, 1024});
+    const size_t per = TABLE_HEAD + sizeof(spg_candidate) * (size_t)cap;
+    for (int d = 0; d < m->n; d++) {
+        MHIP(hipSetDevice(m->dev[d]));
+        if (m->send[d]) MHIP(hipFree(m->send[d]));
+        m->send[d] = nullptr;
+        MHIP(hipMalloc(&m->send[d], per));
     }
-    const size_t rec = sizeof(spg_candidate), per = 8 + rec * (size_t)need;
-    if (need > m->cap) {                 // buffers sized for the largest table (KBs at these call rates)
-        for (int d = 0; d < m->n; d++) {
-            MHIP(hipSetDevice(m->dev[d]));
-            if (m->send[d]) MHIP(hipFree(m->send[d]));
-            m->send[d] = nullptr;
-            MHIP(hipMalloc(&m->send[d], per));
-        }
-        MHIP(hipSetDevice(m->dev[0]));
-        if (m->recv) MHIP(hipFree(m->recv));
-        m->recv = nullptr;
-        MHIP(hipMalloc(&m->recv, per * (size_t)m->n));
-        m->cap = need;
+    MHIP(hipSetDevice(m->dev[0]));
+    if (m->recv) MHIP(hipFree(m->recv));
+    m->recv = nullptr;
+    if (m->rccl) MHIP(hipMalloc(&m->recv, per * (size_t)m->n));
+    for (uint8_t *&h : m->host) {
+        if (h) MHIP(hipHostFree(h));
+        h = nullptr;
+        MHIP(hipHostMalloc((void **)&h, per * (size_t)m->n, hipHostMallocDefault));
     }
-    const size_t per_cap = 8 + rec * (size_t)m->cap;
+    m->cap = cap;
+    return 0;
+}
+
+// Enqueue one table into slot t: per device the table + status copied on its own stream (no host wait), ONE
+// ncclGather to devices[0] (distinct devices) or per-device copies, then the bytes into the slot's pinned buffer.
+static int enqueue_table(spg_multi *m, TSlot &t) {
+    const size_t per = TABLE_HEAD + sizeof(spg_candidate) * (size_t)m->cap;
+    if (t.ev.empty()) {
+        t.ev.assign((size_t)m->n, nullptr);
+        t.ev_used.assign((size_t)m->n, 0);
+    }
+    uint8_t *h = m->host[&t - m->slot];
     std::vector<hipStream_t> st((size_t)m->n);
     for (int d = 0; d < m->n; d++) {
         MCTX(spg_stream(m->ctx[d], (void **)&st[(size_t)d]));
-        MCTX(spg_copy_candidates_device(m->ctx[d], m->send[d], m->cap));
+        int64_t ncopy = 0;
+        MCTX(spg_copy_table_device(m->ctx[d], m->send[d], m->cap, &ncopy));
     }
-    std::vector<uint8_t> h(per_cap * (size_t)m->n);
+    std::fill(t.ev_used.begin(), t.ev_used.end(), 0);
     if (m->rccl) {
         MCCL(ncclGroupStart());
         for (int d = 0; d < m->n; d++) {
             MHIP(hipSetDevice(m->dev[d]));
-            MCCL(ncclGather(m->send[d], d == 0 ? m->recv : nullptr, per_cap, ncclUint8, 0, m->comm[d], st[(size_t)d]));
+            MCCL(ncclGather(m->send[d], d == 0 ? m->recv : nullptr, per, ncclUint8, 0, m->comm[d], st[(size_t)d]));
         }
         MCCL(ncclGroupEnd());
         MHIP(hipSetDevice(m->dev[0]));
-        MHIP(hipMemcpyAsync(h.data(), m->recv, h.size(), hipMemcpyDeviceToHost, st[0]));
-        MHIP(hipStreamSynchronize(st[0]));
+        MHIP(hipMemcpyAsync(h, m->recv, per * (size_t)m->n, hipMemcpyDeviceToHost, st[0]));
+        if (!t.ev[0]) MHIP(hipEventCreateWithFlags(&t.ev[0], hipEventDisableTiming));
+        MHIP(hipEventRecord(t.ev[0], st[0]));
+        t.ev_used[0] = 1;
     } else {
         for (int d = 0; d < m->n; d++) {
             MHIP(hipSetDevice(m->dev[d]));
-            MHIP(hipMemcpyAsync(h.data() + per_cap * (size_t)d, m->send[d], per_cap, hipMemcpyDeviceToHost, st[(size_t)d]));
-            MHIP(hipStreamSynchronize(st[(size_t)d]));
+            MHIP(hipMemcpyAsync(h + per * (size_t)d, m->send[d], per, hipMemcpyDeviceToHost, st[(size_t)d]));
+            if (!t.ev[(size_t)d]) MHIP(hipEventCreateWithFlags(&t.ev[(size_t)d], hipEventDisableTiming));
+            MHIP(hipEventRecord(t.ev[(size_t)d], st[(size_t)d]));
+            t.ev_used[(size_t)d] = 1;
         }
     }
-    std::vector<spg_candidate> all;
+    t.cut = m->ctx_cut;
+    t.collected = false;
+    t.bad = false;
+    t.merged.clear();
+    return 0;
+}
+
+// Wait for slot t's copies and parse them: the devices' tables merged in memory order — (first_batch, pos, allele
+// rank), as the shim orders one context's table — with reference positions; `bad` when one outgrew its copy or carried
+// an error word.
+static int collect(spg_multi *m, TSlot &t) {
+    if (t.collected || !t.ticket) return 0;
+    for (size_t d = 0; d < t.ev.size(); d++)
+        if (t.ev_used[d]) MHIP(hipEventSynchronize(t.ev[d]));
+    const size_t per = TABLE_HEAD + sizeof(spg_candidate) * (size_t)m->cap;
+    const uint8_t *h = m->host[&t - m->slot];
+    size_t total = 0;
+    t.bad = false;
     for (int d = 0; d < m->n; d++) {
-        uint64_t k = 0;
-        memcpy(&k, h.data() + per_cap * (size_t)d, 8);
-        const spg_candidate *r = reinterpret_cast<const spg_candidate *>(h.data() + per_cap * (size_t)d + 8);
-        for (uint64_t i = 0; i < k; i++) {
-            all.push_back(r[i]);
-            all.back().pos += m->ctx_cut[d];
-        }
+        uint32_t head[4];
+        memcpy(head, h + per * (size_t)d, sizeof head);
+        if (head[1] != 0 || head[3] != head[0]) t.bad = true;
+        total += head[3];
     }
-    std::stable_sort(all.begin(), all.end(), [](const spg_candidate &x, const spg_candidate &y) {
-        if (x.first_batch != y.first_batch) return x.first_batch < y.first_batch;
-        if (x.pos != y.pos) return x.pos < y.pos;
-        return x.rank < y.rank;
-    });
+    t.merged.clear();
+    if (!t.bad) {
+        t.merged.reserve(total);
+        for (int d = 0; d < m->n; d++) {
+            uint32_t head[4];
+            memcpy(head, h + per * (size_t)d, sizeof head);
+            const spg_candidate *r = reinterpret_cast<const spg_candidate *>(h + per * (size_t)d + TABLE_HEAD);
+            const size_t at = t.merged.size();
+            t.merged.insert(t.merged.end(), r, r + head[3]);
+            for (size_t i = at; i < t.merged.size(); i++) t.merged[i].pos += t.cut[(size_t)d];
+        }
+        std::sort(t.merged.begin(), t.merged.end(), [](const spg_candidate &x, const spg_candidate &y) {
+            if (x.first_batch != y.first_batch) return x.first_batch < y.first_batch;
+            if (x.pos != y.pos) return x.pos < y.pos;
+            return x.rank < y.rank;
+        });
+    }
+    t.collected = true;
+    return 0;
+}
+
+static int collect_all(spg_multi *m) {
+    for (TSlot &t : m->slot)
+        if (int rc = collect(m, t)) return rc;
+    return 0;
+}
+
+// A free slot for the next table (the older one's ticket retired when both are in flight).
+static TSlot &next_slot(spg_multi *m) {
+    TSlot &a = m->slot[0], &b = m->slot[1];
+    if (!a.ticket) return a;
+    if (!b.ticket) return b;
+    return a.ticket < b.ticket ? a : b;
+}
+
+static int finish_out(const std::vector<spg_candidate> &all, spg_candidate *out, int64_t cap, int64_t *n_out) {
     *n_out = (int64_t)all.size();
     if (*n_out > cap) return mfail("spg_multi_get_candidates: output capacity too small");
-    if (!all.empty() && out) memcpy(out, all.data(), rec * all.size());
+    if (!all.empty() && out) memcpy(out, all.data(), sizeof(spg_candidate) * all.size());
+    return 0;
+}
+
+extern "C" {
+
+int spg_multi_get_candidates(spg_multi *m, spg_candidate *out, int64_t cap, int64_t *n_out) {
+    if (!m || !n_out) return mfail("spg_multi_get_candidates: null");
+    *n_out = 0;
+    if (!m->ctx[0]) return 0;
+    if (int rc = ensure_table_bufs(m, m->cap)) return rc;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        TSlot &t = next_slot(m);
+        if (t.ticket && !t.collected) if (int rc = collect(m, t)) return rc;
+        t.ticket = ++m->tseq;
+        if (int rc = enqueue_table(m, t)) { t.ticket = 0; return rc; }
+        if (int rc = collect(m, t)) { t.ticket = 0; return rc; }
+        t.ticket = 0;                        // (a synchronous table: the slot is free again)
+        if (!t.bad) return finish_out(t.merged, out, cap, n_out);
+        // a table outgrew its copy, or an error word: settle every context (reports the error, or grows its buffers
+        // and finalizes again), size the copies for the largest table, and take it once more
+        int64_t need = 1;
+        for (spg_ctx *c : m->ctx) {
+            int64_t nc = 0, nd = 0;
+            MCTX(spg_count(c, &nc, &nd));
+            need = std::max(need, nc);
+        }
+        if (int rc = ensure_table_bufs(m, need)) return rc;
+    }
+    return mfail("spg_multi_get_candidates: the device tables did not settle");
+}
+
+int spg_multi_get_candidates_async(spg_multi *m, uint64_t *ticket) {
+    if (!m || !ticket) return mfail("spg_multi_get_candidates_async: null");
+    *ticket = 0;
+    if (int rc = ensure_table_bufs(m, m->cap)) return rc;
+    TSlot &t = next_slot(m);
+    if (t.ticket && !t.collected) if (int rc = collect(m, t)) return rc;   // (retired: its wait fails)
+    t.ticket = ++m->tseq;
+    if (!m->ctx[0]) {                        // nothing accumulated, no contexts: an empty table
+        std::fill(t.ev_used.begin(), t.ev_used.end(), 0);
+        t.merged.clear();
+        t.bad = false;
+        t.collected = true;
+    } else if (int rc = enqueue_table(m, t)) {
+        t.ticket = 0;
+        return rc;
+    }
+    *ticket = t.ticket;
+    return 0;
+}
+
+int spg_multi_wait_candidates(spg_multi *m, uint64_t ticket, spg_candidate *out, int64_t cap, int64_t *n_out) {
+    if (!m || !n_out) return mfail("spg_multi_wait_candidates: null");
+    *n_out = 0;
+    TSlot *t = nullptr;
+    for (TSlot &s : m->slot)
+        if (ticket && s.ticket == ticket) t = &s;
+    if (!t) return mfail("spg_multi_wait_candidates: unknown or retired ticket (two tables at most in flight)");
+    if (int rc = collect(m, *t)) return rc;
+    if (t->bad) {
+        t->ticket = 0;
+        g_merr = "spg_multi_wait_candidates: a device table outgrew its copy or carried an error word; take this "
+                 "sample's table with spg_multi_get_candidates before its reset";
+        return 1;
+    }
+    if (int rc = finish_out(t->merged, out, cap, n_out)) return rc;   // (the ticket stays: wait again, larger cap)
+    t->ticket = 0;
+    t->merged.clear();
     return 0;
 }
 

@@ -28,6 +28,11 @@ def plan_cuts(weights, bucket: int, n_pos: int, n: int) -> np.ndarray:
     return cuts
 
 
+class TableRetry(RuntimeError):
+    """spg_multi_wait_candidates returned 1: a device's table did not fit its copy (the copies grow from the tables
+    seen) or carried an error word; the sample's table must be taken synchronously before its reset."""
+
+
 class MultiEngine:
     def __init__(self, devices, n_pos: int, min_base_quality: int = 30, min_total_depth: int = 10,
                  min_allele_depth: int = 5, min_evidence_ratio: float = 0.10, reference: str | None = None,
@@ -196,6 +201,31 @@ class MultiEngine:
                     return arr[:n.value]
                 if n.value <= cap:
                     self._check(rc, "spg_multi_get_candidates")
+                cap = int(n.value)
+
+    def candidates_async(self) -> int:
+        """Enqueue the merged call table without waiting (spg_multi_get_candidates_async): the ticket for
+        wait_candidates.  The next sample's reset / accumulate / finalize may go out before that wait."""
+        t = C.c_uint64()
+        with self._lock:
+            self._check(self._L.spg_multi_get_candidates_async(self._h, C.byref(t)), "spg_multi_get_candidates_async")
+        return t.value
+
+    def wait_candidates(self, ticket: int) -> np.ndarray:
+        """The table a ticket names (spg_multi_wait_candidates), merged in memory order.  Raises TableRetry when a
+        device's table outgrew its copy (take that sample's table with candidates() before its reset)."""
+        n = C.c_int64()
+        cap = 1024
+        with self._lock:
+            while True:
+                arr = np.zeros(cap, N.CANDIDATE_DTYPE)
+                rc = self._L.spg_multi_wait_candidates(self._h, int(ticket), N.ptr(arr), cap, C.byref(n))
+                if rc == 0:
+                    return arr[:n.value]
+                if rc == 1:
+                    raise TableRetry(self._L.spg_multi_last_error().decode())
+                if n.value <= cap:
+                    self._check(rc, "spg_multi_wait_candidates")
                 cap = int(n.value)
 
     def variants(self) -> List[dict]:

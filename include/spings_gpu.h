@@ -240,6 +240,14 @@ int spg_device_results(spg_ctx *ctx, void **candidates, void **n_candidates);
  * order a consumer on another stream (e.g. an RCCL gather) after it through spg_stream. */
 int spg_copy_candidates_device(spg_ctx *ctx, void *dst, int64_t cap);
 
+/* The call table and its status in one device-side copy into caller memory on the ctx device (no host wait; the
+ * multi-device gather's per-context step): dst[0..16) = {u32 candidates (true count), u32 status, u32 details,
+ * u32 records copied}, then min(candidates, *n_copy_cap) spg_candidate records, *n_copy_cap = min(cap, the context's
+ * candidate buffer).  status bits: 1 replay depth mismatch, 2 run error word, 4 fill error word, 8 more candidates
+ * than the copy holds, 16 more details than the context's buffer.  Any bit set: take this finalize's table through
+ * spg_count / spg_get_candidates (they report the error, or grow the buffers and finalize again). */
+int spg_copy_table_device(spg_ctx *ctx, void *dst, int64_t cap, int64_t *n_copy_cap);
+
 /* Bound the HBM held by the context's own copies of accumulated batches (the replay history; borrowed
  * batches are the caller's).  Past `bytes`, the oldest batches already folded into the records (or, calls-only,
  * into the counted totals) move to pinned host memory; the rare readers (exact replay, the exact fold of the
@@ -440,8 +448,21 @@ int spg_multi_accumulate_slices(spg_multi *m, int64_t pos_begin, int64_t n_cols,
                                 const spg_batch *slices, uint32_t flags);
 int spg_multi_wait_input(spg_multi *m);
 int spg_multi_finalize(spg_multi *m);
-/* The merged call table (needs n_out <= cap; *n_out is set either way). */
+/* The merged call table (needs n_out <= cap; *n_out is set either way).  One host wait per call: every device's table
+ * and status are copied on the device (spg_copy_table_device), gathered, and brought down in one copy; only a table that
+ * outgrew the copy (or an error word) takes the settling path per device. */
 int spg_multi_get_candidates(spg_multi *m, spg_candidate *out, int64_t cap, int64_t *n_out);
+/* The same table without waiting (replaces vc_queue.py:142-144's blocking prepare_variants per BAM when the caller
+ * pipelines samples): everything is enqueued — the device copies, the gather, one copy into pinned host memory — and
+ * *ticket names it.  The next sample's spg_multi_reset / accumulate / finalize may be enqueued before its wait.  Two
+ * tables may be in flight; a third enqueue retires the oldest (its wait then fails).  A ticket is waited for once
+ * (repeat the wait with a larger cap while it returns -1 with *n_out > cap). */
+int spg_multi_get_candidates_async(spg_multi *m, uint64_t *ticket);
+/* Wait for a ticket's table and merge it in memory order.  Returns 1 (nothing written, *n_out = 0) when a device's
+ * table did not fit the copy or carried an error word: that sample's table must be taken with spg_multi_get_candidates
+ * before its contexts move on (reset); the copies are sized from every table seen, so this happens at most while the
+ * first tables of a run grow. */
+int spg_multi_wait_candidates(spg_multi *m, uint64_t ticket, spg_candidate *out, int64_t cap, int64_t *n_out);
 /* cuts[0..n]: device i owns positions [cuts[i], cuts[i+1]) (after the sample's first batch). */
 int spg_multi_partition(spg_multi *m, int64_t *cuts);
 int spg_multi_set_rebalance(spg_multi *m, double ratio, int64_t max_batches);

@@ -243,3 +243,119 @@ def test_multi_device_slices_vs_single_context(devices):
             m.accumulate_slices(0, off, bad, borrow=True)
     m.close()
     s.close()
+
+
+@pytest.mark.parametrize("n", [1, 3])
+def test_multi_async_tables_pipelined(n):
+    """spg_multi_get_candidates_async / spg_multi_wait_candidates (verdict r05 item 3): sample k's table is enqueued
+    (device copies + gather + one pinned copy, no host wait) and waited for after sample k + 1 has been reset, accumulated
+    and finalized; every waited table equals a single context's for that sample.  A table larger than the first copies
+    (1,024 records per device) comes back as TableRetry and is then taken synchronously before the reset; the copies grow
+    and the next async tables of that size pass.  A third table in flight retires the oldest ticket."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.engine import PileupEngine
+    from covid_spings_variant_caller_amd.multi import MultiEngine, TableRetry
+    L = 12_000
+    ref = synth.reference(L, seed=71)
+    samples = [[synth.pileup(L, 60, seed=72 + 7 * k + i, ref=ref, snv_every=41 + 6 * k, lo=(i * 900) % 4000,
+                             hi=L - (i * 500) % 3000) for i in range(3)] for k in range(4)]
+    m = MultiEngine([0] * n, L, reference=ref)
+    m.set_rebalance(1e9, 0)
+    s = PileupEngine(L, 30, 10, 5, 0.10, device=0, reference=ref, calls_only=True)
+    expect = []
+    for bs in samples:
+        s.reset()
+        for b in bs:
+            s.accumulate(*b)
+        s.finalize()
+        expect.append(s.candidates())
+    assert all(len(e) > 20 for e in expect)
+    for rnd in range(2):
+        pend = []
+        for k, bs in enumerate(samples):
+            m.reset()
+            for b in bs:
+                m.accumulate(*b)
+            m.finalize()
+            pend.append((k, m.candidates_async()))
+            if len(pend) > 1:
+                j, t = pend.pop(0)
+                assert m.wait_candidates(t).tobytes() == expect[j].tobytes(), (rnd, j)
+        j, t = pend.pop(0)
+        assert m.wait_candidates(t).tobytes() == expect[j].tobytes()
+    # a table that outgrows the first copies: TableRetry, then the synchronous table (and larger copies from then on)
+    big = [synth.pileup(L, 60, seed=90 + i, ref=ref, snv_every=2, lo=0, hi=L) for i in range(2)]
+    s.reset()
+    for b in big:
+        s.accumulate(*b)
+    s.finalize()
+    exp_big = s.candidates()
+    assert len(exp_big) > 1024 * n
+    m2 = MultiEngine([0] * n, L, reference=ref)
+    m2.set_rebalance(1e9, 0)
+    for b in big:
+        m2.accumulate(*b)
+    m2.finalize()
+    t = m2.candidates_async()
+    with pytest.raises(TableRetry):
+        m2.wait_candidates(t)
+    assert m2.candidates().tobytes() == exp_big.tobytes()
+    m2.reset()
+    for b in big:
+        m2.accumulate(*b)
+    m2.finalize()
+    assert m2.wait_candidates(m2.candidates_async()).tobytes() == exp_big.tobytes()
+    # three tables in flight: the oldest ticket is retired
+    t1, t2, t3 = m2.candidates_async(), m2.candidates_async(), m2.candidates_async()
+    with pytest.raises(Exception):
+        m2.wait_candidates(t1)
+    assert m2.wait_candidates(t2).tobytes() == exp_big.tobytes()
+    assert m2.wait_candidates(t3).tobytes() == exp_big.tobytes()
+    m.close()
+    m2.close()
+    s.close()
+
+
+@pytest.mark.parametrize("n", [1, 3])
+def test_multi_async_enqueue_does_not_wait_for_device(n):
+    """The host part of a multi-device step does not grow with a device round trip per context: with every context's
+    stream held busy (a spin kernel of ~0.2 s on it), candidates_async() returns at once and the wait delivers the table
+    once the streams drain."""
+    import ctypes as C
+    import time
+    import torch
+    from covid_spings_variant_caller_amd import _native as N
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.multi import MultiEngine
+    L = 12_000
+    ref = synth.reference(L, seed=81)
+    bs = [synth.pileup(L, 60, seed=82 + i, ref=ref, snv_every=47, lo=0, hi=L) for i in range(2)]
+    m = MultiEngine([0] * n, L, reference=ref)
+    for b in bs:
+        m.accumulate(*b)
+    m.finalize()
+    want = m.candidates()
+    dev = torch.device("cuda", 0)
+    # the spin kernel's rate on this device: cycles for ~0.2 s
+    t0 = time.perf_counter()
+    torch.cuda._sleep(10_000_000)
+    torch.cuda.synchronize(dev)
+    cycles = int(10_000_000 * 0.2 / max(time.perf_counter() - t0, 1e-4))
+    t0 = time.perf_counter()
+    torch.cuda._sleep(cycles)
+    torch.cuda.synchronize(dev)
+    spin = time.perf_counter() - t0
+    assert spin > 0.05
+    for ctx in m._contexts():
+        h = C.c_void_p()
+        N.check(m._L.spg_stream(ctx, C.byref(h)), "spg_stream")
+        with torch.cuda.stream(torch.cuda.ExternalStream(h.value, device=dev)):
+            torch.cuda._sleep(cycles)
+    t0 = time.perf_counter()
+    t = m.candidates_async()
+    dt = time.perf_counter() - t0
+    got = m.wait_candidates(t)
+    total = time.perf_counter() - t0
+    assert got.tobytes() == want.tobytes()
+    assert dt < 0.25 * spin and total > 0.5 * spin, (dt, total, spin)
+    m.close()
