@@ -1109,6 +1109,8 @@ def end_to_end(args, device):
     res["reads"] = n_reads
     res["simulate_s"] = t_sim
     res["host_threads"] = args.e2e_threads
+    from covid_spings_variant_caller_amd import _native as N
+    res["host_inflater"] = N.pileup_lib().spp_host_inflater().decode()     # (records plans / host fills)
     os.remove(bam)
     if args.e2e_many > 0:
         # BASELINE config 4 from files: many 100x BAMs through LiveVariantCaller.process_bams (plans on a thread
@@ -1190,6 +1192,8 @@ def _e2e(e):
             o["host_cap_pairing_ms"] = _r(b.get("host_depth_cap_and_pairing_ms"), 3)
             o["inflate_ms"] = _r(b.get("inflate_kernels_ms"), 3)
         out[tag] = o
+    if "host_inflater" in e:
+        out["host_inflater"] = e["host_inflater"]
     c4 = e.get("config4_process_bams")
     if isinstance(c4, dict):
         out["config4_process_bams_pos_s"] = _r(c4.get("positions_per_s"))

@@ -245,6 +245,7 @@ def pileup_lib():
     L = C.CDLL(PILEUP_LIB)
     vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int32
     _sig(L.spp_last_error, C.c_char_p)
+    _sig(L.spp_host_inflater, C.c_char_p)
     _sig(L.spp_default_params, None, C.POINTER(SppParams))
     _sig(L.spp_open, C.c_int, C.c_char_p, C.POINTER(vp))
     _sig(L.spp_close, C.c_int, vp)

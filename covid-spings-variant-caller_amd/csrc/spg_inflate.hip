@@ -359,7 +359,7 @@ __host__ __device__ __forceinline__ uint32_t inflate_member(const uint8_t *comp,
 // 6 distance too far back; 7 output overrun; 8 input overrun; 9 wrong size; 10 CRC32 mismatch (k_crc32).
 // mpw members per block, one per lane (lanes >= mpw idle), each with its SLICE of the block's LDS.  Latency-bound
 // (a member's symbols are a dependent chain; r04ze: 19.3 ms on the 10,000x BAM at 3 members per block).  Since r05 the
-// fallback of k_inflate_par (only_fallback: the members it left) and the whole inflater of SPG_INFLATE_LANE A/B builds.
+// fallback of k_inflate_par (only_fallback: the members it left).
 constexpr int INFLATE_MPW = 3;
 constexpr uint32_t ST_FALLBACK = 100;   // (k_inflate_par) this member is left to the lane kernel
 __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
@@ -698,15 +698,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
-#if defined(SPG_INFLATE_PROF)          // (A/B builds: k_inflate_par's phase cycles summed over members, spg_bgzf_prof)
-__device__ unsigned long long g_inf_prof[8];
-#define PAR_PROF_T(v) const uint64_t v = clock64()
-#define PAR_PROF_ADD(i, x) do { if (lane == 0) atomicAdd(&g_inf_prof[i], (unsigned long long)(x)); } while (0)
-#else
-#define PAR_PROF_T(v)
-#define PAR_PROF_ADD(i, x)
-#endif
-
 __device__ __forceinline__ uint32_t ring_slot(uint32_t g0, uint32_t x) { return (g0 + x) & (PAR_RING - 1); }
 
 __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
@@ -755,9 +746,7 @@ __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ 
         }
     };
 
-    PAR_PROF_T(t_beg);
     do {
-        PAR_PROF_T(t_h0);
         ib_seek(B, base, p);
         bfinal = (int)B.get(1);
         const uint32_t type = B.get(2);
@@ -778,15 +767,11 @@ __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ 
         SegOut so{};
         SyncOut sy{};
         sy.eob = -1;
-        PAR_PROF_T(t_a0);
-        PAR_PROF_ADD(0, t_a0 - t_h0);
         if ((uint32_t)lane < K) {
             so = decode_seg(B, base, s, stop, T, tokl, posl, cap);
             sy = sync_lane0(so);
         }
         __builtin_amdgcn_wave_barrier();
-        PAR_PROF_T(t_s0);
-        PAR_PROF_ADD(1, t_s0 - t_a0);
         // sync rounds: a lane whose predecessor's true tokens end elsewhere than where it last synchronised from runs again
         // (the first round: every lane but 0; later rounds only behind a lane that never met its own phase-A tokens)
         uint32_t used = s;
@@ -798,12 +783,8 @@ __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ 
                 used = eprev;
                 sy = resync(B, base, s, used, stop, so, tokl, posl, T, redo0 + (uint32_t)lane * PAR_RCAP);
             }
-            PAR_PROF_ADD(7, 1);
         }
         __builtin_amdgcn_wave_barrier();
-        PAR_PROF_T(t_b0);
-        PAR_PROF_ADD(2, t_b0 - t_s0);
-        PAR_PROF_ADD(5, 1);
         const bool bad = (uint32_t)lane < K && (so.ovf || sy.fail);
         const uint64_t badm = __ballot(bad), eobm = __ballot((uint32_t)lane < K && sy.eob >= 0);
         // a lane past the first lane with an end of block decoded another block: only lanes up to it count
@@ -885,7 +866,6 @@ __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ 
                     }
                 }
                 if (st) break;
-                PAR_PROF_ADD(6, 1);
                 w += total;
                 t0 = t1;
                 const uint64_t gb = (gbeg + w) & ~1023ull;    // whole global blocks only; the rest stays in the ring
@@ -894,13 +874,9 @@ __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ 
         }
         if (st) break;
         p = pnext;
-        PAR_PROF_T(t_b1);
-        PAR_PROF_ADD(3, t_b1 - t_b0);
     } while (!bfinal);
     if (!st && w != ulen) st = ST_FALLBACK;
     if (!st) flush(ulen);
-    PAR_PROF_T(t_end);
-    PAR_PROF_ADD(4, t_end - t_beg);
     if (lane == 0) {
         status[m] = st;
         if (st) atomicAdd(n_fallback, 1u);
@@ -1035,19 +1011,10 @@ hipError_t launch_inflate(const uint8_t *comp, uint64_t comp_bytes, const spg_bg
     uint16_t *const pos = reinterpret_cast<uint16_t *>(tok + 2 * (size_t)comp_bytes + 2048 * (size_t)n + 64);
     hipError_t e = hipMemsetAsync(cnt, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-#if defined(SPG_INFLATE_LANE)        // (A/B builds: every member on the lane kernel)
-    (void)comp_bytes;
-    (void)redo;
-    (void)tok;
-    (void)pos;
-    hipLaunchKernelGGL(k_inflate, dim3((unsigned)((n + INFLATE_MPW - 1) / INFLATE_MPW)), dim3(64),
-                       (size_t)INFLATE_MPW * SLICE, st, comp, mem, n, out, status, INFLATE_MPW, 0);
-#else
     (void)comp_bytes;
     hipLaunchKernelGGL(k_inflate_par, dim3((unsigned)n), dim3(64), 0, st, comp, mem, n, out, status, tok, pos, redo, cnt);
     hipLaunchKernelGGL(k_inflate, dim3((unsigned)((n + INFLATE_MPW - 1) / INFLATE_MPW)), dim3(64),
                        (size_t)INFLATE_MPW * SLICE, st, comp, mem, n, out, status, INFLATE_MPW, 1);
-#endif
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     static const uint32_t op1k = host_crc_x8n(1024);
@@ -1118,16 +1085,6 @@ int spg_bgzf_inflate_par_check(const uint8_t *comp, size_t comp_bytes, const spg
                                          reinterpret_cast<uint8_t *>(slice.data()), stats, tok, pos, redo);
     return 0;
 }
-
-#if defined(SPG_INFLATE_PROF)
-// (A/B builds) k_inflate_par's summed phase cycles since the last call: header + tables, phase A, sync, phase B, total,
-// blocks, batches, sync rounds
-extern "C" int spg_bgzf_prof(uint64_t *out8) {
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(spg::g_inf_prof), 8 * sizeof(uint64_t)) != hipSuccess) return -1;
-    static const uint64_t zero[8] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(spg::g_inf_prof), zero, sizeof zero) == hipSuccess ? 0 : -1;
-}
-#endif
 
 int spg_bgzf_fallbacks(int device, int64_t *n) {
     if (!n || device < 0 || device >= MAX_INF_DEV) return ifail("spg_bgzf_fallbacks: bad argument");

@@ -136,15 +136,6 @@ __device__ __forceinline__ void replay_walk(const FParams &F, const Hist *__rest
                 c = e < hi ? h.code[e] : 0xFFu;
                 q = e < hi ? h.qual[e] : 0u;
             };
-#ifdef SPG_REPLAY_NOPF                                         // A/B builds: one step at a time
-            for (uint64_t e0 = lo; e0 < hi; e0 += 64) {
-                uint32_t c, q;
-                ld(e0, c, q);
-                fn(c, q, e0 + (uint64_t)lane < hi, ord + (e0 - lo));
-            }
-            ord += hi - lo;
-            continue;
-#endif
             uint32_t cA, qA, cB, qB, cC, qC;
             ld(lo, cA, qA);
             ld(lo + 64, cB, qB);
@@ -535,9 +526,6 @@ __device__ __forceinline__ bool finalize_position(const FParams &F, const Acc *r
 // process_pileup_column / process_svn's dict bookkeeping (:77-101) thus runs lane-parallel.
 #ifndef SPG_NT_MIB
 #define SPG_NT_MIB 192       // batches whose entries exceed this stream with non-temporal loads
-#endif
-#ifndef SPG_FUSE_SL2
-#define SPG_FUSE_SL2 0       // 1: the fused kernel's second allele keeps Σ ln(1-eps) too (A/B builds)
 #endif
 #ifndef SPG_SEG_WPE
 #define SPG_SEG_WPE 4
@@ -1125,7 +1113,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8))) v
             // FUSE (calls-only): the second allele skips Σ ln(1-eps) but keeps Σ eps (QUAL).  Its H is
             // needed only when its own GL is not exactly 0 — in a deep column the other allele's P
             // underflows to 0 — and then finalize replays the position exactly.
-            if constexpr (FUSE && !SPG_FUSE_SL2) {
+            if constexpr (FUSE) {
                 if (sem || !P.calls_only) body(T_{}, T_{}, F_{});
                 else { body(T_{}, F_{}, F_{}); skipped = true; }
                 skipped2 = true;

@@ -2062,6 +2062,8 @@ extern "C" {
 
 const char *spp_last_error(void) { return g_err.c_str(); }
 
+const char *spp_host_inflater(void) { return Inflater::api().dec ? "libdeflate" : "zlib"; }
+
 void spp_default_params(spp_params *p) {
     memset(p, 0, sizeof(*p));
     p->stepper = SPP_STEPPER_ALL;

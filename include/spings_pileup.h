@@ -52,6 +52,9 @@ typedef struct spp_file spp_file;
 typedef struct spp_batch spp_batch;
 
 const char *spp_last_error(void);
+/* The host BGZF inflater this process uses for records plans and host fills: "libdeflate" (its runtime library is
+ * loaded with dlopen when present) or "zlib" (absent, or SPP_NO_LIBDEFLATE set before the first inflate). */
+const char *spp_host_inflater(void);
 void spp_default_params(spp_params *p);
 
 /* Open a BAM (BGZF) or SAM file and parse its header. */

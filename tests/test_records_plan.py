@@ -234,3 +234,28 @@ def test_parallel_record_scan_equals_serial(tmp_path, max_depth):
         out[par] = r.stdout.strip().splitlines()[-1]
     assert out["1"] == out["0"] == out["1:3"]
     assert int(out["1"].split()[3]) > 300_000
+
+
+def test_host_inflater_reported():
+    """spp_host_inflater names the host BGZF inflater this process uses (bench.py records it)."""
+    import os
+    from covid_spings_variant_caller_amd import _native as N
+    name = N.pileup_lib().spp_host_inflater().decode()
+    assert name in ("libdeflate", "zlib")
+    if os.environ.get("SPP_NO_LIBDEFLATE"):
+        assert name == "zlib"
+
+
+def test_records_plans_on_zlib(tmp_path):
+    """The zlib host inflater (SPP_NO_LIBDEFLATE=1; libdeflate is present in this image, so it is otherwise never run):
+    this file's plan tests once more in a process where the pileup library binds zlib."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, SPP_NO_LIBDEFLATE="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "not gpu",
+                        os.path.join(here, "test_records_plan.py"), "-k", "not test_records_plans_on_zlib"],
+                       env=env, cwd=os.path.dirname(here), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout

@@ -57,11 +57,6 @@ for r in range(4):
     L.spg_bgzf_fallbacks(0, C.byref(fb))
     res["runs"].append({"kernel_ms": ms.value, "call_ms": dt * 1e3, "bad_members": int((st != 0).sum()),
                         "lane_kernel_members": fb.value})
-    if hasattr(L, "spg_bgzf_prof"):            # (SPG_INFLATE_PROF A/B build: k_inflate_par's phase cycles per member)
-        pr = (C.c_uint64 * 8)()
-        L.spg_bgzf_prof(pr)
-        names = ["header_tables", "phase_a", "sync", "phase_b", "total", "blocks", "batches", "sync_rounds"]
-        res["runs"][-1]["prof_per_member"] = {k: pr[i] / n for i, k in enumerate(names)}
 t = time.perf_counter()
 ref_bytes = gzip.decompress(raw)
 res["gzip_1core_ms"] = (time.perf_counter() - t) * 1e3
