@@ -254,8 +254,7 @@ def measure(D, step, eng, K_min, reps, min_ms, every):
             step(k)
         enq.append(time.perf_counter() - t0)       # host time to enqueue the K steps
         flush()                                    # the last steps' gathers complete inside the window
-        eng.sync()
-        torch.cuda.synchronize()
+        torch.cuda.synchronize()                   # (every stream of the device, the engine's included)
         D.barrier()
         times.append(D.max(time.perf_counter() - t0))
         a, _ = eng.kernel_times(4096)
@@ -406,11 +405,14 @@ def run_point(args, D, L, depth, max_depth, local, world, rank, contig, samples=
             pending[j] = D.dist.gather(sends[j], recvs[j], dst=0, async_op=True)   # RCCL over xGMI
 
     def flush():
+        waited = False
         for j in range(2):
             if pending[j] is not None:
                 pending[j].wait()
                 pending[j] = None
-        torch.cuda.synchronize(dev)
+                waited = True
+        if waited:
+            torch.cuda.synchronize(dev)
 
     step.flush = flush
 
@@ -539,12 +541,13 @@ def run_multi_device(args, world, L, depth, max_depth):
 
     pend = []
     got = []
+    desc = mm.prepare_slices(0, full_off, slices)
 
     def step():
         # step k's table is enqueued (spg_multi_get_candidates_async: device copies, the gather, one copy into pinned
         # host memory) and step k - 1's is waited for and merged: step k's launches are out before then
         mm.reset()
-        mm.accumulate_slices(0, full_off, slices, borrow=True)
+        mm.accumulate_slices(0, full_off, desc, borrow=True)
         mm.finalize()
         pend.append(mm.candidates_async())
         if len(pend) > 1:
@@ -1005,9 +1008,43 @@ def end_to_end(args, device):
         t1 = time.perf_counter()
         return caller, calls, t0, t_in, t1
 
+    def device_breakdown_gpu_plan(caller, reps=3):
+        """One BAM through the product's device path (r06): the depth cap and mate pairing on the GPU
+        (spg_bam_plan_build) — nothing comes down; each stage synchronised."""
+        eng, prm = caller.engine, caller.pileup_params
+        rows = []
+        for _ in range(reps):
+            eng.reset()
+            eng.sync()
+            t = [time.perf_counter()]
+            with AlignmentFile(bam) as f:
+                tid = f.tid("NC_045512.2")
+                m = f.bam_map(prm.n_threads)
+                t.append(time.perf_counter())
+                n = eng.bam_open(m, tid, prm)
+                m.close()
+                t.append(time.perf_counter())
+                plan = eng.bam_plan_build(prm.max_depth, prm.ignore_overlaps)
+                assert plan is not None, eng.bam_fallback
+                t.append(time.perf_counter())
+            assert eng.bam_accumulate_planned(plan)
+            eng.wait_input()
+            eng.sync()
+            t.append(time.perf_counter())
+            eng.finalize()
+            eng.sync()
+            t.append(time.perf_counter())
+            rows.append(np.diff(t) * 1e3)
+        r = np.median(np.array(rows), axis=0)
+        return {"map_and_pinned_copy_ms": r[0], "bam_open_ms (H2D + inflate + CRC + record scan + fields)": r[1],
+                "inflate_kernels_ms": eng.bam_inflate_ms(), "gpu_depth_cap_and_pairing_ms": r[2],
+                "tweak_fill_ms": r[3], "finalize_ms": r[4], "reads": int(n), "pairs": int(plan.n_pairs),
+                "sum_ms": float(r.sum())}
+
     def device_breakdown(caller, reps=3):
-        """One BAM through the device path's stages, each synchronised (their sum exceeds the pipelined per-BAM time:
-        process_bam returns once the fill is enqueued)."""
+        """One BAM through the device path's stages with the host plan (r05's product path: fields down, the depth
+        cap / pairing replayed on the host, the plan up), each synchronised (their sum exceeds the pipelined per-BAM
+        time: process_bam returns once the fill is enqueued)."""
         eng, prm = caller.engine, caller.pileup_params
         rows = []
         for _ in range(reps):
@@ -1063,7 +1100,8 @@ def end_to_end(args, device):
         # the product path: the BAM kept in HBM (spg_bam_*)
         caller, calls, t0, t_in, t1 = stream(cap, "device")
         assert [v["start"] for v in calls] == [v["start"] for v in calls_h], "device / host pileup calls differ"
-        brk = device_breakdown(caller)
+        brk = device_breakdown_gpu_plan(caller)
+        brk_host = device_breakdown(caller)
         # the same BAMs through process_bams (the drop-in's many-BAM call: the BAM-in-HBM path pipelined over two device
         # BAM slots, the next BAM opening on the GPU while the host plans this one); a warm-up call first (device buffers)
         caller.process_bams([bam] * 2)
@@ -1097,10 +1135,11 @@ def end_to_end(args, device):
                     "s_per_bam": (t1 - t0) / n_bams, "ingest_s": t_in, "finalize_s": t1 - t0 - t_in,
                     "calls": len(calls), "reads_per_bam": int(brk["reads"]),
                     "path": "BAM kept in HBM (process_bam, pileup='device'): compressed file H2D -> k_inflate_par + k_crc32 "
-                            "-> record scan + stepper filter + fields on the GPU -> fields D2H -> host depth cap / mate "
-                            "pairing (spp_pileup_plan_fields) -> plan H2D -> mate-overlap tweak + k_pileup_fill -> "
-                            "accumulate",
-                    "breakdown_one_bam_device": brk,
+                            "-> record scan + stepper filter + fields on the GPU -> depth cap / mate pairing on the GPU "
+                            "(spg_bam_plan_build: k_plan_sweep + name-group replay) -> mate-overlap tweak + k_pileup_fill "
+                            "-> accumulate",
+                    "breakdown_one_bam_device": brk, "breakdown_one_bam_host_plan": brk_host,
+                    "plan_path": caller.last_plan_path,
                     "records_plan_path": rec_leg, "host_fill_path": host_leg, "process_bams": many_leg,
                     "vcqueue_loop": vq_leg, "vcqueue_loop_write_behind": vq_leg_wb}
         caller.engine.close()
@@ -1189,8 +1228,11 @@ def _e2e(e):
             o["vcqueue_ms_per_bam"] = _r(s["vcqueue_loop"].get("ms_per_bam"))
         b = s.get("breakdown_one_bam_device")
         if isinstance(b, dict):
-            o["host_cap_pairing_ms"] = _r(b.get("host_depth_cap_and_pairing_ms"), 3)
+            o["gpu_cap_pairing_ms"] = _r(b.get("gpu_depth_cap_and_pairing_ms"), 3)
             o["inflate_ms"] = _r(b.get("inflate_kernels_ms"), 3)
+        b = s.get("breakdown_one_bam_host_plan")
+        if isinstance(b, dict):
+            o["host_cap_pairing_ms"] = _r(b.get("host_depth_cap_and_pairing_ms"), 3)
         out[tag] = o
     if "host_inflater" in e:
         out["host_inflater"] = e["host_inflater"]

@@ -164,6 +164,8 @@ def gpu_lib():
     _sig(L.spg_bam_open, i32, vp, vp, u64, vp, i64, u64, i32, i32, C.POINTER(SpgBamFilter), C.POINTER(i64))
     _sig(L.spg_bam_reads_copy, i32, vp, C.POINTER(SpgBamReads))
     _sig(L.spg_bam_accumulate, i32, vp, C.POINTER(SpgBamPlan), C.c_uint32)
+    _sig(L.spg_bam_plan_build, i32, vp, i64, i32, C.POINTER(SpgBamPlan))
+    _sig(L.spg_bam_plan_download, i32, vp, C.POINTER(SpgBamPlan), vp, vp, vp, vp, vp, vp)
     _sig(L.spg_bam_inflate_ms, i32, vp, C.POINTER(C.c_float))
     _sig(L.spg_bam_inflate_fallbacks, i32, vp, C.POINTER(i64))
     _sig(L.spg_bam_slot, i32, vp, i32)

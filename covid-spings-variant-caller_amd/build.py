@@ -21,7 +21,7 @@ LIBDIR = os.path.join(PKG, "_lib")
 INC = os.path.join(ROOT, "include")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-GPU_SOURCES = ["spg_kernels.hip", "spg_tile.hip", "spg_lite.hip", "spg_fill.hip", "spg_inflate.hip", "spg_ckpt.hip", "spg_bam.hip", "spg_api.cpp", "spg_multi.cpp"]
+GPU_SOURCES = ["spg_kernels.hip", "spg_tile.hip", "spg_lite.hip", "spg_fill.hip", "spg_inflate.hip", "spg_ckpt.hip", "spg_bam.hip", "spg_plan.hip", "spg_api.cpp", "spg_multi.cpp"]
 GPU_HEADERS = ["spg_device.h", "spg_common.h"]
 PILEUP_SOURCES = ["spp_pileup.cpp"]
 

@@ -49,6 +49,11 @@ hipError_t launch_ck_pack(uint8_t *oc, const uint8_t *oq, uint64_t m, uint64_t b
                           uint32_t *xn, uint32_t xcap, hipStream_t st);
 hipError_t launch_table_copy(const Counters *ctr, const uint32_t *kerr, const uint32_t *ferr, const void *cand, int64_t cap,
                              int64_t detail_cap, void *dst, hipStream_t st);
+size_t plan_temp_bytes(uint32_t n, int64_t span_n);
+hipError_t launch_plan_reads(const PlanArgs &A, void *tmp, size_t tmp_bytes, hipStream_t st);
+hipError_t launch_plan_cov(const PlanArgs &A, int all, int32_t *cov, void *tmp, size_t tmp_bytes, hipStream_t st);
+hipError_t launch_plan_keep(const PlanArgs &A, bool sweep, hipStream_t st);
+hipError_t launch_plan_rest(const PlanArgs &A, int32_t *cov, bool pairing, void *tmp, size_t tmp_bytes, hipStream_t st);
 size_t inflate_scratch_bytes(uint64_t comp_bytes, int64_t n);
 hipError_t launch_inflate(const uint8_t *comp, uint64_t comp_bytes, const spg_bgzf_member *mem, int64_t n, uint8_t *out,
                           uint32_t *status, void *scratch, hipStream_t st);
@@ -165,6 +170,8 @@ struct DBuf {
 struct BamDev {
     DBuf comp, out, mem, status, uoff, start, cnt, base, lohi, rec, fields, err;
     DBuf kept, pairs, orig, twof, recs_k, tile_first, iscr, rtmp;
+    DBuf plan_rd, plan_sp, plan_tmp;   // spg_bam_plan_build: per-read arrays, per-column arrays, hipcub scratch
+    int32_t tid = 0;                   // the contig spg_bam_open kept
     bool open = false;                 // a BAM is loaded (spg_bam_open succeeded)
     uint64_t total = 0;                // inflated bytes
     int64_t n_members = 0;
@@ -185,7 +192,7 @@ struct BamDev {
     void release() {
         up_pending = false;
         for (DBuf *b : {&comp, &out, &mem, &status, &uoff, &start, &cnt, &base, &lohi, &rec, &fields, &err, &kept, &pairs,
-                        &orig, &twof, &recs_k, &tile_first, &iscr, &rtmp})
+                        &orig, &twof, &recs_k, &tile_first, &iscr, &rtmp, &plan_rd, &plan_sp, &plan_tmp})
             b->release();
         open = false;
     }
@@ -985,6 +992,11 @@ static bool is_pinned(const void *p) {
     if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
     return a.type == hipMemoryTypeHost;
 }
+static bool is_device_mem(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) { (void)hipGetLastError(); return false; }
+    return a.type == hipMemoryTypeDevice;
+}
 
 // One batch: validation, its history copy (arena) or borrowed device buffers, descriptors, bucket
 // index; a deep batch is accumulated right away, a shallow one joins the pending run.
@@ -1184,7 +1196,8 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
         hb.off = reinterpret_cast<uint64_t *>(m + 2 * pad);
         const hipMemcpyKind k = dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
         hipStream_t cs = c->copy_stream;
-        HIPCHK(hipMemcpyAsync(hb.off, offsets, sizeof(uint64_t) * (n_cols + 1), k, cs));
+        // (a device plan's offsets are in HBM: spg_bam_plan_build)
+        HIPCHK(hipMemcpyAsync(hb.off, offsets, sizeof(uint64_t) * (n_cols + 1), dfill ? hipMemcpyDefault : k, cs));
         if (recs) {
             if (int rc = upload_records(c, recs, hb, cs)) return rc;
         } else if (dfill) {                    // spg_bam_accumulate: the records are in HBM already
@@ -1217,7 +1230,7 @@ static int add_batch(spg_ctx *c, int64_t pos_begin, int64_t n_cols, const uint64
             if (!(is_pinned(offsets) && (!recs->data_bytes || is_pinned(recs->data)) && (!recs->n_reads || is_pinned(recs->rec))))
                 *pageable_copy = true;
         } else if (dfill) {
-            if (!is_pinned(offsets)) *pageable_copy = true;
+            if (!is_pinned(offsets) && !is_device_mem(offsets)) *pageable_copy = true;
         } else if (!dev && !(is_pinned(offsets) && (!n_entries || (is_pinned(base_code) && is_pinned(qual))))) {
             *pageable_copy = true;
         }
@@ -2394,6 +2407,7 @@ int spg_bam_open(spg_ctx *c, const uint8_t *comp, uint64_t comp_bytes, const spg
     B.total = total;
     B.n_members = n;
     B.n_reads = (uint32_t)nr;
+    B.tid = tid;
     B.open = true;
     *n_reads = (int64_t)nr;
     return 0;
@@ -2417,8 +2431,121 @@ int spg_bam_reads_copy(spg_ctx *c, const spg_bam_reads *o) {
     return 0;
 }
 
+// The open BAM's pileup plan built in HBM (spg_plan.hip): htslib's depth cap and mate pairing over the reads'
+// fixed fields, the kept list, the CSR offsets and the pairs — what spp_pileup_plan_fields computes on the host from
+// spg_bam_reads_copy's fields, without the fields coming down.  Returns 1 (nothing built) when the device declines.
+int spg_bam_plan_build(spg_ctx *c, int64_t max_depth, int32_t ignore_overlaps, spg_bam_plan *out) {
+    if (!c || !out) return fail("spg_bam_plan_build: null argument");
+    if (max_depth < 0) return fail("spg_bam_plan_build: max_depth < 0");
+    BamDev &B = c->bam_cur();
+    if (!B.open) return fail("spg_bam_plan_build: no BAM open (spg_bam_open)");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t cs = c->copy_stream;
+    *out = spg_bam_plan{};
+    const uint32_t n = B.n_reads;
+    if (n == 0) return 0;
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    // per-read arrays (one buffer): first, didx, dfirst (n + 1), dpos, kept, sval, pairb, pb_list, pa, pbv (n), keep (u8),
+    // skey, pcol, porig, lsa (8-byte), the head
+    const size_t u4 = al(4 * ((size_t)n + 1)), u8 = al(8 * (size_t)n), b1 = al(n);
+    const size_t rd = 10 * u4 + b1 + 4 * u8 + al(sizeof(PlanHead));
+    HIPCHK(B.plan_rd.need(rd));
+    uint8_t *m = B.plan_rd.as<uint8_t>();
+    PlanArgs A{};
+    A.n = n;
+    A.pos = B.pos; A.end = B.end; A.mtid = B.mtid; A.mpos = B.mpos; A.isize = B.isize;
+    A.flag = B.flag; A.l_seq = B.l_seq; A.nhash = B.nhash;
+    A.tid = B.tid;
+    A.olap = ignore_overlaps ? 1 : 0;
+    A.maxcnt = max_depth > 0 ? max_depth : INT64_MAX;
+    uint32_t *w4[10];
+    for (int i = 0; i < 10; i++) w4[i] = reinterpret_cast<uint32_t *>(m + (size_t)i * u4);
+    A.first = w4[0]; A.didx = w4[1]; A.dfirst = w4[2]; A.dpos = reinterpret_cast<int32_t *>(w4[3]); A.kept = w4[4];
+    A.sval = w4[5]; A.pairb = w4[6]; A.pb_list = w4[7]; A.pa = w4[8]; A.pbv = w4[9];
+    uint8_t *q = m + 10 * u4;
+    A.keep = q;
+    q += b1;
+    A.skey = reinterpret_cast<uint64_t *>(q);
+    A.pcol = reinterpret_cast<int64_t *>(q + u8);
+    A.porig = reinterpret_cast<uint64_t *>(q + 2 * u8);
+    A.lsa = reinterpret_cast<uint64_t *>(q + 3 * u8);
+    A.head = reinterpret_cast<PlanHead *>(q + 4 * u8);
+    size_t tb = plan_temp_bytes(n, 0);
+    HIPCHK(B.plan_tmp.need(tb));
+    HIPCHK(launch_plan_reads(A, B.plan_tmp.p, tb, cs));
+    PlanHead h{};
+    HIPCHK(hipMemcpyAsync(&h, A.head, sizeof h, hipMemcpyDeviceToHost, cs));
+    HIPCHK(hipStreamSynchronize(cs));
+    if (h.err & 1u) return bam_fallback("spg_bam_plan_build: a read without reference span, or reads out of order");
+    const bool capped = max_depth > 0;
+    if (capped && (int64_t)h.max_span + 128 > 8192)
+        return bam_fallback("spg_bam_plan_build: a read spans more than the depth-cap sweep's ring");
+    // per-column arrays over [min_pos, max_end]: the coverage difference array, the coverage, the offsets
+    A.span_lo = h.min_pos;
+    A.span_n = h.max_end - h.min_pos;
+    if (A.span_n < 1 || A.span_n > ((int64_t)1 << 31) - 256) return bam_fallback("spg_bam_plan_build: column span out of range");
+    const size_t sn = (size_t)A.span_n + 1;
+    HIPCHK(B.plan_sp.need(2 * al(4 * sn) + al(8 * sn)));
+    uint8_t *sp = B.plan_sp.as<uint8_t>();
+    A.diff = reinterpret_cast<int32_t *>(sp);
+    int32_t *cov = reinterpret_cast<int32_t *>(sp + al(4 * sn));
+    A.offsets = reinterpret_cast<uint64_t *>(sp + 2 * al(4 * sn));
+    tb = plan_temp_bytes(n, A.span_n);
+    HIPCHK(B.plan_tmp.need(tb));
+    bool sweep = capped;
+    if (capped && h.n_distinct > (1u << 22)) {
+        // a long contig: the sweep only when the cap can bite somewhere (U_p <= cov(p) + cov(p - 1) <= 2 max cov)
+        HIPCHK(launch_plan_cov(A, 1, cov, B.plan_tmp.p, tb, cs));
+        HIPCHK(hipMemcpyAsync(&h, A.head, sizeof h, hipMemcpyDeviceToHost, cs));
+        HIPCHK(hipStreamSynchronize(cs));
+        if (2 * (int64_t)h.max_cov > max_depth)
+            return bam_fallback("spg_bam_plan_build: the depth cap bites on a contig with > 4 M start positions");
+        sweep = false;
+    }
+    HIPCHK(launch_plan_keep(A, sweep, cs));
+    HIPCHK(launch_plan_rest(A, cov, A.olap && h.n_cand > 0, B.plan_tmp.p, tb, cs));
+    HIPCHK(hipMemcpyAsync(&h, A.head, sizeof h, hipMemcpyDeviceToHost, cs));
+    HIPCHK(hipStreamSynchronize(cs));
+    if (h.err & 2u) return bam_fallback("spg_bam_plan_build: more than 16 reads share a name hash");
+    if (h.n_kept && h.lo != A.span_lo) return fail("spg_bam_plan_build: internal error (first read not kept)");
+    out->pos_begin = h.lo;
+    out->n_cols = h.hi - h.lo;
+    out->n_entries = h.n_entries;
+    out->offsets = A.offsets;
+    out->n_kept = h.n_kept;
+    out->kept = A.kept;
+    out->n_pairs = h.n_pairs;
+    out->pair_a = A.pa;
+    out->pair_b = A.pbv;
+    out->pair_col = A.pcol;
+    out->pair_orig = A.porig;
+    out->orig_bytes = h.orig_bytes;
+    out->max_span = h.max_span_kept;
+    return 0;
+}
+
+// spg_bam_plan_build's arrays copied to host memory (tests: the device plan against spp_pileup_plan_fields')
+int spg_bam_plan_download(spg_ctx *c, const spg_bam_plan *P, uint64_t *offsets, uint32_t *kept, uint32_t *pair_a,
+                          uint32_t *pair_b, int64_t *pair_col, uint64_t *pair_orig) {
+    if (!c || !P) return fail("spg_bam_plan_download: null argument");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t cs = c->copy_stream;
+    const size_t nc = (size_t)std::max<int64_t>(0, P->n_cols), nk = (size_t)P->n_kept, np = (size_t)P->n_pairs;
+    if (offsets && P->offsets && nc) HIPCHK(hipMemcpyAsync(offsets, P->offsets, 8 * (nc + 1), hipMemcpyDeviceToHost, cs));
+    if (kept && nk) HIPCHK(hipMemcpyAsync(kept, P->kept, 4 * nk, hipMemcpyDeviceToHost, cs));
+    if (np) {
+        if (pair_a) HIPCHK(hipMemcpyAsync(pair_a, P->pair_a, 4 * np, hipMemcpyDeviceToHost, cs));
+        if (pair_b) HIPCHK(hipMemcpyAsync(pair_b, P->pair_b, 4 * np, hipMemcpyDeviceToHost, cs));
+        if (pair_col) HIPCHK(hipMemcpyAsync(pair_col, P->pair_col, 8 * np, hipMemcpyDeviceToHost, cs));
+        if (pair_orig) HIPCHK(hipMemcpyAsync(pair_orig, P->pair_orig, 8 * np, hipMemcpyDeviceToHost, cs));
+    }
+    HIPCHK(hipStreamSynchronize(cs));
+    return 0;
+}
+
 int spg_bam_accumulate(spg_ctx *c, const spg_bam_plan *P, uint32_t flags) {
-    (void)flags;
+    // SPG_IN_DEVICE: the plan's arrays are in HBM (spg_bam_plan_build, trusted); else host arrays (validated here)
+    const bool devp = (flags & SPG_IN_DEVICE) != 0;
     if (!c || !P) return fail("spg_bam_accumulate: null argument");
     if (!c->lut_set) return fail("spg_accumulate: spg_set_eps_lut not called");
     if (!c->ref) return fail("spg_accumulate: spg_set_reference not called");
@@ -2431,17 +2558,20 @@ int spg_bam_accumulate(spg_ctx *c, const spg_bam_plan *P, uint32_t flags) {
                           (P->n_pairs && (!P->pair_a || !P->pair_b || !P->pair_col || !P->pair_orig))))
         return fail("spg_bam_accumulate: null buffer");
     if (P->n_cols == 0) { B.open = false; return 0; }
-    if (P->offsets[0] != 0 || P->offsets[P->n_cols] != P->n_entries)
-        return fail("spg_bam_accumulate: offsets[0] must be 0 and offsets[n_cols] == n_entries");
-    uint64_t desc = 0;
-    for (int64_t i = 0; i < P->n_cols; i++) desc |= (uint64_t)(P->offsets[i + 1] < P->offsets[i]);
-    if (desc) return fail("spg_bam_accumulate: offsets not monotone");
-    uint64_t need_orig = 0;
-    for (int64_t j = 0; j < P->n_pairs; j++) {
-        if (P->pair_a[j] >= B.n_reads || P->pair_b[j] >= B.n_reads) return fail("spg_bam_accumulate: pair read out of range");
-        need_orig = std::max<uint64_t>(need_orig, P->pair_orig[j]);
+    if (!devp) {
+        if (P->offsets[0] != 0 || P->offsets[P->n_cols] != P->n_entries)
+            return fail("spg_bam_accumulate: offsets[0] must be 0 and offsets[n_cols] == n_entries");
+        uint64_t desc = 0;
+        for (int64_t i = 0; i < P->n_cols; i++) desc |= (uint64_t)(P->offsets[i + 1] < P->offsets[i]);
+        if (desc) return fail("spg_bam_accumulate: offsets not monotone");
+        uint64_t need_orig = 0;
+        for (int64_t j = 0; j < P->n_pairs; j++) {
+            if (P->pair_a[j] >= B.n_reads || P->pair_b[j] >= B.n_reads)
+                return fail("spg_bam_accumulate: pair read out of range");
+            need_orig = std::max<uint64_t>(need_orig, P->pair_orig[j]);
+        }
+        if (P->n_pairs && P->orig_bytes < need_orig) return fail("spg_bam_accumulate: orig_bytes too small");
     }
-    if (P->n_pairs && P->orig_bytes < need_orig) return fail("spg_bam_accumulate: orig_bytes too small");
     HIPCHK(hipSetDevice(c->device));
     hipStream_t cs = c->copy_stream;
     const size_t nk = (size_t)P->n_kept, np = (size_t)P->n_pairs, nr = B.n_reads;
@@ -2456,13 +2586,14 @@ int spg_bam_accumulate(spg_ctx *c, const spg_bam_plan *P, uint32_t flags) {
     const int64_t n_tiles = (P->n_cols + 63) / 64;
     const size_t fsb = fill_scratch_bytes(P->n_cols, P->n_kept, P->max_span);
     HIPCHK(B.tile_first.need(fsb));
-    if (nk) HIPCHK(hipMemcpyAsync(B.kept.p, P->kept, 4 * nk, hipMemcpyHostToDevice, cs));
+    const hipMemcpyKind pk = devp ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (nk) HIPCHK(hipMemcpyAsync(B.kept.p, P->kept, 4 * nk, pk, cs));
     uint8_t *pb = B.pairs.as<uint8_t>();
     if (np) {
-        HIPCHK(hipMemcpyAsync(pb, P->pair_a, 4 * np, hipMemcpyHostToDevice, cs));
-        HIPCHK(hipMemcpyAsync(pb + o_pb, P->pair_b, 4 * np, hipMemcpyHostToDevice, cs));
-        HIPCHK(hipMemcpyAsync(pb + o_col, P->pair_col, 8 * np, hipMemcpyHostToDevice, cs));
-        HIPCHK(hipMemcpyAsync(pb + o_oq, P->pair_orig, 8 * np, hipMemcpyHostToDevice, cs));
+        HIPCHK(hipMemcpyAsync(pb, P->pair_a, 4 * np, pk, cs));
+        HIPCHK(hipMemcpyAsync(pb + o_pb, P->pair_b, 4 * np, pk, cs));
+        HIPCHK(hipMemcpyAsync(pb + o_col, P->pair_col, 8 * np, pk, cs));
+        HIPCHK(hipMemcpyAsync(pb + o_oq, P->pair_orig, 8 * np, pk, cs));
         BamPairArgs Q{};
         Q.data = B.out.as<uint8_t>();
         Q.wdata = B.out.as<uint8_t>();

@@ -259,6 +259,49 @@ struct FillArgs {
     uint32_t *err;                 // |= 2: the records disagree with the offsets (inconsistent plan)
 };
 
+// The pileup plan of a BAM in HBM built on the GPU (spg_plan.hip, spg_bam_plan_build): htslib's depth cap and mate
+// pairing over the kept reads' fixed fields (what spp_pileup_plan_fields replays on the host).
+struct PlanHead {                  // reductions and counts (zeroed / initialised by launch_plan_init)
+    int32_t min_span, max_span;    // over every read
+    int32_t max_span_kept, pad0;
+    uint32_t err;                  // 1: a read without reference span or out of order; 2: a name group too large
+    uint32_t n_distinct;           // distinct start positions
+    uint32_t n_kept, n_pairs;
+    int64_t min_pos, max_end;      // over every read
+    int64_t lo, hi;                // kept reads' column range [lo, hi)
+    uint64_t n_entries, orig_bytes;
+    int32_t max_cov, n_cand;       // coverage maximum over every read; pair candidates
+};
+struct PlanArgs {
+    uint32_t n;                    // reads, BAM (= coordinate) order
+    const int32_t *pos, *end, *mtid, *mpos, *isize;
+    const uint16_t *flag;
+    const uint32_t *l_seq;
+    const uint64_t *nhash;
+    int32_t tid;
+    int32_t olap;                  // ignore_overlaps: mate pairing
+    int64_t maxcnt;                // max_depth (INT64_MAX: uncapped)
+    int64_t span_lo;               // column range the diff arrays cover: [span_lo, span_lo + span_n)
+    int64_t span_n;
+    PlanHead *head;
+    uint32_t *first;               // [n + 1] 1 at a read that starts a new position; then (scanned) its distinct index
+    uint32_t *didx;                // [n + 1] exclusive scan of first
+    int32_t *dpos;                 // [n_distinct] distinct start positions
+    uint32_t *dfirst;              // [n_distinct + 1] their first read
+    uint8_t *keep;                 // [n] htslib keeps the read (max_depth)
+    uint32_t *kept;                // [n] kept reads in BAM order
+    int32_t *diff;                 // [span_n + 1] coverage difference array, then coverage
+    uint64_t *offsets;             // [span_n + 1] CSR offsets of the kept reads' columns
+    uint64_t *skey;                // [n] name hashes sorted (with sval: read index)
+    uint32_t *sval;
+    uint32_t *pairb;               // [n] first mate + 1 of a second mate (0: none)
+    uint32_t *pb_list;             // [n] second mates in BAM order
+    uint32_t *pa, *pbv;            // [n_pairs] pairs (first mate, second mate) in push order
+    int64_t *pcol;                 // [n_pairs] tweak column (htslib's iterator position at the second mate's push)
+    uint64_t *porig;               // [n_pairs] offset of the first mate's saved qualities
+    uint64_t *lsa;                 // [n_pairs] the first mates' l_seq (scanned into porig)
+};
+
 // A BAM in HBM (spg_bam.hip, include/spings_gpu.h spg_bam_*)
 constexpr uint64_t BAM_NONE = ~0ull;
 constexpr uint32_t BAM_RTMP = 2048;  // kept records the counting walk lists per member (a 64 KiB member holds <= 1,821)

@@ -1,0 +1,428 @@
+// spg_plan.hip — htslib's depth cap and mate pairing decided on the GPU for a BAM kept in HBM (include/spings_gpu.h
+// spg_bam_plan_build; SURVEY §8 f1 / a3: pysam's pileup() in process_bam, variant_caller/live_variant_caller.py:55-60).
+//
+// The host's device plan (spp_pileup_plan_fields, csrc/spp_pileup.cpp simulate()) replays bam_plp_push / bam_plp_next
+// read by read over the kept reads' fixed fields.  Two facts make it data-parallel here:
+//  * Which reads the iterator keeps does not depend on the mate pairing: with coordinate-sorted reads that each span
+//    >= 1 column, the first read at a start position p is always pushed, and the i-th (i >= 1) is dropped iff
+//    B_p + i + 1 > maxcnt, B_p = the kept reads with pos < p and end >= p (spp_pileup.cpp capped_no_pairs).  So
+//    k_p = min(n_p, max(1, maxcnt - B_p)) reads are kept at p, the first ones in BAM order.  k_plan_sweep carries B_p
+//    over the distinct start positions in windows of at most min(64, shortest span) positions: no read kept inside a
+//    window ends inside it, so a window's frees come from a ring of earlier kept reads' end counts (LDS), one lane per
+//    position, and only a window that can reach maxcnt runs the k recurrence lane by lane.
+//  * The overlap hash (read name -> the first mate waiting) only ever holds one entry per name, and an entry changes
+//    only at events of reads with that name: a push (pair with the entry, or insert), a drop (htslib's olap removal of
+//    the dropped read's name), and a free (the read's end passed: removal of its name).  A free of read y happens
+//    right after the push of the first read q with pos[q] > end[y], i.e. before the push of x iff end[y] < pos[x - 1],
+//    and after the entry e's insert iff pos[e - 1] <= end[y].  So k_plan_groups sorts the reads by name hash and
+//    replays each name's reads on one lane.  A pair's tweak column is htslib's iterator position at the second mate's
+//    push: the position of the last kept read before it.
+// Then the kept list, the kept reads' coverage -> CSR offsets, and the pairs in push order with their saved-quality
+// offsets — exactly spg_bam_plan's arrays, in HBM; spg_bam_accumulate takes them from there (SPG_IN_DEVICE).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "spg_device.h"
+
+namespace spg {
+
+namespace {
+
+constexpr uint32_t F_PAIRED = 0x1u, F_PROPER = 0x2u, F_MUNMAP = 0x8u;
+constexpr int SWEEP_T = 1024;                  // the sweep's one workgroup
+constexpr int RING = 8192;                     // kept-read end counts (LDS ring of end positions)
+constexpr int GROUP_MAX = 16;                  // reads sharing one name hash replayed by one lane (more: the host plans)
+
+__device__ __forceinline__ bool cand_of(const PlanArgs &A, uint32_t r) {        // htslib overlap_push's candidate test
+    const uint32_t fl = A.flag[r];
+    const int64_t is = A.isize[r];
+    return !(fl & F_MUNMAP) && (fl & F_PROPER) && !(A.mtid[r] >= 0 && A.mtid[r] != A.tid) &&
+           !((is < 0 ? -is : is) >= 2 * (int64_t)A.l_seq[r] && A.mpos[r] >= A.end[r]);
+}
+__device__ __forceinline__ bool insert_of(const PlanArgs &A, uint32_t r) {      // the first mate waits for its mate
+    return A.mpos[r] >= A.pos[r] || ((A.flag[r] & F_PAIRED) && A.mpos[r] == -1);
+}
+
+__device__ __forceinline__ int32_t wave_min(int32_t v) {
+    for (int o = 32; o; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int32_t wave_max(int32_t v) {
+    for (int o = 32; o; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int64_t wave_max64(int64_t v) {
+    for (int o = 32; o; o >>= 1) v = max(v, (int64_t)__shfl_xor((long long)v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int64_t wave_min64(int64_t v) {
+    for (int o = 32; o; o >>= 1) v = min(v, (int64_t)__shfl_xor((long long)v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
+    for (int o = 32; o; o >>= 1) v += (int64_t)__shfl_xor((long long)v, o, 64);
+    return v;
+}
+
+__global__ void k_plan_init(PlanHead *h) {
+    h->min_span = INT32_MAX;
+    h->max_span = INT32_MIN;
+    h->max_span_kept = 0;
+    h->err = 0;
+    h->n_distinct = h->n_kept = h->n_pairs = 0;
+    h->min_pos = INT64_MAX;
+    h->max_end = INT64_MIN;
+    h->lo = 0;
+    h->hi = 0;
+    h->n_entries = h->orig_bytes = 0;
+    h->max_cov = 0;
+    h->n_cand = 0;
+}
+
+// every read: its span (>= 1 column, else the host plans), sort order, new-position flag, pair candidates
+__global__ __launch_bounds__(256) void k_plan_reads(PlanArgs A) {
+    int32_t mn = INT32_MAX, mx = INT32_MIN;
+    int64_t pmin = INT64_MAX, emax = INT64_MIN;
+    uint32_t bad = 0, nc = 0;
+    for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < A.n; r += gridDim.x * 256u) {
+        const int32_t p = A.pos[r], e = A.end[r];
+        const int32_t prev = r ? A.pos[r - 1] : INT32_MIN;
+        mn = min(mn, e - p);
+        mx = max(mx, e - p);
+        pmin = min(pmin, (int64_t)p);
+        emax = max(emax, (int64_t)e);
+        bad |= (e <= p || prev > p || p < 0) ? 1u : 0u;
+        A.first[r] = (r == 0 || prev != p) ? 1u : 0u;
+        nc += (A.olap && cand_of(A, r)) ? 1u : 0u;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) A.first[A.n] = 0;
+    mn = wave_min(mn);
+    mx = wave_max(mx);
+    pmin = wave_min64(pmin);
+    emax = wave_max64(emax);
+    const uint64_t badm = __ballot(bad != 0);
+    const int64_t ncs = wave_sum64((int64_t)nc);
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&A.head->min_span, mn);
+        atomicMax(&A.head->max_span, mx);
+        if (pmin != INT64_MAX) atomicMin((unsigned long long *)&A.head->min_pos, (unsigned long long)pmin);
+        if (emax != INT64_MIN) atomicMax((unsigned long long *)&A.head->max_end, (unsigned long long)emax);
+        if (badm) atomicOr(&A.head->err, 1u);
+        if (ncs) atomicAdd((uint32_t *)&A.head->n_cand, (uint32_t)ncs);
+    }
+}
+
+// the distinct start positions and their first reads (didx: exclusive scan of first)
+__global__ __launch_bounds__(256) void k_plan_distinct(PlanArgs A) {
+    for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < A.n; r += gridDim.x * 256u)
+        if (A.first[r]) {
+            A.dpos[A.didx[r]] = A.pos[r];
+            A.dfirst[A.didx[r]] = r;
+        }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        A.dfirst[A.didx[A.n]] = A.n;
+        A.head->n_distinct = A.didx[A.n];
+    }
+}
+
+__device__ __forceinline__ int32_t wave_incl_scan_i32(int32_t v) {
+    const int lane = threadIdx.x & 63;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t u = __shfl_up(v, o, 64);
+        if (lane >= o) v += u;
+    }
+    return v;
+}
+
+// htslib's depth cap over the distinct start positions in order (one workgroup; see the file comment)
+__global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
+    __shared__ int32_t ring[RING];
+    __shared__ uint32_t kk[64], ff[64];
+    __shared__ int32_t jmap[64];
+    __shared__ uint32_t s_r0, s_r1, s_next;
+    __shared__ int32_t s_P;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint32_t D = A.head->n_distinct;
+    const int32_t W0 = min(64, A.head->min_span);
+    const int64_t M = A.maxcnt;
+    for (int i = tid; i < RING; i += SWEEP_T) ring[i] = 0;
+    __syncthreads();
+    int64_t alive = 0;                                 // (wave 0) kept reads not freed yet
+    int32_t at = D ? A.dpos[0] : 0;                    // (wave 0) frees applied for every end < at
+    uint32_t d = 0;
+    while (d < D) {
+        if (tid < 64) {
+            const int32_t P = A.dpos[d];
+            const uint32_t idx = d + (uint32_t)lane;
+            const int32_t pj = idx < D ? A.dpos[idx] : INT32_MAX;
+            const bool valid = idx < D && pj < P + W0;
+            const uint32_t w = (uint32_t)__popcll(__ballot(valid));          // (valid lanes are a prefix)
+            const int32_t plast = __shfl(pj, (int)w - 1, 64);
+            // frees of the ends in [at, P): all of them when the gap exceeds the ring
+            int64_t gap = 0;
+            if ((int64_t)P - at >= RING) {
+                for (int i = lane; i < RING; i += 64) ring[i] = 0;
+                gap = alive;
+            } else {
+                for (int32_t x = at; x < P; x += 64) {
+                    const int32_t s = x + lane;
+                    int32_t v = 0;
+                    if (s < P) { v = ring[s & (RING - 1)]; ring[s & (RING - 1)] = 0; }
+                    gap += wave_sum64(v);
+                }
+            }
+            // frees inside the window: ends in [P, plast), one lane per slot, scanned
+            int32_t c = 0;
+            if (P + lane < plast) { c = ring[(P + lane) & (RING - 1)]; ring[(P + lane) & (RING - 1)] = 0; }
+            const int32_t S = wave_incl_scan_i32(c);
+            const int32_t Sj = __shfl(S, valid && pj > P ? pj - P - 1 : 0, 64);
+            const int64_t Fj = gap + (valid && pj > P ? (int64_t)Sj : 0);
+            const int64_t Ftot = gap + (plast > P ? (int64_t)__shfl(S, plast - P - 1, 64) : 0);
+            const uint32_t f0 = valid ? A.dfirst[idx] : 0u, f1 = valid ? A.dfirst[idx + 1] : 0u;
+            const int64_t nj = (int64_t)(f1 - f0);
+            const int64_t sumn = wave_sum64(nj);
+            int64_t k = nj;
+            if (alive + sumn > M) {                    // the cap may bite: k_j = min(n_j, max(1, M - alive_j)) in order
+                int64_t cum = 0;
+                for (uint32_t j = 0; j < w; j++) {
+                    const int64_t fj = (int64_t)__shfl((long long)Fj, (int)j, 64);
+                    const int64_t n_ = (int64_t)__shfl((long long)nj, (int)j, 64);
+                    const int64_t a = alive - fj + cum;
+                    const int64_t kj = min(n_, max((int64_t)1, M - a));
+                    if ((uint32_t)lane == j) k = kj;
+                    cum += kj;
+                }
+            }
+            alive = alive - Ftot + wave_sum64(valid ? k : 0);
+            at = plast;
+            jmap[lane] = -1;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_wave_barrier();
+            if (valid) {
+                kk[lane] = (uint32_t)k;
+                ff[lane] = f0;
+                jmap[pj - P] = lane;
+            }
+            if (lane == 0) {
+                s_P = P;
+                s_r0 = A.dfirst[d];
+                s_r1 = A.dfirst[d + w];
+                s_next = d + w;
+            }
+        }
+        __syncthreads();
+        const int32_t P = s_P;
+        const uint32_t r0 = s_r0, r1 = s_r1;
+        for (uint32_t r = r0 + (uint32_t)tid; r < r1; r += SWEEP_T) {
+            const int j = jmap[A.pos[r] - P];
+            const bool kp = r - ff[j] < kk[j];
+            A.keep[r] = kp ? 1 : 0;
+            if (kp) atomicAdd(&ring[A.end[r] & (RING - 1)], 1);
+        }
+        d = s_next;
+        __syncthreads();
+    }
+}
+
+// one lane per name hash group: the overlap hash's events for that name, in time order (see the file comment)
+__global__ __launch_bounds__(256) void k_plan_groups(PlanArgs A) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < A.n; i += gridDim.x * 256u) {
+        const uint64_t key = A.skey[i];
+        if (i && A.skey[i - 1] == key) continue;                         // not the group's first
+        uint32_t s = 1;
+        while (i + s < A.n && A.skey[i + s] == key && s <= GROUP_MAX) s++;
+        if (s == 1) continue;
+        if (s > GROUP_MAX) { atomicOr(&A.head->err, 2u); continue; }
+        int64_t e = -1;                                                 // the entry (read index) or none
+        for (uint32_t t = 0; t < s; t++) {
+            const uint32_t x = A.sval[i + t];
+            if (e >= 0) {
+                const int64_t px = A.pos[x - 1];                         // (x > e >= 0)
+                const int64_t pe = e ? A.pos[e - 1] : INT64_MIN;
+                bool gone = false;
+                for (uint32_t u = 0; u < t && !gone; u++) {
+                    const uint32_t y = A.sval[i + u];
+                    if (A.keep[y]) gone = pe <= (int64_t)A.end[y] && (int64_t)A.end[y] < px;   // y freed in between
+                    else gone = (int64_t)y > e;                                                 // y dropped in between
+                }
+                if (gone) e = -1;
+            }
+            if (!A.keep[x] || !cand_of(A, x)) continue;
+            if (e >= 0) {
+                A.pairb[x] = (uint32_t)e + 1u;
+                e = -1;
+            } else if (insert_of(A, x)) {
+                e = x;
+            }
+        }
+    }
+}
+
+// the pairs in push order (second mates ascending): first mate, tweak column, the first mate's l_seq
+__global__ __launch_bounds__(256) void k_plan_pairs(PlanArgs A) {
+    const uint32_t np = A.head->n_pairs;
+    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < np; j += gridDim.x * 256u) {
+        const uint32_t b = A.pb_list[j], a = A.pairb[b] - 1u;
+        uint32_t c = b - 1u;                                             // the last kept read before b (a is one)
+        while (!A.keep[c]) c--;
+        A.pa[j] = a;
+        A.pbv[j] = b;
+        A.pcol[j] = A.pos[c];
+        A.lsa[j] = A.l_seq[a];
+    }
+}
+
+// the kept reads' coverage difference array over [span_lo, span_lo + span_n); all reads when `all`
+__global__ __launch_bounds__(256) void k_plan_diff(PlanArgs A, int all) {
+    const uint32_t n = all ? A.n : A.head->n_kept;
+    int32_t mx = 0;
+    int64_t hi = INT64_MIN;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint32_t r = all ? i : A.kept[i];
+        const int32_t p = A.pos[r], e = A.end[r];
+        atomicAdd(&A.diff[p - A.span_lo], 1);
+        atomicAdd(&A.diff[e - A.span_lo], -1);
+        mx = max(mx, e - p);
+        hi = max(hi, (int64_t)e);
+    }
+    mx = wave_max(mx);
+    hi = wave_max64(hi);
+    if (!all && (threadIdx.x & 63) == 0) {
+        atomicMax(&A.head->max_span_kept, mx);
+        if (hi != INT64_MIN) atomicMax((unsigned long long *)&A.head->hi, (unsigned long long)hi);
+    }
+}
+
+// the coverage maximum (the global cold check of a long contig)
+__global__ __launch_bounds__(256) void k_plan_covmax(PlanArgs A, const int32_t *cov) {
+    int32_t mx = 0;
+    for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < A.span_n; c += (int64_t)gridDim.x * 256)
+        mx = max(mx, cov[c]);
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0) atomicMax(&A.head->max_cov, mx);
+}
+
+__global__ void k_plan_tail(PlanArgs A) {
+    PlanHead *h = A.head;
+    if (h->n_kept) {
+        h->lo = A.pos[A.kept[0]];
+        h->n_entries = A.offsets[h->hi - A.span_lo];
+    } else {
+        h->lo = h->hi = 0;
+    }
+    h->orig_bytes = h->n_pairs ? A.porig[h->n_pairs - 1] + A.lsa[h->n_pairs - 1] : 0;
+}
+
+__global__ __launch_bounds__(256) void k_plan_fill_u8(uint8_t *p, uint32_t n, uint8_t v) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) p[i] = v;
+}
+__global__ __launch_bounds__(256) void k_plan_iota(uint32_t *p, uint32_t n) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) p[i] = i;
+}
+
+struct NonZero {
+    __host__ __device__ __forceinline__ bool operator()(const uint32_t &v) const { return v != 0; }
+};
+struct ToU64 {
+    __host__ __device__ __forceinline__ uint64_t operator()(const int32_t &v) const { return (uint64_t)(int64_t)v; }
+};
+using CovU64 = hipcub::TransformInputIterator<uint64_t, ToU64, const int32_t *>;
+
+unsigned grid_for(uint64_t n) { return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 255) / 256, 4096)); }
+
+}  // namespace
+
+// hipcub scratch the plan's scans / compactions / sort need for n reads and a column span of span_n
+size_t plan_temp_bytes(uint32_t n, int64_t span_n) {
+    size_t need = 0, b = 0;
+    const int ni = (int)n;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint32_t *)nullptr, (uint32_t *)nullptr, ni + 1);
+    need = std::max(need, b);
+    hipcub::CountingInputIterator<uint32_t> it(0);
+    (void)hipcub::DeviceSelect::Flagged(nullptr, b, it, (uint8_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr, ni);
+    need = std::max(need, b);
+    hipcub::TransformInputIterator<bool, NonZero, const uint32_t *> nz((const uint32_t *)nullptr, NonZero());
+    (void)hipcub::DeviceSelect::Flagged(nullptr, b, it, nz, (uint32_t *)nullptr, (uint32_t *)nullptr, ni);
+    need = std::max(need, b);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                             (const uint32_t *)nullptr, (uint32_t *)nullptr, ni);
+    need = std::max(need, b);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint64_t *)nullptr, (uint64_t *)nullptr, ni);
+    need = std::max(need, b);
+    if (span_n > 0) {
+        (void)hipcub::DeviceScan::InclusiveSum(nullptr, b, (int32_t *)nullptr, (int32_t *)nullptr, (int)(span_n + 1));
+        need = std::max(need, b);
+        (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, CovU64((const int32_t *)nullptr, ToU64()), (uint64_t *)nullptr,
+                                               (int)(span_n + 1));
+        need = std::max(need, b);
+    }
+    return need + 256;
+}
+
+// stage 0: every read's fields checked, the distinct start positions listed (then the host reads the head)
+hipError_t launch_plan_reads(const PlanArgs &A, void *tmp, size_t tmp_bytes, hipStream_t st) {
+    k_plan_init<<<1, 1, 0, st>>>(A.head);
+    k_plan_reads<<<grid_for(A.n), 256, 0, st>>>(A);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, A.first, A.didx, (int)A.n + 1, st);
+    if (e != hipSuccess) return e;
+    k_plan_distinct<<<grid_for(A.n), 256, 0, st>>>(A);
+    return hipGetLastError();
+}
+
+// the coverage of every read (all = 1: the global cold check, max_cov) or of the kept ones (CSR offsets)
+hipError_t launch_plan_cov(const PlanArgs &A, int all, int32_t *cov, void *tmp, size_t tmp_bytes, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(A.diff, 0, sizeof(int32_t) * (size_t)(A.span_n + 1), st);
+    if (e != hipSuccess) return e;
+    k_plan_diff<<<grid_for(A.n), 256, 0, st>>>(A, all);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    e = hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, A.diff, cov, (int)(A.span_n + 1), st);
+    if (e != hipSuccess) return e;
+    if (all) {
+        k_plan_covmax<<<grid_for((uint64_t)A.span_n), 256, 0, st>>>(A, cov);
+        return hipGetLastError();
+    }
+    // offsets[c] = the entries of columns before c (cov[span_n] is 0: the difference array sums to 0)
+    return hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, CovU64(cov, ToU64()), A.offsets, (int)(A.span_n + 1), st);
+}
+
+// keep: every read (uncapped, or the cap never reached), or the sweep
+hipError_t launch_plan_keep(const PlanArgs &A, bool sweep, hipStream_t st) {
+    if (!sweep) {
+        k_plan_fill_u8<<<grid_for(A.n), 256, 0, st>>>(A.keep, A.n, 1);
+        return hipGetLastError();
+    }
+    k_plan_sweep<<<1, SWEEP_T, 0, st>>>(A);
+    return hipGetLastError();
+}
+
+// the kept list, the kept reads' CSR offsets, the pairs (when pairing), the head's totals
+hipError_t launch_plan_rest(const PlanArgs &A, int32_t *cov, bool pairing, void *tmp, size_t tmp_bytes, hipStream_t st) {
+    hipcub::CountingInputIterator<uint32_t> it(0);
+    hipError_t e = hipcub::DeviceSelect::Flagged(tmp, tmp_bytes, it, A.keep, A.kept, &A.head->n_kept, (int)A.n, st);
+    if (e != hipSuccess) return e;
+    if ((e = launch_plan_cov(A, 0, cov, tmp, tmp_bytes, st)) != hipSuccess) return e;
+    if (pairing) {
+        if ((e = hipMemsetAsync(A.pairb, 0, sizeof(uint32_t) * A.n, st)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(A.lsa, 0, sizeof(uint64_t) * A.n, st)) != hipSuccess) return e;
+        k_plan_iota<<<grid_for(A.n), 256, 0, st>>>(A.pb_list, A.n);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, (const uint64_t *)A.nhash, A.skey, (const uint32_t *)A.pb_list,
+                                               A.sval, (int)A.n, 0, 64, st);
+        if (e != hipSuccess) return e;
+        k_plan_groups<<<grid_for(A.n), 256, 0, st>>>(A);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipcub::TransformInputIterator<bool, NonZero, const uint32_t *> nz(A.pairb, NonZero());
+        e = hipcub::DeviceSelect::Flagged(tmp, tmp_bytes, it, nz, A.pb_list, &A.head->n_pairs, (int)A.n, st);
+        if (e != hipSuccess) return e;
+        k_plan_pairs<<<grid_for(A.n), 256, 0, st>>>(A);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, A.lsa, A.porig, (int)A.n, st);
+        if (e != hipSuccess) return e;
+    }
+    k_plan_tail<<<1, 1, 0, st>>>(A);
+    return hipGetLastError();
+}
+
+}  // namespace spg

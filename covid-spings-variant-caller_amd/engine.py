@@ -260,6 +260,44 @@ class PileupEngine:
             N.check(rc, "spg_bam_accumulate")
         return True
 
+    def bam_plan_build(self, max_depth: int, ignore_overlaps: bool = True):
+        """spg_bam_plan_build: the open BAM's pileup plan built in HBM — htslib's depth cap and mate pairing on the GPU
+        (what AlignmentFile.pileup_fields computes on the host from bam_reads).  The plan (device pointers, valid until
+        this slot's next bam_open) for bam_accumulate_planned, or None when the device declined (bam_fallback says
+        why: plan on the host)."""
+        p = N.SpgBamPlan()
+        with self._lock:
+            rc = self._L.spg_bam_plan_build(self._h, int(max_depth), 1 if ignore_overlaps else 0, C.byref(p))
+            if rc == 1:
+                self.bam_fallback = self._L.spg_last_error().decode(errors="replace")
+                return None
+            N.check(rc, "spg_bam_plan_build")
+        return p
+
+    def bam_accumulate_planned(self, plan) -> bool:
+        """spg_bam_accumulate of a bam_plan_build plan (SPG_IN_DEVICE).  False when refused (two paired reads whose
+        names differ behind equal hashes: plan the BAM on the host)."""
+        with self._lock:
+            rc = self._L.spg_bam_accumulate(self._h, C.byref(plan), N.SPG_IN_DEVICE)
+            if rc == 1:
+                self.bam_fallback = self._L.spg_last_error().decode(errors="replace")
+                return False
+            N.check(rc, "spg_bam_accumulate")
+        return True
+
+    def bam_plan_arrays(self, plan) -> Dict[str, np.ndarray]:
+        """A bam_plan_build plan's arrays on the host (spg_bam_plan_download; tests)."""
+        nc, nk, npr = max(0, int(plan.n_cols)), int(plan.n_kept), int(plan.n_pairs)
+        out = {"offsets": np.zeros(nc + 1, np.uint64), "kept": np.zeros(nk, np.uint32), "pair_a": np.zeros(npr, np.uint32),
+               "pair_b": np.zeros(npr, np.uint32), "pair_col": np.zeros(npr, np.int64),
+               "pair_orig": np.zeros(npr, np.uint64)}
+        with self._lock:
+            N.check(self._L.spg_bam_plan_download(self._h, C.byref(plan), *[N.ptr(out[k]) for k in
+                                                                            ("offsets", "kept", "pair_a", "pair_b",
+                                                                             "pair_col", "pair_orig")]),
+                    "spg_bam_plan_download")
+        return out
+
     def bam_inflate_ms(self) -> float:
         ms = C.c_float()
         N.check(self._L.spg_bam_inflate_ms(self._h, C.byref(ms)), "spg_bam_inflate_ms")

@@ -152,7 +152,7 @@ class LiveVariantCaller:
                  max_depth: int = 8000, stepper: str = "all", ignore_overlaps: bool = True,
                  n_threads: Optional[int] = None, devices: Optional[List[int]] = None, pileup: str = "device",
                  gpu_inflate: bool = True, device_min_bytes: int = 32 << 20, checkpoint_write_behind: bool = False,
-                 checkpoint_prealloc: bool = True):
+                 checkpoint_prealloc: bool = True, gpu_plan: bool = True):
         """The reference's 7 arguments (:22-32), then the engine's: ``device`` (default LOCAL_RANK or 0), or
         ``devices`` — several GPUs of this host, each owning a coordinate range of the contig (multi.MultiEngine,
         spg_multi_*: BAM records and host batches sliced at equal-entry cuts, one RCCL gather of the call tables);
@@ -180,8 +180,11 @@ class LiveVariantCaller:
         BAM.  This caller's next create_checkpoint, reset_memory, close or flush_checkpoints(), and any caller's
         load_checkpoint of that file in this process, wait for it first (and raise the error it met, if any).
         ``checkpoint_prealloc`` (default on: vc_queue.py:134 checkpoints after every BAM) — a BAM kept in HBM reserves the
-        pinned staging its checkpoint will need on a helper thread while the host plans it, so a caller's first
-        create_checkpoint does not pin ~0.4 GB of pages itself."""
+        pinned staging its checkpoint will need on a helper thread while the GPU works on it, so a caller's first
+        create_checkpoint does not pin ~0.4 GB of pages itself.
+        ``gpu_plan`` (default on) — a BAM kept in HBM has htslib's depth cap and mate pairing decided on the GPU
+        (spg_bam_plan_build); off: its reads' fixed fields come down and the host replays them (spp_pileup_plan_fields),
+        which is also the path of the rare BAMs the GPU plan declines."""
         if pileup not in ("device", "records", "host"):
             raise ValueError(f"pileup must be 'device', 'records' or 'host', not {pileup!r}")
         self.minBaseQuality = minBaseQuality
@@ -221,6 +224,8 @@ class LiveVariantCaller:
         self._ck_bytes = 0                       # shard bytes the last create_checkpoint wrote
         self.checkpoint_write_behind = bool(checkpoint_write_behind)
         self.checkpoint_prealloc = bool(checkpoint_prealloc)
+        self.gpu_plan = bool(gpu_plan)
+        self.last_plan_path = None               # "device" (spg_bam_plan_build) or "host" (spp_pileup_plan_fields)
         self._ck_job = None                      # the write-behind checkpoint in flight (a Future)
         self._ck_pool = None
         self.reset_memory()
@@ -298,7 +303,7 @@ class LiveVariantCaller:
                 raise ValueError(f"invalid contig `{contig}`")
             bgzf = _is_bgzf(inputBam)
             if (self._device_bam and bgzf and os.path.getsize(inputBam) >= self.device_min_bytes
-                    and self._process_bam_device(bam, contig, referenceIndex)):
+                    and self._process_bam_device(bam, contig, referenceIndex, os.path.getsize(inputBam))):
                 self.last_bam_path = "device"
                 return
             if self.device_pileup and bgzf:
@@ -311,11 +316,17 @@ class LiveVariantCaller:
         # copy stream while the next BAM is read
         self._accumulate_plan(batch, referenceIndex)
 
-    def _process_bam_device(self, bam: AlignmentFile, contig: str, referenceIndex: int) -> bool:
-        """The BAM kept in HBM (spg_bam_*): compressed bytes up, inflate + record scan + stepper filter on the GPU, the
-        kept reads' fixed fields down, htslib's depth cap / mate pairing replayed on them on the host
-        (spp_pileup_plan_fields), the plan up, mate-overlap tweak + entries + accumulate on the GPU.  False when the
-        device declined the BAM (nothing accumulated: the caller plans it on the host)."""
+    def _process_bam_device(self, bam: AlignmentFile, contig: str, referenceIndex: int, file_bytes: int = 0) -> bool:
+        """The BAM kept in HBM (spg_bam_*): compressed bytes up, inflate + record scan + stepper filter on the GPU, then
+        htslib's depth cap / mate pairing decided on the GPU too (spg_bam_plan_build), mate-overlap tweak + entries +
+        accumulate — nothing comes down.  When the device declines the plan (spg_bam_plan_build's rare cases), the kept
+        reads' fixed fields come down and the host replays it (spp_pileup_plan_fields), the plan goes up.  False when
+        the device declined the BAM itself (nothing accumulated: the caller plans it on the host)."""
+        if self.checkpoint_prealloc and isinstance(self.engine, PileupEngine) and file_bytes:
+            # the checkpoint's pinned staging for this BAM's batch, pinned on a helper thread while the GPU works (a
+            # BAM's pileup entries are ~1.4 bytes per compressed byte here; vc_queue.py:134 checkpoints after every BAM)
+            self.engine.reserve_staging(self.fastaFile.get_reference_length(contig) + 1, int(1.5 * file_bytes),
+                                        write_behind=self.checkpoint_write_behind)
         bmap = bam.bam_map(self.pileup_params.n_threads)
         try:
             with self._lock:
@@ -326,13 +337,21 @@ class LiveVariantCaller:
             log.info("device BAM path declined %s: %s", contig, self.engine.bam_fallback)
             return False
         with self._lock:
+            if self.gpu_plan:
+                plan = self.engine.bam_plan_build(self.pileup_params.max_depth, self.pileup_params.ignore_overlaps)
+                if plan is not None:
+                    self.last_plan_path = "device"
+                    if plan.n_cols == 0:
+                        return True
+                    self._use_reference(referenceIndex)
+                    if not self.engine.bam_accumulate_planned(plan):
+                        log.info("device BAM plan declined: %s", self.engine.bam_fallback)
+                        return False
+                    self._batch_contig.append(referenceIndex)
+                    return True
+                log.info("GPU plan declined %s: %s (host plan)", contig, self.engine.bam_fallback)
+            self.last_plan_path = "host"
             reads = self.engine.bam_reads(n)
-            if self.checkpoint_prealloc and isinstance(self.engine, PileupEngine):
-                # the checkpoint's pinned staging for this BAM's batch, allocated while the host plans it (entries <=
-                # the kept reads' aligned spans; vc_queue.py:134 checkpoints after every BAM)
-                self.engine.reserve_staging(self.fastaFile.get_reference_length(contig) + 1,
-                                            lambda r=reads: int(r["end"].sum(dtype=np.int64) - r["pos"].sum(dtype=np.int64)),
-                                            write_behind=self.checkpoint_write_behind)
             batch = bam.pileup_fields(contig, reads, self.pileup_params)
             if batch.n_cols == 0:
                 batch.close()
@@ -445,16 +464,38 @@ class LiveVariantCaller:
                     if i + 1 < len(paths):
                         nb, nm = maps[i + 1].result()
                         self.engine.bam_upload(nm, slot ^ 1)
+                    plan = None
                     try:
                         with self._lock:
                             self.engine.bam_slot(slot)
                             n = self.engine.bam_open(bmap, bam.tid(contig), prm)
-                            reads = self.engine.bam_reads(n) if n is not None else None
+                            if n is not None and self.gpu_plan:
+                                # htslib's depth cap / mate pairing on the GPU (spg_bam_plan_build): nothing comes down
+                                plan = self.engine.bam_plan_build(prm.max_depth, prm.ignore_overlaps)
+                            reads = self.engine.bam_reads(n) if n is not None and plan is None else None
                     finally:
                         bmap.close()
                     if pending is not None:           # BAM i - 1: planned on the worker while BAM i opened
                         job, pending = pending, None
                         finish(job)
+                    if plan is not None:              # in order, after BAM i - 1
+                        ok = True
+                        with self._lock:
+                            if plan.n_cols:
+                                self._use_reference(referenceIndex)
+                                self.engine.bam_slot(slot)
+                                ok = self.engine.bam_accumulate_planned(plan)
+                                if ok:
+                                    self._batch_contig.append(referenceIndex)
+                        if not ok:
+                            log.info("device BAM plan declined %s: %s", paths[i], self.engine.bam_fallback)
+                            try:
+                                self._accumulate_plan(bam.pileup_records(contig, prm), referenceIndex)
+                            finally:
+                                bam.close()
+                        else:
+                            bam.close()
+                        continue
                     if reads is None:                 # declined: the records plan, in order
                         log.info("device BAM path declined %s: %s", paths[i], self.engine.bam_fallback)
                         try:

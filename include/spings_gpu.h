@@ -391,7 +391,20 @@ typedef struct spg_bam_plan {
     int64_t max_span;              /* max(end - pos) over the kept reads */
     int64_t reserved[4];
 } spg_bam_plan;
+/* flags: SPG_IN_DEVICE when the plan's arrays are in HBM (spg_bam_plan_build), else host arrays. */
 int spg_bam_accumulate(spg_ctx *ctx, const spg_bam_plan *plan, uint32_t flags);
+/* The open BAM's plan built on the GPU — htslib's depth cap (max_depth 0: none) and, with ignore_overlaps, its mate
+ * pairing over the kept reads' fixed fields: the arrays spp_pileup_plan_fields computes on the host from
+ * spg_bam_reads_copy, here without the fields leaving HBM.  *plan gets device pointers (valid until this slot's next
+ * spg_bam_open / spg_bam_plan_build) for spg_bam_accumulate(..., SPG_IN_DEVICE).  Returns 1 (nothing built, reason in
+ * spg_last_error) when the device declines: a read without reference span, a read spanning more than 8,000 columns
+ * under a cap, more than 16 reads sharing a name hash, a capped contig of > 4 M start positions where the cap bites;
+ * the caller then plans the BAM on the host (spg_bam_reads_copy + spp_pileup_plan_fields). */
+int spg_bam_plan_build(spg_ctx *ctx, int64_t max_depth, int32_t ignore_overlaps, spg_bam_plan *plan);
+/* A built plan's arrays copied to host memory (n_cols + 1 offsets, n_kept reads, n_pairs of each pair array; any may
+ * be NULL). */
+int spg_bam_plan_download(spg_ctx *ctx, const spg_bam_plan *plan, uint64_t *offsets, uint32_t *kept, uint32_t *pair_a,
+                          uint32_t *pair_b, int64_t *pair_col, uint64_t *pair_orig);
 /* ms of the last spg_bam_open's inflate + CRC kernels (HIP events) */
 int spg_bam_inflate_ms(spg_ctx *ctx, float *ms);
 /* members of the last spg_bam_open that the parallel inflater left to the one-lane-per-member decoder */

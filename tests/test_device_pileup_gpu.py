@@ -53,9 +53,10 @@ def device_fill(path, contig, start=None, stop=None, pinned=False, **kw):
         eng.close()
 
 
-def bam_device_fill(path, contig, **kw):
-    """The BAM kept in HBM (spg_bam_open -> spg_bam_reads_copy -> spp_pileup_plan_fields -> spg_bam_accumulate):
-    the batch the engine then holds, or None for a contig without entries."""
+def bam_device_fill(path, contig, gpu_plan=False, **kw):
+    """The BAM kept in HBM (spg_bam_open -> spg_bam_reads_copy -> spp_pileup_plan_fields -> spg_bam_accumulate; with
+    gpu_plan the depth cap / pairing on the GPU: spg_bam_plan_build -> spg_bam_accumulate(SPG_IN_DEVICE)): the batch the
+    engine then holds, or None for a contig without entries."""
     params = PileupParams(n_threads=kw.pop("n_threads", 4), **kw)
     with AlignmentFile(path) as f:
         L = f.get_reference_length(contig)
@@ -65,17 +66,75 @@ def bam_device_fill(path, contig, **kw):
             n = eng.bam_open(bmap, f.tid(contig), params)
             bmap.close()
             assert n is not None, eng.bam_fallback
-            b = f.pileup_fields(contig, eng.bam_reads(n), params)
-            try:
-                if b.n_cols == 0:
+            if gpu_plan:
+                plan = eng.bam_plan_build(params.max_depth, params.ignore_overlaps)
+                assert plan is not None, eng.bam_fallback
+                if plan.n_cols == 0:
                     return None
-                assert eng.bam_accumulate(b), eng.bam_fallback
+                assert eng.bam_accumulate_planned(plan), eng.bam_fallback
+                b = None
+            else:
+                b = f.pileup_fields(contig, eng.bam_reads(n), params)
+            try:
+                if b is not None:
+                    if b.n_cols == 0:
+                        return None
+                    assert eng.bam_accumulate(b), eng.bam_fallback
                 eng.sync()
                 hist = eng.history()
                 assert len(hist) == 1
                 eng.finalize()
                 eng.counts()                  # settles: raises if the fill flagged an inconsistent plan
                 return hist[0]
+            finally:
+                if b is not None:
+                    b.close()
+        finally:
+            eng.close()
+
+
+def _host_plan_arrays(v):
+    """spp_pileup_plan_fields' spg_bam_plan (host pointers) as numpy arrays."""
+    def arr(p, n, t):
+        if n <= 0 or not p:
+            return np.zeros(0, t)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(np.ctypeslib.as_ctypes_type(t))), shape=(n,)).copy()
+    return {"offsets": arr(v.offsets, int(v.n_cols) + 1, np.uint64), "kept": arr(v.kept, int(v.n_kept), np.uint32),
+            "pair_a": arr(v.pair_a, int(v.n_pairs), np.uint32), "pair_b": arr(v.pair_b, int(v.n_pairs), np.uint32),
+            "pair_col": arr(v.pair_col, int(v.n_pairs), np.int64), "pair_orig": arr(v.pair_orig, int(v.n_pairs), np.uint64)}
+
+
+def plan_compare(path, contig, **kw):
+    """spg_bam_plan_build (htslib's depth cap and mate pairing on the GPU) against spp_pileup_plan_fields (the host's
+    replay of bam_plp_push / bam_plp_next on the same reads' fields): every array of the plan identical.  Returns the
+    number of pairs and of kept reads, or None when the GPU declined (then the reads hold one without reference span)."""
+    params = PileupParams(n_threads=kw.pop("n_threads", 4), **kw)
+    with AlignmentFile(path) as f:
+        L = f.get_reference_length(contig)
+        eng = PileupEngine(L + 1, reference="A" * (L + 1))
+        try:
+            bmap = f.bam_map(4)
+            n = eng.bam_open(bmap, f.tid(contig), params)
+            bmap.close()
+            assert n is not None, eng.bam_fallback
+            dplan = eng.bam_plan_build(params.max_depth, params.ignore_overlaps)
+            reads = eng.bam_reads(n)
+            if dplan is None:
+                assert "reference span" in eng.bam_fallback and (reads["end"] <= reads["pos"]).any(), eng.bam_fallback
+                return None
+            dev = eng.bam_plan_arrays(dplan)
+            b = f.pileup_fields(contig, reads, params)
+            try:
+                hv = b.device_plan()
+                host = _host_plan_arrays(hv)
+                if int(hv.n_cols) == 0:
+                    assert int(dplan.n_cols) == 0
+                    return 0, 0
+                for k in ("pos_begin", "n_cols", "n_entries", "n_kept", "n_pairs", "orig_bytes", "max_span"):
+                    assert int(getattr(dplan, k)) == int(getattr(hv, k)), k
+                for k in host:
+                    np.testing.assert_array_equal(dev[k], host[k], err_msg=k)
+                return int(hv.n_pairs), int(hv.n_kept)
             finally:
                 b.close()
         finally:
@@ -177,6 +236,8 @@ def test_hand_derived_fixtures(tmp_path, case):
     got = device_fill(bam, "c", **kw)
     H.expect(got, pb, cols)
     H.expect(bam_device_fill(bam, "c", **kw), pb, cols)
+    H.expect(bam_device_fill(bam, "c", gpu_plan=True, **kw), pb, cols)
+    plan_compare(bam, "c", **kw)
     if all(ord(ch) - 33 <= 93 for r in recs for ch in r["qual"]):
         assert_same(got, _port(recs, "c", [("c", 60)], tmp_path, **kw))
     assert_same(got, host_fill(bam, "c", **kw))
@@ -201,6 +262,8 @@ def test_random_reads(tmp_path, seed, kw):
         assert_same(got, port)
         assert_same(got, host_fill(bam, c, **kw))
         assert_same(bam_device_fill(bam, c, **kw), port)
+        if plan_compare(bam, c, **kw) is not None:
+            assert_same(bam_device_fill(bam, c, gpu_plan=True, **kw), port)
 
 
 @pytest.mark.parametrize("region", [(100, 300), (0, 50), (550, 700), (250, 251)])
@@ -224,6 +287,9 @@ def test_long_spans_and_gaps(tmp_path):
     samgen.write_bam(bam, [("c", 20000)], recs)
     assert_same(device_fill(bam, "c", max_depth=0), host_fill(bam, "c", max_depth=0))
     assert_same(bam_device_fill(bam, "c", max_depth=0), host_fill(bam, "c", max_depth=0))
+    assert_same(bam_device_fill(bam, "c", gpu_plan=True, max_depth=0), host_fill(bam, "c", max_depth=0))
+    plan_compare(bam, "c", max_depth=0)
+    plan_compare(bam, "c", max_depth=7)
 
 
 @pytest.mark.parametrize("depth,max_depth", [(200, 8000), (10000, 8000), (10000, 0)])
@@ -236,6 +302,9 @@ def test_simulated_bams(tmp_path, depth, max_depth):
     host = host_fill(bam, "NC_045512.2", max_depth=max_depth)
     assert_same(device_fill(bam, "NC_045512.2", pinned=True, max_depth=max_depth), host)
     assert_same(bam_device_fill(bam, "NC_045512.2", max_depth=max_depth), host)
+    assert_same(bam_device_fill(bam, "NC_045512.2", gpu_plan=True, max_depth=max_depth), host)
+    n_pairs, n_kept = plan_compare(bam, "NC_045512.2", max_depth=max_depth)
+    assert n_pairs > 0
 
 
 @pytest.mark.parametrize("read_len", [60, 300])
@@ -303,3 +372,49 @@ def test_process_bam_device_pileup_matches_host(tmp_path):
     for o in out[1:]:
         assert o[0] == out[0][0]
         assert o[1] == out[0][1]
+
+
+@pytest.mark.parametrize("max_depth", [0, 1, 2, 50, 333, 2000, 8000])
+@pytest.mark.parametrize("ignore_overlaps", [True, False])
+def test_gpu_plan_caps_and_pairs(tmp_path, max_depth, ignore_overlaps):
+    """spg_bam_plan_build vs spp_pileup_plan_fields over depth caps from 1 (only the first read of each start position)
+    to pysam's 8,000, with and without htslib's mate pairing, on the simulator's 2,000x paired reads (150M, indels,
+    overlapping mates) and on short reads (the sweep's window is min(64, shortest span) positions)."""
+    from covid_spings_variant_caller_amd import synth
+    from covid_spings_variant_caller_amd.pileup import simulate_bam
+    ref = synth.reference(4000, seed=3)
+    for k, kw in enumerate([dict(depth=2000.0), dict(depth=600.0, read_len=40)]):
+        bam = str(tmp_path / f"p{k}.bam")
+        simulate_bam(bam, "NC_045512.2", ref, seed=11 + k, n_threads=8, **kw)
+        got = plan_compare(bam, "NC_045512.2", max_depth=max_depth, ignore_overlaps=ignore_overlaps)
+        assert got is not None
+        if ignore_overlaps:
+            assert got[0] > 0
+        else:
+            assert got[0] == 0
+
+
+def test_gpu_plan_name_groups_and_gaps(tmp_path):
+    """Reads that share a name beyond a pair (secondary-like triples, a mate that is dropped by the cap, a mate freed
+    before its partner arrives) and coverage gaps longer than the sweep's ring: the name-group replay and the sweep's
+    gap handling, vs the host replay and pileup_port."""
+    recs = []
+    rng = np.random.default_rng(5)
+    names = [f"q{i}" for i in range(90)]
+    for i in range(400):
+        pos = 1 + int(rng.integers(0, 300)) if i < 300 else 20000 + int(rng.integers(0, 200))
+        nm = names[int(rng.integers(0, len(names)))]
+        fl = int(rng.choice([0x1 | 0x2 | 0x20, 0x1 | 0x2 | 0x10, 0x1 | 0x2, 0]))
+        mpos = pos + int(rng.integers(-60, 120))
+        recs.append(dict(qname=nm, flag=fl, rname="c", pos=pos, mapq=60, cigar="50M", rnext="=" if fl else "*",
+                         pnext=max(1, mpos) if fl else 0, tlen=int(rng.integers(-300, 300)) if fl else 0,
+                         seq="".join("ACGT"[int(x)] for x in rng.integers(0, 4, 50)),
+                         qual="".join(chr(33 + int(x)) for x in rng.integers(10, 40, 50))))
+    recs.sort(key=lambda r: r["pos"])
+    bam = str(tmp_path / "g.bam")
+    samgen.write_bam(bam, [("c", 30000)], recs, block=4000)
+    for md in (0, 3, 12):
+        got = plan_compare(bam, "c", max_depth=md)
+        assert got is not None
+        port = _port(recs, "c", [("c", 30000)], tmp_path, max_depth=md)
+        assert_same(bam_device_fill(bam, "c", gpu_plan=True, max_depth=md), port)

@@ -11,7 +11,7 @@ import shutil
 import sys
 
 
-def main(src, tag, entries=None, dst="profiles"):
+def main(src, tag, entries=None, dst="profiles", cmd="bench.py --steps 50 --warmup 5"):
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
@@ -45,12 +45,12 @@ def main(src, tag, entries=None, dst="profiles"):
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     with open(os.path.join(dst, f"{tag}_summary.md"), "w") as f:
         f.write(f"# {tag}: rocprofv3 summary of `bench.py` (1x MI355X)\n\n")
-        f.write("Kernel trace (`rocprofv3 --kernel-trace --stats`, bench.py --steps 50 --warmup 5):\n\n")
+        f.write(f"Kernel trace (`rocprofv3 --kernel-trace --stats`, {cmd}):\n\n")
         f.write("| kernel | calls | avg us | min us | max us | % |\n|---|---|---|---|---|---|\n")
         for r in stats:
             f.write(f"| `{r['Name'].split('(')[0]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.1f} | "
                     f"{float(r['MinNs'])/1e3:.1f} | {float(r['MaxNs'])/1e3:.1f} | {float(r['Percentage']):.1f} |\n")
-        f.write("\nPMC (separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes, bench.py --steps 10; "
+        f.write("\nPMC (separate `--pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes of the same command, fewer steps; "
                 "FETCH_SIZE x2 per the gfx950 correction):\n\n")
         f.write("| kernel | read MB/launch | write MB/launch | VGPR | LDS B | scratch |\n|---|---|---|---|---|---|\n")
         for k, r in out.items():
@@ -60,4 +60,5 @@ def main(src, tag, entries=None, dst="profiles"):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None,
+         sys.argv[4] if len(sys.argv) > 4 else "profiles", sys.argv[5] if len(sys.argv) > 5 else "bench.py --steps 50 --warmup 5")
