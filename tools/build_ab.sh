@@ -13,7 +13,7 @@ mkdir -p $L/ab
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$ROOT/include "$@" -c $ROOT/covid-spings-variant-caller_amd/csrc/$SRC \
   -o $L/ab/$N.var.o -Rpass-analysis=kernel-resource-usage 2> $L/ab/$N.remarks
 OBJS=""
-for o in spg_kernels.hip spg_tile.hip spg_lite.hip spg_fill.hip spg_inflate.hip spg_ckpt.hip spg_bam.hip spg_api.cpp spg_multi.cpp; do
+for o in spg_kernels.hip spg_tile.hip spg_lite.hip spg_fill.hip spg_inflate.hip spg_ckpt.hip spg_bam.hip spg_plan.hip spg_api.cpp spg_multi.cpp; do
   [ "$o" = "$SRC" ] || OBJS="$OBJS $L/obj/$o.o"
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -Wl,-z,defs -o $L/ab/$N.so $L/ab/$N.var.o $OBJS -lrccl
