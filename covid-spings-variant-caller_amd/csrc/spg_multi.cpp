@@ -80,8 +80,10 @@ struct spg_multi {
     double rebalance_ratio = 1.25;         // max device load / mean that triggers a re-plan
     int64_t rebalance_max_batches = 256;   // ... while the sample holds at most this many batches
     int64_t n_replans = 0;
-    std::vector<void *> send;              // per device: [16-B table header][cap x spg_candidate]
-    void *recv = nullptr;                  // device 0: n x send size
+    std::vector<void *> send;              // per table slot and device (slot * n + d): [16-B table header][cap records]
+    void *recv[2] = {nullptr, nullptr};    // per table slot, on devices[0]: n x send size
+    std::vector<hipStream_t> tstream;      // per device: the table's gather and copy down (off the context's stream)
+    std::vector<hipEvent_t> tev;           // per device: the table copied out of the context's buffers
     int64_t cap = 0;                       // records per device table copy (grown from the tables seen)
     uint8_t *host[2] = {nullptr, nullptr}; // pinned: n x send size per table slot
     TSlot slot[2];
@@ -167,14 +169,20 @@ int spg_multi_destroy(spg_multi *m) {
     }
     for (uint8_t *h : m->host)
         if (h) (void)hipHostFree(h);
-    for (size_t i = 0; i < m->ctx.size(); i++) {
-        if (m->send.size() > i && m->send[i]) { (void)hipSetDevice(m->dev[i]); (void)hipFree(m->send[i]); }
-        if (m->ctx[i]) spg_destroy(m->ctx[i]);
+    for (size_t i = 0; i < m->send.size(); i++)
+        if (m->send[i]) { (void)hipSetDevice(m->dev[i % m->dev.size()]); (void)hipFree(m->send[i]); }
+    for (size_t i = 0; i < m->tstream.size(); i++) {
+        (void)hipSetDevice(m->dev[i]);
+        if (m->tstream[i]) { (void)hipStreamSynchronize(m->tstream[i]); (void)hipStreamDestroy(m->tstream[i]); }
+        if (m->tev[i]) (void)hipEventDestroy(m->tev[i]);
     }
+    for (size_t i = 0; i < m->ctx.size(); i++)
+        if (m->ctx[i]) spg_destroy(m->ctx[i]);
     for (auto &ring : m->stage)
         for (auto &s : ring)
             if (s.p) (void)hipHostFree(s.p);
-    if (m->recv) { (void)hipSetDevice(m->dev[0]); (void)hipFree(m->recv); }
+    for (void *r : m->recv)
+        if (r) { (void)hipSetDevice(m->dev[0]); (void)hipFree(r); }
     for (ncclComm_t c : m->comm)
         if (c) (void)ncclCommDestroy(c);
     delete m;
@@ -189,7 +197,7 @@ int spg_multi_create(const int *devices, int n, int64_t n_pos, const spg_params 
     m->p = *p;
     m->dev.assign(devices, devices + n);
     m->ctx.assign(n, nullptr);
-    m->send.assign(n, nullptr);
+    m->send.assign(2 * (size_t)n, nullptr);
     m->stage.assign(n, std::vector<Stage>(NSTAGE));
     m->bucket = std::max<int64_t>(64, (n_pos + 65535) / 65536);
     m->w_cur.assign((size_t)((n_pos + m->bucket - 1) / m->bucket), 0);
@@ -598,16 +606,27 @@ static int ensure_table_bufs(spg_multi *m, int64_t need) {
     if (int rc = collect_all(m)) return rc;
     const int64_t cap = std::max<int64_t>({need, m->cap, 1024});
     const size_t per = TABLE_HEAD + sizeof(spg_candidate) * (size_t)cap;
-    for (int d = 0; d < m->n; d++) {
-        MHIP(hipSetDevice(m->dev[d]));
-        if (m->send[d]) MHIP(hipFree(m->send[d]));
-        m->send[d] = nullptr;
-        MHIP(hipMalloc(&m->send[d], per));
+    if (m->tstream.empty()) {
+        m->tstream.assign((size_t)m->n, nullptr);
+        m->tev.assign((size_t)m->n, nullptr);
+        for (int d = 0; d < m->n; d++) {
+            MHIP(hipSetDevice(m->dev[d]));
+            MHIP(hipStreamCreateWithFlags(&m->tstream[(size_t)d], hipStreamNonBlocking));
+            MHIP(hipEventCreateWithFlags(&m->tev[(size_t)d], hipEventDisableTiming));
+        }
+    }
+    for (size_t i = 0; i < m->send.size(); i++) {
+        MHIP(hipSetDevice(m->dev[i % (size_t)m->n]));
+        if (m->send[i]) MHIP(hipFree(m->send[i]));
+        m->send[i] = nullptr;
+        MHIP(hipMalloc(&m->send[i], per));
     }
     MHIP(hipSetDevice(m->dev[0]));
-    if (m->recv) MHIP(hipFree(m->recv));
-    m->recv = nullptr;
-    if (m->rccl) MHIP(hipMalloc(&m->recv, per * (size_t)m->n));
+    for (void *&r : m->recv) {
+        if (r) MHIP(hipFree(r));
+        r = nullptr;
+        if (m->rccl) MHIP(hipMalloc(&r, per * (size_t)m->n));
+    }
     for (uint8_t *&h : m->host) {
         if (h) MHIP(hipHostFree(h));
         h = nullptr;
@@ -617,42 +636,49 @@ static int ensure_table_bufs(spg_multi *m, int64_t need) {
     return 0;
 }
 
-// Enqueue one table into slot t: per device the table + status copied on its own stream (no host wait), ONE
-// ncclGather to devices[0] (distinct devices) or per-device copies, then the bytes into the slot's pinned buffer.
+// Enqueue one table into slot t: per device the table + status copied out of the context's buffers by one small
+// kernel on its stream (the next sample's kernels follow it there), then — on the device's table stream, off the
+// context's — ONE ncclGather to devices[0] (distinct devices) or per-device copies, and the bytes into the slot's
+// pinned buffer.  No host wait.
 static int enqueue_table(spg_multi *m, TSlot &t) {
     const size_t per = TABLE_HEAD + sizeof(spg_candidate) * (size_t)m->cap;
     if (t.ev.empty()) {
         t.ev.assign((size_t)m->n, nullptr);
         t.ev_used.assign((size_t)m->n, 0);
     }
-    uint8_t *h = m->host[&t - m->slot];
-    std::vector<hipStream_t> st((size_t)m->n);
+    const size_t si = (size_t)(&t - m->slot);
+    uint8_t *h = m->host[si];
+    void **send = m->send.data() + si * (size_t)m->n;
     for (int d = 0; d < m->n; d++) {
-        MCTX(spg_stream(m->ctx[d], (void **)&st[(size_t)d]));
+        hipStream_t st = nullptr;
+        MCTX(spg_stream(m->ctx[d], (void **)&st));
         int64_t ncopy = 0;
-        MCTX(spg_copy_table_device(m->ctx[d], m->send[d], m->cap, &ncopy));
+        MCTX(spg_copy_table_device(m->ctx[d], send[d], m->cap, &ncopy));
+        MHIP(hipSetDevice(m->dev[d]));
+        MHIP(hipEventRecord(m->tev[(size_t)d], st));
+        MHIP(hipStreamWaitEvent(m->tstream[(size_t)d], m->tev[(size_t)d], 0));
+        if (!t.ev[(size_t)d]) MHIP(hipEventCreateWithFlags(&t.ev[(size_t)d], hipEventDisableTiming));
     }
     std::fill(t.ev_used.begin(), t.ev_used.end(), 0);
     if (m->rccl) {
         MCCL(ncclGroupStart());
         for (int d = 0; d < m->n; d++) {
             MHIP(hipSetDevice(m->dev[d]));
-            MCCL(ncclGather(m->send[d], d == 0 ? m->recv : nullptr, per, ncclUint8, 0, m->comm[d], st[(size_t)d]));
+            MCCL(ncclGather(send[d], d == 0 ? m->recv[si] : nullptr, per, ncclUint8, 0, m->comm[d], m->tstream[(size_t)d]));
         }
         MCCL(ncclGroupEnd());
         MHIP(hipSetDevice(m->dev[0]));
-        MHIP(hipMemcpyAsync(h, m->recv, per * (size_t)m->n, hipMemcpyDeviceToHost, st[0]));
-        if (!t.ev[0]) MHIP(hipEventCreateWithFlags(&t.ev[0], hipEventDisableTiming));
-        MHIP(hipEventRecord(t.ev[0], st[0]));
-        t.ev_used[0] = 1;
+        MHIP(hipMemcpyAsync(h, m->recv[si], per * (size_t)m->n, hipMemcpyDeviceToHost, m->tstream[0]));
     } else {
         for (int d = 0; d < m->n; d++) {
             MHIP(hipSetDevice(m->dev[d]));
-            MHIP(hipMemcpyAsync(h + per * (size_t)d, m->send[d], per, hipMemcpyDeviceToHost, st[(size_t)d]));
-            if (!t.ev[(size_t)d]) MHIP(hipEventCreateWithFlags(&t.ev[(size_t)d], hipEventDisableTiming));
-            MHIP(hipEventRecord(t.ev[(size_t)d], st[(size_t)d]));
-            t.ev_used[(size_t)d] = 1;
+            MHIP(hipMemcpyAsync(h + per * (size_t)d, send[d], per, hipMemcpyDeviceToHost, m->tstream[(size_t)d]));
         }
+    }
+    for (int d = 0; d < m->n; d++) {           // (every device's send buffer is free once its stream has passed here)
+        MHIP(hipSetDevice(m->dev[d]));
+        MHIP(hipEventRecord(t.ev[(size_t)d], m->tstream[(size_t)d]));
+        t.ev_used[(size_t)d] = 1;
     }
     t.cut = m->ctx_cut;
     t.collected = false;

@@ -70,8 +70,8 @@ __global__ void k_plan_init(PlanHead *h) {
     h->max_span_kept = 0;
     h->err = 0;
     h->n_distinct = h->n_kept = h->n_pairs = 0;
-    h->min_pos = INT64_MAX;
-    h->max_end = INT64_MIN;
+    h->min_pos = INT64_MAX;                      // (both updated with unsigned 64-bit atomics: positions are >= 0)
+    h->max_end = 0;
     h->lo = 0;
     h->hi = 0;
     h->n_entries = h->orig_bytes = 0;
