@@ -134,9 +134,20 @@ __device__ __forceinline__ int32_t wave_incl_scan_i32(int32_t v) {
     return v;
 }
 
-// htslib's depth cap over the distinct start positions in order (one workgroup; see the file comment)
+__device__ __forceinline__ int32_t wave_sum32(int32_t v) {
+    for (int o = 32; o; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// htslib's depth cap over the distinct start positions in order (one workgroup; see the file comment).  Wave 0 decides
+// a window's k values from LDS (the distinct positions and their first reads staged SWEEP_BLK at a time, the ring of
+// kept-read end counts), the k recurrence in scalar registers when the cap can bite; then every wave marks the window's
+// reads and adds the kept ones' ends to the ring (their loads issued SWEEP_U at a time).
+constexpr int SWEEP_BLK = 2048, SWEEP_U = 4;
 __global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
     __shared__ int32_t ring[RING];
+    __shared__ int32_t sdpos[SWEEP_BLK];
+    __shared__ uint32_t sdfirst[SWEEP_BLK + 1];
     __shared__ uint32_t kk[64], ff[64];
     __shared__ int32_t jmap[64];
     __shared__ uint32_t s_r0, s_r1, s_next;
@@ -144,23 +155,32 @@ __global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
     const int tid = threadIdx.x, lane = tid & 63;
     const uint32_t D = A.head->n_distinct;
     const int32_t W0 = min(64, A.head->min_span);
-    const int64_t M = A.maxcnt;
+    const int32_t M = (int32_t)min(A.maxcnt, (int64_t)INT32_MAX);
     for (int i = tid; i < RING; i += SWEEP_T) ring[i] = 0;
-    __syncthreads();
-    int64_t alive = 0;                                 // (wave 0) kept reads not freed yet
+    int32_t alive = 0;                                 // (wave 0) kept reads not freed yet
     int32_t at = D ? A.dpos[0] : 0;                    // (wave 0) frees applied for every end < at
-    uint32_t d = 0;
+    uint32_t d = 0, blk0 = 0, blk1 = 0;                // sdpos / sdfirst hold distinct positions [blk0, blk1)
     while (d < D) {
+        if (d + 65 > blk1 && blk1 < D + 1) {           // (uniform) stage the next block of distinct positions
+            __syncthreads();
+            blk0 = d;
+            blk1 = min(D + 1, d + (uint32_t)SWEEP_BLK);
+            for (uint32_t i = blk0 + (uint32_t)tid; i < blk1; i += SWEEP_T) {
+                sdpos[i - blk0] = i < D ? A.dpos[i] : INT32_MAX;
+                sdfirst[i - blk0] = A.dfirst[i];
+            }
+            __syncthreads();
+        }
         if (tid < 64) {
-            const int32_t P = A.dpos[d];
+            const int32_t P = sdpos[d - blk0];
             const uint32_t idx = d + (uint32_t)lane;
-            const int32_t pj = idx < D ? A.dpos[idx] : INT32_MAX;
+            const int32_t pj = idx < D ? sdpos[idx - blk0] : INT32_MAX;
             const bool valid = idx < D && pj < P + W0;
-            const uint32_t w = (uint32_t)__popcll(__ballot(valid));          // (valid lanes are a prefix)
-            const int32_t plast = __shfl(pj, (int)w - 1, 64);
+            const int w = __popcll(__ballot(valid));                        // (valid lanes are a prefix)
+            const int32_t plast = __builtin_amdgcn_readlane(pj, w - 1);
             // frees of the ends in [at, P): all of them when the gap exceeds the ring
-            int64_t gap = 0;
-            if ((int64_t)P - at >= RING) {
+            int32_t gap = 0;
+            if (P - at >= RING) {
                 for (int i = lane; i < RING; i += 64) ring[i] = 0;
                 gap = alive;
             } else {
@@ -168,7 +188,7 @@ __global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
                     const int32_t s = x + lane;
                     int32_t v = 0;
                     if (s < P) { v = ring[s & (RING - 1)]; ring[s & (RING - 1)] = 0; }
-                    gap += wave_sum64(v);
+                    gap += wave_sum32(v);
                 }
             }
             // frees inside the window: ends in [P, plast), one lane per slot, scanned
@@ -176,24 +196,22 @@ __global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
             if (P + lane < plast) { c = ring[(P + lane) & (RING - 1)]; ring[(P + lane) & (RING - 1)] = 0; }
             const int32_t S = wave_incl_scan_i32(c);
             const int32_t Sj = __shfl(S, valid && pj > P ? pj - P - 1 : 0, 64);
-            const int64_t Fj = gap + (valid && pj > P ? (int64_t)Sj : 0);
-            const int64_t Ftot = gap + (plast > P ? (int64_t)__shfl(S, plast - P - 1, 64) : 0);
-            const uint32_t f0 = valid ? A.dfirst[idx] : 0u, f1 = valid ? A.dfirst[idx + 1] : 0u;
-            const int64_t nj = (int64_t)(f1 - f0);
-            const int64_t sumn = wave_sum64(nj);
-            int64_t k = nj;
-            if (alive + sumn > M) {                    // the cap may bite: k_j = min(n_j, max(1, M - alive_j)) in order
-                int64_t cum = 0;
-                for (uint32_t j = 0; j < w; j++) {
-                    const int64_t fj = (int64_t)__shfl((long long)Fj, (int)j, 64);
-                    const int64_t n_ = (int64_t)__shfl((long long)nj, (int)j, 64);
-                    const int64_t a = alive - fj + cum;
-                    const int64_t kj = min(n_, max((int64_t)1, M - a));
-                    if ((uint32_t)lane == j) k = kj;
+            const int32_t Fj = gap + (valid && pj > P ? Sj : 0);
+            const int32_t Ftot = gap + (plast > P ? __builtin_amdgcn_readlane(S, plast - P - 1) : 0);
+            const uint32_t f0 = valid ? sdfirst[idx - blk0] : 0u, f1 = valid ? sdfirst[idx + 1 - blk0] : 0u;
+            const int32_t nj = (int32_t)(f1 - f0);
+            int32_t k = nj;
+            if ((int64_t)alive + wave_sum32(nj) > (int64_t)M) {
+                // the cap may bite: k_j = min(n_j, max(1, M - alive_j)) in order, in scalar registers
+                int32_t cum = 0;
+                for (int j = 0; j < w; j++) {
+                    const int32_t fj = __builtin_amdgcn_readlane(Fj, j), n_ = __builtin_amdgcn_readlane(nj, j);
+                    const int32_t kj = min(n_, max(1, M - (alive - fj + cum)));
+                    k = lane == j ? kj : k;
                     cum += kj;
                 }
             }
-            alive = alive - Ftot + wave_sum64(valid ? k : 0);
+            alive = alive - Ftot + wave_sum32(valid ? k : 0);
             at = plast;
             jmap[lane] = -1;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -205,19 +223,31 @@ __global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
             }
             if (lane == 0) {
                 s_P = P;
-                s_r0 = A.dfirst[d];
-                s_r1 = A.dfirst[d + w];
-                s_next = d + w;
+                s_r0 = sdfirst[d - blk0];
+                s_r1 = sdfirst[d + (uint32_t)w - blk0];
+                s_next = d + (uint32_t)w;
             }
         }
         __syncthreads();
         const int32_t P = s_P;
         const uint32_t r0 = s_r0, r1 = s_r1;
-        for (uint32_t r = r0 + (uint32_t)tid; r < r1; r += SWEEP_T) {
-            const int j = jmap[A.pos[r] - P];
-            const bool kp = r - ff[j] < kk[j];
-            A.keep[r] = kp ? 1 : 0;
-            if (kp) atomicAdd(&ring[A.end[r] & (RING - 1)], 1);
+        for (uint32_t rb = r0 + (uint32_t)tid; rb < r1; rb += SWEEP_U * SWEEP_T) {
+            int32_t ps[SWEEP_U], es[SWEEP_U];
+#pragma unroll
+            for (int u = 0; u < SWEEP_U; u++) {
+                const uint32_t r = rb + (uint32_t)(u * SWEEP_T);
+                ps[u] = r < r1 ? A.pos[r] : P;
+                es[u] = r < r1 ? A.end[r] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < SWEEP_U; u++) {
+                const uint32_t r = rb + (uint32_t)(u * SWEEP_T);
+                if (r >= r1) continue;
+                const int j = jmap[ps[u] - P];
+                const bool kp = r - ff[j] < kk[j];
+                A.keep[r] = kp ? 1 : 0;
+                if (kp) atomicAdd(&ring[es[u] & (RING - 1)], 1);
+            }
         }
         d = s_next;
         __syncthreads();

@@ -304,7 +304,7 @@ def test_simulated_bams(tmp_path, depth, max_depth):
     assert_same(bam_device_fill(bam, "NC_045512.2", max_depth=max_depth), host)
     assert_same(bam_device_fill(bam, "NC_045512.2", gpu_plan=True, max_depth=max_depth), host)
     n_pairs, n_kept = plan_compare(bam, "NC_045512.2", max_depth=max_depth)
-    assert n_pairs > 0
+    assert n_kept > 0                             # (the simulator's reads are single-end: no pairs)
 
 
 @pytest.mark.parametrize("read_len", [60, 300])
@@ -378,8 +378,9 @@ def test_process_bam_device_pileup_matches_host(tmp_path):
 @pytest.mark.parametrize("ignore_overlaps", [True, False])
 def test_gpu_plan_caps_and_pairs(tmp_path, max_depth, ignore_overlaps):
     """spg_bam_plan_build vs spp_pileup_plan_fields over depth caps from 1 (only the first read of each start position)
-    to pysam's 8,000, with and without htslib's mate pairing, on the simulator's 2,000x paired reads (150M, indels,
-    overlapping mates) and on short reads (the sweep's window is min(64, shortest span) positions)."""
+    to pysam's 8,000, with and without htslib's mate pairing: the simulator's 2,000x single-end reads (150M, indels) and
+    short reads (the sweep's window is min(64, shortest span) positions), and samgen's random reads with overlapping
+    proper pairs, stacks and every CIGAR op."""
     from covid_spings_variant_caller_amd import synth
     from covid_spings_variant_caller_amd.pileup import simulate_bam
     ref = synth.reference(4000, seed=3)
@@ -387,11 +388,16 @@ def test_gpu_plan_caps_and_pairs(tmp_path, max_depth, ignore_overlaps):
         bam = str(tmp_path / f"p{k}.bam")
         simulate_bam(bam, "NC_045512.2", ref, seed=11 + k, n_threads=8, **kw)
         got = plan_compare(bam, "NC_045512.2", max_depth=max_depth, ignore_overlaps=ignore_overlaps)
-        assert got is not None
-        if ignore_overlaps:
-            assert got[0] > 0
-        else:
-            assert got[0] == 0
+        assert got is not None and got[1] > 0
+    contigs = [("chrA", 900)]
+    n_pairs = 0
+    for seed in (21, 22, 23):
+        bam = str(tmp_path / f"r{seed}.bam")
+        samgen.write_bam(bam, contigs, samgen.random_records(seed, contigs, n_reads=600), block=7000)
+        got = plan_compare(bam, "chrA", max_depth=max_depth, ignore_overlaps=ignore_overlaps)
+        if got is not None:
+            n_pairs += got[0]
+    assert (n_pairs > 0) == ignore_overlaps
 
 
 def test_gpu_plan_name_groups_and_gaps(tmp_path):
