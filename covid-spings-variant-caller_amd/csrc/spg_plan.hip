@@ -7,9 +7,9 @@
 //    >= 1 column, the first read at a start position p is always pushed, and the i-th (i >= 1) is dropped iff
 //    B_p + i + 1 > maxcnt, B_p = the kept reads with pos < p and end >= p (spp_pileup.cpp capped_no_pairs).  So
 //    k_p = min(n_p, max(1, maxcnt - B_p)) reads are kept at p, the first ones in BAM order.  k_plan_sweep carries B_p
-//    over the distinct start positions in windows of at most min(64, shortest span) positions: no read kept inside a
-//    window ends inside it, so a window's frees come from a ring of earlier kept reads' end counts (LDS), one lane per
-//    position, and only a window that can reach maxcnt runs the k recurrence lane by lane.
+//    over the distinct start positions in windows of at most min(128, shortest span) positions: no read kept inside a
+//    window ends inside it, so a window's frees come from a ring of earlier kept reads' end counts (LDS), two positions
+//    per lane, and only a window that can reach maxcnt runs the k recurrence position by position.
 //  * The overlap hash (read name -> the first mate waiting) only ever holds one entry per name, and an entry changes
 //    only at events of reads with that name: a push (pair with the entry, or insert), a drop (htslib's olap removal of
 //    the dropped read's name), and a free (the read's end passed: removal of its name).  A free of read y happens
@@ -140,28 +140,30 @@ __device__ __forceinline__ int32_t wave_sum32(int32_t v) {
 }
 
 // htslib's depth cap over the distinct start positions in order (one workgroup; see the file comment).  Wave 0 decides
-// a window's k values from LDS (the distinct positions and their first reads staged SWEEP_BLK at a time, the ring of
-// kept-read end counts), the k recurrence in scalar registers when the cap can bite; then every wave marks the window's
-// reads and adds the kept ones' ends to the ring (their loads issued SWEEP_U at a time).
-constexpr int SWEEP_BLK = 2048, SWEEP_U = 4;
+// a window's k values — up to SWEEP_W positions, two per lane — from LDS (the distinct positions and their first reads
+// staged SWEEP_BLK at a time, the ring of kept-read end counts), the k recurrence in scalar registers when the cap can
+// bite; then every wave marks the window's reads and adds the kept ones' ends to the ring (each thread SWEEP_U
+// consecutive reads, their loads issued together; neighbouring lanes' reads start at different positions, so the ring
+// atomics of one instruction spread over many end slots).
+constexpr int SWEEP_BLK = 2048, SWEEP_U = 4, SWEEP_W = 128;
 __global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
     __shared__ int32_t ring[RING];
     __shared__ int32_t sdpos[SWEEP_BLK];
     __shared__ uint32_t sdfirst[SWEEP_BLK + 1];
-    __shared__ uint32_t kk[64], ff[64];
-    __shared__ int32_t jmap[64];
+    __shared__ uint32_t kk[SWEEP_W], ff[SWEEP_W];
+    __shared__ int32_t jmap[SWEEP_W];
     __shared__ uint32_t s_r0, s_r1, s_next;
     __shared__ int32_t s_P;
     const int tid = threadIdx.x, lane = tid & 63;
     const uint32_t D = A.head->n_distinct;
-    const int32_t W0 = min(64, A.head->min_span);
+    const int32_t W0 = min(SWEEP_W, A.head->min_span);
     const int32_t M = (int32_t)min(A.maxcnt, (int64_t)INT32_MAX);
     for (int i = tid; i < RING; i += SWEEP_T) ring[i] = 0;
     int32_t alive = 0;                                 // (wave 0) kept reads not freed yet
     int32_t at = D ? A.dpos[0] : 0;                    // (wave 0) frees applied for every end < at
     uint32_t d = 0, blk0 = 0, blk1 = 0;                // sdpos / sdfirst hold distinct positions [blk0, blk1)
     while (d < D) {
-        if (d + 65 > blk1 && blk1 < D + 1) {           // (uniform) stage the next block of distinct positions
+        if (d + SWEEP_W + 1 > blk1 && blk1 < D + 1) {  // (uniform) stage the next block of distinct positions
             __syncthreads();
             blk0 = d;
             blk1 = min(D + 1, d + (uint32_t)SWEEP_BLK);
@@ -173,11 +175,12 @@ __global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
         }
         if (tid < 64) {
             const int32_t P = sdpos[d - blk0];
-            const uint32_t idx = d + (uint32_t)lane;
-            const int32_t pj = idx < D ? sdpos[idx - blk0] : INT32_MAX;
-            const bool valid = idx < D && pj < P + W0;
-            const int w = __popcll(__ballot(valid));                        // (valid lanes are a prefix)
-            const int32_t plast = __builtin_amdgcn_readlane(pj, w - 1);
+            // window positions j = lane (half 0) and j = 64 + lane (half 1)
+            const uint32_t ia = d + (uint32_t)lane, ib = ia + 64;
+            const int32_t pa = ia < D ? sdpos[ia - blk0] : INT32_MAX, pb = ib < D ? sdpos[ib - blk0] : INT32_MAX;
+            const bool va = ia < D && pa < P + W0, vb = ib < D && pb < P + W0;
+            const int w = __popcll(__ballot(va)) + __popcll(__ballot(vb));          // (valid positions are a prefix)
+            const int32_t plast = w > 64 ? __builtin_amdgcn_readlane(pb, w - 65) : __builtin_amdgcn_readlane(pa, w - 1);
             // frees of the ends in [at, P): all of them when the gap exceeds the ring
             int32_t gap = 0;
             if (P - at >= RING) {
@@ -191,36 +194,48 @@ __global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
                     gap += wave_sum32(v);
                 }
             }
-            // frees inside the window: ends in [P, plast), one lane per slot, scanned
-            int32_t c = 0;
-            if (P + lane < plast) { c = ring[(P + lane) & (RING - 1)]; ring[(P + lane) & (RING - 1)] = 0; }
-            const int32_t S = wave_incl_scan_i32(c);
-            const int32_t Sj = __shfl(S, valid && pj > P ? pj - P - 1 : 0, 64);
-            const int32_t Fj = gap + (valid && pj > P ? Sj : 0);
-            const int32_t Ftot = gap + (plast > P ? __builtin_amdgcn_readlane(S, plast - P - 1) : 0);
-            const uint32_t f0 = valid ? sdfirst[idx - blk0] : 0u, f1 = valid ? sdfirst[idx + 1 - blk0] : 0u;
-            const int32_t nj = (int32_t)(f1 - f0);
-            int32_t k = nj;
-            if ((int64_t)alive + wave_sum32(nj) > (int64_t)M) {
+            // frees inside the window: ends in [P, plast), two slots per lane, scanned
+            int32_t c0 = 0, c1 = 0;
+            if (P + lane < plast) { c0 = ring[(P + lane) & (RING - 1)]; ring[(P + lane) & (RING - 1)] = 0; }
+            if (P + 64 + lane < plast) { c1 = ring[(P + 64 + lane) & (RING - 1)]; ring[(P + 64 + lane) & (RING - 1)] = 0; }
+            const int32_t S0 = wave_incl_scan_i32(c0);
+            const int32_t S1 = wave_incl_scan_i32(c1) + __builtin_amdgcn_readlane(S0, 63);
+            // frees before position p: the scan at slot p - P - 1 (none when p == P)
+            auto freed = [&](int32_t p) -> int32_t {
+                const int32_t o = p - P - 1;
+                const int32_t a = __shfl(S0, o & 63, 64), b = __shfl(S1, o & 63, 64);
+                return o < 0 ? 0 : (o < 64 ? a : b);
+            };
+            const int32_t Fa = gap + freed(va ? pa : P), Fb = gap + freed(vb ? pb : P);
+            const int32_t o_last = plast - P - 1;
+            const int32_t Ftot = gap + (o_last < 0 ? 0 : o_last < 64 ? __builtin_amdgcn_readlane(S0, o_last)
+                                                                      : __builtin_amdgcn_readlane(S1, o_last - 64));
+            const uint32_t fa0 = va ? sdfirst[ia - blk0] : 0u, fa1 = va ? sdfirst[ia + 1 - blk0] : 0u;
+            const uint32_t fb0 = vb ? sdfirst[ib - blk0] : 0u, fb1 = vb ? sdfirst[ib + 1 - blk0] : 0u;
+            const int32_t na = (int32_t)(fa1 - fa0), nb = (int32_t)(fb1 - fb0);
+            int32_t ka = na, kb = nb;
+            if ((int64_t)alive + wave_sum32(na + nb) > (int64_t)M) {
                 // the cap may bite: k_j = min(n_j, max(1, M - alive_j)) in order, in scalar registers
                 int32_t cum = 0;
                 for (int j = 0; j < w; j++) {
-                    const int32_t fj = __builtin_amdgcn_readlane(Fj, j), n_ = __builtin_amdgcn_readlane(nj, j);
+                    const bool hb = j >= 64;
+                    const int jl = j & 63;
+                    const int32_t fj = hb ? __builtin_amdgcn_readlane(Fb, jl) : __builtin_amdgcn_readlane(Fa, jl);
+                    const int32_t n_ = hb ? __builtin_amdgcn_readlane(nb, jl) : __builtin_amdgcn_readlane(na, jl);
                     const int32_t kj = min(n_, max(1, M - (alive - fj + cum)));
-                    k = lane == j ? kj : k;
+                    if (hb) kb = lane == jl ? kj : kb;
+                    else ka = lane == jl ? kj : ka;
                     cum += kj;
                 }
             }
-            alive = alive - Ftot + wave_sum32(valid ? k : 0);
+            alive = alive - Ftot + wave_sum32((va ? ka : 0) + (vb ? kb : 0));
             at = plast;
             jmap[lane] = -1;
+            jmap[64 + lane] = -1;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_wave_barrier();
-            if (valid) {
-                kk[lane] = (uint32_t)k;
-                ff[lane] = f0;
-                jmap[pj - P] = lane;
-            }
+            if (va) { kk[lane] = (uint32_t)ka; ff[lane] = fa0; jmap[pa - P] = lane; }
+            if (vb) { kk[64 + lane] = (uint32_t)kb; ff[64 + lane] = fb0; jmap[pb - P] = 64 + lane; }
             if (lane == 0) {
                 s_P = P;
                 s_r0 = sdfirst[d - blk0];
@@ -231,17 +246,17 @@ __global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
         __syncthreads();
         const int32_t P = s_P;
         const uint32_t r0 = s_r0, r1 = s_r1;
-        for (uint32_t rb = r0 + (uint32_t)tid; rb < r1; rb += SWEEP_U * SWEEP_T) {
+        for (uint32_t rb = r0 + (uint32_t)(SWEEP_U * tid); rb < r1; rb += SWEEP_U * SWEEP_T) {
             int32_t ps[SWEEP_U], es[SWEEP_U];
 #pragma unroll
             for (int u = 0; u < SWEEP_U; u++) {
-                const uint32_t r = rb + (uint32_t)(u * SWEEP_T);
+                const uint32_t r = rb + (uint32_t)u;
                 ps[u] = r < r1 ? A.pos[r] : P;
                 es[u] = r < r1 ? A.end[r] : 0;
             }
 #pragma unroll
             for (int u = 0; u < SWEEP_U; u++) {
-                const uint32_t r = rb + (uint32_t)(u * SWEEP_T);
+                const uint32_t r = rb + (uint32_t)u;
                 if (r >= r1) continue;
                 const int j = jmap[ps[u] - P];
                 const bool kp = r - ff[j] < kk[j];
