@@ -215,16 +215,21 @@ __global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
             const int32_t na = (int32_t)(fa1 - fa0), nb = (int32_t)(fb1 - fb0);
             int32_t ka = na, kb = nb;
             if ((int64_t)alive + wave_sum32(na + nb) > (int64_t)M) {
-                // the cap may bite: k_j = min(n_j, max(1, M - alive_j)) in order, in scalar registers
+                // the cap may bite: k_j = min(n_j, max(1, M - alive_j)) in order, in scalar registers (no branch in the
+                // loop bodies: one per half of the window)
+                const int32_t base = __builtin_amdgcn_readfirstlane(alive);
                 int32_t cum = 0;
-                for (int j = 0; j < w; j++) {
-                    const bool hb = j >= 64;
-                    const int jl = j & 63;
-                    const int32_t fj = hb ? __builtin_amdgcn_readlane(Fb, jl) : __builtin_amdgcn_readlane(Fa, jl);
-                    const int32_t n_ = hb ? __builtin_amdgcn_readlane(nb, jl) : __builtin_amdgcn_readlane(na, jl);
-                    const int32_t kj = min(n_, max(1, M - (alive - fj + cum)));
-                    if (hb) kb = lane == jl ? kj : kb;
-                    else ka = lane == jl ? kj : ka;
+                const int wa = min(w, 64);
+                for (int j = 0; j < wa; j++) {
+                    const int32_t fj = __builtin_amdgcn_readlane(Fa, j), n_ = __builtin_amdgcn_readlane(na, j);
+                    const int32_t kj = min(n_, max(1, M - (base - fj + cum)));
+                    ka = lane == j ? kj : ka;
+                    cum += kj;
+                }
+                for (int j = 64; j < w; j++) {
+                    const int32_t fj = __builtin_amdgcn_readlane(Fb, j - 64), n_ = __builtin_amdgcn_readlane(nb, j - 64);
+                    const int32_t kj = min(n_, max(1, M - (base - fj + cum)));
+                    kb = lane == j - 64 ? kj : kb;
                     cum += kj;
                 }
             }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # inflate_ab_run.sh <outdir> <variant>...: tools/inflate_bench.py (the 10,000x BAM's BGZF members through
 # spg_bgzf_inflate: kernel ms, identity vs gzip) on the in-tree library ("default") and on A/B builds of
-# tools/inflate_ab.py (_lib/ab/<variant>.so), interleaved twice.  Each run under its own limit; stops at the first failure.
+# tools/src_ab.py (_lib/ab/<variant>.so), interleaved twice.  Each run under its own limit; stops at the first failure.
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/$1
 shift

@@ -1,8 +1,11 @@
-"""inflate_ab.py <name> <edit>...: an A/B build of libspings_gpu.so whose spg_inflate.hip is the product source with
-textual edits applied (diagnostics stay out of the product sources), the other objects shared with the in-tree build
--> _lib/ab/<name>.so; run tools/inflate_bench.py against it with tools/ab_run.py.  Edits (named):
+"""inflate_ab.py <name> <edit>...: an A/B build of libspings_gpu.so whose source (spg_inflate.hip, or the edit's own) is
+the product source with textual edits applied (diagnostics stay out of the product sources), the other objects shared
+with the in-tree build -> _lib/ab/<name>.so; run a dev script (tools/inflate_bench.py, tools/plan_bench.py) against it
+with tools/ab_run.py.  Edits (named):
   noresolve  k_inflate_par skips phase B (the token lists are decoded and synchronised, nothing resolved): phase A +
              sync time; the output is garbage (k_crc32 then flags every member).
+  sweep_nok  (spg_plan.hip) the depth-cap sweep skips its k recurrence (k = n): its cost; the plan is wrong.
+  sweep_noatom (spg_plan.hip) the sweep marks reads but adds no ends to the ring: the atomics' cost; the plan is wrong.
 Dev tool only."""
 import os
 import subprocess
@@ -12,7 +15,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "covid-spings-variant-caller_amd", "csrc")
 LIB = os.path.join(ROOT, "covid-spings-variant-caller_amd", "_lib")
 
+SRC_OF = {"sweep_nok": "spg_plan.hip", "sweep_noatom": "spg_plan.hip"}
 EDITS = {
+    "sweep_nok": [("            if ((int64_t)alive + wave_sum32(na + nb) > (int64_t)M) {",
+                   "            if ((int64_t)alive + wave_sum32(na + nb) > (int64_t)M && M < 0) {")],
+    "sweep_noatom": [("                if (kp) atomicAdd(&ring[es[u] & (RING - 1)], 1);",
+                      "                if (kp && es[u] < 0) atomicAdd(&ring[es[u] & (RING - 1)], 1);")],
     "noresolve": [("        for (int k = 0; k <= kend && !st; k++) {",
                    "        for (int k = 0; k <= kend && !st && kend < 0; k++) {"),
                   ("    if (!st && w != ulen) st = ST_FALLBACK;", "    if (!st) w = ulen;")],
@@ -21,20 +29,21 @@ EDITS = {
 
 def main():
     name, edits = sys.argv[1], sys.argv[2:]
-    src = open(os.path.join(CSRC, "spg_inflate.hip")).read()
+    srcname = SRC_OF.get(edits[0], "spg_inflate.hip") if edits else "spg_inflate.hip"
+    src = open(os.path.join(CSRC, srcname)).read()
     for e in edits:
         for a, b in EDITS[e]:
             assert src.count(a) == 1, (e, a)
             src = src.replace(a, b)
     os.makedirs(os.path.join(LIB, "ab"), exist_ok=True)
-    var = os.path.join(LIB, "ab", f"{name}_spg_inflate.hip")
+    var = os.path.join(LIB, "ab", f"{name}_{srcname}")
     open(var, "w").write(src)
     obj = os.path.join(LIB, "ab", f"{name}.var.o")
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
                            f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}", "-c", var, "-o", obj])
     objs = [os.path.join(LIB, "obj", f + ".o") for f in ("spg_kernels.hip", "spg_tile.hip", "spg_lite.hip", "spg_fill.hip",
-                                                         "spg_ckpt.hip", "spg_bam.hip", "spg_plan.hip", "spg_api.cpp",
-                                                         "spg_multi.cpp")]
+                                                         "spg_inflate.hip", "spg_ckpt.hip", "spg_bam.hip", "spg_plan.hip",
+                                                         "spg_api.cpp", "spg_multi.cpp") if f != srcname]
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-Wl,-z,defs", "-o",
                            os.path.join(LIB, "ab", f"{name}.so"), obj] + objs + ["-lrccl"])
     print(os.path.join(LIB, "ab", f"{name}.so"))
