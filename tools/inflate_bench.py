@@ -57,6 +57,11 @@ for r in range(4):
     L.spg_bgzf_fallbacks(0, C.byref(fb))
     res["runs"].append({"kernel_ms": ms.value, "call_ms": dt * 1e3, "bad_members": int((st != 0).sum()),
                         "lane_kernel_members": fb.value})
+    if hasattr(L, "spg_ab_prof"):              # (tools/src_ab.py prof build: k_inflate_par's phase clocks per member)
+        pr = (C.c_uint64 * 8)()
+        L.spg_ab_prof(pr)
+        names = ["tables", "phase_a", "sync", "phase_b", "member", "members", "blocks"]
+        res["runs"][-1]["clocks_per_member"] = {k: pr[i] / max(1, pr[5]) for i, k in enumerate(names)}
 t = time.perf_counter()
 ref_bytes = gzip.decompress(raw)
 res["gzip_1core_ms"] = (time.perf_counter() - t) * 1e3

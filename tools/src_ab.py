@@ -6,6 +6,7 @@ with tools/ab_run.py.  Edits (named):
              sync time; the output is garbage (k_crc32 then flags every member).
   sweep_nok  (spg_plan.hip) the depth-cap sweep skips its k recurrence (k = n): its cost; the plan is wrong.
   sweep_noatom (spg_plan.hip) the sweep marks reads but adds no ends to the ring: the atomics' cost; the plan is wrong.
+  prof       k_inflate_par's phases timed with the shader clock (spg_ab_prof; tools/inflate_bench.py reports them).
 Dev tool only."""
 import os
 import subprocess
@@ -16,7 +17,37 @@ CSRC = os.path.join(ROOT, "covid-spings-variant-caller_amd", "csrc")
 LIB = os.path.join(ROOT, "covid-spings-variant-caller_amd", "_lib")
 
 SRC_OF = {"sweep_nok": "spg_plan.hip", "sweep_noatom": "spg_plan.hip"}
+PROF_EXPORT = """
+extern "C" int spg_ab_prof(uint64_t *out8) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(spg::g_ab_prof), 8 * sizeof(uint64_t)) != hipSuccess) return -1;
+    static const uint64_t zero[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(spg::g_ab_prof), zero, sizeof zero) == hipSuccess ? 0 : -1;
+}
+"""
 EDITS = {
+    # k_inflate_par's phases timed with the shader clock (summed over members, lane 0): [0] block tables, [1] phase A,
+    # [2] sync rounds, [3] phase B (resolve), [4] whole member, [5] members, [6] blocks
+    "prof": [("__device__ __forceinline__ uint32_t ring_slot(uint32_t g0, uint32_t x) {",
+              "__device__ unsigned long long g_ab_prof[8];\n"
+              "__device__ __forceinline__ uint32_t ring_slot(uint32_t g0, uint32_t x) {"),
+             ("    uint32_t w = 0, flushed = 0, p = pay0, st = 0;",
+              "    uint32_t w = 0, flushed = 0, p = pay0, st = 0;\n    const uint64_t tp0 = clock64();"),
+             ("        const uint32_t hs = block_tables(B, slice, type, fixed_built);",
+              "        const uint64_t t_a = clock64();\n        const uint32_t hs = block_tables(B, slice, type, fixed_built);"),
+             ("        if (hs != 0) { st = ST_FALLBACK; break; }",
+              "        if (hs != 0) { st = ST_FALLBACK; break; }\n        const uint64_t t_b = clock64();\n"
+              "        if (lane == 0) { atomicAdd(&g_ab_prof[0], t_b - t_a); atomicAdd(&g_ab_prof[6], 1ull); }"),
+             ("        __builtin_amdgcn_wave_barrier();\n        // sync rounds",
+              "        const uint64_t t_c = clock64();\n        if (lane == 0) atomicAdd(&g_ab_prof[1], t_c - t_b);\n"
+              "        __builtin_amdgcn_wave_barrier();\n        // sync rounds"),
+             ("        const bool bad = (uint32_t)lane < K && (so.ovf || sy.fail);",
+              "        const uint64_t t_d = clock64();\n        if (lane == 0) atomicAdd(&g_ab_prof[2], t_d - t_c);\n"
+              "        const bool bad = (uint32_t)lane < K && (so.ovf || sy.fail);"),
+             ("        if (st) break;\n        p = pnext;",
+              "        if (st) break;\n        if (lane == 0) atomicAdd(&g_ab_prof[3], clock64() - t_d);\n        p = pnext;"),
+             ("    if (!st) flush(ulen);\n",
+              "    if (!st) flush(ulen);\n    if (lane == 0) { atomicAdd(&g_ab_prof[4], clock64() - tp0); atomicAdd(&g_ab_prof[5], 1ull); }\n"),
+             ("}  // namespace spg\n\n// ---", "}  // namespace spg\n" + "@@EXPORT@@" + "\n// ---")],
     "sweep_nok": [("            if ((int64_t)alive + wave_sum32(na + nb) > (int64_t)M) {",
                    "            if ((int64_t)alive + wave_sum32(na + nb) > (int64_t)M && M < 0) {")],
     "sweep_noatom": [("                if (kp) atomicAdd(&ring[es[u] & (RING - 1)], 1);",
@@ -34,7 +65,7 @@ def main():
     for e in edits:
         for a, b in EDITS[e]:
             assert src.count(a) == 1, (e, a)
-            src = src.replace(a, b)
+            src = src.replace(a, b.replace("@@EXPORT@@", PROF_EXPORT))
     os.makedirs(os.path.join(LIB, "ab"), exist_ok=True)
     var = os.path.join(LIB, "ab", f"{name}_{srcname}")
     open(var, "w").write(src)
