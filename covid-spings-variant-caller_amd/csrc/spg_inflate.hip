@@ -171,6 +171,135 @@ __host__ __device__ __forceinline__ bool build(uint16_t *tab, int cap, uint16_t 
     return true;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// build() by the 64 lanes of a wave at once (k_inflate_par: every lane used to run the serial build, ~16 % of a member's
+// time at 347k clocks per block, r06 tools/src_ab.py prof): lane l holds the lengths of symbols l, l + 64, ...; the
+// counts per length by ballots, each symbol's canonical code from its rank among the symbols of its length (ballot +
+// mbcnt), the root entries of codes <= pb bits written by their own lanes; the codes longer than pb (zlib's sub-table
+// layout, usually a few dozen) then by the serial loop on every lane alike.  The same tables as build().
+__device__ __forceinline__ bool build_wave(uint16_t *tab, int cap, uint16_t *count, uint16_t *sym, const uint8_t *len, int n,
+                                           int pb) {
+    // per-length values live in lanes 0..15 (lane l: length l), not in scalar arrays (which spilled SGPRs kernel-wide)
+    constexpr int NCH = 5;                               // n <= 320 symbols
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t L[NCH];
+#pragma unroll
+    for (int i = 0; i < NCH; i++) L[i] = (int)lane + 64 * i < n ? len[lane + 64 * i] : 0xFFu;
+    uint32_t cntv = 0;                                   // lane l: symbols of length l
+#pragma unroll
+    for (int i = 0; i < NCH; i++)
+#pragma unroll 1
+        for (uint32_t l = 0; l < 16; l++) {
+            const uint32_t c = (uint32_t)__popcll(__ballot(L[i] == l));
+            cntv += lane == l ? c : 0u;
+        }
+    uint64_t *p8 = reinterpret_cast<uint64_t *>(tab);
+    for (int i = (int)lane; i < (1 << pb) / 4; i += 64) p8[i] = 0;
+    if ((int)__builtin_amdgcn_readlane(cntv, 0) == n) return true;   // no codes: every lookup fails (only a distance code may)
+    // Kraft (over-subscribed at any length; incomplete with more than one symbol), the lengths' first canonical codes and
+    // offsets in the sorted symbol list, the codes longer than pb
+    int left = 1;
+    bool over = false;
+    uint32_t o = 0, code = 0, offv = 0, fcv = 0, nlong = 0;
+#pragma unroll 1
+    for (uint32_t l = 1; l < 16; l++) {
+        const uint32_t c = __builtin_amdgcn_readlane(cntv, l);
+        left = (left << 1) - (int)c;
+        over |= left < 0;
+        offv = lane == l ? o : offv;
+        fcv = lane == l ? code : fcv;
+        o += c;
+        code = (code + c) << 1;
+        nlong += l > (uint32_t)pb ? c : 0u;
+    }
+    if (over) return false;
+    if (left > 0 && n - (int)__builtin_amdgcn_readlane(cntv, 0) > 1) return false;
+    // each symbol's rank among the symbols of its length (canonical order = by length, then by symbol): the earlier
+    // chunks' count of its length (basev, lane l) + its rank in this chunk (mbcnt of the length's ballot)
+    uint32_t code_of[NCH];
+    uint32_t basev = 0;
+#pragma unroll
+    for (int i = 0; i < NCH; i++) {
+        uint32_t rin = 0, chunkc = 0;
+#pragma unroll 1
+        for (uint32_t l = 1; l < 16; l++) {
+            const uint64_t mk = __ballot(L[i] == l);
+            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+            rin = L[i] == l ? r : rin;
+            chunkc = lane == l ? (uint32_t)__popcll(mk) : chunkc;
+        }
+        const int li = (int)(L[i] & 15u);
+        const uint32_t b = (uint32_t)__shfl((int)basev, li, 64), of = (uint32_t)__shfl((int)offv, li, 64),
+                       f = (uint32_t)__shfl((int)fcv, li, 64);
+        code_of[i] = 0;
+        if (L[i] >= 1 && L[i] < 16) {
+            sym[of + b + rin] = (uint16_t)(lane + 64 * i);
+            code_of[i] = f + b + rin;
+        }
+        basev += chunkc;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // root entries of the codes of <= pb bits, by their own lanes
+#pragma unroll
+    for (int i = 0; i < NCH; i++) {
+        const uint32_t l = L[i];
+        if (l >= 1 && l <= (uint32_t)pb) {
+            const uint32_t rev = __builtin_bitreverse32(code_of[i]) >> (32 - l);
+            const uint16_t e = (uint16_t)((lane + 64 * i) | (l << 9));
+            for (uint32_t x = rev; x < (1u << pb); x += 1u << l) tab[x] = e;
+        }
+    }
+    if (nlong) {
+        // the codes longer than pb in canonical order, as build()'s loop places them (count[]: the codes of each length
+        // not yet placed, which its sub-table sizing reads)
+        if (lane < 16) count[lane] = (uint16_t)cntv;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t cd = __builtin_amdgcn_readlane(fcv, pb + 1), prefix = ~0u, sub = 0, sbits = 0;
+        int next = 1 << pb, k = (int)__builtin_amdgcn_readlane(offv, pb + 1);
+        for (int l = pb + 1; l <= 15; l++) {
+            for (; count[l]; count[l]--, k++, cd++) {
+                const uint32_t rev = __builtin_bitreverse32(cd) >> (32 - l);
+                const uint16_t e = (uint16_t)(sym[k] | (l << 9));
+                const uint32_t pre = rev & ((1u << pb) - 1);
+                if (pre != prefix) {
+                    uint32_t cur = (uint32_t)(l - pb);
+                    int lf = 1 << cur;
+                    while ((int)cur + pb < 15) {
+                        lf -= count[cur + pb];
+                        if (lf <= 0) break;
+                        cur++;
+                        lf <<= 1;
+                    }
+                    if (next + (1 << cur) > cap) return false;
+                    for (int x = 0; x < (1 << cur); x++) tab[next + x] = 0;
+                    tab[pre] = (uint16_t)(0x8000u | cur << 11 | (uint32_t)next);
+                    prefix = pre;
+                    sub = (uint32_t)next;
+                    sbits = cur;
+                    next += 1 << cur;
+                }
+                for (uint32_t x = rev >> pb; x < (1u << sbits); x += 1u << (l - pb)) tab[sub + x] = e;
+            }
+            cd <<= 1;
+        }
+    }
+    return true;
+}
+#endif
+
+template <bool WAVE>
+__host__ __device__ __forceinline__ bool build_t(uint16_t *tab, int cap, uint16_t *count, uint16_t *sym, const uint8_t *len,
+                                                 int n, int pb) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (WAVE) return build_wave(tab, cap, count, sym, len, n, pb);
+#endif
+    return build(tab, cap, count, sym, len, n, pb);
+}
+
 // one symbol; -1 on an invalid code.  Needs >= 15 bits in the buffer (the caller's fill()).
 __host__ __device__ __forceinline__ int decode(IBits &B, const uint16_t *tab, int pb) {
     uint32_t e = tab[B.peek(pb)];
@@ -196,6 +325,7 @@ __host__ __device__ __forceinline__ uint32_t dist_base(int d) {
 // slice; status 0, 3 bad code lengths, 4 bad table.  fixed_built: the fixed tables are still in the slice (a member's
 // later fixed blocks skip the rebuild).  The device's parallel inflater runs it on every lane of a wave alike (the same
 // bits, the same LDS writes).
+template <bool WAVE = false>
 __host__ __device__ __forceinline__ uint32_t block_tables(IBits &B, uint8_t *slice, uint32_t type, bool &fixed_built) {
     uint16_t *const litp = reinterpret_cast<uint16_t *>(slice + SL_LITP);
     uint16_t *const distp = reinterpret_cast<uint16_t *>(slice + SL_DISTP);
@@ -205,9 +335,9 @@ __host__ __device__ __forceinline__ uint32_t block_tables(IBits &B, uint8_t *sli
     if (type == 1) {                                     // the fixed codes (RFC 1951 3.2.6), built once per member
         if (!fixed_built) {
             for (int s = 0; s < 288; s++) lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
-            build(litp, TAB_LIT, cnt, sym, lens, 288, IB_LIT);
+            build_t<WAVE>(litp, TAB_LIT, cnt, sym, lens, 288, IB_LIT);
             for (int s = 0; s < 32; s++) lens[s] = 5;    // (30 and 31 complete the code; decoding them fails)
-            build(distp, TAB_DIST, cnt, sym, lens, 32, IB_DIST);
+            build_t<WAVE>(distp, TAB_DIST, cnt, sym, lens, 32, IB_DIST);
             fixed_built = true;
         }
         return 0;
@@ -220,7 +350,7 @@ __host__ __device__ __forceinline__ uint32_t block_tables(IBits &B, uint8_t *sli
         const int ord = i < 3 ? 16 + i : i == 3 ? 0 : (i & 1) ? 7 - (i - 5) / 2 : 8 + (i - 4) / 2;   // RFC 1951 3.2.7
         cl[ord] = (uint8_t)B.get(3);
     }
-    if (!build(litp, TAB_LIT, cnt, sym, cl, 19, IB_CL)) return 3;
+    if (!build_t<WAVE>(litp, TAB_LIT, cnt, sym, cl, 19, IB_CL)) return 3;
     int k = 0;
     while (k < hlit + hdist) {
         B.fill();
@@ -242,7 +372,8 @@ __host__ __device__ __forceinline__ uint32_t block_tables(IBits &B, uint8_t *sli
         while (rep--) lens[k++] = v;
     }
     if (lens[256] == 0) return 3;                        // no end-of-block code
-    if (!build(distp, TAB_DIST, cnt, sym, lens + hlit, hdist, IB_DIST) || !build(litp, TAB_LIT, cnt, sym, lens, hlit, IB_LIT))
+    if (!build_t<WAVE>(distp, TAB_DIST, cnt, sym, lens + hlit, hdist, IB_DIST) ||
+        !build_t<WAVE>(litp, TAB_LIT, cnt, sym, lens, hlit, IB_LIT))
         return 4;
     return 0;
 }
@@ -751,8 +882,8 @@ __global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ 
         bfinal = (int)B.get(1);
         const uint32_t type = B.get(2);
         if (type == 0 || type == 3) { st = ST_FALLBACK; break; }
-        // (every lane reads the same header and writes the same tables)
-        const uint32_t hs = block_tables(B, slice, type, fixed_built);
+        // (every lane reads the same header; the tables are built by the whole wave: build_wave)
+        const uint32_t hs = block_tables<true>(B, slice, type, fixed_built);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

@@ -32,8 +32,8 @@ EDITS = {
               "__device__ __forceinline__ uint32_t ring_slot(uint32_t g0, uint32_t x) {"),
              ("    uint32_t w = 0, flushed = 0, p = pay0, st = 0;",
               "    uint32_t w = 0, flushed = 0, p = pay0, st = 0;\n    const uint64_t tp0 = clock64();"),
-             ("        const uint32_t hs = block_tables(B, slice, type, fixed_built);",
-              "        const uint64_t t_a = clock64();\n        const uint32_t hs = block_tables(B, slice, type, fixed_built);"),
+             ("        const uint32_t hs = block_tables<true>(B, slice, type, fixed_built);",
+              "        const uint64_t t_a = clock64();\n        const uint32_t hs = block_tables<true>(B, slice, type, fixed_built);"),
              ("        if (hs != 0) { st = ST_FALLBACK; break; }",
               "        if (hs != 0) { st = ST_FALLBACK; break; }\n        const uint64_t t_b = clock64();\n"
               "        if (lane == 0) { atomicAdd(&g_ab_prof[0], t_b - t_a); atomicAdd(&g_ab_prof[6], 1ull); }"),
