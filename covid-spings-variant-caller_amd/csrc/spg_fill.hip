@@ -534,11 +534,18 @@ __global__ __launch_bounds__(256) void k_f2_base(FillArgs A, F2Lay L) {
 // r05 form kept 8-byte windows in registers with the next one in flight; a refill in any lane waited for every memory
 // operation the wave had issued, its entry stores included — about one L2 round trip per column, 1.12 ms per
 // 10,000x BAM.)  A chunk whose ranges exceed F2_LDS takes those windows.
+//
+// F2_NW waves share a chunk (one workgroup): they copy its bytes into the one LDS image together (a quarter of the 16-B
+// blocks each, all of a wave's loads in flight at once) and then each fills a contiguous quarter of the chunk's column
+// span, every lane catching its CIGAR cursor up to the wave's first column on the way.  With one wave per chunk the
+// 20 KiB image allowed 2 waves per SIMD, and a wave's ~46 us (the copy's round trips, then ~150 dependent column steps)
+// was mostly waiting: r06j PMC, 31,152 waves, VALU 6.8k per wave — 0.77 ms per 10,000x BAM.
 constexpr uint32_t F2_LDS = 20480;
+constexpr int F2_NW = 4;
 
-__global__ __launch_bounds__(64) void k_f2_fill(FillArgs A, F2Lay L) {
+__global__ __launch_bounds__(64 * F2_NW) void k_f2_fill(FillArgs A, F2Lay L) {
     __shared__ __align__(16) uint8_t sb[F2_LDS];
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs; consecutive chunks (which write adjacent runs of
     // the same columns) land on one XCD
     const uint32_t nb = gridDim.x, per = nb >> 3, b = blockIdx.x;
@@ -590,9 +597,10 @@ __global__ __launch_bounds__(64) void k_f2_fill(FillArgs A, F2Lay L) {
     if (lds) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         typedef __attribute__((address_space(1))) const u32x4 gu128;
-        // 16-B blocks, four loads in flight; a block past the array's readable end is copied byte by byte
+        // 16-B blocks, four loads in flight; the wave takes every F2_NW-th group of four blocks; a block past the array's
+        // readable end is copied byte by byte
         auto copy = [&](uint32_t dst, const uint8_t *src, uint64_t a, uint32_t n, uint64_t lim) {
-            for (uint32_t i = 0; i < n; i += 64) {
+            for (uint32_t i = 64u * (uint32_t)wv; i < n; i += 64u * F2_NW) {
                 uint4 v[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
@@ -692,12 +700,14 @@ __global__ __launch_bounds__(64) void k_f2_fill(FillArgs A, F2Lay L) {
         while (k != 15 && !eats_ref(k)) step();
         xe = x + (int32_t)len;
     }
-    for (int32_t c0 = cb; c0 < ce; c0 += 64) {
+    // the wave's part of the span (the cursor catches up at its first covered column)
+    const int32_t part = (ce - cb + F2_NW - 1) / F2_NW, pb = cb + wv * part, pe = min(ce, pb + part);
+    for (int32_t c0 = pb; c0 < pe; c0 += 64) {
         // the next 64 columns' first entry of this chunk (CSR offset + the earlier chunks' entries), one per lane
         uint64_t at0 = 0;
-        if (c0 + lane < ce) at0 = A.off[c0 + lane] + L.base[ro + (uint32_t)(c0 + lane - cb)];
+        if (c0 + lane < pe) at0 = A.off[c0 + lane] + L.base[ro + (uint32_t)(c0 + lane - cb)];
         const uint32_t at_lo = (uint32_t)at0, at_hi = (uint32_t)(at0 >> 32);
-        const int32_t nc = min(64, ce - c0);
+        const int32_t nc = min(64, pe - c0);
         for (int32_t j = 0; j < nc; j++) {
             const int32_t c = c0 + j;
             bool cov = c >= rp && c < re;
@@ -816,7 +826,7 @@ hipError_t launch_pileup_fill(const FillArgs &A, hipStream_t st) {
         const unsigned cb = (unsigned)((L.n_chunks + 3) / 4);
         k_f2_count<<<cb, 256, 0, st>>>(A, L);
         k_f2_base<<<(unsigned)((A.n_tiles + 3) / 4), 256, 0, st>>>(A, L);
-        k_f2_fill<<<(unsigned)((L.n_chunks + 7) & ~7ll), 64, 0, st>>>(A, L);
+        k_f2_fill<<<(unsigned)((L.n_chunks + 7) & ~7ll), 64 * F2_NW, 0, st>>>(A, L);
         return hipGetLastError();
     }
     int32_t fg = 0;
