@@ -79,36 +79,72 @@ __global__ void k_plan_init(PlanHead *h) {
     h->n_cand = 0;
 }
 
+// The reductions into the head: per workgroup (LDS), then one atomic per field per workgroup — the head's fields share a
+// cache line, so per-wave atomics from the whole grid serialised there (r06j: 0.75 ms for 2.0 M reads).
+constexpr int RED_U = 8;                       // reads per thread of the reduction kernels (grid: n / (256 RED_U))
+unsigned grid_red(uint64_t n) {
+    return (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 256 * RED_U - 1) / (256 * RED_U), 1024));
+}
+
 // every read: its span (>= 1 column, else the host plans), sort order, new-position flag, pair candidates
 __global__ __launch_bounds__(256) void k_plan_reads(PlanArgs A) {
+    __shared__ int32_t s_mn[4], s_mx[4];
+    __shared__ int64_t s_pmin[4], s_emax[4];
+    __shared__ uint32_t s_bad[4], s_nc[4];
     int32_t mn = INT32_MAX, mx = INT32_MIN;
     int64_t pmin = INT64_MAX, emax = INT64_MIN;
     uint32_t bad = 0, nc = 0;
-    for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < A.n; r += gridDim.x * 256u) {
-        const int32_t p = A.pos[r], e = A.end[r];
-        const int32_t prev = r ? A.pos[r - 1] : INT32_MIN;
-        mn = min(mn, e - p);
-        mx = max(mx, e - p);
-        pmin = min(pmin, (int64_t)p);
-        emax = max(emax, (int64_t)e);
-        bad |= (e <= p || prev > p || p < 0) ? 1u : 0u;
-        A.first[r] = (r == 0 || prev != p) ? 1u : 0u;
-        nc += (A.olap && cand_of(A, r)) ? 1u : 0u;
+    // RED_U reads per thread per round, every load of the round issued before the first store (the arrays may alias
+    // for the compiler)
+    for (uint32_t r0 = blockIdx.x * 256u * RED_U + threadIdx.x; r0 < A.n; r0 += gridDim.x * 256u * RED_U) {
+        int32_t p[RED_U], e[RED_U], pv[RED_U];
+        bool cd[RED_U];
+#pragma unroll
+        for (int u = 0; u < RED_U; u++) {
+            const uint32_t r = r0 + 256u * u;
+            const bool in = r < A.n;
+            p[u] = in ? A.pos[r] : 0;
+            e[u] = in ? A.end[r] : 1;
+            pv[u] = in && r ? A.pos[r - 1] : INT32_MIN;
+            cd[u] = in && A.olap && cand_of(A, r);
+        }
+#pragma unroll
+        for (int u = 0; u < RED_U; u++) {
+            const uint32_t r = r0 + 256u * u;
+            if (r >= A.n) continue;
+            mn = min(mn, e[u] - p[u]);
+            mx = max(mx, e[u] - p[u]);
+            pmin = min(pmin, (int64_t)p[u]);
+            emax = max(emax, (int64_t)e[u]);
+            bad |= (e[u] <= p[u] || pv[u] > p[u] || p[u] < 0) ? 1u : 0u;
+            A.first[r] = (r == 0 || pv[u] != p[u]) ? 1u : 0u;
+            nc += cd[u] ? 1u : 0u;
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) A.first[A.n] = 0;
+    const int w = threadIdx.x >> 6;
     mn = wave_min(mn);
     mx = wave_max(mx);
     pmin = wave_min64(pmin);
     emax = wave_max64(emax);
-    const uint64_t badm = __ballot(bad != 0);
-    const int64_t ncs = wave_sum64((int64_t)nc);
+    const uint32_t badw = __ballot(bad != 0) ? 1u : 0u;
+    const uint32_t ncw = (uint32_t)wave_sum64((int64_t)nc);
     if ((threadIdx.x & 63) == 0) {
-        atomicMin(&A.head->min_span, mn);
-        atomicMax(&A.head->max_span, mx);
+        s_mn[w] = mn; s_mx[w] = mx; s_pmin[w] = pmin; s_emax[w] = emax; s_bad[w] = badw; s_nc[w] = ncw;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < 4; i++) {
+            mn = min(mn, s_mn[i]); mx = max(mx, s_mx[i]);
+            pmin = min(pmin, s_pmin[i]); emax = max(emax, s_emax[i]);
+        }
+        const uint32_t bd = s_bad[0] | s_bad[1] | s_bad[2] | s_bad[3], ns = s_nc[0] + s_nc[1] + s_nc[2] + s_nc[3];
+        if (mn != INT32_MAX) atomicMin(&A.head->min_span, mn);
+        if (mx != INT32_MIN) atomicMax(&A.head->max_span, mx);
         if (pmin != INT64_MAX) atomicMin((unsigned long long *)&A.head->min_pos, (unsigned long long)pmin);
         if (emax != INT64_MIN) atomicMax((unsigned long long *)&A.head->max_end, (unsigned long long)emax);
-        if (badm) atomicOr(&A.head->err, 1u);
-        if (ncs) atomicAdd((uint32_t *)&A.head->n_cand, (uint32_t)ncs);
+        if (bd) atomicOr(&A.head->err, 1u);
+        if (ns) atomicAdd((uint32_t *)&A.head->n_cand, ns);
     }
 }
 
@@ -322,22 +358,65 @@ __global__ __launch_bounds__(256) void k_plan_pairs(PlanArgs A) {
     }
 }
 
-// the kept reads' coverage difference array over [span_lo, span_lo + span_n); all reads when `all`
+// the kept reads' coverage difference array over [span_lo, span_lo + span_n); all reads when `all`.  A workgroup takes
+// 256 RED_U consecutive reads (coordinate order): their starts and ends fall in a window [first start, max end] that is
+// usually short, so the +1 / -1 go to an LDS histogram of the window first and only its non-zero bins to the global
+// array (one global atomic per read end before: ~67 reads per start position hit one address, r06j 0.46 ms).
+constexpr int DIFF_BINS = 8192;
 __global__ __launch_bounds__(256) void k_plan_diff(PlanArgs A, int all) {
+    __shared__ int32_t bins[DIFF_BINS];
+    __shared__ int32_t s_mx[4];
+    __shared__ int64_t s_hi[4];
     const uint32_t n = all ? A.n : A.head->n_kept;
+    const uint32_t i0 = blockIdx.x * (256u * RED_U);
+    if (i0 >= n) return;                                            // (workgroup-uniform)
+    const int w = threadIdx.x >> 6;
+    int32_t p[RED_U], e[RED_U];
+#pragma unroll
+    for (int u = 0; u < RED_U; u++) {
+        const uint32_t i = i0 + threadIdx.x + 256u * u;
+        const uint32_t r = i < n ? (all ? i : A.kept[i]) : 0u;
+        p[u] = i < n ? A.pos[r] : INT32_MAX;
+        e[u] = i < n ? A.end[r] : INT32_MIN;
+    }
     int32_t mx = 0;
     int64_t hi = INT64_MIN;
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        const uint32_t r = all ? i : A.kept[i];
-        const int32_t p = A.pos[r], e = A.end[r];
-        atomicAdd(&A.diff[p - A.span_lo], 1);
-        atomicAdd(&A.diff[e - A.span_lo], -1);
-        mx = max(mx, e - p);
-        hi = max(hi, (int64_t)e);
+#pragma unroll
+    for (int u = 0; u < RED_U; u++) {
+        if (e[u] != INT32_MIN) {
+            mx = max(mx, e[u] - p[u]);
+            hi = max(hi, (int64_t)e[u]);
+        }
     }
     mx = wave_max(mx);
     hi = wave_max64(hi);
-    if (!all && (threadIdx.x & 63) == 0) {
+    if ((threadIdx.x & 63) == 0) { s_mx[w] = mx; s_hi[w] = hi; }
+    __syncthreads();
+    for (int i = 0; i < 4; i++) { mx = max(mx, s_mx[i]); hi = max(hi, s_hi[i]); }
+    const int32_t lo = A.pos[all ? i0 : A.kept[i0]];                // (the block's first read starts first)
+    const bool lds = hi - (int64_t)lo < DIFF_BINS;                  // (uniform)
+    if (lds) {
+        for (int i = threadIdx.x; i < DIFF_BINS; i += 256) bins[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < RED_U; u++) {
+            if (e[u] == INT32_MIN) continue;
+            atomicAdd(&bins[p[u] - lo], 1);
+            atomicAdd(&bins[e[u] - lo], -1);
+        }
+        __syncthreads();
+        const int nb = (int)(hi - (int64_t)lo) + 1;
+        for (int i = threadIdx.x; i < nb; i += 256)
+            if (bins[i]) atomicAdd(&A.diff[(int64_t)lo + i - A.span_lo], bins[i]);
+    } else {
+#pragma unroll
+        for (int u = 0; u < RED_U; u++) {
+            if (e[u] == INT32_MIN) continue;
+            atomicAdd(&A.diff[p[u] - A.span_lo], 1);
+            atomicAdd(&A.diff[e[u] - A.span_lo], -1);
+        }
+    }
+    if (!all && threadIdx.x == 0) {
         atomicMax(&A.head->max_span_kept, mx);
         if (hi != INT64_MIN) atomicMax((unsigned long long *)&A.head->hi, (unsigned long long)hi);
     }
@@ -412,7 +491,7 @@ size_t plan_temp_bytes(uint32_t n, int64_t span_n) {
 // stage 0: every read's fields checked, the distinct start positions listed (then the host reads the head)
 hipError_t launch_plan_reads(const PlanArgs &A, void *tmp, size_t tmp_bytes, hipStream_t st) {
     k_plan_init<<<1, 1, 0, st>>>(A.head);
-    k_plan_reads<<<grid_for(A.n), 256, 0, st>>>(A);
+    k_plan_reads<<<grid_red(A.n), 256, 0, st>>>(A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, A.first, A.didx, (int)A.n + 1, st);
@@ -425,7 +504,7 @@ hipError_t launch_plan_reads(const PlanArgs &A, void *tmp, size_t tmp_bytes, hip
 hipError_t launch_plan_cov(const PlanArgs &A, int all, int32_t *cov, void *tmp, size_t tmp_bytes, hipStream_t st) {
     hipError_t e = hipMemsetAsync(A.diff, 0, sizeof(int32_t) * (size_t)(A.span_n + 1), st);
     if (e != hipSuccess) return e;
-    k_plan_diff<<<grid_for(A.n), 256, 0, st>>>(A, all);
+    k_plan_diff<<<(unsigned)((A.n + 256u * RED_U - 1) / (256u * RED_U)), 256, 0, st>>>(A, all);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     e = hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, A.diff, cov, (int)(A.span_n + 1), st);
     if (e != hipSuccess) return e;
