@@ -177,37 +177,65 @@ __device__ __forceinline__ int32_t wave_sum32(int32_t v) {
 
 // htslib's depth cap over the distinct start positions in order (one workgroup; see the file comment).  Wave 0 decides
 // a window's k values — up to SWEEP_W positions, two per lane — from LDS (the distinct positions and their first reads
-// staged SWEEP_BLK at a time, the ring of kept-read end counts), the k recurrence in scalar registers when the cap can
-// bite; then every wave marks the window's reads and adds the kept ones' ends to the ring (each thread SWEEP_U
-// consecutive reads, their loads issued together; neighbouring lanes' reads start at different positions, so the ring
-// atomics of one instruction spread over many end slots).
-constexpr int SWEEP_BLK = 2048, SWEEP_U = 4, SWEEP_W = 128;
+// staged SWEEP_BLK at a time, the ring of kept-read end counts); when the cap can bite, the k recurrence runs on one
+// lane (below).  Then every wave marks the window's reads and adds the kept ones' ends to the ring (below).  The
+// barriers fence LDS only (the keep flags are for later kernels).  r06n shader clocks per 10,000x window before the
+// med3 chain and the position-major marking: decide 13.6k (the recurrence 9.8k), mark 23.4k; r06o (med3, read-major
+// marking with run-aggregated atomics): decide 9.3k (5.8k), mark 11.5k — 167k at 100,000x.
+constexpr int SWEEP_BLK = 2048, SWEEP_W = 128, MARK_B = SWEEP_W / (SWEEP_T / 64);
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
 __global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
     __shared__ int32_t ring[RING];
     __shared__ int32_t sdpos[SWEEP_BLK];
     __shared__ uint32_t sdfirst[SWEEP_BLK + 1];
-    __shared__ uint32_t kk[SWEEP_W], ff[SWEEP_W];
-    __shared__ int32_t jmap[SWEEP_W];
-    __shared__ uint32_t s_r0, s_r1, s_next;
-    __shared__ int32_t s_P;
+    __shared__ __align__(16) int32_t kk[SWEEP_W];
+    __shared__ __align__(16) float sg[SWEEP_W], sn[SWEEP_W], scum[SWEEP_W];
+    __shared__ uint32_t ff[SWEEP_W];
+    __shared__ uint32_t s_next;
+    __shared__ int32_t s_w;
     const int tid = threadIdx.x, lane = tid & 63;
     const uint32_t D = A.head->n_distinct;
     const int32_t W0 = min(SWEEP_W, A.head->min_span);
     const int32_t M = (int32_t)min(A.maxcnt, (int64_t)INT32_MAX);
     for (int i = tid; i < RING; i += SWEEP_T) ring[i] = 0;
+    // the next window's positions' first 64 reads' ends (kept or not), loaded while wave 0 decides it: wave wv's
+    // positions wv + 16 b, when their first reads are staged in sdfirst
+    const int wv = tid >> 6;
+    int32_t pe0[MARK_B];
+    bool pok[MARK_B];
+    uint32_t pf_d = UINT32_MAX, blk0 = 0, blk1 = 0;   // (sdpos / sdfirst hold distinct positions [blk0, blk1))
+    auto prefetch = [&](uint32_t dn) __attribute__((always_inline)) {
+        pf_d = dn;
+#pragma unroll
+        for (int b = 0; b < MARK_B; b++) {
+            const uint32_t i = dn + (uint32_t)(wv + (SWEEP_T / 64) * b);
+            pok[b] = i >= blk0 && i + 1 < blk1;
+            const uint32_t f = pok[b] ? sdfirst[i - blk0] : 0u, n = pok[b] ? sdfirst[i + 1 - blk0] - f : 0u;
+            pe0[b] = (uint32_t)lane < n ? A.end[f + (uint32_t)lane] : 0;
+        }
+    };
     int32_t alive = 0;                                 // (wave 0) kept reads not freed yet
     int32_t at = D ? A.dpos[0] : 0;                    // (wave 0) frees applied for every end < at
-    uint32_t d = 0, blk0 = 0, blk1 = 0;                // sdpos / sdfirst hold distinct positions [blk0, blk1)
+    uint32_t d = 0;
     while (d < D) {
         if (d + SWEEP_W + 1 > blk1 && blk1 < D + 1) {  // (uniform) stage the next block of distinct positions
-            __syncthreads();
+            lds_barrier();
             blk0 = d;
             blk1 = min(D + 1, d + (uint32_t)SWEEP_BLK);
             for (uint32_t i = blk0 + (uint32_t)tid; i < blk1; i += SWEEP_T) {
                 sdpos[i - blk0] = i < D ? A.dpos[i] : INT32_MAX;
                 sdfirst[i - blk0] = A.dfirst[i];
             }
-            __syncthreads();
+            lds_barrier();
         }
         if (tid < 64) {
             const int32_t P = sdpos[d - blk0];
@@ -250,63 +278,123 @@ __global__ __launch_bounds__(SWEEP_T) void k_plan_sweep(PlanArgs A) {
             const uint32_t fb0 = vb ? sdfirst[ib - blk0] : 0u, fb1 = vb ? sdfirst[ib + 1 - blk0] : 0u;
             const int32_t na = (int32_t)(fa1 - fa0), nb = (int32_t)(fb1 - fb0);
             int32_t ka = na, kb = nb;
-            if ((int64_t)alive + wave_sum32(na + nb) > (int64_t)M) {
-                // the cap may bite: k_j = min(n_j, max(1, M - alive_j)) in order, in scalar registers (no branch in the
-                // loop bodies: one per half of the window)
+            const int32_t sum_n = wave_sum32(na + nb);
+            if ((int64_t)alive + sum_n > (int64_t)M) {
+                // the cap may bite: k_j = min(n_j, max(1, G_j - cum_j)), G_j = M - alive + F_j (the room at j before the
+                // window's pushes), cum_j = the window's kept reads before j — in order, on one lane.  The chain is
+                // cum_{j+1} = med3(cum_j + 1, G_j, cum_j + n_j) (n_j >= 1): two VALU steps per position, in fp32, exact
+                // while every operand stays below 2^24; the k_j are the differences, taken by every lane afterwards
                 const int32_t base = __builtin_amdgcn_readfirstlane(alive);
-                int32_t cum = 0;
-                const int wa = min(w, 64);
-                for (int j = 0; j < wa; j++) {
-                    const int32_t fj = __builtin_amdgcn_readlane(Fa, j), n_ = __builtin_amdgcn_readlane(na, j);
-                    const int32_t kj = min(n_, max(1, M - (base - fj + cum)));
-                    ka = lane == j ? kj : ka;
-                    cum += kj;
-                }
-                for (int j = 64; j < w; j++) {
-                    const int32_t fj = __builtin_amdgcn_readlane(Fb, j - 64), n_ = __builtin_amdgcn_readlane(nb, j - 64);
-                    const int32_t kj = min(n_, max(1, M - (base - fj + cum)));
-                    kb = lane == j - 64 ? kj : kb;
-                    cum += kj;
+                if (M < (1 << 22) && base < (1 << 22) && sum_n < (1 << 22)) {
+                    sg[lane] = (float)(M - base + Fa);
+                    sn[lane] = (float)(va ? na : 0);       // (n = 0 past the window: its values are never read)
+                    sg[64 + lane] = (float)(M - base + Fb);
+                    sn[64 + lane] = (float)(vb ? nb : 0);
+                    wave_lds_sync();
+                    if (lane == 0) {
+                        // 8 positions per round, the next round's operands read while this one's chain runs
+                        float u = 0.f;
+                        float4 g0 = *reinterpret_cast<const float4 *>(&sg[0]), g1 = *reinterpret_cast<const float4 *>(&sg[4]);
+                        float4 n0 = *reinterpret_cast<const float4 *>(&sn[0]), n1 = *reinterpret_cast<const float4 *>(&sn[4]);
+                        for (int j0 = 0; j0 < w; j0 += 8) {
+                            const int jn = min(j0 + 8, SWEEP_W - 8);
+                            const float4 h0 = *reinterpret_cast<const float4 *>(&sg[jn]);
+                            const float4 h1 = *reinterpret_cast<const float4 *>(&sg[jn + 4]);
+                            const float4 m0 = *reinterpret_cast<const float4 *>(&sn[jn]);
+                            const float4 m1 = *reinterpret_cast<const float4 *>(&sn[jn + 4]);
+                            const float G[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+                            const float Nn[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+                            float Cu[8];
+#pragma unroll
+                            for (int t = 0; t < 8; t++) {
+                                u = __builtin_amdgcn_fmed3f(u + 1.f, G[t], u + Nn[t]);
+                                Cu[t] = u;
+                            }
+                            *reinterpret_cast<float4 *>(&scum[j0]) = make_float4(Cu[0], Cu[1], Cu[2], Cu[3]);
+                            *reinterpret_cast<float4 *>(&scum[j0 + 4]) = make_float4(Cu[4], Cu[5], Cu[6], Cu[7]);
+                            g0 = h0; g1 = h1; n0 = m0; n1 = m1;
+                        }
+                    }
+                    wave_lds_sync();
+                    ka = (int32_t)scum[lane] - (lane ? (int32_t)scum[lane - 1] : 0);
+                    kb = (int32_t)scum[64 + lane] - (int32_t)scum[63 + lane];
+                } else {
+                    int32_t cum = 0;                       // (large operands: the integer form, lane by lane)
+                    const int wa = min(w, 64);
+                    for (int j = 0; j < wa; j++) {
+                        const int32_t fj = __builtin_amdgcn_readlane(Fa, j), n_ = __builtin_amdgcn_readlane(na, j);
+                        const int32_t kj = min(n_, max(1, M - (base - fj + cum)));
+                        ka = lane == j ? kj : ka;
+                        cum += kj;
+                    }
+                    for (int j = 64; j < w; j++) {
+                        const int32_t fj = __builtin_amdgcn_readlane(Fb, j - 64), n_ = __builtin_amdgcn_readlane(nb, j - 64);
+                        const int32_t kj = min(n_, max(1, M - (base - fj + cum)));
+                        kb = lane == j - 64 ? kj : kb;
+                        cum += kj;
+                    }
                 }
             }
             alive = alive - Ftot + wave_sum32((va ? ka : 0) + (vb ? kb : 0));
             at = plast;
-            jmap[lane] = -1;
-            jmap[64 + lane] = -1;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            __builtin_amdgcn_wave_barrier();
-            if (va) { kk[lane] = (uint32_t)ka; ff[lane] = fa0; jmap[pa - P] = lane; }
-            if (vb) { kk[64 + lane] = (uint32_t)kb; ff[64 + lane] = fb0; jmap[pb - P] = 64 + lane; }
+            if (va) { kk[lane] = ka; ff[lane] = fa0; A.first[ia] = (uint32_t)ka; }
+            if (vb) { kk[64 + lane] = kb; ff[64 + lane] = fb0; A.first[ib] = (uint32_t)kb; }
             if (lane == 0) {
-                s_P = P;
-                s_r0 = sdfirst[d - blk0];
-                s_r1 = sdfirst[d + (uint32_t)w - blk0];
+                s_w = w;
                 s_next = d + (uint32_t)w;
             }
         }
-        __syncthreads();
-        const int32_t P = s_P;
-        const uint32_t r0 = s_r0, r1 = s_r1;
-        for (uint32_t rb = r0 + (uint32_t)(SWEEP_U * tid); rb < r1; rb += SWEEP_U * SWEEP_T) {
-            int32_t ps[SWEEP_U], es[SWEEP_U];
+        lds_barrier();
+        // the kept reads' ends into the ring, by position: wave wv takes positions wv, wv + 16, ... of the window
+        // (MARK_B of them).  A position's reads are [ff, ff + n) and the first kk are kept, so only the kept reads' ends
+        // are read (every read's start and end before: 670 reads per position at 100,000x for ~53 kept); lanes = the
+        // position's reads.  Its kept reads mostly end together: consecutive lanes sharing a ring slot add to it with
+        // one atomic (the run's head adds the run's length).  The per-read keep flags are written afterwards by
+        // k_plan_keep from the k of every position (A.first), off this one workgroup.
+        const int wsz = s_w;
+        auto ring_add = [&](int32_t key) __attribute__((always_inline)) {
+            const int32_t prev = __shfl_up(key, 1, 64);
+            const bool head = key >= 0 && (lane == 0 || prev != key);
+            const uint64_t brk = __ballot(head || key < 0);
+            if (head) {
+                const uint64_t above = lane == 63 ? 0ull : (brk >> (lane + 1)) << (lane + 1);
+                const int nxt = above ? __builtin_ctzll(above) : 64;
+                atomicAdd(&ring[key], nxt - lane);
+            }
+        };
+        {
+            uint32_t fj[MARK_B], kj[MARK_B];
+            int32_t e0[MARK_B];
+            const bool pf = pf_d == d;                                 // (uniform) the prefetch is this window's
 #pragma unroll
-            for (int u = 0; u < SWEEP_U; u++) {
-                const uint32_t r = rb + (uint32_t)u;
-                ps[u] = r < r1 ? A.pos[r] : P;
-                es[u] = r < r1 ? A.end[r] : 0;
+            for (int b = 0; b < MARK_B; b++) {
+                const int j = wv + (SWEEP_T / 64) * b;
+                const bool ok = j < wsz;
+                fj[b] = ok ? ff[j] : 0u;
+                kj[b] = ok ? (uint32_t)kk[j] : 0u;
+                e0[b] = pf && pok[b] ? pe0[b] : ((uint32_t)lane < kj[b] ? A.end[fj[b] + (uint32_t)lane] : 0);
             }
 #pragma unroll
-            for (int u = 0; u < SWEEP_U; u++) {
-                const uint32_t r = rb + (uint32_t)u;
-                if (r >= r1) continue;
-                const int j = jmap[ps[u] - P];
-                const bool kp = r - ff[j] < kk[j];
-                A.keep[r] = kp ? 1 : 0;
-                if (kp) atomicAdd(&ring[es[u] & (RING - 1)], 1);
+            for (int b = 0; b < MARK_B; b++) {
+                if (kj[b] == 0) continue;                              // (wave-uniform)
+                ring_add((uint32_t)lane < kj[b] ? (e0[b] & (RING - 1)) : -1);
+                for (uint32_t i0 = 64; i0 < kj[b]; i0 += 64) {          // (more than 64 kept at one position)
+                    const uint32_t i = i0 + (uint32_t)lane;
+                    ring_add(i < kj[b] ? (A.end[fj[b] + i] & (RING - 1)) : -1);
+                }
             }
         }
+        prefetch(s_next);
         d = s_next;
-        __syncthreads();
+        lds_barrier();
+    }
+}
+
+// the keep flags from the sweep's per-position k (A.first[j], j = the read's distinct position: didx[r + 1] - 1)
+__global__ __launch_bounds__(256) void k_plan_keep(PlanArgs A) {
+    for (uint32_t r = blockIdx.x * 256u + threadIdx.x; r < A.n; r += gridDim.x * 256u) {
+        const uint32_t j = A.didx[r + 1] - 1u;
+        A.keep[r] = r - A.dfirst[j] < A.first[j] ? 1 : 0;
     }
 }
 
@@ -523,6 +611,9 @@ hipError_t launch_plan_keep(const PlanArgs &A, bool sweep, hipStream_t st) {
         return hipGetLastError();
     }
     k_plan_sweep<<<1, SWEEP_T, 0, st>>>(A);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    k_plan_keep<<<grid_for(A.n), 256, 0, st>>>(A);
     return hipGetLastError();
 }
 

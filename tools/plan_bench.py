@@ -30,5 +30,11 @@ with AlignmentFile(bam) as f:
         p = eng.bam_plan_build(prm.max_depth, prm.ignore_overlaps)
         eng.sync()
         res["ms"].append(round((time.perf_counter() - t) * 1e3, 3))
+        if hasattr(eng._L, "spg_ab_prof"):     # (tools/src_ab.py sweep_prof build: the sweep's phase clocks)
+            import ctypes as C
+            pr = (C.c_uint64 * 8)()
+            eng._L.spg_ab_prof(pr)
+            names = ["decide", "barrier1", "stage", "recur", "mark", "barrier2", "windows", "total"]
+            res["sweep_clocks"] = {k: int(pr[i]) for i, k in enumerate(names)}
     res.update(reads=n, kept=int(p.n_kept), entries=int(p.n_entries), pairs=int(p.n_pairs))
 print(json.dumps(res), flush=True)

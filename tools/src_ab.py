@@ -7,6 +7,8 @@ with tools/ab_run.py.  Edits (named):
   sweep_nok  (spg_plan.hip) the depth-cap sweep skips its k recurrence (k = n): its cost; the plan is wrong.
   sweep_noatom (spg_plan.hip) the sweep marks reads but adds no ends to the ring: the atomics' cost; the plan is wrong.
   prof       k_inflate_par's phases timed with the shader clock (spg_ab_prof; tools/inflate_bench.py reports them).
+  sweep_prof (spg_plan.hip) the depth-cap sweep's phases timed with the shader clock by thread 0 (spg_ab_prof;
+             tools/plan_bench.py reports them).
 Dev tool only."""
 import os
 import subprocess
@@ -16,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "covid-spings-variant-caller_amd", "csrc")
 LIB = os.path.join(ROOT, "covid-spings-variant-caller_amd", "_lib")
 
-SRC_OF = {"sweep_nok": "spg_plan.hip", "sweep_noatom": "spg_plan.hip"}
+SRC_OF = {"sweep_nok": "spg_plan.hip", "sweep_noatom": "spg_plan.hip", "sweep_prof": "spg_plan.hip"}
 PROF_EXPORT = """
 extern "C" int spg_ab_prof(uint64_t *out8) {
     if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(spg::g_ab_prof), 8 * sizeof(uint64_t)) != hipSuccess) return -1;
@@ -50,8 +52,34 @@ EDITS = {
              ("}  // namespace spg\n\n// ---", "}  // namespace spg\n" + "@@EXPORT@@" + "\n// ---")],
     "sweep_nok": [("            if ((int64_t)alive + wave_sum32(na + nb) > (int64_t)M) {",
                    "            if ((int64_t)alive + wave_sum32(na + nb) > (int64_t)M && M < 0) {")],
-    "sweep_noatom": [("                if (kp) atomicAdd(&ring[es[u] & (RING - 1)], 1);",
-                      "                if (kp && es[u] < 0) atomicAdd(&ring[es[u] & (RING - 1)], 1);")],
+    "sweep_noatom": [("                    atomicAdd(&ring[key], nxt - lane);",
+                      "                    if (nxt < 0) atomicAdd(&ring[key], nxt - lane);")],
+    # the sweep's phases (thread 0's shader clock, summed over windows): [0] wave 0's decision, [1] the barrier after
+    # it, [2] staging, [3] the k recurrence, [4] thread 0's marking, [5] the window's closing barrier, [6] windows,
+    # [7] the whole kernel
+    "sweep_prof": [("namespace spg {\n\nnamespace {", "namespace spg {\n__device__ unsigned long long g_ab_prof[8];\nnamespace {"),
+                   ("    while (d < D) {\n        if (d + SWEEP_W + 1 > blk1 && blk1 < D + 1) {",
+                    "    const uint64_t tq0 = clock64();\n    while (d < D) {\n        const uint64_t t_top = clock64();\n"
+                    "        if (d + SWEEP_W + 1 > blk1 && blk1 < D + 1) {"),
+                   ("            lds_barrier();\n        }\n        if (tid < 64) {",
+                    "            lds_barrier();\n        }\n        const uint64_t t_st = clock64();\n"
+                    "        if (tid == 0) atomicAdd(&g_ab_prof[2], t_st - t_top);\n        if (tid < 64) {"),
+                   ("                const int32_t base = __builtin_amdgcn_readfirstlane(alive);\n                if (M <",
+                    "                const uint64_t t_r0 = clock64();\n"
+                    "                const int32_t base = __builtin_amdgcn_readfirstlane(alive);\n                if (M <"),
+                   ("                    kb = (int32_t)scum[64 + lane] - (int32_t)scum[63 + lane];",
+                    "                    kb = (int32_t)scum[64 + lane] - (int32_t)scum[63 + lane];\n"
+                    "                    if (tid == 0) atomicAdd(&g_ab_prof[3], clock64() - t_r0);"),
+                   ("        lds_barrier();\n        // the kept reads",
+                    "        const uint64_t t_dec = clock64();\n        if (tid == 0) atomicAdd(&g_ab_prof[0], t_dec - t_st);\n"
+                    "        lds_barrier();\n        const uint64_t t_b1 = clock64();\n"
+                    "        if (tid == 0) atomicAdd(&g_ab_prof[1], t_b1 - t_dec);\n        // the kept reads"),
+                   ("        d = s_next;\n        lds_barrier();\n    }",
+                    "        const uint64_t t_mk = clock64();\n        if (tid == 0) atomicAdd(&g_ab_prof[4], t_mk - t_b1);\n"
+                    "        d = s_next;\n        lds_barrier();\n"
+                    "        if (tid == 0) { atomicAdd(&g_ab_prof[5], clock64() - t_mk); atomicAdd(&g_ab_prof[6], 1ull); }\n    }\n"
+                    "    if (tid == 0) atomicAdd(&g_ab_prof[7], clock64() - tq0);"),
+                   ("}  // namespace spg\n", "}  // namespace spg\n" + "@@EXPORT@@")],
     "noresolve": [("        for (int k = 0; k <= kend && !st; k++) {",
                    "        for (int k = 0; k <= kend && !st && kend < 0; k++) {"),
                   ("    if (!st && w != ulen) st = ST_FALLBACK;", "    if (!st) w = ulen;")],
