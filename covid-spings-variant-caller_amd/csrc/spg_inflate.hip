@@ -528,16 +528,18 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp
 //    before the batch are written at once (lane-parallel; matches longer than 32 bytes by the whole wave), then the
 //    matches whose source is an earlier token of the batch, in order, each by the whole wave.  Completed 1 KiB blocks of
 //    global memory are written from the ring with 16-byte stores; sources more than PAR_RECENT bytes back (~40 % of the
-//    matches in BAM data: DEFLATE reaches 32 KiB back) are read from that written output.  A small ring keeps ~13 KiB of
-//    LDS per wave, so three waves per SIMD hide each other's latency: 10,000x BAM 8.56 ms (a 32 KiB ring allowed one
-//    wave per SIMD: 14.0 ms; a 4 KiB ring 8.8 ms, and with 128 VGPRs for 4 waves per SIMD 9.1 ms; r05n).
+//    matches in BAM data: DEFLATE reaches 32 KiB back) are read from that written output.  A small ring keeps LDS per
+//    wave low, so several waves per SIMD hide each other's latency: r05n 10,000x BAM 8.56 ms with an 8 KiB ring (13 KiB,
+//    3 waves per SIMD; a 32 KiB ring allowed one: 14.0 ms); r06t, with 107 VGPRs since the whole-wave table builds, a
+//    4 KiB ring (9.1 KiB: 4 waves per SIMD) 6.07 -> 5.81 ms; r06u, a 2 KiB ring (7.1 KiB) with the VGPRs held to 96 by
+//    the waves-per-EU attribute (no spill): 5 waves per SIMD, 5.22 ms (6 waves, 80 VGPRs with spills: 5.3 ms).
 // Token lists, positions and redo tokens live in global scratch (inflate_scratch_bytes: 12 B per compressed byte + 76 KiB
 // per member).
 // ------------------------------------------------------------------------------------------------------------------
 constexpr uint32_t TK_EOB = 0x40000000u, TK_MATCH = 0x80000000u;   // tokens: literal byte | EOB | match (len-3)<<16 | dist-1
 constexpr uint32_t PAR_RCAP = 256;                                  // redo tokens per lane
 constexpr uint32_t PAR_MIN_SEG = 1024;                              // data bits per lane at least (fewer lanes for short blocks)
-constexpr uint32_t PAR_RING = 8192, PAR_BATCH = 1024;               // LDS window ring (power of two), batch output cap
+constexpr uint32_t PAR_RING = 2048, PAR_BATCH = 1024;               // LDS window ring (power of two), batch output cap
 constexpr uint32_t PAR_RECENT = PAR_RING - PAR_BATCH;               // match sources this close to the batch come from LDS
 // scratch per member m (u32 units unless noted): token lists at 2 coff + 2048 m (2 clen + 2048 of them, split evenly
 // over the block's lanes), token start positions (u16, relative to the lane's first bit) at the same index of a u16 array,
@@ -831,7 +833,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 
 __device__ __forceinline__ uint32_t ring_slot(uint32_t g0, uint32_t x) { return (g0 + x) & (PAR_RING - 1); }
 
-__global__ __launch_bounds__(64) void k_inflate_par(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_inflate_par(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
                                                     int64_t n, uint8_t *__restrict__ out, uint32_t *__restrict__ status,
                                                     uint32_t *__restrict__ scr_tok, uint16_t *__restrict__ scr_pos,
                                                     uint32_t *__restrict__ scr_redo, uint32_t *__restrict__ n_fallback) {
