@@ -527,8 +527,8 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp
 //    ring of the last PAR_RING output bytes (indexed by global output address): literals and matches whose source lies
 //    before the batch are written at once (lane-parallel; matches longer than 32 bytes by the whole wave), then the
 //    matches whose source is an earlier token of the batch, in order, each by the whole wave.  Completed 1 KiB blocks of
-//    global memory are written from the ring with 16-byte stores; sources more than PAR_RECENT bytes back (~40 % of the
-//    matches in BAM data: DEFLATE reaches 32 KiB back) are read from that written output.  A small ring keeps LDS per
+//    global memory are written from the ring with 16-byte stores; source bytes already flushed there (most matches of
+//    BAM data: DEFLATE reaches 32 KiB back) are read from that written output.  A small ring keeps LDS per
 //    wave low, so several waves per SIMD hide each other's latency: r05n 10,000x BAM 8.56 ms with an 8 KiB ring (13 KiB,
 //    3 waves per SIMD; a 32 KiB ring allowed one: 14.0 ms); r06t, with 107 VGPRs since the whole-wave table builds, a
 //    4 KiB ring (9.1 KiB: 4 waves per SIMD) 6.07 -> 5.81 ms; r06u, a 2 KiB ring (7.1 KiB) with the VGPRs held to 96 by
@@ -540,7 +540,8 @@ constexpr uint32_t TK_EOB = 0x40000000u, TK_MATCH = 0x80000000u;   // tokens: li
 constexpr uint32_t PAR_RCAP = 256;                                  // redo tokens per lane
 constexpr uint32_t PAR_MIN_SEG = 1024;                              // data bits per lane at least (fewer lanes for short blocks)
 constexpr uint32_t PAR_RING = 2048, PAR_BATCH = 1024;               // LDS window ring (power of two), batch output cap
-constexpr uint32_t PAR_RECENT = PAR_RING - PAR_BATCH;               // match sources this close to the batch come from LDS
+constexpr uint32_t PAR_RECENT = PAR_RING - PAR_BATCH;               // the ring holds every byte from w - PAR_RECENT on
+static_assert(PAR_RECENT >= 1023, "an unflushed partial 1 KiB block must stay in the ring");
 // scratch per member m (u32 units unless noted): token lists at 2 coff + 2048 m (2 clen + 2048 of them, split evenly
 // over the block's lanes), token start positions (u16, relative to the lane's first bit) at the same index of a u16 array,
 // redo tokens at 64 RCAP m
@@ -955,11 +956,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
                 const uint32_t excl = incl - len, o = w + excl;
                 if (__ballot(in && isM && dist > o) || w + total > ulen) { st = ST_FALLBACK; break; }
                 const uint32_t sb = o - dist;                                            // a match's source start
-                // independent: a literal, or a match whose source lies before the batch.  A source within PAR_RECENT bytes
-                // of the batch is in the LDS ring; one further back was written to global memory already (at most one
-                // partial 1 KiB block stays unflushed) and is read from there (L2)
+                // independent: a literal, or a match whose source lies before the batch.  A source byte already written
+                // to global memory (before `flushed`) is read from there (L2), any later one from the LDS ring: the ring
+                // keeps every byte from w - PAR_RECENT on through the batch, and at most one partial 1 KiB block (<= 1023
+                // bytes <= PAR_RECENT) stays unflushed, so each byte is in one of the two (a match's source may straddle
+                // `flushed` when PAR_RECENT is less than the longest match + 1 KiB)
                 const bool indep = in && (!isM || sb + min(len, dist) <= w);
-                const bool far = sb + PAR_RECENT < w;
                 if (indep && len <= 32) {                                                // lane by lane
                     if (!isM) {
                         ring[ring_slot(g0, o)] = (uint8_t)tk;
@@ -969,7 +971,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
                             uint8_t v[4];
 #pragma unroll
                             for (int u = 0; u < 4; u++) {
-                                v[u] = q + u < len ? (far ? gout[sb + mq] : ring[ring_slot(g0, sb + mq)]) : 0;
+                                v[u] = q + u < len ? (sb + mq < flushed ? gout[sb + mq] : ring[ring_slot(g0, sb + mq)]) : 0;
                                 mq = mq + 1 == dist ? 0 : mq + 1;
                             }
 #pragma unroll
@@ -989,12 +991,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
                     const uint32_t oj = (uint32_t)__builtin_amdgcn_readlane((int)o, j);
                     const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)len, j);
                     const uint32_t dj = (uint32_t)__builtin_amdgcn_readlane((int)dist, j);
-                    const bool farj = oj - dj + PAR_RECENT < w;                         // (wave-uniform)
                     for (uint32_t q0 = 0; q0 < lj; q0 += 64) {
                         const uint32_t q = q0 + (uint32_t)lane;
                         uint8_t v = 0;
                         const uint32_t x = oj - dj + (dj >= lj ? q : q % dj);
-                        if (q < lj) v = farj ? gout[x] : ring[ring_slot(g0, x)];
+                        if (q < lj) v = x < flushed ? gout[x] : ring[ring_slot(g0, x)];
                         if (q < lj) ring[ring_slot(g0, oj + q)] = v;
                     }
                 }
@@ -1016,34 +1017,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
     }
 }
 
-// CRC-32 (zlib's reflected polynomial) arithmetic: a * b mod P and x^(8 n) mod P, as zlib's multmodp / x2nmodp
+// CRC-32 (zlib's reflected polynomial) arithmetic: a * b mod P, as zlib's multmodp (branch-free)
 __device__ __forceinline__ uint32_t crc_multmodp(uint32_t a, uint32_t b) {
-    uint32_t m = 1u << 31, p = 0;
-    for (int i = 0; i < 32; i++) {
-        if (a & m) p ^= b;
-        m >>= 1;
-        b = (b & 1u) ? (b >> 1) ^ 0xEDB88320u : b >> 1;
+    uint32_t p = 0;
+#pragma unroll 8
+    for (int i = 31; i >= 0; i--) {
+        p ^= ((a >> i) & 1u) ? b : 0u;
+        b = (b >> 1) ^ ((b & 1u) ? 0xEDB88320u : 0u);
     }
     return p;
 }
-__device__ __forceinline__ uint32_t crc_x8n(uint32_t n) {     // x^(8 n) mod P
-    uint32_t r = 1u << 31, base = 1u << 30;                     // 1, x
-    for (uint64_t e = 8ull * n; e; e >>= 1) {
-        if (e & 1) r = crc_multmodp(base, r);
-        base = crc_multmodp(base, base);
-    }
-    return r;
-}
+
+// x^(8 * 1024 * 2^l) mod P for l = 0..5: the combine's operators for a right part of 2^l whole 1 KiB segments
+struct CrcOps {
+    uint32_t op[6];
+};
 
 // Each member's output checked against the CRC32 in its BGZF trailer (a member the decoder got wrong with the right
-// length would otherwise pass): one wave per member, lane j the CRC of bytes [1 KiB j, 1 KiB (j + 1)) through an LDS
-// table, the 64 partial CRCs combined in order (crc32_combine: crc(A B) = crc(A) x^(8 |B|) + crc(B) mod P).
+// length would otherwise pass): one wave per member, the member cut into 1 KiB segments aligned to its END (lane 63 the
+// last 1 KiB, lane 0 the partial first segment), lane j the CRC of its segment through slice-by-4 LDS tables, then a
+// 6-level tree over the lanes: crc(A B) = crc(A) x^(8 |B|) + crc(B) mod P (crc32_combine), where every right part B is a
+// whole number of segments, so each level multiplies by one constant.  Lanes read their segment with 16-B loads (the
+// lanes' starts share one alignment; at most 15 bytes at each end go byte by byte).  (r05: segments from the start,
+// dword loads 1 KiB apart across the lanes, and lane 0 folding the 64 partial CRCs in turn with a shift-and-add
+// multiply each: 0.49 ms per 10,000x BAM.)
 __global__ __launch_bounds__(256) void k_crc32(const uint8_t *__restrict__ comp, const spg_bgzf_member *__restrict__ mem,
                                                int64_t n, const uint8_t *__restrict__ out, uint32_t *__restrict__ status,
-                                               uint32_t op1k) {
+                                               CrcOps ops) {
     // slice-by-4 tables: T[k][b] = the CRC register after byte b followed by k zero bytes
     __shared__ uint32_t T[4][256];
-    __shared__ uint32_t part[4][64];
     {
         uint32_t c = (uint32_t)threadIdx.x;
         for (int k = 0; k < 8; k++) c = (c & 1u) ? (c >> 1) ^ 0xEDB88320u : c >> 1;
@@ -1060,56 +1062,67 @@ __global__ __launch_bounds__(256) void k_crc32(const uint8_t *__restrict__ comp,
     if (m >= n) return;                                         // (wave-uniform; no barrier below)
     if (status[m] != 0) return;
     const spg_bgzf_member M = mem[m];
-    const uint32_t a = (uint32_t)lane * 1024u, e = min(M.ulen, a + 1024u);
+    // the lane's segment [a, e) of the member, aligned to its end (ulen <= 64 KiB)
+    const int64_t e64 = (int64_t)M.ulen - 1024ll * (63 - lane), a64 = e64 - 1024;
+    const uint32_t e = (uint32_t)max(e64, (int64_t)0), a = (uint32_t)max(a64, (int64_t)0);
+    typedef __attribute__((address_space(1))) const uint8_t gu8;
+    gu8 *src = (gu8 *)(const void *)(out + M.uoff);
     uint32_t c = 0xFFFFFFFFu;
+    auto byte_step = [&](uint32_t x) { c = T[0][(c ^ x) & 0xFFu] ^ (c >> 8); };
+    auto word_step = [&](uint32_t x) {
+        c ^= x;
+        c = T[3][c & 0xFFu] ^ T[2][(c >> 8) & 0xFFu] ^ T[1][(c >> 16) & 0xFFu] ^ T[0][c >> 24];
+    };
     if (a < e) {
-        // four bytes per step from two aligned dwords (the segment starts at any byte), 16 dwords loaded per batch
-        typedef __attribute__((address_space(1))) const uint32_t gu32;
-        const uint64_t s0 = M.uoff + a;
-        gu32 *d = (gu32 *)(const void *)(out + (s0 & ~3ull));
-        const uint32_t ph = (uint32_t)(s0 & 3) * 8u, nw = (e - a) / 4;
-        uint32_t prev = d[0];
-        uint32_t i = 0;
-        for (; i + 16 <= nw; i += 16) {
-            uint32_t v[16];
+        // head bytes up to a 16-B aligned address, then 16-B blocks (eight loads in flight), then the tail bytes
+        const uint64_t g0 = M.uoff + a;
+        uint32_t b = a, h = (uint32_t)((16 - (g0 & 15)) & 15);
+        if (h > e - a) h = e - a;
+        for (uint32_t i = 0; i < h; i++) byte_step(src[b + i]);
+        b += h;
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(1))) const u32x4 gu128;
+        gu128 *q = (gu128 *)(const void *)(out + M.uoff + b);      // (16-B aligned)
+        const uint32_t nb = (e - b) / 16;
+        uint32_t k = 0;
+        for (; k + 8 <= nb; k += 8) {
+            u32x4 v[8];
 #pragma unroll
-            for (int k = 0; k < 16; k++) v[k] = d[i + k + 1];
+            for (int t = 0; t < 8; t++) v[t] = q[k + t];
 #pragma unroll
-            for (int k = 0; k < 16; k++) {
-                const uint32_t x = ph ? __builtin_amdgcn_alignbyte(v[k], prev, ph >> 3) : prev;
-                prev = v[k];
-                c ^= x;
-                c = T[3][c & 0xFFu] ^ T[2][(c >> 8) & 0xFFu] ^ T[1][(c >> 16) & 0xFFu] ^ T[0][c >> 24];
+            for (int t = 0; t < 8; t++) {
+                word_step(v[t].x);
+                word_step(v[t].y);
+                word_step(v[t].z);
+                word_step(v[t].w);
             }
         }
-        for (; i < nw; i++) {
-            const uint32_t nx = d[i + 1];
-            const uint32_t x = ph ? __builtin_amdgcn_alignbyte(nx, prev, ph >> 3) : prev;
-            prev = nx;
-            c ^= x;
-            c = T[3][c & 0xFFu] ^ T[2][(c >> 8) & 0xFFu] ^ T[1][(c >> 16) & 0xFFu] ^ T[0][c >> 24];
+        for (; k < nb; k++) {
+            const u32x4 v = q[k];
+            word_step(v.x);
+            word_step(v.y);
+            word_step(v.z);
+            word_step(v.w);
         }
-        typedef __attribute__((address_space(1))) const uint8_t gu8;
-        for (uint32_t b = a + 4 * nw; b < e; b++) c = T[0][(c ^ ((gu8 *)(out + M.uoff))[b]) & 0xFFu] ^ (c >> 8);
+        for (uint32_t i = b + 16 * nb; i < e; i++) byte_step(src[i]);
     }
-    part[w][lane] = ~c;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    uint32_t crc = a < e ? ~c : 0u;                             // (an empty segment: crc32 of the empty string)
+    // the tree: at level l, lane j (a multiple of 2^(l+1)) takes the right neighbour part (2^l whole segments)
+#pragma unroll
+    for (int l = 0; l < 6; l++) {
+        const int s = 1 << l;
+        const uint32_t r = __shfl_down(crc, s, 64);
+        if ((lane & (2 * s - 1)) == 0) crc = crc_multmodp(ops.op[l], crc) ^ r;
+    }
     if (lane == 0) {
-        const uint32_t nseg = (M.ulen + 1023u) / 1024u;
-        uint32_t crc = 0;                                       // crc32 of the empty string
-        for (uint32_t j = 0; j < nseg; j++) {
-            const uint32_t len = min(1024u, M.ulen - 1024u * j);
-            crc = crc_multmodp(len == 1024u ? op1k : crc_x8n(len), crc) ^ part[w][j];
-        }
         const uint8_t *t = comp + M.coff + M.clen;
         const uint32_t want = (uint32_t)t[0] | (uint32_t)t[1] << 8 | (uint32_t)t[2] << 16 | (uint32_t)t[3] << 24;
         if (crc != want) status[m] = 10;
     }
 }
 
-// x^(8 * 1024) mod P on the host (the combine's operator for a whole 1 KiB segment)
-static uint32_t host_crc_x8n(uint32_t n) {
+// x^(8 n) mod P on the host (the combine's operators)
+static uint32_t host_crc_x8n(uint64_t n) {
     auto mul = [](uint32_t a, uint32_t b) {
         uint32_t m = 1u << 31, p = 0;
         for (int i = 0; i < 32; i++) {
@@ -1150,9 +1163,13 @@ hipError_t launch_inflate(const uint8_t *comp, uint64_t comp_bytes, const spg_bg
                        (size_t)INFLATE_MPW * SLICE, st, comp, mem, n, out, status, INFLATE_MPW, 1);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    static const uint32_t op1k = host_crc_x8n(1024);
+    static const CrcOps ops = [] {
+        CrcOps o{};
+        for (int l = 0; l < 6; l++) o.op[l] = host_crc_x8n(1024ull << l);
+        return o;
+    }();
     hipLaunchKernelGGL(k_crc32, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, comp, mem, n, (const uint8_t *)out, status,
-                       op1k);
+                       ops);
     return hipGetLastError();
 }
 
