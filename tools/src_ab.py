@@ -80,6 +80,16 @@ EDITS = {
                     "        if (tid == 0) { atomicAdd(&g_ab_prof[5], clock64() - t_mk); atomicAdd(&g_ab_prof[6], 1ull); }\n    }\n"
                     "    if (tid == 0) atomicAdd(&g_ab_prof[7], clock64() - tq0);"),
                    ("}  // namespace spg\n", "}  // namespace spg\n" + "@@EXPORT@@")],
+    # phase B's batches and tokens (summed over members): [0] batches, [1] tokens, [2] output bytes, [5] members
+    "prof_batches": [("__device__ __forceinline__ uint32_t ring_slot(uint32_t g0, uint32_t x) {",
+                      "__device__ unsigned long long g_ab_prof[8];\n"
+                      "__device__ __forceinline__ uint32_t ring_slot(uint32_t g0, uint32_t x) {"),
+                     ("                const uint32_t sb = o - dist;                                            // a match's source start",
+                      "                const uint32_t sb = o - dist;                                            // a match's source start\n"
+                      "                if (lane == 0) { atomicAdd(&g_ab_prof[0], 1ull); atomicAdd(&g_ab_prof[1], (unsigned long long)nb);"
+                      " atomicAdd(&g_ab_prof[2], (unsigned long long)total); }"),
+                     ("    if (!st) flush(ulen);\n", "    if (!st) flush(ulen);\n    if (lane == 0) atomicAdd(&g_ab_prof[5], 1ull);\n"),
+                     ("}  // namespace spg\n\n// ---", "}  // namespace spg\n" + "@@EXPORT@@" + "\n// ---")],
     "noresolve": [("        for (int k = 0; k <= kend && !st; k++) {",
                    "        for (int k = 0; k <= kend && !st && kend < 0; k++) {"),
                   ("    if (!st && w != ulen) st = ST_FALLBACK;", "    if (!st) w = ulen;")],
