@@ -539,7 +539,8 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp
 constexpr uint32_t TK_EOB = 0x40000000u, TK_MATCH = 0x80000000u;   // tokens: literal byte | EOB | match (len-3)<<16 | dist-1
 constexpr uint32_t PAR_RCAP = 256;                                  // redo tokens per lane
 constexpr uint32_t PAR_MIN_SEG = 1024;                              // data bits per lane at least (fewer lanes for short blocks)
-constexpr uint32_t PAR_RING = 2048, PAR_BATCH = 1024;               // LDS window ring (power of two), batch output cap
+constexpr uint32_t PAR_RING = 2048, PAR_BATCH = 1024;
+constexpr int PB_CHUNK = 4;                                         // phase B: a short match's bytes read per round               // LDS window ring (power of two), batch output cap
 constexpr uint32_t PAR_RECENT = PAR_RING - PAR_BATCH;               // the ring holds every byte from w - PAR_RECENT on
 static_assert(PAR_RECENT >= 1023, "an unflushed partial 1 KiB block must stay in the ring");
 // scratch per member m (u32 units unless noted): token lists at 2 coff + 2048 m (2 clen + 2048 of them, split evenly
@@ -962,32 +963,43 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) void k_
                 // bytes <= PAR_RECENT) stays unflushed, so each byte is in one of the two (a match's source may straddle
                 // `flushed` when PAR_RECENT is less than the longest match + 1 KiB)
                 const bool indep = in && (!isM || sb + min(len, dist) <= w);
-                if (indep && len <= 32) {                                                // lane by lane
-                    if (!isM) {
-                        ring[ring_slot(g0, o)] = (uint8_t)tk;
-                    } else {
-                        uint32_t mq = 0;
-                        for (uint32_t q = 0; q < len; q += 4) {
-                            uint8_t v[4];
+                // the independent tokens byte-parallel: lane l writes the batch's bytes [l CH, (l + 1) CH), each from
+                // the token covering it (found by a search over the lanes, then one step per byte), literal or source
+                // byte (read from global memory and from the ring unconditionally, selected after).  (r06ab: a lane per
+                // token, short matches copied lane by lane and long ones by the whole wave, took 1.31 M + part of 0.77 M
+                // of a member-wave's 2.24 M phase-B clocks: the lanes of short tokens idled while the longest copied.)
+                {
+                    const uint32_t ex_s = in ? excl : 0xFFFFFFFFu;                       // (past the batch: never found)
+                    const uint32_t tkx = tk | (indep ? TK_EOB : 0u);                     // bit 30: independent (no EOB here)
+                    const uint32_t CH = (total + 63u) / 64u, P0 = (uint32_t)lane * CH;
+                    int t = 0;                                                           // the last token with excl <= P0
 #pragma unroll
-                            for (int u = 0; u < 4; u++) {
-                                v[u] = q + u < len ? (sb + mq < flushed ? gout[sb + mq] : ring[ring_slot(g0, sb + mq)]) : 0;
-                                mq = mq + 1 == dist ? 0 : mq + 1;
-                            }
-#pragma unroll
-                            for (int u = 0; u < 4; u++)
-                                if (q + u < len) ring[ring_slot(g0, o + q + u)] = v[u];
-                        }
+                    for (int st2 = 32; st2; st2 >>= 1) t += (uint32_t)__shfl((int)ex_s, t + st2, 64) <= P0 ? st2 : 0;
+                    uint32_t et = (uint32_t)__shfl((int)ex_s, t, 64), kt = (uint32_t)__shfl((int)tkx, t, 64);
+                    for (uint32_t i = 0; i < CH; i++) {
+                        const uint32_t P = P0 + i;
+                        const uint32_t lt = (kt & TK_MATCH) ? ((kt >> 16) & 255u) + 3u : 1u;
+                        t = P >= et + lt ? t + 1 : t;                                    // (at most one token per byte)
+                        et = (uint32_t)__shfl((int)ex_s, t & 63, 64);
+                        kt = (uint32_t)__shfl((int)tkx, t & 63, 64);
+                        const bool isMt = (kt & TK_MATCH) != 0;
+                        const uint32_t dt = (kt & 0x7FFFu) + 1u;
+                        uint32_t q = P - et;
+                        if (isMt && q >= dt) q %= dt;
+                        const uint32_t x = w + et - dt + q;                              // (a match's source byte)
+                        const bool fg = x < flushed;
+                        const uint32_t gv = gout[isMt && fg ? x : 0u], lv = ring[ring_slot(g0, isMt ? x : 0u)];
+                        const uint32_t v = isMt ? (fg ? gv : lv) : (kt & 255u);
+                        if (P < total && (kt & TK_EOB)) ring[ring_slot(g0, w + P)] = (uint8_t)v;
                     }
                 }
-                // then one match at a time by the whole wave: the long independent ones, then in order those whose
-                // source is an earlier token of this batch (every earlier token is written by then); byte q of a match
-                // is its source's byte q mod dist, so a match never reads its own bytes
-                uint64_t lm = __ballot(indep && len > 32), dm = __ballot(in && !indep);
-                while (lm | dm) {
-                    uint64_t &mk = lm ? lm : dm;
-                    const int j = __builtin_ctzll(mk);
-                    mk &= mk - 1;
+                // then, in order, the matches whose source is an earlier token of this batch, one at a time by the whole
+                // wave (every earlier token is written by then); byte q of a match is its source's byte q mod dist, so a
+                // match never reads its own bytes
+                uint64_t dm = __ballot(in && !indep);
+                while (dm) {
+                    const int j = __builtin_ctzll(dm);
+                    dm &= dm - 1;
                     const uint32_t oj = (uint32_t)__builtin_amdgcn_readlane((int)o, j);
                     const uint32_t lj = (uint32_t)__builtin_amdgcn_readlane((int)len, j);
                     const uint32_t dj = (uint32_t)__builtin_amdgcn_readlane((int)dist, j);
