@@ -539,8 +539,7 @@ __global__ __launch_bounds__(64) void k_inflate(const uint8_t *__restrict__ comp
 constexpr uint32_t TK_EOB = 0x40000000u, TK_MATCH = 0x80000000u;   // tokens: literal byte | EOB | match (len-3)<<16 | dist-1
 constexpr uint32_t PAR_RCAP = 256;                                  // redo tokens per lane
 constexpr uint32_t PAR_MIN_SEG = 1024;                              // data bits per lane at least (fewer lanes for short blocks)
-constexpr uint32_t PAR_RING = 2048, PAR_BATCH = 1024;
-constexpr int PB_CHUNK = 4;                                         // phase B: a short match's bytes read per round               // LDS window ring (power of two), batch output cap
+constexpr uint32_t PAR_RING = 2048, PAR_BATCH = 1024;               // LDS window ring (power of two), batch output cap
 constexpr uint32_t PAR_RECENT = PAR_RING - PAR_BATCH;               // the ring holds every byte from w - PAR_RECENT on
 static_assert(PAR_RECENT >= 1023, "an unflushed partial 1 KiB block must stay in the ring");
 // scratch per member m (u32 units unless noted): token lists at 2 coff + 2048 m (2 clen + 2048 of them, split evenly
