@@ -58,3 +58,34 @@ def test_corrupt_members_are_reported():
     out, st, _ = inflate(comp, members)
     assert st[0] == 0 and out[:len(good)] == good
     assert (st[1:] != 0).all(), st
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_crc_segment_edges(flip):
+    """k_crc32 cuts a member into 1 KiB segments aligned to its end and combines the lanes' CRCs by a tree: member
+    sizes around the segment edges (0, 1, 1,023-1,025, 2,047-2,049, 63 KiB + 1, 65,535, 65,536) at odd output offsets all
+    pass, and a trailer CRC off by one bit is reported for every size (status 10) without touching the others."""
+    import zlib
+    from inflate_util import deflate
+    rng = np.random.default_rng(17)
+    sizes = [0, 1, 1023, 1024, 1025, 2047, 2048, 2049, 63 * 1024 + 1, 65535, 65536]
+    datas = [rng.integers(0, 6, n, dtype=np.uint8).tobytes() for n in sizes]
+    comp, members, uoff = bytearray(), [], 3                        # (odd output offsets: a 3-byte lead-in member)
+    lead = b"xyz"
+    for raw, data in [(deflate(lead, 6, zlib.Z_DEFAULT_STRATEGY), lead)] + \
+            [(deflate(d, 6, zlib.Z_DEFAULT_STRATEGY), d) for d in datas]:
+        coff = len(comp)
+        comp += raw
+        crc = zlib.crc32(data)
+        if flip and data is not lead:
+            crc ^= 1 << (len(data) % 32)
+        comp += crc.to_bytes(4, "little") + len(data).to_bytes(4, "little")
+        members.append((coff, len(raw), len(data), 0 if data is lead else uoff))
+        uoff += 0 if data is lead else len(data)
+    out, st, _ = inflate(bytes(comp), members)
+    assert st[0] == 0
+    if flip:
+        assert (st[1:] == 10).all(), st
+    else:
+        assert (st == 0).all(), st
+        assert out[3:] == b"".join(datas)
