@@ -6,7 +6,7 @@
 //   k_bam_starts  one wave per BGZF member: the first record that starts inside the member's inflated range — the
 //                 offset where a block_size hop lands on a plausible record eight times in a row (or on the stream's
 //                 end); the member holding the header's end starts there.
-//   k_bam_walk    one lane per member with a start: the block_size chain from its start to the next member's start,
+//   k_bam_walk    one wave per member with a start: the block_size chain from its start to the next member's start,
 //                 counting the records of the contig the stepper keeps and listing them per member (pass 1; k_bam_copy
 //                 moves the lists to the exclusive prefix of the counts — or, for a chain of more than BAM_RTMP, a
 //                 second walk lists them there, pass 2); every chain must land exactly on the next start (else the
@@ -111,44 +111,88 @@ __global__ __launch_bounds__(256) void k_bam_starts(BamArgs A) {
     if (lane == 0) A.start[m] = s;
 }
 
+// One wave per member: the block_size chain is a dependent load per record (~240 per 64 KiB member), so the wave
+// copies a WALK_W-byte window of the stream into LDS with one round of 16-B loads and walks the records' headers there
+// (every lane the same walk, broadcast LDS reads; lane 0 stores), reloading the window at the record that leaves it.
+// (r05-r06: one lane per member walked the chain through L2 — 8,357 lanes in 131 waves, one HBM / MALL round trip per
+// record: 0.41 ms per 10,000x BAM; now 0.30 ms, and the same with the next window prefetched in registers: the walk
+// itself, not the window loads, is what is left, r06ai.)
+constexpr int WALK_W = 4096;
 template <bool WRITE>
-__global__ __launch_bounds__(64) void k_bam_walk(BamArgs A) {
-    const int64_t m = (int64_t)blockIdx.x * 64 + threadIdx.x;
-    if (m >= A.n_members) return;
+__global__ __launch_bounds__(256) void k_bam_walk(BamArgs A) {
+    __shared__ __align__(16) uint32_t win[4][WALK_W / 4 + 4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t m = (int64_t)blockIdx.x * 4 + wv;
+    if (m >= A.n_members) return;                                           // (wave-uniform; no workgroup barrier)
     uint64_t x = A.start[m];
     if (x == BAM_NONE) {
-        if (!WRITE) { A.cnt[m] = 0; A.pos_lo[m] = INT64_MAX; A.pos_hi[m] = -1; }
+        if (!WRITE && lane == 0) { A.cnt[m] = 0; A.pos_lo[m] = INT64_MAX; A.pos_hi[m] = -1; }
         return;
     }
+    // the next member with a start: 64 candidates per round
     uint64_t nx = A.total;
-    for (int64_t k = m + 1; k < A.n_members; k++) {
-        const uint64_t s = A.start[k];
-        if (s != BAM_NONE) { nx = s; break; }
+    for (int64_t k0 = m + 1; k0 < A.n_members; k0 += 64) {
+        const int64_t k = k0 + lane;
+        const uint64_t sk = k < A.n_members ? A.start[k] : BAM_NONE;
+        const uint64_t hit = __ballot(sk != BAM_NONE);
+        if (hit) {
+            nx = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)sk, __builtin_ctzll(hit)) |
+                 (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(sk >> 32), __builtin_ctzll(hit)) << 32;
+            break;
+        }
     }
+    uint32_t *const wl = win[wv];
+    uint64_t wa = ~0ull;                                                    // the window's first byte (none yet)
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) const u32x4 gu128;
+    auto refill = [&](uint64_t xx) __attribute__((always_inline)) {         // the window from xx's 16-B block on
+        const uint64_t a = xx & ~15ull;
+        wa = a;
+        u32x4 v[WALK_W / 1024];
+#pragma unroll
+        for (int k = 0; k < WALK_W / 1024; k++) {
+            const uint64_t g = a + 16ull * (uint64_t)(lane + 64 * k);
+            v[k] = g + 16 <= A.total + 64 ? *(gu128 *)(const void *)(A.data + g) : u32x4{0u, 0u, 0u, 0u};
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int k = 0; k < WALK_W / 1024; k++) *reinterpret_cast<u32x4 *>(&wl[4 * (lane + 64 * k)]) = v[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto rd32 = [&](uint64_t q) -> uint32_t {                               // u32 at stream offset q (in the window)
+        const uint32_t o = (uint32_t)(q - wa);
+        return __builtin_amdgcn_alignbyte(wl[(o >> 2) + 1], wl[o >> 2], o & 3u);
+    };
     uint32_t kept = 0, bad = 0;
     int64_t first = INT64_MAX, last = -1;
     const uint32_t at = WRITE ? A.base[m] : 0u;
     while (x < nx) {
         if (x + 36 > A.total) { bad = 1; break; }
-        const uint32_t bs = ldu32(A.data, x);
+        if (wa == ~0ull || x < wa || x + 36 > wa + WALK_W) refill(x);
+        const uint32_t bs = rd32(x);
         if (bs < 32 || x + 4 + (uint64_t)bs > A.total) { bad = 1; break; }
         const uint64_t b = x + 4;
-        if (ldi32(A.data, b) == A.tid) {
-            const int64_t pos = ldi32(A.data, b + 4);
+        if ((int32_t)rd32(b) == A.tid) {
+            const int64_t pos = (int32_t)rd32(b + 4);
             if (first == INT64_MAX) first = pos;
             if (pos < last) bad |= 2;
             last = pos;
-            const uint32_t w8 = ldu32(A.data, b + 8), w12 = ldu32(A.data, b + 12);
+            const uint32_t w8 = rd32(b + 8), w12 = rd32(b + 12);
             if (keeps(A, w12 >> 16, (w8 >> 8) & 0xFFu)) {
-                if (WRITE) A.rec[at + kept] = b;
-                else if (kept < BAM_RTMP) A.rtmp[(uint64_t)m * BAM_RTMP + kept] = b;
+                if (lane == 0) {
+                    if (WRITE) A.rec[at + kept] = b;
+                    else if (kept < BAM_RTMP) A.rtmp[(uint64_t)m * BAM_RTMP + kept] = b;
+                }
                 kept++;
             }
         }
         x = b + bs;
     }
     if (x != nx) bad |= 1;
-    if (!WRITE) {
+    if (!WRITE && lane == 0) {
         A.cnt[m] = kept;
         A.pos_lo[m] = first;
         A.pos_hi[m] = last;
@@ -184,8 +228,29 @@ __global__ __launch_bounds__(256) void k_bam_fields(BamArgs A) {
         const uint32_t c = ldu32(A.data, co + 4ull * j);
         if (eats_ref(c & 15u)) rl += c >> 4;
     }
-    uint64_t h = 0xcbf29ce484222325ull;                 // FNV-1a 64 over the name (its NUL excluded)
-    for (uint32_t j = 0; j + 1 < l_name; j++) h = (h ^ ldu8(A.data, b + 32 + j)) * 0x100000001b3ull;
+    // FNV-1a 64 over the name (its NUL excluded): the 64 bytes from the name's 16-B aligned start taken with four 16-B
+    // loads, each byte folded in when it lies in the name (one byte load per name byte before: ~30 scattered loads per
+    // read, 0.32 ms per 10,000x BAM); a longer name's rest byte by byte
+    uint64_t h = 0xcbf29ce484222325ull;
+    {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(1))) const u32x4 gu128;
+        const uint64_t n0 = b + 32, n1 = n0 + l_name - 1, a0 = n0 & ~15ull;
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = *(gu128 *)(const void *)(A.data + a0 + 16 * k);   // (inside the record + pad)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t wd[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint64_t at = a0 + 16 * k + i;
+                const uint64_t hx = (h ^ ((wd[i >> 2] >> (8 * (i & 3))) & 0xFFu)) * 0x100000001b3ull;
+                h = at >= n0 && at < n1 ? hx : h;
+            }
+        }
+        for (uint64_t at = a0 + 64; at < n1; at++) h = (h ^ ldu8(A.data, at)) * 0x100000001b3ull;
+    }
     A.pos[i] = pos;
     A.end[i] = (int32_t)(pos + rl);
     A.flag[i] = (uint16_t)(w12 >> 16);
@@ -316,8 +381,8 @@ __global__ __launch_bounds__(256) void k_bam_gather2(BamGatherArgs G) {
 hipError_t launch_bam_scan(const BamArgs &A, int pass, hipStream_t st) {
     const unsigned mb = (unsigned)((A.n_members + 63) / 64), mw = (unsigned)((A.n_members + 3) / 4);
     if (pass == 0) k_bam_starts<<<mw, 256, 0, st>>>(A);
-    else if (pass == 1) k_bam_walk<false><<<mb, 64, 0, st>>>(A);
-    else if (pass == 2) k_bam_walk<true><<<mb, 64, 0, st>>>(A);
+    else if (pass == 1) k_bam_walk<false><<<(unsigned)((A.n_members + 3) / 4), 256, 0, st>>>(A);
+    else if (pass == 2) k_bam_walk<true><<<(unsigned)((A.n_members + 3) / 4), 256, 0, st>>>(A);
     else if (pass == 4) k_bam_copy<<<mw, 256, 0, st>>>(A);
     else if (A.n_reads) k_bam_fields<<<(A.n_reads + 255) / 256, 256, 0, st>>>(A);
     return hipGetLastError();
