@@ -162,25 +162,26 @@ __global__ __launch_bounds__(256) void k_bam_walk(BamArgs A) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
-    auto rd32 = [&](uint64_t q) -> uint32_t {                               // u32 at stream offset q (in the window)
-        const uint32_t o = (uint32_t)(q - wa);
-        return __builtin_amdgcn_alignbyte(wl[(o >> 2) + 1], wl[o >> 2], o & 3u);
-    };
     uint32_t kept = 0, bad = 0;
     int64_t first = INT64_MAX, last = -1;
     const uint32_t at = WRITE ? A.base[m] : 0u;
     while (x < nx) {
         if (x + 36 > A.total) { bad = 1; break; }
         if (wa == ~0ull || x < wa || x + 36 > wa + WALK_W) refill(x);
-        const uint32_t bs = rd32(x);
+        // the header's first 20 bytes (block_size, refID, pos, bin_mq_nl, flag_nc) from six dwords of the window
+        const uint32_t o = (uint32_t)(x - wa), i0 = o >> 2, sh = o & 3u;
+        uint32_t d[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) d[k] = wl[i0 + k];
+        const uint32_t bs = __builtin_amdgcn_alignbyte(d[1], d[0], sh);
         if (bs < 32 || x + 4 + (uint64_t)bs > A.total) { bad = 1; break; }
         const uint64_t b = x + 4;
-        if ((int32_t)rd32(b) == A.tid) {
-            const int64_t pos = (int32_t)rd32(b + 4);
+        if ((int32_t)__builtin_amdgcn_alignbyte(d[2], d[1], sh) == A.tid) {
+            const int64_t pos = (int32_t)__builtin_amdgcn_alignbyte(d[3], d[2], sh);
             if (first == INT64_MAX) first = pos;
             if (pos < last) bad |= 2;
             last = pos;
-            const uint32_t w8 = rd32(b + 8), w12 = rd32(b + 12);
+            const uint32_t w8 = __builtin_amdgcn_alignbyte(d[4], d[3], sh), w12 = __builtin_amdgcn_alignbyte(d[5], d[4], sh);
             if (keeps(A, w12 >> 16, (w8 >> 8) & 0xFFu)) {
                 if (lane == 0) {
                     if (WRITE) A.rec[at + kept] = b;
