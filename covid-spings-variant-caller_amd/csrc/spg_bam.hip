@@ -6,7 +6,7 @@
 //   k_bam_starts  one wave per BGZF member: the first record that starts inside the member's inflated range — the
 //                 offset where a block_size hop lands on a plausible record eight times in a row (or on the stream's
 //                 end); the member holding the header's end starts there.
-//   k_bam_walk    one wave per member with a start: the block_size chain from its start to the next member's start,
+//   k_bam_walk    16 lanes per member with a start: the block_size chain from its start to the next member's start,
 //                 counting the records of the contig the stepper keeps and listing them per member (pass 1; k_bam_copy
 //                 moves the lists to the exclusive prefix of the counts — or, for a chain of more than BAM_RTMP, a
 //                 second walk lists them there, pass 2); every chain must land exactly on the next start (else the
@@ -115,49 +115,49 @@ __global__ __launch_bounds__(256) void k_bam_starts(BamArgs A) {
 // copies a WALK_W-byte window of the stream into LDS with one round of 16-B loads and walks the records' headers there
 // (every lane the same walk, broadcast LDS reads; lane 0 stores), reloading the window at the record that leaves it.
 // (r05-r06: one lane per member walked the chain through L2 — 8,357 lanes in 131 waves, one HBM / MALL round trip per
-// record: 0.41 ms per 10,000x BAM; now 0.30 ms, and the same with the next window prefetched in registers: the walk
-// itself, not the window loads, is what is left, r06ai.)
-constexpr int WALK_W = 4096;
+// record: 0.41 ms per 10,000x BAM; one member per wave 0.30 ms — the same with the next window prefetched in
+// registers, r06ai: the walk's instructions, not the window loads, were left — and 4 members per wave 0.19 ms
+// (8: 0.33, 16: 0.51, r06ao).)
+constexpr int WALK_W = 4096, WALK_G = 4;
 template <bool WRITE>
-__global__ __launch_bounds__(256) void k_bam_walk(BamArgs A) {
-    __shared__ __align__(16) uint32_t win[4][WALK_W / 4 + 4];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t m = (int64_t)blockIdx.x * 4 + wv;
-    if (m >= A.n_members) return;                                           // (wave-uniform; no workgroup barrier)
+__global__ __launch_bounds__(64) void k_bam_walk(BamArgs A) {
+    // WALK_G members per wave, 64 / WALK_G lanes each (a lane group walks its member; the groups run side by side, so
+    // one instruction stream serves WALK_G chains)
+    constexpr int GL = 64 / WALK_G;
+    __shared__ __align__(16) uint32_t win[WALK_G][WALK_W / 4 + 4];
+    const int lane = threadIdx.x, grp = lane / GL, gl = lane % GL;
+    const int64_t m = (int64_t)blockIdx.x * WALK_G + grp;
+    if (m >= A.n_members) return;                                           // (the group's lanes alike)
     uint64_t x = A.start[m];
     if (x == BAM_NONE) {
-        if (!WRITE && lane == 0) { A.cnt[m] = 0; A.pos_lo[m] = INT64_MAX; A.pos_hi[m] = -1; }
+        if (!WRITE && gl == 0) { A.cnt[m] = 0; A.pos_lo[m] = INT64_MAX; A.pos_hi[m] = -1; }
         return;
     }
-    // the next member with a start: 64 candidates per round
-    uint64_t nx = A.total;
-    for (int64_t k0 = m + 1; k0 < A.n_members; k0 += 64) {
-        const int64_t k = k0 + lane;
-        const uint64_t sk = k < A.n_members ? A.start[k] : BAM_NONE;
-        const uint64_t hit = __ballot(sk != BAM_NONE);
-        if (hit) {
-            nx = (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)sk, __builtin_ctzll(hit)) |
-                 (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(sk >> 32), __builtin_ctzll(hit)) << 32;
-            break;
-        }
+    uint64_t nx = A.total;                                                  // the next member with a start
+    for (int64_t k = m + 1; k < A.n_members; k++) {
+        const uint64_t sk = A.start[k];
+        if (sk != BAM_NONE) { nx = sk; break; }
     }
-    uint32_t *const wl = win[wv];
+    uint32_t *const wl = win[grp];
     uint64_t wa = ~0ull;                                                    // the window's first byte (none yet)
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(1))) const u32x4 gu128;
+    constexpr int NV = WALK_W / 16 / GL, NR = NV;                           // 16-B chunks per lane per window
     auto refill = [&](uint64_t xx) __attribute__((always_inline)) {         // the window from xx's 16-B block on
-        const uint64_t a = xx & ~15ull;
-        wa = a;
-        u32x4 v[WALK_W / 1024];
-#pragma unroll
-        for (int k = 0; k < WALK_W / 1024; k++) {
-            const uint64_t g = a + 16ull * (uint64_t)(lane + 64 * k);
-            v[k] = g + 16 <= A.total + 64 ? *(gu128 *)(const void *)(A.data + g) : u32x4{0u, 0u, 0u, 0u};
-        }
+        const uint64_t a0 = xx & ~15ull;
+        wa = a0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        for (int k0 = 0; k0 < NV; k0 += NR) {                               // NR chunks in flight per round
+            u32x4 v[NR];
 #pragma unroll
-        for (int k = 0; k < WALK_W / 1024; k++) *reinterpret_cast<u32x4 *>(&wl[4 * (lane + 64 * k)]) = v[k];
+            for (int k = 0; k < NR; k++) {
+                const uint64_t g = a0 + 16ull * (uint64_t)(gl + GL * (k0 + k));
+                v[k] = g + 16 <= A.total + 64 ? *(gu128 *)(const void *)(A.data + g) : u32x4{0u, 0u, 0u, 0u};
+            }
+#pragma unroll
+            for (int k = 0; k < NR; k++) *reinterpret_cast<u32x4 *>(&wl[4 * (gl + GL * (k0 + k))]) = v[k];
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(256) void k_bam_walk(BamArgs A) {
             last = pos;
             const uint32_t w8 = __builtin_amdgcn_alignbyte(d[4], d[3], sh), w12 = __builtin_amdgcn_alignbyte(d[5], d[4], sh);
             if (keeps(A, w12 >> 16, (w8 >> 8) & 0xFFu)) {
-                if (lane == 0) {
+                if (gl == 0) {
                     if (WRITE) A.rec[at + kept] = b;
                     else if (kept < BAM_RTMP) A.rtmp[(uint64_t)m * BAM_RTMP + kept] = b;
                 }
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void k_bam_walk(BamArgs A) {
         x = b + bs;
     }
     if (x != nx) bad |= 1;
-    if (!WRITE && lane == 0) {
+    if (!WRITE && gl == 0) {
         A.cnt[m] = kept;
         A.pos_lo[m] = first;
         A.pos_hi[m] = last;
@@ -382,8 +382,8 @@ __global__ __launch_bounds__(256) void k_bam_gather2(BamGatherArgs G) {
 hipError_t launch_bam_scan(const BamArgs &A, int pass, hipStream_t st) {
     const unsigned mb = (unsigned)((A.n_members + 63) / 64), mw = (unsigned)((A.n_members + 3) / 4);
     if (pass == 0) k_bam_starts<<<mw, 256, 0, st>>>(A);
-    else if (pass == 1) k_bam_walk<false><<<(unsigned)((A.n_members + 3) / 4), 256, 0, st>>>(A);
-    else if (pass == 2) k_bam_walk<true><<<(unsigned)((A.n_members + 3) / 4), 256, 0, st>>>(A);
+    else if (pass == 1) k_bam_walk<false><<<(unsigned)((A.n_members + WALK_G - 1) / WALK_G), 64, 0, st>>>(A);
+    else if (pass == 2) k_bam_walk<true><<<(unsigned)((A.n_members + WALK_G - 1) / WALK_G), 64, 0, st>>>(A);
     else if (pass == 4) k_bam_copy<<<mw, 256, 0, st>>>(A);
     else if (A.n_reads) k_bam_fields<<<(A.n_reads + 255) / 256, 256, 0, st>>>(A);
     return hipGetLastError();
