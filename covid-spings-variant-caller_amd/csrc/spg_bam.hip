@@ -214,10 +214,31 @@ __global__ __launch_bounds__(256) void k_bam_fields(BamArgs A) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= A.n_reads) return;
     const uint64_t b = A.rec[i];
-    const uint32_t bs = ldu32(A.data, b - 4);
-    const uint32_t w8 = ldu32(A.data, b + 8), w12 = ldu32(A.data, b + 12);
+    // the 36-byte header [b - 4, b + 32) from four 16-B loads of its aligned window: hd[j] = the header's dword j
+    // (block_size, refID, pos, bin_mq_nl, flag_nc, l_seq, next_refID, next_pos, tlen) — eight unaligned-dword reads of
+    // two loads each before
+    uint32_t hd[9];
+    {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(1))) const u32x4 gu128;
+        const uint64_t h0 = b - 4, a0 = h0 & ~15ull;
+        const uint32_t q = (uint32_t)(h0 - a0) >> 2, r = (uint32_t)(h0 - a0) & 3u;
+        uint32_t W[16];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {                                      // (inside the record + pad)
+            const u32x4 v = *(gu128 *)(const void *)(A.data + a0 + 16 * k);
+            W[4 * k] = v.x; W[4 * k + 1] = v.y; W[4 * k + 2] = v.z; W[4 * k + 3] = v.w;
+        }
+        uint32_t S[10];
+#pragma unroll
+        for (int t = 0; t < 10; t++) S[t] = q == 0 ? W[t] : q == 1 ? W[t + 1] : q == 2 ? W[t + 2] : W[t + 3];
+#pragma unroll
+        for (int j = 0; j < 9; j++) hd[j] = __builtin_amdgcn_alignbyte(S[j + 1], S[j], r);
+    }
+    const uint32_t bs = hd[0];
+    const uint32_t w8 = hd[3], w12 = hd[4];
     const uint32_t l_name = w8 & 0xFFu, n_cig = w12 & 0xFFFFu;
-    const int32_t pos = ldi32(A.data, b + 4), l_seq = ldi32(A.data, b + 16);
+    const int32_t pos = (int32_t)hd[2], l_seq = (int32_t)hd[5];
     if (l_name < 1 || l_seq < 0 ||
         32ull + l_name + 4ull * n_cig + ((uint64_t)l_seq + 1) / 2 + (uint64_t)l_seq > (uint64_t)bs) {
         atomicOr(A.err, 4u);
@@ -255,9 +276,9 @@ __global__ __launch_bounds__(256) void k_bam_fields(BamArgs A) {
     A.pos[i] = pos;
     A.end[i] = (int32_t)(pos + rl);
     A.flag[i] = (uint16_t)(w12 >> 16);
-    A.mtid[i] = ldi32(A.data, b + 20);
-    A.mpos[i] = ldi32(A.data, b + 24);
-    A.isize[i] = ldi32(A.data, b + 28);
+    A.mtid[i] = (int32_t)hd[6];
+    A.mpos[i] = (int32_t)hd[7];
+    A.isize[i] = (int32_t)hd[8];
     A.l_seq[i] = (uint32_t)l_seq;
     A.nhash[i] = h;
 }
